@@ -1,0 +1,116 @@
+/*
+ * gsr.h -- C ABI of the MI355X (gfx950) Gaussian-splat rasterizer library
+ * (street-sparse-3dgs_amd/diff_gaussian_rasterization/libgsr_hip.so).
+ *
+ * This is the drop-in boundary for the hot path named in BASELINE.json: the entry points
+ * are the ones the reference's torch extension binds (`diff_gaussian_rasterization._C`,
+ * imported at gaussian_renderer/__init__.py:14,17 of Street-sparse-3DGS; the extension's
+ * source lives in the un-vendored submodule submodules/hierarchy-rasterizer,
+ * .gitmodules:5-7).  Plain pointers and sizes only: no torch types cross this line.
+ *
+ *   gsr_rasterize_forward   replaces  _C.rasterize_gaussians           (called from the
+ *                                     autograd Function's forward)
+ *   gsr_rasterize_backward  replaces  _C.rasterize_gaussians_backward  (autograd backward)
+ *   gsr_mark_visible        replaces  _C.mark_visible                  (GaussianRasterizer.markVisible)
+ *
+ * Conventions:
+ *   - every array pointer is DEVICE memory on the current HIP device, fp32 unless noted,
+ *     row-major and contiguous; `stream` is a hipStream_t (NULL = default stream);
+ *   - viewmatrix / projmatrix are the 4x4 torch row-major tensors W2C^T and (P W2C)^T,
+ *     read column-major (scene/cameras.py:96-99 of the reference);
+ *   - shs is (P, M, 3) coefficient-major / channel-minor; rotations are (r,x,y,z) used as
+ *     given (the caller normalises, scene/gaussian_model.py:47); cov3D is the 6-float
+ *     upper triangle xx,xy,xz,yy,yz,zz;
+ *   - scratch ("geometry", "binning", "image", "backward") buffers are obtained through the
+ *     caller's resize callback so they live in the caller's allocator (the torch caching
+ *     allocator in the Python host) and are handed back to the backward call unchanged.
+ *
+ * Return value: GSR_OK (0) or a negative gsr_status; gsr_last_error() gives the message.
+ */
+#ifndef GSR_H
+#define GSR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSR_ABI_VERSION 1
+
+typedef enum {
+    GSR_OK = 0,
+    GSR_ERR_INVALID_ARGUMENT = -1,
+    GSR_ERR_ALLOCATION = -2,
+    GSR_ERR_DEVICE = -3,
+    GSR_ERR_UNSUPPORTED = -4
+} gsr_status;
+
+/* Resize callback: return a device pointer to at least `bytes` bytes that stays valid until
+ * the caller releases it (after the backward call).  Called at most once per buffer per call.
+ * Returning NULL aborts the call with GSR_ERR_ALLOCATION. */
+typedef void *(*gsr_resize_fn)(void *ctx, size_t bytes);
+
+/* Forward: preprocess -> scan -> duplicate-with-keys -> sort -> tile ranges -> blend.
+ * Mirrors CudaRasterizer::Rasterizer::forward as the reference's
+ * _C.rasterize_gaussians(bg, means3D, colors, opacity, scales, rotations, scale_modifier,
+ * cov3D_precomp, viewmatrix, projmatrix, tanfovx, tanfovy, H, W, sh, degree, campos,
+ * prefiltered, debug, render_indices, parent_indices, interpolation_weights, num_node_kids,
+ * do_depth) drives it.
+ *   shs / colors_precomp: exactly one non-NULL.  scales+rotations / cov3D_precomp: exactly one.
+ *   M = shs.shape[1] (coefficient stride), D = active SH degree (0..3, (D+1)^2 <= M).
+ *   out_color (3,H,W); out_invdepth (1,H,W) or NULL when do_depth is false; radii (P) int32.
+ *   render_indices/parent_indices/interpolation_weights/num_node_kids: the hierarchy-cut
+ *   fields.  num_render == 0 (every reference call path) means plain
+ *   3DGS and the four pointers are never dereferenced (they may be host pointers).
+ *   *num_rendered receives K, the number of tile instances. */
+int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffer, gsr_resize_fn image_buffer,
+                          void *resize_ctx, int P, int D, int M, const float *background, int width, int height,
+                          const float *means3D, const float *shs, const float *colors_precomp,
+                          const float *opacities, const float *scales, float scale_modifier,
+                          const float *rotations, const float *cov3D_precomp, const float *viewmatrix,
+                          const float *projmatrix, const float *cam_pos, float tan_fovx, float tan_fovy,
+                          int prefiltered, float *out_color, float *out_invdepth, int *radii,
+                          const int *render_indices, const int *parent_indices,
+                          const float *interpolation_weights, const int *num_node_kids, int num_render,
+                          int debug, void *stream, int64_t *num_rendered);
+
+/* Backward.  geom/binning/image are the pointers the forward's callbacks returned; R = K.
+ * dL_dpix (3,H,W); dL_dinvdepth (1,H,W) or NULL (no depth gradient).  `scratch` provides
+ * the per-tile-instance gradient workspace.  Every output row is written (zeros where
+ * radii == 0 and beyond the active SH degree), so outputs need no pre-zeroing:
+ *   dL_dmeans2D (P,3)  dL_dcolors (P,3)  dL_dopacity (P,1)  dL_dmeans3D (P,3)
+ *   dL_dcov3D (P,6)  dL_dsh (P,M,3) [ignored if shs == NULL]
+ *   dL_dscales (P,3)  dL_drotations (P,4) [ignored if scales == NULL] */
+int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D, int M, int64_t R,
+                           const float *background, int width, int height, const float *means3D,
+                           const float *shs, const float *colors_precomp, const float *scales,
+                           float scale_modifier, const float *rotations, const float *cov3D_precomp,
+                           const float *viewmatrix, const float *projmatrix, const float *cam_pos,
+                           float tan_fovx, float tan_fovy, const int *radii, void *geom_buffer,
+                           void *binning_buffer, void *image_buffer, const float *dL_dpix,
+                           const float *dL_dinvdepth, float *dL_dmeans2D, float *dL_dcolors, float *dL_dopacity,
+                           float *dL_dmeans3D, float *dL_dcov3D, float *dL_dsh, float *dL_dscales,
+                           float *dL_drotations, int debug, void *stream);
+
+/* Frustum test (view-space z > 0.2), present[P] as bytes 0/1. */
+int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,
+                     uint8_t *present, void *stream);
+
+/* Per-stage device time of the last forward/backward on this thread, filled only when
+ * gsr_set_profiling(1) was called (HIP events; for bench.py's roofline).  Stage order:
+ * 0 preprocess, 1 scan, 2 duplicate, 3 sort, 4 ranges, 5 render_fwd, 6 render_bwd,
+ * 7 preprocess_bwd.  Returns the number of stages written. */
+int gsr_set_profiling(int enable);
+int gsr_stage_times_ms(float *out, int max_stages);
+
+/* Version / diagnostics. */
+int gsr_abi_version(void);
+const char *gsr_last_error(void);
+const char *gsr_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSR_H */

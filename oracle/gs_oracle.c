@@ -1,0 +1,648 @@
+/*
+ * gs_oracle.c -- CPU restatement of the tile-based differentiable Gaussian-splat
+ * rasterizer that Street-sparse-3DGS calls through diff_gaussian_rasterization.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product path (the HIP library or the
+ * diff_gaussian_rasterization package) links, imports or calls this file.  Only
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use it, as the
+ * checker / the reported CPU baseline.
+ *
+ * Provenance.  The rasterizer source (git submodule submodules/hierarchy-rasterizer,
+ * .gitmodules:5-7 of the reference) is NOT vendored in /root/reference, so this is a
+ * restatement of the published graphdeco 3DGS / hierarchy-rasterizer algorithm
+ * (SURVEY.md section 8(a) rows A4-A11), pinned where the reference holds code:
+ *   - SH constants + polynomial      utils/sh_utils.py:26-112, +0.5/clamp at
+ *                                    gaussian_renderer/__init__.py:89
+ *   - cov3D = (R S)(R S)^T, 6-pack    scene/gaussian_model.py:33-37,
+ *                                    utils/general_utils.py:68-114
+ *   - matrix conventions             scene/cameras.py:96-99, utils/graphics_utils.py:38-83
+ *   - boundary contract              gaussian_renderer/__init__.py:44-62,105-113
+ * Golden vectors generated from those reference helpers live in tests/golden/.
+ *
+ * Floating point: compiled with -ffp-contract=off; every expression is written in
+ * the exact operation order the HIP kernels use, so the integer outputs (radii,
+ * tile rects, 64-bit keys, sort order, tile ranges) are bit-identical and the float
+ * outputs differ only through expf() ulps.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define BLOCK_X 16
+#define BLOCK_Y 16
+
+/* utils/sh_utils.py:26-43 */
+static const float SH_C0 = 0.28209479177387814f;
+static const float SH_C1 = 0.4886025119029199f;
+static const float SH_C2[5] = {1.0925484305920792f, -1.0925484305920792f, 0.31539156525252005f,
+                               -1.0925484305920792f, 0.5462742152960396f};
+static const float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457994644658f,
+                               0.3731763325901154f, -0.4570457994644658f, 1.445305721320277f,
+                               -0.5900435899266435f};
+
+typedef struct { float x, y, z; } f3;
+
+static inline float fminf_(float a, float b) { return a < b ? a : b; }
+static inline float fmaxf_(float a, float b) { return a > b ? a : b; }
+
+/* column-major 4x4 (torch row-major of W2C^T, scene/cameras.py:96-98) */
+static inline f3 xf_point43(const float *p, const float *m) {
+    f3 r;
+    r.x = m[0] * p[0] + m[4] * p[1] + m[8] * p[2] + m[12];
+    r.y = m[1] * p[0] + m[5] * p[1] + m[9] * p[2] + m[13];
+    r.z = m[2] * p[0] + m[6] * p[1] + m[10] * p[2] + m[14];
+    return r;
+}
+static inline void xf_point44(const float *p, const float *m, float out[4]) {
+    out[0] = m[0] * p[0] + m[4] * p[1] + m[8] * p[2] + m[12];
+    out[1] = m[1] * p[0] + m[5] * p[1] + m[9] * p[2] + m[13];
+    out[2] = m[2] * p[0] + m[6] * p[1] + m[10] * p[2] + m[14];
+    out[3] = m[3] * p[0] + m[7] * p[1] + m[11] * p[2] + m[15];
+}
+
+/* ndc -> pixel, evaluated in double exactly as upstream's ((v + 1.0) * S - 1.0) * 0.5 */
+static inline float ndc2pix(float v, int S) { return (float)((((double)v + 1.0) * (double)S - 1.0) * 0.5); }
+
+static inline void get_rect(float px, float py, int r, int gx, int gy, int rmin[2], int rmax[2]) {
+    int a;
+    a = (int)((px - (float)r) / (float)BLOCK_X); a = a > 0 ? a : 0; rmin[0] = a < gx ? a : gx;
+    a = (int)((py - (float)r) / (float)BLOCK_Y); a = a > 0 ? a : 0; rmin[1] = a < gy ? a : gy;
+    a = (int)((px + (float)r + (float)(BLOCK_X - 1)) / (float)BLOCK_X); a = a > 0 ? a : 0; rmax[0] = a < gx ? a : gx;
+    a = (int)((py + (float)r + (float)(BLOCK_Y - 1)) / (float)BLOCK_Y); a = a > 0 ? a : 0; rmax[1] = a < gy ? a : gy;
+}
+
+/* cov3D (upper triangle xx,xy,xz,yy,yz,zz) of (R S)(R S)^T; q = (r,x,y,z) used as given */
+static void cov3d_from_scale_rot(const float *s_in, float mod, const float *q, float cov[6]) {
+    float sx = mod * s_in[0], sy = mod * s_in[1], sz = mod * s_in[2];
+    float r = q[0], x = q[1], y = q[2], z = q[3];
+    float R[3][3];
+    R[0][0] = 1.f - 2.f * (y * y + z * z); R[0][1] = 2.f * (x * y - r * z); R[0][2] = 2.f * (x * z + r * y);
+    R[1][0] = 2.f * (x * y + r * z); R[1][1] = 1.f - 2.f * (x * x + z * z); R[1][2] = 2.f * (y * z - r * x);
+    R[2][0] = 2.f * (x * z - r * y); R[2][1] = 2.f * (y * z + r * x); R[2][2] = 1.f - 2.f * (x * x + y * y);
+    float L[3][3];
+    for (int i = 0; i < 3; i++) { L[i][0] = R[i][0] * sx; L[i][1] = R[i][1] * sy; L[i][2] = R[i][2] * sz; }
+    cov[0] = L[0][0] * L[0][0] + L[0][1] * L[0][1] + L[0][2] * L[0][2];
+    cov[1] = L[0][0] * L[1][0] + L[0][1] * L[1][1] + L[0][2] * L[1][2];
+    cov[2] = L[0][0] * L[2][0] + L[0][1] * L[2][1] + L[0][2] * L[2][2];
+    cov[3] = L[1][0] * L[1][0] + L[1][1] * L[1][1] + L[1][2] * L[1][2];
+    cov[4] = L[1][0] * L[2][0] + L[1][1] * L[2][1] + L[1][2] * L[2][2];
+    cov[5] = L[2][0] * L[2][0] + L[2][1] * L[2][1] + L[2][2] * L[2][2];
+}
+
+/* m0,m1 = first two rows of J*W (EWA Jacobian times view rotation); t = view-space mean
+ * with the x/y clamp of 1.3*tanfov applied the upstream way: t.x = clamp(tx/tz)*tz. */
+static void ewa_rows(const float *mean, const float *view, float fx, float fy, float tanx, float tany,
+                     float m0[3], float m1[3], f3 *t_out, float *xmul, float *ymul) {
+    f3 t = xf_point43(mean, view);
+    const float limx = 1.3f * tanx, limy = 1.3f * tany;
+    const float txtz = t.x / t.z, tytz = t.y / t.z;
+    *xmul = (txtz < -limx || txtz > limx) ? 0.f : 1.f;
+    *ymul = (tytz < -limy || tytz > limy) ? 0.f : 1.f;
+    t.x = fminf_(limx, fmaxf_(-limx, txtz)) * t.z;
+    t.y = fminf_(limy, fmaxf_(-limy, tytz)) * t.z;
+    const float j00 = fx / t.z, j02 = -(fx * t.x) / (t.z * t.z);
+    const float j11 = fy / t.z, j12 = -(fy * t.y) / (t.z * t.z);
+    /* view rotation rows: W[r][c] = view[4c + r] */
+    for (int c = 0; c < 3; c++) {
+        m0[c] = j00 * view[4 * c + 0] + j02 * view[4 * c + 2];
+        m1[c] = j11 * view[4 * c + 1] + j12 * view[4 * c + 2];
+    }
+    *t_out = t;
+}
+
+static inline float quad(const float a[3], const float *cov, const float b[3]) {
+    /* a^T Sigma b with Sigma from the 6-pack */
+    float s0 = cov[0] * b[0] + cov[1] * b[1] + cov[2] * b[2];
+    float s1 = cov[1] * b[0] + cov[3] * b[1] + cov[4] * b[2];
+    float s2 = cov[2] * b[0] + cov[4] * b[1] + cov[5] * b[2];
+    return a[0] * s0 + a[1] * s1 + a[2] * s2;
+}
+
+static void sh_to_rgb(int deg, int M, const float *sh /*M*3*/, const float dir[3], float out[3], unsigned char clamp[3]) {
+    float x = dir[0], y = dir[1], z = dir[2];
+    for (int ch = 0; ch < 3; ch++) {
+        float r = SH_C0 * sh[ch];
+        if (deg > 0) {
+            r = r - SH_C1 * y * sh[1 * 3 + ch] + SH_C1 * z * sh[2 * 3 + ch] - SH_C1 * x * sh[3 * 3 + ch];
+            if (deg > 1) {
+                float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+                r = r + SH_C2[0] * xy * sh[4 * 3 + ch] + SH_C2[1] * yz * sh[5 * 3 + ch] +
+                    SH_C2[2] * (2.0f * zz - xx - yy) * sh[6 * 3 + ch] + SH_C2[3] * xz * sh[7 * 3 + ch] +
+                    SH_C2[4] * (xx - yy) * sh[8 * 3 + ch];
+                if (deg > 2) {
+                    r = r + SH_C3[0] * y * (3.0f * xx - yy) * sh[9 * 3 + ch] + SH_C3[1] * xy * z * sh[10 * 3 + ch] +
+                        SH_C3[2] * y * (4.0f * zz - xx - yy) * sh[11 * 3 + ch] +
+                        SH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * sh[12 * 3 + ch] +
+                        SH_C3[4] * x * (4.0f * zz - xx - yy) * sh[13 * 3 + ch] + SH_C3[5] * z * (xx - yy) * sh[14 * 3 + ch] +
+                        SH_C3[6] * x * (xx - 3.0f * yy) * sh[15 * 3 + ch];
+                }
+            }
+        }
+        r += 0.5f;
+        clamp[ch] = r < 0.f;
+        out[ch] = r < 0.f ? 0.f : r;
+    }
+    (void)M;
+}
+
+static inline void sh_dir(const float *mean, const float *campos, float dir[3], float dir_orig[3]) {
+    dir_orig[0] = mean[0] - campos[0];
+    dir_orig[1] = mean[1] - campos[1];
+    dir_orig[2] = mean[2] - campos[2];
+    float len = sqrtf(dir_orig[0] * dir_orig[0] + dir_orig[1] * dir_orig[1] + dir_orig[2] * dir_orig[2]);
+    dir[0] = dir_orig[0] / len; dir[1] = dir_orig[1] / len; dir[2] = dir_orig[2] / len;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Forward preprocess.  Outputs per Gaussian; radii==0 marks culled.
+ * ------------------------------------------------------------------------------------------ */
+void gso_preprocess(int P, int D, int M, const float *means3D, const float *scales, float mod,
+                    const float *rotations, const float *opacities, const float *shs,
+                    const float *colors_precomp, const float *cov3D_precomp, const float *view,
+                    const float *proj, const float *campos, int W, int H, float tanx, float tany,
+                    int *radii, float *depths, float *xy, float *conic_opacity, float *rgb,
+                    unsigned char *clamped, float *cov3D, unsigned int *tiles_touched) {
+    const float fy = (float)H / (2.0f * tany);
+    const float fx = (float)W / (2.0f * tanx);
+    const int gx = (W + BLOCK_X - 1) / BLOCK_X, gy = (H + BLOCK_Y - 1) / BLOCK_Y;
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < P; i++) {
+        radii[i] = 0;
+        tiles_touched[i] = 0;
+        const float *p = means3D + 3 * i;
+        f3 pv = xf_point43(p, view);
+        if (pv.z <= 0.2f) continue;
+        float ph[4];
+        xf_point44(p, proj, ph);
+        float pw = 1.0f / (ph[3] + 0.0000001f);
+        float ndcx = ph[0] * pw, ndcy = ph[1] * pw;
+        float c3[6];
+        if (cov3D_precomp) memcpy(c3, cov3D_precomp + 6 * i, sizeof(c3));
+        else cov3d_from_scale_rot(scales + 3 * i, mod, rotations + 4 * i, c3);
+        memcpy(cov3D + 6 * i, c3, sizeof(c3));
+        float m0[3], m1[3], xm, ym; f3 t;
+        ewa_rows(p, view, fx, fy, tanx, tany, m0, m1, &t, &xm, &ym);
+        float ca = quad(m0, c3, m0) + 0.3f;
+        float cb = quad(m0, c3, m1);
+        float cc = quad(m1, c3, m1) + 0.3f;
+        float det = ca * cc - cb * cb;
+        if (det == 0.0f) continue;
+        float det_inv = 1.f / det;
+        float mid = 0.5f * (ca + cc);
+        float lambda1 = mid + sqrtf(fmaxf_(0.1f, mid * mid - det));
+        float radius = ceilf(3.f * sqrtf(lambda1));
+        float px = ndc2pix(ndcx, W), py = ndc2pix(ndcy, H);
+        int rmin[2], rmax[2];
+        get_rect(px, py, (int)radius, gx, gy, rmin, rmax);
+        int area = (rmax[0] - rmin[0]) * (rmax[1] - rmin[1]);
+        if (area == 0) continue;
+        if (!colors_precomp) {
+            float dir[3], dor[3];
+            sh_dir(p, campos, dir, dor);
+            sh_to_rgb(D, M, shs + (size_t)i * M * 3, dir, rgb + 3 * i, clamped + 3 * i);
+        } else {
+            rgb[3 * i + 0] = colors_precomp[3 * i + 0];
+            rgb[3 * i + 1] = colors_precomp[3 * i + 1];
+            rgb[3 * i + 2] = colors_precomp[3 * i + 2];
+            clamped[3 * i + 0] = clamped[3 * i + 1] = clamped[3 * i + 2] = 0;
+        }
+        depths[i] = pv.z;
+        radii[i] = (int)radius;
+        xy[2 * i] = px; xy[2 * i + 1] = py;
+        conic_opacity[4 * i + 0] = cc * det_inv;
+        conic_opacity[4 * i + 1] = -cb * det_inv;
+        conic_opacity[4 * i + 2] = ca * det_inv;
+        conic_opacity[4 * i + 3] = opacities[i];
+        tiles_touched[i] = (unsigned)area;
+    }
+}
+
+/* markVisible: frustum test only */
+void gso_mark_visible(int P, const float *means3D, const float *view, const float *proj, unsigned char *out) {
+    (void)proj;
+    for (int i = 0; i < P; i++) {
+        f3 pv = xf_point43(means3D + 3 * i, view);
+        out[i] = pv.z > 0.2f;
+    }
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Binning (A5-A8): inclusive scan, duplicate with 64-bit keys (tile<<32 | depth bits),
+ * stable sort, tile ranges.
+ * ------------------------------------------------------------------------------------------ */
+unsigned long long gso_scan(int P, const unsigned int *tiles_touched, unsigned int *offsets_incl) {
+    unsigned long long acc = 0;
+    for (int i = 0; i < P; i++) { acc += tiles_touched[i]; offsets_incl[i] = (unsigned int)acc; }
+    return acc;
+}
+
+void gso_duplicate(int P, const float *xy, const int *radii, const float *depths,
+                   const unsigned int *offsets_incl, int W, int H,
+                   unsigned long long *keys, unsigned int *vals) {
+    const int gx = (W + BLOCK_X - 1) / BLOCK_X, gy = (H + BLOCK_Y - 1) / BLOCK_Y;
+    for (int i = 0; i < P; i++) {
+        if (radii[i] <= 0) continue;
+        unsigned int off = i == 0 ? 0 : offsets_incl[i - 1];
+        int rmin[2], rmax[2];
+        get_rect(xy[2 * i], xy[2 * i + 1], radii[i], gx, gy, rmin, rmax);
+        uint32_t dbits; memcpy(&dbits, depths + i, 4);
+        for (int y = rmin[1]; y < rmax[1]; y++)
+            for (int x = rmin[0]; x < rmax[0]; x++) {
+                keys[off] = ((unsigned long long)(y * gx + x) << 32) | dbits;
+                vals[off] = (unsigned)i;
+                off++;
+            }
+    }
+}
+
+typedef struct { unsigned long long k; unsigned int v; unsigned int pos; } kv_t;
+static int kv_cmp(const void *a, const void *b) {
+    const kv_t *x = a, *y = b;
+    if (x->k != y->k) return x->k < y->k ? -1 : 1;
+    return x->pos < y->pos ? -1 : (x->pos > y->pos);
+}
+/* stable (LSD-radix equivalent) sort of (key, value) pairs */
+void gso_sort(unsigned long long K, unsigned long long *keys, unsigned int *vals) {
+    kv_t *t = (kv_t *)malloc(sizeof(kv_t) * (K ? K : 1));
+    for (unsigned long long i = 0; i < K; i++) { t[i].k = keys[i]; t[i].v = vals[i]; t[i].pos = (unsigned)i; }
+    qsort(t, K, sizeof(kv_t), kv_cmp);
+    for (unsigned long long i = 0; i < K; i++) { keys[i] = t[i].k; vals[i] = t[i].v; }
+    free(t);
+}
+
+void gso_ranges(unsigned long long K, const unsigned long long *keys, int T, unsigned int *ranges) {
+    memset(ranges, 0, sizeof(unsigned) * 2 * (size_t)T);
+    for (unsigned long long i = 0; i < K; i++) {
+        unsigned cur = (unsigned)(keys[i] >> 32);
+        if (i == 0) ranges[2 * cur] = 0;
+        else {
+            unsigned prev = (unsigned)(keys[i - 1] >> 32);
+            if (cur != prev) { ranges[2 * prev + 1] = (unsigned)i; ranges[2 * cur] = (unsigned)i; }
+        }
+        if (i == K - 1) ranges[2 * cur + 1] = (unsigned)K;
+    }
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Render forward (A9): per tile front-to-back alpha blending, colour + inverse depth.
+ * ------------------------------------------------------------------------------------------ */
+void gso_render_fwd(int W, int H, const unsigned int *ranges, const unsigned int *point_list,
+                    const float *xy, const float *conic_opacity, const float *rgb, const float *depths,
+                    const float *bg, int do_depth, float *out_color, float *out_invdepth,
+                    float *final_T, unsigned int *n_contrib) {
+    const int gx = (W + BLOCK_X - 1) / BLOCK_X, gy = (H + BLOCK_Y - 1) / BLOCK_Y;
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int tile = 0; tile < gx * gy; tile++) {
+        int tx = tile % gx, ty = tile / gx;
+        unsigned rs = ranges[2 * tile], re = ranges[2 * tile + 1];
+        for (int ly = 0; ly < BLOCK_Y; ly++)
+            for (int lx = 0; lx < BLOCK_X; lx++) {
+                int px = tx * BLOCK_X + lx, py = ty * BLOCK_Y + ly;
+                if (px >= W || py >= H) continue;
+                float pfx = (float)px, pfy = (float)py;
+                float T = 1.0f, C0 = 0, C1 = 0, C2 = 0, ID = 0;
+                unsigned contributor = 0, last = 0;
+                for (unsigned s = rs; s < re; s++) {
+                    contributor++;
+                    unsigned g = point_list[s];
+                    float dx = xy[2 * g] - pfx, dy = xy[2 * g + 1] - pfy;
+                    const float *co = conic_opacity + 4 * g;
+                    float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                    if (power > 0.0f) continue;
+                    float alpha = fminf_(0.99f, co[3] * expf(power));
+                    if (alpha < 1.0f / 255.0f) continue;
+                    float test_T = T * (1.f - alpha);
+                    if (test_T < 0.0001f) break;
+                    float w = alpha * T;
+                    C0 += rgb[3 * g + 0] * w;
+                    C1 += rgb[3 * g + 1] * w;
+                    C2 += rgb[3 * g + 2] * w;
+                    if (do_depth) ID += (1.f / depths[g]) * w;
+                    T = test_T;
+                    last = contributor;
+                }
+                int pix = py * W + px;
+                final_T[pix] = T;
+                n_contrib[pix] = last;
+                out_color[0 * H * W + pix] = C0 + T * bg[0];
+                out_color[1 * H * W + pix] = C1 + T * bg[1];
+                out_color[2 * H * W + pix] = C2 + T * bg[2];
+                if (do_depth) out_invdepth[pix] = ID;
+            }
+    }
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Render backward (A10): back-to-front replay.  Gradients are accumulated per tile-instance
+ * (sorted position s) into inst[s*10 + k], summing that tile's pixels in row-major order:
+ *   k: 0,1 dL/dmean2D (NDC-scaled, x0.5W / x0.5H)   2,3,4 dL/dconic (upstream convention:
+ *   off-diagonal carries -0.5*G*dx*dy*dL_dG)   5 dL/dopacity   6,7,8 dL/drgb   9 dL/dinvdepth
+ * ------------------------------------------------------------------------------------------ */
+void gso_render_bwd(int W, int H, const unsigned int *ranges, const unsigned int *point_list,
+                    const float *xy, const float *conic_opacity, const float *rgb, const float *depths,
+                    const float *bg, const float *final_T, const unsigned int *n_contrib,
+                    const float *dL_dpix /*3HW*/, const float *dL_dinvd /*HW or NULL*/, float *inst) {
+    const int gx = (W + BLOCK_X - 1) / BLOCK_X, gy = (H + BLOCK_Y - 1) / BLOCK_Y;
+    const float ddelx_dx = 0.5f * (float)W, ddely_dy = 0.5f * (float)H;
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int tile = 0; tile < gx * gy; tile++) {
+        int tx = tile % gx, ty = tile / gx;
+        unsigned rs = ranges[2 * tile], re = ranges[2 * tile + 1];
+        for (unsigned s = rs; s < re; s++) memset(inst + (size_t)s * 10, 0, 10 * sizeof(float));
+        for (int ly = 0; ly < BLOCK_Y; ly++)
+            for (int lx = 0; lx < BLOCK_X; lx++) {
+                int px = tx * BLOCK_X + lx, py = ty * BLOCK_Y + ly;
+                if (px >= W || py >= H) continue;
+                int pix = py * W + px;
+                float pfx = (float)px, pfy = (float)py;
+                const float T_final = final_T[pix];
+                float T = T_final;
+                unsigned last = n_contrib[pix];
+                float dp[3] = {dL_dpix[pix], dL_dpix[H * W + pix], dL_dpix[2 * H * W + pix]};
+                float dID = dL_dinvd ? dL_dinvd[pix] : 0.f;
+                float acc[3] = {0, 0, 0}, acc_id = 0, last_alpha = 0, last_c[3] = {0, 0, 0}, last_id = 0;
+                float bg_dot = bg[0] * dp[0] + bg[1] * dp[1] + bg[2] * dp[2];
+                unsigned contributor = re - rs;
+                for (unsigned s = re; s-- > rs;) {
+                    contributor--;
+                    if (contributor >= last) continue;
+                    unsigned g = point_list[s];
+                    float dx = xy[2 * g] - pfx, dy = xy[2 * g + 1] - pfy;
+                    const float *co = conic_opacity + 4 * g;
+                    float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                    if (power > 0.0f) continue;
+                    float G = expf(power);
+                    float alpha = fminf_(0.99f, co[3] * G);
+                    if (alpha < 1.0f / 255.0f) continue;
+                    T = T / (1.f - alpha);
+                    float dchannel = alpha * T;
+                    float dL_dalpha = 0.f;
+                    float *gi = inst + (size_t)s * 10;
+                    for (int ch = 0; ch < 3; ch++) {
+                        float c = rgb[3 * g + ch];
+                        acc[ch] = last_alpha * last_c[ch] + (1.f - last_alpha) * acc[ch];
+                        last_c[ch] = c;
+                        dL_dalpha += (c - acc[ch]) * dp[ch];
+                        gi[6 + ch] += dchannel * dp[ch];
+                    }
+                    if (dL_dinvd) {
+                        float invd = 1.f / depths[g];
+                        acc_id = last_alpha * last_id + (1.f - last_alpha) * acc_id;
+                        last_id = invd;
+                        dL_dalpha += (invd - acc_id) * dID;
+                        gi[9] += dchannel * dID;
+                    }
+                    dL_dalpha *= T;
+                    last_alpha = alpha;
+                    dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
+                    float dL_dG = co[3] * dL_dalpha;
+                    float gdx = G * dx, gdy = G * dy;
+                    float dG_ddelx = -gdx * co[0] - gdy * co[1];
+                    float dG_ddely = -gdy * co[2] - gdx * co[1];
+                    gi[0] += dL_dG * dG_ddelx * ddelx_dx;
+                    gi[1] += dL_dG * dG_ddely * ddely_dy;
+                    gi[2] += -0.5f * gdx * dx * dL_dG;
+                    gi[3] += -0.5f * gdx * dy * dL_dG;
+                    gi[4] += -0.5f * gdy * dy * dL_dG;
+                    gi[5] += G * dL_dalpha;
+                }
+            }
+    }
+}
+
+/* per-Gaussian sum of its tile-instance gradients, in sorted-list order */
+void gso_reduce_instances(int P, unsigned long long K, const unsigned int *point_list, const float *inst, float *g10) {
+    memset(g10, 0, sizeof(float) * 10 * (size_t)P);
+    for (unsigned long long s = 0; s < K; s++) {
+        float *d = g10 + 10 * (size_t)point_list[s];
+        const float *a = inst + 10 * s;
+        for (int k = 0; k < 10; k++) d[k] += a[k];
+    }
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Preprocess backward (A11).  g10 = per-Gaussian reduced render gradients (see above).
+ * Writes every output row (zeros where radii==0 / beyond the active SH degree).
+ * ------------------------------------------------------------------------------------------ */
+void gso_preprocess_bwd(int P, int D, int M, const float *means3D, const int *radii, const float *shs,
+                        const unsigned char *clamped, const float *scales, const float *rotations,
+                        float mod, const float *cov3D /*P*6 as produced in fwd*/, const float *view,
+                        const float *proj, const float *campos, int W, int H, float tanx, float tany,
+                        const float *g10, int has_shs, int has_scales,
+                        float *dL_dmeans3D, float *dL_dmeans2D, float *dL_dcolors, float *dL_dopacity,
+                        float *dL_dcov3D, float *dL_dsh, float *dL_dscales, float *dL_drots) {
+    const float fy = (float)H / (2.0f * tany);
+    const float fx = (float)W / (2.0f * tanx);
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < P; i++) {
+        float *dm3 = dL_dmeans3D + 3 * i;
+        dm3[0] = dm3[1] = dm3[2] = 0.f;
+        dL_dmeans2D[3 * i] = dL_dmeans2D[3 * i + 1] = dL_dmeans2D[3 * i + 2] = 0.f;
+        dL_dcolors[3 * i] = dL_dcolors[3 * i + 1] = dL_dcolors[3 * i + 2] = 0.f;
+        dL_dopacity[i] = 0.f;
+        for (int k = 0; k < 6; k++) dL_dcov3D[6 * i + k] = 0.f;
+        if (has_shs) for (int k = 0; k < M * 3; k++) dL_dsh[(size_t)i * M * 3 + k] = 0.f;
+        if (has_scales) {
+            for (int k = 0; k < 3; k++) dL_dscales[3 * i + k] = 0.f;
+            for (int k = 0; k < 4; k++) dL_drots[4 * i + k] = 0.f;
+        }
+        if (!(radii[i] > 0)) continue;
+        const float *g = g10 + 10 * (size_t)i;
+        const float *p = means3D + 3 * i;
+        dL_dmeans2D[3 * i] = g[0];
+        dL_dmeans2D[3 * i + 1] = g[1];
+        dL_dopacity[i] = g[5];
+
+        /* ---- conic -> cov2D -> cov3D and mean (computeCov2D backward) ---- */
+        const float *c3 = cov3D + 6 * i;
+        float m0[3], m1[3], xm, ym; f3 t;
+        ewa_rows(p, view, fx, fy, tanx, tany, m0, m1, &t, &xm, &ym);
+        float a = quad(m0, c3, m0) + 0.3f;
+        float b = quad(m0, c3, m1);
+        float c = quad(m1, c3, m1) + 0.3f;
+        float gca = g[2], gcb = g[3], gcc = g[4];
+        float denom = a * c - b * b;
+        float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+        float dL_da = 0.f, dL_db = 0.f, dL_dc = 0.f;
+        float dcov[6] = {0, 0, 0, 0, 0, 0};
+        if (denom2inv != 0.f) {
+            dL_da = denom2inv * (-c * c * gca + 2.f * b * c * gcb + (denom - a * c) * gcc);
+            dL_dc = denom2inv * (-a * a * gcc + 2.f * a * b * gcb + (denom - a * c) * gca);
+            dL_db = denom2inv * 2.f * (b * c * gca - (denom + 2.f * b * b) * gcb + a * b * gcc);
+            dcov[0] = m0[0] * m0[0] * dL_da + m0[0] * m1[0] * dL_db + m1[0] * m1[0] * dL_dc;
+            dcov[3] = m0[1] * m0[1] * dL_da + m0[1] * m1[1] * dL_db + m1[1] * m1[1] * dL_dc;
+            dcov[5] = m0[2] * m0[2] * dL_da + m0[2] * m1[2] * dL_db + m1[2] * m1[2] * dL_dc;
+            dcov[1] = 2.f * m0[0] * m0[1] * dL_da + (m0[0] * m1[1] + m0[1] * m1[0]) * dL_db + 2.f * m1[0] * m1[1] * dL_dc;
+            dcov[2] = 2.f * m0[0] * m0[2] * dL_da + (m0[0] * m1[2] + m0[2] * m1[0]) * dL_db + 2.f * m1[0] * m1[2] * dL_dc;
+            dcov[4] = 2.f * m0[2] * m0[1] * dL_da + (m0[1] * m1[2] + m0[2] * m1[1]) * dL_db + 2.f * m1[1] * m1[2] * dL_dc;
+        }
+        /* dL/dm0, dL/dm1 (rows of T = J W):  A = m0 S m0, B = m0 S m1, C = m1 S m1 */
+        float Sm0[3], Sm1[3];
+        Sm0[0] = c3[0] * m0[0] + c3[1] * m0[1] + c3[2] * m0[2];
+        Sm0[1] = c3[1] * m0[0] + c3[3] * m0[1] + c3[4] * m0[2];
+        Sm0[2] = c3[2] * m0[0] + c3[4] * m0[1] + c3[5] * m0[2];
+        Sm1[0] = c3[0] * m1[0] + c3[1] * m1[1] + c3[2] * m1[2];
+        Sm1[1] = c3[1] * m1[0] + c3[3] * m1[1] + c3[4] * m1[2];
+        Sm1[2] = c3[2] * m1[0] + c3[4] * m1[1] + c3[5] * m1[2];
+        float dm0[3], dm1[3];
+        for (int k = 0; k < 3; k++) {
+            dm0[k] = 2.f * Sm0[k] * dL_da + Sm1[k] * dL_db;
+            dm1[k] = 2.f * Sm1[k] * dL_dc + Sm0[k] * dL_db;
+        }
+        /* m0 = j00*W0 + j02*W2,  m1 = j11*W1 + j12*W2  (W_r[c] = view[4c + r]) */
+        float dj00 = view[0] * dm0[0] + view[4] * dm0[1] + view[8] * dm0[2];
+        float dj02 = view[2] * dm0[0] + view[6] * dm0[1] + view[10] * dm0[2];
+        float dj11 = view[1] * dm1[0] + view[5] * dm1[1] + view[9] * dm1[2];
+        float dj12 = view[2] * dm1[0] + view[6] * dm1[1] + view[10] * dm1[2];
+        float tz = 1.f / t.z, tz2 = tz * tz, tz3 = tz2 * tz;
+        float dtx = xm * -fx * tz2 * dj02;
+        float dty = ym * -fy * tz2 * dj12;
+        float dtz = -fx * tz2 * dj00 - fy * tz2 * dj11 + (2.f * fx * t.x) * tz3 * dj02 + (2.f * fy * t.y) * tz3 * dj12;
+        dm3[0] = view[0] * dtx + view[1] * dty + view[2] * dtz;
+        dm3[1] = view[4] * dtx + view[5] * dty + view[6] * dtz;
+        dm3[2] = view[8] * dtx + view[9] * dty + view[10] * dtz;
+
+        /* ---- screen-space mean -> mean3D through projmatrix ---- */
+        float mh[4];
+        xf_point44(p, proj, mh);
+        float mw = 1.0f / (mh[3] + 0.0000001f);
+        float mul1 = mh[0] * mw * mw, mul2 = mh[1] * mw * mw;
+        dm3[0] += (proj[0] * mw - proj[3] * mul1) * g[0] + (proj[1] * mw - proj[3] * mul2) * g[1];
+        dm3[1] += (proj[4] * mw - proj[7] * mul1) * g[0] + (proj[5] * mw - proj[7] * mul2) * g[1];
+        dm3[2] += (proj[8] * mw - proj[11] * mul1) * g[0] + (proj[9] * mw - proj[11] * mul2) * g[1];
+
+        /* ---- inverse depth -> mean3D:  invd = 1/z_view ---- */
+        {
+            f3 pv = xf_point43(p, view);
+            float dz = -g[9] / (pv.z * pv.z);
+            dm3[0] += dz * view[2];
+            dm3[1] += dz * view[6];
+            dm3[2] += dz * view[10];
+        }
+
+        /* ---- colour ---- */
+        if (has_shs) {
+            float dir[3], dor[3];
+            sh_dir(p, campos, dir, dor);
+            const float *sh = shs + (size_t)i * M * 3;
+            float *dsh = dL_dsh + (size_t)i * M * 3;
+            float dRGB[3];
+            for (int ch = 0; ch < 3; ch++) dRGB[ch] = clamped[3 * i + ch] ? 0.f : g[6 + ch];
+            float x = dir[0], y = dir[1], z = dir[2];
+            float ddx[3] = {0, 0, 0}, ddy[3] = {0, 0, 0}, ddz[3] = {0, 0, 0};
+            for (int ch = 0; ch < 3; ch++) {
+                float gc = dRGB[ch];
+                dsh[ch] = SH_C0 * gc;
+                if (D > 0) {
+                    dsh[1 * 3 + ch] = -SH_C1 * y * gc;
+                    dsh[2 * 3 + ch] = SH_C1 * z * gc;
+                    dsh[3 * 3 + ch] = -SH_C1 * x * gc;
+                    ddx[ch] = -SH_C1 * sh[3 * 3 + ch];
+                    ddy[ch] = -SH_C1 * sh[1 * 3 + ch];
+                    ddz[ch] = SH_C1 * sh[2 * 3 + ch];
+                    if (D > 1) {
+                        float xx = x * x, yy = y * y, zz = z * z, xy_ = x * y, yz = y * z, xz = x * z;
+                        dsh[4 * 3 + ch] = SH_C2[0] * xy_ * gc;
+                        dsh[5 * 3 + ch] = SH_C2[1] * yz * gc;
+                        dsh[6 * 3 + ch] = SH_C2[2] * (2.f * zz - xx - yy) * gc;
+                        dsh[7 * 3 + ch] = SH_C2[3] * xz * gc;
+                        dsh[8 * 3 + ch] = SH_C2[4] * (xx - yy) * gc;
+                        ddx[ch] += SH_C2[0] * y * sh[4 * 3 + ch] + SH_C2[2] * 2.f * -x * sh[6 * 3 + ch] +
+                                   SH_C2[3] * z * sh[7 * 3 + ch] + SH_C2[4] * 2.f * x * sh[8 * 3 + ch];
+                        ddy[ch] += SH_C2[0] * x * sh[4 * 3 + ch] + SH_C2[1] * z * sh[5 * 3 + ch] +
+                                   SH_C2[2] * 2.f * -y * sh[6 * 3 + ch] + SH_C2[4] * 2.f * -y * sh[8 * 3 + ch];
+                        ddz[ch] += SH_C2[1] * y * sh[5 * 3 + ch] + SH_C2[2] * 2.f * 2.f * z * sh[6 * 3 + ch] +
+                                   SH_C2[3] * x * sh[7 * 3 + ch];
+                        if (D > 2) {
+                            dsh[9 * 3 + ch] = SH_C3[0] * y * (3.f * xx - yy) * gc;
+                            dsh[10 * 3 + ch] = SH_C3[1] * xy_ * z * gc;
+                            dsh[11 * 3 + ch] = SH_C3[2] * y * (4.f * zz - xx - yy) * gc;
+                            dsh[12 * 3 + ch] = SH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy) * gc;
+                            dsh[13 * 3 + ch] = SH_C3[4] * x * (4.f * zz - xx - yy) * gc;
+                            dsh[14 * 3 + ch] = SH_C3[5] * z * (xx - yy) * gc;
+                            dsh[15 * 3 + ch] = SH_C3[6] * x * (xx - 3.f * yy) * gc;
+                            ddx[ch] += SH_C3[0] * sh[9 * 3 + ch] * 3.f * 2.f * xy_ +
+                                       SH_C3[1] * sh[10 * 3 + ch] * yz +
+                                       SH_C3[2] * sh[11 * 3 + ch] * -2.f * xy_ +
+                                       SH_C3[3] * sh[12 * 3 + ch] * -3.f * 2.f * xz +
+                                       SH_C3[4] * sh[13 * 3 + ch] * (-3.f * xx + 4.f * zz - yy) +
+                                       SH_C3[5] * sh[14 * 3 + ch] * 2.f * xz +
+                                       SH_C3[6] * sh[15 * 3 + ch] * 3.f * (xx - yy);
+                            ddy[ch] += SH_C3[0] * sh[9 * 3 + ch] * 3.f * (xx - yy) +
+                                       SH_C3[1] * sh[10 * 3 + ch] * xz +
+                                       SH_C3[2] * sh[11 * 3 + ch] * (-3.f * yy + 4.f * zz - xx) +
+                                       SH_C3[3] * sh[12 * 3 + ch] * -3.f * 2.f * yz +
+                                       SH_C3[4] * sh[13 * 3 + ch] * -2.f * xy_ +
+                                       SH_C3[5] * sh[14 * 3 + ch] * -2.f * yz +
+                                       SH_C3[6] * sh[15 * 3 + ch] * -3.f * 2.f * xy_;
+                            ddz[ch] += SH_C3[1] * sh[10 * 3 + ch] * xy_ +
+                                       SH_C3[2] * sh[11 * 3 + ch] * 4.f * 2.f * yz +
+                                       SH_C3[3] * sh[12 * 3 + ch] * 3.f * (2.f * zz - xx - yy) +
+                                       SH_C3[4] * sh[13 * 3 + ch] * 4.f * 2.f * xz +
+                                       SH_C3[5] * sh[14 * 3 + ch] * (xx - yy);
+                        }
+                    }
+                }
+            }
+            float gdir[3];
+            gdir[0] = ddx[0] * dRGB[0] + ddx[1] * dRGB[1] + ddx[2] * dRGB[2];
+            gdir[1] = ddy[0] * dRGB[0] + ddy[1] * dRGB[1] + ddy[2] * dRGB[2];
+            gdir[2] = ddz[0] * dRGB[0] + ddz[1] * dRGB[1] + ddz[2] * dRGB[2];
+            /* d normalize(v) / dv applied to gdir */
+            float s2 = dor[0] * dor[0] + dor[1] * dor[1] + dor[2] * dor[2];
+            float inv32 = 1.0f / sqrtf(s2 * s2 * s2);
+            dm3[0] += ((s2 - dor[0] * dor[0]) * gdir[0] - dor[1] * dor[0] * gdir[1] - dor[2] * dor[0] * gdir[2]) * inv32;
+            dm3[1] += (-dor[0] * dor[1] * gdir[0] + (s2 - dor[1] * dor[1]) * gdir[1] - dor[2] * dor[1] * gdir[2]) * inv32;
+            dm3[2] += (-dor[0] * dor[2] * gdir[0] - dor[1] * dor[2] * gdir[1] + (s2 - dor[2] * dor[2]) * gdir[2]) * inv32;
+        } else {
+            dL_dcolors[3 * i + 0] = g[6];
+            dL_dcolors[3 * i + 1] = g[7];
+            dL_dcolors[3 * i + 2] = g[8];
+        }
+
+        /* ---- cov3D -> scale / rotation ---- */
+        if (has_scales) {
+            const float *q = rotations + 4 * i;
+            float r = q[0], x = q[1], y = q[2], z = q[3];
+            float s[3] = {mod * scales[3 * i], mod * scales[3 * i + 1], mod * scales[3 * i + 2]};
+            float R[3][3];
+            R[0][0] = 1.f - 2.f * (y * y + z * z); R[0][1] = 2.f * (x * y - r * z); R[0][2] = 2.f * (x * z + r * y);
+            R[1][0] = 2.f * (x * y + r * z); R[1][1] = 1.f - 2.f * (x * x + z * z); R[1][2] = 2.f * (y * z - r * x);
+            R[2][0] = 2.f * (x * z - r * y); R[2][1] = 2.f * (y * z + r * x); R[2][2] = 1.f - 2.f * (x * x + y * y);
+            /* G = dL/dSigma with halved off-diagonals; dL/dL = 2 G L, L = R diag(s) */
+            float G3[3][3] = {{dcov[0], 0.5f * dcov[1], 0.5f * dcov[2]},
+                              {0.5f * dcov[1], dcov[3], 0.5f * dcov[4]},
+                              {0.5f * dcov[2], 0.5f * dcov[4], dcov[5]}};
+            float dLL[3][3];
+            for (int rr = 0; rr < 3; rr++)
+                for (int cc = 0; cc < 3; cc++)
+                    dLL[rr][cc] = 2.f * (G3[rr][0] * R[0][cc] * s[cc] + G3[rr][1] * R[1][cc] * s[cc] + G3[rr][2] * R[2][cc] * s[cc]);
+            for (int k = 0; k < 3; k++)
+                dL_dscales[3 * i + k] = mod * (dLL[0][k] * R[0][k] + dLL[1][k] * R[1][k] + dLL[2][k] * R[2][k]);
+            float Gr[3][3];
+            for (int rr = 0; rr < 3; rr++)
+                for (int cc = 0; cc < 3; cc++) Gr[rr][cc] = dLL[rr][cc] * s[cc];
+            dL_drots[4 * i + 0] = 2.f * (-z * Gr[0][1] + y * Gr[0][2] + z * Gr[1][0] - x * Gr[1][2] - y * Gr[2][0] + x * Gr[2][1]);
+            dL_drots[4 * i + 1] = 2.f * (y * Gr[0][1] + z * Gr[0][2] + y * Gr[1][0] - 2.f * x * Gr[1][1] - r * Gr[1][2] +
+                                         z * Gr[2][0] + r * Gr[2][1] - 2.f * x * Gr[2][2]);
+            dL_drots[4 * i + 2] = 2.f * (-2.f * y * Gr[0][0] + x * Gr[0][1] + r * Gr[0][2] + x * Gr[1][0] + z * Gr[1][2] -
+                                         r * Gr[2][0] + z * Gr[2][1] - 2.f * y * Gr[2][2]);
+            dL_drots[4 * i + 3] = 2.f * (-2.f * z * Gr[0][0] - r * Gr[0][1] + x * Gr[0][2] + r * Gr[1][0] - 2.f * z * Gr[1][1] +
+                                         y * Gr[1][2] + x * Gr[2][0] + y * Gr[2][1]);
+        } else {
+            for (int k = 0; k < 6; k++) dL_dcov3D[6 * i + k] = dcov[k];
+        }
+    }
+}
+
+int gso_num_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}

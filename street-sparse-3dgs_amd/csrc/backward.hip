@@ -1,0 +1,271 @@
+// backward.hip -- per-Gaussian backward: sums the Gaussian's
+// per-tile-instance records written by render_bwd (one contiguous run per Gaussian, at its
+// exclusive-scan offset), then chains conic -> 2D covariance -> (3D covariance, mean) with the
+// EWA Jacobian, screen-space mean -> mean3D through projmatrix, inverse depth -> mean3D,
+// SH -> (coefficients, view direction -> mean3D) and 3D covariance -> (scale, rotation).
+// Every output row is written (zeros for culled Gaussians and unused SH coefficients), so
+// the caller's gradient tensors need no memset pass.
+#include "gsr_launch.h"
+
+namespace gsr {
+
+__global__ __launch_bounds__(256) void preprocess_bwd_kernel(
+    int P, int D, int M, const float *__restrict__ means3D, const int *__restrict__ radii,
+    const float *__restrict__ shs, const uint8_t *__restrict__ clamped, const float *__restrict__ scales,
+    const float *__restrict__ rotations, float mod, const float *__restrict__ cov3D_precomp,
+    const float *__restrict__ viewmatrix, const float *__restrict__ projmatrix, const float *__restrict__ campos_p,
+    float tanx, float tany, float fx, float fy, const uint32_t *__restrict__ tiles,
+    const uint32_t *__restrict__ offsets, BwdScratch sc, GaussianGrads out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const bool has_shs = shs != nullptr;
+    const bool has_scales = cov3D_precomp == nullptr;
+    const bool vis = radii[i] > 0;
+
+    float g[10];
+#pragma unroll
+    for (int k = 0; k < 10; k++) g[k] = 0.f;
+    if (vis) {
+        const uint32_t n = tiles[i];
+        const uint32_t off = i == 0 ? 0u : offsets[i - 1];
+        for (uint32_t u = off; u < off + n; u++) {
+            const float4 a = sc.ga[u];
+            const float4 b = sc.gb[u];
+            const float2 c = sc.gc[u];
+            g[0] += a.x; g[1] += a.y; g[2] += a.z; g[3] += a.w;
+            g[4] += b.x; g[5] += b.y; g[6] += b.z; g[7] += b.w;
+            g[8] += c.x; g[9] += c.y;
+        }
+    }
+    out.dmeans2D[3 * i + 0] = g[0];
+    out.dmeans2D[3 * i + 1] = g[1];
+    out.dmeans2D[3 * i + 2] = 0.f;
+    out.dopacity[i] = g[5];
+
+    float dm[3] = {0.f, 0.f, 0.f};
+    float dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const Mat4 V = load_mat4(viewmatrix);
+    const float3 p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
+    float c3[6];
+    float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+    float3 s_in = make_float3(0.f, 0.f, 0.f);
+    if (vis) {
+        // ---- conic -> cov2D -> cov3D and mean ----
+        if (has_scales) {
+            s_in = make_float3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
+            q = reinterpret_cast<const float4 *>(rotations)[i];
+            cov3d_from_scale_rot(s_in, mod, q, c3);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 6; k++) c3[k] = cov3D_precomp[6 * i + k];
+        }
+        const Ewa e = ewa_rows(p, V, fx, fy, tanx, tany);
+        const float a = quad_form(e.m0, c3, e.m0) + 0.3f;
+        const float b = quad_form(e.m0, c3, e.m1);
+        const float c = quad_form(e.m1, c3, e.m1) + 0.3f;
+        const float gca = g[2], gcb = g[3], gcc = g[4];
+        const float denom = a * c - b * b;
+        const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+        float dL_da = 0.f, dL_db = 0.f, dL_dc = 0.f;
+        if (denom2inv != 0.f) {
+            dL_da = denom2inv * (-c * c * gca + 2.f * b * c * gcb + (denom - a * c) * gcc);
+            dL_dc = denom2inv * (-a * a * gcc + 2.f * a * b * gcb + (denom - a * c) * gca);
+            dL_db = denom2inv * 2.f * (b * c * gca - (denom + 2.f * b * b) * gcb + a * b * gcc);
+            const float *m0 = e.m0, *m1 = e.m1;
+            dcov[0] = m0[0] * m0[0] * dL_da + m0[0] * m1[0] * dL_db + m1[0] * m1[0] * dL_dc;
+            dcov[3] = m0[1] * m0[1] * dL_da + m0[1] * m1[1] * dL_db + m1[1] * m1[1] * dL_dc;
+            dcov[5] = m0[2] * m0[2] * dL_da + m0[2] * m1[2] * dL_db + m1[2] * m1[2] * dL_dc;
+            dcov[1] = 2.f * m0[0] * m0[1] * dL_da + (m0[0] * m1[1] + m0[1] * m1[0]) * dL_db +
+                      2.f * m1[0] * m1[1] * dL_dc;
+            dcov[2] = 2.f * m0[0] * m0[2] * dL_da + (m0[0] * m1[2] + m0[2] * m1[0]) * dL_db +
+                      2.f * m1[0] * m1[2] * dL_dc;
+            dcov[4] = 2.f * m0[2] * m0[1] * dL_da + (m0[1] * m1[2] + m0[2] * m1[1]) * dL_db +
+                      2.f * m1[1] * m1[2] * dL_dc;
+        }
+        float Sm0[3], Sm1[3];
+        const float *m0 = e.m0, *m1 = e.m1;
+        Sm0[0] = c3[0] * m0[0] + c3[1] * m0[1] + c3[2] * m0[2];
+        Sm0[1] = c3[1] * m0[0] + c3[3] * m0[1] + c3[4] * m0[2];
+        Sm0[2] = c3[2] * m0[0] + c3[4] * m0[1] + c3[5] * m0[2];
+        Sm1[0] = c3[0] * m1[0] + c3[1] * m1[1] + c3[2] * m1[2];
+        Sm1[1] = c3[1] * m1[0] + c3[3] * m1[1] + c3[4] * m1[2];
+        Sm1[2] = c3[2] * m1[0] + c3[4] * m1[1] + c3[5] * m1[2];
+        float dm0[3], dm1[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            dm0[k] = 2.f * Sm0[k] * dL_da + Sm1[k] * dL_db;
+            dm1[k] = 2.f * Sm1[k] * dL_dc + Sm0[k] * dL_db;
+        }
+        const float *v = V.m;
+        const float dj00 = v[0] * dm0[0] + v[4] * dm0[1] + v[8] * dm0[2];
+        const float dj02 = v[2] * dm0[0] + v[6] * dm0[1] + v[10] * dm0[2];
+        const float dj11 = v[1] * dm1[0] + v[5] * dm1[1] + v[9] * dm1[2];
+        const float dj12 = v[2] * dm1[0] + v[6] * dm1[1] + v[10] * dm1[2];
+        const float tz = 1.f / e.t.z, tz2 = tz * tz, tz3 = tz2 * tz;
+        const float dtx = e.xmul * -fx * tz2 * dj02;
+        const float dty = e.ymul * -fy * tz2 * dj12;
+        const float dtz = -fx * tz2 * dj00 - fy * tz2 * dj11 + (2.f * fx * e.t.x) * tz3 * dj02 +
+                          (2.f * fy * e.t.y) * tz3 * dj12;
+        dm[0] = v[0] * dtx + v[1] * dty + v[2] * dtz;
+        dm[1] = v[4] * dtx + v[5] * dty + v[6] * dtz;
+        dm[2] = v[8] * dtx + v[9] * dty + v[10] * dtz;
+
+        // ---- screen-space mean -> mean3D ----
+        const Mat4 Pm = load_mat4(projmatrix);
+        const float *pr = Pm.m;
+        const float4 mh = xf_point44(p, Pm);
+        const float mw = 1.0f / (mh.w + 0.0000001f);
+        const float mul1 = mh.x * mw * mw, mul2 = mh.y * mw * mw;
+        dm[0] += (pr[0] * mw - pr[3] * mul1) * g[0] + (pr[1] * mw - pr[3] * mul2) * g[1];
+        dm[1] += (pr[4] * mw - pr[7] * mul1) * g[0] + (pr[5] * mw - pr[7] * mul2) * g[1];
+        dm[2] += (pr[8] * mw - pr[11] * mul1) * g[0] + (pr[9] * mw - pr[11] * mul2) * g[1];
+
+        // ---- inverse depth -> mean3D ----
+        {
+            const float3 pv = xf_point43(p, V);
+            const float dz = -g[9] / (pv.z * pv.z);
+            dm[0] += dz * v[2];
+            dm[1] += dz * v[6];
+            dm[2] += dz * v[10];
+        }
+    }
+
+    // ---- colour ----
+    if (has_shs) {
+        float *dsh = out.dsh + (size_t)i * M * 3;
+        const int nc = (D + 1) * (D + 1);
+        if (!vis) {
+            for (int k = 0; k < M * 3; k++) dsh[k] = 0.f;
+        } else {
+            float dir[3], dor[3];
+            sh_dir(p, make_float3(campos_p[0], campos_p[1], campos_p[2]), dir, dor);
+            const float *sh = shs + (size_t)i * M * 3;
+            const uint8_t cl = clamped[i];
+            const float x = dir[0], y = dir[1], z = dir[2];
+            float gd0 = 0.f, gd1 = 0.f, gd2 = 0.f;
+            for (int ch = 0; ch < 3; ch++) {
+                const float gc = (cl >> ch) & 1 ? 0.f : g[6 + ch];
+                float ddx = 0.f, ddy = 0.f, ddz = 0.f;
+                dsh[ch] = GSR_SH_C0 * gc;
+                if (D > 0) {
+                    const float *s = sh + ch;
+                    dsh[1 * 3 + ch] = -GSR_SH_C1 * y * gc;
+                    dsh[2 * 3 + ch] = GSR_SH_C1 * z * gc;
+                    dsh[3 * 3 + ch] = -GSR_SH_C1 * x * gc;
+                    ddx = -GSR_SH_C1 * s[3 * 3];
+                    ddy = -GSR_SH_C1 * s[1 * 3];
+                    ddz = GSR_SH_C1 * s[2 * 3];
+                    if (D > 1) {
+                        const float xx = x * x, yy = y * y, zz = z * z, xy_ = x * y, yz = y * z, xz = x * z;
+                        dsh[4 * 3 + ch] = GSR_SH_C2_0 * xy_ * gc;
+                        dsh[5 * 3 + ch] = GSR_SH_C2_1 * yz * gc;
+                        dsh[6 * 3 + ch] = GSR_SH_C2_2 * (2.f * zz - xx - yy) * gc;
+                        dsh[7 * 3 + ch] = GSR_SH_C2_3 * xz * gc;
+                        dsh[8 * 3 + ch] = GSR_SH_C2_4 * (xx - yy) * gc;
+                        ddx += GSR_SH_C2_0 * y * s[4 * 3] + GSR_SH_C2_2 * 2.f * -x * s[6 * 3] +
+                               GSR_SH_C2_3 * z * s[7 * 3] + GSR_SH_C2_4 * 2.f * x * s[8 * 3];
+                        ddy += GSR_SH_C2_0 * x * s[4 * 3] + GSR_SH_C2_1 * z * s[5 * 3] +
+                               GSR_SH_C2_2 * 2.f * -y * s[6 * 3] + GSR_SH_C2_4 * 2.f * -y * s[8 * 3];
+                        ddz += GSR_SH_C2_1 * y * s[5 * 3] + GSR_SH_C2_2 * 2.f * 2.f * z * s[6 * 3] +
+                               GSR_SH_C2_3 * x * s[7 * 3];
+                        if (D > 2) {
+                            dsh[9 * 3 + ch] = GSR_SH_C3_0 * y * (3.f * xx - yy) * gc;
+                            dsh[10 * 3 + ch] = GSR_SH_C3_1 * xy_ * z * gc;
+                            dsh[11 * 3 + ch] = GSR_SH_C3_2 * y * (4.f * zz - xx - yy) * gc;
+                            dsh[12 * 3 + ch] = GSR_SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy) * gc;
+                            dsh[13 * 3 + ch] = GSR_SH_C3_4 * x * (4.f * zz - xx - yy) * gc;
+                            dsh[14 * 3 + ch] = GSR_SH_C3_5 * z * (xx - yy) * gc;
+                            dsh[15 * 3 + ch] = GSR_SH_C3_6 * x * (xx - 3.f * yy) * gc;
+                            ddx += GSR_SH_C3_0 * s[9 * 3] * 3.f * 2.f * xy_ + GSR_SH_C3_1 * s[10 * 3] * yz +
+                                   GSR_SH_C3_2 * s[11 * 3] * -2.f * xy_ + GSR_SH_C3_3 * s[12 * 3] * -3.f * 2.f * xz +
+                                   GSR_SH_C3_4 * s[13 * 3] * (-3.f * xx + 4.f * zz - yy) +
+                                   GSR_SH_C3_5 * s[14 * 3] * 2.f * xz + GSR_SH_C3_6 * s[15 * 3] * 3.f * (xx - yy);
+                            ddy += GSR_SH_C3_0 * s[9 * 3] * 3.f * (xx - yy) + GSR_SH_C3_1 * s[10 * 3] * xz +
+                                   GSR_SH_C3_2 * s[11 * 3] * (-3.f * yy + 4.f * zz - xx) +
+                                   GSR_SH_C3_3 * s[12 * 3] * -3.f * 2.f * yz + GSR_SH_C3_4 * s[13 * 3] * -2.f * xy_ +
+                                   GSR_SH_C3_5 * s[14 * 3] * -2.f * yz + GSR_SH_C3_6 * s[15 * 3] * -3.f * 2.f * xy_;
+                            ddz += GSR_SH_C3_1 * s[10 * 3] * xy_ + GSR_SH_C3_2 * s[11 * 3] * 4.f * 2.f * yz +
+                                   GSR_SH_C3_3 * s[12 * 3] * 3.f * (2.f * zz - xx - yy) +
+                                   GSR_SH_C3_4 * s[13 * 3] * 4.f * 2.f * xz + GSR_SH_C3_5 * s[14 * 3] * (xx - yy);
+                        }
+                    }
+                }
+                gd0 += ddx * gc;
+                gd1 += ddy * gc;
+                gd2 += ddz * gc;
+            }
+            for (int k = nc * 3; k < M * 3; k++) dsh[k] = 0.f;
+            const float s2 = dor[0] * dor[0] + dor[1] * dor[1] + dor[2] * dor[2];
+            const float inv32 = 1.0f / sqrtf(s2 * s2 * s2);
+            dm[0] += ((s2 - dor[0] * dor[0]) * gd0 - dor[1] * dor[0] * gd1 - dor[2] * dor[0] * gd2) * inv32;
+            dm[1] += (-dor[0] * dor[1] * gd0 + (s2 - dor[1] * dor[1]) * gd1 - dor[2] * dor[1] * gd2) * inv32;
+            dm[2] += (-dor[0] * dor[2] * gd0 - dor[1] * dor[2] * gd1 + (s2 - dor[2] * dor[2]) * gd2) * inv32;
+        }
+        out.dcolors[3 * i + 0] = 0.f;
+        out.dcolors[3 * i + 1] = 0.f;
+        out.dcolors[3 * i + 2] = 0.f;
+    } else {
+        out.dcolors[3 * i + 0] = g[6];
+        out.dcolors[3 * i + 1] = g[7];
+        out.dcolors[3 * i + 2] = g[8];
+    }
+    out.dmeans3D[3 * i + 0] = dm[0];
+    out.dmeans3D[3 * i + 1] = dm[1];
+    out.dmeans3D[3 * i + 2] = dm[2];
+
+    // ---- cov3D -> scale / rotation ----
+    if (has_scales) {
+        float ds[3] = {0.f, 0.f, 0.f};
+        float dq[4] = {0.f, 0.f, 0.f, 0.f};
+        if (vis) {
+            const float r = q.x, x = q.y, y = q.z, z = q.w;
+            const float s[3] = {mod * s_in.x, mod * s_in.y, mod * s_in.z};
+            const Rot3 R = quat_to_rot(q);
+            const float G3[3][3] = {{dcov[0], 0.5f * dcov[1], 0.5f * dcov[2]},
+                                    {0.5f * dcov[1], dcov[3], 0.5f * dcov[4]},
+                                    {0.5f * dcov[2], 0.5f * dcov[4], dcov[5]}};
+            float dLL[3][3];
+#pragma unroll
+            for (int rr = 0; rr < 3; rr++)
+#pragma unroll
+                for (int cc = 0; cc < 3; cc++)
+                    dLL[rr][cc] = 2.f * (G3[rr][0] * R.m[0][cc] * s[cc] + G3[rr][1] * R.m[1][cc] * s[cc] +
+                                         G3[rr][2] * R.m[2][cc] * s[cc]);
+#pragma unroll
+            for (int k = 0; k < 3; k++)
+                ds[k] = mod * (dLL[0][k] * R.m[0][k] + dLL[1][k] * R.m[1][k] + dLL[2][k] * R.m[2][k]);
+            float Gr[3][3];
+#pragma unroll
+            for (int rr = 0; rr < 3; rr++)
+#pragma unroll
+                for (int cc = 0; cc < 3; cc++) Gr[rr][cc] = dLL[rr][cc] * s[cc];
+            dq[0] = 2.f * (-z * Gr[0][1] + y * Gr[0][2] + z * Gr[1][0] - x * Gr[1][2] - y * Gr[2][0] + x * Gr[2][1]);
+            dq[1] = 2.f * (y * Gr[0][1] + z * Gr[0][2] + y * Gr[1][0] - 2.f * x * Gr[1][1] - r * Gr[1][2] +
+                           z * Gr[2][0] + r * Gr[2][1] - 2.f * x * Gr[2][2]);
+            dq[2] = 2.f * (-2.f * y * Gr[0][0] + x * Gr[0][1] + r * Gr[0][2] + x * Gr[1][0] + z * Gr[1][2] -
+                           r * Gr[2][0] + z * Gr[2][1] - 2.f * y * Gr[2][2]);
+            dq[3] = 2.f * (-2.f * z * Gr[0][0] - r * Gr[0][1] + x * Gr[0][2] + r * Gr[1][0] - 2.f * z * Gr[1][1] +
+                           y * Gr[1][2] + x * Gr[2][0] + y * Gr[2][1]);
+        }
+        out.dscales[3 * i + 0] = ds[0];
+        out.dscales[3 * i + 1] = ds[1];
+        out.dscales[3 * i + 2] = ds[2];
+        reinterpret_cast<float4 *>(out.drots)[i] = make_float4(dq[0], dq[1], dq[2], dq[3]);
+#pragma unroll
+        for (int k = 0; k < 6; k++) out.dcov3D[6 * i + k] = 0.f;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 6; k++) out.dcov3D[6 * i + k] = dcov[k];
+    }
+}
+
+void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const GeomState &gs, const int *radii,
+                           const BwdScratch &sc, const GaussianGrads &out, hipStream_t s) {
+    if (in.P == 0) return;
+    hipLaunchKernelGGL(preprocess_bwd_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, in.D, in.M, in.means3D,
+                       radii, in.shs, gs.clamped, in.scales, in.rotations, in.scale_modifier, in.cov3D_precomp,
+                       cam.view, cam.proj, cam.campos, cam.tanx, cam.tany, cam.fx, cam.fy, gs.tiles, gs.offsets, sc,
+                       out);
+}
+
+}  // namespace gsr

@@ -1,0 +1,217 @@
+// gsr_device.h -- device-side maths and state layouts shared by the gfx950 kernels.
+//
+// Every index-producing expression (projection, EWA covariance, radius, tile rect, depth key)
+// is evaluated in a fixed IEEE operation order and compiled with -ffp-contract=off, so the
+// integer outputs (radii, tiles, keys, ranges, n_contrib away from exp() ulp ties) are
+// reproducible bit for bit by the CPU restatement in oracle/gs_oracle.c.
+//
+// Algorithm: the graphdeco 3DGS / hierarchy-rasterizer preprocess,
+// whose CUDA source is not vendored in the reference; the pure-Python twins it must agree
+// with are utils/sh_utils.py:57-112 (SH), scene/gaussian_model.py:33-37 +
+// utils/general_utils.py:68-114 (cov3D) and scene/cameras.py:96-99 (matrices).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gsr {
+
+constexpr int kTile = 16;              // 16x16 pixel tiles (T = ceil(W/16)*ceil(H/16))
+constexpr int kWave = 64;              // CDNA wavefront
+constexpr int kPixPerLane = kTile * kTile / kWave;  // 4: one wave owns one tile
+
+// ---- SH constants: utils/sh_utils.py:26-43 ----
+#define GSR_SH_C0 0.28209479177387814f
+#define GSR_SH_C1 0.4886025119029199f
+#define GSR_SH_C2_0 1.0925484305920792f
+#define GSR_SH_C2_1 -1.0925484305920792f
+#define GSR_SH_C2_2 0.31539156525252005f
+#define GSR_SH_C2_3 -1.0925484305920792f
+#define GSR_SH_C2_4 0.5462742152960396f
+#define GSR_SH_C3_0 -0.5900435899266435f
+#define GSR_SH_C3_1 2.890611442640554f
+#define GSR_SH_C3_2 -0.4570457994644658f
+#define GSR_SH_C3_3 0.3731763325901154f
+#define GSR_SH_C3_4 -0.4570457994644658f
+#define GSR_SH_C3_5 1.445305721320277f
+#define GSR_SH_C3_6 -0.5900435899266435f
+
+__device__ __forceinline__ float fmin_(float a, float b) { return a < b ? a : b; }
+__device__ __forceinline__ float fmax_(float a, float b) { return a > b ? a : b; }
+
+struct Mat4 {  // column-major 4x4 held in registers (wave-uniform -> SGPRs)
+    float m[16];
+};
+
+__device__ __forceinline__ Mat4 load_mat4(const float *__restrict__ p) {
+    Mat4 r;
+    const float4 *q = reinterpret_cast<const float4 *>(p);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        float4 v = q[i];
+        r.m[4 * i + 0] = v.x; r.m[4 * i + 1] = v.y; r.m[4 * i + 2] = v.z; r.m[4 * i + 3] = v.w;
+    }
+    return r;
+}
+
+__device__ __forceinline__ float3 xf_point43(float3 p, const Mat4 &M) {
+    const float *m = M.m;
+    return make_float3(m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12],
+                       m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
+                       m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14]);
+}
+
+__device__ __forceinline__ float4 xf_point44(float3 p, const Mat4 &M) {
+    const float *m = M.m;
+    return make_float4(m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12],
+                       m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
+                       m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14],
+                       m[3] * p.x + m[7] * p.y + m[11] * p.z + m[15]);
+}
+
+// upstream evaluates ((v + 1.0) * S - 1.0) * 0.5 in double
+__device__ __forceinline__ float ndc2pix(float v, int S) {
+    return (float)((((double)v + 1.0) * (double)S - 1.0) * 0.5);
+}
+
+struct Rect { int x0, y0, x1, y1; };
+
+__device__ __forceinline__ int clampi(int a, int hi) { a = a > 0 ? a : 0; return a < hi ? a : hi; }
+
+__device__ __forceinline__ Rect get_rect(float px, float py, int r, int gx, int gy) {
+    Rect R;
+    R.x0 = clampi((int)((px - (float)r) / (float)kTile), gx);
+    R.y0 = clampi((int)((py - (float)r) / (float)kTile), gy);
+    R.x1 = clampi((int)((px + (float)r + (float)(kTile - 1)) / (float)kTile), gx);
+    R.y1 = clampi((int)((py + (float)r + (float)(kTile - 1)) / (float)kTile), gy);
+    return R;
+}
+
+struct Rot3 { float m[3][3]; };
+
+__device__ __forceinline__ Rot3 quat_to_rot(float4 q) {
+    const float r = q.x, x = q.y, y = q.z, z = q.w;
+    Rot3 R;
+    R.m[0][0] = 1.f - 2.f * (y * y + z * z); R.m[0][1] = 2.f * (x * y - r * z); R.m[0][2] = 2.f * (x * z + r * y);
+    R.m[1][0] = 2.f * (x * y + r * z); R.m[1][1] = 1.f - 2.f * (x * x + z * z); R.m[1][2] = 2.f * (y * z - r * x);
+    R.m[2][0] = 2.f * (x * z - r * y); R.m[2][1] = 2.f * (y * z + r * x); R.m[2][2] = 1.f - 2.f * (x * x + y * y);
+    return R;
+}
+
+// cov3D = (R S)(R S)^T, S = diag(mod * s); 6-pack xx,xy,xz,yy,yz,zz
+__device__ __forceinline__ void cov3d_from_scale_rot(float3 s_in, float mod, float4 q, float c[6]) {
+    const float sx = mod * s_in.x, sy = mod * s_in.y, sz = mod * s_in.z;
+    Rot3 R = quat_to_rot(q);
+    float L[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) { L[i][0] = R.m[i][0] * sx; L[i][1] = R.m[i][1] * sy; L[i][2] = R.m[i][2] * sz; }
+    c[0] = L[0][0] * L[0][0] + L[0][1] * L[0][1] + L[0][2] * L[0][2];
+    c[1] = L[0][0] * L[1][0] + L[0][1] * L[1][1] + L[0][2] * L[1][2];
+    c[2] = L[0][0] * L[2][0] + L[0][1] * L[2][1] + L[0][2] * L[2][2];
+    c[3] = L[1][0] * L[1][0] + L[1][1] * L[1][1] + L[1][2] * L[1][2];
+    c[4] = L[1][0] * L[2][0] + L[1][1] * L[2][1] + L[1][2] * L[2][2];
+    c[5] = L[2][0] * L[2][0] + L[2][1] * L[2][1] + L[2][2] * L[2][2];
+}
+
+struct Ewa {
+    float m0[3], m1[3];  // first two rows of J * W_view
+    float3 t;            // view-space mean with the 1.3*tanfov clamp applied
+    float xmul, ymul;    // 0 where the clamp is active (gradient mask)
+};
+
+__device__ __forceinline__ Ewa ewa_rows(float3 mean, const Mat4 &V, float fx, float fy, float tanx, float tany) {
+    Ewa e;
+    float3 t = xf_point43(mean, V);
+    const float limx = 1.3f * tanx, limy = 1.3f * tany;
+    const float txtz = t.x / t.z, tytz = t.y / t.z;
+    e.xmul = (txtz < -limx || txtz > limx) ? 0.f : 1.f;
+    e.ymul = (tytz < -limy || tytz > limy) ? 0.f : 1.f;
+    t.x = fmin_(limx, fmax_(-limx, txtz)) * t.z;
+    t.y = fmin_(limy, fmax_(-limy, tytz)) * t.z;
+    const float j00 = fx / t.z, j02 = -(fx * t.x) / (t.z * t.z);
+    const float j11 = fy / t.z, j12 = -(fy * t.y) / (t.z * t.z);
+    const float *v = V.m;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        e.m0[c] = j00 * v[4 * c + 0] + j02 * v[4 * c + 2];
+        e.m1[c] = j11 * v[4 * c + 1] + j12 * v[4 * c + 2];
+    }
+    e.t = t;
+    return e;
+}
+
+__device__ __forceinline__ float quad_form(const float a[3], const float c[6], const float b[3]) {
+    const float s0 = c[0] * b[0] + c[1] * b[1] + c[2] * b[2];
+    const float s1 = c[1] * b[0] + c[3] * b[1] + c[4] * b[2];
+    const float s2 = c[2] * b[0] + c[4] * b[1] + c[5] * b[2];
+    return a[0] * s0 + a[1] * s1 + a[2] * s2;
+}
+
+__device__ __forceinline__ void sh_dir(float3 mean, float3 campos, float dir[3], float dor[3]) {
+    dor[0] = mean.x - campos.x;
+    dor[1] = mean.y - campos.y;
+    dor[2] = mean.z - campos.z;
+    const float len = sqrtf(dor[0] * dor[0] + dor[1] * dor[1] + dor[2] * dor[2]);
+    dir[0] = dor[0] / len; dir[1] = dor[1] / len; dir[2] = dor[2] / len;
+}
+
+// SH -> RGB for one channel; sh points at coefficient 0 of that channel, stride 3 floats
+__device__ __forceinline__ float sh_channel(int deg, const float *sh, float x, float y, float z) {
+    float r = GSR_SH_C0 * sh[0];
+    if (deg > 0) {
+        r = r - GSR_SH_C1 * y * sh[1 * 3] + GSR_SH_C1 * z * sh[2 * 3] - GSR_SH_C1 * x * sh[3 * 3];
+        if (deg > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+            r = r + GSR_SH_C2_0 * xy * sh[4 * 3] + GSR_SH_C2_1 * yz * sh[5 * 3] +
+                GSR_SH_C2_2 * (2.0f * zz - xx - yy) * sh[6 * 3] + GSR_SH_C2_3 * xz * sh[7 * 3] +
+                GSR_SH_C2_4 * (xx - yy) * sh[8 * 3];
+            if (deg > 2) {
+                r = r + GSR_SH_C3_0 * y * (3.0f * xx - yy) * sh[9 * 3] + GSR_SH_C3_1 * xy * z * sh[10 * 3] +
+                    GSR_SH_C3_2 * y * (4.0f * zz - xx - yy) * sh[11 * 3] +
+                    GSR_SH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * sh[12 * 3] +
+                    GSR_SH_C3_4 * x * (4.0f * zz - xx - yy) * sh[13 * 3] + GSR_SH_C3_5 * z * (xx - yy) * sh[14 * 3] +
+                    GSR_SH_C3_6 * x * (xx - 3.0f * yy) * sh[15 * 3];
+            }
+        }
+    }
+    return r + 0.5f;
+}
+
+// ------------------------------------------------------------------------------------------
+// Scratch-state layouts (carved out of the caller's byte buffers, 256-B aligned arrays)
+// ------------------------------------------------------------------------------------------
+__host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+struct GeomState {          // per Gaussian, written by preprocess
+    float *depth;           // view-space z (sort key low 32 bits)
+    uint32_t *tiles;        // tiles_touched
+    uint32_t *offsets;      // inclusive scan of tiles
+    float2 *xy;             // pixel-space mean
+    float4 *conic_o;        // (a, b, c, opacity) of the inverse 2D covariance
+    float4 *rgbd;           // (r, g, b, 1/depth)
+    uint8_t *clamped;       // bit c set: SH channel c clamped at 0
+    void *scan_tmp;
+    size_t scan_tmp_bytes;
+};
+
+struct BinningState {       // per tile instance
+    uint64_t *keys_unsorted;
+    uint64_t *keys_sorted;
+    uint32_t *vals_unsorted;
+    uint32_t *point_list;   // gaussian id in (tile, depth) order
+    void *sort_tmp;
+    size_t sort_tmp_bytes;
+};
+
+struct ImageState {
+    uint2 *ranges;          // per tile [start, end) in point_list
+    float *final_T;         // per pixel
+    uint32_t *n_contrib;    // per pixel: 1-based list position of the last contributor
+};
+
+struct BwdScratch {         // per tile instance, indexed by unsorted (gaussian-major) position
+    float4 *ga;             // dmean2D.x, dmean2D.y, dconic.a, dconic.b
+    float4 *gb;             // dconic.c, dopacity, drgb.r, drgb.g
+    float2 *gc;             // drgb.b, dinvdepth
+};
+
+}  // namespace gsr

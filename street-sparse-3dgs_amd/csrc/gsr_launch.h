@@ -1,0 +1,52 @@
+// gsr_launch.h -- host-side launchers for the gfx950 kernels (one translation unit each).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "gsr_device.h"
+
+namespace gsr {
+
+struct Camera {
+    const float *view;  // device, 16
+    const float *proj;  // device, 16
+    const float *campos;  // device, 3
+    float tanx, tany, fx, fy;
+    int W, H, gx, gy;
+};
+
+struct GaussianInputs {
+    int P, D, M;
+    const float *means3D, *shs, *colors_precomp, *opacities, *scales, *rotations, *cov3D_precomp;
+    float scale_modifier;
+};
+
+// preprocess.hip
+void launch_preprocess(const GaussianInputs &in, const Camera &cam, const GeomState &gs, int *radii,
+                       hipStream_t s);
+void launch_duplicate(int P, const Camera &cam, const GeomState &gs, const int *radii, const BinningState &bs,
+                      hipStream_t s);
+void launch_ranges(int64_t K, int T, const BinningState &bs, const ImageState &is, hipStream_t s);
+void launch_mark_visible(int P, const float *means3D, const float *view, uint8_t *present, hipStream_t s);
+
+// sort.hip (rocPRIM)
+size_t scan_temp_bytes(int P);
+hipError_t inclusive_scan_u32(void *tmp, size_t tmp_bytes, const uint32_t *in, uint32_t *out, int P, hipStream_t s);
+size_t sort_temp_bytes(int64_t K, int end_bit);
+hipError_t sort_pairs_u64(void *tmp, size_t tmp_bytes, const uint64_t *kin, uint64_t *kout, const uint32_t *vin,
+                          uint32_t *vout, int64_t K, int end_bit, hipStream_t s);
+
+// render.hip
+void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
+                       const float *bg, float *out_color, float *out_invdepth, hipStream_t s);
+void launch_render_bwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
+                       const int *radii, const float *bg, const float *dL_dpix, const float *dL_dinvdepth,
+                       const BwdScratch &sc, hipStream_t s);
+
+// backward.hip
+struct GaussianGrads {
+    float *dmeans2D, *dcolors, *dopacity, *dmeans3D, *dcov3D, *dsh, *dscales, *drots;
+};
+void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const GeomState &gs, const int *radii,
+                           const BwdScratch &sc, const GaussianGrads &out, hipStream_t s);
+
+}  // namespace gsr

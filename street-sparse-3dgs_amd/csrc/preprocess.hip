@@ -1,0 +1,185 @@
+// preprocess.hip -- per-Gaussian forward preprocess, per-instance key duplication, tile
+// ranges and the frustum test.
+//
+// Layout: inputs are the caller's AoS tensors (means (P,3), scales (P,3), rotations (P,4),
+// shs (P,M,3)); outputs are SoA arrays in GeomState so that the render kernels gather one
+// 8-B xy, one 16-B conic/opacity and one 16-B rgb/invdepth record per tile instance.
+#include "gsr_launch.h"
+
+namespace gsr {
+
+template <bool kVecSH>
+__global__ __launch_bounds__(256) void preprocess_kernel(
+    int P, int D, int M, const float *__restrict__ means3D, const float *__restrict__ scales, float mod,
+    const float *__restrict__ rotations, const float *__restrict__ opacities, const float *__restrict__ shs,
+    const float *__restrict__ colors_precomp, const float *__restrict__ cov3D_precomp,
+    const float *__restrict__ viewmatrix, const float *__restrict__ projmatrix, const float *__restrict__ campos,
+    int W, int H, float tanx, float tany, float fx, float fy, int gx, int gy, GeomState gs, int *__restrict__ radii) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const Mat4 V = load_mat4(viewmatrix);
+    const Mat4 Pm = load_mat4(projmatrix);
+    radii[i] = 0;
+    gs.tiles[i] = 0;
+    const float3 p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
+    const float3 pv = xf_point43(p, V);
+    if (pv.z <= 0.2f) return;  // in_frustum (prefiltered is treated as a plain cull)
+    const float4 ph = xf_point44(p, Pm);
+    const float pw = 1.0f / (ph.w + 0.0000001f);
+    const float ndcx = ph.x * pw, ndcy = ph.y * pw;
+
+    float c3[6];
+    if (cov3D_precomp) {
+#pragma unroll
+        for (int k = 0; k < 6; k++) c3[k] = cov3D_precomp[6 * i + k];
+    } else {
+        const float3 s = make_float3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
+        const float4 q = reinterpret_cast<const float4 *>(rotations)[i];
+        cov3d_from_scale_rot(s, mod, q, c3);
+    }
+    const Ewa e = ewa_rows(p, V, fx, fy, tanx, tany);
+    const float ca = quad_form(e.m0, c3, e.m0) + 0.3f;
+    const float cb = quad_form(e.m0, c3, e.m1);
+    const float cc = quad_form(e.m1, c3, e.m1) + 0.3f;
+    const float det = ca * cc - cb * cb;
+    if (det == 0.0f) return;
+    const float det_inv = 1.f / det;
+    const float mid = 0.5f * (ca + cc);
+    const float lambda1 = mid + sqrtf(fmax_(0.1f, mid * mid - det));
+    const float radius = ceilf(3.f * sqrtf(lambda1));
+    const float px = ndc2pix(ndcx, W), py = ndc2pix(ndcy, H);
+    const Rect r = get_rect(px, py, (int)radius, gx, gy);
+    const int area = (r.x1 - r.x0) * (r.y1 - r.y0);
+    if (area == 0) return;
+
+    float4 col;
+    uint8_t clamp_bits = 0;
+    if (colors_precomp) {
+        col = make_float4(colors_precomp[3 * i], colors_precomp[3 * i + 1], colors_precomp[3 * i + 2], 0.f);
+    } else {
+        float dir[3], dor[3];
+        sh_dir(p, make_float3(campos[0], campos[1], campos[2]), dir, dor);
+        const int nc = (D + 1) * (D + 1);
+        float sh[48];
+        const float *src = shs + (size_t)i * M * 3;
+        if (kVecSH) {
+            const float4 *s4 = reinterpret_cast<const float4 *>(src);
+#pragma unroll
+            for (int k = 0; k < 12; k++) {
+                if (4 * k < nc * 3) {
+                    const float4 v = s4[k];
+                    sh[4 * k] = v.x; sh[4 * k + 1] = v.y; sh[4 * k + 2] = v.z; sh[4 * k + 3] = v.w;
+                } else {
+                    sh[4 * k] = sh[4 * k + 1] = sh[4 * k + 2] = sh[4 * k + 3] = 0.f;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 48; k++) sh[k] = k < nc * 3 ? src[k] : 0.f;
+        }
+        float rgb[3];
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) {
+            const float v = sh_channel(D, sh + ch, dir[0], dir[1], dir[2]);
+            if (v < 0.f) clamp_bits |= (uint8_t)(1u << ch);
+            rgb[ch] = v < 0.f ? 0.f : v;
+        }
+        col = make_float4(rgb[0], rgb[1], rgb[2], 0.f);
+    }
+    col.w = 1.f / pv.z;
+    gs.depth[i] = pv.z;
+    radii[i] = (int)radius;
+    gs.xy[i] = make_float2(px, py);
+    gs.conic_o[i] = make_float4(cc * det_inv, -cb * det_inv, ca * det_inv, opacities[i]);
+    gs.rgbd[i] = col;
+    gs.clamped[i] = clamp_bits;
+    gs.tiles[i] = (uint32_t)area;
+}
+
+void launch_preprocess(const GaussianInputs &in, const Camera &cam, const GeomState &gs, int *radii,
+                       hipStream_t s) {
+    if (in.P == 0) return;
+    const int blocks = (in.P + 255) / 256;
+    const bool vec = in.shs && (in.M * 3) % 4 == 0 && (reinterpret_cast<uintptr_t>(in.shs) % 16 == 0) && in.M >= 16;
+    if (vec)
+        hipLaunchKernelGGL(preprocess_kernel<true>, dim3(blocks), dim3(256), 0, s, in.P, in.D, in.M, in.means3D,
+                           in.scales, in.scale_modifier, in.rotations, in.opacities, in.shs, in.colors_precomp,
+                           in.cov3D_precomp, cam.view, cam.proj, cam.campos, cam.W, cam.H, cam.tanx, cam.tany, cam.fx,
+                           cam.fy, cam.gx, cam.gy, gs, radii);
+    else
+        hipLaunchKernelGGL(preprocess_kernel<false>, dim3(blocks), dim3(256), 0, s, in.P, in.D, in.M, in.means3D,
+                           in.scales, in.scale_modifier, in.rotations, in.opacities, in.shs, in.colors_precomp,
+                           in.cov3D_precomp, cam.view, cam.proj, cam.campos, cam.W, cam.H, cam.tanx, cam.tany, cam.fx,
+                           cam.fy, cam.gx, cam.gy, gs, radii);
+}
+
+// One lane per Gaussian writes its (tile << 32 | depth bits, id) pairs in rect row-major order
+// at its exclusive-scan offset -- the "unsorted" instance index u used again in the backward.
+__global__ __launch_bounds__(256) void duplicate_kernel(int P, int gx, int gy, const float2 *__restrict__ xy,
+                                                        const float *__restrict__ depth,
+                                                        const uint32_t *__restrict__ offsets,
+                                                        const int *__restrict__ radii, uint64_t *__restrict__ keys,
+                                                        uint32_t *__restrict__ vals) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const int rad = radii[i];
+    if (rad <= 0) return;
+    uint32_t off = i == 0 ? 0u : offsets[i - 1];
+    const float2 p = xy[i];
+    const Rect r = get_rect(p.x, p.y, rad, gx, gy);
+    const uint64_t dbits = (uint64_t)__float_as_uint(depth[i]);
+    for (int y = r.y0; y < r.y1; y++)
+        for (int x = r.x0; x < r.x1; x++) {
+            keys[off] = ((uint64_t)(uint32_t)(y * gx + x) << 32) | dbits;
+            vals[off] = (uint32_t)i;
+            off++;
+        }
+}
+
+void launch_duplicate(int P, const Camera &cam, const GeomState &gs, const int *radii, const BinningState &bs,
+                      hipStream_t s) {
+    if (P == 0) return;
+    hipLaunchKernelGGL(duplicate_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, cam.gx, cam.gy, gs.xy, gs.depth,
+                       gs.offsets, radii, bs.keys_unsorted, bs.vals_unsorted);
+}
+
+__global__ __launch_bounds__(256) void ranges_kernel(int64_t K, const uint64_t *__restrict__ keys,
+                                                     uint2 *__restrict__ ranges) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= K) return;
+    const uint32_t cur = (uint32_t)(keys[idx] >> 32);
+    if (idx == 0) {
+        ranges[cur].x = 0;
+    } else {
+        const uint32_t prev = (uint32_t)(keys[idx - 1] >> 32);
+        if (cur != prev) {
+            ranges[prev].y = (uint32_t)idx;
+            ranges[cur].x = (uint32_t)idx;
+        }
+    }
+    if (idx == K - 1) ranges[cur].y = (uint32_t)K;
+}
+
+void launch_ranges(int64_t K, int T, const BinningState &bs, const ImageState &is, hipStream_t s) {
+    (void)hipMemsetAsync(is.ranges, 0, sizeof(uint2) * (size_t)T, s);
+    if (K == 0) return;
+    hipLaunchKernelGGL(ranges_kernel, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, s, K, bs.keys_sorted,
+                       is.ranges);
+}
+
+__global__ __launch_bounds__(256) void mark_visible_kernel(int P, const float *__restrict__ means3D,
+                                                           const float *__restrict__ viewmatrix,
+                                                           uint8_t *__restrict__ present) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const Mat4 V = load_mat4(viewmatrix);
+    const float3 p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
+    present[i] = xf_point43(p, V).z > 0.2f ? 1 : 0;
+}
+
+void launch_mark_visible(int P, const float *means3D, const float *view, uint8_t *present, hipStream_t s) {
+    if (P == 0) return;
+    hipLaunchKernelGGL(mark_visible_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, means3D, view, present);
+}
+
+}  // namespace gsr

@@ -1,0 +1,351 @@
+// rasterizer.hip -- the C ABI (include/gsr.h): buffer carving, stage orchestration, the one
+// device->host read of K (num_rendered), debug checking and per-stage HIP-event timing.
+//
+// Flow per frame:  preprocess -> inclusive scan -> [D2H K] ->
+// duplicate-with-keys -> radix sort (32 + bits(T) bits) -> tile ranges -> render fwd;
+// backward: render bwd (per-instance records) -> preprocess bwd (per-Gaussian sum + chain).
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/gsr.h"
+#include "gsr_launch.h"
+
+using namespace gsr;
+
+namespace {
+
+thread_local std::string g_err;
+thread_local int g_profile = 0;
+thread_local hipEvent_t g_ev[12];
+thread_local bool g_ev_init = false;
+thread_local int g_ev_fwd_recorded = 0, g_ev_bwd_recorded = 0;
+thread_local uint32_t *g_pinned = nullptr;
+
+constexpr int kStages = 8;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+void ensure_events() {
+    if (g_ev_init) return;
+    for (auto &e : g_ev) (void)hipEventCreate(&e);
+    g_ev_init = true;
+}
+
+void mark(int idx, hipStream_t s) {
+    if (g_profile) (void)hipEventRecord(g_ev[idx], s);
+}
+
+int check(const char *stage, int debug, hipStream_t s) {
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && debug) {
+        e = hipStreamSynchronize(s);
+        if (e == hipSuccess) e = hipGetLastError();
+    }
+    if (e != hipSuccess) return fail(GSR_ERR_DEVICE, std::string(stage) + ": " + hipGetErrorString(e));
+    return GSR_OK;
+}
+
+struct Carver {
+    char *base;
+    size_t off = 0;
+    explicit Carver(void *b) : base(static_cast<char *>(b)) {}
+    template <class T>
+    T *take(size_t n) {
+        off = align_up(off, 256);
+        T *p = base ? reinterpret_cast<T *>(base + off) : nullptr;
+        off += n * sizeof(T);
+        return p;
+    }
+};
+
+GeomState carve_geom(void *base, int P, size_t *bytes) {
+    Carver c(base);
+    GeomState g;
+    g.depth = c.take<float>(P);
+    g.tiles = c.take<uint32_t>(P);
+    g.offsets = c.take<uint32_t>(P);
+    g.xy = c.take<float2>(P);
+    g.conic_o = c.take<float4>(P);
+    g.rgbd = c.take<float4>(P);
+    g.clamped = c.take<uint8_t>(P);
+    g.scan_tmp_bytes = scan_temp_bytes(P);
+    g.scan_tmp = c.take<char>(g.scan_tmp_bytes);
+    if (bytes) *bytes = align_up(c.off, 256);
+    return g;
+}
+
+int bits_for(int n) {  // smallest b with n <= 2^b  (upstream getHigherMsb)
+    int b = 0;
+    while ((1ll << b) < (long long)n) b++;
+    return b;
+}
+
+BinningState carve_binning(void *base, int64_t K, int end_bit, size_t *bytes) {
+    Carver c(base);
+    BinningState b;
+    b.keys_unsorted = c.take<uint64_t>(K);
+    b.keys_sorted = c.take<uint64_t>(K);
+    b.vals_unsorted = c.take<uint32_t>(K);
+    b.point_list = c.take<uint32_t>(K);
+    b.sort_tmp_bytes = sort_temp_bytes(K, end_bit);
+    b.sort_tmp = c.take<char>(b.sort_tmp_bytes);
+    if (bytes) *bytes = align_up(c.off, 256);
+    return b;
+}
+
+ImageState carve_image(void *base, int T, int npix, size_t *bytes) {
+    Carver c(base);
+    ImageState s;
+    s.ranges = c.take<uint2>(T);
+    s.final_T = c.take<float>(npix);
+    s.n_contrib = c.take<uint32_t>(npix);
+    if (bytes) *bytes = align_up(c.off, 256);
+    return s;
+}
+
+BwdScratch carve_bwd(void *base, int64_t K, size_t *bytes) {
+    Carver c(base);
+    BwdScratch s;
+    s.ga = c.take<float4>(K);
+    s.gb = c.take<float4>(K);
+    s.gc = c.take<float2>(K);
+    if (bytes) *bytes = align_up(c.off, 256);
+    return s;
+}
+
+Camera make_camera(const float *view, const float *proj, const float *campos, float tanx, float tany, int W, int H) {
+    Camera c;
+    c.view = view;
+    c.proj = proj;
+    c.campos = campos;
+    c.tanx = tanx;
+    c.tany = tany;
+    // rasterizer_impl: focal = size / (2 * tan(fov/2)), evaluated in fp32
+    c.fy = (float)H / (2.0f * tany);
+    c.fx = (float)W / (2.0f * tanx);
+    c.W = W;
+    c.H = H;
+    c.gx = (W + kTile - 1) / kTile;
+    c.gy = (H + kTile - 1) / kTile;
+    return c;
+}
+
+int validate_common(int P, int D, int M, const float *shs, const float *colors_precomp, const float *scales,
+                    const float *rotations, const float *cov3D_precomp, int W, int H) {
+    if (P < 0) return fail(GSR_ERR_INVALID_ARGUMENT, "P must be >= 0");
+    if (W <= 0 || H <= 0) return fail(GSR_ERR_INVALID_ARGUMENT, "image size must be positive");
+    if ((shs == nullptr) == (colors_precomp == nullptr) && P > 0)
+        return fail(GSR_ERR_INVALID_ARGUMENT, "Please provide exactly one of either SHs or precomputed colors!");
+    if (((scales == nullptr || rotations == nullptr) && cov3D_precomp == nullptr) ||
+        ((scales != nullptr || rotations != nullptr) && cov3D_precomp != nullptr)) {
+        if (P > 0)
+            return fail(GSR_ERR_INVALID_ARGUMENT,
+                        "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
+    }
+    if (shs && (D < 0 || D > 3 || (D + 1) * (D + 1) > M || M > 16))
+        return fail(GSR_ERR_INVALID_ARGUMENT, "sh degree / coefficient count out of range (need (D+1)^2 <= M <= 16)");
+    return GSR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gsr_abi_version(void) { return GSR_ABI_VERSION; }
+
+const char *gsr_last_error(void) { return g_err.c_str(); }
+
+const char *gsr_build_info(void) {
+    return "gsr_hip gfx950: preprocess/duplicate/ranges (preprocess.hip), rocPRIM scan+radix sort (sort.hip), "
+           "wave-per-tile render fwd/bwd with DPP reductions (render.hip), per-Gaussian backward (backward.hip)";
+}
+
+int gsr_set_profiling(int enable) {
+    g_profile = enable ? 1 : 0;
+    if (g_profile) ensure_events();
+    g_ev_fwd_recorded = g_ev_bwd_recorded = 0;
+    return GSR_OK;
+}
+
+int gsr_stage_times_ms(float *out, int max_stages) {
+    if (!g_profile) return 0;
+    int n = 0;
+    auto el = [](hipEvent_t a, hipEvent_t b) {
+        float ms = 0.f;
+        if (hipEventSynchronize(b) != hipSuccess) return 0.f;
+        if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.f;
+        return ms;
+    };
+    float t[kStages] = {0};
+    if (g_ev_fwd_recorded)
+        for (int k = 0; k < 6; k++) t[k] = el(g_ev[k], g_ev[k + 1]);
+    if (g_ev_bwd_recorded) {
+        t[6] = el(g_ev[7], g_ev[8]);
+        t[7] = el(g_ev[8], g_ev[9]);
+    }
+    for (; n < kStages && n < max_stages; n++) out[n] = t[n];
+    return n;
+}
+
+int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffer, gsr_resize_fn image_buffer,
+                          void *resize_ctx, int P, int D, int M, const float *background, int width, int height,
+                          const float *means3D, const float *shs, const float *colors_precomp,
+                          const float *opacities, const float *scales, float scale_modifier,
+                          const float *rotations, const float *cov3D_precomp, const float *viewmatrix,
+                          const float *projmatrix, const float *cam_pos, float tan_fovx, float tan_fovy,
+                          int prefiltered, float *out_color, float *out_invdepth, int *radii,
+                          const int *render_indices, const int *parent_indices,
+                          const float *interpolation_weights, const int *num_node_kids, int num_render,
+                          int debug, void *stream, int64_t *num_rendered) {
+    (void)prefiltered;
+    (void)render_indices;
+    (void)parent_indices;
+    (void)interpolation_weights;
+    (void)num_node_kids;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (num_rendered) *num_rendered = 0;
+    int rc = validate_common(P, D, M, shs, colors_precomp, scales, rotations, cov3D_precomp, width, height);
+    if (rc) return rc;
+    if (num_render != 0)
+        return fail(GSR_ERR_UNSUPPORTED,
+                    "in-kernel hierarchy interpolation (non-empty render_indices) is not implemented; every "
+                    "reference call path passes empty render_indices (SURVEY.md 0.6)");
+    if (!geom_buffer || !binning_buffer || !image_buffer)
+        return fail(GSR_ERR_INVALID_ARGUMENT, "resize callbacks must be non-NULL");
+    if (!background || !out_color || !viewmatrix || !projmatrix || !cam_pos || (P > 0 && !radii))
+        return fail(GSR_ERR_INVALID_ARGUMENT, "NULL required pointer");
+    if (P > 0 && (!means3D || !opacities))
+        return fail(GSR_ERR_INVALID_ARGUMENT, "NULL means3D / opacities");
+
+    const Camera cam = make_camera(viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, width, height);
+    const int T = cam.gx * cam.gy;
+    const int npix = width * height;
+
+    size_t gbytes = 0, ibytes = 0;
+    carve_geom(nullptr, P, &gbytes);
+    carve_image(nullptr, T, npix, &ibytes);
+    void *gbase = geom_buffer(resize_ctx, gbytes);
+    void *ibase = image_buffer(resize_ctx, ibytes);
+    if (!gbase || !ibase) return fail(GSR_ERR_ALLOCATION, "geometry/image buffer allocation failed");
+    const GeomState gs = carve_geom(gbase, P, nullptr);
+    const ImageState is = carve_image(ibase, T, npix, nullptr);
+
+    GaussianInputs in{P, D, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp,
+                      scale_modifier};
+    if (g_profile) {
+        ensure_events();
+        g_ev_fwd_recorded = 1;
+    }
+    mark(0, s);
+    launch_preprocess(in, cam, gs, radii, s);
+    if ((rc = check("preprocess", debug, s))) return rc;
+    mark(1, s);
+    if (inclusive_scan_u32(gs.scan_tmp, gs.scan_tmp_bytes, gs.tiles, gs.offsets, P, s) != hipSuccess)
+        return fail(GSR_ERR_DEVICE, "inclusive scan failed");
+    if ((rc = check("scan", debug, s))) return rc;
+    mark(2, s);
+
+    int64_t K = 0;
+    if (P > 0) {
+        if (!g_pinned) {
+            if (hipHostMalloc(reinterpret_cast<void **>(&g_pinned), sizeof(uint32_t)) != hipSuccess)
+                return fail(GSR_ERR_ALLOCATION, "pinned host allocation failed");
+        }
+        if (hipMemcpyAsync(g_pinned, gs.offsets + (P - 1), sizeof(uint32_t), hipMemcpyDeviceToHost, s) != hipSuccess)
+            return fail(GSR_ERR_DEVICE, "num_rendered copy failed");
+        if (hipStreamSynchronize(s) != hipSuccess) return fail(GSR_ERR_DEVICE, "stream sync failed");
+        K = (int64_t)*g_pinned;
+    }
+    const int end_bit = 32 + bits_for(T);
+    size_t bbytes = 0;
+    carve_binning(nullptr, K, end_bit, &bbytes);
+    void *bbase = binning_buffer(resize_ctx, bbytes);
+    if (!bbase) return fail(GSR_ERR_ALLOCATION, "binning buffer allocation failed");
+    const BinningState bs = carve_binning(bbase, K, end_bit, nullptr);
+
+    if (K > 0) launch_duplicate(P, cam, gs, radii, bs, s);
+    if ((rc = check("duplicateWithKeys", debug, s))) return rc;
+    mark(3, s);
+    if (sort_pairs_u64(bs.sort_tmp, bs.sort_tmp_bytes, bs.keys_unsorted, bs.keys_sorted, bs.vals_unsorted,
+                       bs.point_list, K, end_bit, s) != hipSuccess)
+        return fail(GSR_ERR_DEVICE, "radix sort failed");
+    if ((rc = check("sort", debug, s))) return rc;
+    mark(4, s);
+    launch_ranges(K, T, bs, is, s);
+    if ((rc = check("identifyTileRanges", debug, s))) return rc;
+    mark(5, s);
+    launch_render_fwd(cam, gs, bs, is, background, out_color, out_invdepth, s);
+    if ((rc = check("render", debug, s))) return rc;
+    mark(6, s);
+    if (num_rendered) *num_rendered = K;
+    return GSR_OK;
+}
+
+int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D, int M, int64_t R,
+                           const float *background, int width, int height, const float *means3D,
+                           const float *shs, const float *colors_precomp, const float *scales,
+                           float scale_modifier, const float *rotations, const float *cov3D_precomp,
+                           const float *viewmatrix, const float *projmatrix, const float *cam_pos,
+                           float tan_fovx, float tan_fovy, const int *radii, void *geom_buffer,
+                           void *binning_buffer, void *image_buffer, const float *dL_dpix,
+                           const float *dL_dinvdepth, float *dL_dmeans2D, float *dL_dcolors, float *dL_dopacity,
+                           float *dL_dmeans3D, float *dL_dcov3D, float *dL_dsh, float *dL_dscales,
+                           float *dL_drotations, int debug, void *stream) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int rc = validate_common(P, D, M, shs, colors_precomp, scales, rotations, cov3D_precomp, width, height);
+    if (rc) return rc;
+    if (R < 0) return fail(GSR_ERR_INVALID_ARGUMENT, "num_rendered must be >= 0");
+    if (!scratch) return fail(GSR_ERR_INVALID_ARGUMENT, "scratch callback must be non-NULL");
+    if (!geom_buffer || !binning_buffer || !image_buffer || !dL_dpix)
+        return fail(GSR_ERR_INVALID_ARGUMENT, "NULL state buffer / dL_dpix");
+    if (!dL_dmeans2D || !dL_dcolors || !dL_dopacity || !dL_dmeans3D || !dL_dcov3D)
+        return fail(GSR_ERR_INVALID_ARGUMENT, "NULL gradient output");
+    if (shs && !dL_dsh) return fail(GSR_ERR_INVALID_ARGUMENT, "NULL dL_dsh");
+    if (!cov3D_precomp && (!dL_dscales || !dL_drotations))
+        return fail(GSR_ERR_INVALID_ARGUMENT, "NULL dL_dscales / dL_drotations");
+
+    const Camera cam = make_camera(viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, width, height);
+    const int T = cam.gx * cam.gy;
+    const int end_bit = 32 + bits_for(T);
+    const GeomState gs = carve_geom(geom_buffer, P, nullptr);
+    const BinningState bs = carve_binning(binning_buffer, R, end_bit, nullptr);
+    const ImageState is = carve_image(image_buffer, T, width * height, nullptr);
+    size_t sbytes = 0;
+    carve_bwd(nullptr, R, &sbytes);
+    void *sbase = scratch(resize_ctx, sbytes);
+    if (!sbase) return fail(GSR_ERR_ALLOCATION, "backward scratch allocation failed");
+    const BwdScratch sc = carve_bwd(sbase, R, nullptr);
+
+    GaussianInputs in{P, D, M, means3D, shs, colors_precomp, nullptr, scales, rotations, cov3D_precomp,
+                      scale_modifier};
+    GaussianGrads out{dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
+                      dL_drotations};
+    if (g_profile) {
+        ensure_events();
+        g_ev_bwd_recorded = 1;
+    }
+    mark(7, s);
+    if (R > 0) launch_render_bwd(cam, gs, bs, is, radii, background, dL_dpix, dL_dinvdepth, sc, s);
+    if ((rc = check("render backward", debug, s))) return rc;
+    mark(8, s);
+    launch_preprocess_bwd(in, cam, gs, radii, sc, out, s);
+    if ((rc = check("preprocess backward", debug, s))) return rc;
+    mark(9, s);
+    return GSR_OK;
+}
+
+int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,
+                     uint8_t *present, void *stream) {
+    (void)projmatrix;
+    if (P < 0) return fail(GSR_ERR_INVALID_ARGUMENT, "P must be >= 0");
+    if (P > 0 && (!means3D || !viewmatrix || !present)) return fail(GSR_ERR_INVALID_ARGUMENT, "NULL pointer");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    launch_mark_visible(P, means3D, viewmatrix, present, s);
+    return check("markVisible", 0, s);
+}
+
+}  // extern "C"

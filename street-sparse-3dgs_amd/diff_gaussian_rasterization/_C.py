@@ -1,0 +1,195 @@
+"""`diff_gaussian_rasterization._C` -- the operator surface the reference's autograd Function
+binds (imported at gaussian_renderer/__init__.py:17 of Street-sparse-3DGS), implemented over
+the gfx950 C ABI (include/gsr.h) instead of a CUDA torch extension.
+
+Same function names, positional argument order, return tuples and error behaviour as the
+upstream extension:
+
+  rasterize_gaussians(bg, means3D, colors, opacity, scales, rotations, scale_modifier,
+      cov3D_precomp, viewmatrix, projmatrix, tanfovx, tanfovy, image_height, image_width, sh,
+      degree, campos, prefiltered, debug, render_indices, parent_indices,
+      interpolation_weights, num_node_kids, do_depth)
+    -> (num_rendered, color, invdepth, radii, geomBuffer, binningBuffer, imgBuffer)
+
+  rasterize_gaussians_backward(bg, means3D, radii, colors, scales, rotations, scale_modifier,
+      cov3D_precomp, viewmatrix, projmatrix, tanfovx, tanfovy, dL_dout_color,
+      dL_dout_invdepth, sh, degree, campos, geomBuffer, num_rendered, binningBuffer,
+      imgBuffer, render_indices, parent_indices, interpolation_weights, num_node_kids, debug)
+    -> (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
+        dL_drotations)
+
+  mark_visible(means3D, viewmatrix, projmatrix) -> bool tensor (P,)
+
+Scratch buffers are torch uint8 tensors created by resize callbacks, so they come from the
+torch caching allocator and are freed with the autograd graph, as upstream's are.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+
+_L = _lib.load()
+
+
+def _ptr(t):
+    if t is None or t.numel() == 0:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _dev_f32(t, name, device):
+    if t is None or t.numel() == 0:
+        return None
+    if t.device != device:
+        raise RuntimeError(f"{name} must be on {device} (got {t.device})")
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"{name} must be float32 (got {t.dtype})")
+    return t.contiguous()
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class _Resizer:
+    """Holds the uint8 tensors the library asks for through gsr_resize_fn callbacks."""
+
+    def __init__(self, device):
+        self.device = device
+        self.bufs = {}
+        self.fns = {}
+
+    def fn(self, name):
+        def cb(_ctx, nbytes):
+            t = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=self.device)
+            self.bufs[name] = t
+            return t.data_ptr()
+        f = _lib.RESIZE_FN(cb)
+        self.fns[name] = f
+        return f
+
+    def get(self, name):
+        return self.bufs.get(name, torch.empty(0, dtype=torch.uint8, device=self.device))
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed ({rc}): {_lib.last_error()}")
+
+
+def _require_gpu(t):
+    if not t.is_cuda:
+        raise RuntimeError("diff_gaussian_rasterization (gfx950) requires tensors on a ROCm GPU device; "
+                           "there is no CPU path")
+
+
+def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                        viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
+                        prefiltered, debug, render_indices=None, parent_indices=None, interpolation_weights=None,
+                        num_node_kids=None, do_depth=True):
+    if means3D.ndimension() != 2 or means3D.size(1) != 3:
+        raise RuntimeError("means3D must have dimensions (num_points, 3)")
+    _require_gpu(means3D)
+    dev = means3D.device
+    P = means3D.size(0)
+    H, W = int(image_height), int(image_width)
+    M = sh.size(1) if (sh is not None and sh.numel() != 0) else 0
+    means3D_c = _dev_f32(means3D, "means3D", dev)
+    sh_c = _dev_f32(sh, "sh", dev)
+    colors_c = _dev_f32(colors, "colors_precomp", dev)
+    opac_c = _dev_f32(opacity, "opacities", dev)
+    scales_c = _dev_f32(scales, "scales", dev)
+    rots_c = _dev_f32(rotations, "rotations", dev)
+    cov_c = _dev_f32(cov3D_precomp, "cov3D_precomp", dev)
+    view_c = _dev_f32(viewmatrix, "viewmatrix", dev)
+    proj_c = _dev_f32(projmatrix, "projmatrix", dev)
+    campos_c = _dev_f32(campos, "campos", dev)
+    bg_c = _dev_f32(background, "bg", dev)
+    if P > 0 and opac_c is None:
+        raise RuntimeError("opacities must be provided")
+    n_render = 0 if render_indices is None else int(render_indices.numel())
+
+    out_color = torch.empty(3, H, W, dtype=torch.float32, device=dev)
+    out_invdepth = torch.zeros(1, H, W, dtype=torch.float32, device=dev)
+    radii = torch.empty(P, dtype=torch.int32, device=dev)
+    res = _Resizer(dev)
+    K = ctypes.c_int64(0)
+    with torch.cuda.device(dev):
+        rc = _L.gsr_rasterize_forward(
+            res.fn("geom"), res.fn("binning"), res.fn("image"), None, P, int(degree), M, _ptr(bg_c), W, H,
+            _ptr(means3D_c), _ptr(sh_c), _ptr(colors_c), _ptr(opac_c), _ptr(scales_c), float(scale_modifier),
+            _ptr(rots_c), _ptr(cov_c), _ptr(view_c), _ptr(proj_c), _ptr(campos_c), float(tan_fovx),
+            float(tan_fovy), int(bool(prefiltered)), _ptr(out_color), _ptr(out_invdepth) if do_depth else None,
+            _ptr(radii), None, None, None, None, n_render, int(bool(debug)), _stream(dev), ctypes.byref(K))
+    _check(rc, "rasterize_gaussians")
+    return int(K.value), out_color, out_invdepth, radii, res.get("geom"), res.get("binning"), res.get("image")
+
+
+def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier,
+                                 cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color,
+                                 dL_dout_invdepth, sh, degree, campos, geomBuffer, R, binningBuffer, imageBuffer,
+                                 render_indices=None, parent_indices=None, interpolation_weights=None,
+                                 num_node_kids=None, debug=False):
+    _require_gpu(means3D)
+    dev = means3D.device
+    P = means3D.size(0)
+    H, W = dL_dout_color.size(1), dL_dout_color.size(2)
+    M = sh.size(1) if (sh is not None and sh.numel() != 0) else 0
+    f = lambda t, n: _dev_f32(t, n, dev)
+    means3D_c, sh_c, colors_c = f(means3D, "means3D"), f(sh, "sh"), f(colors, "colors_precomp")
+    scales_c, rots_c, cov_c = f(scales, "scales"), f(rotations, "rotations"), f(cov3D_precomp, "cov3D_precomp")
+    view_c, proj_c, campos_c, bg_c = f(viewmatrix, "viewmatrix"), f(projmatrix, "projmatrix"), f(campos, "campos"), \
+        f(background, "bg")
+    dpix = f(dL_dout_color, "dL_dout_color")
+    dinv = f(dL_dout_invdepth, "dL_dout_invdepth") if dL_dout_invdepth is not None else None
+    radii_c = radii.contiguous()
+
+    e = lambda *shape: torch.empty(*shape, dtype=torch.float32, device=dev)
+    dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D = e(P, 3), e(P, 3), e(P, 1), e(P, 3), e(P, 6)
+    dL_dsh = e(P, M, 3) if sh_c is not None else torch.zeros(P, 0, 3, device=dev)
+    if cov_c is None:
+        dL_dscales, dL_drotations = e(P, 3), e(P, 4)
+    else:
+        dL_dscales, dL_drotations = torch.zeros(P, 3, device=dev), torch.zeros(P, 4, device=dev)
+    res = _Resizer(dev)
+    with torch.cuda.device(dev):
+        rc = _L.gsr_rasterize_backward(
+            res.fn("scratch"), None, P, int(degree), M, int(R), _ptr(bg_c), W, H, _ptr(means3D_c), _ptr(sh_c),
+            _ptr(colors_c), _ptr(scales_c), float(scale_modifier), _ptr(rots_c), _ptr(cov_c), _ptr(view_c),
+            _ptr(proj_c), _ptr(campos_c), float(tan_fovx), float(tan_fovy), _ptr(radii_c), _ptr(geomBuffer),
+            _ptr(binningBuffer), _ptr(imageBuffer), _ptr(dpix), _ptr(dinv), _ptr(dL_dmeans2D), _ptr(dL_dcolors),
+            _ptr(dL_dopacity), _ptr(dL_dmeans3D), _ptr(dL_dcov3D), _ptr(dL_dsh) if sh_c is not None else None,
+            _ptr(dL_dscales) if cov_c is None else None, _ptr(dL_drotations) if cov_c is None else None,
+            int(bool(debug)), _stream(dev))
+    _check(rc, "rasterize_gaussians_backward")
+    return dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations
+
+
+def mark_visible(means3D, viewmatrix, projmatrix):
+    _require_gpu(means3D)
+    dev = means3D.device
+    P = means3D.size(0)
+    present = torch.empty(P, dtype=torch.uint8, device=dev)
+    m = _dev_f32(means3D, "means3D", dev)
+    v = _dev_f32(viewmatrix, "viewmatrix", dev)
+    p = _dev_f32(projmatrix, "projmatrix", dev)
+    with torch.cuda.device(dev):
+        rc = _L.gsr_mark_visible(P, _ptr(m), _ptr(v), _ptr(p), _ptr(present), _stream(dev))
+    _check(rc, "mark_visible")
+    return present.bool()
+
+
+def set_profiling(enable: bool) -> None:
+    _L.gsr_set_profiling(int(bool(enable)))
+
+
+STAGES = ("preprocess", "scan", "duplicate", "sort", "ranges", "render_fwd", "render_bwd", "preprocess_bwd")
+
+
+def stage_times_ms() -> dict:
+    buf = (ctypes.c_float * len(STAGES))()
+    n = _L.gsr_stage_times_ms(buf, len(STAGES))
+    return {STAGES[i]: float(buf[i]) for i in range(n)}

@@ -1,0 +1,158 @@
+"""diff_gaussian_rasterization -- MI355X (gfx950) drop-in for the differentiable Gaussian-splat
+rasterizer Street-sparse-3DGS imports at gaussian_renderer/__init__.py:14,17:
+
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    from diff_gaussian_rasterization import _C
+
+Public surface: the 17-field settings NamedTuple, the nn.Module whose forward
+takes means3D / means2D / opacities / shs | colors_precomp / scales+rotations | cov3D_precomp
+by keyword and returns (color (3,H,W), radii (P,) int32, invdepth (1,H,W)), markVisible, and
+the autograd Function that routes gradients to means3D, means2D (screen-space, NDC-scaled),
+shs, colors_precomp, opacities, scales, rotations and cov3D_precomp.  Compute runs in the
+hand-written HIP kernels of libgsr_hip.so (street-sparse-3dgs_amd/csrc); there is no CPU path.
+"""
+from __future__ import annotations
+
+from typing import NamedTuple
+
+import torch
+import torch.nn as nn
+
+from . import _C
+
+__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "_C"]
+
+
+def cpu_deep_copy_tuple(input_tuple):
+    return tuple(item.cpu().clone() if isinstance(item, torch.Tensor) else item for item in input_tuple)
+
+
+def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
+                        raster_settings):
+    return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
+                                     cov3Ds_precomp, raster_settings)
+
+
+def _hier(rs, name):
+    t = getattr(rs, name, None)
+    return torch.empty(0) if t is None else t
+
+
+class _RasterizeGaussians(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
+                raster_settings):
+        rs = raster_settings
+        do_depth = bool(getattr(rs, "do_depth", True))
+        args = (rs.bg, means3D, colors_precomp, opacities, scales, rotations, rs.scale_modifier, cov3Ds_precomp,
+                rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, sh,
+                rs.sh_degree, rs.campos, rs.prefiltered, rs.debug, _hier(rs, "render_indices"),
+                _hier(rs, "parent_indices"), _hier(rs, "interpolation_weights"), _hier(rs, "num_node_kids"),
+                do_depth)
+        if rs.debug:
+            cpu_args = cpu_deep_copy_tuple(args)
+            try:
+                num_rendered, color, invdepth, radii, geomBuffer, binningBuffer, imgBuffer = \
+                    _C.rasterize_gaussians(*args)
+            except Exception as ex:
+                torch.save(cpu_args, "snapshot_fw.dump")
+                print("\nAn error occured in forward. Please forward snapshot_fw.dump for debugging.")
+                raise ex
+        else:
+            num_rendered, color, invdepth, radii, geomBuffer, binningBuffer, imgBuffer = _C.rasterize_gaussians(*args)
+
+        ctx.raster_settings = rs
+        ctx.num_rendered = num_rendered
+        ctx.do_depth = do_depth
+        ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer,
+                              binningBuffer, imgBuffer)
+        ctx.mark_non_differentiable(radii)
+        return color, radii, invdepth
+
+    @staticmethod
+    def backward(ctx, grad_out_color, _grad_radii, grad_out_depth):
+        rs = ctx.raster_settings
+        colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer, binningBuffer, \
+            imgBuffer = ctx.saved_tensors
+        if grad_out_color is None:
+            grad_out_color = torch.zeros(3, rs.image_height, rs.image_width, device=means3D.device)
+        dinv = grad_out_depth if (ctx.do_depth and grad_out_depth is not None) else None
+        args = (rs.bg, means3D, radii, colors_precomp, scales, rotations, rs.scale_modifier, cov3Ds_precomp,
+                rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color.contiguous(),
+                dinv.contiguous() if dinv is not None else None, sh, rs.sh_degree, rs.campos, geomBuffer,
+                ctx.num_rendered, binningBuffer, imgBuffer, _hier(rs, "render_indices"), _hier(rs, "parent_indices"),
+                _hier(rs, "interpolation_weights"), _hier(rs, "num_node_kids"), rs.debug)
+        if rs.debug:
+            cpu_args = cpu_deep_copy_tuple(args)
+            try:
+                grads = _C.rasterize_gaussians_backward(*args)
+            except Exception as ex:
+                torch.save(cpu_args, "snapshot_bw.dump")
+                print("\nAn error occured in backward. Writing snapshot_bw.dump for debugging.\n")
+                raise ex
+        else:
+            grads = _C.rasterize_gaussians_backward(*args)
+        (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_sh, grad_scales,
+         grad_rotations) = grads
+
+        def keep(g, inp):
+            return g if (inp is not None and inp.numel() != 0) else None
+
+        return (grad_means3D, grad_means2D, keep(grad_sh, sh), keep(grad_colors_precomp, colors_precomp),
+                grad_opacities, keep(grad_scales, scales), keep(grad_rotations, rotations),
+                keep(grad_cov3Ds_precomp, cov3Ds_precomp), None)
+
+
+class GaussianRasterizationSettings(NamedTuple):
+    image_height: int
+    image_width: int
+    tanfovx: float
+    tanfovy: float
+    bg: torch.Tensor
+    scale_modifier: float
+    viewmatrix: torch.Tensor
+    projmatrix: torch.Tensor
+    sh_degree: int
+    campos: torch.Tensor
+    prefiltered: bool
+    debug: bool
+    do_depth: bool = True
+    render_indices: torch.Tensor = None
+    parent_indices: torch.Tensor = None
+    interpolation_weights: torch.Tensor = None
+    num_node_kids: torch.Tensor = None
+
+
+class GaussianRasterizer(nn.Module):
+    def __init__(self, raster_settings):
+        super().__init__()
+        self.raster_settings = raster_settings
+
+    def markVisible(self, positions):
+        # Mark visible points (based on frustum culling for camera) with a boolean
+        with torch.no_grad():
+            rs = self.raster_settings
+            visible = _C.mark_visible(positions, rs.viewmatrix, rs.projmatrix)
+        return visible
+
+    def forward(self, means3D, means2D, opacities, shs=None, colors_precomp=None, scales=None, rotations=None,
+                cov3D_precomp=None):
+        rs = self.raster_settings
+        if (shs is None and colors_precomp is None) or (shs is not None and colors_precomp is not None):
+            raise Exception('Please provide excatly one of either SHs or precomputed colors!')
+        if ((scales is None or rotations is None) and cov3D_precomp is None) or \
+                ((scales is not None or rotations is not None) and cov3D_precomp is not None):
+            raise Exception('Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!')
+        empty = torch.Tensor([])
+        if shs is None:
+            shs = empty
+        if colors_precomp is None:
+            colors_precomp = empty
+        if scales is None:
+            scales = empty
+        if rotations is None:
+            rotations = empty
+        if cov3D_precomp is None:
+            cov3D_precomp = empty
+        return rasterize_gaussians(means3D, means2D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp,
+                                   rs)

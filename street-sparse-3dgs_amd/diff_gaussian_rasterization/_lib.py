@@ -1,0 +1,69 @@
+"""ctypes binding of libgsr_hip.so (the C ABI declared in include/gsr.h).
+
+There is no fallback: if the gfx950 library is missing or fails to load, importing the
+rasterizer's _C module raises, so a GPU run can never silently use another path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+LIB_PATH = os.environ.get("GSR_LIBRARY", os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgsr_hip.so"))
+
+RESIZE_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+_f = ctypes.c_float
+_i64 = ctypes.c_int64
+
+# exported symbol -> (restype, argtypes); must match include/gsr.h
+SIGNATURES = {
+    "gsr_rasterize_forward": (_i, [RESIZE_FN, RESIZE_FN, RESIZE_FN, _vp, _i, _i, _i, _vp, _i, _i,
+                                   _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _f, _f,
+                                   _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp,
+                                   ctypes.POINTER(_i64)]),
+    "gsr_rasterize_backward": (_i, [RESIZE_FN, _vp, _i, _i, _i, _i64, _vp, _i, _i, _vp, _vp, _vp, _vp, _f,
+                                    _vp, _vp, _vp, _vp, _vp, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp,
+                                    _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
+    "gsr_mark_visible": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
+    "gsr_set_profiling": (_i, [_i]),
+    "gsr_stage_times_ms": (_i, [ctypes.POINTER(_f), _i]),
+    "gsr_abi_version": (_i, []),
+    "gsr_last_error": (ctypes.c_char_p, []),
+    "gsr_build_info": (ctypes.c_char_p, []),
+}
+
+ABI_VERSION = 1
+_lib = None
+
+
+class RasterizerLibraryError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load and type the library; raises RasterizerLibraryError if absent or mismatched."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RasterizerLibraryError(
+            f"gfx950 rasterizer library not found at {path}; build it with "
+            f"`python street-sparse-3dgs_amd/build_hip.py` (or __graft_entry__.build())")
+    try:
+        lib = ctypes.CDLL(path)
+    except OSError as e:  # pragma: no cover - depends on the host
+        raise RasterizerLibraryError(f"failed to load {path}: {e}") from e
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.gsr_abi_version() != ABI_VERSION:
+        raise RasterizerLibraryError("libgsr_hip.so ABI version mismatch; rebuild it")
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    return load().gsr_last_error().decode("utf-8", "replace")

@@ -1,0 +1,109 @@
+"""Shared test helpers: scene construction, running the HIP path through the public API, and
+decoding the scratch buffers (GeomState / BinningState / ImageState carve order of
+csrc/rasterizer.hip) so integer intermediates can be compared bit-exactly with the oracle."""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+ALIGN = 256
+
+
+def _align(x):
+    return (x + ALIGN - 1) // ALIGN * ALIGN
+
+
+def carve(sizes):
+    """sizes: list of (name, nbytes) in carve order -> {name: (offset, nbytes)}."""
+    off, out = 0, {}
+    for name, nb in sizes:
+        off = _align(off)
+        out[name] = (off, nb)
+        off += nb
+    return out
+
+
+def geom_layout(P):
+    return carve([("depth", 4 * P), ("tiles", 4 * P), ("offsets", 4 * P), ("xy", 8 * P), ("conic_o", 16 * P),
+                  ("rgbd", 16 * P), ("clamped", P)])
+
+
+def binning_layout(K):
+    return carve([("keys_unsorted", 8 * K), ("keys_sorted", 8 * K), ("vals_unsorted", 4 * K), ("point_list", 4 * K)])
+
+
+def image_layout(T, npix):
+    return carve([("ranges", 8 * T), ("final_T", 4 * npix), ("n_contrib", 4 * npix)])
+
+
+def view(buf_np, layout, name, dtype, shape=None):
+    off, nb = layout[name]
+    a = buf_np[off:off + nb].view(dtype)
+    return a if shape is None else a.reshape(shape)
+
+
+def decode_state(geom, binning, image, P, K, W, H):
+    g = geom.cpu().numpy()
+    b = binning.cpu().numpy()
+    im = image.cpu().numpy()
+    gl, bl = geom_layout(P), binning_layout(K)
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    il = image_layout(gx * gy, W * H)
+    return dict(
+        depths=view(g, gl, "depth", np.float32), tiles_touched=view(g, gl, "tiles", np.uint32),
+        offsets=view(g, gl, "offsets", np.uint32), xy=view(g, gl, "xy", np.float32, (P, 2)),
+        conic_opacity=view(g, gl, "conic_o", np.float32, (P, 4)), rgbd=view(g, gl, "rgbd", np.float32, (P, 4)),
+        clamped=view(g, gl, "clamped", np.uint8),
+        keys_unsorted=view(b, bl, "keys_unsorted", np.uint64), keys=view(b, bl, "keys_sorted", np.uint64),
+        vals_unsorted=view(b, bl, "vals_unsorted", np.uint32), point_list=view(b, bl, "point_list", np.uint32),
+        ranges=view(im, il, "ranges", np.uint32, (gx * gy, 2)), final_T=view(im, il, "final_T", np.float32, (H, W)),
+        n_contrib=view(im, il, "n_contrib", np.uint32, (H, W)))
+
+
+def rel_l2(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def psnr(a, b, peak=1.0):
+    mse = float(np.mean((np.asarray(a, np.float64) - np.asarray(b, np.float64)) ** 2))
+    return float("inf") if mse == 0 else 10 * math.log10(peak * peak / mse)
+
+
+def torch_inputs(scene, device, sh_degree=None, use_precomp_colors=False, use_precomp_cov=False,
+                 requires_grad=True, colors_precomp=None, cov3D_precomp=None):
+    """numpy synthetic scene (oracle.gs_oracle.synthetic_scene) -> torch tensors on device."""
+    import torch
+    t = lambda a: torch.tensor(np.asarray(a), dtype=torch.float32, device=device)
+    P = scene["means3D"].shape[0]
+    d = dict(means3D=t(scene["means3D"]), opacities=t(scene["opacities"]).reshape(P, 1),
+             means2D=torch.zeros(P, 3, device=device))
+    if use_precomp_colors:
+        d["colors_precomp"] = t(colors_precomp)
+    else:
+        d["shs"] = t(scene["shs"])
+    if use_precomp_cov:
+        d["cov3D_precomp"] = t(cov3D_precomp)
+    else:
+        d["scales"] = t(scene["scales"])
+        d["rotations"] = t(scene["rotations"])
+    if requires_grad:
+        for k, v in d.items():
+            v.requires_grad_(True)
+    return d
+
+
+def settings(scene, device, sh_degree, scale_modifier=1.0, do_depth=True, debug=False, bg=None):
+    import torch
+    from diff_gaussian_rasterization import GaussianRasterizationSettings
+    t = lambda a: torch.tensor(np.asarray(a), dtype=torch.float32, device=device)
+    return GaussianRasterizationSettings(
+        image_height=int(scene["H"]), image_width=int(scene["W"]), tanfovx=float(scene["tanfovx"]),
+        tanfovy=float(scene["tanfovy"]), bg=t(scene["bg"] if bg is None else bg), scale_modifier=scale_modifier,
+        viewmatrix=t(scene["view"]).reshape(4, 4), projmatrix=t(scene["proj"]).reshape(4, 4), sh_degree=sh_degree,
+        campos=t(scene["campos"]), prefiltered=False, debug=debug, do_depth=do_depth,
+        render_indices=torch.empty(0, dtype=torch.int32), parent_indices=torch.empty(0, dtype=torch.int32),
+        interpolation_weights=torch.empty(0, dtype=torch.float32, device=device),
+        num_node_kids=torch.empty(0, dtype=torch.int32, device=device))

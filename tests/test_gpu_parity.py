@@ -1,0 +1,260 @@
+"""GPU parity: the HIP path (through the public diff_gaussian_rasterization API) against the
+CPU oracle (oracle/gs_oracle.c, itself checked against the reference's helpers and against
+fp64 autograd in tests/test_oracle.py) on the same seeded inputs.
+
+Bars (stated here, SURVEY.md 8 / BASELINE.json north_star):
+  * integer / index work bit-exact: radii, tiles_touched, K, sorted 64-bit keys, point list,
+    tile ranges;
+  * n_contrib: exact except where an exp() ulp flips the alpha < 1/255 or T < 1e-4 test:
+    mismatching pixel fraction <= 1e-3;
+  * colour / inverse depth: PSNR vs oracle >= 80 dB and at most 1e-3 of pixels off by
+    > 1e-4;
+  * gradients: relative L2 error <= GRAD_TOL per tensor (fp32, summation order differs).
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from helpers import decode_state, psnr, rel_l2, settings, torch_inputs
+
+GRAD_TOL = 2e-4
+
+CASES = [
+    dict(name="tiny_deg3", P=300, W=64, H=48, deg=3, seed=1, log_scale=-2.5),
+    dict(name="odd_size_deg1", P=800, W=70, H=50, deg=1, seed=2, log_scale=-2.8),
+    dict(name="big_splats_deg0", P=200, W=96, H=64, deg=0, seed=3, log_scale=-1.3),
+    dict(name="offcenter_modifier_deg2", P=2000, W=96, H=64, deg=2, seed=4, log_scale=-3.0, primx=0.4, primy=0.6,
+         scale_modifier=1.7),
+    dict(name="no_depth", P=1500, W=80, H=64, deg=3, seed=5, log_scale=-3.0, do_depth=False),
+    dict(name="behind_camera", P=1500, W=96, H=64, deg=3, seed=6, log_scale=-3.0, behind=0.3),
+    dict(name="coarse_M4", P=1500, W=96, H=64, deg=1, seed=7, log_scale=-3.0, M=4),
+    dict(name="config1_10k_256", P=10000, W=256, H=256, deg=3, seed=0, log_scale=-4.0),
+]
+
+
+def make_scene(c):
+    import gs_oracle as O
+    s = O.synthetic_scene(c["P"], c["W"], c["H"], seed=c["seed"], sh_degree=3, log_scale_mean=c["log_scale"],
+                          primx=c.get("primx", 0.5), primy=c.get("primy", 0.5))
+    if c.get("M", 16) != 16:
+        s["shs"] = np.ascontiguousarray(s["shs"][:, :c["M"], :])
+    if c.get("behind"):
+        rng = np.random.default_rng(c["seed"] + 100)
+        idx = rng.random(c["P"]) < c["behind"]
+        s["means3D"][idx, 2] = rng.uniform(-5.0, 0.25, idx.sum()).astype(np.float32)
+    return s
+
+
+def run_oracle(s, c, dcol, dinv, colors_precomp=None, cov3D_precomp=None):
+    import gs_oracle as O
+    st = O.forward(s["means3D"], s["opacities"], s["view"], s["proj"], s["campos"], s["bg"], s["W"], s["H"],
+                   s["tanfovx"], s["tanfovy"], sh_degree=c["deg"],
+                   shs=None if colors_precomp is not None else s["shs"], colors_precomp=colors_precomp,
+                   scales=None if cov3D_precomp is not None else s["scales"],
+                   rotations=None if cov3D_precomp is not None else s["rotations"], cov3D_precomp=cov3D_precomp,
+                   scale_modifier=c.get("scale_modifier", 1.0), do_depth=c.get("do_depth", True))
+    g = O.backward(st, dcol, dinv)
+    return st, g
+
+
+def run_hip(s, c, dcol, dinv, colors_precomp=None, cov3D_precomp=None):
+    import torch
+    from diff_gaussian_rasterization import GaussianRasterizer, _C
+    dev = torch.device("cuda:0")
+    inp = torch_inputs(s, dev, use_precomp_colors=colors_precomp is not None,
+                       use_precomp_cov=cov3D_precomp is not None, colors_precomp=colors_precomp,
+                       cov3D_precomp=cov3D_precomp)
+    rs = settings(s, dev, c["deg"], c.get("scale_modifier", 1.0), c.get("do_depth", True))
+    # one raw _C call to get the scratch buffers for the bit-exact intermediate checks
+    e = torch.empty(0, device=dev)
+    raw = _C.rasterize_gaussians(rs.bg, inp["means3D"].detach(), inp.get("colors_precomp", e).detach(),
+                                 inp["opacities"].detach(), inp.get("scales", e).detach(),
+                                 inp.get("rotations", e).detach(), rs.scale_modifier,
+                                 inp.get("cov3D_precomp", e).detach(), rs.viewmatrix, rs.projmatrix, rs.tanfovx,
+                                 rs.tanfovy, rs.image_height, rs.image_width, inp.get("shs", e).detach(),
+                                 rs.sh_degree, rs.campos, False, False, rs.render_indices, rs.parent_indices,
+                                 rs.interpolation_weights, rs.num_node_kids, rs.do_depth)
+    torch.cuda.synchronize()
+    K = raw[0]
+    state = decode_state(raw[4], raw[5], raw[6], c["P"], K, s["W"], s["H"])
+    color, radii, invd = GaussianRasterizer(rs)(**inp)
+    loss = (color * torch.tensor(dcol, device=dev)).sum()
+    if c.get("do_depth", True):
+        loss = loss + (invd * torch.tensor(dinv, device=dev)).sum()
+    loss.backward()
+    torch.cuda.synchronize()
+    grads = {k: (v.grad.detach().cpu().numpy() if v.grad is not None else None) for k, v in inp.items()}
+    return dict(K=K, state=state, color=color.detach().cpu().numpy(), invdepth=invd.detach().cpu().numpy(),
+                radii=radii.cpu().numpy(), grads=grads)
+
+
+def compare(c, st, g, h, check_grads=True):
+    assert h["K"] == st["K"], f"K {h['K']} vs oracle {st['K']}"
+    np.testing.assert_array_equal(h["radii"], st["radii"])
+    S = h["state"]
+    np.testing.assert_array_equal(S["tiles_touched"], st["tiles_touched"])
+    np.testing.assert_array_equal(S["keys"], st["keys"])
+    np.testing.assert_array_equal(S["point_list"], st["point_list"])
+    np.testing.assert_array_equal(S["ranges"], st["ranges"])
+    nc_bad = float(np.mean(S["n_contrib"] != st["n_contrib"]))
+    assert nc_bad <= 1e-3, f"n_contrib mismatch fraction {nc_bad}"
+    assert psnr(h["color"], st["color"]) >= 80.0, psnr(h["color"], st["color"])
+    assert float(np.mean(np.abs(h["color"] - st["color"]) > 1e-4)) <= 1e-3
+    if c.get("do_depth", True):
+        assert rel_l2(h["invdepth"], st["invdepth"]) <= 1e-4
+    if not check_grads:
+        return
+    G = h["grads"]
+    pairs = [("means3D", "dL_dmeans3D"), ("means2D", "dL_dmeans2D"), ("opacities", "dL_dopacity")]
+    if G.get("shs") is not None:
+        pairs.append(("shs", "dL_dsh"))
+    if G.get("colors_precomp") is not None:
+        pairs.append(("colors_precomp", "dL_dcolors"))
+    if G.get("scales") is not None:
+        pairs += [("scales", "dL_dscales"), ("rotations", "dL_drotations")]
+    if G.get("cov3D_precomp") is not None:
+        pairs.append(("cov3D_precomp", "dL_dcov3D"))
+    for hk, ok in pairs:
+        err = rel_l2(G[hk].reshape(g[ok].shape), g[ok])
+        assert err <= GRAD_TOL, f"{c['name']}: grad {hk} rel L2 {err}"
+
+
+def upstream_grads(c, seed=99):
+    rng = np.random.default_rng(seed)
+    n = c["W"] * c["H"]
+    return ((rng.normal(size=(3, c["H"], c["W"])) / n * 1e3).astype(np.float32),
+            (rng.normal(size=(1, c["H"], c["W"])) / n * 1e3).astype(np.float32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c", CASES, ids=[c["name"] for c in CASES])
+def test_parity_vs_oracle(c):
+    s = make_scene(c)
+    dcol, dinv = upstream_grads(c)
+    st, g = run_oracle(s, c, dcol, dinv)
+    h = run_hip(s, c, dcol, dinv)
+    compare(c, st, g, h)
+
+
+@pytest.mark.gpu
+def test_precomputed_paths_and_cross_identity():
+    """colors_precomp / cov3D_precomp paths against the oracle, and the cross-path identity
+    pinned by reference code: rasterizing (shs, scales, rotations) equals rasterizing the
+    reference's python paths (eval_sh + 0.5 clamp, get_covariance) -- SURVEY.md 8(c)(ii)."""
+    import dense_torch as DT
+    import torch
+    c = dict(name="precomp", P=1500, W=96, H=64, deg=3, seed=11, log_scale=-3.0)
+    s = make_scene(c)
+    dcol, dinv = upstream_grads(c)
+    means = torch.tensor(s["means3D"], dtype=torch.float64)
+    d = means - torch.tensor(s["campos"], dtype=torch.float64)
+    d = d / d.norm(dim=1, keepdim=True)
+    colors = torch.clamp_min(DT.eval_sh_t(3, torch.tensor(s["shs"], dtype=torch.float64), d) + 0.5, 0.0)
+    colors = colors.float().numpy()
+    L = DT.quat_to_R(torch.tensor(s["rotations"], dtype=torch.float64)) * torch.tensor(
+        s["scales"], dtype=torch.float64)[:, None, :]
+    S3 = (L @ L.transpose(1, 2)).numpy()
+    cov = np.stack([S3[:, 0, 0], S3[:, 0, 1], S3[:, 0, 2], S3[:, 1, 1], S3[:, 1, 2], S3[:, 2, 2]], 1)
+    cov = cov.astype(np.float32)
+    st, g = run_oracle(s, c, dcol, dinv, colors_precomp=colors, cov3D_precomp=cov)
+    h = run_hip(s, c, dcol, dinv, colors_precomp=colors, cov3D_precomp=cov)
+    compare(c, st, g, h)
+    base = run_hip(s, c, dcol, dinv)
+    assert psnr(base["color"], h["color"]) > 60.0
+    assert float(np.mean(base["radii"] != h["radii"])) < 1e-2
+
+
+@pytest.mark.gpu
+def test_boundary_contract_and_determinism():
+    import torch
+    from diff_gaussian_rasterization import GaussianRasterizer
+    c = dict(name="contract", P=3000, W=120, H=72, deg=3, seed=12, log_scale=-3.2)
+    s = make_scene(c)
+    dev = torch.device("cuda:0")
+    outs = []
+    for _ in range(2):
+        inp = torch_inputs(s, dev)
+        inp["means2D"].retain_grad()
+        rs = settings(s, dev, 3)
+        color, radii, invd = GaussianRasterizer(rs)(**inp)
+        assert color.shape == (3, 72, 120) and color.dtype == torch.float32
+        assert radii.shape == (3000,) and radii.dtype == torch.int32
+        assert invd.shape == (1, 72, 120) and invd.dtype == torch.float32
+        (color.sum() + invd.sum()).backward()
+        g2 = inp["means2D"].grad
+        assert torch.all(g2[:, 2] == 0)
+        vis = radii > 0
+        assert torch.all(g2[~vis] == 0)
+        outs.append([color.detach().cpu()] + [v.grad.detach().cpu() for v in inp.values()])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b), "fwd+bwd must be bitwise reproducible (no float atomics)"
+
+
+@pytest.mark.gpu
+def test_empty_and_degenerate_inputs():
+    import torch
+    from diff_gaussian_rasterization import GaussianRasterizer, _C
+    dev = torch.device("cuda:0")
+    c = dict(name="empty", P=0, W=40, H=30, deg=0, seed=0, log_scale=-3.0)
+    s = make_scene(dict(c, P=10))
+    rs = settings(s, dev, 0)
+    inp = dict(means3D=torch.zeros(0, 3, device=dev, requires_grad=True),
+               means2D=torch.zeros(0, 3, device=dev, requires_grad=True),
+               opacities=torch.zeros(0, 1, device=dev, requires_grad=True),
+               shs=torch.zeros(0, 16, 3, device=dev, requires_grad=True),
+               scales=torch.zeros(0, 3, device=dev, requires_grad=True),
+               rotations=torch.zeros(0, 4, device=dev, requires_grad=True))
+    color, radii, invd = GaussianRasterizer(rs)(**inp)
+    bg = torch.tensor(s["bg"], device=dev)
+    assert torch.allclose(color, bg[:, None, None].expand(3, 30, 40))
+    assert radii.numel() == 0
+    color.sum().backward()
+    # all Gaussians behind the camera: K == 0 but the image is background
+    s2 = make_scene(dict(name="behind", P=50, W=40, H=30, deg=0, seed=1, log_scale=-3.0))
+    s2["means3D"][:, 2] = -3.0
+    inp2 = torch_inputs(s2, dev)
+    color2, radii2, _ = GaussianRasterizer(settings(s2, dev, 0))(**inp2)
+    assert int((radii2 > 0).sum()) == 0
+    assert torch.allclose(color2, torch.tensor(s2["bg"], device=dev)[:, None, None].expand(3, 30, 40))
+    color2.sum().backward()
+    assert torch.all(inp2["means3D"].grad == 0)
+    vis = _C.mark_visible(inp2["means3D"].detach(), settings(s2, dev, 0).viewmatrix, settings(s2, dev, 0).projmatrix)
+    assert not bool(vis.any())
+
+
+@pytest.mark.gpu
+def test_input_validation_errors():
+    import torch
+    from diff_gaussian_rasterization import GaussianRasterizer
+    dev = torch.device("cuda:0")
+    s = make_scene(dict(name="v", P=20, W=32, H=32, deg=0, seed=0, log_scale=-3.0))
+    inp = torch_inputs(s, dev, requires_grad=False)
+    rs = settings(s, dev, 0)
+    with pytest.raises(Exception, match="one of either SHs or precomputed colors"):
+        GaussianRasterizer(rs)(means3D=inp["means3D"], means2D=inp["means2D"], opacities=inp["opacities"],
+                               scales=inp["scales"], rotations=inp["rotations"])
+    with pytest.raises(Exception, match="scale/rotation pair"):
+        GaussianRasterizer(rs)(means3D=inp["means3D"], means2D=inp["means2D"], opacities=inp["opacities"],
+                               shs=inp["shs"], scales=inp["scales"])
+    with pytest.raises(RuntimeError, match="means3D must have dimensions"):
+        GaussianRasterizer(rs)(means3D=inp["means3D"][:, :2], means2D=inp["means2D"], opacities=inp["opacities"],
+                               shs=inp["shs"], scales=inp["scales"], rotations=inp["rotations"])
+
+
+@pytest.mark.gpu
+def test_config2_full_size_vs_oracle():
+    """Config 2 (500k Gaussians, 1920x1080): full-size bit-exact binning + image/gradient parity,
+    plus size-independent structure checks (sortedness, range partition)."""
+    c = dict(name="config2", P=500_000, W=1920, H=1080, deg=3, seed=0, log_scale=-4.0)
+    s = make_scene(c)
+    dcol, dinv = upstream_grads(c)
+    st, g = run_oracle(s, c, dcol, dinv)
+    h = run_hip(s, c, dcol, dinv)
+    S = h["state"]
+    keys = S["keys"]
+    assert np.all(keys[1:] >= keys[:-1])
+    r = S["ranges"]
+    nz = r[:, 1] > r[:, 0]
+    assert int((r[nz, 1] - r[nz, 0]).sum()) == h["K"]
+    compare(c, st, g, h)
