@@ -1,0 +1,239 @@
+"""bench.py -- fwd+bwd Mpix/s of the gfx950 Gaussian-splat rasterizer (BASELINE.json metric).
+
+One step = one forward + backward of GaussianRasterizer through its public API (autograd) on a
+1920x1080 frame of 1M synthetic Gaussians (SH degree 3), inputs resident in HBM, upstream
+gradients dL/dcolor and dL/dinvdepth ~ N(0,1)/Npix.  Multi-GPU (driver-launched
+via torch.distributed.run): one process per GPU, each rank rasterizes its own synthetic chunk
+(seed = rank) -- the product's one-chunk-per-GPU sharding, no data-path collective -- and
+`value` is the aggregate Mpix/s over all ranks (weak scaling).
+
+Prints ONE JSON line on rank 0.  Extras: "roofline" for the dominant kernel (algorithmic bytes
+per launch from SURVEY.md 8(d) / its HIP-event-measured average duration on the rasterizer's
+stream), "stages_ms" for every kernel, and "cpu_baseline" (the C oracle, timed on the host cores
+on one full-size fwd+bwd frame, rank 0 at N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "street-sparse-3dgs_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--gaussians", type=int, default=1_000_000)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--sh-degree", type=int, default=3)
+    ap.add_argument("--profile-steps", type=int, default=5, help="extra steps with per-stage HIP events")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--diag", action="store_true", help="print synced per-step fwd/bwd wall times to stderr")
+    return ap.parse_args()
+
+
+def algorithmic_bytes(P, Pv, K, T, npix, M=16):
+    """SURVEY.md 8(d) per-unit figures (M=16 constants; the SH term scales with M)."""
+    sh = 12 * M
+    n_pass = math.ceil((32 + max(1, math.ceil(math.log2(max(T, 2))))) / 8)
+    return {
+        "preprocess": (44 + sh) * P + 80 * P,
+        "scan": 4 * P,
+        "duplicate": 12 * K,
+        "sort": 24 * K * n_pass,
+        "ranges": 8 * K + 8 * T,
+        "render_fwd": 44 * K + 24 * npix,
+        "render_bwd": 44 * K + 24 * npix + 40 * Pv,
+        "preprocess_bwd": (356 + sh - 192) * P + (260 + sh - 192) * P,
+    }
+
+
+def make_inputs(P, W, H, deg, seed, device):
+    import numpy as np
+    import torch
+    import gs_oracle as O
+    s = O.synthetic_scene(P, W, H, seed=seed, sh_degree=deg)
+    t = lambda a: torch.tensor(np.asarray(a), dtype=torch.float32, device=device)
+    inp = dict(means3D=t(s["means3D"]), means2D=torch.zeros(P, 3, device=device), opacities=t(s["opacities"]),
+               shs=t(s["shs"]), scales=t(s["scales"]), rotations=t(s["rotations"]))
+    for v in inp.values():
+        v.requires_grad_(True)
+    rng = np.random.default_rng(seed + 1000)
+    gcol = t(rng.normal(size=(3, H, W)) / (W * H))
+    ginv = t(rng.normal(size=(1, H, W)) / (W * H))
+    return s, inp, gcol, ginv
+
+
+def cpu_baseline(s, P, W, H, deg):
+    """The C oracle (oracle/gs_oracle.c, OpenMP) on one full-size fwd+bwd frame."""
+    import numpy as np
+    import gs_oracle as O
+    rng = np.random.default_rng(7)
+    dcol = (rng.normal(size=(3, H, W)) / (W * H)).astype(np.float32)
+    dinv = (rng.normal(size=(1, H, W)) / (W * H)).astype(np.float32)
+    t0 = time.perf_counter()
+    st = O.forward(s["means3D"], s["opacities"], s["view"], s["proj"], s["campos"], s["bg"], W, H, s["tanfovx"],
+                   s["tanfovy"], sh_degree=deg, shs=s["shs"], scales=s["scales"], rotations=s["rotations"])
+    O.backward(st, dcol, dinv)
+    dt = time.perf_counter() - t0
+    return {"value": round(W * H / dt / 1e6, 4), "unit": "Mpix/s", "cores": O.num_threads(), "kind": "port",
+            "sample": f"1 fwd+bwd frame of the bench workload ({P} Gaussians, {W}x{H}, SH deg {deg}) through "
+                      f"the C oracle, {dt:.2f} s"}
+
+
+def latest_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/*pmc*.json)."""
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")), key=os.path.getmtime)
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+            if kernel in d.get("kernels", {}):
+                return d["kernels"][kernel].get("hbm_bytes_per_launch"), os.path.basename(f)
+        except Exception:
+            continue
+    return None, None
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer, _C
+
+    P, W, H, deg = a.gaussians, a.width, a.height, a.sh_degree
+    s, inp, gcol, ginv = make_inputs(P, W, H, deg, seed=rank, device=dev)
+    t = lambda x: torch.tensor(x, dtype=torch.float32, device=dev)
+    rs = GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=float(s["tanfovx"]), tanfovy=float(s["tanfovy"]), bg=t(s["bg"]),
+        scale_modifier=1.0, viewmatrix=t(s["view"]).reshape(4, 4), projmatrix=t(s["proj"]).reshape(4, 4),
+        sh_degree=deg, campos=t(s["campos"]), prefiltered=False, debug=False, do_depth=True,
+        render_indices=torch.empty(0, dtype=torch.int32), parent_indices=torch.empty(0, dtype=torch.int32),
+        interpolation_weights=torch.empty(0, device=dev), num_node_kids=torch.empty(0, dtype=torch.int32, device=dev))
+    raster = GaussianRasterizer(rs)
+    leaves = list(inp.values())
+
+    def step():
+        for v in leaves:
+            v.grad = None
+        color, radii, invd = raster(**inp)
+        torch.autograd.backward([color, invd], [gcol, ginv])
+        return radii
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if a.diag:
+        for it in range(5):
+            for v in leaves:
+                v.grad = None
+            torch.cuda.synchronize()
+            t_a = time.perf_counter()
+            color, radii, invd = raster(**inp)
+            torch.cuda.synchronize()
+            t_b = time.perf_counter()
+            torch.autograd.backward([color, invd], [gcol, ginv])
+            torch.cuda.synchronize()
+            t_c = time.perf_counter()
+            print(f"diag step {it}: fwd {1e3 * (t_b - t_a):.3f} ms  bwd {1e3 * (t_c - t_b):.3f} ms", file=sys.stderr)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        radii = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+
+    # per-stage device time with HIP events on the rasterizer's stream (separate, untimed steps)
+    _C.set_profiling(True)
+    acc = {}
+    for _ in range(max(1, a.profile_steps)):
+        radii = step()
+        for k, v in _C.stage_times_ms().items():
+            acc[k] = acc.get(k, 0.0) + v
+    _C.set_profiling(False)
+    stages = {k: v / max(1, a.profile_steps) for k, v in acc.items()}
+
+    # workload statistics for the algorithmic-bytes model
+    with torch.no_grad():
+        raw = _C.rasterize_gaussians(rs.bg, inp["means3D"], torch.empty(0, device=dev), inp["opacities"],
+                                     inp["scales"], inp["rotations"], 1.0, torch.empty(0, device=dev), rs.viewmatrix,
+                                     rs.projmatrix, rs.tanfovx, rs.tanfovy, H, W, inp["shs"], deg, rs.campos, False,
+                                     False, rs.render_indices, rs.parent_indices, rs.interpolation_weights,
+                                     rs.num_node_kids, True)
+    K = int(raw[0])
+    Pv = int((raw[3] > 0).sum().item())
+    T = ((W + 15) // 16) * ((H + 15) // 16)
+    npix = W * H
+    abytes = algorithmic_bytes(P, Pv, K, T, npix, M=inp["shs"].shape[1])
+    dom = max(stages, key=lambda k: stages[k]) if stages else "render_bwd"
+    dom_ms = stages.get(dom, 0.0)
+    achieved = abytes[dom] / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+    traffic, traffic_src = latest_traffic(dom)
+
+    ms_per_step = elapsed / a.steps * 1e3
+    value = world * npix * a.steps / elapsed / 1e6
+    out = {
+        "metric": "fwd+bwd Mpix/s at 1080p (1M Gaussians)",
+        "value": round(value, 3),
+        "unit": "Mpix/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded Gaussians in the frustum, SURVEY.md 8(d); one chunk per rank, seed = rank)",
+        "config": {"workload": f"rasterizer fwd+bwd, {P} Gaussians, SH degree {deg}, {W}x{H}, do_depth",
+                   "gaussians": P, "width": W, "height": H, "sh_degree": deg, "visible": Pv, "tile_instances": K,
+                   "tiles": T, "parallelism": f"chunk-per-gpu x{world}"},
+        "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                     "algorithmic_bytes": abytes[dom], "avg_ms": round(dom_ms, 5),
+                     "traffic_source": traffic_src},
+        "stages_ms": {k: round(v, 5) for k, v in stages.items()},
+        "pipeline_roofline": {"algorithmic_bytes": sum(abytes.values()),
+                              "frac": round(sum(abytes.values()) / (sum(stages.values()) * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+                              if stages else None},
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(s, P, W, H, deg)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -9,6 +9,8 @@
 
 namespace gsr {
 
+constexpr uint32_t kRedSerial = 32;
+
 __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
     int P, int D, int M, const float *__restrict__ means3D, const int *__restrict__ radii,
     const float *__restrict__ shs, const uint8_t *__restrict__ clamped, const float *__restrict__ scales,
@@ -17,17 +19,21 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
     float tanx, float tany, float fx, float fy, const uint32_t *__restrict__ tiles,
     const uint32_t *__restrict__ offsets, BwdScratch sc, GaussianGrads out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P) return;
+    const int lane = threadIdx.x & (kWave - 1);
+    const bool valid = i < P;
     const bool has_shs = shs != nullptr;
     const bool has_scales = cov3D_precomp == nullptr;
-    const bool vis = radii[i] > 0;
+    const bool vis = valid && radii[i] > 0;
 
+    // Sum this Gaussian's per-tile records (contiguous at its exclusive-scan offset).  Runs of
+    // more than kRedSerial records are summed by the whole wave (coalesced loads + DPP) so one
+    // large splat does not serialise its 63 neighbours.
     float g[10];
 #pragma unroll
     for (int k = 0; k < 10; k++) g[k] = 0.f;
-    if (vis) {
-        const uint32_t n = tiles[i];
-        const uint32_t off = i == 0 ? 0u : offsets[i - 1];
+    const uint32_t n = vis ? tiles[i] : 0u;
+    const uint32_t off = (vis && i > 0) ? offsets[i - 1] : 0u;
+    if (n <= kRedSerial) {
         for (uint32_t u = off; u < off + n; u++) {
             const float4 a = sc.ga[u];
             const float4 b = sc.gb[u];
@@ -37,6 +43,30 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
             g[8] += c.x; g[9] += c.y;
         }
     }
+    uint64_t big = __ballot(n > kRedSerial);
+    while (big) {
+        const int bl = __ffsll((unsigned long long)big) - 1;
+        big &= big - 1;
+        const uint32_t boff = (uint32_t)__shfl((int)off, bl);
+        const uint32_t bn = (uint32_t)__shfl((int)n, bl);
+        float q[10];
+#pragma unroll
+        for (int k = 0; k < 10; k++) q[k] = 0.f;
+        for (uint32_t u = boff + lane; u < boff + bn; u += kWave) {
+            const float4 a = sc.ga[u];
+            const float4 b = sc.gb[u];
+            const float2 c = sc.gc[u];
+            q[0] += a.x; q[1] += a.y; q[2] += a.z; q[3] += a.w;
+            q[4] += b.x; q[5] += b.y; q[6] += b.z; q[7] += b.w;
+            q[8] += c.x; q[9] += c.y;
+        }
+#pragma unroll
+        for (int k = 0; k < 10; k++) {
+            const float t = wave_sum(q[k]);
+            if (lane == bl) g[k] = t;
+        }
+    }
+    if (!valid) return;
     out.dmeans2D[3 * i + 0] = g[0];
     out.dmeans2D[3 * i + 1] = g[1];
     out.dmeans2D[3 * i + 2] = 0.f;

@@ -177,6 +177,35 @@ __device__ __forceinline__ float sh_channel(int deg, const float *sh, float x, f
 }
 
 // ------------------------------------------------------------------------------------------
+// Wave64 primitives (DPP; no LDS)
+// ------------------------------------------------------------------------------------------
+template <int kCtrl, int kRowMask = 0xF, int kBankMask = 0xF>
+__device__ __forceinline__ float dpp_f(float src) {
+    return __int_as_float(
+        __builtin_amdgcn_update_dpp(0, __float_as_int(src), kCtrl, kRowMask, kBankMask, false));
+}
+
+// Sum over the 64 lanes; result is wave-uniform.  Requires a full exec mask.
+__device__ __forceinline__ float wave_sum(float v) {
+    v += dpp_f<0xB1>(v);        // quad_perm [1,0,3,2]
+    v += dpp_f<0x4E>(v);        // quad_perm [2,3,0,1]
+    v += dpp_f<0x124>(v);       // row_ror:4
+    v += dpp_f<0x128>(v);       // row_ror:8  -> every lane holds its row (16 lanes) sum
+    v += dpp_f<0x142, 0xA>(v);  // row_bcast:15 -> rows 1,3 += rows 0,2
+    v += dpp_f<0x143, 0xC>(v);  // row_bcast:31 -> rows 2,3 += lane 31
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        const uint32_t o = (uint32_t)__shfl_xor((int)v, m, 64);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+// ------------------------------------------------------------------------------------------
 // Scratch-state layouts (carved out of the caller's byte buffers, 256-B aligned arrays)
 // ------------------------------------------------------------------------------------------
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }

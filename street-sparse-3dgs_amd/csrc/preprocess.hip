@@ -113,27 +113,58 @@ void launch_preprocess(const GaussianInputs &in, const Camera &cam, const GeomSt
                            cam.fy, cam.gx, cam.gy, gs, radii);
 }
 
-// One lane per Gaussian writes its (tile << 32 | depth bits, id) pairs in rect row-major order
-// at its exclusive-scan offset -- the "unsorted" instance index u used again in the backward.
+// Key duplication.  Lane i writes Gaussian i's (tile << 32 | depth bits, id) pairs in rect
+// row-major order at its exclusive-scan offset (the "unsorted" instance index u used again in
+// the backward).  Splats touching more than kDupSerial tiles would serialise their wave (a
+// 3-sigma outlier can cover hundreds of tiles), so those are written cooperatively by all 64
+// lanes of the wave, one ballot bit at a time.
+constexpr int kDupSerial = 16;
+
 __global__ __launch_bounds__(256) void duplicate_kernel(int P, int gx, int gy, const float2 *__restrict__ xy,
                                                         const float *__restrict__ depth,
                                                         const uint32_t *__restrict__ offsets,
                                                         const int *__restrict__ radii, uint64_t *__restrict__ keys,
                                                         uint32_t *__restrict__ vals) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P) return;
-    const int rad = radii[i];
-    if (rad <= 0) return;
-    uint32_t off = i == 0 ? 0u : offsets[i - 1];
-    const float2 p = xy[i];
-    const Rect r = get_rect(p.x, p.y, rad, gx, gy);
-    const uint64_t dbits = (uint64_t)__float_as_uint(depth[i]);
-    for (int y = r.y0; y < r.y1; y++)
-        for (int x = r.x0; x < r.x1; x++) {
-            keys[off] = ((uint64_t)(uint32_t)(y * gx + x) << 32) | dbits;
-            vals[off] = (uint32_t)i;
-            off++;
+    const int lane = threadIdx.x & (kWave - 1);
+    Rect r = {0, 0, 0, 0};
+    uint32_t off = 0;
+    uint32_t dbits = 0;
+    int area = 0;
+    if (i < P) {
+        const int rad = radii[i];
+        if (rad > 0) {
+            off = i == 0 ? 0u : offsets[i - 1];
+            const float2 p = xy[i];
+            r = get_rect(p.x, p.y, rad, gx, gy);
+            area = (r.x1 - r.x0) * (r.y1 - r.y0);
+            dbits = __float_as_uint(depth[i]);
         }
+    }
+    if (area <= kDupSerial) {
+        uint32_t o = off;
+        for (int y = r.y0; y < r.y1; y++)
+            for (int x = r.x0; x < r.x1; x++) {
+                keys[o] = ((uint64_t)(uint32_t)(y * gx + x) << 32) | (uint64_t)dbits;
+                vals[o] = (uint32_t)i;
+                o++;
+            }
+    }
+    uint64_t big = __ballot(area > kDupSerial);
+    while (big) {
+        const int b = __ffsll((unsigned long long)big) - 1;
+        big &= big - 1;
+        const int bx0 = __shfl(r.x0, b), by0 = __shfl(r.y0, b), bw = __shfl(r.x1 - r.x0, b);
+        const int barea = __shfl(area, b);
+        const uint32_t boff = (uint32_t)__shfl((int)off, b);
+        const uint64_t bd = (uint64_t)(uint32_t)__shfl((int)dbits, b);
+        const uint32_t bi = (uint32_t)__shfl(i, b);
+        for (int idx = lane; idx < barea; idx += kWave) {
+            const int y = by0 + idx / bw, x = bx0 + idx % bw;
+            keys[boff + idx] = ((uint64_t)(uint32_t)(y * gx + x) << 32) | bd;
+            vals[boff + idx] = bi;
+        }
+    }
 }
 
 void launch_duplicate(int P, const Camera &cam, const GeomState &gs, const int *radii, const BinningState &bs,

@@ -6,6 +6,7 @@
 // backward: render bwd (per-instance records) -> preprocess bwd (per-Gaussian sum + chain).
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 
 #include "../../include/gsr.h"
@@ -16,13 +17,15 @@ using namespace gsr;
 namespace {
 
 thread_local std::string g_err;
-thread_local int g_profile = 0;
-thread_local hipEvent_t g_ev[12];
-thread_local bool g_ev_init = false;
-thread_local int g_ev_fwd_recorded = 0, g_ev_bwd_recorded = 0;
 thread_local uint32_t *g_pinned = nullptr;
 
+// Stage profiling is process-wide: torch runs the backward on its autograd device thread.
 constexpr int kStages = 8;
+std::mutex g_prof_mu;
+int g_profile = 0;
+bool g_ev_init = false;
+hipEvent_t g_ev_begin[kStages], g_ev_end[kStages];
+bool g_ev_recorded[kStages];
 
 int fail(int code, const std::string &msg) {
     g_err = msg;
@@ -31,13 +34,29 @@ int fail(int code, const std::string &msg) {
 
 void ensure_events() {
     if (g_ev_init) return;
-    for (auto &e : g_ev) (void)hipEventCreate(&e);
+    for (int k = 0; k < kStages; k++) {
+        (void)hipEventCreate(&g_ev_begin[k]);
+        (void)hipEventCreate(&g_ev_end[k]);
+        g_ev_recorded[k] = false;
+    }
     g_ev_init = true;
 }
 
-void mark(int idx, hipStream_t s) {
-    if (g_profile) (void)hipEventRecord(g_ev[idx], s);
-}
+// Brackets exactly the device work of one stage (no host gaps inside the bracket).
+struct StageTimer {
+    int k;
+    hipStream_t s;
+    bool on;
+    StageTimer(int stage, hipStream_t stream) : k(stage), s(stream), on(g_profile != 0) {
+        if (on) (void)hipEventRecord(g_ev_begin[k], s);
+    }
+    ~StageTimer() {
+        if (on) {
+            (void)hipEventRecord(g_ev_end[k], s);
+            g_ev_recorded[k] = true;
+        }
+    }
+};
 
 int check(const char *stage, int debug, hipStream_t s) {
     hipError_t e = hipGetLastError();
@@ -165,29 +184,25 @@ const char *gsr_build_info(void) {
 }
 
 int gsr_set_profiling(int enable) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    if (enable) ensure_events();
+    for (int k = 0; k < kStages; k++) g_ev_recorded[k] = false;
     g_profile = enable ? 1 : 0;
-    if (g_profile) ensure_events();
-    g_ev_fwd_recorded = g_ev_bwd_recorded = 0;
     return GSR_OK;
 }
 
 int gsr_stage_times_ms(float *out, int max_stages) {
-    if (!g_profile) return 0;
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    if (!g_ev_init) return 0;
     int n = 0;
-    auto el = [](hipEvent_t a, hipEvent_t b) {
+    for (; n < kStages && n < max_stages; n++) {
         float ms = 0.f;
-        if (hipEventSynchronize(b) != hipSuccess) return 0.f;
-        if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.f;
-        return ms;
-    };
-    float t[kStages] = {0};
-    if (g_ev_fwd_recorded)
-        for (int k = 0; k < 6; k++) t[k] = el(g_ev[k], g_ev[k + 1]);
-    if (g_ev_bwd_recorded) {
-        t[6] = el(g_ev[7], g_ev[8]);
-        t[7] = el(g_ev[8], g_ev[9]);
+        if (g_ev_recorded[n] && hipEventSynchronize(g_ev_end[n]) == hipSuccess &&
+            hipEventElapsedTime(&ms, g_ev_begin[n], g_ev_end[n]) == hipSuccess)
+            out[n] = ms;
+        else
+            out[n] = 0.f;
     }
-    for (; n < kStages && n < max_stages; n++) out[n] = t[n];
     return n;
 }
 
@@ -236,18 +251,17 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
 
     GaussianInputs in{P, D, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp,
                       scale_modifier};
-    if (g_profile) {
-        ensure_events();
-        g_ev_fwd_recorded = 1;
+    {
+        StageTimer st(0, s);
+        launch_preprocess(in, cam, gs, radii, s);
     }
-    mark(0, s);
-    launch_preprocess(in, cam, gs, radii, s);
     if ((rc = check("preprocess", debug, s))) return rc;
-    mark(1, s);
-    if (inclusive_scan_u32(gs.scan_tmp, gs.scan_tmp_bytes, gs.tiles, gs.offsets, P, s) != hipSuccess)
-        return fail(GSR_ERR_DEVICE, "inclusive scan failed");
+    {
+        StageTimer st(1, s);
+        if (inclusive_scan_u32(gs.scan_tmp, gs.scan_tmp_bytes, gs.tiles, gs.offsets, P, s) != hipSuccess)
+            return fail(GSR_ERR_DEVICE, "inclusive scan failed");
+    }
     if ((rc = check("scan", debug, s))) return rc;
-    mark(2, s);
 
     int64_t K = 0;
     if (P > 0) {
@@ -267,20 +281,28 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
     if (!bbase) return fail(GSR_ERR_ALLOCATION, "binning buffer allocation failed");
     const BinningState bs = carve_binning(bbase, K, end_bit, nullptr);
 
-    if (K > 0) launch_duplicate(P, cam, gs, radii, bs, s);
+    {
+        StageTimer st(2, s);
+        if (K > 0) launch_duplicate(P, cam, gs, radii, bs, s);
+    }
     if ((rc = check("duplicateWithKeys", debug, s))) return rc;
-    mark(3, s);
-    if (sort_pairs_u64(bs.sort_tmp, bs.sort_tmp_bytes, bs.keys_unsorted, bs.keys_sorted, bs.vals_unsorted,
-                       bs.point_list, K, end_bit, s) != hipSuccess)
-        return fail(GSR_ERR_DEVICE, "radix sort failed");
+    {
+        StageTimer st(3, s);
+        if (sort_pairs_u64(bs.sort_tmp, bs.sort_tmp_bytes, bs.keys_unsorted, bs.keys_sorted, bs.vals_unsorted,
+                           bs.point_list, K, end_bit, s) != hipSuccess)
+            return fail(GSR_ERR_DEVICE, "radix sort failed");
+    }
     if ((rc = check("sort", debug, s))) return rc;
-    mark(4, s);
-    launch_ranges(K, T, bs, is, s);
+    {
+        StageTimer st(4, s);
+        launch_ranges(K, T, bs, is, s);
+    }
     if ((rc = check("identifyTileRanges", debug, s))) return rc;
-    mark(5, s);
-    launch_render_fwd(cam, gs, bs, is, background, out_color, out_invdepth, s);
+    {
+        StageTimer st(5, s);
+        launch_render_fwd(cam, gs, bs, is, background, out_color, out_invdepth, s);
+    }
     if ((rc = check("render", debug, s))) return rc;
-    mark(6, s);
     if (num_rendered) *num_rendered = K;
     return GSR_OK;
 }
@@ -302,10 +324,11 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
     if (!scratch) return fail(GSR_ERR_INVALID_ARGUMENT, "scratch callback must be non-NULL");
     if (!geom_buffer || !binning_buffer || !image_buffer || !dL_dpix)
         return fail(GSR_ERR_INVALID_ARGUMENT, "NULL state buffer / dL_dpix");
-    if (!dL_dmeans2D || !dL_dcolors || !dL_dopacity || !dL_dmeans3D || !dL_dcov3D)
+    if (P > 0 && !radii) return fail(GSR_ERR_INVALID_ARGUMENT, "NULL radii");
+    if (P > 0 && (!dL_dmeans2D || !dL_dcolors || !dL_dopacity || !dL_dmeans3D || !dL_dcov3D))
         return fail(GSR_ERR_INVALID_ARGUMENT, "NULL gradient output");
-    if (shs && !dL_dsh) return fail(GSR_ERR_INVALID_ARGUMENT, "NULL dL_dsh");
-    if (!cov3D_precomp && (!dL_dscales || !dL_drotations))
+    if (P > 0 && shs && !dL_dsh) return fail(GSR_ERR_INVALID_ARGUMENT, "NULL dL_dsh");
+    if (P > 0 && !cov3D_precomp && (!dL_dscales || !dL_drotations))
         return fail(GSR_ERR_INVALID_ARGUMENT, "NULL dL_dscales / dL_drotations");
 
     const Camera cam = make_camera(viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, width, height);
@@ -324,17 +347,16 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
                       scale_modifier};
     GaussianGrads out{dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
                       dL_drotations};
-    if (g_profile) {
-        ensure_events();
-        g_ev_bwd_recorded = 1;
+    {
+        StageTimer st(6, s);
+        if (R > 0) launch_render_bwd(cam, gs, bs, is, radii, background, dL_dpix, dL_dinvdepth, sc, s);
     }
-    mark(7, s);
-    if (R > 0) launch_render_bwd(cam, gs, bs, is, radii, background, dL_dpix, dL_dinvdepth, sc, s);
     if ((rc = check("render backward", debug, s))) return rc;
-    mark(8, s);
-    launch_preprocess_bwd(in, cam, gs, radii, sc, out, s);
+    {
+        StageTimer st(7, s);
+        launch_preprocess_bwd(in, cam, gs, radii, sc, out, s);
+    }
     if ((rc = check("preprocess backward", debug, s))) return rc;
-    mark(9, s);
     return GSR_OK;
 }
 
