@@ -646,3 +646,12 @@ int gso_num_threads(void) {
     return 1;
 #endif
 }
+
+/* ---- test hooks: the pieces the reference's Python twins pin (tests/golden) ---- */
+void gso_eval_sh(int n, int deg, int M, const float *shs, const float *dirs, float *rgb, unsigned char *clamped) {
+    for (int i = 0; i < n; i++) sh_to_rgb(deg, M, shs + (size_t)i * M * 3, dirs + 3 * i, rgb + 3 * i, clamped + 3 * i);
+}
+
+void gso_cov3d(int n, const float *scales, float mod, const float *rots, float *cov) {
+    for (int i = 0; i < n; i++) cov3d_from_scale_rot(scales + 3 * i, mod, rots + 4 * i, cov + 6 * i);
+}

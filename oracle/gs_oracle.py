@@ -218,6 +218,45 @@ def camera(W, H, fovx_deg=60.0, R=None, t=None, znear=0.01, zfar=100.0, primx=0.
     return view, proj, campos, math.tan(fovx * 0.5), math.tan(fovy * 0.5)
 
 
+def camera_from(W, H, R, T, FoVx, FoVy, primx=0.5, primy=0.5, znear=0.01, zfar=100.0):
+    """scene/cameras.py:96-99 restated: (viewmatrix, projmatrix, campos, tanfovx, tanfovy)
+    for a COLMAP-style camera (R = camera-to-world rotation as stored by the reference, T =
+    world-to-camera translation)."""
+    Rt = np.zeros((4, 4))
+    Rt[:3, :3] = np.asarray(R, np.float64).T
+    Rt[:3, 3] = T
+    Rt[3, 3] = 1.0
+    C2W = np.linalg.inv(Rt)
+    Rt = np.linalg.inv(C2W)  # getWorld2View2 round trip (trans = 0, scale = 1)
+    view = np.float32(Rt).T.copy()
+    Pm = projection_matrix(znear, zfar, FoVx, FoVy, primx, primy)
+    proj = (view.astype(np.float32) @ Pm.T.astype(np.float32)).astype(np.float32)
+    campos = np.linalg.inv(view.astype(np.float64))[3, :3].astype(np.float32)
+    return view, proj, campos, math.tan(FoVx * 0.5), math.tan(FoVy * 0.5)
+
+
+def eval_sh(deg, shs, dirs):
+    """C restatement of the SH colour (utils/sh_utils.py:57-112 + the +0.5 / clamp_min(0) of
+    gaussian_renderer/__init__.py:89): shs (n, M, 3), dirs (n, 3) -> rgb (n, 3), clamped."""
+    shs = _f32(shs)
+    n, M = shs.shape[0], shs.shape[1]
+    dirs = _f32(dirs).reshape(n, 3)
+    rgb = np.zeros((n, 3), np.float32)
+    cl = np.zeros((n, 3), np.uint8)
+    lib().gso_eval_sh(ctypes.c_int(n), ctypes.c_int(deg), ctypes.c_int(M), _p(shs), _p(dirs), _p(rgb), _p(cl))
+    return rgb, cl.astype(bool)
+
+
+def cov3d(scales, rotations, scale_modifier=1.0):
+    """C restatement of cov3D = (R S)(R S)^T as 6 floats (scene/gaussian_model.py:33-37)."""
+    scales = _f32(scales).reshape(-1, 3)
+    rotations = _f32(rotations).reshape(-1, 4)
+    out = np.zeros((scales.shape[0], 6), np.float32)
+    lib().gso_cov3d(ctypes.c_int(scales.shape[0]), _p(scales), ctypes.c_float(scale_modifier), _p(rotations),
+                    _p(out))
+    return out
+
+
 def synthetic_scene(P, W, H, seed=0, sh_degree=3, fovx_deg=60.0, zmin=2.0, zmax=20.0, log_scale_mean=-4.0,
                     log_scale_std=0.5, primx=0.5, primy=0.5):
     """Seeded synthetic Gaussians as SURVEY.md section 8(d) defines them."""

@@ -1,0 +1,174 @@
+"""CPU tests of the oracle: pinned against the reference's own helpers (golden fixtures made by
+tests/golden/make_golden.py from /root/reference) and against an independent fp64 autograd
+formulation (oracle/dense_torch.py) of the same renderer."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+import dense_torch as DT
+import gs_oracle as O
+from helpers import rel_l2
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def test_sh_matches_reference_eval_sh():
+    g = np.load(os.path.join(GOLD, "sh_eval.npz"))
+    for deg in range(4):
+        rgb, clamped = O.eval_sh(deg, g["sh"], g["dirs"])
+        np.testing.assert_array_equal(rgb, g[f"rgb_deg{deg}"])  # bit-exact
+        np.testing.assert_array_equal(clamped, (g[f"eval_deg{deg}"] + 0.5) < 0)
+
+
+def test_covariance_matches_reference_get_covariance():
+    c = np.load(os.path.join(GOLD, "covariance.npz"))
+    for mod in (1.0, 0.5, 2.0):
+        np.testing.assert_array_equal(O.cov3d(c["scales"], c["rot_normalized"], mod), c[f"cov_mod{mod}"])
+
+
+def test_camera_matrices_match_reference():
+    cams = np.load(os.path.join(GOLD, "cameras.npz"))
+    for i in range(int(cams["n"])):
+        k = lambda n: cams[f"cam{i}_{n}"]
+        v, p, cp, tx, ty = O.camera_from(int(k("W")), int(k("H")), k("R"), k("T"), float(k("FoVx")),
+                                         float(k("FoVy")), float(k("primx")), float(k("primy")))
+        np.testing.assert_array_equal(v, k("viewmatrix"))
+        np.testing.assert_array_equal(p, k("projmatrix"))
+        np.testing.assert_allclose(cp, k("campos"), atol=1e-6)
+        assert tx == pytest.approx(float(k("tanfovx")), abs=0)
+        assert ty == pytest.approx(float(k("tanfovy")), abs=0)
+
+
+def _scene(P, W, H, seed, deg, log_scale=-3.0, spread=0.95, **kw):
+    s = O.synthetic_scene(P, W, H, seed=seed, sh_degree=3, log_scale_mean=log_scale, **kw)
+    if spread != 0.95:  # push some means outside the 1.3*tanfov clamp
+        rng = np.random.default_rng(seed + 7)
+        m = s["means3D"]
+        m[:, 0] = rng.uniform(-spread, spread, P) * s["tanfovx"] * m[:, 2]
+        m[:, 1] = rng.uniform(-spread, spread, P) * s["tanfovy"] * m[:, 2]
+    return s
+
+
+def _fwd(s, W, H, deg, **kw):
+    return O.forward(s["means3D"], s["opacities"], s["view"], s["proj"], s["campos"], s["bg"], W, H, s["tanfovx"],
+                     s["tanfovy"], sh_degree=deg, **kw)
+
+
+DENSE_CASES = [
+    dict(P=300, W=64, H=48, seed=3, deg=3, log_scale=-2.5),
+    dict(P=600, W=70, H=50, seed=4, deg=1, log_scale=-2.7),
+    dict(P=400, W=64, H=64, seed=5, deg=2, log_scale=-2.6, spread=1.8),   # 1.3*tanfov clamp active
+    dict(P=400, W=80, H=48, seed=6, deg=0, log_scale=-2.4, mod=1.6),      # scale_modifier != 1
+    dict(P=400, W=64, H=48, seed=8, deg=3, log_scale=-2.5, primx=0.35, primy=0.6),
+]
+
+
+@pytest.mark.parametrize("c", DENSE_CASES)
+def test_oracle_backward_matches_fp64_autograd(c):
+    W, H, deg = c["W"], c["H"], c["deg"]
+    kw = {k: c[k] for k in ("primx", "primy") if k in c}
+    s = _scene(c["P"], W, H, c["seed"], deg, c["log_scale"], c.get("spread", 0.95), **kw)
+    st = _fwd(s, W, H, deg, shs=s["shs"], scales=s["scales"], rotations=s["rotations"],
+              scale_modifier=c.get("mod", 1.0))
+    rng = np.random.default_rng(0)
+    gc = rng.normal(size=(3, H, W))
+    gd = rng.normal(size=(1, H, W))
+    b = O.backward(st, gc, gd)
+    d = DT.dense_grads(st, gc, gd)
+    assert rel_l2(st["color"], d["color"]) < 1e-5
+    assert rel_l2(st["invdepth"], d["invdepth"]) < 1e-5
+    for dk, ok in [("dL_dmeans3D", "dL_dmeans3D"), ("dL_dmeans2D", "dL_dmeans2D"), ("dL_dopacities", "dL_dopacity"),
+                   ("dL_dshs", "dL_dsh"), ("dL_dscales", "dL_dscales"), ("dL_drotations", "dL_drotations")]:
+        assert rel_l2(b[ok].reshape(d[dk].shape), d[dk]) < 5e-5, dk
+
+
+def test_oracle_precomputed_paths_match_fp64_autograd():
+    W, H = 64, 48
+    s = _scene(400, W, H, 9, 3, -2.5)
+    colors = np.random.default_rng(1).uniform(0, 1, (400, 3)).astype(np.float32)
+    cov = O.cov3d(s["scales"], s["rotations"])
+    st = _fwd(s, W, H, 3, colors_precomp=colors, cov3D_precomp=cov)
+    rng = np.random.default_rng(2)
+    gc, gd = rng.normal(size=(3, H, W)), rng.normal(size=(1, H, W))
+    b = O.backward(st, gc, gd)
+    d = DT.dense_grads(st, gc, gd)
+    for dk, ok in [("dL_dmeans3D", "dL_dmeans3D"), ("dL_dopacities", "dL_dopacity"), ("dL_dcolors", "dL_dcolors"),
+                   ("dL_dcov3D", "dL_dcov3D")]:
+        assert rel_l2(b[ok].reshape(d[dk].shape), d[dk]) < 5e-5, dk
+
+
+def test_cross_path_identity_in_oracle():
+    """(shs, scales, rotations) == (colors_precomp from eval_sh, cov3D_precomp from cov3d) exactly."""
+    W, H = 96, 64
+    s = _scene(1500, W, H, 10, 3)
+    a = _fwd(s, W, H, 3, shs=s["shs"], scales=s["scales"], rotations=s["rotations"])
+    d = s["means3D"] - s["campos"]
+    dn = (d / np.sqrt((d.astype(np.float32) ** 2).sum(1, keepdims=True))).astype(np.float32)
+    # direction normalisation differs in rounding between numpy and C: compare images, not bits
+    rgb, _ = O.eval_sh(3, s["shs"], dn)
+    b = _fwd(s, W, H, 3, colors_precomp=rgb, cov3D_precomp=O.cov3d(s["scales"], s["rotations"]))
+    np.testing.assert_array_equal(a["radii"], b["radii"])
+    np.testing.assert_array_equal(a["point_list"], b["point_list"])
+    assert np.abs(a["color"] - b["color"]).max() < 1e-5
+
+
+def test_binning_invariants():
+    W, H = 200, 120
+    s = _scene(3000, W, H, 11, 3, -3.2)
+    st = _fwd(s, W, H, 3, shs=s["shs"], scales=s["scales"], rotations=s["rotations"])
+    keys, pl, rng_ = st["keys"], st["point_list"], st["ranges"]
+    assert st["K"] == int(st["tiles_touched"].sum())
+    assert np.all(keys[1:] >= keys[:-1])
+    tiles = (keys >> np.uint64(32)).astype(np.int64)
+    dbits = (keys & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    np.testing.assert_array_equal(dbits, st["depths"][pl].view(np.uint32))
+    for t in np.unique(tiles):
+        lo, hi = rng_[t]
+        assert np.all(tiles[lo:hi] == t)
+    # stable: equal keys keep Gaussian-index order
+    same = keys[1:] == keys[:-1]
+    assert np.all(pl[1:][same] > pl[:-1][same])
+    # n_contrib never exceeds the tile's list length
+    gx = (W + 15) // 16
+    for y in range(0, H, 7):
+        for x in range(0, W, 7):
+            t = (y // 16) * gx + x // 16
+            assert st["n_contrib"][y, x] <= rng_[t, 1] - rng_[t, 0]
+
+
+def test_empty_and_culled_inputs():
+    W, H = 40, 30
+    s = _scene(20, W, H, 12, 0)
+    s["means3D"][:, 2] = -1.0
+    st = _fwd(s, W, H, 0, shs=s["shs"], scales=s["scales"], rotations=s["rotations"])
+    assert st["K"] == 0 and np.all(st["radii"] == 0)
+    np.testing.assert_allclose(st["color"], np.broadcast_to(s["bg"][:, None, None], (3, H, W)))
+    b = O.backward(st, np.ones((3, H, W)), np.ones((1, H, W)))
+    assert np.all(b["dL_dmeans3D"] == 0)
+    assert not O.mark_visible(s["means3D"], s["view"], s["proj"]).any()
+
+
+def test_render_post_interpolation_fixture():
+    """Pins the hierarchy LOD interpolation render_post performs before rasterizing
+    (gaussian_renderer/__init__.py:200-243) -- the input contract of SURVEY 8(f) row 3."""
+    f = np.load(os.path.join(GOLD, "render_post.npz"))
+    ri, pi, w = f["render_indices"].astype(np.int64), f["parent_indices"].astype(np.int64), f["interpolation_weights"]
+    n, sky = len(ri), int(f["skybox"])
+    t = w[:n, None]
+    means = t * f["xyz"][ri] + (1 - t) * f["xyz"][pi]
+    scal = t * f["scaling"][ri] + (1 - t) * f["scaling"][pi]
+    par = f["rotation"][pi].copy()
+    rot = f["rotation"][ri]
+    par[(rot * par).sum(1) < 0] *= -1
+    rots = t * rot + (1 - t) * par
+    op = t * f["opacity"][ri] + (1 - t) * f["opacity"][pi]
+    N = f["xyz"].shape[0]
+    sk = np.arange(N - sky, N)
+    np.testing.assert_allclose(f["out_means3D"], np.concatenate([means, f["xyz"][sk]]), atol=1e-6)
+    np.testing.assert_allclose(f["out_scales"], np.concatenate([scal, f["scaling"][sk]]), atol=1e-6)
+    np.testing.assert_allclose(f["out_rotations"], np.concatenate([rots, f["rotation"][sk]]), atol=1e-6)
+    np.testing.assert_allclose(f["out_opacities"], np.concatenate([op, f["opacity"][sk]]), atol=1e-6)
+    assert f["out_shs"].shape == (n + sky, 16, 3)
