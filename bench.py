@@ -156,6 +156,19 @@ def main():
             torch.cuda.synchronize()
             t_c = time.perf_counter()
             print(f"diag step {it}: fwd {1e3 * (t_b - t_a):.3f} ms  bwd {1e3 * (t_c - t_b):.3f} ms", file=sys.stderr)
+        ms = torch.cuda.memory_stats(dev)
+        print("diag alloc:", {k: ms.get(k) for k in ("num_alloc_retries", "num_device_alloc", "num_device_free",
+                                                      "reserved_bytes.all.current", "allocated_bytes.all.peak")},
+              file=sys.stderr)
+        import cProfile
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        pr.disable()
+        pstats.Stats(pr, stream=sys.stderr).sort_stats("cumulative").print_stats(18)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

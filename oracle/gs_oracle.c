@@ -287,6 +287,17 @@ void gso_ranges(unsigned long long K, const unsigned long long *keys, int T, uns
     }
 }
 
+/* Gaussian exponent at pixel offset d = mean2D - pixel, in the fixed FMA order the HIP kernels
+ * use:  power = -0.5 (a dx^2 + c dy^2) - b dx dy.  G = exp(power) evaluated as exp2(power*log2e)
+ * (the GPU's v_exp_f32 form). */
+static const float GS_LOG2E = 1.4426950408889634f;
+static inline float gauss_power(const float *co, float dx, float dy) {
+    const float adxdx = co[0] * dx * dx;
+    const float t = fmaf(co[2] * dy, dy, adxdx);
+    return fmaf(-(co[1] * dx), dy, -0.5f * t);
+}
+static inline float gexp(float power) { return exp2f(power * GS_LOG2E); }
+
 /* ------------------------------------------------------------------------------------------
  * Render forward (A9): per tile front-to-back alpha blending, colour + inverse depth.
  * ------------------------------------------------------------------------------------------ */
@@ -311,17 +322,17 @@ void gso_render_fwd(int W, int H, const unsigned int *ranges, const unsigned int
                     unsigned g = point_list[s];
                     float dx = xy[2 * g] - pfx, dy = xy[2 * g + 1] - pfy;
                     const float *co = conic_opacity + 4 * g;
-                    float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                    float power = gauss_power(co, dx, dy);
                     if (power > 0.0f) continue;
-                    float alpha = fminf_(0.99f, co[3] * expf(power));
+                    float alpha = fminf_(0.99f, co[3] * gexp(power));
                     if (alpha < 1.0f / 255.0f) continue;
                     float test_T = T * (1.f - alpha);
                     if (test_T < 0.0001f) break;
                     float w = alpha * T;
-                    C0 += rgb[3 * g + 0] * w;
-                    C1 += rgb[3 * g + 1] * w;
-                    C2 += rgb[3 * g + 2] * w;
-                    if (do_depth) ID += (1.f / depths[g]) * w;
+                    C0 = fmaf(rgb[3 * g + 0], w, C0);
+                    C1 = fmaf(rgb[3 * g + 1], w, C1);
+                    C2 = fmaf(rgb[3 * g + 2], w, C2);
+                    if (do_depth) ID = fmaf(1.f / depths[g], w, ID);
                     T = test_T;
                     last = contributor;
                 }
@@ -364,53 +375,60 @@ void gso_render_bwd(int W, int H, const unsigned int *ranges, const unsigned int
                 unsigned last = n_contrib[pix];
                 float dp[3] = {dL_dpix[pix], dL_dpix[H * W + pix], dL_dpix[2 * H * W + pix]};
                 float dID = dL_dinvd ? dL_dinvd[pix] : 0.f;
-                float acc[3] = {0, 0, 0}, acc_id = 0, last_alpha = 0, last_c[3] = {0, 0, 0}, last_id = 0;
+                /* A = blended colour / inverse depth of everything behind the current splat */
+                float A[3] = {0, 0, 0}, Ai = 0;
                 float bg_dot = bg[0] * dp[0] + bg[1] * dp[1] + bg[2] * dp[2];
-                unsigned contributor = re - rs;
                 for (unsigned s = re; s-- > rs;) {
-                    contributor--;
-                    if (contributor >= last) continue;
+                    if (s - rs >= last) continue;
                     unsigned g = point_list[s];
                     float dx = xy[2 * g] - pfx, dy = xy[2 * g + 1] - pfy;
                     const float *co = conic_opacity + 4 * g;
-                    float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                    float power = gauss_power(co, dx, dy);
                     if (power > 0.0f) continue;
-                    float G = expf(power);
+                    float G = gexp(power);
                     float alpha = fminf_(0.99f, co[3] * G);
                     if (alpha < 1.0f / 255.0f) continue;
-                    T = T / (1.f - alpha);
+                    float rc = 1.f / (1.f - alpha);
+                    T = T * rc;
                     float dchannel = alpha * T;
                     float dL_dalpha = 0.f;
                     float *gi = inst + (size_t)s * 10;
                     for (int ch = 0; ch < 3; ch++) {
-                        float c = rgb[3 * g + ch];
-                        acc[ch] = last_alpha * last_c[ch] + (1.f - last_alpha) * acc[ch];
-                        last_c[ch] = c;
-                        dL_dalpha += (c - acc[ch]) * dp[ch];
-                        gi[6 + ch] += dchannel * dp[ch];
+                        float diff = rgb[3 * g + ch] - A[ch];
+                        dL_dalpha = fmaf(diff, dp[ch], dL_dalpha);
+                        A[ch] = fmaf(alpha, diff, A[ch]);
+                        gi[6 + ch] = fmaf(dchannel, dp[ch], gi[6 + ch]);
                     }
                     if (dL_dinvd) {
-                        float invd = 1.f / depths[g];
-                        acc_id = last_alpha * last_id + (1.f - last_alpha) * acc_id;
-                        last_id = invd;
-                        dL_dalpha += (invd - acc_id) * dID;
-                        gi[9] += dchannel * dID;
+                        float diff = 1.f / depths[g] - Ai;
+                        dL_dalpha = fmaf(diff, dID, dL_dalpha);
+                        Ai = fmaf(alpha, diff, Ai);
+                        gi[9] = fmaf(dchannel, dID, gi[9]);
                     }
-                    dL_dalpha *= T;
-                    last_alpha = alpha;
-                    dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
+                    dL_dalpha = fmaf(-T_final * rc, bg_dot, dL_dalpha * T);
                     float dL_dG = co[3] * dL_dalpha;
                     float gdx = G * dx, gdy = G * dy;
-                    float dG_ddelx = -gdx * co[0] - gdy * co[1];
-                    float dG_ddely = -gdy * co[2] - gdx * co[1];
-                    gi[0] += dL_dG * dG_ddelx * ddelx_dx;
-                    gi[1] += dL_dG * dG_ddely * ddely_dy;
-                    gi[2] += -0.5f * gdx * dx * dL_dG;
-                    gi[3] += -0.5f * gdx * dy * dL_dG;
-                    gi[4] += -0.5f * gdy * dy * dL_dG;
-                    gi[5] += G * dL_dalpha;
+                    float dG_ddelx = fmaf(-gdy, co[1], -gdx * co[0]);
+                    float dG_ddely = fmaf(-gdx, co[1], -gdy * co[2]);
+                    gi[0] = fmaf(dL_dG, dG_ddelx, gi[0]);
+                    gi[1] = fmaf(dL_dG, dG_ddely, gi[1]);
+                    float tx_ = dL_dG * gdx;
+                    gi[2] = fmaf(tx_, dx, gi[2]);
+                    gi[3] = fmaf(tx_, dy, gi[3]);
+                    gi[4] = fmaf(dL_dG * gdy, dy, gi[4]);
+                    gi[5] = fmaf(G, dL_dalpha, gi[5]);
                 }
             }
+        /* raw per-instance sums -> the upstream gradient convention (NDC-scaled mean2D,
+         * -0.5 factor on the conic terms) */
+        for (unsigned s = rs; s < re; s++) {
+            float *gi = inst + (size_t)s * 10;
+            gi[0] *= ddelx_dx;
+            gi[1] *= ddely_dy;
+            gi[2] *= -0.5f;
+            gi[3] *= -0.5f;
+            gi[4] *= -0.5f;
+        }
     }
 }
 

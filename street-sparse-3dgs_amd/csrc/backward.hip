@@ -16,8 +16,8 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
     const float *__restrict__ shs, const uint8_t *__restrict__ clamped, const float *__restrict__ scales,
     const float *__restrict__ rotations, float mod, const float *__restrict__ cov3D_precomp,
     const float *__restrict__ viewmatrix, const float *__restrict__ projmatrix, const float *__restrict__ campos_p,
-    float tanx, float tany, float fx, float fy, const uint32_t *__restrict__ tiles,
-    const uint32_t *__restrict__ offsets, BwdScratch sc, GaussianGrads out) {
+    float tanx, float tany, float fx, float fy, int gx, const uint32_t *__restrict__ tiles,
+    const GRec *__restrict__ rec, const uint64_t *__restrict__ boundary, BwdScratch sc, GaussianGrads out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & (kWave - 1);
     const bool valid = i < P;
@@ -25,23 +25,41 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
     const bool has_scales = cov3D_precomp == nullptr;
     const bool vis = valid && radii[i] > 0;
 
-    // Sum this Gaussian's per-tile records (contiguous at its exclusive-scan offset).  Runs of
-    // more than kRedSerial records are summed by the whole wave (coalesced loads + DPP) so one
-    // large splat does not serialise its 63 neighbours.
+    // Sum this Gaussian's per-tile records (contiguous at its exclusive-scan offset).  A record
+    // exists only for tiles where this Gaussian sits in front of the tile's boundary (the last
+    // list entry any pixel used, render.hip); elsewhere the instance contributed nothing.  Runs of
+    // more than kRedSerial tiles are summed by the whole wave (coalesced loads + DPP) so one large
+    // splat does not serialise its 63 neighbours.
     float g[10];
 #pragma unroll
     for (int k = 0; k < 10; k++) g[k] = 0.f;
-    const uint32_t n = vis ? tiles[i] : 0u;
-    const uint32_t off = (vis && i > 0) ? offsets[i - 1] : 0u;
-    if (n <= kRedSerial) {
-        for (uint32_t u = off; u < off + n; u++) {
-            const float4 a = sc.ga[u];
-            const float4 b = sc.gb[u];
-            const float2 c = sc.gc[u];
-            g[0] += a.x; g[1] += a.y; g[2] += a.z; g[3] += a.w;
-            g[4] += b.x; g[5] += b.y; g[6] += b.z; g[7] += b.w;
-            g[8] += c.x; g[9] += c.y;
-        }
+    uint32_t n = 0, x0 = 0, y0 = 0, w = 1, off = 0;
+    uint64_t key = 0;
+    if (vis) {
+        n = tiles[i];
+        const uint4 q3 = reinterpret_cast<const uint4 *>(rec + i)[3];
+        x0 = q3.x & 0xFFFFu;
+        y0 = q3.x >> 16;
+        w = q3.y;
+        key = ((uint64_t)q3.z << 32) | (uint32_t)i;
+        off = q3.w;
+    }
+    auto accumulate = [&](float *acc, uint32_t u) {
+        const float4 a = sc.rec[4 * (size_t)u + 0];
+        const float4 b = sc.rec[4 * (size_t)u + 1];
+        const float4 c = sc.rec[4 * (size_t)u + 2];
+        acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+        acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+        acc[8] += c.x; acc[9] += c.y;
+    };
+    if (n <= kRedSerial && n > 0) {
+        const uint32_t h = n / w;
+        uint32_t u = off;
+        for (uint32_t y = y0; y < y0 + h; y++)
+            for (uint32_t x = x0; x < x0 + w; x++, u++) {
+                const uint64_t bk = boundary[y * (uint32_t)gx + x];
+                if (bk != 0 && key <= bk) accumulate(g, u);
+            }
     }
     uint64_t big = __ballot(n > kRedSerial);
     while (big) {
@@ -49,16 +67,17 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
         big &= big - 1;
         const uint32_t boff = (uint32_t)__shfl((int)off, bl);
         const uint32_t bn = (uint32_t)__shfl((int)n, bl);
+        const uint32_t bx0 = (uint32_t)__shfl((int)x0, bl), by0 = (uint32_t)__shfl((int)y0, bl);
+        const uint32_t bw = (uint32_t)__shfl((int)w, bl);
+        const uint64_t bkey = ((uint64_t)(uint32_t)__shfl((int)(key >> 32), bl) << 32) |
+                              (uint32_t)__shfl((int)(uint32_t)key, bl);
         float q[10];
 #pragma unroll
         for (int k = 0; k < 10; k++) q[k] = 0.f;
-        for (uint32_t u = boff + lane; u < boff + bn; u += kWave) {
-            const float4 a = sc.ga[u];
-            const float4 b = sc.gb[u];
-            const float2 c = sc.gc[u];
-            q[0] += a.x; q[1] += a.y; q[2] += a.z; q[3] += a.w;
-            q[4] += b.x; q[5] += b.y; q[6] += b.z; q[7] += b.w;
-            q[8] += c.x; q[9] += c.y;
+        for (uint32_t idx = lane; idx < bn; idx += kWave) {
+            const uint32_t t = (by0 + idx / bw) * (uint32_t)gx + bx0 + idx % bw;
+            const uint64_t bk = boundary[t];
+            if (bk != 0 && bkey <= bk) accumulate(q, boff + idx);
         }
 #pragma unroll
         for (int k = 0; k < 10; k++) {
@@ -289,13 +308,13 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
     }
 }
 
-void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const GeomState &gs, const int *radii,
-                           const BwdScratch &sc, const GaussianGrads &out, hipStream_t s) {
+void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const GeomState &gs, const ImageState &is,
+                           const int *radii, const BwdScratch &sc, const GaussianGrads &out, hipStream_t s) {
     if (in.P == 0) return;
     hipLaunchKernelGGL(preprocess_bwd_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, in.D, in.M, in.means3D,
                        radii, in.shs, gs.clamped, in.scales, in.rotations, in.scale_modifier, in.cov3D_precomp,
-                       cam.view, cam.proj, cam.campos, cam.tanx, cam.tany, cam.fx, cam.fy, gs.tiles, gs.offsets, sc,
-                       out);
+                       cam.view, cam.proj, cam.campos, cam.tanx, cam.tany, cam.fx, cam.fy, cam.gx, gs.tiles, gs.rec,
+                       is.boundary, sc, out);
 }
 
 }  // namespace gsr

@@ -208,15 +208,30 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 // ------------------------------------------------------------------------------------------
 // Scratch-state layouts (carved out of the caller's byte buffers, 256-B aligned arrays)
 // ------------------------------------------------------------------------------------------
+constexpr float kLog2e = 1.4426950408889634f;
+
+// power = -0.5 (a dx^2 + c dy^2) - b dx dy in the fixed FMA order the oracle restates
+__device__ __forceinline__ float gauss_power(float adxdx, float bdx, float c, float dy) {
+    return fmaf(-bdx, dy, -0.5f * fmaf(c * dy, dy, adxdx));
+}
+
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// One 64-B render record per Gaussian (written by preprocess, off by duplicate): everything a
+// tile instance needs sits in one cache line, so the render kernels gather 1 line per instance.
+struct alignas(16) GRec {
+    float x, y, ca, cb;       // q0: pixel-space mean, conic (a, b)
+    float cc, op, ex, ey;     // q1: conic c, opacity, half-extents of the alpha >= 1/255 ellipse
+                              //     (ex < 0: can never reach alpha >= 1/255)
+    float r, g, b, invd;      // q2: colour, 1 / view depth
+    uint32_t rect0, rectw, dbits, off;  // q3: tile rect x0 | y0 << 16, width; depth bits; scan offset
+};
+static_assert(sizeof(GRec) == 64, "GRec must be one 64-B line");
+
 struct GeomState {          // per Gaussian, written by preprocess
-    float *depth;           // view-space z (sort key low 32 bits)
+    GRec *rec;
     uint32_t *tiles;        // tiles_touched
     uint32_t *offsets;      // inclusive scan of tiles
-    float2 *xy;             // pixel-space mean
-    float4 *conic_o;        // (a, b, c, opacity) of the inverse 2D covariance
-    float4 *rgbd;           // (r, g, b, 1/depth)
     uint8_t *clamped;       // bit c set: SH channel c clamped at 0
     void *scan_tmp;
     size_t scan_tmp_bytes;
@@ -233,14 +248,17 @@ struct BinningState {       // per tile instance
 
 struct ImageState {
     uint2 *ranges;          // per tile [start, end) in point_list
+    uint64_t *boundary;     // per tile: (depth bits << 32 | id) of the last instance any pixel uses
     float *final_T;         // per pixel
     uint32_t *n_contrib;    // per pixel: 1-based list position of the last contributor
 };
 
-struct BwdScratch {         // per tile instance, indexed by unsorted (gaussian-major) position
-    float4 *ga;             // dmean2D.x, dmean2D.y, dconic.a, dconic.b
-    float4 *gb;             // dconic.c, dopacity, drgb.r, drgb.g
-    float2 *gc;             // drgb.b, dinvdepth
+// Backward per-instance gradient records, one 64-B line each, indexed by the instance's unsorted
+// (Gaussian-major) position u:  q0 = dmean2D.x, dmean2D.y, dconic.a, dconic.b;
+// q1 = dconic.c, dopacity, drgb.r, drgb.g;  q2 = drgb.b, dinvdepth, 0, 0;  q3 = 0.
+// Only instances at list positions below their tile's boundary are written.
+struct BwdScratch {
+    float4 *rec;
 };
 
 }  // namespace gsr

@@ -46,7 +46,7 @@ void launch_render_bwd(const Camera &cam, const GeomState &gs, const BinningStat
 struct GaussianGrads {
     float *dmeans2D, *dcolors, *dopacity, *dmeans3D, *dcov3D, *dsh, *dscales, *drots;
 };
-void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const GeomState &gs, const int *radii,
-                           const BwdScratch &sc, const GaussianGrads &out, hipStream_t s);
+void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const GeomState &gs, const ImageState &is,
+                           const int *radii, const BwdScratch &sc, const GaussianGrads &out, hipStream_t s);
 
 }  // namespace gsr

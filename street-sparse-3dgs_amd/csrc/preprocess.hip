@@ -2,8 +2,8 @@
 // ranges and the frustum test.
 //
 // Layout: inputs are the caller's AoS tensors (means (P,3), scales (P,3), rotations (P,4),
-// shs (P,M,3)); outputs are SoA arrays in GeomState so that the render kernels gather one
-// 8-B xy, one 16-B conic/opacity and one 16-B rgb/invdepth record per tile instance.
+// shs (P,M,3)); the output is one 64-B GRec per Gaussian (gsr_device.h) so that every tile
+// instance the render kernels touch is a single cache-line gather.
 #include "gsr_launch.h"
 
 namespace gsr {
@@ -87,11 +87,31 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
         col = make_float4(rgb[0], rgb[1], rgb[2], 0.f);
     }
     col.w = 1.f / pv.z;
-    gs.depth[i] = pv.z;
+    const float op = opacities[i];
+    const float ca_ = cc * det_inv, cb_ = -cb * det_inv, cc_ = ca * det_inv;
+    // Half-extents of the region where alpha = op * exp(power) can reach 1/255:
+    // power >= -t, t = ln(255 op)  <=>  d^T Q d <= 2t  ->  |dx| <= sqrt(2t (Q^-1)_xx).  Evaluated
+    // from the stored conic in double with a relative + absolute margin, so culling against it
+    // never drops an instance that changes any pixel (render.hip).
+    float ex = -1.f, ey = -1.f;
+    const double t = log(255.0 * (double)op);
+    if (t >= 0.0) {
+        const double qa = ca_, qb = cb_, qc = cc_;
+        const double dq = qa * qc - qb * qb;
+        if (dq > 0.0 && qa > 0.0 && qc > 0.0) {
+            ex = (float)(sqrt(2.0 * t * qc / dq) * 1.001 + 0.1);
+            ey = (float)(sqrt(2.0 * t * qa / dq) * 1.001 + 0.1);
+        } else {
+            ex = ey = 3.0e38f;  // degenerate conic: never cull
+        }
+    }
     radii[i] = (int)radius;
-    gs.xy[i] = make_float2(px, py);
-    gs.conic_o[i] = make_float4(cc * det_inv, -cb * det_inv, ca * det_inv, opacities[i]);
-    gs.rgbd[i] = col;
+    float4 *R = reinterpret_cast<float4 *>(gs.rec + i);
+    R[0] = make_float4(px, py, ca_, cb_);
+    R[1] = make_float4(cc_, op, ex, ey);
+    R[2] = col;
+    R[3] = make_float4(__uint_as_float((uint32_t)r.x0 | ((uint32_t)r.y0 << 16)), __uint_as_float((uint32_t)(r.x1 - r.x0)),
+                       __uint_as_float(__float_as_uint(pv.z)), 0.f);
     gs.clamped[i] = clamp_bits;
     gs.tiles[i] = (uint32_t)area;
 }
@@ -120,31 +140,31 @@ void launch_preprocess(const GaussianInputs &in, const Camera &cam, const GeomSt
 // lanes of the wave, one ballot bit at a time.
 constexpr int kDupSerial = 16;
 
-__global__ __launch_bounds__(256) void duplicate_kernel(int P, int gx, int gy, const float2 *__restrict__ xy,
-                                                        const float *__restrict__ depth,
+__global__ __launch_bounds__(256) void duplicate_kernel(int P, int gx, GRec *__restrict__ rec,
+                                                        const uint32_t *__restrict__ tiles,
                                                         const uint32_t *__restrict__ offsets,
-                                                        const int *__restrict__ radii, uint64_t *__restrict__ keys,
-                                                        uint32_t *__restrict__ vals) {
+                                                        uint64_t *__restrict__ keys, uint32_t *__restrict__ vals) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & (kWave - 1);
-    Rect r = {0, 0, 0, 0};
-    uint32_t off = 0;
-    uint32_t dbits = 0;
-    int area = 0;
+    int x0 = 0, y0 = 0, w = 1, area = 0;
+    uint32_t off = 0, dbits = 0;
     if (i < P) {
-        const int rad = radii[i];
-        if (rad > 0) {
+        area = (int)tiles[i];
+        if (area > 0) {
             off = i == 0 ? 0u : offsets[i - 1];
-            const float2 p = xy[i];
-            r = get_rect(p.x, p.y, rad, gx, gy);
-            area = (r.x1 - r.x0) * (r.y1 - r.y0);
-            dbits = __float_as_uint(depth[i]);
+            const uint4 q3 = reinterpret_cast<const uint4 *>(rec + i)[3];
+            x0 = (int)(q3.x & 0xFFFFu);
+            y0 = (int)(q3.x >> 16);
+            w = (int)q3.y;
+            dbits = q3.z;
+            rec[i].off = off;  // the backward maps (Gaussian, tile) -> unsorted index with it
         }
     }
     if (area <= kDupSerial) {
         uint32_t o = off;
-        for (int y = r.y0; y < r.y1; y++)
-            for (int x = r.x0; x < r.x1; x++) {
+        const int h = area / w;
+        for (int y = y0; y < y0 + h; y++)
+            for (int x = x0; x < x0 + w; x++) {
                 keys[o] = ((uint64_t)(uint32_t)(y * gx + x) << 32) | (uint64_t)dbits;
                 vals[o] = (uint32_t)i;
                 o++;
@@ -154,7 +174,7 @@ __global__ __launch_bounds__(256) void duplicate_kernel(int P, int gx, int gy, c
     while (big) {
         const int b = __ffsll((unsigned long long)big) - 1;
         big &= big - 1;
-        const int bx0 = __shfl(r.x0, b), by0 = __shfl(r.y0, b), bw = __shfl(r.x1 - r.x0, b);
+        const int bx0 = __shfl(x0, b), by0 = __shfl(y0, b), bw = __shfl(w, b);
         const int barea = __shfl(area, b);
         const uint32_t boff = (uint32_t)__shfl((int)off, b);
         const uint64_t bd = (uint64_t)(uint32_t)__shfl((int)dbits, b);
@@ -170,8 +190,9 @@ __global__ __launch_bounds__(256) void duplicate_kernel(int P, int gx, int gy, c
 void launch_duplicate(int P, const Camera &cam, const GeomState &gs, const int *radii, const BinningState &bs,
                       hipStream_t s) {
     if (P == 0) return;
-    hipLaunchKernelGGL(duplicate_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, cam.gx, cam.gy, gs.xy, gs.depth,
-                       gs.offsets, radii, bs.keys_unsorted, bs.vals_unsorted);
+    (void)radii;
+    hipLaunchKernelGGL(duplicate_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, cam.gx, gs.rec, gs.tiles,
+                       gs.offsets, bs.keys_unsorted, bs.vals_unsorted);
 }
 
 __global__ __launch_bounds__(256) void ranges_kernel(int64_t K, const uint64_t *__restrict__ keys,

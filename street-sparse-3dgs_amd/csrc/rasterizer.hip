@@ -84,12 +84,9 @@ struct Carver {
 GeomState carve_geom(void *base, int P, size_t *bytes) {
     Carver c(base);
     GeomState g;
-    g.depth = c.take<float>(P);
+    g.rec = c.take<GRec>(P);
     g.tiles = c.take<uint32_t>(P);
     g.offsets = c.take<uint32_t>(P);
-    g.xy = c.take<float2>(P);
-    g.conic_o = c.take<float4>(P);
-    g.rgbd = c.take<float4>(P);
     g.clamped = c.take<uint8_t>(P);
     g.scan_tmp_bytes = scan_temp_bytes(P);
     g.scan_tmp = c.take<char>(g.scan_tmp_bytes);
@@ -120,6 +117,7 @@ ImageState carve_image(void *base, int T, int npix, size_t *bytes) {
     Carver c(base);
     ImageState s;
     s.ranges = c.take<uint2>(T);
+    s.boundary = c.take<uint64_t>(T);
     s.final_T = c.take<float>(npix);
     s.n_contrib = c.take<uint32_t>(npix);
     if (bytes) *bytes = align_up(c.off, 256);
@@ -129,9 +127,7 @@ ImageState carve_image(void *base, int T, int npix, size_t *bytes) {
 BwdScratch carve_bwd(void *base, int64_t K, size_t *bytes) {
     Carver c(base);
     BwdScratch s;
-    s.ga = c.take<float4>(K);
-    s.gb = c.take<float4>(K);
-    s.gc = c.take<float2>(K);
+    s.rec = c.take<float4>(4 * (size_t)K);
     if (bytes) *bytes = align_up(c.off, 256);
     return s;
 }
@@ -354,7 +350,7 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
     if ((rc = check("render backward", debug, s))) return rc;
     {
         StageTimer st(7, s);
-        launch_preprocess_bwd(in, cam, gs, radii, sc, out, s);
+        launch_preprocess_bwd(in, cam, gs, is, radii, sc, out, s);
     }
     if ((rc = check("preprocess backward", debug, s))) return rc;
     return GSR_OK;

@@ -1,32 +1,56 @@
 // render.hip -- tile blending forward and backward.
 //
-// MI355X mapping: one 64-lane wave owns one 16x16 tile; lane l holds pixels
-// (l & 15, (l >> 4) + 4k), k = 0..3.  A workgroup is a single wave, so the batch staging
-// through LDS needs no workgroup barrier cost beyond the wave's own s_waitcnt, and the
-// tile-wide early exit of the upstream design (__syncthreads_count) becomes a wave vote.
+// MI355X mapping: one 64-lane wave owns one 16x16 tile.  Lane l holds pixels
+// (x = l & 15, y = (l >> 4) + 4k), k = 0..3, so for a fixed k the wave covers the 16x4 sub-block
+// k of the tile.  Instances are staged through LDS 64 at a time: every lane gathers one 64-B
+// GRec (one cache line), tests the instance's opacity-aware ellipse AABB against the four
+// sub-blocks, and a wave ballot + mbcnt prefix sum compacts the survivors (with their 4-bit
+// sub-block masks) into LDS.  The blend loop then runs over survivors only and skips masked-out
+// sub-blocks with a scalar branch.  The cull is conservative (preprocess.hip), so colour, depth,
+// final T and n_contrib are exactly those of the uncompacted upstream loop.  The per-pixel work
+// is branch-free (selects, no exec-mask divergence); the tile-wide early exit of the upstream
+// design (__syncthreads_count) becomes a wave vote.
 //
-// Backward: upstream accumulates ~10 float atomics per (pixel, Gaussian) pair.  On gfx950
-// float atomics execute at the memory side (MI355X_MICROARCH.md, Global float atomics) and
-// 64 lanes adding into one address serialise, so instead every wave reduces each instance's
-// 10 gradient terms across its 256 pixels with DPP (row_ror + row_bcast, no LDS), parks the
-// sum in lane j of the batch (lane-select), and stores one 40-B record per tile instance
-// with plain stores at the instance's unsorted (Gaussian-major) index.  backward.hip then sums
-// each Gaussian's contiguous run of records: no atomics, bitwise reproducible.
+// Backward: upstream accumulates ~10 float atomics per (pixel, Gaussian) pair.  On gfx950 float
+// atomics execute at the memory side (MI355X_MICROARCH.md, Global float atomics) and 64 lanes
+// adding into one address serialise, so each wave instead reduces every instance's 10 gradient
+// terms over its 256 pixels with DPP (gsr_device.h wave_sum), parks the sum in the instance's
+// lane and stores one 64-B record per instance with plain stores at the instance's unsorted
+// (Gaussian-major) index.  Only instances in front of the tile's last contributor are visited
+// (13% of them on the 1M-Gaussian bench scene); the tile's boundary key tells backward.hip
+// which records exist.  No atomics: fwd+bwd is bitwise reproducible.
 #include "gsr_launch.h"
 
 namespace gsr {
+
+__device__ __forceinline__ float gexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+__device__ __forceinline__ uint32_t sub_block_mask(float X, float Y, float ex, float ey, float tx0, float ty0) {
+    // bit k: the alpha >= 1/255 ellipse box of the instance overlaps pixel rows ty0+4k..ty0+4k+3
+    if (!(X + ex >= tx0 && X - ex <= tx0 + 15.f)) return 0u;
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < kPixPerLane; k++) {
+        const float y0 = ty0 + (float)(4 * k);
+        if (Y + ey >= y0 && Y - ey <= y0 + 3.f) m |= 1u << k;
+    }
+    return m;
+}
+
+__device__ __forceinline__ uint32_t lane_prefix(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
 
 // ------------------------------------------------------------------------------------------
 // Forward
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void render_fwd_kernel(
     const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list, int W, int H, int gx,
-    const float2 *__restrict__ xy, const float4 *__restrict__ conic_o, const float4 *__restrict__ rgbd,
-    const float *__restrict__ bg, float *__restrict__ out_color, float *__restrict__ out_invd,
-    float *__restrict__ final_T, uint32_t *__restrict__ n_contrib) {
-    __shared__ float4 s_pa[kWave];  // x, y, conic.a, conic.b
-    __shared__ float2 s_pb[kWave];  // conic.c, opacity
-    __shared__ float4 s_c[kWave];   // r, g, b, 1/depth
+    const GRec *__restrict__ rec, const float *__restrict__ bg, float *__restrict__ out_color,
+    float *__restrict__ out_invd, float *__restrict__ final_T, uint32_t *__restrict__ n_contrib) {
+    __shared__ float4 s_a[kWave];  // x, y, conic.a, conic.b
+    __shared__ float4 s_b[kWave];  // conic.c, opacity, contributor index, sub-block mask
+    __shared__ float4 s_c[kWave];  // r, g, b, 1/depth
 
     const int tile = blockIdx.x;
     const int tx = tile % gx, ty = tile / gx;
@@ -34,54 +58,67 @@ __global__ __launch_bounds__(64) void render_fwd_kernel(
     const int px = tx * kTile + (lane & 15);
     const int py0 = ty * kTile + (lane >> 4);
     const float pfx = (float)px;
+    const float tx0 = (float)(tx * kTile), ty0 = (float)(ty * kTile);
 
-    float T[kPixPerLane], C0[kPixPerLane], C1[kPixPerLane], C2[kPixPerLane], ID[kPixPerLane];
+    float T[kPixPerLane], C0[kPixPerLane], C1[kPixPerLane], C2[kPixPerLane], ID[kPixPerLane], pfy[kPixPerLane];
     uint32_t last[kPixPerLane];
-    bool done[kPixPerLane];
+    bool alive[kPixPerLane];
 #pragma unroll
     for (int k = 0; k < kPixPerLane; k++) {
         T[k] = 1.f; C0[k] = C1[k] = C2[k] = ID[k] = 0.f; last[k] = 0;
-        done[k] = !(px < W && py0 + 4 * k < H);
+        alive[k] = px < W && py0 + 4 * k < H;
+        pfy[k] = (float)(py0 + 4 * k);
     }
     const uint2 rg = ranges[tile];
     for (uint32_t base = rg.x; base < rg.y; base += kWave) {
-        const bool lane_done = done[0] && done[1] && done[2] && done[3];
-        if (__all(lane_done)) break;
+        if (!__any(alive[0] || alive[1] || alive[2] || alive[3])) break;
         const uint32_t n = min((uint32_t)kWave, rg.y - base);
+        uint32_t m = 0;
+        float4 qa, qb, qc;
         if ((uint32_t)lane < n) {
             const uint32_t g = point_list[base + lane];
-            const float2 p = xy[g];
-            const float4 co = conic_o[g];
-            s_pa[lane] = make_float4(p.x, p.y, co.x, co.y);
-            s_pb[lane] = make_float2(co.z, co.w);
-            s_c[lane] = rgbd[g];
+            const float4 *R = reinterpret_cast<const float4 *>(rec + g);
+            qa = R[0];
+            qb = R[1];
+            qc = R[2];
+            m = sub_block_mask(qa.x, qa.y, qb.z, qb.w, tx0, ty0);
+        }
+        const uint64_t keep = __ballot(m != 0u);
+        const uint32_t cnt = (uint32_t)__popcll(keep);
+        if (m) {
+            const uint32_t slot = lane_prefix(keep);
+            s_a[slot] = qa;
+            s_b[slot] = make_float4(qb.x, qb.y, __uint_as_float(base - rg.x + (uint32_t)lane + 1u), __uint_as_float(m));
+            s_c[slot] = qc;
         }
         __syncthreads();
-        for (uint32_t j = 0; j < n; j++) {
-            const float4 a = s_pa[j];
-            const float2 b = s_pb[j];
-            const uint32_t contributor = base - rg.x + j + 1;
+        for (uint32_t j = 0; j < cnt; j++) {
+            const float4 a = s_a[j];
+            const float4 b = s_b[j];
+            const float4 c = s_c[j];
+            const uint32_t mk = __builtin_amdgcn_readfirstlane(__float_as_uint(b.w));
+            const uint32_t contributor = __builtin_amdgcn_readfirstlane(__float_as_uint(b.z));
             const float dx = a.x - pfx;
             const float adxdx = a.z * dx * dx;
             const float bdx = a.w * dx;
 #pragma unroll
             for (int k = 0; k < kPixPerLane; k++) {
-                if (done[k]) continue;
-                const float dy = a.y - (float)(py0 + 4 * k);
-                const float power = -0.5f * (adxdx + b.x * dy * dy) - bdx * dy;
-                if (power > 0.0f) continue;
-                const float alpha = fmin_(0.99f, b.y * expf(power));
-                if (alpha < 1.0f / 255.0f) continue;
+                if (!(mk & (1u << k))) continue;  // scalar branch: sub-block k culled
+                const float dy = a.y - pfy[k];
+                const float power = gauss_power(adxdx, bdx, b.x, dy);
+                const float alpha = fmin_(0.99f, b.y * gexp2(power * kLog2e));
+                const bool ok = alive[k] && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
                 const float test_T = T[k] * (1.f - alpha);
-                if (test_T < 0.0001f) { done[k] = true; continue; }
-                const float w = alpha * T[k];
-                const float4 c = s_c[j];
-                C0[k] += c.x * w;
-                C1[k] += c.y * w;
-                C2[k] += c.z * w;
-                ID[k] += c.w * w;
-                T[k] = test_T;
-                last[k] = contributor;
+                const bool stop = test_T < 0.0001f;
+                const bool acc = ok && !stop;
+                alive[k] = alive[k] && !(ok && stop);
+                const float w = acc ? alpha * T[k] : 0.f;
+                C0[k] = fmaf(c.x, w, C0[k]);
+                C1[k] = fmaf(c.y, w, C1[k]);
+                C2[k] = fmaf(c.z, w, C2[k]);
+                ID[k] = fmaf(c.w, w, ID[k]);
+                T[k] = acc ? test_T : T[k];
+                last[k] = acc ? contributor : last[k];
             }
         }
         __syncthreads();
@@ -107,7 +144,7 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
     const int T = cam.gx * cam.gy;
     if (T == 0) return;
     hipLaunchKernelGGL(render_fwd_kernel, dim3(T), dim3(kWave), 0, s, is.ranges, bs.point_list, cam.W, cam.H, cam.gx,
-                       gs.xy, gs.conic_o, gs.rgbd, bg, out_color, out_invdepth, is.final_T, is.n_contrib);
+                       gs.rec, bg, out_color, out_invdepth, is.final_T, is.n_contrib);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -115,14 +152,14 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
 // ------------------------------------------------------------------------------------------
 template <bool kDepth>
 __global__ __launch_bounds__(64) void render_bwd_kernel(
-    const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list, int W, int H, int gx, int gy,
-    const float2 *__restrict__ xy, const float4 *__restrict__ conic_o, const float4 *__restrict__ rgbd,
-    const int *__restrict__ radii, const uint32_t *__restrict__ offsets, const float *__restrict__ bg,
-    const float *__restrict__ final_Ts, const uint32_t *__restrict__ n_contrib, const float *__restrict__ dL_dpix,
-    const float *__restrict__ dL_dinvd, BwdScratch sc) {
-    __shared__ float4 s_pa[kWave];
-    __shared__ float2 s_pb[kWave];
+    const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list, int W, int H, int gx,
+    const GRec *__restrict__ rec, const float *__restrict__ bg, const float *__restrict__ final_Ts,
+    const uint32_t *__restrict__ n_contrib, const float *__restrict__ dL_dpix, const float *__restrict__ dL_dinvd,
+    uint64_t *__restrict__ boundary, float4 *__restrict__ out) {
+    __shared__ float4 s_a[kWave];
+    __shared__ float4 s_b[kWave];  // conic.c, opacity, list position, sub-block mask
     __shared__ float4 s_c[kWave];
+    __shared__ uint32_t s_u[kWave];
 
     const int tile = blockIdx.x;
     const int tx = tile % gx, ty = tile / gx;
@@ -130,20 +167,19 @@ __global__ __launch_bounds__(64) void render_bwd_kernel(
     const int px = tx * kTile + (lane & 15);
     const int py0 = ty * kTile + (lane >> 4);
     const float pfx = (float)px;
-    const float ddelx_dx = 0.5f * (float)W, ddely_dy = 0.5f * (float)H;
+    const float tx0 = (float)(tx * kTile), ty0 = (float)(ty * kTile);
     const float b0 = bg[0], b1 = bg[1], b2 = bg[2];
 
     float T[kPixPerLane], Tf[kPixPerLane], dp0[kPixPerLane], dp1[kPixPerLane], dp2[kPixPerLane], did[kPixPerLane];
-    float acc0[kPixPerLane], acc1[kPixPerLane], acc2[kPixPerLane], acci[kPixPerLane];
-    float la[kPixPerLane], lc0[kPixPerLane], lc1[kPixPerLane], lc2[kPixPerLane], lid[kPixPerLane];
-    float bgdot[kPixPerLane];
-    uint32_t last[kPixPerLane];
-    uint32_t mylast = 0;
+    float A0[kPixPerLane], A1[kPixPerLane], A2[kPixPerLane], Ai[kPixPerLane], bgdot[kPixPerLane], pfy[kPixPerLane];
+    uint32_t last[kPixPerLane], lastk[kPixPerLane];
+    uint32_t maxlast = 0;
 #pragma unroll
     for (int k = 0; k < kPixPerLane; k++) {
         const int py = py0 + 4 * k;
         const bool inside = px < W && py < H;
         const int pix = py * W + px;
+        pfy[k] = (float)py;
         Tf[k] = inside ? final_Ts[pix] : 0.f;
         T[k] = Tf[k];
         last[k] = inside ? n_contrib[pix] : 0u;
@@ -151,50 +187,64 @@ __global__ __launch_bounds__(64) void render_bwd_kernel(
         dp1[k] = inside ? dL_dpix[H * W + pix] : 0.f;
         dp2[k] = inside ? dL_dpix[2 * H * W + pix] : 0.f;
         did[k] = (kDepth && inside) ? dL_dinvd[pix] : 0.f;
-        acc0[k] = acc1[k] = acc2[k] = acci[k] = 0.f;
-        la[k] = lc0[k] = lc1[k] = lc2[k] = lid[k] = 0.f;
+        A0[k] = A1[k] = A2[k] = Ai[k] = 0.f;
         bgdot[k] = b0 * dp0[k] + b1 * dp1[k] + b2 * dp2[k];
-        mylast = last[k] > mylast ? last[k] : mylast;
+        lastk[k] = wave_max_u32(last[k]);  // sub-block k needs list positions < lastk[k]
+        maxlast = lastk[k] > maxlast ? lastk[k] : maxlast;
     }
     const uint2 rg = ranges[tile];
-    const uint32_t len = rg.y - rg.x;
-    const uint32_t maxlast = wave_max_u32(mylast);
-
-    // unsorted (Gaussian-major) index of the instance of `g` that lives in this tile
-    auto unsorted_index = [&](uint32_t g) -> uint32_t {
-        const float2 p = xy[g];
-        const Rect r = get_rect(p.x, p.y, radii[g], gx, gy);
-        const uint32_t off = g == 0 ? 0u : offsets[g - 1];
-        return off + (uint32_t)((ty - r.y0) * (r.x1 - r.x0) + (tx - r.x0));
-    };
-
-    // instances behind every pixel's last contributor receive zero gradient
-    for (uint32_t pos = maxlast + lane; pos < len; pos += kWave) {
-        const uint32_t u = unsorted_index(point_list[rg.x + pos]);
-        sc.ga[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-        sc.gb[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-        sc.gc[u] = make_float2(0.f, 0.f);
+    if (lane == 0) {
+        uint64_t bkey = 0;
+        if (maxlast > 0) {
+            const uint32_t gb = point_list[rg.x + maxlast - 1];
+            bkey = ((uint64_t)rec[gb].dbits << 32) | gb;
+        }
+        boundary[tile] = bkey;
     }
+    const float sx = 0.5f * (float)W, sy = 0.5f * (float)H;
 
     for (int hi = (int)maxlast; hi > 0; hi -= kWave) {
         const int n = hi < kWave ? hi : kWave;
-        uint32_t my_u = 0;
+        uint32_t m = 0, u = 0, pos = 0;
+        float4 qa, qb, qc;
         if (lane < n) {
-            const uint32_t g = point_list[rg.x + (uint32_t)(hi - 1 - lane)];
-            const float2 p = xy[g];
-            const float4 co = conic_o[g];
-            s_pa[lane] = make_float4(p.x, p.y, co.x, co.y);
-            s_pb[lane] = make_float2(co.z, co.w);
-            s_c[lane] = rgbd[g];
-            my_u = unsorted_index(g);
+            pos = (uint32_t)(hi - 1 - lane);
+            const uint32_t g = point_list[rg.x + pos];
+            const float4 *R = reinterpret_cast<const float4 *>(rec + g);
+            qa = R[0];
+            qb = R[1];
+            qc = R[2];
+            const uint4 q3 = reinterpret_cast<const uint4 *>(rec + g)[3];
+            u = q3.w + (uint32_t)((ty - (int)(q3.x >> 16)) * (int)q3.y + (tx - (int)(q3.x & 0xFFFFu)));
+            m = sub_block_mask(qa.x, qa.y, qb.z, qb.w, tx0, ty0);
+#pragma unroll
+            for (int k = 0; k < kPixPerLane; k++)
+                if (pos >= lastk[k]) m &= ~(1u << k);
+            if (m == 0u) {  // in the live range but touches no pixel that needs it: zero record
+                const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+                out[4 * (size_t)u + 0] = z;
+                out[4 * (size_t)u + 1] = z;
+                out[4 * (size_t)u + 2] = z;
+                out[4 * (size_t)u + 3] = z;
+            }
+        }
+        const uint64_t keep = __ballot(m != 0u);
+        const uint32_t cnt = (uint32_t)__popcll(keep);
+        if (m) {
+            const uint32_t slot = lane_prefix(keep);
+            s_a[slot] = qa;
+            s_b[slot] = make_float4(qb.x, qb.y, __uint_as_float(pos), __uint_as_float(m));
+            s_c[slot] = qc;
+            s_u[slot] = u;
         }
         __syncthreads();
         float r0 = 0.f, r1 = 0.f, r2 = 0.f, r3 = 0.f, r4 = 0.f, r5 = 0.f, r6 = 0.f, r7 = 0.f, r8 = 0.f, r9 = 0.f;
-        for (int j = 0; j < n; j++) {
-            const uint32_t pos = (uint32_t)(hi - 1 - j);
-            const float4 a = s_pa[j];
-            const float2 b = s_pb[j];
+        for (uint32_t j = 0; j < cnt; j++) {
+            const float4 a = s_a[j];
+            const float4 b = s_b[j];
             const float4 c = s_c[j];
+            const uint32_t mk = __builtin_amdgcn_readfirstlane(__float_as_uint(b.w));
+            const uint32_t jpos = __builtin_amdgcn_readfirstlane(__float_as_uint(b.z));
             const float dx = a.x - pfx;
             const float adxdx = a.z * dx * dx;
             const float bdx = a.w * dx;
@@ -202,51 +252,50 @@ __global__ __launch_bounds__(64) void render_bwd_kernel(
             bool any = false;
 #pragma unroll
             for (int k = 0; k < kPixPerLane; k++) {
-                if (pos >= last[k]) continue;
-                const float dy = a.y - (float)(py0 + 4 * k);
-                const float power = -0.5f * (adxdx + b.x * dy * dy) - bdx * dy;
-                if (power > 0.0f) continue;
-                const float G = expf(power);
+                if (!(mk & (1u << k))) continue;
+                const float dy = a.y - pfy[k];
+                const float power = gauss_power(adxdx, bdx, b.x, dy);
+                const float G = gexp2(power * kLog2e);
                 const float alpha = fmin_(0.99f, b.y * G);
-                if (alpha < 1.0f / 255.0f) continue;
-                any = true;
-                T[k] = T[k] / (1.f - alpha);
-                const float dchannel = alpha * T[k];
-                float dL_dalpha = 0.f;
-                acc0[k] = la[k] * lc0[k] + (1.f - la[k]) * acc0[k];
-                lc0[k] = c.x;
-                dL_dalpha += (c.x - acc0[k]) * dp0[k];
-                q6 += dchannel * dp0[k];
-                acc1[k] = la[k] * lc1[k] + (1.f - la[k]) * acc1[k];
-                lc1[k] = c.y;
-                dL_dalpha += (c.y - acc1[k]) * dp1[k];
-                q7 += dchannel * dp1[k];
-                acc2[k] = la[k] * lc2[k] + (1.f - la[k]) * acc2[k];
-                lc2[k] = c.z;
-                dL_dalpha += (c.z - acc2[k]) * dp2[k];
-                q8 += dchannel * dp2[k];
+                const bool ok = jpos < last[k] && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+                any = any || ok;
+                const float ae = ok ? alpha : 0.f;
+                const float Ge = ok ? G : 0.f;
+                const float rc = __builtin_amdgcn_rcpf(1.f - ae);
+                T[k] = T[k] * rc;
+                const float dch = ae * T[k];
+                const float d0 = c.x - A0[k];
+                float dla = d0 * dp0[k];
+                A0[k] = fmaf(ae, d0, A0[k]);
+                q6 = fmaf(dch, dp0[k], q6);
+                const float d1 = c.y - A1[k];
+                dla = fmaf(d1, dp1[k], dla);
+                A1[k] = fmaf(ae, d1, A1[k]);
+                q7 = fmaf(dch, dp1[k], q7);
+                const float d2 = c.z - A2[k];
+                dla = fmaf(d2, dp2[k], dla);
+                A2[k] = fmaf(ae, d2, A2[k]);
+                q8 = fmaf(dch, dp2[k], q8);
                 if (kDepth) {
-                    acci[k] = la[k] * lid[k] + (1.f - la[k]) * acci[k];
-                    lid[k] = c.w;
-                    dL_dalpha += (c.w - acci[k]) * did[k];
-                    q9 += dchannel * did[k];
+                    const float di = c.w - Ai[k];
+                    dla = fmaf(di, did[k], dla);
+                    Ai[k] = fmaf(ae, di, Ai[k]);
+                    q9 = fmaf(dch, did[k], q9);
                 }
-                dL_dalpha *= T[k];
-                la[k] = alpha;
-                dL_dalpha += (-Tf[k] / (1.f - alpha)) * bgdot[k];
-                const float dL_dG = b.y * dL_dalpha;
-                const float gdx = G * dx, gdy = G * dy;
-                const float dG_ddelx = -gdx * a.z - gdy * a.w;
-                const float dG_ddely = -gdy * b.x - gdx * a.w;
-                q0 += dL_dG * dG_ddelx * ddelx_dx;
-                q1 += dL_dG * dG_ddely * ddely_dy;
-                q2 += -0.5f * gdx * dx * dL_dG;
-                q3 += -0.5f * gdx * dy * dL_dG;
-                q4 += -0.5f * gdy * dy * dL_dG;
-                q5 += G * dL_dalpha;
+                dla = fmaf(-Tf[k] * rc, bgdot[k], dla * T[k]);
+                dla = ok ? dla : 0.f;
+                const float dLdG = b.y * dla;
+                const float gdx = Ge * dx, gdy = Ge * dy;
+                q0 = fmaf(dLdG, fmaf(-gdy, a.w, -gdx * a.z), q0);
+                q1 = fmaf(dLdG, fmaf(-gdx, a.w, -gdy * b.x), q1);
+                const float tg = dLdG * gdx;
+                q2 = fmaf(tg, dx, q2);
+                q3 = fmaf(tg, dy, q3);
+                q4 = fmaf(dLdG * gdy, dy, q4);
+                q5 = fmaf(Ge, dla, q5);
             }
             if (__any(any)) {
-                const bool mine = lane == j;  // park instance j's sums in lane j
+                const bool mine = (uint32_t)lane == j;  // park instance j's sums in lane j
                 { const float t = wave_sum(q0); r0 = mine ? t : r0; }
                 { const float t = wave_sum(q1); r1 = mine ? t : r1; }
                 { const float t = wave_sum(q2); r2 = mine ? t : r2; }
@@ -256,17 +305,18 @@ __global__ __launch_bounds__(64) void render_bwd_kernel(
                 { const float t = wave_sum(q6); r6 = mine ? t : r6; }
                 { const float t = wave_sum(q7); r7 = mine ? t : r7; }
                 { const float t = wave_sum(q8); r8 = mine ? t : r8; }
-                if (kDepth)
-                {
+                if (kDepth) {
                     const float t = wave_sum(q9);
                     r9 = mine ? t : r9;
                 }
             }
         }
-        if (lane < n) {
-            sc.ga[my_u] = make_float4(r0, r1, r2, r3);
-            sc.gb[my_u] = make_float4(r4, r5, r6, r7);
-            sc.gc[my_u] = make_float2(r8, r9);
+        if ((uint32_t)lane < cnt) {
+            const size_t o = 4 * (size_t)s_u[lane];
+            out[o + 0] = make_float4(r0 * sx, r1 * sy, -0.5f * r2, -0.5f * r3);
+            out[o + 1] = make_float4(-0.5f * r4, r5, r6, r7);
+            out[o + 2] = make_float4(r8, r9, 0.f, 0.f);
+            out[o + 3] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
         __syncthreads();
     }
@@ -275,16 +325,17 @@ __global__ __launch_bounds__(64) void render_bwd_kernel(
 void launch_render_bwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                        const int *radii, const float *bg, const float *dL_dpix, const float *dL_dinvdepth,
                        const BwdScratch &sc, hipStream_t s) {
+    (void)radii;
     const int T = cam.gx * cam.gy;
     if (T == 0) return;
     if (dL_dinvdepth)
         hipLaunchKernelGGL(render_bwd_kernel<true>, dim3(T), dim3(kWave), 0, s, is.ranges, bs.point_list, cam.W,
-                           cam.H, cam.gx, cam.gy, gs.xy, gs.conic_o, gs.rgbd, radii, gs.offsets, bg, is.final_T,
-                           is.n_contrib, dL_dpix, dL_dinvdepth, sc);
+                           cam.H, cam.gx, gs.rec, bg, is.final_T, is.n_contrib, dL_dpix, dL_dinvdepth, is.boundary,
+                           sc.rec);
     else
         hipLaunchKernelGGL(render_bwd_kernel<false>, dim3(T), dim3(kWave), 0, s, is.ranges, bs.point_list, cam.W,
-                           cam.H, cam.gx, cam.gy, gs.xy, gs.conic_o, gs.rgbd, radii, gs.offsets, bg, is.final_T,
-                           is.n_contrib, dL_dpix, dL_dinvdepth, sc);
+                           cam.H, cam.gx, gs.rec, bg, is.final_T, is.n_contrib, dL_dpix, dL_dinvdepth, is.boundary,
+                           sc.rec);
 }
 
 }  // namespace gsr

@@ -55,7 +55,12 @@ def _stream(device):
 
 
 class _Resizer:
-    """Holds the uint8 tensors the library asks for through gsr_resize_fn callbacks."""
+    """Holds the uint8 tensors the library asks for through gsr_resize_fn callbacks.
+
+    The callbacks close over `bufs` and `device` only (not over the resizer), and `release()`
+    drops the ctypes thunks after the call: no reference cycle, so every frame's scratch is
+    returned to the caching allocator as soon as autograd releases it instead of waiting for
+    Python's cyclic GC (which let ~10 frames of scratch pile up and forced fresh hipMallocs)."""
 
     def __init__(self, device):
         self.device = device
@@ -63,13 +68,18 @@ class _Resizer:
         self.fns = {}
 
     def fn(self, name):
+        bufs, device = self.bufs, self.device
+
         def cb(_ctx, nbytes):
-            t = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=self.device)
-            self.bufs[name] = t
+            t = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+            bufs[name] = t
             return t.data_ptr()
         f = _lib.RESIZE_FN(cb)
         self.fns[name] = f
         return f
+
+    def release(self):
+        self.fns.clear()
 
     def get(self, name):
         return self.bufs.get(name, torch.empty(0, dtype=torch.uint8, device=self.device))
@@ -113,7 +123,8 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     n_render = 0 if render_indices is None else int(render_indices.numel())
 
     out_color = torch.empty(3, H, W, dtype=torch.float32, device=dev)
-    out_invdepth = torch.zeros(1, H, W, dtype=torch.float32, device=dev)
+    # written for every pixel when do_depth; zeros otherwise (callers ignore it)
+    out_invdepth = (torch.empty if do_depth else torch.zeros)(1, H, W, dtype=torch.float32, device=dev)
     radii = torch.empty(P, dtype=torch.int32, device=dev)
     res = _Resizer(dev)
     K = ctypes.c_int64(0)
@@ -124,6 +135,7 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
             _ptr(rots_c), _ptr(cov_c), _ptr(view_c), _ptr(proj_c), _ptr(campos_c), float(tan_fovx),
             float(tan_fovy), int(bool(prefiltered)), _ptr(out_color), _ptr(out_invdepth) if do_depth else None,
             _ptr(radii), None, None, None, None, n_render, int(bool(debug)), _stream(dev), ctypes.byref(K))
+    res.release()
     _check(rc, "rasterize_gaussians")
     return int(K.value), out_color, out_invdepth, radii, res.get("geom"), res.get("binning"), res.get("image")
 
@@ -164,6 +176,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
             _ptr(dL_dopacity), _ptr(dL_dmeans3D), _ptr(dL_dcov3D), _ptr(dL_dsh) if sh_c is not None else None,
             _ptr(dL_dscales) if cov_c is None else None, _ptr(dL_drotations) if cov_c is None else None,
             int(bool(debug)), _stream(dev))
+    res.release()
     _check(rc, "rasterize_gaussians_backward")
     return dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations
 

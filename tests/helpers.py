@@ -25,8 +25,7 @@ def carve(sizes):
 
 
 def geom_layout(P):
-    return carve([("depth", 4 * P), ("tiles", 4 * P), ("offsets", 4 * P), ("xy", 8 * P), ("conic_o", 16 * P),
-                  ("rgbd", 16 * P), ("clamped", P)])
+    return carve([("rec", 64 * P), ("tiles", 4 * P), ("offsets", 4 * P), ("clamped", P)])
 
 
 def binning_layout(K):
@@ -34,7 +33,7 @@ def binning_layout(K):
 
 
 def image_layout(T, npix):
-    return carve([("ranges", 8 * T), ("final_T", 4 * npix), ("n_contrib", 4 * npix)])
+    return carve([("ranges", 8 * T), ("boundary", 8 * T), ("final_T", 4 * npix), ("n_contrib", 4 * npix)])
 
 
 def view(buf_np, layout, name, dtype, shape=None):
@@ -50,10 +49,10 @@ def decode_state(geom, binning, image, P, K, W, H):
     gl, bl = geom_layout(P), binning_layout(K)
     gx, gy = (W + 15) // 16, (H + 15) // 16
     il = image_layout(gx * gy, W * H)
+    rec = view(g, gl, "rec", np.float32, (P, 16))
     return dict(
-        depths=view(g, gl, "depth", np.float32), tiles_touched=view(g, gl, "tiles", np.uint32),
-        offsets=view(g, gl, "offsets", np.uint32), xy=view(g, gl, "xy", np.float32, (P, 2)),
-        conic_opacity=view(g, gl, "conic_o", np.float32, (P, 4)), rgbd=view(g, gl, "rgbd", np.float32, (P, 4)),
+        rec=rec, depths=rec[:, 14].view(np.float32).copy(), xy=rec[:, 0:2], conic_opacity=rec[:, 2:6],
+        rgbd=rec[:, 8:12], tiles_touched=view(g, gl, "tiles", np.uint32), offsets=view(g, gl, "offsets", np.uint32),
         clamped=view(g, gl, "clamped", np.uint8),
         keys_unsorted=view(b, bl, "keys_unsorted", np.uint64), keys=view(b, bl, "keys_sorted", np.uint64),
         vals_unsorted=view(b, bl, "vals_unsorted", np.uint32), point_list=view(b, bl, "point_list", np.uint32),

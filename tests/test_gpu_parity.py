@@ -258,3 +258,30 @@ def test_config2_full_size_vs_oracle():
     nz = r[:, 1] > r[:, 0]
     assert int((r[nz, 1] - r[nz, 0]).sum()) == h["K"]
     compare(c, st, g, h)
+
+
+@pytest.mark.gpu
+def test_scratch_is_released_every_frame():
+    """Scratch buffers must go back to the caching allocator when autograd releases them (no
+    reference cycles through the ctypes resize callbacks)."""
+    import torch
+    from diff_gaussian_rasterization import GaussianRasterizer
+    c = dict(name="mem", P=20000, W=320, H=240, deg=3, seed=13, log_scale=-3.5)
+    s = make_scene(c)
+    dev = torch.device("cuda:0")
+    inp = torch_inputs(s, dev)
+    rs = settings(s, dev, 3)
+
+    def step():
+        for v in inp.values():
+            v.grad = None
+        color, radii, invd = GaussianRasterizer(rs)(**inp)
+        (color.sum() + invd.sum()).backward()
+
+    step()
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated(dev)
+    for _ in range(5):
+        step()
+    torch.cuda.synchronize()
+    assert torch.cuda.memory_allocated(dev) <= base + (1 << 20)

@@ -1,0 +1,87 @@
+"""Summarise rocprofv3 runs into profiles/<tag>_*.json for bench.py / DESIGN.md.
+
+    python tools/pmc_summary.py --trace DIR --fetch DIR --write DIR --out profiles/r01_pmc.json
+
+--trace: a `rocprofv3 --kernel-trace --stats --output-format csv` directory (kernel_stats.csv)
+--fetch / --write: `rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE` runs (separate passes:
+the two do not fit one pass of the 4 TCC slots).  gfx950 corrections (MI355X_MICROARCH.md,
+HBM): FETCH_SIZE is in KiB and reports half the bytes of wide (16 B/lane) streaming reads, so
+read bytes = 2 * FETCH_SIZE * 1024; WRITE_SIZE * 1024 is exact for 16 B/lane stores.
+The FETCH doubling is exact only for wide coalesced reads; gathers (the render kernels' 4..16 B
+per-lane gathers) are uncalibrated, so both the raw and the corrected figure are kept.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+from collections import defaultdict
+
+STAGE_OF = [("render_bwd_kernel", "render_bwd"), ("render_fwd_kernel", "render_fwd"),
+            ("preprocess_bwd_kernel", "preprocess_bwd"), ("preprocess_kernel", "preprocess"),
+            ("duplicate_kernel", "duplicate"), ("ranges_kernel", "ranges"), ("mark_visible", "mark_visible"),
+            ("radix", "sort"), ("onesweep", "sort"), ("scan", "scan"), ("rocprim", "rocprim")]
+
+
+def stage(name):
+    for k, v in STAGE_OF:
+        if k in name:
+            return v
+    return name.split("(")[0][:60]
+
+
+def read_pmc(d, counter):
+    vals = defaultdict(list)
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r.get("Counter_Name") != counter:
+                continue
+            vals[stage(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+    return vals
+
+
+def read_stats(d):
+    out = {}
+    for f in glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            s = stage(r["Name"])
+            e = out.setdefault(s, {"calls": 0, "total_ns": 0.0})
+            e["calls"] += int(r["Calls"])
+            e["total_ns"] += float(r["TotalDurationNs"])
+    for e in out.values():
+        e["avg_us"] = e["total_ns"] / max(1, e["calls"]) / 1e3
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--trace")
+    ap.add_argument("--fetch")
+    ap.add_argument("--write")
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--note", default="")
+    a = ap.parse_args()
+    res = {"note": a.note, "kernels": {}}
+    stats = read_stats(a.trace) if a.trace else {}
+    fetch = read_pmc(a.fetch, "FETCH_SIZE") if a.fetch else {}
+    write = read_pmc(a.write, "WRITE_SIZE") if a.write else {}
+    for s in sorted(set(stats) | set(fetch) | set(write)):
+        e = dict(stats.get(s, {}))
+        if s in fetch:
+            f = sum(fetch[s]) / len(fetch[s])
+            e["fetch_size_kib_raw"] = f
+            e["read_bytes_corrected"] = 2 * f * 1024
+        if s in write:
+            w = sum(write[s]) / len(write[s])
+            e["write_size_kib"] = w
+            e["write_bytes"] = w * 1024
+        if "read_bytes_corrected" in e and "write_bytes" in e:
+            e["hbm_bytes_per_launch"] = e["read_bytes_corrected"] + e["write_bytes"]
+        res["kernels"][s] = e
+    os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+    json.dump(res, open(a.out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
