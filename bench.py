@@ -45,15 +45,20 @@ def parse():
 
 
 def algorithmic_bytes(P, Pv, K, T, npix, M=16):
-    """SURVEY.md 8(d) per-unit figures (M=16 constants; the SH term scales with M)."""
+    """Per-launch algorithmic bytes per stage.  SURVEY.md 8(d) figures (M=16 constants; the SH
+    term scales with M) for the stages it defines; the binning stages follow this build's
+    algorithm: a 32-bit depth sort of P ids (4 LSD passes, 16 B/elem/pass) + the
+    gathered scan, duplicate writing 2-B tile ids + 4-B ids, and a 2-pass stable tile sort
+    (12 B/elem/pass); upstream's 64-bit 6-pass sort would be 24*K*6."""
     sh = 12 * M
-    n_pass = math.ceil((32 + max(1, math.ceil(math.log2(max(T, 2))))) / 8)
+    tile_bits = max(1, math.ceil(math.log2(max(T, 2))))
+    kb = 2 if T <= 65536 else 4
     return {
         "preprocess": (44 + sh) * P + 80 * P,
-        "scan": 4 * P,
-        "duplicate": 12 * K,
-        "sort": 24 * K * n_pass,
-        "ranges": 8 * K + 8 * T,
+        "depth_sort_scan": 16 * P * 4 + 12 * P,
+        "duplicate": (kb + 4) * K + 16 * Pv,
+        "tile_sort": 2 * (kb + 4) * K * math.ceil(tile_bits / 8),
+        "ranges": kb * K + 8 * T,
         "render_fwd": 44 * K + 24 * npix,
         "render_bwd": 44 * K + 24 * npix + 40 * Pv,
         "preprocess_bwd": (356 + sh - 192) * P + (260 + sh - 192) * P,

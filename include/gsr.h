@@ -100,7 +100,7 @@ int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const
 
 /* Per-stage device time of the last forward/backward on this thread, filled only when
  * gsr_set_profiling(1) was called (HIP events; for bench.py's roofline).  Stage order:
- * 0 preprocess, 1 scan, 2 duplicate, 3 sort, 4 ranges, 5 render_fwd, 6 render_bwd,
+ * 0 preprocess, 1 depth sort + scan, 2 duplicate, 3 tile sort, 4 ranges, 5 render_fwd, 6 render_bwd,
  * 7 preprocess_bwd.  Returns the number of stages written. */
 int gsr_set_profiling(int enable);
 int gsr_stage_times_ms(float *out, int max_stages);

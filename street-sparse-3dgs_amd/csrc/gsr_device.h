@@ -231,17 +231,22 @@ static_assert(sizeof(GRec) == 64, "GRec must be one 64-B line");
 struct GeomState {          // per Gaussian, written by preprocess
     GRec *rec;
     uint32_t *tiles;        // tiles_touched
-    uint32_t *offsets;      // inclusive scan of tiles
+    uint32_t *dkey;         // depth sort key: depth bits, 0xFFFFFFFF when culled
+    uint32_t *dkey_sorted;
+    uint32_t *ids;          // 0..P-1
+    uint32_t *order;        // Gaussian ids in (depth, id) order
+    uint32_t *offsets;      // inclusive scan of tiles_touched in depth order
     uint8_t *clamped;       // bit c set: SH channel c clamped at 0
-    void *scan_tmp;
-    size_t scan_tmp_bytes;
+    void *tmp;              // depth-sort / scan temp storage
+    size_t tmp_bytes;
 };
 
 struct BinningState {       // per tile instance
-    uint64_t *keys_unsorted;
-    uint64_t *keys_sorted;
+    void *tkeys_unsorted;   // tile ids (uint16 when T <= 65536, else uint32), depth-major order
+    void *tkeys_sorted;
+    bool wide;
     uint32_t *vals_unsorted;
-    uint32_t *point_list;   // gaussian id in (tile, depth) order
+    uint32_t *point_list;   // gaussian id in (tile, depth, id) order
     void *sort_tmp;
     size_t sort_tmp_bytes;
 };

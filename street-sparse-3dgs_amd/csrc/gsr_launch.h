@@ -30,10 +30,14 @@ void launch_mark_visible(int P, const float *means3D, const float *view, uint8_t
 
 // sort.hip (rocPRIM)
 size_t scan_temp_bytes(int P);
-hipError_t inclusive_scan_u32(void *tmp, size_t tmp_bytes, const uint32_t *in, uint32_t *out, int P, hipStream_t s);
-size_t sort_temp_bytes(int64_t K, int end_bit);
-hipError_t sort_pairs_u64(void *tmp, size_t tmp_bytes, const uint64_t *kin, uint64_t *kout, const uint32_t *vin,
-                          uint32_t *vout, int64_t K, int end_bit, hipStream_t s);
+hipError_t inclusive_scan_gathered(void *tmp, size_t tmp_bytes, const uint32_t *order, const uint32_t *tiles,
+                                   uint32_t *out, int P, hipStream_t s);
+size_t depth_sort_temp_bytes(int P);
+hipError_t depth_sort(void *tmp, size_t tmp_bytes, const uint32_t *kin, uint32_t *kout, const uint32_t *vin,
+                      uint32_t *vout, int P, hipStream_t s);
+size_t tile_sort_temp_bytes(int64_t K, int end_bit, bool wide);
+hipError_t tile_sort(void *tmp, size_t tmp_bytes, const void *kin, void *kout, const uint32_t *vin, uint32_t *vout,
+                     int64_t K, int end_bit, bool wide, hipStream_t s);
 
 // render.hip
 void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,

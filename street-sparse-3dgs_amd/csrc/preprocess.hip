@@ -21,6 +21,8 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
     const Mat4 Pm = load_mat4(projmatrix);
     radii[i] = 0;
     gs.tiles[i] = 0;
+    gs.dkey[i] = 0xFFFFFFFFu;  // culled Gaussians sort behind every visible one
+    gs.ids[i] = (uint32_t)i;
     const float3 p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
     const float3 pv = xf_point43(p, V);
     if (pv.z <= 0.2f) return;  // in_frustum (prefiltered is treated as a plain cull)
@@ -114,6 +116,7 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
                        __uint_as_float(__float_as_uint(pv.z)), 0.f);
     gs.clamped[i] = clamp_bits;
     gs.tiles[i] = (uint32_t)area;
+    gs.dkey[i] = __float_as_uint(pv.z);
 }
 
 void launch_preprocess(const GaussianInputs &in, const Camera &cam, const GeomState &gs, int *radii,
@@ -133,31 +136,34 @@ void launch_preprocess(const GaussianInputs &in, const Camera &cam, const GeomSt
                            cam.fy, cam.gx, cam.gy, gs, radii);
 }
 
-// Key duplication.  Lane i writes Gaussian i's (tile << 32 | depth bits, id) pairs in rect
-// row-major order at its exclusive-scan offset (the "unsorted" instance index u used again in
-// the backward).  Splats touching more than kDupSerial tiles would serialise their wave (a
-// 3-sigma outlier can cover hundreds of tiles), so those are written cooperatively by all 64
-// lanes of the wave, one ballot bit at a time.
+// Key duplication, in depth order.  Lane j takes the j-th Gaussian of the depth sort and writes
+// its tile ids + id in rect row-major order at its (depth-order) exclusive-scan offset; that
+// offset is also recorded in the GRec: the backward maps (Gaussian, tile) -> record index with
+// it.  Splats touching more than kDupSerial tiles would serialise their wave (a 3-sigma outlier
+// can cover hundreds of tiles), so those are written cooperatively by all 64 lanes of the
+// wave, one ballot bit at a time.
 constexpr int kDupSerial = 16;
 
+template <typename TK>
 __global__ __launch_bounds__(256) void duplicate_kernel(int P, int gx, GRec *__restrict__ rec,
+                                                        const uint32_t *__restrict__ order,
                                                         const uint32_t *__restrict__ tiles,
-                                                        const uint32_t *__restrict__ offsets,
-                                                        uint64_t *__restrict__ keys, uint32_t *__restrict__ vals) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+                                                        const uint32_t *__restrict__ offsets, TK *__restrict__ tkeys,
+                                                        uint32_t *__restrict__ vals) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & (kWave - 1);
     int x0 = 0, y0 = 0, w = 1, area = 0;
-    uint32_t off = 0, dbits = 0;
-    if (i < P) {
-        area = (int)tiles[i];
+    uint32_t off = 0, g = 0;
+    if (j < P) {
+        g = order[j];
+        area = (int)tiles[g];
         if (area > 0) {
-            off = i == 0 ? 0u : offsets[i - 1];
-            const uint4 q3 = reinterpret_cast<const uint4 *>(rec + i)[3];
+            off = j == 0 ? 0u : offsets[j - 1];
+            const uint4 q3 = reinterpret_cast<const uint4 *>(rec + g)[3];
             x0 = (int)(q3.x & 0xFFFFu);
             y0 = (int)(q3.x >> 16);
             w = (int)q3.y;
-            dbits = q3.z;
-            rec[i].off = off;  // the backward maps (Gaussian, tile) -> unsorted index with it
+            rec[g].off = off;
         }
     }
     if (area <= kDupSerial) {
@@ -165,8 +171,8 @@ __global__ __launch_bounds__(256) void duplicate_kernel(int P, int gx, GRec *__r
         const int h = area / w;
         for (int y = y0; y < y0 + h; y++)
             for (int x = x0; x < x0 + w; x++) {
-                keys[o] = ((uint64_t)(uint32_t)(y * gx + x) << 32) | (uint64_t)dbits;
-                vals[o] = (uint32_t)i;
+                tkeys[o] = (TK)(y * gx + x);
+                vals[o] = g;
                 o++;
             }
     }
@@ -177,33 +183,39 @@ __global__ __launch_bounds__(256) void duplicate_kernel(int P, int gx, GRec *__r
         const int bx0 = __shfl(x0, b), by0 = __shfl(y0, b), bw = __shfl(w, b);
         const int barea = __shfl(area, b);
         const uint32_t boff = (uint32_t)__shfl((int)off, b);
-        const uint64_t bd = (uint64_t)(uint32_t)__shfl((int)dbits, b);
-        const uint32_t bi = (uint32_t)__shfl(i, b);
+        const uint32_t bg = (uint32_t)__shfl((int)g, b);
         for (int idx = lane; idx < barea; idx += kWave) {
             const int y = by0 + idx / bw, x = bx0 + idx % bw;
-            keys[boff + idx] = ((uint64_t)(uint32_t)(y * gx + x) << 32) | bd;
-            vals[boff + idx] = bi;
+            tkeys[boff + idx] = (TK)(y * gx + x);
+            vals[boff + idx] = bg;
         }
     }
 }
 
 void launch_duplicate(int P, const Camera &cam, const GeomState &gs, const int *radii, const BinningState &bs,
                       hipStream_t s) {
-    if (P == 0) return;
     (void)radii;
-    hipLaunchKernelGGL(duplicate_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, cam.gx, gs.rec, gs.tiles,
-                       gs.offsets, bs.keys_unsorted, bs.vals_unsorted);
+    if (P == 0) return;
+    if (bs.wide)
+        hipLaunchKernelGGL(duplicate_kernel<uint32_t>, dim3((P + 255) / 256), dim3(256), 0, s, P, cam.gx, gs.rec,
+                           gs.order, gs.tiles, gs.offsets, static_cast<uint32_t *>(bs.tkeys_unsorted),
+                           bs.vals_unsorted);
+    else
+        hipLaunchKernelGGL(duplicate_kernel<uint16_t>, dim3((P + 255) / 256), dim3(256), 0, s, P, cam.gx, gs.rec,
+                           gs.order, gs.tiles, gs.offsets, static_cast<uint16_t *>(bs.tkeys_unsorted),
+                           bs.vals_unsorted);
 }
 
-__global__ __launch_bounds__(256) void ranges_kernel(int64_t K, const uint64_t *__restrict__ keys,
+template <typename TK>
+__global__ __launch_bounds__(256) void ranges_kernel(int64_t K, const TK *__restrict__ tkeys,
                                                      uint2 *__restrict__ ranges) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= K) return;
-    const uint32_t cur = (uint32_t)(keys[idx] >> 32);
+    const uint32_t cur = (uint32_t)tkeys[idx];
     if (idx == 0) {
         ranges[cur].x = 0;
     } else {
-        const uint32_t prev = (uint32_t)(keys[idx - 1] >> 32);
+        const uint32_t prev = (uint32_t)tkeys[idx - 1];
         if (cur != prev) {
             ranges[prev].y = (uint32_t)idx;
             ranges[cur].x = (uint32_t)idx;
@@ -215,8 +227,13 @@ __global__ __launch_bounds__(256) void ranges_kernel(int64_t K, const uint64_t *
 void launch_ranges(int64_t K, int T, const BinningState &bs, const ImageState &is, hipStream_t s) {
     (void)hipMemsetAsync(is.ranges, 0, sizeof(uint2) * (size_t)T, s);
     if (K == 0) return;
-    hipLaunchKernelGGL(ranges_kernel, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, s, K, bs.keys_sorted,
-                       is.ranges);
+    const dim3 grid((unsigned)((K + 255) / 256));
+    if (bs.wide)
+        hipLaunchKernelGGL(ranges_kernel<uint32_t>, grid, dim3(256), 0, s, K,
+                           static_cast<const uint32_t *>(bs.tkeys_sorted), is.ranges);
+    else
+        hipLaunchKernelGGL(ranges_kernel<uint16_t>, grid, dim3(256), 0, s, K,
+                           static_cast<const uint16_t *>(bs.tkeys_sorted), is.ranges);
 }
 
 __global__ __launch_bounds__(256) void mark_visible_kernel(int P, const float *__restrict__ means3D,

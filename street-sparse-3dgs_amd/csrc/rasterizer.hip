@@ -86,10 +86,15 @@ GeomState carve_geom(void *base, int P, size_t *bytes) {
     GeomState g;
     g.rec = c.take<GRec>(P);
     g.tiles = c.take<uint32_t>(P);
+    g.dkey = c.take<uint32_t>(P);
+    g.dkey_sorted = c.take<uint32_t>(P);
+    g.ids = c.take<uint32_t>(P);
+    g.order = c.take<uint32_t>(P);
     g.offsets = c.take<uint32_t>(P);
     g.clamped = c.take<uint8_t>(P);
-    g.scan_tmp_bytes = scan_temp_bytes(P);
-    g.scan_tmp = c.take<char>(g.scan_tmp_bytes);
+    const size_t a = scan_temp_bytes(P), b = depth_sort_temp_bytes(P);
+    g.tmp_bytes = a > b ? a : b;
+    g.tmp = c.take<char>(g.tmp_bytes);
     if (bytes) *bytes = align_up(c.off, 256);
     return g;
 }
@@ -100,14 +105,21 @@ int bits_for(int n) {  // smallest b with n <= 2^b  (upstream getHigherMsb)
     return b;
 }
 
-BinningState carve_binning(void *base, int64_t K, int end_bit, size_t *bytes) {
+BinningState carve_binning(void *base, int64_t K, int T, size_t *bytes) {
     Carver c(base);
     BinningState b;
-    b.keys_unsorted = c.take<uint64_t>(K);
-    b.keys_sorted = c.take<uint64_t>(K);
+    b.wide = T > 65536;
+    const int end_bit = bits_for(T) > 0 ? bits_for(T) : 1;
+    if (b.wide) {
+        b.tkeys_unsorted = c.take<uint32_t>(K);
+        b.tkeys_sorted = c.take<uint32_t>(K);
+    } else {
+        b.tkeys_unsorted = c.take<uint16_t>(K);
+        b.tkeys_sorted = c.take<uint16_t>(K);
+    }
     b.vals_unsorted = c.take<uint32_t>(K);
     b.point_list = c.take<uint32_t>(K);
-    b.sort_tmp_bytes = sort_temp_bytes(K, end_bit);
+    b.sort_tmp_bytes = tile_sort_temp_bytes(K, end_bit, b.wide);
     b.sort_tmp = c.take<char>(b.sort_tmp_bytes);
     if (bytes) *bytes = align_up(c.off, 256);
     return b;
@@ -175,7 +187,7 @@ int gsr_abi_version(void) { return GSR_ABI_VERSION; }
 const char *gsr_last_error(void) { return g_err.c_str(); }
 
 const char *gsr_build_info(void) {
-    return "gsr_hip gfx950: preprocess/duplicate/ranges (preprocess.hip), rocPRIM scan+radix sort (sort.hip), "
+    return "gsr_hip gfx950: preprocess/duplicate/ranges (preprocess.hip), rocPRIM depth sort + tile sort (sort.hip), "
            "wave-per-tile render fwd/bwd with DPP reductions (render.hip), per-Gaussian backward (backward.hip)";
 }
 
@@ -254,11 +266,12 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
     if ((rc = check("preprocess", debug, s))) return rc;
     {
         StageTimer st(1, s);
-        if (inclusive_scan_u32(gs.scan_tmp, gs.scan_tmp_bytes, gs.tiles, gs.offsets, P, s) != hipSuccess)
+        if (depth_sort(gs.tmp, gs.tmp_bytes, gs.dkey, gs.dkey_sorted, gs.ids, gs.order, P, s) != hipSuccess)
+            return fail(GSR_ERR_DEVICE, "depth sort failed");
+        if (inclusive_scan_gathered(gs.tmp, gs.tmp_bytes, gs.order, gs.tiles, gs.offsets, P, s) != hipSuccess)
             return fail(GSR_ERR_DEVICE, "inclusive scan failed");
     }
-    if ((rc = check("scan", debug, s))) return rc;
-
+    if ((rc = check("depth sort / scan", debug, s))) return rc;
     int64_t K = 0;
     if (P > 0) {
         if (!g_pinned) {
@@ -270,12 +283,12 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
         if (hipStreamSynchronize(s) != hipSuccess) return fail(GSR_ERR_DEVICE, "stream sync failed");
         K = (int64_t)*g_pinned;
     }
-    const int end_bit = 32 + bits_for(T);
+    const int end_bit = bits_for(T) > 0 ? bits_for(T) : 1;
     size_t bbytes = 0;
-    carve_binning(nullptr, K, end_bit, &bbytes);
+    carve_binning(nullptr, K, T, &bbytes);
     void *bbase = binning_buffer(resize_ctx, bbytes);
     if (!bbase) return fail(GSR_ERR_ALLOCATION, "binning buffer allocation failed");
-    const BinningState bs = carve_binning(bbase, K, end_bit, nullptr);
+    const BinningState bs = carve_binning(bbase, K, T, nullptr);
 
     {
         StageTimer st(2, s);
@@ -284,8 +297,8 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
     if ((rc = check("duplicateWithKeys", debug, s))) return rc;
     {
         StageTimer st(3, s);
-        if (sort_pairs_u64(bs.sort_tmp, bs.sort_tmp_bytes, bs.keys_unsorted, bs.keys_sorted, bs.vals_unsorted,
-                           bs.point_list, K, end_bit, s) != hipSuccess)
+        if (tile_sort(bs.sort_tmp, bs.sort_tmp_bytes, bs.tkeys_unsorted, bs.tkeys_sorted, bs.vals_unsorted,
+                      bs.point_list, K, end_bit, bs.wide, s) != hipSuccess)
             return fail(GSR_ERR_DEVICE, "radix sort failed");
     }
     if ((rc = check("sort", debug, s))) return rc;
@@ -329,9 +342,8 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
 
     const Camera cam = make_camera(viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, width, height);
     const int T = cam.gx * cam.gy;
-    const int end_bit = 32 + bits_for(T);
     const GeomState gs = carve_geom(geom_buffer, P, nullptr);
-    const BinningState bs = carve_binning(binning_buffer, R, end_bit, nullptr);
+    const BinningState bs = carve_binning(binning_buffer, R, T, nullptr);
     const ImageState is = carve_image(image_buffer, T, width * height, nullptr);
     size_t sbytes = 0;
     carve_bwd(nullptr, R, &sbytes);

@@ -1,35 +1,73 @@
-// sort.hip -- device scan (tiles_touched -> offsets) and the LSD radix sort of the
-// (tile << 32 | depth) keys, on rocPRIM.  Kept in its own
-// translation unit: rocPRIM's templates dominate compile time.
+// sort.hip -- device scans and radix sorts on rocPRIM.
+//
+// Binning order.  Upstream sorts K (tile << 32 | depth bits) 64-bit keys over 32 + bits(T)
+// bits (6 LSD passes of 8 bits at 1080p).  Here the same total order is produced with far less
+// traffic: (1) the P Gaussians are stably sorted by their 32-bit depth bits, (2) instances are
+// emitted in that order, (3) the K instances are stably sorted by tile id alone (bits(T) = 13 at
+// 1080p: 2 passes over 2-byte keys).  Stability makes the result (tile, depth, id) order --
+// exactly the upstream key order, tie-breaks included.  Kept in its own translation unit:
+// rocPRIM's templates dominate compile time.
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 #include "gsr_launch.h"
 
 namespace gsr {
 
+namespace {
+struct GatherTiles {
+    const uint32_t *tiles;
+    __host__ __device__ uint32_t operator()(uint32_t g) const { return tiles[g]; }
+};
+}  // namespace
+
 size_t scan_temp_bytes(int P) {
     size_t bytes = 0;
-    rocprim::inclusive_scan(nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)(P > 0 ? P : 1),
+    auto it = rocprim::make_transform_iterator((const uint32_t *)nullptr, GatherTiles{nullptr});
+    rocprim::inclusive_scan(nullptr, bytes, it, (uint32_t *)nullptr, (size_t)(P > 0 ? P : 1),
                             rocprim::plus<uint32_t>());
     return bytes;
 }
 
-hipError_t inclusive_scan_u32(void *tmp, size_t tmp_bytes, const uint32_t *in, uint32_t *out, int P, hipStream_t s) {
+hipError_t inclusive_scan_gathered(void *tmp, size_t tmp_bytes, const uint32_t *order, const uint32_t *tiles,
+                                   uint32_t *out, int P, hipStream_t s) {
     if (P == 0) return hipSuccess;
-    return rocprim::inclusive_scan(tmp, tmp_bytes, in, out, (size_t)P, rocprim::plus<uint32_t>(), s);
+    auto it = rocprim::make_transform_iterator(order, GatherTiles{tiles});
+    return rocprim::inclusive_scan(tmp, tmp_bytes, it, out, (size_t)P, rocprim::plus<uint32_t>(), s);
 }
 
-size_t sort_temp_bytes(int64_t K, int end_bit) {
+size_t depth_sort_temp_bytes(int P) {
     size_t bytes = 0;
-    rocprim::radix_sort_pairs(nullptr, bytes, (const uint64_t *)nullptr, (uint64_t *)nullptr,
-                              (const uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)(K > 0 ? K : 1), 0, end_bit);
+    rocprim::radix_sort_pairs(nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                              (const uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)(P > 0 ? P : 1), 0, 32);
     return bytes;
 }
 
-hipError_t sort_pairs_u64(void *tmp, size_t tmp_bytes, const uint64_t *kin, uint64_t *kout, const uint32_t *vin,
-                          uint32_t *vout, int64_t K, int end_bit, hipStream_t s) {
+hipError_t depth_sort(void *tmp, size_t tmp_bytes, const uint32_t *kin, uint32_t *kout, const uint32_t *vin,
+                      uint32_t *vout, int P, hipStream_t s) {
+    if (P == 0) return hipSuccess;
+    return rocprim::radix_sort_pairs(tmp, tmp_bytes, kin, kout, vin, vout, (size_t)P, 0, 32, s);
+}
+
+size_t tile_sort_temp_bytes(int64_t K, int end_bit, bool wide) {
+    size_t bytes = 0;
+    const size_t n = (size_t)(K > 0 ? K : 1);
+    if (wide)
+        rocprim::radix_sort_pairs(nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                  (const uint32_t *)nullptr, (uint32_t *)nullptr, n, 0, end_bit);
+    else
+        rocprim::radix_sort_pairs(nullptr, bytes, (const uint16_t *)nullptr, (uint16_t *)nullptr,
+                                  (const uint32_t *)nullptr, (uint32_t *)nullptr, n, 0, end_bit);
+    return bytes;
+}
+
+hipError_t tile_sort(void *tmp, size_t tmp_bytes, const void *kin, void *kout, const uint32_t *vin, uint32_t *vout,
+                     int64_t K, int end_bit, bool wide, hipStream_t s) {
     if (K == 0) return hipSuccess;
-    return rocprim::radix_sort_pairs(tmp, tmp_bytes, kin, kout, vin, vout, (size_t)K, 0, end_bit, s);
+    if (wide)
+        return rocprim::radix_sort_pairs(tmp, tmp_bytes, static_cast<const uint32_t *>(kin),
+                                         static_cast<uint32_t *>(kout), vin, vout, (size_t)K, 0, end_bit, s);
+    return rocprim::radix_sort_pairs(tmp, tmp_bytes, static_cast<const uint16_t *>(kin), static_cast<uint16_t *>(kout),
+                                     vin, vout, (size_t)K, 0, end_bit, s);
 }
 
 }  // namespace gsr

@@ -199,7 +199,8 @@ def set_profiling(enable: bool) -> None:
     _L.gsr_set_profiling(int(bool(enable)))
 
 
-STAGES = ("preprocess", "scan", "duplicate", "sort", "ranges", "render_fwd", "render_bwd", "preprocess_bwd")
+STAGES = ("preprocess", "depth_sort_scan", "duplicate", "tile_sort", "ranges", "render_fwd", "render_bwd",
+          "preprocess_bwd")
 
 
 def stage_times_ms() -> dict:

@@ -25,11 +25,14 @@ def carve(sizes):
 
 
 def geom_layout(P):
-    return carve([("rec", 64 * P), ("tiles", 4 * P), ("offsets", 4 * P), ("clamped", P)])
+    return carve([("rec", 64 * P), ("tiles", 4 * P), ("dkey", 4 * P), ("dkey_sorted", 4 * P), ("ids", 4 * P),
+                  ("order", 4 * P), ("offsets", 4 * P), ("clamped", P)])
 
 
-def binning_layout(K):
-    return carve([("keys_unsorted", 8 * K), ("keys_sorted", 8 * K), ("vals_unsorted", 4 * K), ("point_list", 4 * K)])
+def binning_layout(K, T):
+    ks = 4 if T > 65536 else 2
+    return carve([("tkeys_unsorted", ks * K), ("tkeys_sorted", ks * K), ("vals_unsorted", 4 * K),
+                  ("point_list", 4 * K)])
 
 
 def image_layout(T, npix):
@@ -46,16 +49,22 @@ def decode_state(geom, binning, image, P, K, W, H):
     g = geom.cpu().numpy()
     b = binning.cpu().numpy()
     im = image.cpu().numpy()
-    gl, bl = geom_layout(P), binning_layout(K)
     gx, gy = (W + 15) // 16, (H + 15) // 16
-    il = image_layout(gx * gy, W * H)
+    T = gx * gy
+    gl, bl = geom_layout(P), binning_layout(K, T)
+    il = image_layout(T, W * H)
     rec = view(g, gl, "rec", np.float32, (P, 16))
+    kt = np.uint32 if T > 65536 else np.uint16
+    tiles_sorted = view(b, bl, "tkeys_sorted", kt).astype(np.uint64)
+    point_list = view(b, bl, "point_list", np.uint32)
+    dbits = rec[:, 14].view(np.uint32)
+    # the 64-bit (tile << 32 | depth bits) keys upstream sorts, rebuilt from the sorted tile ids
+    keys = (tiles_sorted << np.uint64(32)) | dbits[point_list].astype(np.uint64)
     return dict(
-        rec=rec, depths=rec[:, 14].view(np.float32).copy(), xy=rec[:, 0:2], conic_opacity=rec[:, 2:6],
+        rec=rec, depths=dbits.view(np.float32).copy(), xy=rec[:, 0:2], conic_opacity=rec[:, 2:6],
         rgbd=rec[:, 8:12], tiles_touched=view(g, gl, "tiles", np.uint32), offsets=view(g, gl, "offsets", np.uint32),
-        clamped=view(g, gl, "clamped", np.uint8),
-        keys_unsorted=view(b, bl, "keys_unsorted", np.uint64), keys=view(b, bl, "keys_sorted", np.uint64),
-        vals_unsorted=view(b, bl, "vals_unsorted", np.uint32), point_list=view(b, bl, "point_list", np.uint32),
+        order=view(g, gl, "order", np.uint32), clamped=view(g, gl, "clamped", np.uint8),
+        keys=keys, vals_unsorted=view(b, bl, "vals_unsorted", np.uint32), point_list=point_list,
         ranges=view(im, il, "ranges", np.uint32, (gx * gy, 2)), final_T=view(im, il, "final_T", np.float32, (H, W)),
         n_contrib=view(im, il, "n_contrib", np.uint32, (H, W)))
 
