@@ -377,7 +377,7 @@ void gso_render_bwd(int W, int H, const unsigned int *ranges, const unsigned int
                 float dID = dL_dinvd ? dL_dinvd[pix] : 0.f;
                 /* A = blended colour / inverse depth of everything behind the current splat */
                 float A[3] = {0, 0, 0}, Ai = 0;
-                float bg_dot = bg[0] * dp[0] + bg[1] * dp[1] + bg[2] * dp[2];
+                const float TfB = -T_final * (bg[0] * dp[0] + bg[1] * dp[1] + bg[2] * dp[2]);
                 for (unsigned s = re; s-- > rs;) {
                     if (s - rs >= last) continue;
                     unsigned g = point_list[s];
@@ -405,7 +405,7 @@ void gso_render_bwd(int W, int H, const unsigned int *ranges, const unsigned int
                         Ai = fmaf(alpha, diff, Ai);
                         gi[9] = fmaf(dchannel, dID, gi[9]);
                     }
-                    dL_dalpha = fmaf(-T_final * rc, bg_dot, dL_dalpha * T);
+                    dL_dalpha = fmaf(TfB, rc, dL_dalpha * T);
                     float dL_dG = co[3] * dL_dalpha;
                     float gdx = G * dx, gdy = G * dy;
                     float dG_ddelx = fmaf(-gdy, co[1], -gdx * co[0]);

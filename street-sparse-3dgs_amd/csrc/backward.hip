@@ -11,6 +11,96 @@ namespace gsr {
 
 constexpr uint32_t kRedSerial = 32;
 
+// SH backward for degree D: rgb_ch = sum_k B_k(dir) sh[k][ch] (+0.5, clamp handled by the caller
+// zeroing gc).  dL/dsh[k][ch] = B_k gc[ch];  dL/ddir = sum_k dB_k/ddir * (sum_ch sh[k][ch] gc[ch]).
+// The basis and its gradient are evaluated once and shared by the three channels; with M = 16
+// the 192-B coefficient row is read and the gradient row written as 12 float4s.
+template <int D>
+__device__ __forceinline__ void sh_backward(const float *__restrict__ sh, int M, bool vec, const float dir[3],
+                                            const float gc[3], float *__restrict__ dsh, float gd[3]) {
+    constexpr int NC = (D + 1) * (D + 1);
+    const float x = dir[0], y = dir[1], z = dir[2];
+    float B[16], Bx[16], By[16], Bz[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) B[k] = Bx[k] = By[k] = Bz[k] = 0.f;
+    B[0] = GSR_SH_C0;
+    if (D > 0) {
+        B[1] = -GSR_SH_C1 * y; By[1] = -GSR_SH_C1;
+        B[2] = GSR_SH_C1 * z;  Bz[2] = GSR_SH_C1;
+        B[3] = -GSR_SH_C1 * x; Bx[3] = -GSR_SH_C1;
+    }
+    if (D > 1) {
+        const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+        B[4] = GSR_SH_C2_0 * xy; Bx[4] = GSR_SH_C2_0 * y; By[4] = GSR_SH_C2_0 * x;
+        B[5] = GSR_SH_C2_1 * yz; By[5] = GSR_SH_C2_1 * z; Bz[5] = GSR_SH_C2_1 * y;
+        B[6] = GSR_SH_C2_2 * (2.f * zz - xx - yy);
+        Bx[6] = GSR_SH_C2_2 * 2.f * -x; By[6] = GSR_SH_C2_2 * 2.f * -y; Bz[6] = GSR_SH_C2_2 * 2.f * 2.f * z;
+        B[7] = GSR_SH_C2_3 * xz; Bx[7] = GSR_SH_C2_3 * z; Bz[7] = GSR_SH_C2_3 * x;
+        B[8] = GSR_SH_C2_4 * (xx - yy); Bx[8] = GSR_SH_C2_4 * 2.f * x; By[8] = GSR_SH_C2_4 * 2.f * -y;
+        if (D > 2) {
+            B[9] = GSR_SH_C3_0 * y * (3.f * xx - yy);
+            Bx[9] = GSR_SH_C3_0 * 3.f * 2.f * xy; By[9] = GSR_SH_C3_0 * 3.f * (xx - yy);
+            B[10] = GSR_SH_C3_1 * xy * z;
+            Bx[10] = GSR_SH_C3_1 * yz; By[10] = GSR_SH_C3_1 * xz; Bz[10] = GSR_SH_C3_1 * xy;
+            B[11] = GSR_SH_C3_2 * y * (4.f * zz - xx - yy);
+            Bx[11] = GSR_SH_C3_2 * -2.f * xy; By[11] = GSR_SH_C3_2 * (-3.f * yy + 4.f * zz - xx);
+            Bz[11] = GSR_SH_C3_2 * 4.f * 2.f * yz;
+            B[12] = GSR_SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy);
+            Bx[12] = GSR_SH_C3_3 * -3.f * 2.f * xz; By[12] = GSR_SH_C3_3 * -3.f * 2.f * yz;
+            Bz[12] = GSR_SH_C3_3 * 3.f * (2.f * zz - xx - yy);
+            B[13] = GSR_SH_C3_4 * x * (4.f * zz - xx - yy);
+            Bx[13] = GSR_SH_C3_4 * (-3.f * xx + 4.f * zz - yy); By[13] = GSR_SH_C3_4 * -2.f * xy;
+            Bz[13] = GSR_SH_C3_4 * 4.f * 2.f * xz;
+            B[14] = GSR_SH_C3_5 * z * (xx - yy);
+            Bx[14] = GSR_SH_C3_5 * 2.f * xz; By[14] = GSR_SH_C3_5 * -2.f * yz; Bz[14] = GSR_SH_C3_5 * (xx - yy);
+            B[15] = GSR_SH_C3_6 * x * (xx - 3.f * yy);
+            Bx[15] = GSR_SH_C3_6 * 3.f * (xx - yy); By[15] = GSR_SH_C3_6 * -3.f * 2.f * xy;
+        }
+    }
+    float c[48];
+    if (vec) {
+        const float4 *s4 = reinterpret_cast<const float4 *>(sh);
+#pragma unroll
+        for (int q = 0; q < 12; q++) {
+            if (4 * q < NC * 3) {
+                const float4 v = s4[q];
+                c[4 * q] = v.x; c[4 * q + 1] = v.y; c[4 * q + 2] = v.z; c[4 * q + 3] = v.w;
+            } else {
+                c[4 * q] = c[4 * q + 1] = c[4 * q + 2] = c[4 * q + 3] = 0.f;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < 48; e++) c[e] = e < NC * 3 ? sh[e] : 0.f;
+    }
+    gd[0] = gd[1] = gd[2] = 0.f;
+#pragma unroll
+    for (int k = 1; k < NC; k++) {
+        const float vk = c[3 * k] * gc[0] + c[3 * k + 1] * gc[1] + c[3 * k + 2] * gc[2];
+        gd[0] = fmaf(Bx[k], vk, gd[0]);
+        gd[1] = fmaf(By[k], vk, gd[1]);
+        gd[2] = fmaf(Bz[k], vk, gd[2]);
+    }
+    if (vec) {
+        float4 *d4 = reinterpret_cast<float4 *>(dsh);
+#pragma unroll
+        for (int q = 0; q < 12; q++) {
+            float e4[4];
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const int e = 4 * q + t;
+                e4[t] = e < NC * 3 ? B[e / 3] * gc[e % 3] : 0.f;
+            }
+            d4[q] = make_float4(e4[0], e4[1], e4[2], e4[3]);
+        }
+    } else {
+        for (int e = 0; e < M * 3; e++) dsh[e] = 0.f;
+#pragma unroll
+        for (int e = 0; e < NC * 3; e++) dsh[e] = B[e / 3] * gc[e % 3];
+    }
+}
+
+
 __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
     int P, int D, int M, const float *__restrict__ means3D, const int *__restrict__ radii,
     const float *__restrict__ shs, const uint8_t *__restrict__ clamped, const float *__restrict__ scales,
@@ -24,6 +114,8 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
     const bool has_shs = shs != nullptr;
     const bool has_scales = cov3D_precomp == nullptr;
     const bool vis = valid && radii[i] > 0;
+    const bool vec_sh = M == 16 && (reinterpret_cast<uintptr_t>(shs) % 16 == 0) &&
+                        (reinterpret_cast<uintptr_t>(out.dsh) % 16 == 0);
 
     // Sum this Gaussian's per-tile records (contiguous at its exclusive-scan offset).  A record
     // exists only for tiles where this Gaussian sits in front of the tile's boundary (the last
@@ -182,73 +274,35 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
     // ---- colour ----
     if (has_shs) {
         float *dsh = out.dsh + (size_t)i * M * 3;
-        const int nc = (D + 1) * (D + 1);
         if (!vis) {
-            for (int k = 0; k < M * 3; k++) dsh[k] = 0.f;
+            if (vec_sh) {
+                float4 *d4 = reinterpret_cast<float4 *>(dsh);
+#pragma unroll
+                for (int c = 0; c < 12; c++) d4[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+            } else {
+                for (int k = 0; k < M * 3; k++) dsh[k] = 0.f;
+            }
         } else {
             float dir[3], dor[3];
             sh_dir(p, make_float3(campos_p[0], campos_p[1], campos_p[2]), dir, dor);
-            const float *sh = shs + (size_t)i * M * 3;
             const uint8_t cl = clamped[i];
-            const float x = dir[0], y = dir[1], z = dir[2];
-            float gd0 = 0.f, gd1 = 0.f, gd2 = 0.f;
-            for (int ch = 0; ch < 3; ch++) {
-                const float gc = (cl >> ch) & 1 ? 0.f : g[6 + ch];
-                float ddx = 0.f, ddy = 0.f, ddz = 0.f;
-                dsh[ch] = GSR_SH_C0 * gc;
-                if (D > 0) {
-                    const float *s = sh + ch;
-                    dsh[1 * 3 + ch] = -GSR_SH_C1 * y * gc;
-                    dsh[2 * 3 + ch] = GSR_SH_C1 * z * gc;
-                    dsh[3 * 3 + ch] = -GSR_SH_C1 * x * gc;
-                    ddx = -GSR_SH_C1 * s[3 * 3];
-                    ddy = -GSR_SH_C1 * s[1 * 3];
-                    ddz = GSR_SH_C1 * s[2 * 3];
-                    if (D > 1) {
-                        const float xx = x * x, yy = y * y, zz = z * z, xy_ = x * y, yz = y * z, xz = x * z;
-                        dsh[4 * 3 + ch] = GSR_SH_C2_0 * xy_ * gc;
-                        dsh[5 * 3 + ch] = GSR_SH_C2_1 * yz * gc;
-                        dsh[6 * 3 + ch] = GSR_SH_C2_2 * (2.f * zz - xx - yy) * gc;
-                        dsh[7 * 3 + ch] = GSR_SH_C2_3 * xz * gc;
-                        dsh[8 * 3 + ch] = GSR_SH_C2_4 * (xx - yy) * gc;
-                        ddx += GSR_SH_C2_0 * y * s[4 * 3] + GSR_SH_C2_2 * 2.f * -x * s[6 * 3] +
-                               GSR_SH_C2_3 * z * s[7 * 3] + GSR_SH_C2_4 * 2.f * x * s[8 * 3];
-                        ddy += GSR_SH_C2_0 * x * s[4 * 3] + GSR_SH_C2_1 * z * s[5 * 3] +
-                               GSR_SH_C2_2 * 2.f * -y * s[6 * 3] + GSR_SH_C2_4 * 2.f * -y * s[8 * 3];
-                        ddz += GSR_SH_C2_1 * y * s[5 * 3] + GSR_SH_C2_2 * 2.f * 2.f * z * s[6 * 3] +
-                               GSR_SH_C2_3 * x * s[7 * 3];
-                        if (D > 2) {
-                            dsh[9 * 3 + ch] = GSR_SH_C3_0 * y * (3.f * xx - yy) * gc;
-                            dsh[10 * 3 + ch] = GSR_SH_C3_1 * xy_ * z * gc;
-                            dsh[11 * 3 + ch] = GSR_SH_C3_2 * y * (4.f * zz - xx - yy) * gc;
-                            dsh[12 * 3 + ch] = GSR_SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy) * gc;
-                            dsh[13 * 3 + ch] = GSR_SH_C3_4 * x * (4.f * zz - xx - yy) * gc;
-                            dsh[14 * 3 + ch] = GSR_SH_C3_5 * z * (xx - yy) * gc;
-                            dsh[15 * 3 + ch] = GSR_SH_C3_6 * x * (xx - 3.f * yy) * gc;
-                            ddx += GSR_SH_C3_0 * s[9 * 3] * 3.f * 2.f * xy_ + GSR_SH_C3_1 * s[10 * 3] * yz +
-                                   GSR_SH_C3_2 * s[11 * 3] * -2.f * xy_ + GSR_SH_C3_3 * s[12 * 3] * -3.f * 2.f * xz +
-                                   GSR_SH_C3_4 * s[13 * 3] * (-3.f * xx + 4.f * zz - yy) +
-                                   GSR_SH_C3_5 * s[14 * 3] * 2.f * xz + GSR_SH_C3_6 * s[15 * 3] * 3.f * (xx - yy);
-                            ddy += GSR_SH_C3_0 * s[9 * 3] * 3.f * (xx - yy) + GSR_SH_C3_1 * s[10 * 3] * xz +
-                                   GSR_SH_C3_2 * s[11 * 3] * (-3.f * yy + 4.f * zz - xx) +
-                                   GSR_SH_C3_3 * s[12 * 3] * -3.f * 2.f * yz + GSR_SH_C3_4 * s[13 * 3] * -2.f * xy_ +
-                                   GSR_SH_C3_5 * s[14 * 3] * -2.f * yz + GSR_SH_C3_6 * s[15 * 3] * -3.f * 2.f * xy_;
-                            ddz += GSR_SH_C3_1 * s[10 * 3] * xy_ + GSR_SH_C3_2 * s[11 * 3] * 4.f * 2.f * yz +
-                                   GSR_SH_C3_3 * s[12 * 3] * 3.f * (2.f * zz - xx - yy) +
-                                   GSR_SH_C3_4 * s[13 * 3] * 4.f * 2.f * xz + GSR_SH_C3_5 * s[14 * 3] * (xx - yy);
-                        }
-                    }
-                }
-                gd0 += ddx * gc;
-                gd1 += ddy * gc;
-                gd2 += ddz * gc;
+            float gc[3];
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++) gc[ch] = (cl >> ch) & 1 ? 0.f : g[6 + ch];
+            float gd[3];
+            const float *sh = shs + (size_t)i * M * 3;
+            switch (D) {
+                case 0: sh_backward<0>(sh, M, vec_sh, dir, gc, dsh, gd); break;
+                case 1: sh_backward<1>(sh, M, vec_sh, dir, gc, dsh, gd); break;
+                case 2: sh_backward<2>(sh, M, vec_sh, dir, gc, dsh, gd); break;
+                default: sh_backward<3>(sh, M, vec_sh, dir, gc, dsh, gd); break;
             }
-            for (int k = nc * 3; k < M * 3; k++) dsh[k] = 0.f;
+            // d normalize(v)/dv applied to the direction gradient
             const float s2 = dor[0] * dor[0] + dor[1] * dor[1] + dor[2] * dor[2];
             const float inv32 = 1.0f / sqrtf(s2 * s2 * s2);
-            dm[0] += ((s2 - dor[0] * dor[0]) * gd0 - dor[1] * dor[0] * gd1 - dor[2] * dor[0] * gd2) * inv32;
-            dm[1] += (-dor[0] * dor[1] * gd0 + (s2 - dor[1] * dor[1]) * gd1 - dor[2] * dor[1] * gd2) * inv32;
-            dm[2] += (-dor[0] * dor[2] * gd0 - dor[1] * dor[2] * gd1 + (s2 - dor[2] * dor[2]) * gd2) * inv32;
+            dm[0] += ((s2 - dor[0] * dor[0]) * gd[0] - dor[1] * dor[0] * gd[1] - dor[2] * dor[0] * gd[2]) * inv32;
+            dm[1] += (-dor[0] * dor[1] * gd[0] + (s2 - dor[1] * dor[1]) * gd[1] - dor[2] * dor[1] * gd[2]) * inv32;
+            dm[2] += (-dor[0] * dor[2] * gd[0] - dor[1] * dor[2] * gd[1] + (s2 - dor[2] * dor[2]) * gd[2]) * inv32;
         }
         out.dcolors[3 * i + 0] = 0.f;
         out.dcolors[3 * i + 1] = 0.f;

@@ -196,6 +196,33 @@ __device__ __forceinline__ float wave_sum(float v) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
+// Sum each of N independent values over the 64 lanes; every lane receives every total.
+// Stage-major order (each DPP stage issued for all N values before the next) lets the N chains
+// hide each other's DPP read-after-write hazards instead of padding every step with s_nop.
+// Rows of 16 are reduced with DPP (quad_perm, row_ror); the row pairs and wave halves are
+// combined with gfx950's v_permlane16_swap / v_permlane32_swap (no LDS, no readlane).
+template <int N>
+__device__ __forceinline__ void wave_allreduce(float *v) {
+#pragma unroll
+    for (int i = 0; i < N; i++) v[i] += dpp_f<0xB1>(v[i]);
+#pragma unroll
+    for (int i = 0; i < N; i++) v[i] += dpp_f<0x4E>(v[i]);
+#pragma unroll
+    for (int i = 0; i < N; i++) v[i] += dpp_f<0x124>(v[i]);
+#pragma unroll
+    for (int i = 0; i < N; i++) v[i] += dpp_f<0x128>(v[i]);
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[i]), false, false);
+        v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[i]), false, false);
+        v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
+}
+
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) {
