@@ -100,7 +100,7 @@ def cpu_baseline(s, P, W, H, deg):
 
 def latest_traffic(kernel):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/*pmc*.json)."""
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")), key=os.path.getmtime)
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")))  # named r<round><letter>_...
     for f in reversed(files):
         try:
             d = json.load(open(f))

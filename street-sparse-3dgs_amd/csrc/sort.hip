@@ -14,6 +14,11 @@
 namespace gsr {
 
 namespace {
+// rocPRIM routes radix sorts of up to 2^20 items through block-sort + 10 merge passes; for the
+// P ~ 1M depth keys that is ~150 us/frame on MI355X vs a few onesweep passes.  Cap the merge path.
+using OnesweepCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                               rocprim::default_config, 8192>;
+
 struct GatherTiles {
     const uint32_t *tiles;
     __host__ __device__ uint32_t operator()(uint32_t g) const { return tiles[g]; }
@@ -37,15 +42,16 @@ hipError_t inclusive_scan_gathered(void *tmp, size_t tmp_bytes, const uint32_t *
 
 size_t depth_sort_temp_bytes(int P) {
     size_t bytes = 0;
-    rocprim::radix_sort_pairs(nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                              (const uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)(P > 0 ? P : 1), 0, 32);
+    rocprim::radix_sort_pairs<OnesweepCfg>(nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                           (const uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)(P > 0 ? P : 1),
+                                           0, 32);
     return bytes;
 }
 
 hipError_t depth_sort(void *tmp, size_t tmp_bytes, const uint32_t *kin, uint32_t *kout, const uint32_t *vin,
                       uint32_t *vout, int P, hipStream_t s) {
     if (P == 0) return hipSuccess;
-    return rocprim::radix_sort_pairs(tmp, tmp_bytes, kin, kout, vin, vout, (size_t)P, 0, 32, s);
+    return rocprim::radix_sort_pairs<OnesweepCfg>(tmp, tmp_bytes, kin, kout, vin, vout, (size_t)P, 0, 32, s);
 }
 
 size_t tile_sort_temp_bytes(int64_t K, int end_bit, bool wide) {

@@ -15,18 +15,32 @@ import csv
 import glob
 import json
 import os
+import re
 from collections import defaultdict
 
 STAGE_OF = [("render_bwd_kernel", "render_bwd"), ("render_fwd_kernel", "render_fwd"),
             ("preprocess_bwd_kernel", "preprocess_bwd"), ("preprocess_kernel", "preprocess"),
-            ("duplicate_kernel", "duplicate"), ("ranges_kernel", "ranges"), ("mark_visible", "mark_visible"),
-            ("radix", "sort"), ("onesweep", "sort"), ("scan", "scan"), ("rocprim", "rocprim")]
+            ("duplicate_kernel", "duplicate"), ("ranges_kernel", "ranges"), ("mark_visible", "mark_visible")]
+# rocPRIM kernels are all `trampoline_kernel<wrapped_<algo>_config<cfg, KeyT, ...>>`: the algorithm
+# and key type tell the depth sort (u32 keys over P) from the tile sort (u16 keys over K).
+ROCPRIM = re.compile(r"wrapped_(\w+?)_config<[^,]+(?:<[^>]*>)?, (unsigned \w+)")
 
 
 def stage(name):
     for k, v in STAGE_OF:
         if k in name:
             return v
+    m = ROCPRIM.search(name)
+    if m:
+        algo, key = m.groups()
+        if algo == "scan":
+            return "depth_sort_scan:scan"
+        if "lookback" in name:
+            return "rocprim:init_lookback"
+        who = "tile_sort" if key == "unsigned short" else "sort_u32"
+        return f"{who}:{algo}"
+    if "init_lookback" in name:
+        return "rocprim:init_lookback"
     return name.split("(")[0][:60]
 
 
