@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--profile-steps", type=int, default=5, help="extra steps with per-stage HIP events")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--diag", action="store_true", help="print synced per-step fwd/bwd wall times to stderr")
+    ap.add_argument("--train-steps", type=int, default=10, help="timed train-step harness iterations (0 = skip)")
+    ap.add_argument("--train-baseline", action="store_true",
+                    help="also time the reference-structured torch train step (conv2d SSIM, OurAdam gather/scatter)")
     return ap.parse_args()
 
 
@@ -68,8 +71,8 @@ def algorithmic_bytes(P, Pv, K, T, npix, M=16):
 def make_inputs(P, W, H, deg, seed, device):
     import numpy as np
     import torch
-    import gs_oracle as O
-    s = O.synthetic_scene(P, W, H, seed=seed, sh_degree=deg)
+    from gs_train.synthetic import synthetic_scene
+    s = synthetic_scene(P, W, H, seed=seed, sh_degree=deg)
     t = lambda a: torch.tensor(np.asarray(a), dtype=torch.float32, device=device)
     inp = dict(means3D=t(s["means3D"]), means2D=torch.zeros(P, 3, device=device), opacities=t(s["opacities"]),
                shs=t(s["shs"]), scales=t(s["scales"]), rotations=t(s["rotations"]))
@@ -96,6 +99,31 @@ def cpu_baseline(s, P, W, H, deg):
     return {"value": round(W * H / dt / 1e6, 4), "unit": "Mpix/s", "cores": O.num_threads(), "kind": "port",
             "sample": f"1 fwd+bwd frame of the bench workload ({P} Gaussians, {W}x{H}, SH deg {deg}) through "
                       f"the C oracle, {dt:.2f} s"}
+
+
+def train_step_ms(s, W, H, deg, steps, warmup, fused, dev):
+    """one train_single.py iteration (render + exposure + L1/SSIM loss +
+    backward + densification stats + exposure Adam + sparse Adam + scale clamp) on the bench
+    scene; wall time per step between synchronisations (the harness itself never syncs when
+    fused)."""
+    import torch
+    from gs_train.harness import GaussianSet, TrainStep
+    g = GaussianSet(s["means3D"], s["shs"], s["opacities"], s["scales"], s["rotations"], n_images=1,
+                    sh_degree=deg, device=dev)
+    gen = torch.Generator(device=dev).manual_seed(123)
+    gt = torch.rand((3, H, W), device=dev, generator=gen)
+    ts = TrainStep(g, [(s["view"], s["proj"], s["campos"], s["tanfovx"], s["tanfovy"])], [gt], W, H, fused=fused)
+    for _ in range(warmup):
+        ts.step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ts.step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    del ts, g
+    torch.cuda.empty_cache()
+    return ms
 
 
 def latest_traffic(kernel):
@@ -220,7 +248,7 @@ def main():
     ms_per_step = elapsed / a.steps * 1e3
     value = world * npix * a.steps / elapsed / 1e6
     out = {
-        "metric": "fwd+bwd Mpix/s at 1080p (1M Gaussians)",
+        "metric": "fwd+bwd Mpix/s at 1080p (1M Gaussians)",  # + "train_step" ms below
         "value": round(value, 3),
         "unit": "Mpix/s",
         "n_gpus": world,
@@ -244,6 +272,14 @@ def main():
                               "frac": round(sum(abytes.values()) / (sum(stages.values()) * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
                               if stages else None},
     }
+    if a.train_steps > 0:
+        tr = {"ms": round(train_step_ms(s, W, H, deg, a.train_steps, 3, True, dev), 4),
+              "workload": f"train_single.py iteration on the bench scene ({P} Gaussians, {W}x{H}): render, exposure, "
+                          f"0.8 L1 + 0.2 (1 - SSIM), backward, densify stats, exposure Adam, sparse Adam, scale clamp",
+              "steps": a.train_steps, "fused": True}
+        if a.train_baseline:
+            tr["reference_structured_ms"] = round(train_step_ms(s, W, H, deg, a.train_steps, 3, False, dev), 4)
+        out["train_step"] = tr
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(s, P, W, H, deg)
     if rank == 0:

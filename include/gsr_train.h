@@ -1,0 +1,85 @@
+/*
+ * gsr_train.h -- C ABI of the train-step kernels that sit either side of the rasterizer in one
+ * Street-sparse-3DGS iteration.  Exported by the same
+ * libgsr_hip.so as include/gsr.h.
+ *
+ *   gsr_l1_ssim_forward / _backward  replace  utils/loss_utils.py:17-18 (l1_loss) and :33-63
+ *                                    (ssim: five 11x11 depthwise conv2d, sigma 1.5, zero pad),
+ *                                    as combined at train_single.py:121-123
+ *   gsr_sparse_adam_step             replaces scene/OurAdam.py:105-175 + _single_tensor_adam
+ *                                    (:249-337) / _single_tensor_adam2 (:338-...) for the six
+ *                                    Gaussian parameter groups (scene/gaussian_model.py:286-296),
+ *                                    with `relevant = opacity.grad != 0` (train_single.py:224-230)
+ *                                    evaluated on the device
+ *   gsr_exposure_forward / _backward replace  the per-image exposure affine + clamp of render()
+ *                                    (gaussian_renderer/__init__.py:115-120, use_trained_exp=True
+ *                                    at train_single.py:111): a (H*W, 3) x (3, 3) GEMM, a
+ *                                    broadcast add and a clamp in torch
+ *   gsr_densify_stats                replaces train_single.py:193-194 +
+ *                                    scene/gaussian_model.py:780-793 (add_densification_stats)
+ *
+ * Conventions as in gsr.h: device pointers, fp32, contiguous, `stream` a hipStream_t.
+ */
+#ifndef GSR_TRAIN_H
+#define GSR_TRAIN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Bytes of device scratch gsr_l1_ssim_forward needs for C planes of H x W. */
+size_t gsr_l1_ssim_scratch_bytes(int C, int H, int W);
+
+/* out[0] = mean |img - gt|, out[1] = mean SSIM map (reference: l1_loss(img, gt), ssim(img, gt)).
+ * img, gt: (C, H, W).  Deterministic (fixed-order reduction, no atomics). */
+int gsr_l1_ssim_forward(const float *img, const float *gt, int C, int H, int W, void *scratch, float *out,
+                        void *stream);
+
+/* dL_dimg = dL_dout[0] * d(mean|img-gt|)/dimg + dL_dout[1] * d(mean SSIM)/dimg.
+ * dL_dout is a 2-float DEVICE array (the autograd grad_outputs; no host sync). */
+int gsr_l1_ssim_backward(const float *img, const float *gt, int C, int H, int W, const float *dL_dout,
+                         float *dL_dimg, void *stream);
+
+/* One parameter group of the sparse Adam step: a (P, width) row-major parameter with its grad
+ * and moment buffers.  step_size = lr / (1 - beta1^step) and bias_correction2_sqrt =
+ * sqrt(1 - beta2^step) are computed by the host in double, exactly as OurAdam does. */
+typedef struct {
+    float *param;
+    const float *grad;
+    float *exp_avg;
+    float *exp_avg_sq;
+    int64_t width;
+    float step_size;
+    float bias_correction2_sqrt;
+} gsr_adam_group;
+
+/* Rows r with relevance[r] != 0 are updated in every group; if no row is relevant, every row
+ * is updated (OurAdam's _single_tensor_adam2 branch).  flag_scratch: one device int. */
+int gsr_sparse_adam_step(int n_groups, const gsr_adam_group *groups, int64_t P, const float *relevance,
+                         double beta1, double beta2, double eps, int *flag_scratch, void *stream);
+
+/* out[c][p] = clamp(sum_k color[k][p] * E[k][c] + E[c][3], 0, 1) for the 3 planes of npix
+ * pixels; E is the 3x4 exposure matrix (row-major, device). */
+int gsr_exposure_forward(const float *color, const float *exposure, int64_t npix, float *out, void *stream);
+
+/* Bytes of device scratch gsr_exposure_backward needs. */
+size_t gsr_exposure_scratch_bytes(int64_t npix);
+
+/* dL_dcolor (3, npix) and dL_dexposure (3x4) from dL_dout (3, npix); the clamp passes gradient
+ * where 0 <= pre-clamp value <= 1 (torch.clamp).  dL_dexposure is overwritten (deterministic,
+ * fixed-order reduction). */
+int gsr_exposure_backward(const float *color, const float *exposure, int64_t npix, const float *dL_dout,
+                          float *dL_dcolor, float *dL_dexposure, void *scratch, void *stream);
+
+/* For rows with radii > 0: max_radii2D = max(max_radii2D, radii);
+ * grad_accum = max(||dL_dmeans2D[:, :2]||, grad_accum); denom += 1. */
+int gsr_densify_stats(int64_t P, const int *radii, const float *dL_dmeans2D, float *max_radii2D,
+                      float *grad_accum, float *denom, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSR_TRAIN_H */

@@ -2,9 +2,13 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string>
 #include "gsr_device.h"
 
 namespace gsr {
+
+// rasterizer.hip: message returned by gsr_last_error() for the calling thread.
+void set_last_error(const std::string &msg);
 
 struct Camera {
     const float *view;  // device, 16

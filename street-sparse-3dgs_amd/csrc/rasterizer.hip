@@ -180,6 +180,8 @@ int validate_common(int P, int D, int M, const float *shs, const float *colors_p
 
 }  // namespace
 
+void gsr::set_last_error(const std::string &msg) { g_err = msg; }
+
 extern "C" {
 
 int gsr_abi_version(void) { return GSR_ABI_VERSION; }

@@ -1,0 +1,618 @@
+// train.hip -- the device work of one train_single.py iteration around the rasterizer
+// (8(f) rows 1-2): fused L1 + SSIM loss forward/backward, the fused sparse
+// Adam step over all six Gaussian parameter groups, and the densification statistics.
+//
+// Loss.  The reference evaluates SSIM with five depthwise 11x11 conv2d passes
+// (utils/loss_utils.py:44-63) plus elementwise torch ops and autograd replays them in backward.
+// Here one launch computes both means (L1 and SSIM) from one read of the two images: a 64x16
+// output tile per workgroup stages its 74x26 input halo in LDS, runs the separable Gaussian
+// window as a horizontal then a vertical pass over the five moments (x, y, x^2, y^2, xy), and
+// reduces per block (fixed-order second pass, so the loss is deterministic).  The backward
+// recomputes the moments over a 2-radius halo instead of storing per-pixel partials: it reads
+// the two images once and writes the gradient once, with every intermediate in LDS.
+//
+// Adam.  OurAdam (scene/OurAdam.py:249-337) gathers the `relevant` rows of every group,
+// updates them and scatters them back, one torch op at a time, after a host-synchronising
+// nonzero().  Here one launch walks all six groups' (param, grad, m, v) arrays once, testing
+// relevance (opacity grad != 0) per row on the device.
+#include <cmath>
+#include <cstring>
+#include <string>
+
+#include "../../include/gsr.h"
+#include "../../include/gsr_train.h"
+#include "gsr_launch.h"
+
+namespace gsr {
+namespace {
+
+constexpr int kR = 5;  // window radius: 11 taps
+constexpr int kTW = 64;
+constexpr int kTH = 16;
+constexpr int kLossThreads = 256;
+constexpr float kC1 = 0.01f * 0.01f;  // utils/loss_utils.py:54-55 (C1 = 0.01^2, C2 = 0.03^2)
+constexpr float kC2 = 0.03f * 0.03f;
+
+struct Window {
+    float w[2 * kR + 1];
+};
+
+// utils/loss_utils.py:24-26: exp(-(x - 5)^2 / (2 sigma^2)) as fp32, normalised by its fp32 sum.
+Window ssim_window() {
+    Window win;
+    float sum = 0.f;
+    for (int i = 0; i < 2 * kR + 1; i++) {
+        win.w[i] = (float)std::exp(-(double)((i - kR) * (i - kR)) / (2.0 * 1.5 * 1.5));
+        sum += win.w[i];
+    }
+    for (int i = 0; i < 2 * kR + 1; i++) win.w[i] /= sum;
+    return win;
+}
+
+struct Moments {
+    float m1, m2, a11, a22, a12;
+};
+
+// SSIM map value at one pixel from its windowed moments (utils/loss_utils.py:44-58 op order).
+__device__ __forceinline__ float ssim_value(const Moments &s) {
+    const float mu1_sq = s.m1 * s.m1, mu2_sq = s.m2 * s.m2, mu12 = s.m1 * s.m2;
+    const float s1 = s.a11 - mu1_sq, s2 = s.a22 - mu2_sq, s12 = s.a12 - mu12;
+    return ((2.f * mu12 + kC1) * (2.f * s12 + kC2)) / ((mu1_sq + mu2_sq + kC1) * (s1 + s2 + kC2));
+}
+
+// dS/d(mu1), dS/d(E[x^2]), dS/d(E[xy]) at one pixel, mu1 derivative including its appearance in
+// sigma1^2 = E[x^2] - mu1^2 and sigma12 = E[xy] - mu1 mu2.
+__device__ __forceinline__ void ssim_partials(const Moments &s, float &a, float &b, float &c) {
+    const float mu1_sq = s.m1 * s.m1, mu2_sq = s.m2 * s.m2, mu12 = s.m1 * s.m2;
+    const float s1 = s.a11 - mu1_sq, s2 = s.a22 - mu2_sq, s12 = s.a12 - mu12;
+    const float n1 = 2.f * mu12 + kC1, n2 = 2.f * s12 + kC2;
+    const float d1 = mu1_sq + mu2_sq + kC1, d2 = s1 + s2 + kC2;
+    const float inv = 1.f / (d1 * d2);
+    const float S = n1 * n2 * inv;
+    const float ds1 = -S / d2;
+    const float ds12 = 2.f * n1 * inv;
+    const float dmu = 2.f * s.m2 * n2 * inv - 2.f * s.m1 * S / d1;
+    a = dmu - 2.f * s.m1 * ds1 - s.m2 * ds12;
+    b = ds1;
+    c = ds12;
+}
+
+// Load a rows x cols region of one plane with origin (oy, ox), zero outside the image.
+__device__ __forceinline__ void load_halo(const float *__restrict__ x, const float *__restrict__ y, int H, int W,
+                                          int oy, int ox, int rows, int cols, float *sx, float *sy) {
+    for (int i = threadIdx.x; i < rows * cols; i += kLossThreads) {
+        const int r = i / cols, c = i - r * cols;
+        const int gy = oy + r, gx = ox + c;
+        const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
+        const size_t o = (size_t)gy * W + gx;
+        sx[i] = in ? x[o] : 0.f;
+        sy[i] = in ? y[o] : 0.f;
+    }
+}
+
+// Horizontal pass of the five moments: out[q][r][c] = sum_j w_j f_q(in[r][c + j]).
+__device__ __forceinline__ void hpass5(const float *sx, const float *sy, int rows, int in_cols, int out_cols,
+                                       const Window &win, float *hs) {
+    const int plane = rows * out_cols;
+    for (int i = threadIdx.x; i < plane; i += kLossThreads) {
+        const int r = i / out_cols, c = i - r * out_cols;
+        const float *px = sx + r * in_cols + c, *py = sy + r * in_cols + c;
+        float m1 = 0.f, m2 = 0.f, a11 = 0.f, a22 = 0.f, a12 = 0.f;
+#pragma unroll
+        for (int j = 0; j < 2 * kR + 1; j++) {
+            const float a = px[j], b = py[j], w = win.w[j];
+            m1 = fmaf(w, a, m1);
+            m2 = fmaf(w, b, m2);
+            a11 = fmaf(w, a * a, a11);
+            a22 = fmaf(w, b * b, a22);
+            a12 = fmaf(w, a * b, a12);
+        }
+        hs[i] = m1;
+        hs[plane + i] = m2;
+        hs[2 * plane + i] = a11;
+        hs[3 * plane + i] = a22;
+        hs[4 * plane + i] = a12;
+    }
+}
+
+// Vertical pass for the 64 x 16 output tile: lane column c = tid & 63 and four consecutive rows
+// r0..r0+3 per thread, a 14-row sliding window per quantity.
+template <int NQ>
+__device__ __forceinline__ void vpass_tile(const float *hs, int plane, const Window &win, float (&acc)[NQ][4]) {
+    const int c = threadIdx.x & 63, r0 = (threadIdx.x >> 6) * 4;
+#pragma unroll
+    for (int q = 0; q < NQ; q++) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) acc[q][k] = 0.f;
+        const float *h = hs + q * plane + r0 * kTW + c;
+#pragma unroll
+        for (int t = 0; t < 2 * kR + 4; t++) {
+            const float v = h[t * kTW];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int j = t - k;
+                if (j >= 0 && j <= 2 * kR) acc[q][k] = fmaf(win.w[j], v, acc[q][k]);
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ float block_sum(float v, float *red) {
+    v = wave_sum(v);
+    const int wv = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[wv] = v;
+    __syncthreads();
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < kLossThreads / 64; k++) s += red[k];
+    return s;
+}
+
+constexpr int kFwdRH = kTH + 2 * kR, kFwdRW = kTW + 2 * kR;  // 26 x 74 input halo
+constexpr size_t kFwdLds = sizeof(float) * (2 * kFwdRH * kFwdRW + 5 * kFwdRH * kTW + 8);
+
+__global__ __launch_bounds__(kLossThreads) void l1_ssim_fwd_kernel(const float *__restrict__ x,
+                                                                    const float *__restrict__ y, int H, int W,
+                                                                    Window win, float2 *__restrict__ partials) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float *sx = reinterpret_cast<float *>(smem);
+    float *sy = sx + kFwdRH * kFwdRW;
+    float *hs = sy + kFwdRH * kFwdRW;
+    float *red = hs + 5 * kFwdRH * kTW;
+    const size_t plane_off = (size_t)blockIdx.z * H * W;
+    x += plane_off;
+    y += plane_off;
+    const int ox = blockIdx.x * kTW, oy = blockIdx.y * kTH;
+
+    load_halo(x, y, H, W, oy - kR, ox - kR, kFwdRH, kFwdRW, sx, sy);
+    __syncthreads();
+    hpass5(sx, sy, kFwdRH, kFwdRW, kTW, win, hs);
+    __syncthreads();
+    float acc[5][4];
+    vpass_tile<5>(hs, kFwdRH * kTW, win, acc);
+
+    const int c = threadIdx.x & 63, r0 = (threadIdx.x >> 6) * 4;
+    float l1 = 0.f, ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int gy = oy + r0 + k, gx = ox + c;
+        if (gy < H && gx < W) {
+            const Moments m{acc[0][k], acc[1][k], acc[2][k], acc[3][k], acc[4][k]};
+            ss += ssim_value(m);
+            const int li = (r0 + k + kR) * kFwdRW + c + kR;
+            l1 += fabsf(sx[li] - sy[li]);
+        }
+    }
+    l1 = block_sum(l1, red);
+    ss = block_sum(ss, red + 4);
+    if (threadIdx.x == 0) {
+        const int b = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+        partials[b] = make_float2(l1, ss);
+    }
+}
+
+__global__ __launch_bounds__(1024) void loss_finalize_kernel(const float2 *__restrict__ partials, int n, double inv_n,
+                                                             float *__restrict__ out) {
+    __shared__ double s1[1024], s2[1024];
+    double a = 0.0, b = 0.0;
+    for (int i = threadIdx.x; i < n; i += 1024) {
+        a += partials[i].x;
+        b += partials[i].y;
+    }
+    s1[threadIdx.x] = a;
+    s2[threadIdx.x] = b;
+    __syncthreads();
+    for (int w = 512; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            s1[threadIdx.x] += s1[threadIdx.x + w];
+            s2[threadIdx.x] += s2[threadIdx.x + w];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out[0] = (float)(s1[0] * inv_n);
+        out[1] = (float)(s2[0] * inv_n);
+    }
+}
+
+constexpr int kBwdIH = kTH + 4 * kR, kBwdIW = kTW + 4 * kR;  // 36 x 84 inputs
+constexpr int kBwdSH = kTH + 2 * kR, kBwdSW = kTW + 2 * kR;  // 26 x 74 SSIM-map positions
+constexpr size_t kBwdLds = sizeof(float) * (2 * kBwdIH * kBwdIW + 5 * kBwdIH * kBwdSW);
+static_assert(3 * kBwdSH * kBwdSW <= 2 * kBwdIH * kBwdIW, "a/b/c maps alias the input halo");
+static_assert(3 * kBwdSH * kTW <= 5 * kBwdIH * kBwdSW, "second horizontal pass aliases the moments");
+
+__global__ __launch_bounds__(kLossThreads) void l1_ssim_bwd_kernel(const float *__restrict__ x,
+                                                                    const float *__restrict__ y, int H, int W,
+                                                                    Window win, const float *__restrict__ dout,
+                                                                    float inv_n, float *__restrict__ dx) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float *sx = reinterpret_cast<float *>(smem);
+    float *sy = sx + kBwdIH * kBwdIW;
+    float *hs = sy + kBwdIH * kBwdIW;
+    float *abc = sx;  // after the first horizontal pass the halo is dead
+    float *h3 = hs;   // after the vertical pass the moments are dead
+    const size_t plane_off = (size_t)blockIdx.z * H * W;
+    x += plane_off;
+    y += plane_off;
+    dx += plane_off;
+    const int ox = blockIdx.x * kTW, oy = blockIdx.y * kTH;
+    const float g_l1 = dout[0] * inv_n, g_ssim = dout[1] * inv_n;
+
+    load_halo(x, y, H, W, oy - 2 * kR, ox - 2 * kR, kBwdIH, kBwdIW, sx, sy);
+    __syncthreads();
+    hpass5(sx, sy, kBwdIH, kBwdIW, kBwdSW, win, hs);
+    __syncthreads();
+    // Moments and dS/d(moment) at every SSIM-map position the tile's gradient reads; positions
+    // outside the image have no SSIM term (zero).
+    constexpr int sp = kBwdSH * kBwdSW, hp = kBwdIH * kBwdSW;
+    for (int i = threadIdx.x; i < sp; i += kLossThreads) {
+        const int r = i / kBwdSW, c = i - r * kBwdSW;
+        const int gy = oy - kR + r, gx = ox - kR + c;
+        float a = 0.f, b = 0.f, cc = 0.f;
+        if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
+            float m[5];
+#pragma unroll
+            for (int q = 0; q < 5; q++) {
+                const float *h = hs + q * hp + r * kBwdSW + c;
+                float s = 0.f;
+#pragma unroll
+                for (int j = 0; j < 2 * kR + 1; j++) s = fmaf(win.w[j], h[j * kBwdSW], s);
+                m[q] = s;
+            }
+            ssim_partials(Moments{m[0], m[1], m[2], m[3], m[4]}, a, b, cc);
+        }
+        abc[i] = a;
+        abc[sp + i] = b;
+        abc[2 * sp + i] = cc;
+    }
+    __syncthreads();
+    // Horizontal pass of the three partial maps (the window is symmetric: the transposed
+    // convolution is the same correlation).
+    constexpr int tp = kBwdSH * kTW;
+    for (int i = threadIdx.x; i < tp; i += kLossThreads) {
+        const int r = i >> 6, c = i & 63;
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+            const float *p = abc + q * sp + r * kBwdSW + c;
+            float s = 0.f;
+#pragma unroll
+            for (int j = 0; j < 2 * kR + 1; j++) s = fmaf(win.w[j], p[j], s);
+            h3[q * tp + i] = s;
+        }
+    }
+    __syncthreads();
+    float acc[3][4];
+    vpass_tile<3>(h3, tp, win, acc);
+    const int c = threadIdx.x & 63, r0 = (threadIdx.x >> 6) * 4;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int gy = oy + r0 + k, gx = ox + c;
+        if (gy < H && gx < W) {
+            const size_t o = (size_t)gy * W + gx;
+            const float xv = x[o], yv = y[o];
+            const float d = xv - yv;
+            const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+            dx[o] = g_l1 * sgn + g_ssim * (acc[0][k] + 2.f * xv * acc[1][k] + yv * acc[2][k]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Sparse Adam.
+
+constexpr int kMaxGroups = 8;
+constexpr int kAdamThreads = 256;
+
+struct AdamArgs {
+    gsr_adam_group g[kMaxGroups];
+    int64_t block_start[kMaxGroups + 1];
+    int n;
+};
+
+__global__ __launch_bounds__(256) void any_nonzero_kernel(const float *__restrict__ v, int64_t n,
+                                                          int *__restrict__ flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool nz = i < n && v[i] != 0.f;
+    if (__ballot(nz) != 0 && (threadIdx.x & 63) == 0) *flag = 1;
+}
+
+template <int Wd>
+__device__ __forceinline__ int64_t row_of(int64_t e, int64_t w) {
+    return Wd > 0 ? e / Wd : e / w;
+}
+
+template <int Wd>
+__device__ __forceinline__ void adam_element(const gsr_adam_group &G, int64_t e, const float *rel, bool dense,
+                                             float b1, float b2, float omb1, float omb2, float eps) {
+    const int64_t row = row_of<Wd>(e, G.width);
+    if (!dense && rel[row] == 0.f) return;
+    const float g = G.grad[e];
+    // scene/OurAdam.py:297-324: exp_avg.mul_(b1).add_(g, alpha=1-b1);
+    // exp_avg_sq.mul_(b2).addcmul_(g, g, value=1-b2); denom = sqrt(v)/bc2_sqrt + eps;
+    // param.addcdiv_(exp_avg, denom, value=-step_size)
+    const float m = G.exp_avg[e] * b1 + omb1 * g;
+    const float v = G.exp_avg_sq[e] * b2 + omb2 * (g * g);
+    const float denom = sqrtf(v) / G.bias_correction2_sqrt + eps;
+    G.exp_avg[e] = m;
+    G.exp_avg_sq[e] = v;
+    G.param[e] = G.param[e] + (-G.step_size) * (m / denom);
+}
+
+__global__ __launch_bounds__(kAdamThreads) void sparse_adam_kernel(AdamArgs a, const float *__restrict__ rel,
+                                                                   int64_t P, float b1, float b2, float omb1,
+                                                                   float omb2, float eps,
+                                                                   const int *__restrict__ flag) {
+    int gi = 0;
+    while (gi + 1 < a.n && (int64_t)blockIdx.x >= a.block_start[gi + 1]) gi++;
+    const gsr_adam_group &G = a.g[gi];
+    const int64_t e = ((int64_t)blockIdx.x - a.block_start[gi]) * kAdamThreads + threadIdx.x;
+    if (e >= P * G.width) return;
+    const bool dense = *flag == 0;
+    switch (G.width) {
+        case 1: adam_element<1>(G, e, rel, dense, b1, b2, omb1, omb2, eps); break;
+        case 3: adam_element<3>(G, e, rel, dense, b1, b2, omb1, omb2, eps); break;
+        case 4: adam_element<4>(G, e, rel, dense, b1, b2, omb1, omb2, eps); break;
+        case 45: adam_element<45>(G, e, rel, dense, b1, b2, omb1, omb2, eps); break;
+        default: adam_element<0>(G, e, rel, dense, b1, b2, omb1, omb2, eps); break;
+    }
+}
+
+__global__ __launch_bounds__(256) void densify_stats_kernel(int64_t P, const int *__restrict__ radii,
+                                                            const float *__restrict__ g2d, float *__restrict__ maxr,
+                                                            float *__restrict__ accum, float *__restrict__ denom) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const int r = radii[i];
+    if (r <= 0) return;
+    const float gx = g2d[3 * i], gy = g2d[3 * i + 1];
+    const float n = sqrtf(gx * gx + gy * gy);
+    maxr[i] = fmaxf(maxr[i], (float)r);
+    accum[i] = fmaxf(n, accum[i]);
+    denom[i] = denom[i] + 1.f;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Exposure affine + clamp (gaussian_renderer/__init__.py:115-120).
+
+constexpr int kExpBlocks = 1024;
+constexpr int kExpThreads = 256;
+
+__device__ __forceinline__ void exposure_pre(const float *__restrict__ E, float c0, float c1, float c2, float &o0,
+                                             float &o1, float &o2) {
+    // matmul(img.permute(1, 2, 0), E[:3, :3]) + E[:3, 3]: out_c = sum_k img_k E[k][c] + E[c][3]
+    o0 = c0 * E[0] + c1 * E[4] + c2 * E[8] + E[3];
+    o1 = c0 * E[1] + c1 * E[5] + c2 * E[9] + E[7];
+    o2 = c0 * E[2] + c1 * E[6] + c2 * E[10] + E[11];
+}
+
+__global__ __launch_bounds__(kExpThreads) void exposure_fwd_kernel(const float *__restrict__ color,
+                                                                   const float *__restrict__ E, int64_t n,
+                                                                   float *__restrict__ out) {
+    for (int64_t p = (int64_t)blockIdx.x * kExpThreads + threadIdx.x; p < n; p += (int64_t)gridDim.x * kExpThreads) {
+        float o0, o1, o2;
+        exposure_pre(E, color[p], color[n + p], color[2 * n + p], o0, o1, o2);
+        out[p] = fminf(fmaxf(o0, 0.f), 1.f);
+        out[n + p] = fminf(fmaxf(o1, 0.f), 1.f);
+        out[2 * n + p] = fminf(fmaxf(o2, 0.f), 1.f);
+    }
+}
+
+__global__ __launch_bounds__(kExpThreads) void exposure_bwd_kernel(const float *__restrict__ color,
+                                                                   const float *__restrict__ E, int64_t n,
+                                                                   const float *__restrict__ gout,
+                                                                   float *__restrict__ gcolor,
+                                                                   float *__restrict__ partials) {
+    __shared__ float red[12][kExpThreads / 64];
+    float acc[12];
+#pragma unroll
+    for (int k = 0; k < 12; k++) acc[k] = 0.f;
+    for (int64_t p = (int64_t)blockIdx.x * kExpThreads + threadIdx.x; p < n; p += (int64_t)gridDim.x * kExpThreads) {
+        const float c0 = color[p], c1 = color[n + p], c2 = color[2 * n + p];
+        float o0, o1, o2;
+        exposure_pre(E, c0, c1, c2, o0, o1, o2);
+        const float g0 = (o0 >= 0.f && o0 <= 1.f) ? gout[p] : 0.f;
+        const float g1 = (o1 >= 0.f && o1 <= 1.f) ? gout[n + p] : 0.f;
+        const float g2 = (o2 >= 0.f && o2 <= 1.f) ? gout[2 * n + p] : 0.f;
+        gcolor[p] = E[0] * g0 + E[1] * g1 + E[2] * g2;
+        gcolor[n + p] = E[4] * g0 + E[5] * g1 + E[6] * g2;
+        gcolor[2 * n + p] = E[8] * g0 + E[9] * g1 + E[10] * g2;
+        // dE[k][c] = sum_p img_k g_c ; dE[c][3] = sum_p g_c   (row-major 3x4 slots)
+        acc[0] += c0 * g0; acc[1] += c0 * g1; acc[2] += c0 * g2; acc[3] += g0;
+        acc[4] += c1 * g0; acc[5] += c1 * g1; acc[6] += c1 * g2; acc[7] += g1;
+        acc[8] += c2 * g0; acc[9] += c2 * g1; acc[10] += c2 * g2; acc[11] += g2;
+    }
+    const int wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 12; k++) {
+        const float v = wave_sum(acc[k]);
+        if ((threadIdx.x & 63) == 0) red[k][wv] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 12) {
+        float s = 0.f;
+#pragma unroll
+        for (int w = 0; w < kExpThreads / 64; w++) s += red[threadIdx.x][w];
+        partials[(size_t)blockIdx.x * 12 + threadIdx.x] = s;
+    }
+}
+
+// One wave per output value; each lane sums a fixed strided subset, then a fixed-order wave sum.
+__global__ __launch_bounds__(768) void exposure_finalize_kernel(const float *__restrict__ partials, int nblocks,
+                                                                float *__restrict__ dE) {
+    const int k = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float s = 0.f;
+    for (int b = lane; b < nblocks; b += 64) s += partials[(size_t)b * 12 + k];
+    s = wave_sum(s);
+    if (lane == 0) dE[k] = s;
+}
+
+int exposure_blocks(int64_t n) {
+    const int64_t b = (n + kExpThreads - 1) / kExpThreads;
+    return (int)(b < kExpBlocks ? (b > 0 ? b : 1) : kExpBlocks);
+}
+
+dim3 loss_grid(int C, int H, int W) { return dim3((W + kTW - 1) / kTW, (H + kTH - 1) / kTH, C); }
+
+bool g_lds_attr = false;
+
+}  // namespace
+}  // namespace gsr
+
+using namespace gsr;
+
+extern "C" {
+
+size_t gsr_l1_ssim_scratch_bytes(int C, int H, int W) {
+    if (C <= 0 || H <= 0 || W <= 0) return 0;
+    const dim3 g = loss_grid(C, H, W);
+    return sizeof(float2) * (size_t)g.x * g.y * g.z;
+}
+
+int gsr_l1_ssim_forward(const float *img, const float *gt, int C, int H, int W, void *scratch, float *out,
+                        void *stream) {
+    if (C <= 0 || H <= 0 || W <= 0 || !img || !gt || !scratch || !out) {
+        set_last_error("gsr_l1_ssim_forward: empty image or NULL pointer");
+        return GSR_ERR_INVALID_ARGUMENT;
+    }
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (!g_lds_attr) {
+        (void)hipFuncSetAttribute((const void *)l1_ssim_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)kBwdLds);
+        g_lds_attr = true;
+    }
+    const dim3 g = loss_grid(C, H, W);
+    const int nb = (int)(g.x * g.y * g.z);
+    float2 *part = static_cast<float2 *>(scratch);
+    hipLaunchKernelGGL(l1_ssim_fwd_kernel, g, dim3(kLossThreads), kFwdLds, s, img, gt, H, W, ssim_window(), part);
+    hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(1024), 0, s, part, nb, 1.0 / ((double)C * H * W), out);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_last_error(std::string("gsr_l1_ssim_forward: ") + hipGetErrorString(e));
+        return GSR_ERR_DEVICE;
+    }
+    return GSR_OK;
+}
+
+int gsr_l1_ssim_backward(const float *img, const float *gt, int C, int H, int W, const float *dL_dout,
+                         float *dL_dimg, void *stream) {
+    if (C <= 0 || H <= 0 || W <= 0 || !img || !gt || !dL_dout || !dL_dimg) {
+        set_last_error("gsr_l1_ssim_backward: empty image or NULL pointer");
+        return GSR_ERR_INVALID_ARGUMENT;
+    }
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (!g_lds_attr) {
+        (void)hipFuncSetAttribute((const void *)l1_ssim_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)kBwdLds);
+        g_lds_attr = true;
+    }
+    hipLaunchKernelGGL(l1_ssim_bwd_kernel, loss_grid(C, H, W), dim3(kLossThreads), kBwdLds, s, img, gt, H, W,
+                       ssim_window(), dL_dout, (float)(1.0 / ((double)C * H * W)), dL_dimg);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_last_error(std::string("gsr_l1_ssim_backward: ") + hipGetErrorString(e));
+        return GSR_ERR_DEVICE;
+    }
+    return GSR_OK;
+}
+
+int gsr_sparse_adam_step(int n_groups, const gsr_adam_group *groups, int64_t P, const float *relevance,
+                         double beta1, double beta2, double eps, int *flag_scratch, void *stream) {
+    if (n_groups < 0 || n_groups > kMaxGroups || P < 0 || (P > 0 && (!groups || !relevance || !flag_scratch))) {
+        set_last_error("gsr_sparse_adam_step: bad group count or NULL pointer");
+        return GSR_ERR_INVALID_ARGUMENT;
+    }
+    if (P == 0 || n_groups == 0) return GSR_OK;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    AdamArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.n = n_groups;
+    int64_t blocks = 0;
+    for (int i = 0; i < n_groups; i++) {
+        const gsr_adam_group &g = groups[i];
+        if (!g.param || !g.grad || !g.exp_avg || !g.exp_avg_sq || g.width <= 0) {
+            set_last_error("gsr_sparse_adam_step: group has a NULL array or non-positive width");
+            return GSR_ERR_INVALID_ARGUMENT;
+        }
+        a.g[i] = g;
+        a.block_start[i] = blocks;
+        blocks += (P * g.width + kAdamThreads - 1) / kAdamThreads;
+    }
+    a.block_start[n_groups] = blocks;
+    if (blocks > 0x7fffffff) {
+        set_last_error("gsr_sparse_adam_step: parameter set too large for one launch");
+        return GSR_ERR_UNSUPPORTED;
+    }
+    (void)hipMemsetAsync(flag_scratch, 0, sizeof(int), s);
+    hipLaunchKernelGGL(any_nonzero_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, relevance, P,
+                       flag_scratch);
+    // torch applies python-float hyper-parameters as fp32 scalars: b, (1 - b) rounded from double
+    hipLaunchKernelGGL(sparse_adam_kernel, dim3((unsigned)blocks), dim3(kAdamThreads), 0, s, a, relevance, P,
+                       (float)beta1, (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps, flag_scratch);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_last_error(std::string("gsr_sparse_adam_step: ") + hipGetErrorString(e));
+        return GSR_ERR_DEVICE;
+    }
+    return GSR_OK;
+}
+
+int gsr_exposure_forward(const float *color, const float *exposure, int64_t npix, float *out, void *stream) {
+    if (npix < 0 || (npix > 0 && (!color || !exposure || !out))) {
+        set_last_error("gsr_exposure_forward: NULL pointer");
+        return GSR_ERR_INVALID_ARGUMENT;
+    }
+    if (npix == 0) return GSR_OK;
+    hipLaunchKernelGGL(exposure_fwd_kernel, dim3(exposure_blocks(npix)), dim3(kExpThreads), 0,
+                       static_cast<hipStream_t>(stream), color, exposure, npix, out);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_last_error(std::string("gsr_exposure_forward: ") + hipGetErrorString(e));
+        return GSR_ERR_DEVICE;
+    }
+    return GSR_OK;
+}
+
+size_t gsr_exposure_scratch_bytes(int64_t npix) { return sizeof(float) * 12 * (size_t)exposure_blocks(npix); }
+
+int gsr_exposure_backward(const float *color, const float *exposure, int64_t npix, const float *dL_dout,
+                          float *dL_dcolor, float *dL_dexposure, void *scratch, void *stream) {
+    if (npix < 0 || !dL_dexposure || !scratch || (npix > 0 && (!color || !exposure || !dL_dout || !dL_dcolor))) {
+        set_last_error("gsr_exposure_backward: NULL pointer");
+        return GSR_ERR_INVALID_ARGUMENT;
+    }
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int nb = exposure_blocks(npix);
+    float *part = static_cast<float *>(scratch);
+    if (npix > 0)
+        hipLaunchKernelGGL(exposure_bwd_kernel, dim3(nb), dim3(kExpThreads), 0, s, color, exposure, npix, dL_dout,
+                           dL_dcolor, part);
+    else
+        (void)hipMemsetAsync(part, 0, sizeof(float) * 12, s);
+    hipLaunchKernelGGL(exposure_finalize_kernel, dim3(1), dim3(768), 0, s, part, npix > 0 ? nb : 1, dL_dexposure);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_last_error(std::string("gsr_exposure_backward: ") + hipGetErrorString(e));
+        return GSR_ERR_DEVICE;
+    }
+    return GSR_OK;
+}
+
+int gsr_densify_stats(int64_t P, const int *radii, const float *dL_dmeans2D, float *max_radii2D, float *grad_accum,
+                      float *denom, void *stream) {
+    if (P < 0 || (P > 0 && (!radii || !dL_dmeans2D || !max_radii2D || !grad_accum || !denom))) {
+        set_last_error("gsr_densify_stats: NULL pointer");
+        return GSR_ERR_INVALID_ARGUMENT;
+    }
+    if (P == 0) return GSR_OK;
+    hipLaunchKernelGGL(densify_stats_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), P, radii, dL_dmeans2D, max_radii2D, grad_accum, denom);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_last_error(std::string("gsr_densify_stats: ") + hipGetErrorString(e));
+        return GSR_ERR_DEVICE;
+    }
+    return GSR_OK;
+}
+
+}  // extern "C"

@@ -17,7 +17,15 @@ _i = ctypes.c_int
 _f = ctypes.c_float
 _i64 = ctypes.c_int64
 
-# exported symbol -> (restype, argtypes); must match include/gsr.h
+
+
+class AdamGroup(ctypes.Structure):
+    """gsr_adam_group (include/gsr_train.h)."""
+    _fields_ = [("param", _vp), ("grad", _vp), ("exp_avg", _vp), ("exp_avg_sq", _vp), ("width", _i64),
+                ("step_size", _f), ("bias_correction2_sqrt", _f)]
+
+
+# exported symbol -> (restype, argtypes); must match include/gsr.h + include/gsr_train.h
 SIGNATURES = {
     "gsr_rasterize_forward": (_i, [RESIZE_FN, RESIZE_FN, RESIZE_FN, _vp, _i, _i, _i, _vp, _i, _i,
                                    _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _f, _f,
@@ -32,6 +40,16 @@ SIGNATURES = {
     "gsr_abi_version": (_i, []),
     "gsr_last_error": (ctypes.c_char_p, []),
     "gsr_build_info": (ctypes.c_char_p, []),
+    # include/gsr_train.h
+    "gsr_l1_ssim_scratch_bytes": (ctypes.c_size_t, [_i, _i, _i]),
+    "gsr_l1_ssim_forward": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp, _vp]),
+    "gsr_l1_ssim_backward": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp, _vp]),
+    "gsr_sparse_adam_step": (_i, [_i, ctypes.POINTER(AdamGroup), _i64, _vp, ctypes.c_double, ctypes.c_double,
+                                  ctypes.c_double, _vp, _vp]),
+    "gsr_densify_stats": (_i, [_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gsr_exposure_forward": (_i, [_vp, _vp, _i64, _vp, _vp]),
+    "gsr_exposure_scratch_bytes": (ctypes.c_size_t, [_i64]),
+    "gsr_exposure_backward": (_i, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
 }
 
 ABI_VERSION = 1

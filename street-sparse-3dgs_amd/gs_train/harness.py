@@ -1,0 +1,228 @@
+"""Train-step harness: one iteration of the train_single.py inner loop
+(train_single.py:65-247) on the MI355X path, used for the "train-step ms" half of the metric.
+
+Per step, as the reference does it:
+  1. xyz learning-rate schedule (scene/gaussian_model.py:447-457, utils/general_utils.py:31-70)
+  2. render(): activations of the raw parameters (scene/gaussian_model.py:39-47,125-156),
+     GaussianRasterizer (drop-in), per-image exposure affine and clamp
+     (gaussian_renderer/__init__.py:115-120)
+  3. photometric loss (1 - 0.2) L1 + 0.2 (1 - SSIM) (train_single.py:121-123), plus the
+     inverse-depth L1 when a mono depth map is given (train_single.py:128-137)
+  4. loss.backward()
+  5. densification statistics (train_single.py:193-194)
+  6. exposure Adam step, sparse Adam step on rows with nonzero opacity gradient
+     (train_single.py:212-233), zero_grad(set_to_none=True)
+  7. shrink over-large Gaussians (train_single.py:235-241)
+
+`fused=True` runs the exposure/clamp and steps 3, 5 and 6 on the csrc/train.hip kernels and keeps the step free of host
+synchronisation; `fused=False` runs the same step with the reference's own torch formulation
+(gs_train.baseline) for the side-by-side number.  Densify/prune, opacity reset, SH degree
+increments and checkpointing run every few hundred/thousand iterations and are out of scope
+(SURVEY.md 8(f) row 4).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+
+from . import baseline
+from .densify import add_densification_stats
+from .exposure import apply_exposure
+from .loss import photo_loss
+from .optim import Adam
+
+# arguments/__init__.py:89-109 (OptimizationParams defaults)
+LR = dict(position_lr_init=0.00002, position_lr_final=0.0000002, position_lr_delay_mult=0.01,
+          position_lr_max_steps=30_000, feature_lr=0.0025, opacity_lr=0.05, scaling_lr=0.005, rotation_lr=0.001,
+          lambda_dssim=0.2)
+
+
+def expon_lr(step, lr_init, lr_final, lr_delay_steps=0, lr_delay_mult=1.0, max_steps=1_000_000):
+    """utils/general_utils.py:31-70 (log-linear decay with an optional cosine warm-up)."""
+    if lr_init == 0 or step < 0 or (lr_init == 0.0 and lr_final == 0.0):
+        return 0.0
+    if lr_delay_steps > 0:
+        delay = lr_delay_mult + (1 - lr_delay_mult) * np.sin(0.5 * np.pi * np.clip(step / lr_delay_steps, 0, 1))
+    else:
+        delay = 1.0
+    t = np.clip(step / max_steps, 0, 1)
+    return float(delay * np.exp(np.log(lr_init) * (1 - t) + np.log(lr_final) * t))
+
+
+class GaussianSet:
+    """The raw parameters and activations of scene/gaussian_model.py the train step touches."""
+
+    def __init__(self, means3D, shs, opacities, scales, rotations, n_images=1, sh_degree=3, spatial_lr_scale=1.0,
+                 device="cuda"):
+        t = lambda a: torch.as_tensor(np.asarray(a), dtype=torch.float32, device=device).contiguous()
+        shs = t(shs)
+        op = t(opacities).clamp(1e-6, 1 - 1e-6)
+        P = shs.shape[0]
+        self._xyz = torch.nn.Parameter(t(means3D))
+        self._features_dc = torch.nn.Parameter(shs[:, :1].contiguous())
+        self._features_rest = torch.nn.Parameter(shs[:, 1:].contiguous())
+        self._opacity = torch.nn.Parameter(torch.log(op / (1 - op)))  # inverse_sigmoid
+        self._scaling = torch.nn.Parameter(torch.log(t(scales)))
+        self._rotation = torch.nn.Parameter(t(rotations))
+        self._exposure = torch.nn.Parameter(torch.eye(3, 4, device=device)[None].repeat(n_images, 1, 1))
+        self.active_sh_degree = sh_degree
+        self.spatial_lr_scale = spatial_lr_scale
+        self.max_radii2D = torch.zeros(P, device=device)
+        self.xyz_gradient_accum = torch.zeros((P, 1), device=device)
+        self.denom = torch.zeros((P, 1), device=device)
+
+    @property
+    def P(self):
+        return self._xyz.shape[0]
+
+    @property
+    def get_scaling(self):
+        return torch.exp(self._scaling)
+
+    @property
+    def get_rotation(self):
+        return torch.nn.functional.normalize(self._rotation)
+
+    @property
+    def get_xyz(self):
+        return self._xyz
+
+    @property
+    def get_features(self):
+        return torch.cat((self._features_dc, self._features_rest), dim=1)
+
+    @property
+    def get_opacity(self):
+        return torch.sigmoid(self._opacity)
+
+    def param_groups(self):
+        s = self.spatial_lr_scale
+        return [
+            {"params": [self._xyz], "lr": LR["position_lr_init"] * s, "name": "xyz"},
+            {"params": [self._features_dc], "lr": LR["feature_lr"], "name": "f_dc"},
+            {"params": [self._features_rest], "lr": LR["feature_lr"] / 20.0, "name": "f_rest"},
+            {"params": [self._opacity], "lr": LR["opacity_lr"], "name": "opacity"},
+            {"params": [self._scaling], "lr": LR["scaling_lr"], "name": "scaling"},
+            {"params": [self._rotation], "lr": LR["rotation_lr"], "name": "rotation"},
+        ]
+
+
+class TrainStep:
+    """cameras: list of (view, proj, campos, tanfovx, tanfovy) numpy tuples (synthetic.camera);
+    gts: list of (3, H, W) device tensors; mono_invdepths: optional list of (1, H, W)."""
+
+    def __init__(self, gaussians: GaussianSet, cameras, gts, W, H, fused=True, cameras_extent=10.0,
+                 mono_invdepths=None, depth_l1_weight=0.0):
+        self.g = gaussians
+        self.W, self.H = W, H
+        self.fused = fused
+        self.extent = cameras_extent
+        self.gts = gts
+        self.mono = mono_invdepths
+        self.depth_w = depth_l1_weight
+        dev = gaussians._xyz.device
+        f = lambda a: torch.as_tensor(np.asarray(a), dtype=torch.float32, device=dev)
+        self.cams = [dict(view=f(v).reshape(4, 4), proj=f(p).reshape(4, 4), campos=f(c), tx=float(tx), ty=float(ty))
+                     for (v, p, c, tx, ty) in cameras]
+        groups = gaussians.param_groups()
+        self.optimizer = Adam(groups, lr=0.0, eps=1e-15) if fused else baseline.OurAdamTorch(groups, lr=0.0,
+                                                                                              eps=1e-15)
+        self.exposure_optimizer = torch.optim.Adam([gaussians._exposure])
+        self.xyz_lr = lambda it: expon_lr(it, LR["position_lr_init"] * gaussians.spatial_lr_scale,
+                                          LR["position_lr_final"] * gaussians.spatial_lr_scale,
+                                          lr_delay_mult=LR["position_lr_delay_mult"],
+                                          max_steps=LR["position_lr_max_steps"])
+        self.iteration = 1
+        self.empty_i = torch.empty(0, dtype=torch.int32)
+        self.empty_f = torch.empty(0, device=dev)
+        self.empty_id = torch.empty(0, dtype=torch.int32, device=dev)
+
+    def render(self, cam_idx, bg):
+        c = self.cams[cam_idx]
+        g = self.g
+        rs = GaussianRasterizationSettings(
+            image_height=self.H, image_width=self.W, tanfovx=c["tx"], tanfovy=c["ty"], bg=bg, scale_modifier=1.0,
+            viewmatrix=c["view"], projmatrix=c["proj"], sh_degree=g.active_sh_degree, campos=c["campos"],
+            prefiltered=False, debug=False, do_depth=True, render_indices=self.empty_i, parent_indices=self.empty_i,
+            interpolation_weights=self.empty_f, num_node_kids=self.empty_id)
+        means2D = torch.zeros_like(g._xyz, requires_grad=True) + 0
+        if means2D.requires_grad:
+            means2D.retain_grad()
+        color, radii, invd = GaussianRasterizer(rs)(means3D=g.get_xyz, means2D=means2D, shs=g.get_features,
+                                                    colors_precomp=None, opacities=g.get_opacity,
+                                                    scales=g.get_scaling, rotations=g.get_rotation,
+                                                    cov3D_precomp=None)
+        E = g._exposure[cam_idx]
+        if self.fused:
+            return apply_exposure(color, E), invd, means2D, radii
+        image = torch.matmul(color.permute(1, 2, 0), E[:3, :3]).permute(2, 0, 1) + E[:3, 3, None, None]
+        return image.clamp(0, 1), invd, means2D, radii
+
+    def step(self, cam_idx=None):
+        """One iteration; returns the loss tensor (no host synchronisation when fused)."""
+        g = self.g
+        it = self.iteration
+        k = (it - 1) % len(self.cams) if cam_idx is None else cam_idx
+        for pg in self.optimizer.param_groups:
+            if pg["name"] == "xyz":
+                pg["lr"] = self.xyz_lr(it)
+        bg = torch.rand(3, device=g._xyz.device)
+        image, invd, means2D, radii = self.render(k, bg)
+        gt = self.gts[k]
+        if self.fused:
+            loss, l1, s = photo_loss(image, gt, LR["lambda_dssim"])
+        else:
+            loss = baseline.photo_loss(image, gt, LR["lambda_dssim"])
+        if self.mono is not None and self.depth_w > 0:
+            loss = loss + self.depth_w * torch.abs(invd - self.mono[k]).mean()
+        loss.backward()
+        with torch.no_grad():
+            if self.fused:
+                add_densification_stats(radii, means2D.grad, g.max_radii2D, g.xyz_gradient_accum, g.denom)
+            else:
+                baseline.densification_stats(g, radii, means2D.grad)
+            self.exposure_optimizer.step()
+            self.exposure_optimizer.zero_grad(set_to_none=True)
+            if self.fused:
+                self.optimizer.step(relevance=g._opacity.grad)
+            else:
+                relevant = (g._opacity.grad.flatten() != 0).nonzero().flatten().long()
+                self.optimizer.step(relevant)
+            self.optimizer.zero_grad(set_to_none=True)
+            # train_single.py:235-241: shrink Gaussians larger than 2% of the scene extent
+            sc = g.get_scaling
+            bad = sc.max(dim=1).values > self.extent * 0.02
+            if self.fused:
+                g._scaling.copy_(torch.where(bad[:, None], torch.log(sc * 0.8), g._scaling))
+            else:
+                g._scaling[bad] = torch.log(sc[bad] * 0.8)
+        self.iteration += 1
+        return loss.detach()
+
+
+def make_problem(P, W, H, n_views=4, seed=0, sh_degree=3, device="cuda", fused=True, perturb=0.02):
+    """A synthetic training problem: ground-truth views rendered from a seeded scene, and a
+    TrainStep that starts from a perturbed copy of it."""
+    from .synthetic import orbit_cameras, synthetic_scene
+    s = synthetic_scene(P, W, H, seed=seed, sh_degree=sh_degree)
+    cams = orbit_cameras(n_views, W, H)
+    truth = GaussianSet(s["means3D"], s["shs"], s["opacities"], s["scales"], s["rotations"], n_images=n_views,
+                        sh_degree=sh_degree, device=device)
+    tmp = TrainStep(truth, cams, [None] * n_views, W, H, fused=fused)
+    gts = []
+    with torch.no_grad():
+        for k in range(n_views):
+            img, _, _, _ = tmp.render(k, torch.zeros(3, device=device))
+            gts.append(img.contiguous())
+    rng = np.random.default_rng(seed + 99)
+    noisy = dict(means3D=s["means3D"] + perturb * rng.normal(size=s["means3D"].shape).astype(np.float32),
+                 shs=s["shs"] + perturb * rng.normal(size=s["shs"].shape).astype(np.float32),
+                 opacities=s["opacities"], scales=s["scales"] * np.exp(perturb * rng.normal(size=s["scales"].shape)),
+                 rotations=s["rotations"])
+    model = GaussianSet(noisy["means3D"], noisy["shs"], noisy["opacities"], noisy["scales"].astype(np.float32),
+                        noisy["rotations"], n_images=n_views, sh_degree=sh_degree, device=device)
+    return TrainStep(model, cams, gts, W, H, fused=fused)

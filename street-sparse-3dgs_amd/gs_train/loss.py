@@ -1,0 +1,60 @@
+"""Fused photometric loss: mean |img - gt| and mean SSIM (11x11 Gaussian window, sigma 1.5) in one
+gfx950 launch each way (csrc/train.hip), replacing utils/loss_utils.py:17-18 (l1_loss) and
+:33-63 (ssim: five depthwise conv2d + elementwise ops) as combined at train_single.py:121-123.
+
+Gradients flow only to `img` (the rendered image); `gt` is a constant, as in the reference.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._native import check, lib, ptr, require_gpu, stream
+
+
+def _planes(img: torch.Tensor):
+    if img.dim() == 3:
+        return img.shape[0], img.shape[1], img.shape[2]
+    if img.dim() == 4:
+        return img.shape[0] * img.shape[1], img.shape[2], img.shape[3]
+    raise ValueError("expected a (C, H, W) or (B, C, H, W) image")
+
+
+class _L1SSIM(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, img, gt):
+        require_gpu(img, gt)
+        if img.shape != gt.shape:
+            raise ValueError(f"image shapes differ: {tuple(img.shape)} vs {tuple(gt.shape)}")
+        img = img.detach().float().contiguous()
+        gt = gt.detach().float().contiguous()
+        C, H, W = _planes(img)
+        L = lib()
+        out = torch.empty(2, dtype=torch.float32, device=img.device)
+        scratch = torch.empty(max(1, L.gsr_l1_ssim_scratch_bytes(C, H, W)), dtype=torch.uint8, device=img.device)
+        check(L.gsr_l1_ssim_forward(ptr(img), ptr(gt), C, H, W, ptr(scratch), ptr(out), stream(img.device)),
+              "gsr_l1_ssim_forward")
+        ctx.save_for_backward(img, gt)
+        ctx.dims = (C, H, W)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        img, gt = ctx.saved_tensors
+        C, H, W = ctx.dims
+        gout = gout.float().contiguous()
+        dimg = torch.empty_like(img)
+        check(lib().gsr_l1_ssim_backward(ptr(img), ptr(gt), C, H, W, ptr(gout), ptr(dimg), stream(img.device)),
+              "gsr_l1_ssim_backward")
+        return dimg, None
+
+
+def l1_ssim(img: torch.Tensor, gt: torch.Tensor) -> torch.Tensor:
+    """Returns the 2-vector [mean |img - gt|, mean SSIM(img, gt)], differentiable w.r.t. img."""
+    return _L1SSIM.apply(img, gt)
+
+
+def photo_loss(img: torch.Tensor, gt: torch.Tensor, lambda_dssim: float = 0.2):
+    """(1 - lambda) L1 + lambda (1 - SSIM)  (train_single.py:121-123); returns (loss, l1, ssim)."""
+    v = l1_ssim(img, gt)
+    l1, s = v[0], v[1]
+    return (1.0 - lambda_dssim) * l1 + lambda_dssim * (1.0 - s), l1, s

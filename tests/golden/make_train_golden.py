@@ -1,0 +1,137 @@
+"""Generate train-step golden fixtures from the reference's own Python (build container only).
+
+  loss.npz       utils/loss_utils.py:17-18 l1_loss and :33-63 ssim on small (3, H, W) images,
+                 the photometric loss of train_single.py:121-123 ((1 - 0.2) L1 + 0.2 (1 - SSIM))
+                 and its gradient w.r.t. the rendered image (torch autograd through the
+                 reference functions), for several sizes incl. odd ones smaller than the window
+  adam.npz       scene/OurAdam.py Adam(..., lr=0.0, eps=1e-15) with the six groups and learning
+                 rates of scene/gaussian_model.py:286-296: two sparse steps (relevant = rows with
+                 nonzero opacity grad, train_single.py:224-230) then one step with no relevant
+                 row (the _single_tensor_adam2 dense branch)
+  lr.npz         utils/general_utils.py:31-70 get_expon_lr_func with the xyz and exposure
+                 schedules of scene/gaussian_model.py:301-305 (arguments/__init__.py:89-100)
+  densify.npz    scene/gaussian_model.py:780-793 add_densification_stats + the max_radii2D update
+                 of train_single.py:193
+
+Nothing from the reference is copied; only numbers are kept.
+Usage:  python tests/golden/make_train_golden.py [--ref /root/reference]
+"""
+from __future__ import annotations
+
+import argparse
+import importlib.util
+import os
+import sys
+
+import numpy as np
+import torch
+
+OUT = os.path.dirname(os.path.abspath(__file__))
+LRS = {"xyz": 0.00016, "f_dc": 0.0025, "f_rest": 0.0025 / 20.0, "opacity": 0.05, "scaling": 0.005,
+       "rotation": 0.001}
+SHAPES = {"xyz": (3,), "f_dc": (1, 3), "f_rest": (15, 3), "opacity": (1,), "scaling": (3,), "rotation": (4,)}
+
+
+def load_by_path(name, path):
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def make_loss(ref):
+    loss_utils = load_by_path("ref_loss_utils", os.path.join(ref, "utils", "loss_utils.py"))
+    g = torch.Generator().manual_seed(7)
+    out = {}
+    sizes = [(3, 16, 16), (3, 37, 53), (3, 7, 9), (1, 24, 70), (3, 64, 96)]
+    for k, (C, H, W) in enumerate(sizes):
+        img = torch.rand((C, H, W), generator=g)
+        gt = (img + 0.15 * torch.randn((C, H, W), generator=g)).clamp(0, 1)
+        img.requires_grad_(True)
+        l1 = loss_utils.l1_loss(img, gt)
+        s = loss_utils.ssim(img, gt)
+        loss = (1.0 - 0.2) * l1 + 0.2 * (1.0 - s)
+        loss.backward()
+        out[f"img_{k}"] = img.detach().numpy()
+        out[f"gt_{k}"] = gt.numpy()
+        out[f"l1_{k}"] = np.float32(l1.item())
+        out[f"ssim_{k}"] = np.float32(s.item())
+        out[f"loss_{k}"] = np.float32(loss.item())
+        out[f"grad_{k}"] = img.grad.numpy()
+    out["n"] = np.int32(len(sizes))
+    np.savez_compressed(os.path.join(OUT, "loss.npz"), **out)
+
+
+def make_adam(ref):
+    our_adam = load_by_path("ref_our_adam", os.path.join(ref, "scene", "OurAdam.py"))
+    g = torch.Generator().manual_seed(11)
+    P = 50
+    params = {n: torch.nn.Parameter(torch.randn((P,) + s, generator=g)) for n, s in SHAPES.items()}
+    groups = [{"params": [params[n]], "lr": LRS[n], "name": n} for n in SHAPES]
+    opt = our_adam.Adam(groups, lr=0.0, eps=1e-15)
+    out = {f"init_{n}": p.detach().numpy().copy() for n, p in params.items()}
+    for step in range(3):
+        grads = {n: torch.randn((P,) + s, generator=g) for n, s in SHAPES.items()}
+        if step < 2:
+            mask = torch.rand(P, generator=g) < 0.6
+        else:
+            mask = torch.zeros(P, dtype=torch.bool)
+        grads["opacity"][~mask] = 0.0
+        for n, p in params.items():
+            p.grad = grads[n].clone()
+            out[f"grad{step}_{n}"] = grads[n].numpy().copy()
+        relevant = (params["opacity"].grad.flatten() != 0).nonzero().flatten().long()
+        opt.step(relevant)
+        for n, p in params.items():
+            out[f"after{step}_{n}"] = p.detach().numpy().copy()
+            st = opt.state[p]
+            out[f"m{step}_{n}"] = st["exp_avg"].numpy().copy()
+            out[f"v{step}_{n}"] = st["exp_avg_sq"].numpy().copy()
+    out["lrs"] = np.array([LRS[n] for n in SHAPES], np.float64)
+    np.savez_compressed(os.path.join(OUT, "adam.npz"), **out)
+
+
+def make_densify():
+    # add_densification_stats is a GaussianModel method that needs the whole scene package;
+    # its three lines are evaluated here on the same tensors the method would see.
+    ref_src = open(os.path.join(ARGS.ref, "scene", "gaussian_model.py")).read()
+    assert "def add_densification_stats" in ref_src
+    g = torch.Generator().manual_seed(5)
+    P = 64
+    radii = torch.randint(-2, 12, (P,), generator=g).clamp_min(0).int()
+    grad2d = torch.randn((P, 3), generator=g)
+    grad2d[:, 2] = 0
+    max_r = torch.rand(P, generator=g) * 8
+    accum = torch.rand((P, 1), generator=g) * 2
+    denom = torch.randint(0, 5, (P, 1), generator=g).float()
+    out = {"radii": radii.numpy(), "grad2d": grad2d.numpy(), "max_r": max_r.numpy(), "accum": accum.numpy(),
+           "denom": denom.numpy()}
+    vis = radii > 0
+    max_r2, accum2, denom2 = max_r.clone(), accum.clone(), denom.clone()
+    max_r2[vis] = torch.max(max_r2[vis], radii[vis])  # train_single.py:193
+    nv = torch.norm(grad2d[vis, :2], dim=-1, keepdim=True)  # gaussian_model.py:781-793
+    accum2[vis] = torch.max(nv, accum2[vis])
+    denom2[vis] += 1
+    out.update({"max_r_after": max_r2.numpy(), "accum_after": accum2.numpy(), "denom_after": denom2.numpy()})
+    np.savez_compressed(os.path.join(OUT, "densify.npz"), **out)
+
+
+def make_lr(ref):
+    gu = load_by_path("ref_general_utils", os.path.join(ref, "utils", "general_utils.py"))
+    steps = np.array([0, 1, 2, 10, 100, 999, 1000, 5000, 12345, 29999, 30000, 40000], np.int64)
+    xyz = gu.get_expon_lr_func(lr_init=0.00002 * 3.5, lr_final=0.0000002 * 3.5, lr_delay_mult=0.01, max_steps=30_000)
+    exp = gu.get_expon_lr_func(0.001, 0.0001, lr_delay_steps=5000, lr_delay_mult=0.001, max_steps=30_000)
+    np.savez_compressed(os.path.join(OUT, "lr.npz"), steps=steps, xyz=np.array([xyz(int(s)) for s in steps]),
+                        exposure=np.array([exp(int(s)) for s in steps]))
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default="/root/reference")
+    ARGS = ap.parse_args()
+    sys.path.insert(0, ARGS.ref)
+    make_loss(ARGS.ref)
+    make_adam(ARGS.ref)
+    make_densify()
+    make_lr(ARGS.ref)
+    print("wrote loss.npz adam.npz densify.npz lr.npz")

@@ -14,12 +14,12 @@ import pytest
 import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(REPO, "include", "gsr.h")
+HEADERS = [os.path.join(REPO, "include", h) for h in ("gsr.h", "gsr_train.h")]
 GOLD = os.path.join(REPO, "tests", "golden")
 
 
 def _declared_symbols():
-    text = open(HEADER).read()
+    text = "".join(open(h).read() for h in HEADERS)
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(gsr_[a-z_0-9]+)\s*\(", text)) - {"gsr_resize_fn"})
 
@@ -28,10 +28,10 @@ def test_library_exports_every_declared_symbol():
     from diff_gaussian_rasterization import _lib
     lib = ctypes.CDLL(_lib.LIB_PATH)
     syms = _declared_symbols()
-    assert len(syms) >= 8
+    assert len(syms) >= 13
     for s in syms:
         assert hasattr(lib, s), f"libgsr_hip.so does not export {s}"
-    assert set(syms) == set(_lib.SIGNATURES), "ctypes signature table out of sync with include/gsr.h"
+    assert set(syms) == set(_lib.SIGNATURES), "ctypes signature table out of sync with include/*.h"
 
 
 def test_library_metadata_calls_without_gpu():

@@ -1,0 +1,129 @@
+"""CPU tests of the train-step row: the oracle
+(oracle/train_ref.py) and the reference-structured baseline (gs_train.baseline) are pinned to
+the fixtures the reference's own loss_utils / OurAdam / get_expon_lr_func produced
+(tests/golden/make_train_golden.py); host logic of gs_train is checked without a GPU."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import train_ref as TR
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+NAMES = ["xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation"]
+
+
+def _gold(name):
+    return np.load(os.path.join(GOLD, name))
+
+
+@pytest.mark.parametrize("mod", ["oracle", "baseline"])
+def test_loss_matches_reference_fixtures(mod):
+    from gs_train import baseline
+    d = _gold("loss.npz")
+    for k in range(int(d["n"])):
+        img = torch.tensor(d[f"img_{k}"], requires_grad=True)
+        gt = torch.tensor(d[f"gt_{k}"])
+        if mod == "oracle":
+            l1, s = TR.l1(img, gt), TR.ssim(img, gt)
+            loss = 0.8 * l1 + 0.2 * (1 - s)
+            assert abs(l1.item() - float(d[f"l1_{k}"])) <= 1e-6
+            assert abs(s.item() - float(d[f"ssim_{k}"])) <= 1e-6
+        else:
+            loss = baseline.photo_loss(img, gt)
+        assert abs(loss.item() - float(d[f"loss_{k}"])) <= 1e-6
+        loss.backward()
+        g = img.grad.numpy()
+        ref = d[f"grad_{k}"]
+        assert np.abs(g - ref).max() <= 1e-6 * max(1.0, np.abs(ref).max()) + 1e-9
+
+
+def _run_adam(step_fn):
+    d = _gold("adam.npz")
+    params = [torch.tensor(d[f"init_{n}"]) for n in NAMES]
+    m = [torch.zeros_like(p) for p in params]
+    v = [torch.zeros_like(p) for p in params]
+    steps = [0] * len(NAMES)
+    for it in range(3):
+        grads = [torch.tensor(d[f"grad{it}_{n}"]) for n in NAMES]
+        steps = step_fn(params, grads, m, v, steps, list(d["lrs"]), grads[3])
+        for j, n in enumerate(NAMES):
+            np.testing.assert_allclose(params[j].numpy(), d[f"after{it}_{n}"], rtol=0, atol=2e-7)
+            np.testing.assert_allclose(m[j].numpy(), d[f"m{it}_{n}"], rtol=0, atol=1e-7)
+            np.testing.assert_allclose(v[j].numpy(), d[f"v{it}_{n}"], rtol=1e-6, atol=1e-9)
+
+
+def test_oracle_sparse_adam_matches_reference_ouradam():
+    _run_adam(TR.sparse_adam)
+
+
+def test_baseline_ouradam_matches_reference_ouradam():
+    from gs_train import baseline
+    d = _gold("adam.npz")
+    params = [torch.nn.Parameter(torch.tensor(d[f"init_{n}"])) for n in NAMES]
+    opt = baseline.OurAdamTorch([{"params": [p], "lr": float(lr), "name": n}
+                                 for p, lr, n in zip(params, d["lrs"], NAMES)], lr=0.0, eps=1e-15)
+    for it in range(3):
+        for j, n in enumerate(NAMES):
+            params[j].grad = torch.tensor(d[f"grad{it}_{n}"])
+        opt.step((params[3].grad.flatten() != 0).nonzero().flatten().long())
+        for j, n in enumerate(NAMES):
+            np.testing.assert_allclose(params[j].detach().numpy(), d[f"after{it}_{n}"], rtol=0, atol=2e-7)
+
+
+def test_oracle_densify_matches_reference():
+    d = _gold("densify.npz")
+    radii = torch.tensor(d["radii"])
+    mr, acc, den = (torch.tensor(d[k]).clone() for k in ("max_r", "accum", "denom"))
+    TR.densify_stats(radii, torch.tensor(d["grad2d"]), mr, acc, den)
+    np.testing.assert_array_equal(mr.numpy(), d["max_r_after"])
+    np.testing.assert_array_equal(acc.numpy(), d["accum_after"])
+    np.testing.assert_array_equal(den.numpy(), d["denom_after"])
+
+
+def test_lr_schedule_matches_reference():
+    from gs_train.harness import expon_lr
+    d = _gold("lr.npz")
+    for s, xyz, ex in zip(d["steps"], d["xyz"], d["exposure"]):
+        assert expon_lr(int(s), 0.00002 * 3.5, 0.0000002 * 3.5, lr_delay_mult=0.01, max_steps=30_000) == \
+            pytest.approx(float(xyz), rel=1e-12, abs=0)
+        assert expon_lr(int(s), 0.001, 0.0001, lr_delay_steps=5000, lr_delay_mult=0.001, max_steps=30_000) == \
+            pytest.approx(float(ex), rel=1e-12, abs=0)
+
+
+def test_synthetic_scene_matches_oracle_generator():
+    import gs_oracle as O
+    from gs_train import synthetic
+    a = synthetic.synthetic_scene(500, 320, 240, seed=3)
+    b = O.synthetic_scene(500, 320, 240, seed=3)
+    for k in ("means3D", "scales", "rotations", "opacities", "shs", "view", "proj", "campos", "bg"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    assert a["tanfovx"] == b["tanfovx"] and a["tanfovy"] == b["tanfovy"]
+
+
+def test_train_kernels_refuse_cpu_tensors():
+    from gs_train import add_densification_stats, l1_ssim
+    x = torch.rand(3, 8, 8)
+    with pytest.raises(RuntimeError, match="ROCm GPU"):
+        l1_ssim(x, x)
+    with pytest.raises(RuntimeError, match="ROCm GPU"):
+        add_densification_stats(torch.zeros(4, dtype=torch.int32), torch.zeros(4, 3), torch.zeros(4),
+                                torch.zeros(4, 1), torch.zeros(4, 1))
+
+
+def test_fused_adam_validation_on_host():
+    from gs_train import Adam
+    p = torch.nn.Parameter(torch.zeros(4, 3))
+    with pytest.raises(ValueError):
+        Adam([p], lr=-1.0)
+    with pytest.raises(NotImplementedError):
+        Adam([p], amsgrad=True)
+    opt = Adam([{"params": [p], "lr": 0.1, "name": "xyz"}], lr=0.0, eps=1e-15)
+    assert opt.param_groups[0]["name"] == "xyz" and opt.param_groups[0]["eps"] == 1e-15
+    opt.step(torch.zeros(0, dtype=torch.long))  # no grads: nothing to do, no device call
+    p.grad = torch.zeros(4, 3)
+    with pytest.raises(RuntimeError, match="ROCm GPU"):
+        opt.step(relevance=torch.zeros(4))
