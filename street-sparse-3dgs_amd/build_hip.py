@@ -38,10 +38,10 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def _compile(src, force):
-    obj = os.path.join(OBJ, os.path.basename(src) + ".o")
+def _compile(src, force, objdir=OBJ, defines=()):
+    obj = os.path.join(objdir, os.path.basename(src) + ".o")
     if force or _stale(obj, [src] + _headers()):
-        cmd = [HIPCC] + CFLAGS + ["-c", src, "-o", obj + ".tmp"]
+        cmd = [HIPCC] + CFLAGS + ["-D" + d for d in defines] + ["-c", src, "-o", obj + ".tmp"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
@@ -49,24 +49,31 @@ def _compile(src, force):
     return obj
 
 
-def build(force: bool = False, jobs: int = 4) -> str:
-    os.makedirs(OBJ, exist_ok=True)
+def build(force: bool = False, jobs: int = 4, defines=(), lib: str = LIB) -> str:
+    """Build the library; `defines` (NAME or NAME=VALUE) with a different `lib` path builds a
+    measurement variant in its own object directory (load it with GSR_LIBRARY=path)."""
+    objdir = OBJ if not defines else os.path.join(PKG_ROOT, "build", "obj_" + "_".join(
+        d.replace("=", "-") for d in defines))
+    os.makedirs(objdir, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, force), srcs))
-    if force or _stale(LIB, objs):
-        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB + ".tmp"] + objs
+        objs = list(ex.map(lambda s: _compile(s, force, objdir, tuple(defines)), srcs))
+    if force or _stale(lib, objs):
+        os.makedirs(os.path.dirname(lib), exist_ok=True)
+        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib + ".tmp"] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
-        os.replace(LIB + ".tmp", LIB)
-    return LIB
+        os.replace(lib + ".tmp", lib)
+    return lib
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--jobs", type=int, default=4)
+    ap.add_argument("--define", action="append", default=[], help="extra -D for a measurement variant")
+    ap.add_argument("--out", default=LIB, help="library path (variants: anywhere outside the package)")
     a = ap.parse_args()
-    print(build(a.force, a.jobs))
+    print(build(a.force, a.jobs, a.define, a.out))
     sys.exit(0)

@@ -223,6 +223,77 @@ __device__ __forceinline__ void wave_allreduce(float *v) {
     }
 }
 
+// Sum each of N values over its 16-lane row; every lane of row r receives row r's totals.  The
+// four row partials are combined later, off the per-instance path.  Written as one asm block of
+// fused DPP adds (v_add_f32 with a quad_perm / row_ror source modifier), stage-major over the N
+// values: left to the compiler, the SLP vectoriser pairs the adds into v_pk_add_f32 fed by
+// separate v_mov_b32_dpp + register-pair moves, ~2.5x the instructions.  The leading s_nop
+// covers the VALU-write -> DPP-read hazard of the first stage; later stages read values
+// written >= N-1 instructions earlier.
+template <int N>
+__device__ __forceinline__ void wave_rowsum(float *v);
+
+#define GSR_DPP_STAGE(CTRL)                                                                               \
+    "v_add_f32_dpp %0, %0, %0 " CTRL " row_mask:0xf bank_mask:0xf\n"                                       \
+    "v_add_f32_dpp %1, %1, %1 " CTRL " row_mask:0xf bank_mask:0xf\n"                                       \
+    "v_add_f32_dpp %2, %2, %2 " CTRL " row_mask:0xf bank_mask:0xf\n"                                       \
+    "v_add_f32_dpp %3, %3, %3 " CTRL " row_mask:0xf bank_mask:0xf\n"                                       \
+    "v_add_f32_dpp %4, %4, %4 " CTRL " row_mask:0xf bank_mask:0xf\n"                                       \
+    "v_add_f32_dpp %5, %5, %5 " CTRL " row_mask:0xf bank_mask:0xf\n"                                       \
+    "v_add_f32_dpp %6, %6, %6 " CTRL " row_mask:0xf bank_mask:0xf\n"                                       \
+    "v_add_f32_dpp %7, %7, %7 " CTRL " row_mask:0xf bank_mask:0xf\n"                                       \
+    "v_add_f32_dpp %8, %8, %8 " CTRL " row_mask:0xf bank_mask:0xf\n"                                       \
+    "v_add_f32_dpp %9, %9, %9 " CTRL " row_mask:0xf bank_mask:0xf\n"
+
+template <>
+__device__ __forceinline__ void wave_rowsum<10>(float *v) {
+    asm volatile("s_nop 1\n" GSR_DPP_STAGE("quad_perm:[1,0,3,2]") GSR_DPP_STAGE("quad_perm:[2,3,0,1]")
+                     GSR_DPP_STAGE("row_ror:4") GSR_DPP_STAGE("row_ror:8")
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
+                   "+v"(v[7]), "+v"(v[8]), "+v"(v[9]));
+}
+#undef GSR_DPP_STAGE
+
+#define GSR_DPP_BCAST15(I) "v_add_f32_dpp %" #I ", %" #I ", %" #I " row_bcast:15 row_mask:0xa bank_mask:0xf\n"
+// wave_rowsum, then rows 1 and 3 add the row before them (row_bcast:15): lanes 16-31 hold
+// rows 0+1 and lanes 48-63 rows 2+3 -- two half-wave partials per value.
+template <int N>
+__device__ __forceinline__ void wave_halfsum(float *v);
+
+template <>
+__device__ __forceinline__ void wave_halfsum<10>(float *v) {
+    wave_rowsum<10>(v);
+    asm volatile("s_nop 1\n" GSR_DPP_BCAST15(0) GSR_DPP_BCAST15(1) GSR_DPP_BCAST15(2) GSR_DPP_BCAST15(3)
+                     GSR_DPP_BCAST15(4) GSR_DPP_BCAST15(5) GSR_DPP_BCAST15(6) GSR_DPP_BCAST15(7)
+                         GSR_DPP_BCAST15(8) GSR_DPP_BCAST15(9)
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
+                   "+v"(v[7]), "+v"(v[8]), "+v"(v[9]));
+}
+#undef GSR_DPP_BCAST15
+
+template <>
+__device__ __forceinline__ void wave_halfsum<9>(float *v) {
+    float t[10];
+#pragma unroll
+    for (int i = 0; i < 9; i++) t[i] = v[i];
+    t[9] = 0.f;
+    wave_halfsum<10>(t);
+#pragma unroll
+    for (int i = 0; i < 9; i++) v[i] = t[i];
+}
+
+// N = 9 (no depth term): pad with a dummy value so one asm block serves both.
+template <>
+__device__ __forceinline__ void wave_rowsum<9>(float *v) {
+    float t[10];
+#pragma unroll
+    for (int i = 0; i < 9; i++) t[i] = v[i];
+    t[9] = 0.f;
+    wave_rowsum<10>(t);
+#pragma unroll
+    for (int i = 0; i < 9; i++) v[i] = t[i];
+}
+
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) {
@@ -283,6 +354,12 @@ struct ImageState {
     uint64_t *boundary;     // per tile: (depth bits << 32 | id) of the last instance any pixel uses
     float *final_T;         // per pixel
     uint32_t *n_contrib;    // per pixel: 1-based list position of the last contributor
+    uint32_t *tile_work;    // per tile: backward work (last contributor position, max over pixels)
+    uint32_t *tile_ids;     // per tile: its own index (sort payload)
+    uint32_t *work_sorted;  // tile_work sorted descending
+    uint32_t *tile_order;   // tiles by descending backward work: render_bwd's launch order
+    void *order_tmp;
+    size_t order_tmp_bytes;
 };
 
 // Backward per-instance gradient records, one 64-B line each, indexed by the instance's unsorted

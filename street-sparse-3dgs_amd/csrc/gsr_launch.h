@@ -39,6 +39,10 @@ hipError_t inclusive_scan_gathered(void *tmp, size_t tmp_bytes, const uint32_t *
 size_t depth_sort_temp_bytes(int P);
 hipError_t depth_sort(void *tmp, size_t tmp_bytes, const uint32_t *kin, uint32_t *kout, const uint32_t *vin,
                       uint32_t *vout, int P, hipStream_t s);
+// Tiles by descending backward work (longest-processing-time-first launch order for render_bwd).
+size_t tile_order_temp_bytes(int T);
+hipError_t tile_order(void *tmp, size_t tmp_bytes, const uint32_t *work, uint32_t *work_sorted, const uint32_t *ids,
+                      uint32_t *order, int T, hipStream_t s);
 size_t tile_sort_temp_bytes(int64_t K, int end_bit, bool wide);
 hipError_t tile_sort(void *tmp, size_t tmp_bytes, const void *kin, void *kout, const uint32_t *vin, uint32_t *vout,
                      int64_t K, int end_bit, bool wide, hipStream_t s);

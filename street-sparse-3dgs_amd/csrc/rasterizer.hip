@@ -132,6 +132,12 @@ ImageState carve_image(void *base, int T, int npix, size_t *bytes) {
     s.boundary = c.take<uint64_t>(T);
     s.final_T = c.take<float>(npix);
     s.n_contrib = c.take<uint32_t>(npix);
+    s.tile_work = c.take<uint32_t>(T);
+    s.tile_ids = c.take<uint32_t>(T);
+    s.work_sorted = c.take<uint32_t>(T);
+    s.tile_order = c.take<uint32_t>(T);
+    s.order_tmp_bytes = tile_order_temp_bytes(T);
+    s.order_tmp = c.take<char>(s.order_tmp_bytes);
     if (bytes) *bytes = align_up(c.off, 256);
     return s;
 }
@@ -312,6 +318,9 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
     {
         StageTimer st(5, s);
         launch_render_fwd(cam, gs, bs, is, background, out_color, out_invdepth, s);
+        if (tile_order(is.order_tmp, is.order_tmp_bytes, is.tile_work, is.work_sorted, is.tile_ids, is.tile_order, T,
+                       s) != hipSuccess)
+            return fail(GSR_ERR_DEVICE, "tile order sort failed");
     }
     if ((rc = check("render", debug, s))) return rc;
     if (num_rendered) *num_rendered = K;

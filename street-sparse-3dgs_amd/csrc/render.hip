@@ -14,8 +14,9 @@
 // Backward: upstream accumulates ~10 float atomics per (pixel, Gaussian) pair.  On gfx950 float
 // atomics execute at the memory side (MI355X_MICROARCH.md, Global float atomics) and 64 lanes
 // adding into one address serialise, so each wave instead reduces every instance's 10 gradient
-// terms over its 256 pixels (gsr_device.h wave_allreduce: DPP + permlane swaps), parks the sum in the instance's
-// lane and stores one 64-B record per instance with plain stores at the instance's unsorted
+// terms over its 256 pixels: per instance a 5-stage DPP sum over each half wave
+// (gsr_device.h wave_halfsum) whose 2 partials go to LDS; once per batch of 64 instances each
+// lane adds its instance's halves and stores one 64-B record with plain stores at the instance's unsorted
 // (Gaussian-major) index.  Only instances in front of the tile's last contributor are visited
 // (13% of them on the 1M-Gaussian bench scene); the tile's boundary key tells backward.hip
 // which records exist.  No atomics: fwd+bwd is bitwise reproducible.
@@ -49,7 +50,8 @@ __device__ __forceinline__ uint32_t lane_prefix(uint64_t mask) {
 __global__ __launch_bounds__(64) void render_fwd_kernel(
     const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list, int W, int H, int gx,
     const GRec *__restrict__ rec, const float *__restrict__ bg, float *__restrict__ out_color,
-    float *__restrict__ out_invd, float *__restrict__ final_T, uint32_t *__restrict__ n_contrib) {
+    float *__restrict__ out_invd, float *__restrict__ final_T, uint32_t *__restrict__ n_contrib,
+    uint32_t *__restrict__ tile_work, uint32_t *__restrict__ tile_ids) {
     __shared__ float4 s_a[kWave];  // x, y, conic.a, conic.b
     __shared__ float4 s_b[kWave];  // conic.c, opacity, contributor index, sub-block mask
     __shared__ float4 s_c[kWave];  // r, g, b, 1/depth
@@ -125,6 +127,15 @@ __global__ __launch_bounds__(64) void render_fwd_kernel(
         }
         __syncthreads();
     }
+    // backward work estimate for the launch order of render_bwd: its last contributor position
+    uint32_t wl = last[0];
+#pragma unroll
+    for (int k = 1; k < kPixPerLane; k++) wl = last[k] > wl ? last[k] : wl;
+    wl = wave_max_u32(wl);
+    if (lane == 0) {
+        tile_work[tile] = wl < 0xFFFFu ? wl : 0xFFFFu;
+        tile_ids[tile] = (uint32_t)tile;
+    }
     const float b0 = bg[0], b1 = bg[1], b2 = bg[2];
 #pragma unroll
     for (int k = 0; k < kPixPerLane; k++) {
@@ -146,7 +157,7 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
     const int T = cam.gx * cam.gy;
     if (T == 0) return;
     hipLaunchKernelGGL(render_fwd_kernel, dim3(T), dim3(kWave), 0, s, is.ranges, bs.point_list, cam.W, cam.H, cam.gx,
-                       gs.rec, bg, out_color, out_invdepth, is.final_T, is.n_contrib);
+                       gs.rec, bg, out_color, out_invdepth, is.final_T, is.n_contrib, is.tile_work, is.tile_ids);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -155,18 +166,27 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
 // The four 16x4 sub-blocks are evaluated in one basic block (a culled sub-block only clears the
 // predicate) so their dependency chains interleave: 0.78 ms vs 0.82-0.85 ms for the branchy
 // forms on the 1M-Gaussian 1080p bench scene.
+#ifndef GSR_BWD_WAVES_PER_EU
+#define GSR_BWD_WAVES_PER_EU 1
+#endif
+#ifndef GSR_TILE_REVERSE
+#define GSR_TILE_REVERSE 0
+#endif
 template <bool kDepth>
-__global__ __launch_bounds__(64) void render_bwd_kernel(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVES_PER_EU))) void render_bwd_kernel(
     const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list, int W, int H, int gx,
     const GRec *__restrict__ rec, const float *__restrict__ bg, const float *__restrict__ final_Ts,
     const uint32_t *__restrict__ n_contrib, const float *__restrict__ dL_dpix, const float *__restrict__ dL_dinvd,
-    uint64_t *__restrict__ boundary, float4 *__restrict__ out) {
+    const uint32_t *__restrict__ tile_order, uint64_t *__restrict__ boundary, float4 *__restrict__ out) {
     __shared__ float4 s_a[kWave];
     __shared__ float4 s_b[kWave];  // conic.c, opacity, list position, sub-block mask
     __shared__ float4 s_c[kWave];
     __shared__ uint32_t s_u[kWave];
+    __shared__ float2 s_red[kWave * 2 * 5];  // per instance, per half wave: 10 partial sums
 
-    const int tile = blockIdx.x;
+    // Tiles run heaviest first (longest-processing-time order from the forward's per-tile work):
+    // with ~2.7 tiles per wave slot, index order leaves a tail of a few heavy tiles.
+    const int tile = GSR_TILE_REVERSE ? (int)blockIdx.x : (int)tile_order[blockIdx.x];
     const int tx = tile % gx, ty = tile / gx;
     const int lane = threadIdx.x;
     const int px = tx * kTile + (lane & 15);
@@ -243,7 +263,6 @@ __global__ __launch_bounds__(64) void render_bwd_kernel(
             s_u[slot] = u;
         }
         __syncthreads();
-        float r0 = 0.f, r1 = 0.f, r2 = 0.f, r3 = 0.f, r4 = 0.f, r5 = 0.f, r6 = 0.f, r7 = 0.f, r8 = 0.f, r9 = 0.f;
         for (uint32_t j = 0; j < cnt; j++) {
             const float4 a = s_a[j];
             const float4 b = s_b[j];
@@ -300,20 +319,29 @@ __global__ __launch_bounds__(64) void render_bwd_kernel(
                 q[4] = fmaf(dLdG * gdy, dy, q[4]);
                 q[5] = fmaf(Ge, dla, q[5]);
             }
-            if (__any(any)) {
-                wave_allreduce<kDepth ? 10 : 9>(q);
-                const bool mine = (uint32_t)lane == j;  // park instance j's sums in lane j
-                r0 = mine ? q[0] : r0; r1 = mine ? q[1] : r1; r2 = mine ? q[2] : r2; r3 = mine ? q[3] : r3;
-                r4 = mine ? q[4] : r4; r5 = mine ? q[5] : r5; r6 = mine ? q[6] : r6; r7 = mine ? q[7] : r7;
-                r8 = mine ? q[8] : r8;
-                if (kDepth) r9 = mine ? q[9] : r9;
+            // Half-wave sums only (5 DPP stages); lanes 16 and 48 park the two partials in LDS
+            // and they are added once per batch below instead of per instance.
+            if (__any(any)) wave_halfsum<kDepth ? 10 : 9>(q);
+            if ((lane & 31) == 16) {
+                float2 *d = s_red + (j * 2 + (lane >> 5)) * 5;
+#pragma unroll
+                for (int t = 0; t < 5; t++) d[t] = make_float2(q[2 * t], (kDepth || t < 4) ? q[2 * t + 1] : 0.f);
             }
         }
+        __syncthreads();
         if ((uint32_t)lane < cnt) {
+            const float2 *d = s_red + lane * 10;
+            float r[10];
+#pragma unroll
+            for (int t = 0; t < 5; t++) {
+                const float2 p0 = d[t], p1 = d[5 + t];
+                r[2 * t] = p0.x + p1.x;
+                r[2 * t + 1] = p0.y + p1.y;
+            }
             const size_t o = 4 * (size_t)s_u[lane];
-            out[o + 0] = make_float4(r0 * sx, r1 * sy, -0.5f * r2, -0.5f * r3);
-            out[o + 1] = make_float4(-0.5f * r4, r5, r6, r7);
-            out[o + 2] = make_float4(r8, r9, 0.f, 0.f);
+            out[o + 0] = make_float4(r[0] * sx, r[1] * sy, -0.5f * r[2], -0.5f * r[3]);
+            out[o + 1] = make_float4(-0.5f * r[4], r[5], r[6], r[7]);
+            out[o + 2] = make_float4(r[8], r[9], 0.f, 0.f);
             out[o + 3] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
         __syncthreads();
@@ -328,12 +356,12 @@ void launch_render_bwd(const Camera &cam, const GeomState &gs, const BinningStat
     if (T == 0) return;
     if (dL_dinvdepth)
         hipLaunchKernelGGL(render_bwd_kernel<true>, dim3(T), dim3(kWave), 0, s, is.ranges, bs.point_list, cam.W,
-                           cam.H, cam.gx, gs.rec, bg, is.final_T, is.n_contrib, dL_dpix, dL_dinvdepth, is.boundary,
-                           sc.rec);
+                           cam.H, cam.gx, gs.rec, bg, is.final_T, is.n_contrib, dL_dpix, dL_dinvdepth, is.tile_order,
+                           is.boundary, sc.rec);
     else
         hipLaunchKernelGGL(render_bwd_kernel<false>, dim3(T), dim3(kWave), 0, s, is.ranges, bs.point_list, cam.W,
-                           cam.H, cam.gx, gs.rec, bg, is.final_T, is.n_contrib, dL_dpix, dL_dinvdepth, is.boundary,
-                           sc.rec);
+                           cam.H, cam.gx, gs.rec, bg, is.final_T, is.n_contrib, dL_dpix, dL_dinvdepth, is.tile_order,
+                           is.boundary, sc.rec);
 }
 
 }  // namespace gsr

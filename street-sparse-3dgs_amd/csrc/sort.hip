@@ -76,4 +76,19 @@ hipError_t tile_sort(void *tmp, size_t tmp_bytes, const void *kin, void *kout, c
                                      vin, vout, (size_t)K, 0, end_bit, s);
 }
 
+size_t tile_order_temp_bytes(int T) {
+    size_t bytes = 0;
+    rocprim::radix_sort_pairs_desc(nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                   (const uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)(T > 0 ? T : 1), 0, 16);
+    return bytes;
+}
+
+// Stable descending sort of the T per-tile work estimates (clamped to 16 bits by the producer):
+// equal-work tiles keep index order, so the launch order is deterministic.
+hipError_t tile_order(void *tmp, size_t tmp_bytes, const uint32_t *work, uint32_t *work_sorted, const uint32_t *ids,
+                      uint32_t *order, int T, hipStream_t s) {
+    if (T == 0) return hipSuccess;
+    return rocprim::radix_sort_pairs_desc(tmp, tmp_bytes, work, work_sorted, ids, order, (size_t)T, 0, 16, s);
+}
+
 }  // namespace gsr
