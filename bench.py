@@ -17,7 +17,6 @@ from __future__ import annotations
 import argparse
 import glob
 import json
-import math
 import os
 import sys
 import time
@@ -51,17 +50,18 @@ def algorithmic_bytes(P, Pv, K, T, npix, M=16):
     """Per-launch algorithmic bytes per stage.  SURVEY.md 8(d) figures (M=16 constants; the SH
     term scales with M) for the stages it defines; the binning stages follow this build's
     algorithm: a 32-bit depth sort of P ids (4 LSD passes, 16 B/elem/pass) + the
-    gathered scan, duplicate writing 2-B tile ids + 4-B ids, and a 2-pass stable tile sort
-    (12 B/elem/pass); upstream's 64-bit 6-pass sort would be 24*K*6."""
+    gathered scan; level-1 binning reads (order, tiles, rect) twice per Gaussian and writes the
+    superblock lists (P1 ~ 1.5 P entries, not measured here); level 2 re-reads them with the
+    rects twice and writes the K-entry point list + ranges.  Upstream's 64-bit 6-pass key sort
+    alone would be 24*K*6."""
     sh = 12 * M
-    tile_bits = max(1, math.ceil(math.log2(max(T, 2))))
-    kb = 2 if T <= 65536 else 4
+    P1 = 1.5 * P
     return {
         "preprocess": (44 + sh) * P + 80 * P,
         "depth_sort_scan": 16 * P * 4 + 12 * P,
-        "duplicate": (kb + 4) * K + 16 * Pv,
-        "tile_sort": 2 * (kb + 4) * K * math.ceil(tile_bits / 8),
-        "ranges": kb * K + 8 * T,
+        "bin_superblocks": 2 * 24 * Pv + 8 * Pv + 4 * P1,
+        "bin_tiles": 2 * 24 * P1 + 4 * K + 8 * T,
+        "tile_order": 16 * T,
         "render_fwd": 44 * K + 24 * npix,
         "render_bwd": 44 * K + 24 * npix + 40 * Pv,
         "preprocess_bwd": (356 + sh - 192) * P + (260 + sh - 192) * P,

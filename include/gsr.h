@@ -52,7 +52,7 @@ typedef enum {
  * Returning NULL aborts the call with GSR_ERR_ALLOCATION. */
 typedef void *(*gsr_resize_fn)(void *ctx, size_t bytes);
 
-/* Forward: preprocess -> scan -> duplicate-with-keys -> sort -> tile ranges -> blend.
+/* Forward: preprocess -> depth sort + scan -> binning (per-tile lists + ranges) -> blend.
  * Mirrors CudaRasterizer::Rasterizer::forward as the reference's
  * _C.rasterize_gaussians(bg, means3D, colors, opacity, scales, rotations, scale_modifier,
  * cov3D_precomp, viewmatrix, projmatrix, tanfovx, tanfovy, H, W, sh, degree, campos,
@@ -100,8 +100,8 @@ int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const
 
 /* Per-stage device time of the last forward/backward on this thread, filled only when
  * gsr_set_profiling(1) was called (HIP events; for bench.py's roofline).  Stage order:
- * 0 preprocess, 1 depth sort + scan, 2 duplicate, 3 tile sort, 4 ranges, 5 render_fwd, 6 render_bwd,
- * 7 preprocess_bwd.  Returns the number of stages written. */
+ * 0 preprocess, 1 depth sort + scan, 2 binning level 1 (superblocks), 3 binning level 2 (tiles and
+ * ranges), 4 forward tile order, 5 render_fwd (+ backward tile order), 6 render_bwd, 7 preprocess_bwd.  Returns the number of stages written. */
 int gsr_set_profiling(int enable);
 int gsr_stage_times_ms(float *out, int max_stages);
 

@@ -1,0 +1,481 @@
+// binning.hip -- tile lists without a K-element sort.
+//
+// Upstream emits K (tile << 32 | depth) keys and radix-sorts them (6 passes over 24-B pairs at
+// 1080p), then scans the sorted keys for tile ranges.  Here the Gaussians are already in depth
+// order (one 32-bit sort of P keys, sort.hip), and the per-tile lists are built by two stable
+// counting passes that exploit each splat's footprint being a rectangle of tiles:
+//
+//   level 1  Gaussian -> superblock (SB = 2^s x 2^s tiles, ~500 at 1080p).  Chunks of 2048
+//            depth-ordered Gaussians count their SB footprints in LDS (sb_count), per-SB column
+//            scans over chunks give every chunk its offsets (sb_colscan, sb_base), and a second
+//            pass writes each SB's Gaussian list in depth order (sb_scatter): per batch of 64
+//            Gaussians, each lane ORs its bit into an LDS lane mask per SB it covers, and its
+//            rank in an SB's list is the popcount of the lower lanes of that mask.
+//   level 2  SB -> tiles (tile_bin): one workgroup per SB counts its tiles' instances, writes the
+//            tile ranges, and re-walks the SB list with the same lane-mask ranking per tile to
+//            place every instance at its stable position.
+//
+// The result is the upstream order inside every tile -- (depth bits, Gaussian id) -- with tiles
+// laid out SB-major instead of row-major; every consumer goes through `ranges`, so the layout of
+// whole tiles in point_list is free.  Also writes rec[g].off (the Gaussian-major instance offset
+// the backward records use).  Traffic ~ 8 B per SB instance + 4 B per tile instance written.
+#include "gsr_launch.h"
+
+namespace gsr {
+
+namespace {
+
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+struct TileRect {
+    int x0, y0, x1, y1;  // inclusive tile bounds; x1 < x0 when empty
+};
+
+__device__ __forceinline__ TileRect unpack_rect(uint2 d) {
+    TileRect r;
+    r.x0 = (int)(d.x & 0xFFFFu);
+    r.y0 = (int)(d.x >> 16);
+    r.x1 = (int)(d.y & 0xFFFFu) - 1;  // stored exclusive so that 0/0 means "no tiles"
+    r.y1 = (int)(d.y >> 16) - 1;
+    return r;
+}
+
+// Depth-ordered rect / tile count of every Gaussian: the one random gather of the binning.
+__global__ __launch_bounds__(256) void depth_gather_kernel(int P, const GRec *__restrict__ rec,
+                                                           const uint32_t *__restrict__ order,
+                                                           const uint32_t *__restrict__ tiles, uint2 *__restrict__ drect,
+                                                           uint32_t *__restrict__ dtiles) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= P) return;
+    const uint32_t g = order[j];
+    const uint32_t area = tiles[g];
+    uint2 d = make_uint2(0u, 0u);
+    if (area > 0) {
+        const uint4 q3 = reinterpret_cast<const uint4 *>(rec + g)[3];
+        const uint32_t w = q3.y, x0 = q3.x & 0xFFFFu, y0 = q3.x >> 16;
+        d = make_uint2(q3.x, (x0 + w) | ((y0 + area / w) << 16));
+    }
+    drect[j] = d;
+    dtiles[j] = area;
+}
+
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Level 1, pass 1: per chunk and SB, the number of Gaussians and of tile instances.
+__global__ __launch_bounds__(1024) void sb_count_kernel(int P, SBGrid sg, GRec *__restrict__ rec,
+                                                       const uint32_t *__restrict__ order,
+                                                       const uint2 *__restrict__ drect,
+                                                       const uint32_t *__restrict__ offsets,
+                                                       uint32_t *__restrict__ cnt_g, uint32_t *__restrict__ cnt_i) {
+    extern __shared__ uint32_t lds[];
+    uint32_t *cg = lds, *ci = lds + sg.nsb;
+    for (int i = threadIdx.x; i < 2 * sg.nsb; i += 1024) lds[i] = 0u;
+    __syncthreads();
+    const int chunk = blockIdx.x;
+    const int j0 = chunk * kSBChunk, j1 = min(P, j0 + kSBChunk);
+    for (int j = j0 + (int)threadIdx.x; j < j1; j += 1024) {
+        const TileRect r = unpack_rect(drect[j]);
+        if (r.x1 < r.x0) continue;
+        rec[order[j]].off = j == 0 ? 0u : offsets[j - 1];
+        const int side = 1 << sg.shift;
+        for (int sy = r.y0 >> sg.shift; sy <= r.y1 >> sg.shift; sy++) {
+            const int h = min(r.y1, sy * side + side - 1) - max(r.y0, sy * side) + 1;
+            for (int sx = r.x0 >> sg.shift; sx <= r.x1 >> sg.shift; sx++) {
+                const int w = min(r.x1, sx * side + side - 1) - max(r.x0, sx * side) + 1;
+                const int sb = sy * sg.nsbx + sx;
+                atomicAdd(&cg[sb], 1u);
+                atomicAdd(&ci[sb], (uint32_t)(w * h));
+            }
+        }
+    }
+    __syncthreads();
+    for (int s = threadIdx.x; s < sg.nsb; s += 1024) {
+        cnt_g[(size_t)s * sg.nchunks + chunk] = cg[s];
+        cnt_i[(size_t)s * sg.nchunks + chunk] = ci[s];
+    }
+}
+
+// Exclusive scan of 256 values held one per thread; returns the exclusive prefix and the total.
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t *wsum, uint32_t &total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    __syncthreads();
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t before = 0;
+    for (int k = 0; k < w; k++) before += wsum[k];
+    total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    return before + incl - v;
+}
+
+// Level 1, pass 2a: per SB, exclusive scan of the Gaussian counts over chunks (in place) and the
+// SB totals of Gaussians and instances.
+__global__ __launch_bounds__(256) void sb_colscan_kernel(SBGrid sg, uint32_t *__restrict__ cnt_g,
+                                                         const uint32_t *__restrict__ cnt_i,
+                                                         uint32_t *__restrict__ base_g, uint32_t *__restrict__ base_i) {
+    __shared__ uint32_t wsum[4];
+    const int s = blockIdx.x;
+    uint32_t *row = cnt_g + (size_t)s * sg.nchunks;
+    const uint32_t *rowi = cnt_i + (size_t)s * sg.nchunks;
+    uint32_t carry = 0, isum = 0;
+    for (int b = 0; b < sg.nchunks; b += 256) {
+        const int c = b + (int)threadIdx.x;
+        const uint32_t v = c < sg.nchunks ? row[c] : 0u;
+        isum += c < sg.nchunks ? rowi[c] : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_exclusive_scan(v, wsum, tot);
+        if (c < sg.nchunks) row[c] = carry + ex;
+        carry += tot;
+    }
+    uint32_t itot;
+    (void)block_exclusive_scan(isum, wsum, itot);
+    if (threadIdx.x == 0) {
+        base_g[s] = carry;
+        base_i[s] = itot;
+    }
+}
+
+// Level 1, pass 2b: exclusive scans of the SB totals (one workgroup); base[nsb] = the total.
+__global__ __launch_bounds__(256) void sb_base_kernel(int nsb, uint32_t *__restrict__ base_g,
+                                                      uint32_t *__restrict__ base_i) {
+    __shared__ uint32_t wsum[4];
+    uint32_t cg = 0, ci = 0;
+    for (int b = 0; b < nsb; b += 256) {
+        const int s = b + (int)threadIdx.x;
+        const uint32_t vg = s < nsb ? base_g[s] : 0u, vi = s < nsb ? base_i[s] : 0u;
+        uint32_t tg, ti;
+        const uint32_t eg = block_exclusive_scan(vg, wsum, tg);
+        const uint32_t ei = block_exclusive_scan(vi, wsum, ti);
+        if (s < nsb) {
+            base_g[s] = cg + eg;
+            base_i[s] = ci + ei;
+        }
+        cg += tg;
+        ci += ti;
+    }
+    if (threadIdx.x == 0) {
+        base_g[nsb] = cg;
+        base_i[nsb] = ci;
+    }
+}
+
+// Level 1, pass 3: stable scatter of (chunk, wave, batch, lane)-ordered Gaussians into the SB
+// lists.  Ranks come from LDS lane masks: every lane ORs its bit into the mask of each SB it
+// covers, its rank in that SB's list is the popcount of the lower lanes, and the highest lane of
+// each mask advances the SB's position and clears the mask.  Footprints of up to kSmallSB SBs
+// are walked per lane; larger ones (rare, 3-sigma splats) by the whole wave, one at a time, so
+// one outlier does not serialise its batch.
+#ifndef GSR_SCATTER_WAVES
+#define GSR_SCATTER_WAVES 8
+#endif
+#ifndef GSR_SMALL_SB
+#define GSR_SMALL_SB 16
+#endif
+constexpr int kScatterWaves = GSR_SCATTER_WAVES;
+constexpr int kSmallSB = GSR_SMALL_SB;
+
+struct SBFoot {
+    int sx0, sy0, sw, n;
+};
+
+__device__ __forceinline__ SBFoot sb_foot(const TileRect &r, int shift) {
+    SBFoot f{0, 0, 1, 0};
+    if (r.x1 < r.x0) return f;
+    f.sx0 = r.x0 >> shift;
+    f.sy0 = r.y0 >> shift;
+    f.sw = (r.x1 >> shift) - f.sx0 + 1;
+    f.n = f.sw * ((r.y1 >> shift) - f.sy0 + 1);
+    return f;
+}
+
+__device__ __forceinline__ uint32_t sb_key(const SBFoot &f, int k, int nsbx) {
+    return (uint32_t)((f.sy0 + k / f.sw) * nsbx + f.sx0 + k % f.sw);
+}
+
+// footprint clipped to SB `key`, in SB-local tile coordinates (8 bits each)
+__device__ __forceinline__ uint32_t sb_local(const TileRect &r, uint32_t key, const SBGrid &sg) {
+    const int side = 1 << sg.shift;
+    const int ox = (int)(key % (uint32_t)sg.nsbx) * side, oy = (int)(key / (uint32_t)sg.nsbx) * side;
+    return (uint32_t)(max(r.x0, ox) - ox) | ((uint32_t)(max(r.y0, oy) - oy) << 8) |
+           ((uint32_t)(min(r.x1, ox + side - 1) - ox) << 16) | ((uint32_t)(min(r.y1, oy + side - 1) - oy) << 24);
+}
+
+// lane b's value; b is wave-uniform, so v_readlane (no LDS round trip as with __shfl)
+__device__ __forceinline__ int rl(int v, int b) { return __builtin_amdgcn_readlane(v, b); }
+
+__device__ __forceinline__ TileRect lane_rect(const TileRect &r, int b) {
+    return TileRect{rl(r.x0, b), rl(r.y0, b), rl(r.x1, b), rl(r.y1, b)};
+}
+
+__device__ __forceinline__ SBFoot lane_foot(const SBFoot &f, int b) {
+    return SBFoot{rl(f.sx0, b), rl(f.sy0, b), rl(f.sw, b), rl(f.n, b)};
+}
+
+__global__ __launch_bounds__(64 * kScatterWaves) void sb_scatter_kernel(int P, SBGrid sg,
+                                                                         const uint32_t *__restrict__ order,
+                                                                         const uint2 *__restrict__ drect,
+                                                                         const uint32_t *__restrict__ col,
+                                                                         const uint32_t *__restrict__ base_g,
+                                                                         uint2 *__restrict__ sblist) {
+    extern __shared__ uint32_t wc[];  // [W][nsb] per-wave running positions, then [W][nsb] u64 masks
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int nsb = sg.nsb;
+    for (int i = threadIdx.x; i < 3 * kScatterWaves * nsb; i += 64 * kScatterWaves) wc[i] = 0u;
+    __syncthreads();
+    const int chunk = blockIdx.x;
+    constexpr int kPerWave = kSBChunk / kScatterWaves;
+    const int jw0 = chunk * kSBChunk + w * kPerWave, jw1 = min(P, jw0 + kPerWave);
+    uint32_t *run = wc + w * nsb;
+    uint64_t *msk = reinterpret_cast<uint64_t *>(wc + kScatterWaves * nsb) + w * nsb;
+    const uint64_t lt = (1ull << lane) - 1ull;
+
+    // per-wave SB counts
+    for (int jb = jw0; jb < jw1; jb += 64) {
+        const int j = jb + lane;
+        const TileRect r = j < jw1 ? unpack_rect(drect[j]) : TileRect{0, 0, -1, -1};
+        const SBFoot f = sb_foot(r, sg.shift);
+        const bool small = f.n <= kSmallSB;
+#pragma unroll
+        for (int k = 0; k < kSmallSB; k++)
+            if (small && k < f.n) atomicAdd(&run[sb_key(f, k, sg.nsbx)], 1u);
+        for (uint64_t big = __ballot(!small); big; big &= big - 1) {
+            const int b = __ffsll((unsigned long long)big) - 1;
+            const SBFoot fb = lane_foot(f, b);
+            for (int k = lane; k < fb.n; k += 64) atomicAdd(&run[sb_key(fb, k, sg.nsbx)], 1u);
+        }
+    }
+    __syncthreads();
+    for (int s = threadIdx.x; s < nsb; s += 64 * kScatterWaves) {
+        uint32_t b = base_g[s] + col[(size_t)s * sg.nchunks + chunk];
+        for (int k = 0; k < kScatterWaves; k++) {
+            const uint32_t c = wc[k * nsb + s];
+            wc[k * nsb + s] = b;
+            b += c;
+        }
+    }
+    __syncthreads();
+
+    for (int jb = jw0; jb < jw1; jb += 64) {
+        const int j = jb + lane;
+        uint32_t g = 0;
+        TileRect r{0, 0, -1, -1};
+        if (j < jw1) {
+            g = order[j];
+            r = unpack_rect(drect[j]);
+        }
+        const SBFoot f = sb_foot(r, sg.shift);
+        const bool small = f.n <= kSmallSB;
+        const uint64_t bigs = __ballot(!small);
+        // 1. masks
+#pragma unroll
+        for (int k = 0; k < kSmallSB; k++)
+            if (small && k < f.n) atomicOr(reinterpret_cast<unsigned long long *>(&msk[sb_key(f, k, sg.nsbx)]), 1ull << lane);
+        for (uint64_t big = bigs; big; big &= big - 1) {
+            const int b = __ffsll((unsigned long long)big) - 1;
+            const SBFoot fb = lane_foot(f, b);
+            for (int k = lane; k < fb.n; k += 64)
+                atomicOr(reinterpret_cast<unsigned long long *>(&msk[sb_key(fb, k, sg.nsbx)]), 1ull << b);
+        }
+        // 2. ranked writes
+#pragma unroll
+        for (int k = 0; k < kSmallSB; k++)
+            if (small && k < f.n) {
+                const uint32_t key = sb_key(f, k, sg.nsbx);
+                sblist[run[key] + (uint32_t)__popcll(msk[key] & lt)] = make_uint2(g, sb_local(r, key, sg));
+            }
+        for (uint64_t big = bigs; big; big &= big - 1) {
+            const int b = __ffsll((unsigned long long)big) - 1;
+            const SBFoot fb = lane_foot(f, b);
+            const TileRect rb = lane_rect(r, b);
+            const uint32_t gb = (uint32_t)rl((int)g, b);
+            for (int k = lane; k < fb.n; k += 64) {
+                const uint32_t key = sb_key(fb, k, sg.nsbx);
+                sblist[run[key] + (uint32_t)__popcll(msk[key] & ((1ull << b) - 1ull))] = make_uint2(gb, sb_local(rb, key, sg));
+            }
+        }
+        // 3. the highest lane of every mask advances the SB position and clears the mask
+#pragma unroll
+        for (int k = 0; k < kSmallSB; k++)
+            if (small && k < f.n) {
+                const uint32_t key = sb_key(f, k, sg.nsbx);
+                const uint64_t m = msk[key];
+                if (m != 0 && 63 - __clzll((long long)m) == lane) {
+                    run[key] += (uint32_t)__popcll(m);
+                    msk[key] = 0ull;
+                }
+            }
+        for (uint64_t big = bigs; big; big &= big - 1) {
+            const int b = __ffsll((unsigned long long)big) - 1;
+            const SBFoot fb = lane_foot(f, b);
+            for (int k = lane; k < fb.n; k += 64) {
+                const uint32_t key = sb_key(fb, k, sg.nsbx);
+                const uint64_t m = msk[key];
+                if (m != 0 && 63 - __clzll((long long)m) == b) {
+                    run[key] += (uint32_t)__popcll(m);
+                    msk[key] = 0ull;
+                }
+            }
+        }
+    }
+}
+
+// Level 2: one workgroup per SB; wave w owns a contiguous 1/kTBWaves of the SB's list (entries
+// carry the footprint clipped to the SB, so the list is read sequentially).  For each batch of 64
+// entries and each of the SB's tiles (16 at a time), a ballot of "footprint contains the tile"
+// gives the tile's count (pass A) or, after the tile scan, the stable rank of every covering
+// entry (pass B).  Counters and positions are wave-uniform registers: no LDS in the loops.
+constexpr int kTBWaves = 8;
+constexpr int kTileGroup = 16;
+
+__device__ __forceinline__ bool rect_has(uint32_t r, int lx, int ly) {
+    return lx >= (int)(r & 0xFFu) && ly >= (int)((r >> 8) & 0xFFu) && lx <= (int)((r >> 16) & 0xFFu) &&
+           ly <= (int)(r >> 24);
+}
+
+__global__ __launch_bounds__(64 * kTBWaves) void tile_bin_kernel(SBGrid sg, int gx, int gy,
+                                                                 const uint32_t *__restrict__ base_g,
+                                                                 const uint32_t *__restrict__ base_i,
+                                                                 const uint2 *__restrict__ sblist,
+                                                                 uint32_t *__restrict__ point_list,
+                                                                 uint2 *__restrict__ ranges) {
+    __shared__ uint32_t tc[kTBWaves][kMaxTilesPerSB];
+    const int s = blockIdx.x;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int side = 1 << sg.shift, tps = side * side;
+    const int ox = (s % sg.nsbx) * side, oy = (s / sg.nsbx) * side;
+    const uint32_t L0 = base_g[s], L = base_g[s + 1] - L0;
+    const uint32_t seg0 = (uint32_t)(((uint64_t)L * w) / kTBWaves), seg1 = (uint32_t)(((uint64_t)L * (w + 1)) / kTBWaves);
+    const uint64_t lt = (1ull << lane) - 1ull;
+
+    // pass A: per-wave tile counts
+    for (int tg = 0; tg < tps; tg += kTileGroup) {
+        uint32_t cnt[kTileGroup];
+#pragma unroll
+        for (int k = 0; k < kTileGroup; k++) cnt[k] = 0u;
+        for (uint32_t ib = seg0; ib < seg1; ib += 64) {
+            const uint32_t i = ib + lane;
+            const uint32_t r = i < seg1 ? sblist[L0 + i].y : 0xFFu;
+#pragma unroll
+            for (int k = 0; k < kTileGroup; k++) {
+                const int t = tg + k;
+                cnt[k] += (uint32_t)__popcll(__ballot(rect_has(r, t & (side - 1), t >> sg.shift)));
+            }
+        }
+        if (lane == 0)
+#pragma unroll
+            for (int k = 0; k < kTileGroup; k++)
+                if (tg + k < tps) tc[w][tg + k] = cnt[k];
+    }
+    __syncthreads();
+    // tile bases (SB-local row-major tile order, waves in list order) and the tile ranges
+    if (w == 0) {
+        uint32_t carry = 0;
+        for (int t0 = 0; t0 < tps; t0 += 64) {
+            const int t = t0 + lane;
+            uint32_t c = 0;
+            if (t < tps)
+                for (int k = 0; k < kTBWaves; k++) c += tc[k][t];
+            uint32_t incl = c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t v = (uint32_t)__shfl_up((int)incl, o, 64);
+                if (lane >= o) incl += v;
+            }
+            if (t < tps) {
+                uint32_t b = base_i[s] + carry + incl - c;
+                const int x = ox + (t & (side - 1)), y = oy + (t >> sg.shift);
+                if (x < gx && y < gy) ranges[y * gx + x] = make_uint2(b, b + c);
+                for (int k = 0; k < kTBWaves; k++) {
+                    const uint32_t ck = tc[k][t];
+                    tc[k][t] = b;
+                    b += ck;
+                }
+            }
+            carry += (uint32_t)__shfl((int)incl, 63, 64);
+        }
+    }
+    __syncthreads();
+    // pass B: stable placement
+    for (int tg = 0; tg < tps; tg += kTileGroup) {
+        uint32_t pos[kTileGroup];
+#pragma unroll
+        for (int k = 0; k < kTileGroup; k++) pos[k] = tg + k < tps ? tc[w][tg + k] : 0u;
+        for (uint32_t ib = seg0; ib < seg1; ib += 64) {
+            const uint32_t i = ib + lane;
+            uint2 e = make_uint2(0u, 0xFFu);
+            if (i < seg1) e = sblist[L0 + i];
+#pragma unroll
+            for (int k = 0; k < kTileGroup; k++) {
+                const int t = tg + k;
+                const bool hit = rect_has(e.y, t & (side - 1), t >> sg.shift);
+                const uint64_t m = __ballot(hit);
+                if (hit) point_list[pos[k] + (uint32_t)__popcll(m & lt)] = e.x;
+                pos[k] += (uint32_t)__popcll(m);
+            }
+        }
+    }
+}
+
+}  // namespace
+
+void launch_depth_gather(int P, const GeomState &gs, hipStream_t s) {
+    if (P == 0) return;
+    hipLaunchKernelGGL(depth_gather_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, gs.rec, gs.order, gs.tiles,
+                       gs.drect, gs.dtiles);
+}
+
+SBGrid sb_grid(int gx, int gy, int P) {
+    SBGrid g;
+    g.shift = 2;
+    for (;;) {
+        const int side = 1 << g.shift;
+        g.nsbx = (gx + side - 1) / side;
+        g.nsby = (gy + side - 1) / side;
+        g.nsb = g.nsbx * g.nsby;
+        if (g.nsb <= kMaxSB || (1 << (2 * (g.shift + 1))) > kMaxTilesPerSB) break;
+        g.shift++;
+    }
+    g.nchunks = (P + kSBChunk - 1) / kSBChunk;
+    if (g.nchunks < 1) g.nchunks = 1;
+    return g;
+}
+
+bool sb_grid_supported(const SBGrid &g) { return g.nsb <= kMaxSB; }
+
+void launch_binning_superblocks(int P, const Camera &cam, const GeomState &gs, const BinningState &bs,
+                                const ImageState &is, hipStream_t s) {
+    (void)is;
+    const SBGrid &sg = gs.sb;
+    if (P == 0 || cam.gx * cam.gy == 0) return;
+    const size_t l1 = sizeof(uint32_t) * 2 * (size_t)sg.nsb;
+    const size_t l3 = sizeof(uint32_t) * 3 * kScatterWaves * (size_t)sg.nsb;
+    hipLaunchKernelGGL(sb_count_kernel, dim3(sg.nchunks), dim3(1024), l1, s, P, sg, gs.rec, gs.order, gs.drect,
+                       gs.offsets, gs.sb_cnt_g, gs.sb_cnt_i);
+    hipLaunchKernelGGL(sb_colscan_kernel, dim3(sg.nsb), dim3(256), 0, s, sg, gs.sb_cnt_g, gs.sb_cnt_i, gs.sb_base_g,
+                       gs.sb_base_i);
+    hipLaunchKernelGGL(sb_base_kernel, dim3(1), dim3(256), 0, s, sg.nsb, gs.sb_base_g, gs.sb_base_i);
+    hipLaunchKernelGGL(sb_scatter_kernel, dim3(sg.nchunks), dim3(64 * kScatterWaves), l3, s, P, sg, gs.order, gs.drect,
+                       gs.sb_cnt_g, gs.sb_base_g, bs.sblist);
+}
+
+void launch_binning_tiles(int P, const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
+                          hipStream_t s) {
+    const SBGrid &sg = gs.sb;
+    const int T = cam.gx * cam.gy;
+    if (T == 0) return;
+    if (P == 0) {
+        (void)hipMemsetAsync(is.ranges, 0, sizeof(uint2) * (size_t)T, s);
+        return;
+    }
+    hipLaunchKernelGGL(tile_bin_kernel, dim3(sg.nsb), dim3(64 * kTBWaves), 0, s, sg, cam.gx, cam.gy, gs.sb_base_g,
+                       gs.sb_base_i, bs.sblist, bs.point_list, is.ranges);
+}
+
+}  // namespace gsr

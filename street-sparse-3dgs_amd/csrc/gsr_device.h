@@ -326,6 +326,17 @@ struct alignas(16) GRec {
 };
 static_assert(sizeof(GRec) == 64, "GRec must be one 64-B line");
 
+// Superblock grid of the two-level binning (binning.hip): SB = 2^shift x 2^shift tiles.
+#ifndef GSR_SB_CHUNK
+#define GSR_SB_CHUNK 1024
+#endif
+constexpr int kSBChunk = GSR_SB_CHUNK;  // depth-ordered Gaussians per level-1 chunk
+constexpr int kMaxSB = 1536;          // superblocks (3 x 8 waves x 4 B of LDS each in sb_scatter)
+constexpr int kMaxTilesPerSB = 256;   // up to 16 x 16 tiles per superblock
+struct SBGrid {
+    int shift, nsbx, nsby, nsb, nchunks;
+};
+
 struct GeomState {          // per Gaussian, written by preprocess
     GRec *rec;
     uint32_t *tiles;        // tiles_touched
@@ -337,16 +348,18 @@ struct GeomState {          // per Gaussian, written by preprocess
     uint8_t *clamped;       // bit c set: SH channel c clamped at 0
     void *tmp;              // depth-sort / scan temp storage
     size_t tmp_bytes;
+    uint2 *drect;           // per depth-order slot: tile rect (x0 | y0 << 16, x1 | y1 << 16), 0/0 = none
+    uint32_t *dtiles;       // per depth-order slot: tiles_touched (the scan input)
+    SBGrid sb;              // level-1 binning counters: [nsb][nchunks] Gaussians / instances,
+    uint32_t *sb_cnt_g;     // per-SB bases (nsb + 1 each)
+    uint32_t *sb_cnt_i;
+    uint32_t *sb_base_g;
+    uint32_t *sb_base_i;
 };
 
 struct BinningState {       // per tile instance
-    void *tkeys_unsorted;   // tile ids (uint16 when T <= 65536, else uint32), depth-major order
-    void *tkeys_sorted;
-    bool wide;
-    uint32_t *vals_unsorted;
-    uint32_t *point_list;   // gaussian id in (tile, depth, id) order
-    void *sort_tmp;
-    size_t sort_tmp_bytes;
+    uint2 *sblist;          // level 1: (Gaussian id, footprint in SB-local tiles) per superblock, depth order
+    uint32_t *point_list;   // Gaussian ids, per tile contiguous in (depth, id) order; tiles SB-major
 };
 
 struct ImageState {
@@ -355,11 +368,8 @@ struct ImageState {
     float *final_T;         // per pixel
     uint32_t *n_contrib;    // per pixel: 1-based list position of the last contributor
     uint32_t *tile_work;    // per tile: backward work (last contributor position, max over pixels)
-    uint32_t *tile_ids;     // per tile: its own index (sort payload)
-    uint32_t *work_sorted;  // tile_work sorted descending
-    uint32_t *tile_order;   // tiles by descending backward work: render_bwd's launch order
-    void *order_tmp;
-    size_t order_tmp_bytes;
+    uint32_t *tile_ids;     // forward launch order (tiles by descending list length)
+    uint32_t *tile_order;   // backward launch order (tiles by descending tile_work)
 };
 
 // Backward per-instance gradient records, one 64-B line each, indexed by the instance's unsorted

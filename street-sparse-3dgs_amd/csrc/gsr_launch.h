@@ -27,25 +27,25 @@ struct GaussianInputs {
 // preprocess.hip
 void launch_preprocess(const GaussianInputs &in, const Camera &cam, const GeomState &gs, int *radii,
                        hipStream_t s);
-void launch_duplicate(int P, const Camera &cam, const GeomState &gs, const int *radii, const BinningState &bs,
-                      hipStream_t s);
-void launch_ranges(int64_t K, int T, const BinningState &bs, const ImageState &is, hipStream_t s);
+// render.hip: tiles ordered heaviest first by work[t] (or, with work == NULL, by list length).
+void launch_tile_order(const uint32_t *work, const uint2 *ranges, int T, int shift, uint32_t *order, hipStream_t s);
 void launch_mark_visible(int P, const float *means3D, const float *view, uint8_t *present, hipStream_t s);
 
 // sort.hip (rocPRIM)
 size_t scan_temp_bytes(int P);
-hipError_t inclusive_scan_gathered(void *tmp, size_t tmp_bytes, const uint32_t *order, const uint32_t *tiles,
-                                   uint32_t *out, int P, hipStream_t s);
+hipError_t inclusive_scan(void *tmp, size_t tmp_bytes, const uint32_t *in, uint32_t *out, int P, hipStream_t s);
 size_t depth_sort_temp_bytes(int P);
 hipError_t depth_sort(void *tmp, size_t tmp_bytes, const uint32_t *kin, uint32_t *kout, const uint32_t *vin,
                       uint32_t *vout, int P, hipStream_t s);
-// Tiles by descending backward work (longest-processing-time-first launch order for render_bwd).
-size_t tile_order_temp_bytes(int T);
-hipError_t tile_order(void *tmp, size_t tmp_bytes, const uint32_t *work, uint32_t *work_sorted, const uint32_t *ids,
-                      uint32_t *order, int T, hipStream_t s);
-size_t tile_sort_temp_bytes(int64_t K, int end_bit, bool wide);
-hipError_t tile_sort(void *tmp, size_t tmp_bytes, const void *kin, void *kout, const uint32_t *vin, uint32_t *vout,
-                     int64_t K, int end_bit, bool wide, hipStream_t s);
+// binning.hip: per-tile lists from the depth-ordered Gaussians (two stable counting levels).
+SBGrid sb_grid(int gx, int gy, int P);
+// Depth-ordered copies of each Gaussian's tile rect and tile count (one gather pass after the sort).
+void launch_depth_gather(int P, const GeomState &gs, hipStream_t s);
+bool sb_grid_supported(const SBGrid &g);
+void launch_binning_superblocks(int P, const Camera &cam, const GeomState &gs, const BinningState &bs,
+                                const ImageState &is, hipStream_t s);
+void launch_binning_tiles(int P, const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
+                          hipStream_t s);
 
 // render.hip
 void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,

@@ -1,5 +1,5 @@
-// preprocess.hip -- per-Gaussian forward preprocess, per-instance key duplication, tile
-// ranges and the frustum test.
+// preprocess.hip -- per-Gaussian forward preprocess and the frustum test (SURVEY.md 8(a) rows
+// A4, A12).  Key duplication / sorting / tile ranges (A6-A8) are binning.hip.
 //
 // Layout: inputs are the caller's AoS tensors (means (P,3), scales (P,3), rotations (P,4),
 // shs (P,M,3)); the output is one 64-B GRec per Gaussian (gsr_device.h) so that every tile
@@ -136,105 +136,7 @@ void launch_preprocess(const GaussianInputs &in, const Camera &cam, const GeomSt
                            cam.fy, cam.gx, cam.gy, gs, radii);
 }
 
-// Key duplication, in depth order.  Lane j takes the j-th Gaussian of the depth sort and writes
-// its tile ids + id in rect row-major order at its (depth-order) exclusive-scan offset; that
-// offset is also recorded in the GRec: the backward maps (Gaussian, tile) -> record index with
-// it.  Splats touching more than kDupSerial tiles would serialise their wave (a 3-sigma outlier
-// can cover hundreds of tiles), so those are written cooperatively by all 64 lanes of the
-// wave, one ballot bit at a time.
-constexpr int kDupSerial = 16;
 
-template <typename TK>
-__global__ __launch_bounds__(256) void duplicate_kernel(int P, int gx, GRec *__restrict__ rec,
-                                                        const uint32_t *__restrict__ order,
-                                                        const uint32_t *__restrict__ tiles,
-                                                        const uint32_t *__restrict__ offsets, TK *__restrict__ tkeys,
-                                                        uint32_t *__restrict__ vals) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    const int lane = threadIdx.x & (kWave - 1);
-    int x0 = 0, y0 = 0, w = 1, area = 0;
-    uint32_t off = 0, g = 0;
-    if (j < P) {
-        g = order[j];
-        area = (int)tiles[g];
-        if (area > 0) {
-            off = j == 0 ? 0u : offsets[j - 1];
-            const uint4 q3 = reinterpret_cast<const uint4 *>(rec + g)[3];
-            x0 = (int)(q3.x & 0xFFFFu);
-            y0 = (int)(q3.x >> 16);
-            w = (int)q3.y;
-            rec[g].off = off;
-        }
-    }
-    if (area <= kDupSerial) {
-        uint32_t o = off;
-        const int h = area / w;
-        for (int y = y0; y < y0 + h; y++)
-            for (int x = x0; x < x0 + w; x++) {
-                tkeys[o] = (TK)(y * gx + x);
-                vals[o] = g;
-                o++;
-            }
-    }
-    uint64_t big = __ballot(area > kDupSerial);
-    while (big) {
-        const int b = __ffsll((unsigned long long)big) - 1;
-        big &= big - 1;
-        const int bx0 = __shfl(x0, b), by0 = __shfl(y0, b), bw = __shfl(w, b);
-        const int barea = __shfl(area, b);
-        const uint32_t boff = (uint32_t)__shfl((int)off, b);
-        const uint32_t bg = (uint32_t)__shfl((int)g, b);
-        for (int idx = lane; idx < barea; idx += kWave) {
-            const int y = by0 + idx / bw, x = bx0 + idx % bw;
-            tkeys[boff + idx] = (TK)(y * gx + x);
-            vals[boff + idx] = bg;
-        }
-    }
-}
-
-void launch_duplicate(int P, const Camera &cam, const GeomState &gs, const int *radii, const BinningState &bs,
-                      hipStream_t s) {
-    (void)radii;
-    if (P == 0) return;
-    if (bs.wide)
-        hipLaunchKernelGGL(duplicate_kernel<uint32_t>, dim3((P + 255) / 256), dim3(256), 0, s, P, cam.gx, gs.rec,
-                           gs.order, gs.tiles, gs.offsets, static_cast<uint32_t *>(bs.tkeys_unsorted),
-                           bs.vals_unsorted);
-    else
-        hipLaunchKernelGGL(duplicate_kernel<uint16_t>, dim3((P + 255) / 256), dim3(256), 0, s, P, cam.gx, gs.rec,
-                           gs.order, gs.tiles, gs.offsets, static_cast<uint16_t *>(bs.tkeys_unsorted),
-                           bs.vals_unsorted);
-}
-
-template <typename TK>
-__global__ __launch_bounds__(256) void ranges_kernel(int64_t K, const TK *__restrict__ tkeys,
-                                                     uint2 *__restrict__ ranges) {
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= K) return;
-    const uint32_t cur = (uint32_t)tkeys[idx];
-    if (idx == 0) {
-        ranges[cur].x = 0;
-    } else {
-        const uint32_t prev = (uint32_t)tkeys[idx - 1];
-        if (cur != prev) {
-            ranges[prev].y = (uint32_t)idx;
-            ranges[cur].x = (uint32_t)idx;
-        }
-    }
-    if (idx == K - 1) ranges[cur].y = (uint32_t)K;
-}
-
-void launch_ranges(int64_t K, int T, const BinningState &bs, const ImageState &is, hipStream_t s) {
-    (void)hipMemsetAsync(is.ranges, 0, sizeof(uint2) * (size_t)T, s);
-    if (K == 0) return;
-    const dim3 grid((unsigned)((K + 255) / 256));
-    if (bs.wide)
-        hipLaunchKernelGGL(ranges_kernel<uint32_t>, grid, dim3(256), 0, s, K,
-                           static_cast<const uint32_t *>(bs.tkeys_sorted), is.ranges);
-    else
-        hipLaunchKernelGGL(ranges_kernel<uint16_t>, grid, dim3(256), 0, s, K,
-                           static_cast<const uint16_t *>(bs.tkeys_sorted), is.ranges);
-}
 
 __global__ __launch_bounds__(256) void mark_visible_kernel(int P, const float *__restrict__ means3D,
                                                            const float *__restrict__ viewmatrix,

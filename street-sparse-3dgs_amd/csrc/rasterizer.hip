@@ -81,7 +81,7 @@ struct Carver {
     }
 };
 
-GeomState carve_geom(void *base, int P, size_t *bytes) {
+GeomState carve_geom(void *base, int P, int gx, int gy, size_t *bytes) {
     Carver c(base);
     GeomState g;
     g.rec = c.take<GRec>(P);
@@ -95,32 +95,22 @@ GeomState carve_geom(void *base, int P, size_t *bytes) {
     const size_t a = scan_temp_bytes(P), b = depth_sort_temp_bytes(P);
     g.tmp_bytes = a > b ? a : b;
     g.tmp = c.take<char>(g.tmp_bytes);
+    g.drect = c.take<uint2>(P);
+    g.dtiles = c.take<uint32_t>(P);
+    g.sb = sb_grid(gx, gy, P);
+    g.sb_cnt_g = c.take<uint32_t>((size_t)g.sb.nsb * g.sb.nchunks);
+    g.sb_cnt_i = c.take<uint32_t>((size_t)g.sb.nsb * g.sb.nchunks);
+    g.sb_base_g = c.take<uint32_t>((size_t)g.sb.nsb + 1);
+    g.sb_base_i = c.take<uint32_t>((size_t)g.sb.nsb + 1);
     if (bytes) *bytes = align_up(c.off, 256);
     return g;
 }
 
-int bits_for(int n) {  // smallest b with n <= 2^b  (upstream getHigherMsb)
-    int b = 0;
-    while ((1ll << b) < (long long)n) b++;
-    return b;
-}
-
-BinningState carve_binning(void *base, int64_t K, int T, size_t *bytes) {
+BinningState carve_binning(void *base, int64_t K, size_t *bytes) {
     Carver c(base);
     BinningState b;
-    b.wide = T > 65536;
-    const int end_bit = bits_for(T) > 0 ? bits_for(T) : 1;
-    if (b.wide) {
-        b.tkeys_unsorted = c.take<uint32_t>(K);
-        b.tkeys_sorted = c.take<uint32_t>(K);
-    } else {
-        b.tkeys_unsorted = c.take<uint16_t>(K);
-        b.tkeys_sorted = c.take<uint16_t>(K);
-    }
-    b.vals_unsorted = c.take<uint32_t>(K);
+    b.sblist = c.take<uint2>(K);
     b.point_list = c.take<uint32_t>(K);
-    b.sort_tmp_bytes = tile_sort_temp_bytes(K, end_bit, b.wide);
-    b.sort_tmp = c.take<char>(b.sort_tmp_bytes);
     if (bytes) *bytes = align_up(c.off, 256);
     return b;
 }
@@ -134,10 +124,7 @@ ImageState carve_image(void *base, int T, int npix, size_t *bytes) {
     s.n_contrib = c.take<uint32_t>(npix);
     s.tile_work = c.take<uint32_t>(T);
     s.tile_ids = c.take<uint32_t>(T);
-    s.work_sorted = c.take<uint32_t>(T);
     s.tile_order = c.take<uint32_t>(T);
-    s.order_tmp_bytes = tile_order_temp_bytes(T);
-    s.order_tmp = c.take<char>(s.order_tmp_bytes);
     if (bytes) *bytes = align_up(c.off, 256);
     return s;
 }
@@ -257,12 +244,14 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
     const int npix = width * height;
 
     size_t gbytes = 0, ibytes = 0;
-    carve_geom(nullptr, P, &gbytes);
+    carve_geom(nullptr, P, cam.gx, cam.gy, &gbytes);
+    if (!sb_grid_supported(sb_grid(cam.gx, cam.gy, P)))
+        return fail(GSR_ERR_UNSUPPORTED, "image too large for the superblock grid (more than 2048 superblocks of 16x16 tiles)");
     carve_image(nullptr, T, npix, &ibytes);
     void *gbase = geom_buffer(resize_ctx, gbytes);
     void *ibase = image_buffer(resize_ctx, ibytes);
     if (!gbase || !ibase) return fail(GSR_ERR_ALLOCATION, "geometry/image buffer allocation failed");
-    const GeomState gs = carve_geom(gbase, P, nullptr);
+    const GeomState gs = carve_geom(gbase, P, cam.gx, cam.gy, nullptr);
     const ImageState is = carve_image(ibase, T, npix, nullptr);
 
     GaussianInputs in{P, D, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp,
@@ -276,7 +265,8 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
         StageTimer st(1, s);
         if (depth_sort(gs.tmp, gs.tmp_bytes, gs.dkey, gs.dkey_sorted, gs.ids, gs.order, P, s) != hipSuccess)
             return fail(GSR_ERR_DEVICE, "depth sort failed");
-        if (inclusive_scan_gathered(gs.tmp, gs.tmp_bytes, gs.order, gs.tiles, gs.offsets, P, s) != hipSuccess)
+        launch_depth_gather(P, gs, s);
+        if (inclusive_scan(gs.tmp, gs.tmp_bytes, gs.dtiles, gs.offsets, P, s) != hipSuccess)
             return fail(GSR_ERR_DEVICE, "inclusive scan failed");
     }
     if ((rc = check("depth sort / scan", debug, s))) return rc;
@@ -291,36 +281,31 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
         if (hipStreamSynchronize(s) != hipSuccess) return fail(GSR_ERR_DEVICE, "stream sync failed");
         K = (int64_t)*g_pinned;
     }
-    const int end_bit = bits_for(T) > 0 ? bits_for(T) : 1;
     size_t bbytes = 0;
-    carve_binning(nullptr, K, T, &bbytes);
+    carve_binning(nullptr, K, &bbytes);
     void *bbase = binning_buffer(resize_ctx, bbytes);
     if (!bbase) return fail(GSR_ERR_ALLOCATION, "binning buffer allocation failed");
-    const BinningState bs = carve_binning(bbase, K, T, nullptr);
+    const BinningState bs = carve_binning(bbase, K, nullptr);
 
     {
         StageTimer st(2, s);
-        if (K > 0) launch_duplicate(P, cam, gs, radii, bs, s);
+        launch_binning_superblocks(P, cam, gs, bs, is, s);
     }
-    if ((rc = check("duplicateWithKeys", debug, s))) return rc;
+    if ((rc = check("binning (superblocks)", debug, s))) return rc;
     {
         StageTimer st(3, s);
-        if (tile_sort(bs.sort_tmp, bs.sort_tmp_bytes, bs.tkeys_unsorted, bs.tkeys_sorted, bs.vals_unsorted,
-                      bs.point_list, K, end_bit, bs.wide, s) != hipSuccess)
-            return fail(GSR_ERR_DEVICE, "radix sort failed");
+        launch_binning_tiles(P, cam, gs, bs, is, s);
     }
-    if ((rc = check("sort", debug, s))) return rc;
+    if ((rc = check("binning (tiles)", debug, s))) return rc;
     {
         StageTimer st(4, s);
-        launch_ranges(K, T, bs, is, s);
+        launch_tile_order(nullptr, is.ranges, T, 4, is.tile_ids, s);  // forward order: by list length
     }
-    if ((rc = check("identifyTileRanges", debug, s))) return rc;
+    if ((rc = check("tile order", debug, s))) return rc;
     {
         StageTimer st(5, s);
         launch_render_fwd(cam, gs, bs, is, background, out_color, out_invdepth, s);
-        if (tile_order(is.order_tmp, is.order_tmp_bytes, is.tile_work, is.work_sorted, is.tile_ids, is.tile_order, T,
-                       s) != hipSuccess)
-            return fail(GSR_ERR_DEVICE, "tile order sort failed");
+        launch_tile_order(is.tile_work, is.ranges, T, 2, is.tile_order, s);
     }
     if ((rc = check("render", debug, s))) return rc;
     if (num_rendered) *num_rendered = K;
@@ -353,8 +338,8 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
 
     const Camera cam = make_camera(viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, width, height);
     const int T = cam.gx * cam.gy;
-    const GeomState gs = carve_geom(geom_buffer, P, nullptr);
-    const BinningState bs = carve_binning(binning_buffer, R, T, nullptr);
+    const GeomState gs = carve_geom(geom_buffer, P, cam.gx, cam.gy, nullptr);
+    const BinningState bs = carve_binning(binning_buffer, R, nullptr);
     const ImageState is = carve_image(image_buffer, T, width * height, nullptr);
     size_t sbytes = 0;
     carve_bwd(nullptr, R, &sbytes);

@@ -132,10 +132,8 @@ __global__ __launch_bounds__(64) void render_fwd_kernel(
 #pragma unroll
     for (int k = 1; k < kPixPerLane; k++) wl = last[k] > wl ? last[k] : wl;
     wl = wave_max_u32(wl);
-    if (lane == 0) {
-        tile_work[tile] = wl < 0xFFFFu ? wl : 0xFFFFu;
-        tile_ids[tile] = (uint32_t)tile;
-    }
+    if (lane == 0) tile_work[tile] = wl;
+    (void)tile_ids;
     const float b0 = bg[0], b1 = bg[1], b2 = bg[2];
 #pragma unroll
     for (int k = 0; k < kPixPerLane; k++) {
@@ -152,12 +150,160 @@ __global__ __launch_bounds__(64) void render_fwd_kernel(
     }
 }
 
+// Sub-block forward: a 256-thread workgroup per tile, wave w owning the 16x4 sub-block w with one
+// pixel per lane.  Each wave walks the tile's list on its own (gather, cull to its sub-block,
+// ballot-compact into its own LDS slice) and stops when its own 64 pixels saturate, so a heavy
+// tile is spread over four waves and culled sub-blocks cost nothing.  The per-pixel blend is the
+// same as render_fwd_kernel's (bit-identical outputs).
+__global__ __launch_bounds__(256) void render_fwd_sb_kernel(
+    const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list, int W, int H, int gx,
+    const GRec *__restrict__ rec, const float *__restrict__ bg, float *__restrict__ out_color,
+    float *__restrict__ out_invd, float *__restrict__ final_T, uint32_t *__restrict__ n_contrib,
+    uint32_t *__restrict__ tile_work, const uint32_t *__restrict__ fwd_order) {
+    __shared__ float4 s_a[4][kWave];  // x, y, conic.a, conic.b
+    __shared__ float2 s_b[4][kWave];  // conic.c, opacity
+    __shared__ float4 s_c[4][kWave];  // r, g, b, 1/depth
+    __shared__ uint32_t s_pos[4][kWave];
+    __shared__ uint32_t s_work[4];
+
+    const int tile = (int)fwd_order[blockIdx.x];
+    const int tx = tile % gx, ty = tile / gx;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int px = tx * kTile + (lane & 15);
+    const int py = ty * kTile + 4 * w + (lane >> 4);
+    const float pfx = (float)px, pfy = (float)py;
+    const float tx0 = (float)(tx * kTile), sy0 = (float)(ty * kTile + 4 * w);
+    const bool inside = px < W && py < H;
+
+    float T = 1.f, C0 = 0.f, C1 = 0.f, C2 = 0.f, ID = 0.f;
+    uint32_t last = 0;
+    bool alive = inside;
+    const uint2 rg = ranges[tile];
+    for (uint32_t base = rg.x; base < rg.y; base += kWave) {
+        if (!__any(alive)) break;
+        const uint32_t n = min((uint32_t)kWave, rg.y - base);
+        bool hit = false;
+        float4 qa, qb, qc;
+        if ((uint32_t)lane < n) {
+            const uint32_t g = point_list[base + lane];
+            const float4 *R = reinterpret_cast<const float4 *>(rec + g);
+            qa = R[0];
+            qb = R[1];
+            qc = R[2];
+            hit = qa.x + qb.z >= tx0 && qa.x - qb.z <= tx0 + 15.f && qa.y + qb.w >= sy0 && qa.y - qb.w <= sy0 + 3.f;
+        }
+        const uint64_t keep = __ballot(hit);
+        const uint32_t cnt = (uint32_t)__popcll(keep);
+        if (hit) {
+            const uint32_t slot = lane_prefix(keep);
+            s_a[w][slot] = qa;
+            s_b[w][slot] = make_float2(qb.x, qb.y);
+            s_c[w][slot] = qc;
+            s_pos[w][slot] = base - rg.x + (uint32_t)lane + 1u;
+        }
+        // wave-private LDS slice: the wave's own writes are visible after its lgkmcnt drain
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t j = 0; j < cnt; j++) {
+            const float4 a = s_a[w][j];
+            const float2 b = s_b[w][j];
+            const float4 c = s_c[w][j];
+            const uint32_t contributor = __builtin_amdgcn_readfirstlane(s_pos[w][j]);
+            const float dx = a.x - pfx;
+            const float dy = a.y - pfy;
+            const float power = gauss_power(a.z * dx * dx, a.w * dx, b.x, dy);
+            const float alpha = fmin_(0.99f, b.y * gexp2(power * kLog2e));
+            const bool ok = alive && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+            const float test_T = T * (1.f - alpha);
+            const bool stop = test_T < 0.0001f;
+            const bool acc = ok && !stop;
+            alive = alive && !(ok && stop);
+            const float wgt = acc ? alpha * T : 0.f;
+            C0 = fmaf(c.x, wgt, C0);
+            C1 = fmaf(c.y, wgt, C1);
+            C2 = fmaf(c.z, wgt, C2);
+            ID = fmaf(c.w, wgt, ID);
+            T = acc ? test_T : T;
+            last = acc ? contributor : last;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    const uint32_t wl = wave_max_u32(last);
+    if (lane == 0) s_work[w] = wl;
+    if (inside) {
+        const int pix = py * W + px;
+        final_T[pix] = T;
+        n_contrib[pix] = last;
+        out_color[pix] = C0 + T * bg[0];
+        out_color[H * W + pix] = C1 + T * bg[1];
+        out_color[2 * H * W + pix] = C2 + T * bg[2];
+        if (out_invd) out_invd[pix] = ID;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t m = s_work[0];
+        for (int k = 1; k < 4; k++) m = s_work[k] > m ? s_work[k] : m;
+        tile_work[tile] = m;
+    }
+}
+
+#ifndef GSR_FWD_SUBBLOCK
+#define GSR_FWD_SUBBLOCK 1
+#endif
+
+// Launch order for a tile pass, heaviest first (longest-processing-time-first list scheduling):
+// one 1024-thread workgroup buckets the T work estimates into 256 descending classes of
+// 2^shift instances (LDS histogram, scan, scatter).  Order within a class is arbitrary; every
+// tile writes only its own outputs, so results do not depend on it.
+__global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t *__restrict__ work, const uint2 *__restrict__ ranges,
+                                                          int T, int shift, uint32_t *__restrict__ order) {
+    __shared__ uint32_t hist[256];
+    if (threadIdx.x < 256) hist[threadIdx.x] = 0u;
+    __syncthreads();
+    auto bucket = [&](int t) {
+        const uint32_t wk = work ? work[t] : ranges[t].y - ranges[t].x;
+        const uint32_t k = wk >> shift;
+        return 255u - (k < 255u ? k : 255u);
+    };
+    for (int t = threadIdx.x; t < T; t += 1024) atomicAdd(&hist[bucket(t)], 1u);
+    __syncthreads();
+    if (threadIdx.x < 64) {  // exclusive scan of 256 counts, 4 per lane
+        const int l = threadIdx.x;
+        const uint32_t a = hist[4 * l], b = hist[4 * l + 1], c = hist[4 * l + 2], d = hist[4 * l + 3];
+        uint32_t sum = a + b + c + d, incl = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = (uint32_t)__shfl_up((int)incl, o, 64);
+            if (l >= o) incl += v;
+        }
+        const uint32_t ex = incl - sum;
+        hist[4 * l] = ex;
+        hist[4 * l + 1] = ex + a;
+        hist[4 * l + 2] = ex + a + b;
+        hist[4 * l + 3] = ex + a + b + c;
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < T; t += 1024) order[atomicAdd(&hist[bucket(t)], 1u)] = (uint32_t)t;
+}
+
+void launch_tile_order(const uint32_t *work, const uint2 *ranges, int T, int shift, uint32_t *order, hipStream_t s) {
+    if (T == 0) return;
+    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, s, work, ranges, T, shift, order);
+}
+
 void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                        const float *bg, float *out_color, float *out_invdepth, hipStream_t s) {
     const int T = cam.gx * cam.gy;
     if (T == 0) return;
-    hipLaunchKernelGGL(render_fwd_kernel, dim3(T), dim3(kWave), 0, s, is.ranges, bs.point_list, cam.W, cam.H, cam.gx,
-                       gs.rec, bg, out_color, out_invdepth, is.final_T, is.n_contrib, is.tile_work, is.tile_ids);
+    if (GSR_FWD_SUBBLOCK) {  // launch order: is.tile_ids (rasterizer.hip, by list length)
+        hipLaunchKernelGGL(render_fwd_sb_kernel, dim3(T), dim3(4 * kWave), 0, s, is.ranges, bs.point_list, cam.W,
+                           cam.H, cam.gx, gs.rec, bg, out_color, out_invdepth, is.final_T, is.n_contrib, is.tile_work,
+                           is.tile_ids);
+    }
+    else
+        hipLaunchKernelGGL(render_fwd_kernel, dim3(T), dim3(kWave), 0, s, is.ranges, bs.point_list, cam.W, cam.H,
+                           cam.gx, gs.rec, bg, out_color, out_invdepth, is.final_T, is.n_contrib, is.tile_work,
+                           is.tile_ids);
 }
 
 // ------------------------------------------------------------------------------------------

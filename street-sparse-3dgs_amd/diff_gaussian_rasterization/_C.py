@@ -199,7 +199,7 @@ def set_profiling(enable: bool) -> None:
     _L.gsr_set_profiling(int(bool(enable)))
 
 
-STAGES = ("preprocess", "depth_sort_scan", "duplicate", "tile_sort", "ranges", "render_fwd", "render_bwd",
+STAGES = ("preprocess", "depth_sort_scan", "bin_superblocks", "bin_tiles", "tile_order", "render_fwd", "render_bwd",
           "preprocess_bwd")
 
 

@@ -30,13 +30,12 @@ def geom_layout(P):
 
 
 def binning_layout(K, T):
-    ks = 4 if T > 65536 else 2
-    return carve([("tkeys_unsorted", ks * K), ("tkeys_sorted", ks * K), ("vals_unsorted", 4 * K),
-                  ("point_list", 4 * K)])
+    return carve([("sblist", 8 * K), ("point_list", 4 * K)])
 
 
 def image_layout(T, npix):
-    return carve([("ranges", 8 * T), ("boundary", 8 * T), ("final_T", 4 * npix), ("n_contrib", 4 * npix)])
+    return carve([("ranges", 8 * T), ("boundary", 8 * T), ("final_T", 4 * npix), ("n_contrib", 4 * npix),
+                  ("tile_work", 4 * T), ("tile_ids", 4 * T), ("tile_order", 4 * T)])
 
 
 def view(buf_np, layout, name, dtype, shape=None):
@@ -46,6 +45,10 @@ def view(buf_np, layout, name, dtype, shape=None):
 
 
 def decode_state(geom, binning, image, P, K, W, H):
+    """Decode the HIP scratch state.  The HIP binning lays tiles out superblock-major
+    (binning.hip); `point_list` / `ranges` / `keys` are re-expressed in upstream's row-major tile
+    order (each tile's list unchanged) so they compare bit-exactly with the oracle, and the raw
+    layout is returned as `ranges_raw` / `point_list_raw`."""
     g = geom.cpu().numpy()
     b = binning.cpu().numpy()
     im = image.cpu().numpy()
@@ -54,19 +57,26 @@ def decode_state(geom, binning, image, P, K, W, H):
     gl, bl = geom_layout(P), binning_layout(K, T)
     il = image_layout(T, W * H)
     rec = view(g, gl, "rec", np.float32, (P, 16))
-    kt = np.uint32 if T > 65536 else np.uint16
-    tiles_sorted = view(b, bl, "tkeys_sorted", kt).astype(np.uint64)
-    point_list = view(b, bl, "point_list", np.uint32)
+    pl_raw = view(b, bl, "point_list", np.uint32)
+    r_raw = view(im, il, "ranges", np.uint32, (T, 2))
+    lens = (r_raw[:, 1].astype(np.int64) - r_raw[:, 0].astype(np.int64))
+    point_list = np.concatenate([pl_raw[r_raw[t, 0]:r_raw[t, 1]] for t in range(T)]) if K > 0 else \
+        np.zeros(0, np.uint32)
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint32)
+    ranges = np.zeros((T, 2), np.uint32)
+    nz = lens > 0
+    ranges[nz, 0] = starts[nz]
+    ranges[nz, 1] = starts[nz] + lens[nz].astype(np.uint32)
     dbits = rec[:, 14].view(np.uint32)
-    # the 64-bit (tile << 32 | depth bits) keys upstream sorts, rebuilt from the sorted tile ids
-    keys = (tiles_sorted << np.uint64(32)) | dbits[point_list].astype(np.uint64)
+    tile_of = np.repeat(np.arange(T, dtype=np.uint64), np.maximum(lens, 0))
+    # the 64-bit (tile << 32 | depth bits) keys upstream sorts, rebuilt from the per-tile lists
+    keys = (tile_of << np.uint64(32)) | dbits[point_list].astype(np.uint64)
     return dict(
         rec=rec, depths=dbits.view(np.float32).copy(), xy=rec[:, 0:2], conic_opacity=rec[:, 2:6],
         rgbd=rec[:, 8:12], tiles_touched=view(g, gl, "tiles", np.uint32), offsets=view(g, gl, "offsets", np.uint32),
         order=view(g, gl, "order", np.uint32), clamped=view(g, gl, "clamped", np.uint8),
-        keys=keys, vals_unsorted=view(b, bl, "vals_unsorted", np.uint32), point_list=point_list,
-        ranges=view(im, il, "ranges", np.uint32, (gx * gy, 2)), final_T=view(im, il, "final_T", np.float32, (H, W)),
-        n_contrib=view(im, il, "n_contrib", np.uint32, (H, W)))
+        keys=keys, point_list=point_list, ranges=ranges, ranges_raw=r_raw, point_list_raw=pl_raw,
+        final_T=view(im, il, "final_T", np.float32, (H, W)), n_contrib=view(im, il, "n_contrib", np.uint32, (H, W)))
 
 
 def rel_l2(a, b):

@@ -97,6 +97,13 @@ def compare(c, st, g, h, check_grads=True):
     np.testing.assert_array_equal(S["keys"], st["keys"])
     np.testing.assert_array_equal(S["point_list"], st["point_list"])
     np.testing.assert_array_equal(S["ranges"], st["ranges"])
+    # the raw (superblock-major) ranges partition [0, K) exactly
+    r = S["ranges_raw"].astype(np.int64)
+    o = np.argsort(r[:, 0], kind="stable")
+    assert np.all(r[:, 1] >= r[:, 0])
+    rs = r[o]
+    nzr = rs[rs[:, 1] > rs[:, 0]]
+    assert len(nzr) == 0 or (nzr[0, 0] == 0 and nzr[-1, 1] == h["K"] and np.all(nzr[1:, 0] == nzr[:-1, 1]))
     nc_bad = float(np.mean(S["n_contrib"] != st["n_contrib"]))
     assert nc_bad <= 1e-3, f"n_contrib mismatch fraction {nc_bad}"
     assert psnr(h["color"], st["color"]) >= 80.0, psnr(h["color"], st["color"])
