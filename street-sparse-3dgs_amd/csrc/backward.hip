@@ -101,27 +101,22 @@ __device__ __forceinline__ void sh_backward(const float *__restrict__ sh, int M,
 }
 
 
-__global__ __launch_bounds__(256) void preprocess_bwd_kernel(
-    int P, int D, int M, const float *__restrict__ means3D, const int *__restrict__ radii,
-    const float *__restrict__ shs, const uint8_t *__restrict__ clamped, const float *__restrict__ scales,
-    const float *__restrict__ rotations, float mod, const float *__restrict__ cov3D_precomp,
-    const float *__restrict__ viewmatrix, const float *__restrict__ projmatrix, const float *__restrict__ campos_p,
-    float tanx, float tany, float fx, float fy, int gx, const uint32_t *__restrict__ tiles,
-    const GRec *__restrict__ rec, const uint64_t *__restrict__ boundary, BwdScratch sc, GaussianGrads out) {
+// Per-Gaussian sum of its per-tile records (contiguous at its exclusive-scan offset).  A record
+// exists only for tiles where this Gaussian sits in front of the tile's boundary (the last list
+// entry any pixel used, render.hip); elsewhere the instance contributed nothing.  The liveness of
+// all (<= kRedSerial) tiles is gathered first so the boundary loads and then the record loads are
+// issued back to back; larger splats are summed by the whole wave (coalesced loads + DPP).  Kept
+// apart from the chain rule below: this half is memory-latency bound and wants occupancy
+// (few VGPRs), the other half is arithmetic with ~130 VGPRs.
+__global__ __launch_bounds__(256) void record_sum_kernel(int P, int gx, const int *__restrict__ radii,
+                                                         const uint32_t *__restrict__ tiles,
+                                                         const GRec *__restrict__ rec,
+                                                         const uint64_t *__restrict__ boundary, BwdScratch sc,
+                                                         float *__restrict__ dmeans2D, float *__restrict__ dopacity) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & (kWave - 1);
     const bool valid = i < P;
-    const bool has_shs = shs != nullptr;
-    const bool has_scales = cov3D_precomp == nullptr;
     const bool vis = valid && radii[i] > 0;
-    const bool vec_sh = M == 16 && (reinterpret_cast<uintptr_t>(shs) % 16 == 0) &&
-                        (reinterpret_cast<uintptr_t>(out.dsh) % 16 == 0);
-
-    // Sum this Gaussian's per-tile records (contiguous at its exclusive-scan offset).  A record
-    // exists only for tiles where this Gaussian sits in front of the tile's boundary (the last
-    // list entry any pixel used, render.hip); elsewhere the instance contributed nothing.  Runs of
-    // more than kRedSerial tiles are summed by the whole wave (coalesced loads + DPP) so one large
-    // splat does not serialise its 63 neighbours.
     float g[10];
 #pragma unroll
     for (int k = 0; k < 10; k++) g[k] = 0.f;
@@ -145,24 +140,32 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
         acc[8] += c.x; acc[9] += c.y;
     };
     if (n <= kRedSerial && n > 0) {
-        const uint32_t h = n / w;
-        uint32_t u = off;
-        for (uint32_t y = y0; y < y0 + h; y++)
-            for (uint32_t x = x0; x < x0 + w; x++, u++) {
-                const uint64_t bk = boundary[y * (uint32_t)gx + x];
-                if (bk != 0 && key <= bk) accumulate(g, u);
+        uint32_t live = 0, x = x0, y = y0;
+        const uint32_t xe = x0 + w;
+#pragma unroll 4
+        for (uint32_t k = 0; k < n; k++) {
+            const uint64_t bk = boundary[y * (uint32_t)gx + x];
+            live |= (uint32_t)(bk != 0 && key <= bk) << k;
+            if (++x == xe) {
+                x = x0;
+                ++y;
             }
+        }
+        while (live) {
+            const uint32_t k = (uint32_t)__ffs(live) - 1u;
+            live &= live - 1u;
+            accumulate(g, off + k);
+        }
     }
-    uint64_t big = __ballot(n > kRedSerial);
-    while (big) {
+    for (uint64_t big = __ballot(n > kRedSerial); big; big &= big - 1) {
         const int bl = __ffsll((unsigned long long)big) - 1;
-        big &= big - 1;
-        const uint32_t boff = (uint32_t)__shfl((int)off, bl);
-        const uint32_t bn = (uint32_t)__shfl((int)n, bl);
-        const uint32_t bx0 = (uint32_t)__shfl((int)x0, bl), by0 = (uint32_t)__shfl((int)y0, bl);
-        const uint32_t bw = (uint32_t)__shfl((int)w, bl);
-        const uint64_t bkey = ((uint64_t)(uint32_t)__shfl((int)(key >> 32), bl) << 32) |
-                              (uint32_t)__shfl((int)(uint32_t)key, bl);
+        const uint32_t boff = (uint32_t)__builtin_amdgcn_readlane((int)off, bl);
+        const uint32_t bn = (uint32_t)__builtin_amdgcn_readlane((int)n, bl);
+        const uint32_t bx0 = (uint32_t)__builtin_amdgcn_readlane((int)x0, bl);
+        const uint32_t by0 = (uint32_t)__builtin_amdgcn_readlane((int)y0, bl);
+        const uint32_t bw = (uint32_t)__builtin_amdgcn_readlane((int)w, bl);
+        const uint64_t bkey = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(key >> 32), bl) << 32) |
+                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key, bl);
         float q[10];
 #pragma unroll
         for (int k = 0; k < 10; k++) q[k] = 0.f;
@@ -178,10 +181,42 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
         }
     }
     if (!valid) return;
-    out.dmeans2D[3 * i + 0] = g[0];
-    out.dmeans2D[3 * i + 1] = g[1];
-    out.dmeans2D[3 * i + 2] = 0.f;
-    out.dopacity[i] = g[5];
+    dmeans2D[3 * i + 0] = g[0];
+    dmeans2D[3 * i + 1] = g[1];
+    dmeans2D[3 * i + 2] = 0.f;
+    dopacity[i] = g[5];
+    sc.gsum[2 * (size_t)i] = make_float4(g[2], g[3], g[4], g[9]);
+    sc.gsum[2 * (size_t)i + 1] = make_float4(g[6], g[7], g[8], 0.f);
+}
+
+__global__ __launch_bounds__(256) void preprocess_bwd_kernel(
+    int P, int D, int M, const float *__restrict__ means3D, const int *__restrict__ radii,
+    const float *__restrict__ shs, const uint8_t *__restrict__ clamped, const float *__restrict__ scales,
+    const float *__restrict__ rotations, float mod, const float *__restrict__ cov3D_precomp,
+    const float *__restrict__ viewmatrix, const float *__restrict__ projmatrix, const float *__restrict__ campos_p,
+    float tanx, float tany, float fx, float fy, int gx, const uint32_t *__restrict__ tiles,
+    const GRec *__restrict__ rec, const uint64_t *__restrict__ boundary, BwdScratch sc, GaussianGrads out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & (kWave - 1);
+    const bool valid = i < P;
+    const bool has_shs = shs != nullptr;
+    const bool has_scales = cov3D_precomp == nullptr;
+    const bool vis = valid && radii[i] > 0;
+    const bool vec_sh = M == 16 && (reinterpret_cast<uintptr_t>(shs) % 16 == 0) &&
+                        (reinterpret_cast<uintptr_t>(out.dsh) % 16 == 0);
+
+    if (!valid) return;
+    float g[10];
+    {
+        const float4 s0 = sc.gsum[2 * (size_t)i], s1 = sc.gsum[2 * (size_t)i + 1];
+        g[0] = g[1] = g[5] = 0.f;  // screen-space mean and opacity: written by record_sum_kernel
+        g[2] = s0.x; g[3] = s0.y; g[4] = s0.z; g[9] = s0.w;
+        g[6] = s1.x; g[7] = s1.y; g[8] = s1.z;
+        if (vis) {
+            g[0] = out.dmeans2D[3 * i + 0];
+            g[1] = out.dmeans2D[3 * i + 1];
+        }
+    }
 
     float dm[3] = {0.f, 0.f, 0.f};
     float dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -365,6 +400,8 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
 void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const GeomState &gs, const ImageState &is,
                            const int *radii, const BwdScratch &sc, const GaussianGrads &out, hipStream_t s) {
     if (in.P == 0) return;
+    hipLaunchKernelGGL(record_sum_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, cam.gx, radii, gs.tiles,
+                       gs.rec, is.boundary, sc, out.dmeans2D, out.dopacity);
     hipLaunchKernelGGL(preprocess_bwd_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, in.D, in.M, in.means3D,
                        radii, in.shs, gs.clamped, in.scales, in.rotations, in.scale_modifier, in.cov3D_precomp,
                        cam.view, cam.proj, cam.campos, cam.tanx, cam.tany, cam.fx, cam.fy, cam.gx, gs.tiles, gs.rec,

@@ -378,6 +378,7 @@ struct ImageState {
 // Only instances at list positions below their tile's boundary are written.
 struct BwdScratch {
     float4 *rec;
+    float4 *gsum;  // per Gaussian: {dconic a, b, c, dinvdepth}, {drgb r, g, b, 0} (record_sum -> preprocess_bwd)
 };
 
 }  // namespace gsr

@@ -129,10 +129,11 @@ ImageState carve_image(void *base, int T, int npix, size_t *bytes) {
     return s;
 }
 
-BwdScratch carve_bwd(void *base, int64_t K, size_t *bytes) {
+BwdScratch carve_bwd(void *base, int64_t K, int P, size_t *bytes) {
     Carver c(base);
     BwdScratch s;
     s.rec = c.take<float4>(4 * (size_t)K);
+    s.gsum = c.take<float4>(2 * (size_t)P);
     if (bytes) *bytes = align_up(c.off, 256);
     return s;
 }
@@ -342,10 +343,10 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
     const BinningState bs = carve_binning(binning_buffer, R, nullptr);
     const ImageState is = carve_image(image_buffer, T, width * height, nullptr);
     size_t sbytes = 0;
-    carve_bwd(nullptr, R, &sbytes);
+    carve_bwd(nullptr, R, P, &sbytes);
     void *sbase = scratch(resize_ctx, sbytes);
     if (!sbase) return fail(GSR_ERR_ALLOCATION, "backward scratch allocation failed");
-    const BwdScratch sc = carve_bwd(sbase, R, nullptr);
+    const BwdScratch sc = carve_bwd(sbase, R, P, nullptr);
 
     GaussianInputs in{P, D, M, means3D, shs, colors_precomp, nullptr, scales, rotations, cov3D_precomp,
                       scale_modifier};
