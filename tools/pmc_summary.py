@@ -18,9 +18,14 @@ import os
 import re
 from collections import defaultdict
 
-STAGE_OF = [("render_bwd_kernel", "render_bwd"), ("render_fwd_kernel", "render_fwd"),
-            ("preprocess_bwd_kernel", "preprocess_bwd"), ("preprocess_kernel", "preprocess"),
-            ("duplicate_kernel", "duplicate"), ("ranges_kernel", "ranges"), ("mark_visible", "mark_visible")]
+STAGE_OF = [("render_bwd_kernel", "render_bwd"), ("render_fwd", "render_fwd"),
+            ("preprocess_bwd_kernel", "preprocess_bwd"), ("record_sum_kernel", "record_sum"),
+            ("preprocess_kernel", "preprocess"), ("depth_gather_kernel", "depth_gather"),
+            ("sb_count_kernel", "bin_superblocks:count"), ("sb_colscan_kernel", "bin_superblocks:colscan"),
+            ("sb_base_kernel", "bin_superblocks:base"), ("sb_scatter_kernel", "bin_superblocks:scatter"),
+            ("tile_bin_kernel", "bin_tiles"), ("tile_order_kernel", "tile_order"), ("mark_visible", "mark_visible"),
+            ("l1_ssim_fwd", "loss_fwd"), ("l1_ssim_bwd", "loss_bwd"), ("sparse_adam", "adam"),
+            ("exposure_", "exposure"), ("densify_stats", "densify")]
 # rocPRIM kernels are all `trampoline_kernel<wrapped_<algo>_config<cfg, KeyT, ...>>`: the algorithm
 # and key type tell the depth sort (u32 keys over P) from the tile sort (u16 keys over K).
 ROCPRIM = re.compile(r"wrapped_(\w+?)_config<[^,]+(?:<[^>]*>)?, (unsigned \w+)")
