@@ -41,6 +41,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--diag", action="store_true", help="print synced per-step fwd/bwd wall times to stderr")
     ap.add_argument("--train-steps", type=int, default=10, help="timed train-step harness iterations (0 = skip)")
+    ap.add_argument("--config5", action="store_true",
+                    help="also time config 5: hierarchy cut blend + forward render of the cut at 1080p")
+    ap.add_argument("--c5-nodes", type=int, default=50_000_000)
+    ap.add_argument("--c5-cut", type=int, default=5_000_000)
     ap.add_argument("--train-baseline", action="store_true",
                     help="also time the reference-structured torch train step (conv2d SSIM, OurAdam gather/scatter)")
     return ap.parse_args()
@@ -124,6 +128,52 @@ def train_step_ms(s, W, H, deg, steps, warmup, fused, dev):
     del ts, g
     torch.cuda.empty_cache()
     return ms
+
+
+def config5(a, dev):
+    """render_hierarchy.py's per-frame work on a synthetic merged
+    hierarchy -- render_post's LOD blend of the cut (fused kernel) and the forward render of the
+    cut at 1920x1080 (no_grad, do_depth), timed together per frame."""
+    import torch
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    from gs_train.hier import interpolate_cut
+    from gs_train.synthetic import synthetic_hierarchy
+    W, H = a.width, a.height
+    h = synthetic_hierarchy(a.c5_nodes, a.c5_cut, 100_000, W, H, dev, seed=5)
+    t = lambda x: torch.tensor(x, dtype=torch.float32, device=dev)
+    rs = GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=float(h["tanfovx"]), tanfovy=float(h["tanfovy"]), bg=t([0, 0, 0]),
+        scale_modifier=1.0, viewmatrix=t(h["view"]).reshape(4, 4), projmatrix=t(h["proj"]).reshape(4, 4),
+        sh_degree=3, campos=t(h["campos"]), prefiltered=False, debug=False, do_depth=True,
+        render_indices=torch.empty(0, dtype=torch.int32), parent_indices=torch.empty(0, dtype=torch.int32),
+        interpolation_weights=h["interpolation_weights"],
+        num_node_kids=torch.ones(a.c5_nodes, dtype=torch.int32, device=dev))
+    raster = GaussianRasterizer(rs)
+
+    def frame():
+        with torch.no_grad():
+            m, sc, rot, op, sh = interpolate_cut(h["means3D"], h["scales"], h["rotations"], h["opacities"], h["shs"],
+                                                 h["render_indices"], h["parent_indices"],
+                                                 h["interpolation_weights"], h["skybox"])
+            return raster(means3D=m, means2D=torch.zeros_like(m), shs=sh, colors_precomp=None, opacities=op,
+                          scales=sc, rotations=rot, cov3D_precomp=None)
+
+    for _ in range(3):
+        frame()
+    torch.cuda.synchronize()
+    n = 10
+    t0 = time.perf_counter()
+    for _ in range(n):
+        color, radii, _ = frame()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / n * 1e3
+    out = {"ms_per_frame": round(ms, 3), "fwd_mpix_s": round(W * H / ms / 1e3, 1), "nodes": a.c5_nodes,
+           "rendered": a.c5_cut + 100_000, "visible": int((radii > 0).sum().item()), "width": W, "height": H,
+           "workload": "render_post LOD blend (fused) + rasterizer forward of the cut, no_grad, do_depth",
+           "data": "synthetic hierarchy generated on the device (random cut; .hier / expand_to_size unavailable)"}
+    del h, raster
+    torch.cuda.empty_cache()
+    return out
 
 
 def latest_traffic(kernel):
@@ -280,6 +330,8 @@ def main():
         if a.train_baseline:
             tr["reference_structured_ms"] = round(train_step_ms(s, W, H, deg, a.train_steps, 3, False, dev), 4)
         out["train_step"] = tr
+    if a.config5:
+        out["config5"] = config5(a, dev)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(s, P, W, H, deg)
     if rank == 0:

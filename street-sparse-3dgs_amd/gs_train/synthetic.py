@@ -86,3 +86,31 @@ def orbit_cameras(n, W, H, fovx_deg=60.0, radius_deg=4.0, shift=0.3):
         t = np.array([shift * math.sin(a * 7), shift * math.cos(b * 7) - shift, 0.0])
         cams.append(camera(W, H, fovx_deg, R=Rw2c.T, t=t))
     return cams
+
+
+def synthetic_hierarchy(N, R, S, W, H, device, seed=0, sh_degree=3, fovx_deg=60.0, zmin=2.0, zmax=40.0,
+                        log_scale_mean=-4.5, log_scale_std=0.5):
+    """Config-5 stand-in: N hierarchy nodes generated on the device (torch), a cut
+    of R rendered nodes with random parents and blend weights, and S skybox Gaussians at the end.
+    The node attributes are *activated* tensors, as render_post reads them (pc.get_xyz, ...).
+    The merged .hier files and expand_to_size are not available here, so the cut
+    is random: what it stresses is the size of the gather and of the rendered set."""
+    import torch
+    g = torch.Generator(device=device).manual_seed(seed)
+    view, proj, campos, tx, ty = camera(W, H, fovx_deg)
+    u = lambda *s: torch.rand(*s, generator=g, device=device)
+    z = zmin + (zmax - zmin) * u(N)
+    means = torch.stack([(u(N) * 1.9 - 0.95) * tx * z, (u(N) * 1.9 - 0.95) * ty * z, z], 1)
+    scales = torch.exp(log_scale_mean + log_scale_std * torch.randn(N, 3, generator=g, device=device))
+    q = torch.randn(N, 4, generator=g, device=device)
+    q = q / q.norm(dim=1, keepdim=True)
+    opac = 0.05 + 0.94 * u(N, 1)
+    M = 16 if sh_degree == 3 else max((sh_degree + 1) ** 2, 1)
+    shs = 0.05 * torch.randn(N, M, 3, generator=g, device=device)
+    shs[:, 0, :] = 0.5 * torch.randn(N, 3, generator=g, device=device)
+    ri = torch.randperm(N - S, generator=g, device=device)[:R].int()
+    pi = torch.randint(0, N - S, (R,), generator=g, device=device).int()
+    w = u(N)
+    return dict(means3D=means, scales=scales, rotations=q, opacities=opac, shs=shs, render_indices=ri,
+                parent_indices=pi, interpolation_weights=w, skybox=S, view=view, proj=proj, campos=campos,
+                tanfovx=tx, tanfovy=ty, W=W, H=H, sh_degree=sh_degree)
