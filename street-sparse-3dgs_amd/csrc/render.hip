@@ -309,6 +309,11 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
 // ------------------------------------------------------------------------------------------
 // Backward
 // ------------------------------------------------------------------------------------------
+// Per pixel the replay keeps only S = sum_c A_c dL/dpix_c (not the four accumulated channels) and
+// sums G dL/dalpha moments in dy (sum u, sum u dy, sum u dy^2); the lane's dx, the opacity and
+// the conic are applied once per instance after the k loop / the wave sum.  37 instead of 52
+// VALU per active (instance, pixel), 104 instead of 152 VGPRs: 0.35 vs 0.48 ms.
+//
 // Sub-blocks an instance cannot touch (ellipse box, or past the sub-block's last contributor) are
 // skipped with a scalar branch on the wave-uniform mask: 0.479 vs 0.502 ms for the predicated
 // form on the 1M-Gaussian 1080p bench scene once tiles run heaviest-first.
@@ -320,6 +325,9 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
 #endif
 #ifndef GSR_BWD_BRANCH
 #define GSR_BWD_BRANCH 1
+#endif
+#ifndef GSR_BWD_FACTORED
+#define GSR_BWD_FACTORED 1
 #endif
 template <bool kDepth>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVES_PER_EU))) void render_bwd_kernel(
@@ -345,7 +353,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
     const float b0 = bg[0], b1 = bg[1], b2 = bg[2];
 
     float T[kPixPerLane], TfB[kPixPerLane], dp0[kPixPerLane], dp1[kPixPerLane], dp2[kPixPerLane], did[kPixPerLane];
+#if GSR_BWD_FACTORED
+    // S = sum_c A_c dL/dpix_c: the colour (and inverse depth) accumulated behind the current
+    // instance, already dotted with the pixel's upstream gradient -- the only form dL/dalpha needs
+    float S[kPixPerLane], pfy[kPixPerLane];
+#else
     float A0[kPixPerLane], A1[kPixPerLane], A2[kPixPerLane], Ai[kPixPerLane], pfy[kPixPerLane];
+#endif
     uint32_t last[kPixPerLane], lastk[kPixPerLane];
     uint32_t maxlast = 0;
 #pragma unroll
@@ -360,7 +374,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
         dp1[k] = inside ? dL_dpix[H * W + pix] : 0.f;
         dp2[k] = inside ? dL_dpix[2 * H * W + pix] : 0.f;
         did[k] = (kDepth && inside) ? dL_dinvd[pix] : 0.f;
+#if GSR_BWD_FACTORED
+        S[k] = 0.f;
+#else
         A0[k] = A1[k] = A2[k] = Ai[k] = 0.f;
+#endif
         // background term of dL/dalpha: -T_final / (1 - alpha) * (bg . dL/dpix)
         TfB[k] = -T[k] * (b0 * dp0[k] + b1 * dp1[k] + b2 * dp2[k]);
         lastk[k] = wave_max_u32(last[k]);  // sub-block k needs list positions < lastk[k]
@@ -437,10 +455,30 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
                 const bool ok = ((mk >> k) & 1u) && jpos < last[k] && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
                 any = any || ok;
                 const float ae = ok ? alpha : 0.f;
-                const float Ge = ok ? G : 0.f;
                 const float rc = __builtin_amdgcn_rcpf(1.f - ae);
                 T[k] = T[k] * rc;
                 const float dch = ae * T[k];
+#if GSR_BWD_FACTORED
+                // dL/dalpha colour part: sum_c (c_c - A_c) dp_c = (c . dp) - S;  S += alpha (c . dp - S)
+                float cd = fmaf(c.z, dp2[k], fmaf(c.y, dp1[k], c.x * dp0[k]));
+                if (kDepth) cd = fmaf(c.w, did[k], cd);
+                const float dlac = cd - S[k];
+                S[k] = fmaf(ae, dlac, S[k]);
+                q[6] = fmaf(dch, dp0[k], q[6]);
+                q[7] = fmaf(dch, dp1[k], q[7]);
+                q[8] = fmaf(dch, dp2[k], q[8]);
+                if (kDepth) q[9] = fmaf(dch, did[k], q[9]);
+                float dla = fmaf(TfB[k], rc, dlac * T[k]);
+                // u = G dL/dalpha: the conic / mean terms are opacity * u times (dx, dy) moments,
+                // summed here as sum u, sum u dy, sum u dy^2 (dx is the lane's column: applied
+                // once per instance below; opacity and the conic after the wave sum)
+                const float u = ok ? G * dla : 0.f;
+                q[5] += u;
+                const float uy = u * dy;
+                q[1] += uy;
+                q[4] = fmaf(uy, dy, q[4]);
+#else
+                const float Ge = ok ? G : 0.f;
                 const float d0 = c.x - A0[k];
                 float dla = d0 * dp0[k];
                 A0[k] = fmaf(ae, d0, A0[k]);
@@ -470,7 +508,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
                 q[3] = fmaf(tg, dy, q[3]);
                 q[4] = fmaf(dLdG * gdy, dy, q[4]);
                 q[5] = fmaf(Ge, dla, q[5]);
+#endif
             }
+#if GSR_BWD_FACTORED
+            // lane moments in dx: q0 = sum u dx, q2 = sum u dx^2, q3 = sum u dx dy (q1 = sum u dy,
+            // q4 = sum u dy^2, q5 = sum u)
+            q[0] = dx * q[5];
+            q[2] = dx * q[0];
+            q[3] = dx * q[1];
+#endif
             // Half-wave sums only (5 DPP stages); lanes 16 and 48 park the two partials in LDS
             // and they are added once per batch below instead of per instance.
             if (__any(any)) wave_halfsum<kDepth ? 10 : 9>(q);
@@ -491,6 +537,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
                 r[2 * t + 1] = p0.y + p1.y;
             }
             const size_t o = 4 * (size_t)s_u[lane];
+#if GSR_BWD_FACTORED
+            {
+                // moments -> (dmean2D, dconic): dL/dG = opacity dL/dalpha, dG/d(dx) = -G (a dx + b dy), ...
+                const float4 ia = s_a[lane];
+                const float4 ib = s_b[lane];
+                const float op = ib.y, ca = ia.z, cb = ia.w, cc = ib.x;
+                const float m0 = r[0], m1 = r[1], mxx = r[2], mxy = r[3], myy = r[4];
+                r[0] = -op * fmaf(cb, m1, ca * m0);
+                r[1] = -op * fmaf(cb, m0, cc * m1);
+                r[2] = op * mxx;
+                r[3] = op * mxy;
+                r[4] = op * myy;
+            }
+#endif
             out[o + 0] = make_float4(r[0] * sx, r[1] * sy, -0.5f * r[2], -0.5f * r[3]);
             out[o + 1] = make_float4(-0.5f * r[4], r[5], r[6], r[7]);
             out[o + 2] = make_float4(r[8], r[9], 0.f, 0.f);

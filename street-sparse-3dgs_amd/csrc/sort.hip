@@ -16,8 +16,19 @@ namespace gsr {
 namespace {
 // rocPRIM routes radix sorts of up to 2^20 items through block-sort + 10 merge passes; for the
 // P ~ 1M depth keys that is ~150 us/frame on MI355X vs a few onesweep passes.  Cap the merge path.
+#ifndef GSR_DEPTH_RADIX_BITS
+#define GSR_DEPTH_RADIX_BITS 0
+#endif
+#if GSR_DEPTH_RADIX_BITS
+using OnesweepCfg = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 12>, rocprim::kernel_config<256, 12>,
+                                        GSR_DEPTH_RADIX_BITS>,
+    8192>;
+#else
 using OnesweepCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
                                                rocprim::default_config, 8192>;
+#endif
 
 }  // namespace
 
