@@ -176,6 +176,34 @@ __device__ __forceinline__ float sh_channel(int deg, const float *sh, float x, f
     return r + 0.5f;
 }
 
+// True if some pixel centre of the box [x0, x1] x [y0, y1] may reach alpha >= 1/255, i.e. the
+// conic form Q(d) = a dx^2 + 2 b dx dy + c dy^2 (power = -Q/2) gets down to tau = 2 ln(255 op)
+// somewhere on the box.  The minimum of the convex Q over a box not containing the centre lies on
+// a face turned towards the centre; each face is a 1-D quadratic minimised in closed form.  A
+// relative + absolute margin on tau keeps the test conservative against the kernels' float
+// evaluation of power and exp, so culling with it never changes an output.
+__device__ __forceinline__ bool ellipse_meets_box(float cx, float cy, float a, float b, float c, float op, float x0,
+                                                  float x1, float y0, float y1) {
+    if (!(a > 0.f && c > 0.f)) return true;
+    const float X0 = x0 - cx, X1 = x1 - cx, Y0 = y0 - cy, Y1 = y1 - cy;
+    const bool outx = X0 > 0.f || X1 < 0.f, outy = Y0 > 0.f || Y1 < 0.f;
+    if (!outx && !outy) return true;
+    const float tau = 2.f * 0.6931471805599453f * __builtin_amdgcn_logf(255.f * op);  // v_log_f32 = log2
+    const float tm = fmaf(fabsf(tau), 1.0e-3f, tau) + 1.0e-2f;
+    float q = 3.0e38f;
+    if (outx) {
+        const float xe = X0 > 0.f ? X0 : X1;
+        const float ys = fminf(fmaxf(-b * xe / c, Y0), Y1);
+        q = fminf(q, fmaf(a * xe, xe, fmaf(2.f * b * xe, ys, c * ys * ys)));
+    }
+    if (outy) {
+        const float ye = Y0 > 0.f ? Y0 : Y1;
+        const float xs = fminf(fmaxf(-b * ye / a, X0), X1);
+        q = fminf(q, fmaf(a * xs, xs, fmaf(2.f * b * xs, ye, c * ye * ye)));
+    }
+    return q <= tm;
+}
+
 // ------------------------------------------------------------------------------------------
 // Wave64 primitives (DPP; no LDS)
 // ------------------------------------------------------------------------------------------

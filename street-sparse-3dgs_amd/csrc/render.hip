@@ -26,14 +26,22 @@ namespace gsr {
 
 __device__ __forceinline__ float gexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
-__device__ __forceinline__ uint32_t sub_block_mask(float X, float Y, float ex, float ey, float tx0, float ty0) {
-    // bit k: the alpha >= 1/255 ellipse box of the instance overlaps pixel rows ty0+4k..ty0+4k+3
+#ifndef GSR_EXACT_CULL
+#define GSR_EXACT_CULL 3  // bit 0: forward, bit 1: backward
+#endif
+
+__device__ __forceinline__ uint32_t sub_block_mask(const float4 &qa, const float4 &qb, float tx0, float ty0) {
+    // bit k: the alpha >= 1/255 ellipse of the instance (its box, then the ellipse itself) meets
+    // pixel rows ty0+4k..ty0+4k+3
+    const float X = qa.x, Y = qa.y, ex = qb.z, ey = qb.w;
     if (!(X + ex >= tx0 && X - ex <= tx0 + 15.f)) return 0u;
     uint32_t m = 0;
 #pragma unroll
     for (int k = 0; k < kPixPerLane; k++) {
         const float y0 = ty0 + (float)(4 * k);
-        if (Y + ey >= y0 && Y - ey <= y0 + 3.f) m |= 1u << k;
+        if (Y + ey >= y0 && Y - ey <= y0 + 3.f &&
+            (!(GSR_EXACT_CULL & 2) || ellipse_meets_box(X, Y, qa.z, qa.w, qb.x, qb.y, tx0, tx0 + 15.f, y0, y0 + 3.f)))
+            m |= 1u << k;
     }
     return m;
 }
@@ -85,7 +93,7 @@ __global__ __launch_bounds__(64) void render_fwd_kernel(
             qa = R[0];
             qb = R[1];
             qc = R[2];
-            m = sub_block_mask(qa.x, qa.y, qb.z, qb.w, tx0, ty0);
+            m = sub_block_mask(qa, qb, tx0, ty0);
         }
         const uint64_t keep = __ballot(m != 0u);
         const uint32_t cnt = (uint32_t)__popcll(keep);
@@ -160,10 +168,9 @@ __global__ __launch_bounds__(256) void render_fwd_sb_kernel(
     const GRec *__restrict__ rec, const float *__restrict__ bg, float *__restrict__ out_color,
     float *__restrict__ out_invd, float *__restrict__ final_T, uint32_t *__restrict__ n_contrib,
     uint32_t *__restrict__ tile_work, const uint32_t *__restrict__ fwd_order) {
-    __shared__ float4 s_a[4][kWave];  // x, y, conic.a, conic.b
-    __shared__ float2 s_b[4][kWave];  // conic.c, opacity
-    __shared__ float4 s_c[4][kWave];  // r, g, b, 1/depth
-    __shared__ uint32_t s_pos[4][kWave];
+    // per wave, three 64-entry planes: {x, y, conic.a, conic.b}, {conic.c, opacity, -, -},
+    // {r, g, b, 1/depth}; one base address serves all three (offsets 0 / 1 / 2 KiB)
+    __shared__ float4 s_q[4][3][kWave];
     __shared__ uint32_t s_work[4];
 
     const int tile = (int)fwd_order[blockIdx.x];
@@ -190,25 +197,31 @@ __global__ __launch_bounds__(256) void render_fwd_sb_kernel(
             qa = R[0];
             qb = R[1];
             qc = R[2];
-            hit = qa.x + qb.z >= tx0 && qa.x - qb.z <= tx0 + 15.f && qa.y + qb.w >= sy0 && qa.y - qb.w <= sy0 + 3.f;
+            hit = qa.x + qb.z >= tx0 && qa.x - qb.z <= tx0 + 15.f && qa.y + qb.w >= sy0 && qa.y - qb.w <= sy0 + 3.f &&
+                  (!(GSR_EXACT_CULL & 1) ||
+                   ellipse_meets_box(qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, tx0, tx0 + 15.f, sy0, sy0 + 3.f));
         }
         const uint64_t keep = __ballot(hit);
         const uint32_t cnt = (uint32_t)__popcll(keep);
         if (hit) {
             const uint32_t slot = lane_prefix(keep);
-            s_a[w][slot] = qa;
-            s_b[w][slot] = make_float2(qb.x, qb.y);
-            s_c[w][slot] = qc;
-            s_pos[w][slot] = base - rg.x + (uint32_t)lane + 1u;
+            s_q[w][0][slot] = qa;
+            s_q[w][1][slot] = qb;
+            s_q[w][2][slot] = qc;
         }
         // wave-private LDS slice: the wave's own writes are visible after its lgkmcnt drain
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
+        // the j-th compacted entry is the j-th set bit of `keep`: its list position comes from a
+        // scalar bit scan, not from LDS
+        uint64_t rem = keep;
+        const uint32_t pos0 = base - rg.x + 1u;
         for (uint32_t j = 0; j < cnt; j++) {
-            const float4 a = s_a[w][j];
-            const float2 b = s_b[w][j];
-            const float4 c = s_c[w][j];
-            const uint32_t contributor = __builtin_amdgcn_readfirstlane(s_pos[w][j]);
+            const float4 a = s_q[w][0][j];
+            const float4 b = s_q[w][1][j];
+            const float4 c = s_q[w][2][j];
+            const uint32_t contributor = pos0 + (uint32_t)__builtin_ctzll(rem);
+            rem &= rem - 1ull;
             const float dx = a.x - pfx;
             const float dy = a.y - pfy;
             const float power = gauss_power(a.z * dx * dx, a.w * dx, b.x, dy);
@@ -408,7 +421,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
             qc = R[2];
             const uint4 q3 = reinterpret_cast<const uint4 *>(rec + g)[3];
             u = q3.w + (uint32_t)((ty - (int)(q3.x >> 16)) * (int)q3.y + (tx - (int)(q3.x & 0xFFFFu)));
-            m = sub_block_mask(qa.x, qa.y, qb.z, qb.w, tx0, ty0);
+            m = sub_block_mask(qa, qb, tx0, ty0);
 #pragma unroll
             for (int k = 0; k < kPixPerLane; k++)
                 if (pos >= lastk[k]) m &= ~(1u << k);
