@@ -80,9 +80,11 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
  * dL_dpix (3,H,W); dL_dinvdepth (1,H,W) or NULL (no depth gradient).  `scratch` provides
  * the per-tile-instance gradient workspace.  Every output row is written (zeros where
  * radii == 0 and beyond the active SH degree), so outputs need no pre-zeroing:
- *   dL_dmeans2D (P,3)  dL_dcolors (P,3)  dL_dopacity (P,1)  dL_dmeans3D (P,3)
- *   dL_dcov3D (P,6)  dL_dsh (P,M,3) [ignored if shs == NULL]
- *   dL_dscales (P,3)  dL_drotations (P,4) [ignored if scales == NULL] */
+ *   dL_dmeans2D (P,3)  dL_dcolors (P,3) [may be NULL when shs != NULL]  dL_dopacity (P,1)
+ *   dL_dmeans3D (P,3)  dL_dcov3D (P,6) [may be NULL when cov3D_precomp == NULL]
+ *   dL_dsh (P,M,3) [ignored if shs == NULL]
+ *   dL_dscales (P,3)  dL_drotations (P,4) [ignored if scales == NULL]
+ * (the optional ones are identically zero there: the caller need not allocate them) */
 int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D, int M, int64_t R,
                            const float *background, int width, int height, const float *means3D,
                            const float *shs, const float *colors_precomp, const float *scales,

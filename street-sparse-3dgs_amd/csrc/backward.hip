@@ -142,7 +142,7 @@ __global__ __launch_bounds__(256) void record_sum_kernel(int P, int gx, const in
     if (n <= kRedSerial && n > 0) {
         uint32_t live = 0, x = x0, y = y0;
         const uint32_t xe = x0 + w;
-#pragma unroll 4
+#pragma unroll 8
         for (uint32_t k = 0; k < n; k++) {
             const uint64_t bk = boundary[y * (uint32_t)gx + x];
             live |= (uint32_t)(bk != 0 && key <= bk) << k;
@@ -339,9 +339,11 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
             dm[1] += (-dor[0] * dor[1] * gd[0] + (s2 - dor[1] * dor[1]) * gd[1] - dor[2] * dor[1] * gd[2]) * inv32;
             dm[2] += (-dor[0] * dor[2] * gd[0] - dor[1] * dor[2] * gd[1] + (s2 - dor[2] * dor[2]) * gd[2]) * inv32;
         }
-        out.dcolors[3 * i + 0] = 0.f;
-        out.dcolors[3 * i + 1] = 0.f;
-        out.dcolors[3 * i + 2] = 0.f;
+        if (out.dcolors) {  // optional with shs (no colors_precomp input to differentiate)
+            out.dcolors[3 * i + 0] = 0.f;
+            out.dcolors[3 * i + 1] = 0.f;
+            out.dcolors[3 * i + 2] = 0.f;
+        }
     } else {
         out.dcolors[3 * i + 0] = g[6];
         out.dcolors[3 * i + 1] = g[7];
@@ -389,8 +391,9 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
         out.dscales[3 * i + 1] = ds[1];
         out.dscales[3 * i + 2] = ds[2];
         reinterpret_cast<float4 *>(out.drots)[i] = make_float4(dq[0], dq[1], dq[2], dq[3]);
+        if (out.dcov3D)  // optional with scales/rotations (no cov3D_precomp input)
 #pragma unroll
-        for (int k = 0; k < 6; k++) out.dcov3D[6 * i + k] = 0.f;
+            for (int k = 0; k < 6; k++) out.dcov3D[6 * i + k] = 0.f;
     } else {
 #pragma unroll
         for (int k = 0; k < 6; k++) out.dcov3D[6 * i + k] = dcov[k];

@@ -331,7 +331,8 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
     if (!geom_buffer || !binning_buffer || !image_buffer || !dL_dpix)
         return fail(GSR_ERR_INVALID_ARGUMENT, "NULL state buffer / dL_dpix");
     if (P > 0 && !radii) return fail(GSR_ERR_INVALID_ARGUMENT, "NULL radii");
-    if (P > 0 && (!dL_dmeans2D || !dL_dcolors || !dL_dopacity || !dL_dmeans3D || !dL_dcov3D))
+    if (P > 0 && (!dL_dmeans2D || !dL_dopacity || !dL_dmeans3D || (!shs && !dL_dcolors) ||
+                  (cov3D_precomp && !dL_dcov3D)))
         return fail(GSR_ERR_INVALID_ARGUMENT, "NULL gradient output");
     if (P > 0 && shs && !dL_dsh) return fail(GSR_ERR_INVALID_ARGUMENT, "NULL dL_dsh");
     if (P > 0 && !cov3D_precomp && (!dL_dscales || !dL_drotations))

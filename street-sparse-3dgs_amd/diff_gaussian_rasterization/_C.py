@@ -160,20 +160,26 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     radii_c = radii.contiguous()
 
     e = lambda *shape: torch.empty(*shape, dtype=torch.float32, device=dev)
-    dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D = e(P, 3), e(P, 3), e(P, 1), e(P, 3), e(P, 6)
+    # gradients of inputs that were not given are identically zero: returned as zero-stride views
+    # (upstream's shapes, no memory traffic) and not computed by the kernels
+    z = lambda *shape: torch.zeros(1, dtype=torch.float32, device=dev).expand(*shape)
+    dL_dmeans2D, dL_dopacity, dL_dmeans3D = e(P, 3), e(P, 1), e(P, 3)
+    dL_dcolors = e(P, 3) if sh_c is None else z(P, 3)
+    dL_dcov3D = e(P, 6) if cov_c is not None else z(P, 6)
     dL_dsh = e(P, M, 3) if sh_c is not None else torch.zeros(P, 0, 3, device=dev)
     if cov_c is None:
         dL_dscales, dL_drotations = e(P, 3), e(P, 4)
     else:
-        dL_dscales, dL_drotations = torch.zeros(P, 3, device=dev), torch.zeros(P, 4, device=dev)
+        dL_dscales, dL_drotations = z(P, 3), z(P, 4)
     res = _Resizer(dev)
     with torch.cuda.device(dev):
         rc = _L.gsr_rasterize_backward(
             res.fn("scratch"), None, P, int(degree), M, int(R), _ptr(bg_c), W, H, _ptr(means3D_c), _ptr(sh_c),
             _ptr(colors_c), _ptr(scales_c), float(scale_modifier), _ptr(rots_c), _ptr(cov_c), _ptr(view_c),
             _ptr(proj_c), _ptr(campos_c), float(tan_fovx), float(tan_fovy), _ptr(radii_c), _ptr(geomBuffer),
-            _ptr(binningBuffer), _ptr(imageBuffer), _ptr(dpix), _ptr(dinv), _ptr(dL_dmeans2D), _ptr(dL_dcolors),
-            _ptr(dL_dopacity), _ptr(dL_dmeans3D), _ptr(dL_dcov3D), _ptr(dL_dsh) if sh_c is not None else None,
+            _ptr(binningBuffer), _ptr(imageBuffer), _ptr(dpix), _ptr(dinv), _ptr(dL_dmeans2D),
+            _ptr(dL_dcolors) if sh_c is None else None, _ptr(dL_dopacity), _ptr(dL_dmeans3D),
+            _ptr(dL_dcov3D) if cov_c is not None else None, _ptr(dL_dsh) if sh_c is not None else None,
             _ptr(dL_dscales) if cov_c is None else None, _ptr(dL_drotations) if cov_c is None else None,
             int(bool(debug)), _stream(dev))
     res.release()
