@@ -43,6 +43,16 @@ int gsr_l1_ssim_forward(const float *img, const float *gt, int C, int H, int W, 
 int gsr_l1_ssim_backward(const float *img, const float *gt, int C, int H, int W, const float *dL_dout,
                          float *dL_dimg, void *stream);
 
+/* Training form of the pair above.  _forward_with_map computes out (as gsr_l1_ssim_forward, same
+ * scratch) and, in the same pass, the per-pixel field G = d(sum of the SSIM map)/dimg into
+ * ssim_grad_map (C, H, W); dL/dimg is linear in dL_dout, so _backward_from_map is then the
+ * elementwise dL_dimg = (dL_dout[0] sign(img - gt) + dL_dout[1] G) / (C H W), equal to
+ * gsr_l1_ssim_backward's result.  One halo recomputation per step instead of two. */
+int gsr_l1_ssim_forward_with_map(const float *img, const float *gt, int C, int H, int W, void *scratch, float *out,
+                                 float *ssim_grad_map, void *stream);
+int gsr_l1_ssim_backward_from_map(const float *img, const float *gt, const float *ssim_grad_map, int C, int H, int W,
+                                  const float *dL_dout, float *dL_dimg, void *stream);
+
 /* One parameter group of the sparse Adam step: a (P, width) row-major parameter with its grad
  * and moment buffers.  step_size = lr / (1 - beta1^step) and bias_correction2_sqrt =
  * sqrt(1 - beta2^step) are computed by the host in double, exactly as OurAdam does. */

@@ -17,6 +17,7 @@
 // relevance (opacity grad != 0) per row on the device.
 #include <cmath>
 #include <cstring>
+#include <algorithm>
 #include <string>
 
 #include "../../include/gsr.h"
@@ -67,67 +68,92 @@ __device__ __forceinline__ void ssim_partials(const Moments &s, float &a, float 
     const float s1 = s.a11 - mu1_sq, s2 = s.a22 - mu2_sq, s12 = s.a12 - mu12;
     const float n1 = 2.f * mu12 + kC1, n2 = 2.f * s12 + kC2;
     const float d1 = mu1_sq + mu2_sq + kC1, d2 = s1 + s2 + kC2;
+    // one division: S / d2 = S d1 inv and S / d1 = S d2 inv
     const float inv = 1.f / (d1 * d2);
     const float S = n1 * n2 * inv;
-    const float ds1 = -S / d2;
+    const float Sinv = S * inv;
+    const float ds1 = -Sinv * d1;
     const float ds12 = 2.f * n1 * inv;
-    const float dmu = 2.f * s.m2 * n2 * inv - 2.f * s.m1 * S / d1;
+    const float dmu = 2.f * s.m2 * n2 * inv - 2.f * s.m1 * (Sinv * d2);
     a = dmu - 2.f * s.m1 * ds1 - s.m2 * ds12;
     b = ds1;
     c = ds12;
 }
 
-// Load a rows x cols region of one plane with origin (oy, ox), zero outside the image.
+// LDS layout: every staged map is row-major with an odd row pitch (an odd number of floats), so
+// the passes below, whose 32-lane halves walk down consecutive rows of a map, touch 32
+// different banks.
+constexpr int odd_pitch(int cols) { return cols | 1; }
+
+// Load a rows x cols region of one plane with origin (oy, ox), zero outside the image, into a
+// map of row pitch `pitch`.
 __device__ __forceinline__ void load_halo(const float *__restrict__ x, const float *__restrict__ y, int H, int W,
-                                          int oy, int ox, int rows, int cols, float *sx, float *sy) {
+                                          int oy, int ox, int rows, int cols, int pitch, float *sx, float *sy) {
     for (int i = threadIdx.x; i < rows * cols; i += kLossThreads) {
         const int r = i / cols, c = i - r * cols;
         const int gy = oy + r, gx = ox + c;
         const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
         const size_t o = (size_t)gy * W + gx;
-        sx[i] = in ? x[o] : 0.f;
-        sy[i] = in ? y[o] : 0.f;
+        sx[r * pitch + c] = in ? x[o] : 0.f;
+        sy[r * pitch + c] = in ? y[o] : 0.f;
     }
 }
 
-// Horizontal pass of the five moments: out[q][r][c] = sum_j w_j f_q(in[r][c + j]).
-__device__ __forceinline__ void hpass5(const float *sx, const float *sy, int rows, int in_cols, int out_cols,
-                                       const Window &win, float *hs) {
-    const int plane = rows * out_cols;
-    for (int i = threadIdx.x; i < plane; i += kLossThreads) {
-        const int r = i / out_cols, c = i - r * out_cols;
-        const float *px = sx + r * in_cols + c, *py = sy + r * in_cols + c;
-        float m1 = 0.f, m2 = 0.f, a11 = 0.f, a22 = 0.f, a12 = 0.f;
+// Horizontal pass of the five moments: out[q][r][c] = sum_j w_j f_q(in[r][c + j]).  A task is a
+// kS-column segment of one row: kS + 10 inputs are loaded once into registers, so LDS reads drop
+// from 22 per output to (2 kS + 20) / kS.  Consecutive tasks (lanes) take consecutive rows.
+template <int kS>
+__device__ __forceinline__ void hpass5(const float *sx, const float *sy, int rows, int in_cols, int in_pitch,
+                                       int out_cols, int out_pitch, int plane, const Window &win, float *hs) {
+    const int segs = (out_cols + kS - 1) / kS;
+    for (int task = threadIdx.x; task < rows * segs; task += kLossThreads) {
+        const int s = task / rows, r = task - s * rows, c0 = s * kS;
+        const float *px = sx + r * in_pitch + c0, *py = sy + r * in_pitch + c0;
+        float u[kS + 2 * kR], v[kS + 2 * kR];
 #pragma unroll
-        for (int j = 0; j < 2 * kR + 1; j++) {
-            const float a = px[j], b = py[j], w = win.w[j];
-            m1 = fmaf(w, a, m1);
-            m2 = fmaf(w, b, m2);
-            a11 = fmaf(w, a * a, a11);
-            a22 = fmaf(w, b * b, a22);
-            a12 = fmaf(w, a * b, a12);
+        for (int k = 0; k < kS + 2 * kR; k++) {
+            const bool ok = c0 + k < in_cols;
+            u[k] = ok ? px[k] : 0.f;
+            v[k] = ok ? py[k] : 0.f;
         }
-        hs[i] = m1;
-        hs[plane + i] = m2;
-        hs[2 * plane + i] = a11;
-        hs[3 * plane + i] = a22;
-        hs[4 * plane + i] = a12;
+#pragma unroll
+        for (int o = 0; o < kS; o++) {
+            float m1 = 0.f, m2 = 0.f, a11 = 0.f, a22 = 0.f, a12 = 0.f;
+#pragma unroll
+            for (int j = 0; j < 2 * kR + 1; j++) {
+                const float w = win.w[j];
+                m1 = fmaf(w, u[o + j], m1);
+                m2 = fmaf(w, v[o + j], m2);
+                a11 = fmaf(w, u[o + j] * u[o + j], a11);
+                a22 = fmaf(w, v[o + j] * v[o + j], a22);
+                a12 = fmaf(w, u[o + j] * v[o + j], a12);
+            }
+            if (c0 + o < out_cols) {
+                const int i = r * out_pitch + c0 + o;
+                hs[i] = m1;
+                hs[plane + i] = m2;
+                hs[2 * plane + i] = a11;
+                hs[3 * plane + i] = a22;
+                hs[4 * plane + i] = a12;
+            }
+        }
     }
 }
 
 // Vertical pass for the 64 x 16 output tile: lane column c = tid & 63 and four consecutive rows
 // r0..r0+3 per thread, a 14-row sliding window per quantity.
 template <int NQ>
-__device__ __forceinline__ void vpass_tile(const float *hs, int plane, const Window &win, float (&acc)[NQ][4]) {
+__device__ __forceinline__ void vpass_tile(const float *hs, int pitch, int plane, const Window &win,
+                                           float (&acc)[NQ][4]) {
     const int c = threadIdx.x & 63, r0 = (threadIdx.x >> 6) * 4;
 #pragma unroll
     for (int q = 0; q < NQ; q++) {
 #pragma unroll
         for (int k = 0; k < 4; k++) acc[q][k] = 0.f;
-        const float *h = hs + q * plane + r0 * kTW + c;
+        const float *h = hs + q * plane + r0 * pitch + c;
 #pragma unroll
         for (int t = 0; t < 2 * kR + 4; t++) {
-            const float v = h[t * kTW];
+            const float v = h[t * pitch];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 const int j = t - k;
@@ -150,27 +176,31 @@ __device__ __forceinline__ float block_sum(float v, float *red) {
 }
 
 constexpr int kFwdRH = kTH + 2 * kR, kFwdRW = kTW + 2 * kR;  // 26 x 74 input halo
-constexpr size_t kFwdLds = sizeof(float) * (2 * kFwdRH * kFwdRW + 5 * kFwdRH * kTW + 8);
+constexpr int kFwdIP = odd_pitch(kFwdRW), kFwdHP = odd_pitch(kTW);
+constexpr size_t kFwdLds = sizeof(float) * (2 * kFwdRH * kFwdIP + 5 * kFwdRH * kFwdHP + 8);
 
 __global__ __launch_bounds__(kLossThreads) void l1_ssim_fwd_kernel(const float *__restrict__ x,
                                                                     const float *__restrict__ y, int H, int W,
                                                                     Window win, float2 *__restrict__ partials) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float *sx = reinterpret_cast<float *>(smem);
-    float *sy = sx + kFwdRH * kFwdRW;
-    float *hs = sy + kFwdRH * kFwdRW;
-    float *red = hs + 5 * kFwdRH * kTW;
+    float *sy = sx + kFwdRH * kFwdIP;
+    float *hs = sy + kFwdRH * kFwdIP;
+    float *red = hs + 5 * kFwdRH * kFwdHP;
     const size_t plane_off = (size_t)blockIdx.z * H * W;
     x += plane_off;
     y += plane_off;
     const int ox = blockIdx.x * kTW, oy = blockIdx.y * kTH;
 
-    load_halo(x, y, H, W, oy - kR, ox - kR, kFwdRH, kFwdRW, sx, sy);
+    load_halo(x, y, H, W, oy - kR, ox - kR, kFwdRH, kFwdRW, kFwdIP, sx, sy);
     __syncthreads();
-    hpass5(sx, sy, kFwdRH, kFwdRW, kTW, win, hs);
+#ifndef GSR_SSIM_FWD_SEG
+#define GSR_SSIM_FWD_SEG 8
+#endif
+    hpass5<GSR_SSIM_FWD_SEG>(sx, sy, kFwdRH, kFwdRW, kFwdIP, kTW, kFwdHP, kFwdRH * kFwdHP, win, hs);  // 26 x 8 tasks
     __syncthreads();
     float acc[5][4];
-    vpass_tile<5>(hs, kFwdRH * kTW, win, acc);
+    vpass_tile<5>(hs, kFwdHP, kFwdRH * kFwdHP, win, acc);
 
     const int c = threadIdx.x & 63, r0 = (threadIdx.x >> 6) * 4;
     float l1 = 0.f, ss = 0.f;
@@ -180,7 +210,7 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_fwd_kernel(const float *
         if (gy < H && gx < W) {
             const Moments m{acc[0][k], acc[1][k], acc[2][k], acc[3][k], acc[4][k]};
             ss += ssim_value(m);
-            const int li = (r0 + k + kR) * kFwdRW + c + kR;
+            const int li = (r0 + k + kR) * kFwdIP + c + kR;
             l1 += fabsf(sx[li] - sy[li]);
         }
     }
@@ -218,18 +248,28 @@ __global__ __launch_bounds__(1024) void loss_finalize_kernel(const float2 *__res
 
 constexpr int kBwdIH = kTH + 4 * kR, kBwdIW = kTW + 4 * kR;  // 36 x 84 inputs
 constexpr int kBwdSH = kTH + 2 * kR, kBwdSW = kTW + 2 * kR;  // 26 x 74 SSIM-map positions
-constexpr size_t kBwdLds = sizeof(float) * (2 * kBwdIH * kBwdIW + 5 * kBwdIH * kBwdSW);
-static_assert(3 * kBwdSH * kBwdSW <= 2 * kBwdIH * kBwdIW, "a/b/c maps alias the input halo");
-static_assert(3 * kBwdSH * kTW <= 5 * kBwdIH * kBwdSW, "second horizontal pass aliases the moments");
+constexpr int kBwdIP = odd_pitch(kBwdIW), kBwdSP = odd_pitch(kBwdSW), kBwdTP = odd_pitch(kTW);
+constexpr int kBwdVS = 9;  // rows per task of the vertical stats pass; its last task reads one row past the moments
+constexpr size_t kBwdLds = sizeof(float) * (2 * kBwdIH * kBwdIP + 5 * kBwdIH * kBwdSP + kBwdSP);
+static_assert(3 * kBwdVS - 1 + 2 * kR <= kBwdIH, "vertical stats pass reads at most one row past the moments");
+static_assert(3 * kBwdSH * kBwdSP <= 2 * kBwdIH * kBwdIP, "a/b/c maps alias the input halo");
+static_assert(3 * kBwdSH * kBwdTP <= 5 * kBwdIH * kBwdSP, "second horizontal pass aliases the moments");
 
-__global__ __launch_bounds__(kLossThreads) void l1_ssim_bwd_kernel(const float *__restrict__ x,
-                                                                    const float *__restrict__ y, int H, int W,
-                                                                    Window win, const float *__restrict__ dout,
-                                                                    float inv_n, float *__restrict__ dx) {
+// kMap = false: dx = dL/d(img) for the upstream 2-vector dout (the backward proper).
+// kMap = true: the forward with the gradient field: per block the L1 and SSIM sums (as
+// l1_ssim_fwd_kernel) and per pixel G = dSSIM_sum/dx (unscaled), from which the backward is the
+// elementwise dx = (dout[0] sign(x - y) + dout[1] G) / n.  dL/dx is linear in dout, so a training
+// step pays the halo recomputation once instead of twice.
+template <bool kMap>
+__global__ __launch_bounds__(kLossThreads) void l1_ssim_grad_kernel(const float *__restrict__ x,
+                                                                     const float *__restrict__ y, int H, int W,
+                                                                     Window win, const float *__restrict__ dout,
+                                                                     float inv_n, float *__restrict__ dx,
+                                                                     float2 *__restrict__ partials) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float *sx = reinterpret_cast<float *>(smem);
-    float *sy = sx + kBwdIH * kBwdIW;
-    float *hs = sy + kBwdIH * kBwdIW;
+    float *sy = sx + kBwdIH * kBwdIP;
+    float *hs = sy + kBwdIH * kBwdIP;
     float *abc = sx;  // after the first horizontal pass the halo is dead
     float *h3 = hs;   // after the vertical pass the moments are dead
     const size_t plane_off = (size_t)blockIdx.z * H * W;
@@ -237,54 +277,80 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_bwd_kernel(const float *
     y += plane_off;
     dx += plane_off;
     const int ox = blockIdx.x * kTW, oy = blockIdx.y * kTH;
-    const float g_l1 = dout[0] * inv_n, g_ssim = dout[1] * inv_n;
+    const float g_l1 = kMap ? 0.f : dout[0] * inv_n, g_ssim = kMap ? 0.f : dout[1] * inv_n;
+    float ss = 0.f;  // kMap: SSIM summed over this thread's interior positions
+    constexpr int hp = kBwdIH * kBwdSP, sp = kBwdSH * kBwdSP, tp = kBwdSH * kBwdTP;
 
-    load_halo(x, y, H, W, oy - 2 * kR, ox - 2 * kR, kBwdIH, kBwdIW, sx, sy);
+    load_halo(x, y, H, W, oy - 2 * kR, ox - 2 * kR, kBwdIH, kBwdIW, kBwdIP, sx, sy);
     __syncthreads();
-    hpass5(sx, sy, kBwdIH, kBwdIW, kBwdSW, win, hs);
+    hpass5<12>(sx, sy, kBwdIH, kBwdIW, kBwdIP, kBwdSW, kBwdSP, hp, win, hs);  // 36 x 7 tasks
     __syncthreads();
     // Moments and dS/d(moment) at every SSIM-map position the tile's gradient reads; positions
-    // outside the image have no SSIM term (zero).
-    constexpr int sp = kBwdSH * kBwdSW, hp = kBwdIH * kBwdSW;
-    for (int i = threadIdx.x; i < sp; i += kLossThreads) {
-        const int r = i / kBwdSW, c = i - r * kBwdSW;
-        const int gy = oy - kR + r, gx = ox - kR + c;
-        float a = 0.f, b = 0.f, cc = 0.f;
-        if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
-            float m[5];
+    // outside the image have no SSIM term (zero).  A task is a kVS-row column segment: kVS + 10
+    // rows of the five horizontal moments are read once.
+    constexpr int kVS = kBwdVS, rsegs = (kBwdSH + kVS - 1) / kVS;  // 74 x 3 tasks
+    for (int task = threadIdx.x; task < kBwdSW * rsegs; task += kLossThreads) {
+        const int sg = task / kBwdSW, c = task - sg * kBwdSW, r0 = sg * kVS;
+        float m[5][kVS];
 #pragma unroll
-            for (int q = 0; q < 5; q++) {
-                const float *h = hs + q * hp + r * kBwdSW + c;
-                float s = 0.f;
+        for (int q = 0; q < 5; q++) {
 #pragma unroll
-                for (int j = 0; j < 2 * kR + 1; j++) s = fmaf(win.w[j], h[j * kBwdSW], s);
-                m[q] = s;
+            for (int o = 0; o < kVS; o++) m[q][o] = 0.f;
+            const float *h = hs + q * hp + r0 * kBwdSP + c;
+#pragma unroll
+            for (int t = 0; t < kVS + 2 * kR; t++) {
+                const float v = h[t * kBwdSP];  // rows past kBwdIH only feed discarded outputs
+#pragma unroll
+                for (int o = 0; o < kVS; o++) {
+                    const int j = t - o;
+                    if (j >= 0 && j <= 2 * kR) m[q][o] = fmaf(win.w[j], v, m[q][o]);
+                }
             }
-            ssim_partials(Moments{m[0], m[1], m[2], m[3], m[4]}, a, b, cc);
         }
-        abc[i] = a;
-        abc[sp + i] = b;
-        abc[2 * sp + i] = cc;
+        const int gx = ox - kR + c;
+        const bool col_in = gx >= 0 && gx < W;
+#pragma unroll
+        for (int o = 0; o < kVS; o++) {
+            const int r = r0 + o, gy = oy - kR + r;
+            float a, b, cc;
+            ssim_partials(Moments{m[0][o], m[1][o], m[2][o], m[3][o], m[4][o]}, a, b, cc);
+            const bool in = col_in && gy >= 0 && gy < H;
+            if (kMap && in && r >= kR && r < kR + kTH && c >= kR && c < kR + kTW)
+                ss += ssim_value(Moments{m[0][o], m[1][o], m[2][o], m[3][o], m[4][o]});
+            if (r < kBwdSH) {
+                const int i = r * kBwdSP + c;
+                abc[i] = in ? a : 0.f;
+                abc[sp + i] = in ? b : 0.f;
+                abc[2 * sp + i] = in ? cc : 0.f;
+            }
+        }
     }
     __syncthreads();
     // Horizontal pass of the three partial maps (the window is symmetric: the transposed
-    // convolution is the same correlation).
-    constexpr int tp = kBwdSH * kTW;
-    for (int i = threadIdx.x; i < tp; i += kLossThreads) {
-        const int r = i >> 6, c = i & 63;
+    // convolution is the same correlation), 8-column segments, lanes down consecutive rows.
+    constexpr int kHS = 8, csegs = kTW / kHS;  // 26 x 8 tasks
+    for (int task = threadIdx.x; task < kBwdSH * csegs; task += kLossThreads) {
+        const int sg = task / kBwdSH, r = task - sg * kBwdSH, c0 = sg * kHS;
 #pragma unroll
         for (int q = 0; q < 3; q++) {
-            const float *p = abc + q * sp + r * kBwdSW + c;
-            float s = 0.f;
+            const float *p = abc + q * sp + r * kBwdSP + c0;
+            float v[kHS + 2 * kR];
 #pragma unroll
-            for (int j = 0; j < 2 * kR + 1; j++) s = fmaf(win.w[j], p[j], s);
-            h3[q * tp + i] = s;
+            for (int k = 0; k < kHS + 2 * kR; k++) v[k] = p[k];
+#pragma unroll
+            for (int o = 0; o < kHS; o++) {
+                float sum = 0.f;
+#pragma unroll
+                for (int j = 0; j < 2 * kR + 1; j++) sum = fmaf(win.w[j], v[o + j], sum);
+                h3[q * tp + r * kBwdTP + c0 + o] = sum;
+            }
         }
     }
     __syncthreads();
     float acc[3][4];
-    vpass_tile<3>(h3, tp, win, acc);
+    vpass_tile<3>(h3, kBwdTP, tp, win, acc);
     const int c = threadIdx.x & 63, r0 = (threadIdx.x >> 6) * 4;
+    float l1 = 0.f;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int gy = oy + r0 + k, gx = ox + c;
@@ -292,10 +358,55 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_bwd_kernel(const float *
             const size_t o = (size_t)gy * W + gx;
             const float xv = x[o], yv = y[o];
             const float d = xv - yv;
-            const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
-            dx[o] = g_l1 * sgn + g_ssim * (acc[0][k] + 2.f * xv * acc[1][k] + yv * acc[2][k]);
+            const float G = acc[0][k] + 2.f * xv * acc[1][k] + yv * acc[2][k];
+            if (kMap) {
+                dx[o] = G;
+                l1 += fabsf(d);
+            } else {
+                const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+                dx[o] = g_l1 * sgn + g_ssim * G;
+            }
         }
     }
+    if (kMap) {
+        float *red = sx;  // the a/b/c maps are dead after the second horizontal pass
+        l1 = block_sum(l1, red);
+        ss = block_sum(ss, red + 4);
+        if (threadIdx.x == 0) {
+            const int b = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+            partials[b] = make_float2(l1, ss);
+        }
+    }
+}
+
+// dx = (dout[0] sign(x - y) + dout[1] G) / n from the field l1_ssim_grad_kernel<true> stored.
+__global__ __launch_bounds__(256) void l1_ssim_bwd_map_kernel(const float4 *__restrict__ x, const float4 *__restrict__ y,
+                                                              const float4 *__restrict__ G, int64_t n4,
+                                                              const float *__restrict__ dout, float inv_n,
+                                                              float4 *__restrict__ dx) {
+    const float g_l1 = dout[0] * inv_n, g_ssim = dout[1] * inv_n;
+    const auto one = [&](float xv, float yv, float gv) {
+        const float d = xv - yv;
+        const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+        return g_l1 * sgn + g_ssim * gv;
+    };
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+        const float4 a = x[i], b = y[i], g = G[i];
+        dx[i] = make_float4(one(a.x, b.x, g.x), one(a.y, b.y, g.y), one(a.z, b.z, g.z), one(a.w, b.w, g.w));
+    }
+}
+
+__global__ __launch_bounds__(256) void l1_ssim_bwd_map_tail_kernel(const float *__restrict__ x,
+                                                                   const float *__restrict__ y,
+                                                                   const float *__restrict__ G, int64_t begin,
+                                                                   int64_t n, const float *__restrict__ dout,
+                                                                   float inv_n, float *__restrict__ dx) {
+    const int64_t i = begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float g_l1 = dout[0] * inv_n, g_ssim = dout[1] * inv_n;
+    const float d = x[i] - y[i];
+    const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+    dx[i] = g_l1 * sgn + g_ssim * G[i];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -456,6 +567,15 @@ dim3 loss_grid(int C, int H, int W) { return dim3((W + kTW - 1) / kTW, (H + kTH 
 
 bool g_lds_attr = false;
 
+void set_lds_attr() {
+    if (g_lds_attr) return;
+    (void)hipFuncSetAttribute((const void *)l1_ssim_grad_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kBwdLds);
+    (void)hipFuncSetAttribute((const void *)l1_ssim_grad_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kBwdLds);
+    g_lds_attr = true;
+}
+
 }  // namespace
 }  // namespace gsr
 
@@ -476,11 +596,7 @@ int gsr_l1_ssim_forward(const float *img, const float *gt, int C, int H, int W, 
         return GSR_ERR_INVALID_ARGUMENT;
     }
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (!g_lds_attr) {
-        (void)hipFuncSetAttribute((const void *)l1_ssim_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)kBwdLds);
-        g_lds_attr = true;
-    }
+    set_lds_attr();
     const dim3 g = loss_grid(C, H, W);
     const int nb = (int)(g.x * g.y * g.z);
     float2 *part = static_cast<float2 *>(scratch);
@@ -501,16 +617,66 @@ int gsr_l1_ssim_backward(const float *img, const float *gt, int C, int H, int W,
         return GSR_ERR_INVALID_ARGUMENT;
     }
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (!g_lds_attr) {
-        (void)hipFuncSetAttribute((const void *)l1_ssim_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)kBwdLds);
-        g_lds_attr = true;
-    }
-    hipLaunchKernelGGL(l1_ssim_bwd_kernel, loss_grid(C, H, W), dim3(kLossThreads), kBwdLds, s, img, gt, H, W,
-                       ssim_window(), dL_dout, (float)(1.0 / ((double)C * H * W)), dL_dimg);
+    set_lds_attr();
+    hipLaunchKernelGGL(l1_ssim_grad_kernel<false>, loss_grid(C, H, W), dim3(kLossThreads), kBwdLds, s, img, gt, H, W,
+                       ssim_window(), dL_dout, (float)(1.0 / ((double)C * H * W)), dL_dimg, nullptr);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_last_error(std::string("gsr_l1_ssim_backward: ") + hipGetErrorString(e));
+        return GSR_ERR_DEVICE;
+    }
+    return GSR_OK;
+}
+
+int gsr_l1_ssim_forward_with_map(const float *img, const float *gt, int C, int H, int W, void *scratch, float *out,
+                                 float *ssim_grad_map, void *stream) {
+    if (C <= 0 || H <= 0 || W <= 0 || !img || !gt || !scratch || !out || !ssim_grad_map) {
+        set_last_error("gsr_l1_ssim_forward_with_map: empty image or NULL pointer");
+        return GSR_ERR_INVALID_ARGUMENT;
+    }
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    set_lds_attr();
+    const dim3 g = loss_grid(C, H, W);
+    const int nb = (int)(g.x * g.y * g.z);
+    float2 *part = static_cast<float2 *>(scratch);
+    hipLaunchKernelGGL(l1_ssim_grad_kernel<true>, g, dim3(kLossThreads), kBwdLds, s, img, gt, H, W, ssim_window(),
+                       nullptr, 0.f, ssim_grad_map, part);
+    hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(1024), 0, s, part, nb, 1.0 / ((double)C * H * W), out);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_last_error(std::string("gsr_l1_ssim_forward_with_map: ") + hipGetErrorString(e));
+        return GSR_ERR_DEVICE;
+    }
+    return GSR_OK;
+}
+
+int gsr_l1_ssim_backward_from_map(const float *img, const float *gt, const float *ssim_grad_map, int C, int H, int W,
+                                  const float *dL_dout, float *dL_dimg, void *stream) {
+    if (C <= 0 || H <= 0 || W <= 0 || !img || !gt || !ssim_grad_map || !dL_dout || !dL_dimg) {
+        set_last_error("gsr_l1_ssim_backward_from_map: empty image or NULL pointer");
+        return GSR_ERR_INVALID_ARGUMENT;
+    }
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int64_t n = (int64_t)C * H * W;
+    const float inv_n = (float)(1.0 / (double)n);
+    const bool vec = ((reinterpret_cast<uintptr_t>(img) | reinterpret_cast<uintptr_t>(gt) |
+                       reinterpret_cast<uintptr_t>(ssim_grad_map) | reinterpret_cast<uintptr_t>(dL_dimg)) & 15) == 0;
+    const int64_t n4 = vec ? n / 4 : 0;
+    if (n4 > 0) {
+        const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 256 * 8);
+        hipLaunchKernelGGL(l1_ssim_bwd_map_kernel, dim3(blocks), dim3(256), 0, s,
+                           reinterpret_cast<const float4 *>(img), reinterpret_cast<const float4 *>(gt),
+                           reinterpret_cast<const float4 *>(ssim_grad_map), n4, dL_dout, inv_n,
+                           reinterpret_cast<float4 *>(dL_dimg));
+    }
+    if (4 * n4 < n) {
+        const int64_t rest = n - 4 * n4;
+        hipLaunchKernelGGL(l1_ssim_bwd_map_tail_kernel, dim3((unsigned)((rest + 255) / 256)), dim3(256), 0, s, img, gt,
+                           ssim_grad_map, 4 * n4, n, dL_dout, inv_n, dL_dimg);
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_last_error(std::string("gsr_l1_ssim_backward_from_map: ") + hipGetErrorString(e));
         return GSR_ERR_DEVICE;
     }
     return GSR_OK;

@@ -1,5 +1,6 @@
 """Fused photometric loss: mean |img - gt| and mean SSIM (11x11 Gaussian window, sigma 1.5) in one
-gfx950 launch each way (csrc/train.hip), replacing utils/loss_utils.py:17-18 (l1_loss) and
+gfx950 launch each way (in training the forward also stores the SSIM gradient field and the
+backward is elementwise) (csrc/train.hip), replacing utils/loss_utils.py:17-18 (l1_loss) and
 :33-63 (ssim: five depthwise conv2d + elementwise ops) as combined at train_single.py:121-123.
 
 Gradients flow only to `img` (the rendered image); `gt` is a constant, as in the reference.
@@ -31,20 +32,33 @@ class _L1SSIM(torch.autograd.Function):
         L = lib()
         out = torch.empty(2, dtype=torch.float32, device=img.device)
         scratch = torch.empty(max(1, L.gsr_l1_ssim_scratch_bytes(C, H, W)), dtype=torch.uint8, device=img.device)
-        check(L.gsr_l1_ssim_forward(ptr(img), ptr(gt), C, H, W, ptr(scratch), ptr(out), stream(img.device)),
-              "gsr_l1_ssim_forward")
-        ctx.save_for_backward(img, gt)
+        s = stream(img.device)
+        if ctx.needs_input_grad[0]:
+            # training: the forward also stores the SSIM gradient field, the backward is elementwise
+            gmap = torch.empty_like(img)
+            check(L.gsr_l1_ssim_forward_with_map(ptr(img), ptr(gt), C, H, W, ptr(scratch), ptr(out), ptr(gmap), s),
+                  "gsr_l1_ssim_forward_with_map")
+            ctx.save_for_backward(img, gt, gmap)
+        else:
+            check(L.gsr_l1_ssim_forward(ptr(img), ptr(gt), C, H, W, ptr(scratch), ptr(out), s), "gsr_l1_ssim_forward")
+            ctx.save_for_backward(img, gt)
         ctx.dims = (C, H, W)
         return out
 
     @staticmethod
     def backward(ctx, gout):
-        img, gt = ctx.saved_tensors
+        saved = ctx.saved_tensors
+        img, gt = saved[0], saved[1]
         C, H, W = ctx.dims
         gout = gout.float().contiguous()
         dimg = torch.empty_like(img)
-        check(lib().gsr_l1_ssim_backward(ptr(img), ptr(gt), C, H, W, ptr(gout), ptr(dimg), stream(img.device)),
-              "gsr_l1_ssim_backward")
+        s = stream(img.device)
+        if len(saved) == 3:
+            check(lib().gsr_l1_ssim_backward_from_map(ptr(img), ptr(gt), ptr(saved[2]), C, H, W, ptr(gout), ptr(dimg),
+                                                      s), "gsr_l1_ssim_backward_from_map")
+        else:
+            check(lib().gsr_l1_ssim_backward(ptr(img), ptr(gt), C, H, W, ptr(gout), ptr(dimg), s),
+                  "gsr_l1_ssim_backward")
         return dimg, None
 
 

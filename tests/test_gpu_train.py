@@ -75,6 +75,29 @@ def test_l1_ssim_is_deterministic_and_gt_gets_no_grad():
     assert gt.grad is None
 
 
+@pytest.mark.parametrize("shape", [(3, 1080, 1920), (3, 77, 131)])
+def test_l1_ssim_map_path_equals_direct_backward(shape):
+    """Training runs gsr_l1_ssim_forward_with_map + the elementwise backward; the gradient must be
+    bit-identical to gsr_l1_ssim_backward's and the loss equal to the plain forward's (up to the
+    order of the per-block sums)."""
+    from gs_train import l1_ssim
+    from gs_train._native import lib, ptr, stream
+    g = torch.Generator().manual_seed(7)
+    img = torch.rand(shape, generator=g).to(DEV).requires_grad_(True)
+    gt = torch.rand(shape, generator=g).to(DEV)
+    v = l1_ssim(img, gt)
+    up = torch.tensor([0.8, -0.2], device=DEV)
+    (v * up).sum().backward()
+    with torch.no_grad():
+        v0 = l1_ssim(img, gt)
+    assert torch.allclose(v, v0, rtol=0, atol=1e-6)
+    direct = torch.empty_like(img)
+    C, H, W = shape
+    assert lib().gsr_l1_ssim_backward(ptr(img.detach()), ptr(gt), C, H, W, ptr(up), ptr(direct), stream(img.device)) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(img.grad, direct)
+
+
 def _adam_from_fixture(use_index):
     from gs_train import Adam
     d = np.load(os.path.join(GOLD, "adam.npz"))
