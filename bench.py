@@ -113,7 +113,7 @@ def train_step_ms(s, W, H, deg, steps, warmup, fused, dev):
     import torch
     from gs_train.harness import GaussianSet, TrainStep
     g = GaussianSet(s["means3D"], s["shs"], s["opacities"], s["scales"], s["rotations"], n_images=1,
-                    sh_degree=deg, device=dev)
+                    sh_degree=deg, device=dev, joined_features=fused)
     gen = torch.Generator(device=dev).manual_seed(123)
     gt = torch.rand((3, H, W), device=dev, generator=gen)
     ts = TrainStep(g, [(s["view"], s["proj"], s["campos"], s["tanfovx"], s["tanfovy"])], [gt], W, H, fused=fused)

@@ -17,6 +17,9 @@
  *                                    broadcast add and a clamp in torch
  *   gsr_densify_stats                replaces train_single.py:193-194 +
  *                                    scene/gaussian_model.py:780-793 (add_densification_stats)
+ *   gsr_activate_forward / _backward replace  the exp / normalize / sigmoid getters
+ *                                    (scene/gaussian_model.py:39-47, 125-156) and their autograd
+ *   gsr_shrink_scales                replaces train_single.py:235-241
  *
  * Conventions as in gsr.h: device pointers, fp32, contiguous, `stream` a hipStream_t.
  */
@@ -64,6 +67,10 @@ typedef struct {
     int64_t width;
     float step_size;
     float bias_correction2_sqrt;
+    /* Elements between consecutive rows of the four arrays (0 = width): a group may be a column
+     * block of a wider array, e.g. the DC and rest SH coefficients of one (P, 16, 3) buffer,
+     * each with its own learning rate, without splitting the buffer every step. */
+    int64_t row_stride;
 } gsr_adam_group;
 
 /* Rows r with relevance[r] != 0 are updated in every group; if no row is relevant, every row
@@ -88,6 +95,22 @@ int gsr_exposure_backward(const float *color, const float *exposure, int64_t npi
  * grad_accum = max(||dL_dmeans2D[:, :2]||, grad_accum); denom += 1. */
 int gsr_densify_stats(int64_t P, const int *radii, const float *dL_dmeans2D, float *max_radii2D,
                       float *grad_accum, float *denom, void *stream);
+
+/* scales = exp(scaling_raw) (P,3), rotations = normalize(rotation_raw) (P,4; 16-B aligned),
+ * opacities = sigmoid(opacity_raw) (P,1): the getters of scene/gaussian_model.py:125-156 in one
+ * pass. */
+int gsr_activate_forward(int64_t P, const float *scaling_raw, const float *rotation_raw, const float *opacity_raw,
+                         float *scales, float *rotations, float *opacities, void *stream);
+
+/* Gradients of the raw parameters from those of the activated ones (torch autograd's formulas);
+ * outputs are overwritten. */
+int gsr_activate_backward(int64_t P, const float *rotation_raw, const float *scales, const float *opacities,
+                          const float *dL_dscales, const float *dL_drotations, const float *dL_dopacities,
+                          float *dL_dscaling_raw, float *dL_drotation_raw, float *dL_dopacity_raw, void *stream);
+
+/* train_single.py:235-241: rows r >= first_row (the scaffold points come first) whose largest
+ * exp(scaling_raw) exceeds max_scale get scaling_raw = log(exp(scaling_raw) * 0.8), in place. */
+int gsr_shrink_scales(int64_t P, int64_t first_row, float *scaling_raw, float max_scale, void *stream);
 
 #ifdef __cplusplus
 }

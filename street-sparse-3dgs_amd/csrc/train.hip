@@ -438,6 +438,9 @@ __device__ __forceinline__ void adam_element(const gsr_adam_group &G, int64_t e,
                                              float b1, float b2, float omb1, float omb2, float eps) {
     const int64_t row = row_of<Wd>(e, G.width);
     if (!dense && rel[row] == 0.f) return;
+    // element e of the group's (P, width) block sits at row * row_stride + col of its arrays
+    const int64_t width = Wd > 0 ? Wd : G.width;
+    e += row * (G.row_stride - width);
     const float g = G.grad[e];
     // scene/OurAdam.py:297-324: exp_avg.mul_(b1).add_(g, alpha=1-b1);
     // exp_avg_sq.mul_(b2).addcmul_(g, g, value=1-b2); denom = sqrt(v)/bc2_sqrt + eps;
@@ -481,6 +484,59 @@ __global__ __launch_bounds__(256) void densify_stats_kernel(int64_t P, const int
     maxr[i] = fmaxf(maxr[i], (float)r);
     accum[i] = fmaxf(n, accum[i]);
     denom[i] = denom[i] + 1.f;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Parameter activations (scene/gaussian_model.py:39-47, getters :125-156) and the per-step
+// shrink of over-large Gaussians (train_single.py:235-241).  One lane per Gaussian; the
+// backward follows torch's autograd formulas (exp: g*y; sigmoid: g*(1-y)*y; normalize =
+// x / max(||x||, 1e-12): dx = g/d - x * (sum(g * ((x/d)/d)) / n)).
+
+__global__ __launch_bounds__(256) void activate_fwd_kernel(int64_t P, const float *__restrict__ s_raw,
+                                                           const float4 *__restrict__ q_raw,
+                                                           const float *__restrict__ o_raw, float *__restrict__ scales,
+                                                           float4 *__restrict__ rots, float *__restrict__ opac) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+#pragma unroll
+    for (int k = 0; k < 3; k++) scales[3 * i + k] = expf(s_raw[3 * i + k]);
+    const float4 q = q_raw[i];
+    const float d = fmaxf(sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w), 1e-12f);
+    rots[i] = make_float4(q.x / d, q.y / d, q.z / d, q.w / d);
+    opac[i] = 1.f / (1.f + expf(-o_raw[i]));
+}
+
+__global__ __launch_bounds__(256) void activate_bwd_kernel(int64_t P, const float4 *__restrict__ q_raw,
+                                                           const float *__restrict__ scales,
+                                                           const float *__restrict__ opac,
+                                                           const float *__restrict__ g_s,
+                                                           const float4 *__restrict__ g_q,
+                                                           const float *__restrict__ g_o, float *__restrict__ d_s,
+                                                           float4 *__restrict__ d_q, float *__restrict__ d_o) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+#pragma unroll
+    for (int k = 0; k < 3; k++) d_s[3 * i + k] = g_s[3 * i + k] * scales[3 * i + k];
+    const float4 x = q_raw[i], g = g_q[i];
+    const float n = sqrtf(x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w);
+    const float d = fmaxf(n, 1e-12f);
+    const float gd = -(g.x * ((x.x / d) / d) + g.y * ((x.y / d) / d) + g.z * ((x.z / d) / d) + g.w * ((x.w / d) / d));
+    const float gn = n >= 1e-12f && n != 0.f ? gd / n : 0.f;  // clamp_min and norm backward
+    d_q[i] = make_float4(g.x / d + x.x * gn, g.y / d + x.y * gn, g.z / d + x.z * gn, g.w / d + x.w * gn);
+    const float y = opac[i];
+    d_o[i] = g_o[i] * (1.f - y) * y;
+}
+
+__global__ __launch_bounds__(256) void shrink_scales_kernel(int64_t P, int64_t first, float *__restrict__ s_raw,
+                                                            float limit) {
+    const int64_t i = first + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const float a = expf(s_raw[3 * i]), b = expf(s_raw[3 * i + 1]), c = expf(s_raw[3 * i + 2]);
+    if (fmaxf(fmaxf(a, b), c) > limit) {
+        s_raw[3 * i] = logf(a * 0.8f);
+        s_raw[3 * i + 1] = logf(b * 0.8f);
+        s_raw[3 * i + 2] = logf(c * 0.8f);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -696,11 +752,13 @@ int gsr_sparse_adam_step(int n_groups, const gsr_adam_group *groups, int64_t P, 
     int64_t blocks = 0;
     for (int i = 0; i < n_groups; i++) {
         const gsr_adam_group &g = groups[i];
-        if (!g.param || !g.grad || !g.exp_avg || !g.exp_avg_sq || g.width <= 0) {
-            set_last_error("gsr_sparse_adam_step: group has a NULL array or non-positive width");
+        if (!g.param || !g.grad || !g.exp_avg || !g.exp_avg_sq || g.width <= 0 ||
+            (g.row_stride != 0 && g.row_stride < g.width)) {
+            set_last_error("gsr_sparse_adam_step: group has a NULL array, non-positive width or row_stride < width");
             return GSR_ERR_INVALID_ARGUMENT;
         }
         a.g[i] = g;
+        if (a.g[i].row_stride == 0) a.g[i].row_stride = g.width;
         a.block_start[i] = blocks;
         blocks += (P * g.width + kAdamThreads - 1) / kAdamThreads;
     }
@@ -776,6 +834,66 @@ int gsr_densify_stats(int64_t P, const int *radii, const float *dL_dmeans2D, flo
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_last_error(std::string("gsr_densify_stats: ") + hipGetErrorString(e));
+        return GSR_ERR_DEVICE;
+    }
+    return GSR_OK;
+}
+
+int gsr_activate_forward(int64_t P, const float *scaling_raw, const float *rotation_raw, const float *opacity_raw,
+                         float *scales, float *rotations, float *opacities, void *stream) {
+    if (P < 0 || (P > 0 && (!scaling_raw || !rotation_raw || !opacity_raw || !scales || !rotations || !opacities)) ||
+        (P > 0 && ((reinterpret_cast<uintptr_t>(rotation_raw) | reinterpret_cast<uintptr_t>(rotations)) & 15))) {
+        set_last_error("gsr_activate_forward: NULL or misaligned (rotations need 16 B) pointer");
+        return GSR_ERR_INVALID_ARGUMENT;
+    }
+    if (P == 0) return GSR_OK;
+    hipLaunchKernelGGL(activate_fwd_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), P, scaling_raw,
+                       reinterpret_cast<const float4 *>(rotation_raw), opacity_raw, scales,
+                       reinterpret_cast<float4 *>(rotations), opacities);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_last_error(std::string("gsr_activate_forward: ") + hipGetErrorString(e));
+        return GSR_ERR_DEVICE;
+    }
+    return GSR_OK;
+}
+
+int gsr_activate_backward(int64_t P, const float *rotation_raw, const float *scales, const float *opacities,
+                          const float *dL_dscales, const float *dL_drotations, const float *dL_dopacities,
+                          float *dL_dscaling_raw, float *dL_drotation_raw, float *dL_dopacity_raw, void *stream) {
+    if (P < 0 || (P > 0 && (!rotation_raw || !scales || !opacities || !dL_dscales || !dL_drotations ||
+                            !dL_dopacities || !dL_dscaling_raw || !dL_drotation_raw || !dL_dopacity_raw)) ||
+        (P > 0 && ((reinterpret_cast<uintptr_t>(rotation_raw) | reinterpret_cast<uintptr_t>(dL_drotations) |
+                    reinterpret_cast<uintptr_t>(dL_drotation_raw)) & 15))) {
+        set_last_error("gsr_activate_backward: NULL or misaligned (rotations need 16 B) pointer");
+        return GSR_ERR_INVALID_ARGUMENT;
+    }
+    if (P == 0) return GSR_OK;
+    hipLaunchKernelGGL(activate_bwd_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), P, reinterpret_cast<const float4 *>(rotation_raw), scales,
+                       opacities, dL_dscales, reinterpret_cast<const float4 *>(dL_drotations), dL_dopacities,
+                       dL_dscaling_raw, reinterpret_cast<float4 *>(dL_drotation_raw), dL_dopacity_raw);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_last_error(std::string("gsr_activate_backward: ") + hipGetErrorString(e));
+        return GSR_ERR_DEVICE;
+    }
+    return GSR_OK;
+}
+
+int gsr_shrink_scales(int64_t P, int64_t first_row, float *scaling_raw, float max_scale, void *stream) {
+    if (P < 0 || first_row < 0 || (P > 0 && !scaling_raw)) {
+        set_last_error("gsr_shrink_scales: bad sizes or NULL pointer");
+        return GSR_ERR_INVALID_ARGUMENT;
+    }
+    if (first_row >= P) return GSR_OK;
+    const int64_t n = P - first_row;
+    hipLaunchKernelGGL(shrink_scales_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), P, first_row, scaling_raw, max_scale);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_last_error(std::string("gsr_shrink_scales: ") + hipGetErrorString(e));
         return GSR_ERR_DEVICE;
     }
     return GSR_OK;

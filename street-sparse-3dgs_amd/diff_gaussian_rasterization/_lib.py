@@ -22,7 +22,7 @@ _i64 = ctypes.c_int64
 class AdamGroup(ctypes.Structure):
     """gsr_adam_group (include/gsr_train.h)."""
     _fields_ = [("param", _vp), ("grad", _vp), ("exp_avg", _vp), ("exp_avg_sq", _vp), ("width", _i64),
-                ("step_size", _f), ("bias_correction2_sqrt", _f)]
+                ("step_size", _f), ("bias_correction2_sqrt", _f), ("row_stride", _i64)]
 
 
 # exported symbol -> (restype, argtypes); must match include/gsr.h, gsr_train.h, gsr_hier.h
@@ -49,6 +49,9 @@ SIGNATURES = {
     "gsr_sparse_adam_step": (_i, [_i, ctypes.POINTER(AdamGroup), _i64, _vp, ctypes.c_double, ctypes.c_double,
                                   ctypes.c_double, _vp, _vp]),
     "gsr_densify_stats": (_i, [_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gsr_activate_forward": (_i, [_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gsr_activate_backward": (_i, [_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gsr_shrink_scales": (_i, [_i64, _i64, _vp, _f, _vp]),
     "gsr_exposure_forward": (_i, [_vp, _vp, _i64, _vp, _vp]),
     "gsr_exposure_scratch_bytes": (ctypes.c_size_t, [_i64]),
     "gsr_exposure_backward": (_i, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),

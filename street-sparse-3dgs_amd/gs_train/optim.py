@@ -3,7 +3,10 @@ model uses it (scene/gaussian_model.py:286-296, train_single.py:224-231).
 
 Same constructor, `param_groups` and per-parameter state keys ('step', 'exp_avg',
 'exp_avg_sq'), so GaussianModel's learning-rate schedule and its densification bookkeeping
-(which edits optimizer.state directly) keep working.  `step(relevant)` accepts the reference's
+(which edits optimizer.state directly) keep working.  A group may also carry
+`column_lrs = [(start, stop, lr), ...]`: column blocks of each row of its parameter, each with its
+own learning rate, so the DC and rest SH coefficients can live in one (P, 16, 3) tensor (no
+torch.cat / split per step) and still get f_dc's and f_rest's rates.  `step(relevant)` accepts the reference's
 index tensor; `step(relevance=opacity.grad)` skips the host-synchronising nonzero() and tests
 relevance per row on the device.  Either way all groups are updated by ONE gfx950 launch
 (csrc/train.hip) that reads (param, grad, m, v) and writes (param, m, v) once for the relevant
@@ -78,14 +81,15 @@ class Adam(torch.optim.Optimizer):
                     state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 state["step"] += 1
                 st = state["step"].item()
-                entries.append((p, state, group["lr"] / (1 - beta1 ** st), math.sqrt(1 - beta2 ** st)))
+                for start, stop, lr in group.get("column_lrs", [(None, None, group["lr"])]):
+                    entries.append((p, state, lr / (1 - beta1 ** st), math.sqrt(1 - beta2 ** st), start, stop))
         if not entries:
             return loss
         P = entries[0][0].shape[0]
         dev = entries[0][0].device
         groups = (AdamGroup * len(entries))()
         keep = []
-        for k, (p, state, step_size, bc2s) in enumerate(entries):
+        for k, (p, state, step_size, bc2s, start, stop) in enumerate(entries):
             require_gpu(p)
             if p.shape[0] != P or p.device != dev:
                 raise ValueError("fused sparse Adam: every parameter must have the same number of rows")
@@ -96,8 +100,14 @@ class Adam(torch.optim.Optimizer):
             if not (m.is_contiguous() and v.is_contiguous()):
                 raise ValueError("fused sparse Adam: moment buffers must be contiguous")
             keep.append(g)
-            groups[k] = AdamGroup(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel() // max(P, 1),
-                                  step_size, bc2s)
+            row = p.numel() // max(P, 1)
+            if start is None:
+                start, stop = 0, row
+            if not 0 <= start < stop <= row:
+                raise ValueError(f"column_lrs block ({start}, {stop}) outside a row of {row} values")
+            off = 4 * start  # bytes
+            groups[k] = AdamGroup(p.data_ptr() + off, g.data_ptr() + off, m.data_ptr() + off, v.data_ptr() + off,
+                                  stop - start, step_size, bc2s, row)
         if relevance is not None:
             rel = relevance.detach().reshape(-1)
             if rel.numel() != P:

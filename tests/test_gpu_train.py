@@ -210,3 +210,68 @@ def test_exposure_matches_torch_reference_formula():
     assert (out.double() - ref).abs().max().item() <= 1e-6
     assert (color.grad.double() - c64.grad).abs().max().item() <= 1e-6
     assert (E.grad.double() - e64.grad).abs().max().item() <= 1e-4 * e64.grad.abs().max().item()
+
+
+def test_activate_matches_torch_getters_and_autograd():
+    """gsr_activate_forward/_backward against scene/gaussian_model.py's getters (exp, normalize,
+    sigmoid) and torch autograd through them."""
+    from gs_train import activate
+    g = torch.Generator().manual_seed(11)
+    P = 100_003
+    s = (torch.randn(P, 3, generator=g) - 3).to(DEV).requires_grad_(True)
+    q = torch.randn(P, 4, generator=g)
+    q[:5] = 0.0  # zero quaternions: normalize's eps clamp
+    q = q.to(DEV).requires_grad_(True)
+    o = torch.randn(P, 1, generator=g).to(DEV).requires_grad_(True)
+    ups = [torch.randn(P, k, generator=g).to(DEV) for k in (3, 4, 1)]
+    outs = activate(s, q, o)
+    sum((a * u).sum() for a, u in zip(outs, ups)).backward()
+    s2, q2, o2 = (t.detach().clone().requires_grad_(True) for t in (s, q, o))
+    refs = (torch.exp(s2), torch.nn.functional.normalize(q2), torch.sigmoid(o2))
+    sum((a * u).sum() for a, u in zip(refs, ups)).backward()
+    for a, b in zip(outs, refs):
+        torch.testing.assert_close(a, b, rtol=2e-7, atol=1e-7)
+    for a, b in ((s, s2), (o, o2)):
+        torch.testing.assert_close(a.grad, b.grad, rtol=1e-6, atol=1e-7)
+    # normalize's gradient g/d - x (g.x)/d^3 cancels: bound the error by the size of its terms
+    d = q.detach().norm(dim=1, keepdim=True).clamp_min(1e-12)
+    scale = ups[1].norm(dim=1, keepdim=True) / d
+    assert ((q.grad - q2.grad).abs() <= 4e-7 * scale + 1e-7).all()
+
+
+def test_shrink_scales_matches_reference_indexing():
+    from gs_train import shrink_scales
+    g = torch.Generator().manual_seed(12)
+    s = (torch.randn(50_000, 3, generator=g) * 2 - 3).to(DEV)
+    ref = s.clone()
+    limit, first = 0.2, 100
+    sc = torch.exp(ref)
+    bad = sc.max(dim=1).values > limit
+    bad[:first] = False  # scaffold points
+    ref[bad] = torch.log(sc[bad] * 0.8)
+    shrink_scales(s, limit, first_row=first)
+    assert bad.sum() > 1000
+    torch.testing.assert_close(s, ref, rtol=0, atol=0)
+
+
+def test_adam_column_blocks_equal_separate_groups():
+    """One (P,16,3) SH tensor with column_lrs == the reference's f_dc / f_rest groups, bitwise."""
+    from gs_train import Adam
+    g = torch.Generator().manual_seed(13)
+    P = 30_000
+    base = torch.randn(P, 16, 3, generator=g).to(DEV)
+    grads = [torch.randn(P, 16, 3, generator=g).to(DEV) for _ in range(3)]
+    rel = (torch.rand(P, generator=g) < 0.7).float().to(DEV)
+    joined = torch.nn.Parameter(base.clone())
+    dc = torch.nn.Parameter(base[:, :1].clone())
+    rest = torch.nn.Parameter(base[:, 1:].clone())
+    oj = Adam([{"params": [joined], "lr": 0.0025, "column_lrs": [(0, 3, 0.0025), (3, 48, 0.0025 / 20.0)]}], eps=1e-15)
+    os_ = Adam([{"params": [dc], "lr": 0.0025}, {"params": [rest], "lr": 0.0025 / 20.0}], eps=1e-15)
+    for gr in grads:
+        joined.grad = gr.clone()
+        dc.grad, rest.grad = gr[:, :1].contiguous(), gr[:, 1:].contiguous()
+        oj.step(relevance=rel)
+        os_.step(relevance=rel)
+    assert torch.equal(joined.detach()[:, :1], dc.detach())
+    assert torch.equal(joined.detach()[:, 1:], rest.detach())
+    assert torch.equal(oj.state[joined]["exp_avg_sq"][:, 1:], os_.state[rest]["exp_avg_sq"])

@@ -30,7 +30,8 @@ def main():
     from gs_train.synthetic import synthetic_scene
     dev = torch.device("cuda", 0)
     s = synthetic_scene(a.gaussians, a.width, a.height, seed=0)
-    g = GaussianSet(s["means3D"], s["shs"], s["opacities"], s["scales"], s["rotations"], device=dev)
+    g = GaussianSet(s["means3D"], s["shs"], s["opacities"], s["scales"], s["rotations"], device=dev,
+                    joined_features=not a.baseline)
     gt = torch.rand((3, a.height, a.width), device=dev)
     ts = TrainStep(g, [(s["view"], s["proj"], s["campos"], s["tanfovx"], s["tanfovy"])], [gt], a.width, a.height,
                    fused=not a.baseline)
