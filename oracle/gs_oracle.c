@@ -673,3 +673,41 @@ void gso_eval_sh(int n, int deg, int M, const float *shs, const float *dirs, flo
 void gso_cov3d(int n, const float *scales, float mod, const float *rots, float *cov) {
     for (int i = 0; i < n; i++) cov3d_from_scale_rot(scales + 3 * i, mod, rots + 4 * i, cov + 6 * i);
 }
+
+/* ---------------------------------------------------------------------------------------------
+ * Nearest-neighbour scale initialisation: simple_knn._C.distCUDA2 as
+ * called at scene/gaussian_model.py:207.  simple-knn (submodules/simple-knn) is not vendored in
+ * the reference and the reference holds no outputs of it, so this row's parity is UNPINNED
+ * against the real extension: this is a restatement of its published definition -- for every
+ * point, the mean of the three smallest squared distances to the OTHER points (by index; equal
+ * positions count as 0), best list initialised to FLT_MAX and updated by strict-greater
+ * insertion (updateKBest<3>), summed (b0 + b1 + b2) / 3 in fp32.  Brute force O(N^2); the HIP
+ * version prunes with boxes, which must not change the result.  Squared distance order:
+ * fmaf(dz, dz, fmaf(dy, dy, dx * dx)) with d = p_j - p_i.
+ */
+#include <float.h>
+static void knn_one(long long N, const float *p, long long i, float *out);
+void gso_knn_mean_dist2(long long N, const float *p, float *out) {
+#pragma omp parallel for schedule(dynamic, 64)
+    for (long long i = 0; i < N; i++) knn_one(N, p, i, out + i);
+}
+/* the same for the queries qidx[0..nq) only (large-N spot checks) */
+void gso_knn_mean_dist2_at(long long N, const float *p, long long nq, const long long *qidx, float *out) {
+#pragma omp parallel for schedule(dynamic, 4)
+    for (long long k = 0; k < nq; k++) knn_one(N, p, qidx[k], out + k);
+}
+static void knn_one(long long N, const float *p, long long i, float *out) {
+    {
+        float b0 = FLT_MAX, b1 = FLT_MAX, b2 = FLT_MAX;
+        const float qx = p[3 * i], qy = p[3 * i + 1], qz = p[3 * i + 2];
+        for (long long j = 0; j < N; j++) {
+            if (j == i) continue;
+            const float dx = p[3 * j] - qx, dy = p[3 * j + 1] - qy, dz = p[3 * j + 2] - qz;
+            float d = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+            if (b0 > d) { const float t = b0; b0 = d; d = t; }
+            if (b1 > d) { const float t = b1; b1 = d; d = t; }
+            if (b2 > d) b2 = d;
+        }
+        *out = (b0 + b1 + b2) / 3.0f;
+    }
+}

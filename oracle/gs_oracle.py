@@ -280,3 +280,21 @@ def synthetic_scene(P, W, H, seed=0, sh_degree=3, fovx_deg=60.0, zmin=2.0, zmax=
     return dict(means3D=means, scales=scales, rotations=rots, opacities=opac, shs=shs.astype(np.float32),
                 view=view, proj=proj, campos=campos, tanfovx=tx, tanfovy=ty, bg=bg, W=W, H=H,
                 sh_degree=sh_degree)
+
+
+def knn_mean_dist2(points) -> np.ndarray:
+    """simple_knn distCUDA2 restated (gso_knn_mean_dist2): exact brute force, parity unpinned
+    against the real extension (not vendored; see gs_oracle.c)."""
+    p = _f32(points).reshape(-1, 3)
+    out = np.empty(p.shape[0], np.float32)
+    lib().gso_knn_mean_dist2(ctypes.c_longlong(p.shape[0]), _p(p), _p(out))
+    return out
+
+
+def knn_mean_dist2_at(points, queries) -> np.ndarray:
+    """knn_mean_dist2 for the given query indices only (all N points are candidates)."""
+    p = _f32(points).reshape(-1, 3)
+    q = np.ascontiguousarray(np.asarray(queries, dtype=np.int64))
+    out = np.empty(q.shape[0], np.float32)
+    lib().gso_knn_mean_dist2_at(ctypes.c_longlong(p.shape[0]), _p(p), ctypes.c_longlong(q.shape[0]), _p(q), _p(out))
+    return out

@@ -34,6 +34,10 @@ void launch_mark_visible(int P, const float *means3D, const float *view, uint8_t
 // sort.hip (rocPRIM)
 size_t scan_temp_bytes(int P);
 hipError_t inclusive_scan(void *tmp, size_t tmp_bytes, const uint32_t *in, uint32_t *out, int P, hipStream_t s);
+// Stable LSD sort of n (key, value) pairs over key bits [0, end_bit) (kNN Morton order).
+size_t sort_pairs_temp_bytes(size_t n, int end_bit);
+hipError_t sort_pairs(void *tmp, size_t tmp_bytes, const uint32_t *kin, uint32_t *kout, const uint32_t *vin,
+                      uint32_t *vout, size_t n, int end_bit, hipStream_t s);
 size_t depth_sort_temp_bytes(int P);
 hipError_t depth_sort(void *tmp, size_t tmp_bytes, const uint32_t *kin, uint32_t *kout, const uint32_t *vin,
                       uint32_t *vout, int P, hipStream_t s);

@@ -58,4 +58,17 @@ hipError_t depth_sort(void *tmp, size_t tmp_bytes, const uint32_t *kin, uint32_t
     return rocprim::radix_sort_pairs<OnesweepCfg>(tmp, tmp_bytes, kin, kout, vin, vout, (size_t)P, 0, 32, s);
 }
 
+size_t sort_pairs_temp_bytes(size_t n, int end_bit) {
+    size_t bytes = 0;
+    rocprim::radix_sort_pairs<OnesweepCfg>(nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                           (const uint32_t *)nullptr, (uint32_t *)nullptr, n > 0 ? n : 1, 0, end_bit);
+    return bytes;
+}
+
+hipError_t sort_pairs(void *tmp, size_t tmp_bytes, const uint32_t *kin, uint32_t *kout, const uint32_t *vin,
+                      uint32_t *vout, size_t n, int end_bit, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    return rocprim::radix_sort_pairs<OnesweepCfg>(tmp, tmp_bytes, kin, kout, vin, vout, n, 0, end_bit, s);
+}
+
 }  // namespace gsr

@@ -25,7 +25,7 @@ class AdamGroup(ctypes.Structure):
                 ("step_size", _f), ("bias_correction2_sqrt", _f), ("row_stride", _i64)]
 
 
-# exported symbol -> (restype, argtypes); must match include/gsr.h, gsr_train.h, gsr_hier.h
+# exported symbol -> (restype, argtypes); must match include/gsr.h, gsr_train.h, gsr_hier.h, gsr_knn.h
 SIGNATURES = {
     "gsr_rasterize_forward": (_i, [RESIZE_FN, RESIZE_FN, RESIZE_FN, _vp, _i, _i, _i, _vp, _i, _i,
                                    _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _f, _f,
@@ -58,6 +58,8 @@ SIGNATURES = {
     # include/gsr_hier.h
     "gsr_interpolate_cut_forward": (_i, [_i64, _i, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                          _vp, _vp, _vp]),
+    "gsr_knn_scratch_bytes": (ctypes.c_size_t, [_i64]),
+    "gsr_knn_mean_dist2": (_i, [_i64, _vp, _vp, _vp, _vp]),
     "gsr_interpolate_cut_backward": (_i, [_i64, _i, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                           _vp, _vp, _vp, _vp, _vp]),
 }

@@ -161,3 +161,21 @@ def test_render_post_interpolation_fixture():
                                  f["render_indices"], f["parent_indices"], f["interpolation_weights"], int(f["skybox"]))
     for k in ("means3D", "scales", "rotations", "opacities", "shs"):
         np.testing.assert_allclose(o[k], f["out_" + k], rtol=0, atol=1e-6, err_msg=k)
+
+
+def test_knn_oracle_matches_float64_brute_force():
+    """The distCUDA2 restatement (parity unpinned: simple-knn is not vendored) against an fp64
+    numpy brute force, plus its small-N conventions (missing neighbours are FLT_MAX)."""
+    rng = np.random.default_rng(3)
+    p = rng.normal(size=(1500, 3)).astype(np.float32)
+    p[100:110] = p[50]  # duplicates count as distance 0
+    got = O.knn_mean_dist2(p)
+    d = ((p[None].astype(np.float64) - p[:, None]) ** 2).sum(-1)
+    np.fill_diagonal(d, np.inf)
+    ref = np.sort(d, 1)[:, :3].mean(1)
+    assert np.abs(got - ref).max() <= 1e-6 * ref.max()
+    assert (got[100:110] == 0).all()
+    flt_max = np.finfo(np.float32).max
+    assert np.all(O.knn_mean_dist2(np.zeros((3, 3))) == np.float32((0 + 0 + flt_max) / 3))
+    two = O.knn_mean_dist2(np.array([[0, 0, 0], [1, 0, 0]], np.float32))
+    assert np.all(np.isinf(two))  # (1 + FLT_MAX + FLT_MAX) overflows in fp32, as upstream's sum
