@@ -25,7 +25,12 @@ class AdamGroup(ctypes.Structure):
                 ("step_size", _f), ("bias_correction2_sqrt", _f), ("row_stride", _i64)]
 
 
-# exported symbol -> (restype, argtypes); must match include/gsr.h, gsr_train.h, gsr_hier.h, gsr_knn.h
+class RowGroup(ctypes.Structure):
+    """gsr_row_group (include/gsr_densify.h)."""
+    _fields_ = [("param", _vp), ("exp_avg", _vp), ("exp_avg_sq", _vp), ("width", _i64)]
+
+
+# exported symbol -> (restype, argtypes); must match include/gsr.h, gsr_train.h, gsr_hier.h, gsr_knn.h, gsr_densify.h
 SIGNATURES = {
     "gsr_rasterize_forward": (_i, [RESIZE_FN, RESIZE_FN, RESIZE_FN, _vp, _i, _i, _i, _vp, _i, _i,
                                    _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _f, _f,
@@ -58,6 +63,10 @@ SIGNATURES = {
     # include/gsr_hier.h
     "gsr_interpolate_cut_forward": (_i, [_i64, _i, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                          _vp, _vp, _vp]),
+    "gsr_densify_scratch_bytes": (ctypes.c_size_t, [_i64]),
+    "gsr_densify_plan": (_i, [_i64, _i64, _vp, _vp, _vp, _vp, _f, _f, _f, _vp, _vp, _vp]),
+    "gsr_densify_apply": (_i, [_i64, _i, ctypes.POINTER(RowGroup), ctypes.POINTER(RowGroup), _i, _i, _i, _vp, _i64,
+                               _vp, _i64, _vp]),
     "gsr_knn_scratch_bytes": (ctypes.c_size_t, [_i64]),
     "gsr_knn_mean_dist2": (_i, [_i64, _vp, _vp, _vp, _vp]),
     "gsr_interpolate_cut_backward": (_i, [_i64, _i, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,

@@ -85,3 +85,110 @@ def densification_stats(g, radii, grad2d):
     n = torch.norm(grad2d[vis, :2], dim=-1, keepdim=True)
     g.xyz_gradient_accum[vis] = torch.max(n, g.xyz_gradient_accum[vis])
     g.denom[vis] += 1
+
+
+# ---- densify_and_prune in the reference's own formulation (scene/gaussian_model.py:560-778,
+# gt_point_cloud_constraints off), on a split-layout GaussianSet and OurAdamTorch: the side-by-side
+# for gs_train.densify.densify_and_prune ----------------------------------------------------------
+_ATTR = {"xyz": "_xyz", "f_dc": "_features_dc", "f_rest": "_features_rest", "opacity": "_opacity",
+         "scaling": "_scaling", "rotation": "_rotation"}
+
+
+def _build_rotation(r):
+    norm = torch.sqrt(r[:, 0] * r[:, 0] + r[:, 1] * r[:, 1] + r[:, 2] * r[:, 2] + r[:, 3] * r[:, 3])
+    q = r / norm[:, None]
+    R = torch.zeros((q.size(0), 3, 3), device=r.device)
+    r, x, y, z = q[:, 0], q[:, 1], q[:, 2], q[:, 3]
+    R[:, 0, 0] = 1 - 2 * (y * y + z * z)
+    R[:, 0, 1] = 2 * (x * y - r * z)
+    R[:, 0, 2] = 2 * (x * z + r * y)
+    R[:, 1, 0] = 2 * (x * y + r * z)
+    R[:, 1, 1] = 1 - 2 * (x * x + z * z)
+    R[:, 1, 2] = 2 * (y * z - r * x)
+    R[:, 2, 0] = 2 * (x * z - r * y)
+    R[:, 2, 1] = 2 * (y * z + r * x)
+    R[:, 2, 2] = 1 - 2 * (x * x + y * y)
+    return R
+
+
+def _prune_optimizer(g, opt, mask):
+    for group in opt.param_groups:
+        p = group["params"][0]
+        st = opt.state.get(p, None)
+        newp = torch.nn.Parameter(p[mask].requires_grad_(True))
+        if st is not None:
+            st["exp_avg"] = st["exp_avg"][mask]
+            st["exp_avg_sq"] = st["exp_avg_sq"][mask]
+            del opt.state[p]
+            opt.state[newp] = st
+        group["params"][0] = newp
+        setattr(g, _ATTR[group["name"]], newp)
+
+
+def _cat_to_optimizer(g, opt, ext):
+    for group in opt.param_groups:
+        p = group["params"][0]
+        e = ext[group["name"]]
+        st = opt.state.get(p, None)
+        newp = torch.nn.Parameter(torch.cat((p, e), dim=0).requires_grad_(True))
+        if st is not None:
+            st["exp_avg"] = torch.cat((st["exp_avg"], torch.zeros_like(e)), dim=0)
+            st["exp_avg_sq"] = torch.cat((st["exp_avg_sq"], torch.zeros_like(e)), dim=0)
+            del opt.state[p]
+            opt.state[newp] = st
+        group["params"][0] = newp
+        setattr(g, _ATTR[group["name"]], newp)
+
+
+def _postfix(g, opt, d):
+    _cat_to_optimizer(g, opt, d)
+    n = g._xyz.shape[0]
+    dev = g._xyz.device
+    g.xyz_gradient_accum = torch.zeros((n, 1), device=dev)
+    g.denom = torch.zeros((n, 1), device=dev)
+    g.max_radii2D = torch.cat((g.max_radii2D, torch.zeros((d["xyz"].shape[0]), device=dev)))
+
+
+def _prune_points(g, opt, mask):
+    valid = ~mask
+    _prune_optimizer(g, opt, valid)
+    g.xyz_gradient_accum = g.xyz_gradient_accum[valid]
+    g.denom = g.denom[valid]
+    g.max_radii2D = g.max_radii2D[valid]
+
+
+def densify_and_prune(g, opt, max_grad, min_opacity, extent, percent_dense, first_row=0, N=2):
+    grads = g.xyz_gradient_accum
+    grads[grads.isnan()] = 0.0
+    dev = g._xyz.device
+    # densify_and_clone (:708-731)
+    sel = torch.where(torch.norm(grads, dim=-1) * g.max_radii2D * torch.pow(g.get_opacity.flatten(), 1 / 5.0)
+                      >= max_grad, True, False)
+    sel = torch.logical_and(sel, g.get_opacity.flatten() > 0.15)
+    sel = torch.logical_and(sel, torch.max(g.get_scaling, dim=1).values <= percent_dense * extent)
+    sel[:first_row] = False
+    _postfix(g, opt, {"xyz": g._xyz[sel], "f_dc": g._features_dc[sel], "f_rest": g._features_rest[sel],
+                      "opacity": g._opacity[sel], "scaling": g._scaling[sel], "rotation": g._rotation[sel]})
+    # densify_and_split (:672-706)
+    n_init = g._xyz.shape[0]
+    padded = torch.zeros((n_init), device=dev)
+    padded[:grads.shape[0]] = grads.squeeze()
+    sel = torch.where(padded * g.max_radii2D * torch.pow(g.get_opacity.flatten(), 1 / 5.0) >= max_grad, True, False)
+    sel = torch.logical_and(sel, g.get_opacity.flatten() > 0.15)
+    sel = torch.logical_and(sel, torch.max(g.get_scaling, dim=1).values > percent_dense * extent)
+    sel[:first_row] = False
+    stds = g.get_scaling[sel].repeat(N, 1)
+    means = torch.zeros((stds.size(0), 3), device=dev)
+    samples = torch.normal(mean=means, std=stds)
+    rots = _build_rotation(g._rotation[sel]).repeat(N, 1, 1)
+    new_xyz = torch.bmm(rots, samples.unsqueeze(-1)).squeeze(-1) + g.get_xyz[sel].repeat(N, 1)
+    new_scaling = torch.log(g.get_scaling[sel].repeat(N, 1) / (0.8 * N))
+    _postfix(g, opt, {"xyz": new_xyz, "f_dc": g._features_dc[sel].repeat(N, 1, 1),
+                      "f_rest": g._features_rest[sel].repeat(N, 1, 1), "opacity": g._opacity[sel].repeat(N, 1),
+                      "scaling": new_scaling, "rotation": g._rotation[sel].repeat(N, 1)})
+    _prune_points(g, opt, torch.cat((sel, torch.zeros(N * sel.sum(), device=dev, dtype=bool))))
+    # opacity prune (:753-770)
+    prune = (g.get_opacity < min_opacity).squeeze()
+    prune[:first_row] = False
+    _prune_points(g, opt, prune)
+    g.max_radii2D = torch.zeros((g._xyz.shape[0]), device=dev)

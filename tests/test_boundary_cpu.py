@@ -14,7 +14,7 @@ import pytest
 import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(REPO, "include", h) for h in ("gsr.h", "gsr_train.h", "gsr_hier.h", "gsr_knn.h")]
+HEADERS = [os.path.join(REPO, "include", h) for h in ("gsr.h", "gsr_train.h", "gsr_hier.h", "gsr_knn.h", "gsr_densify.h")]
 GOLD = os.path.join(REPO, "tests", "golden")
 
 
