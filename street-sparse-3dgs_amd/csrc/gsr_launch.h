@@ -26,7 +26,11 @@ struct GaussianInputs {
 
 // preprocess.hip
 void launch_preprocess(const GaussianInputs &in, const Camera &cam, const GeomState &gs, int *radii,
-                       hipStream_t s);
+                       hipStream_t s, bool split_color);
+// SH colour of the visible Gaussians (rec.col, clamped) after a split_color preprocess
+bool color_split_supported(const GaussianInputs &in);
+void launch_preprocess_color(const GaussianInputs &in, const Camera &cam, const GeomState &gs, const int *radii,
+                             hipStream_t s);
 // render.hip: tiles ordered heaviest first by work[t] (or, with work == NULL, by list length).
 void launch_tile_order(const uint32_t *work, const uint2 *ranges, int T, int shift, uint32_t *order, hipStream_t s);
 void launch_mark_visible(int P, const float *means3D, const float *view, uint8_t *present, hipStream_t s);

@@ -8,7 +8,7 @@
 
 namespace gsr {
 
-template <bool kVecSH>
+template <bool kVecSH, bool kSplitColor>
 __global__ __launch_bounds__(256) void preprocess_kernel(
     int P, int D, int M, const float *__restrict__ means3D, const float *__restrict__ scales, float mod,
     const float *__restrict__ rotations, const float *__restrict__ opacities, const float *__restrict__ shs,
@@ -54,9 +54,11 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
     const int area = (r.x1 - r.x0) * (r.y1 - r.y0);
     if (area == 0) return;
 
-    float4 col;
+    float4 col = make_float4(0.f, 0.f, 0.f, 0.f);
     uint8_t clamp_bits = 0;
-    if (colors_precomp) {
+    if (kSplitColor) {
+        // colour + clamp bits come from preprocess_color_kernel on the side stream
+    } else if (colors_precomp) {
         col = make_float4(colors_precomp[3 * i], colors_precomp[3 * i + 1], colors_precomp[3 * i + 2], 0.f);
     } else {
         float dir[3], dor[3];
@@ -88,7 +90,7 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
         }
         col = make_float4(rgb[0], rgb[1], rgb[2], 0.f);
     }
-    col.w = 1.f / pv.z;
+    if (!kSplitColor) col.w = 1.f / pv.z;
     const float op = opacities[i];
     const float ca_ = cc * det_inv, cb_ = -cb * det_inv, cc_ = ca * det_inv;
     // Half-extents of the region where alpha = op * exp(power) can reach 1/255:
@@ -111,32 +113,113 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
     float4 *R = reinterpret_cast<float4 *>(gs.rec + i);
     R[0] = make_float4(px, py, ca_, cb_);
     R[1] = make_float4(cc_, op, ex, ey);
-    R[2] = col;
+    if (!kSplitColor) R[2] = col;
     R[3] = make_float4(__uint_as_float((uint32_t)r.x0 | ((uint32_t)r.y0 << 16)), __uint_as_float((uint32_t)(r.x1 - r.x0)),
                        __uint_as_float(__float_as_uint(pv.z)), 0.f);
-    gs.clamped[i] = clamp_bits;
+    if (!kSplitColor) gs.clamped[i] = clamp_bits;
     gs.tiles[i] = (uint32_t)area;
     gs.dkey[i] = __float_as_uint(pv.z);
 }
 
+// The SH colour of the visible Gaussians, split off the preprocess so that it streams its 192 B
+// SH rows on a side stream while the depth sort and the binning (latency-bound, little HBM
+// traffic) run on the main one.  Each wave stages its 64 rows (12 KiB, contiguous) through LDS:
+// load k of lane l is float4 k*64 + l of the block, so every load instruction reads 1 KiB
+// contiguously (one lane per row would put 64 rows, 192 B apart, under each instruction), and
+// rows land in a per-wave tile padded to 13 float4 (ds_read_b128 of one row per lane is then
+// conflict-free: 52-dword stride).  Rows of culled Gaussians and coefficients above the active
+// degree are not fetched.
+constexpr int kShRow = 12;                 // float4 per row (M = 16)
+constexpr int kShPitch = 13;               // padded LDS row pitch, in float4
+constexpr int kColorWaves = 2;             // 2 waves per block: 26 KiB of LDS
+constexpr int kColorThreads = kColorWaves * kWave;
+
+__global__ __launch_bounds__(kColorThreads) void preprocess_color_kernel(int P, int D, const float *__restrict__ means3D,
+                                                                         const float *__restrict__ shs,
+                                                                         const float *__restrict__ campos,
+                                                                         const int *__restrict__ radii, GeomState gs) {
+    __shared__ float4 s_sh[kColorWaves * kWave * kShPitch];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool vis = i < P && radii[i] > 0;
+    const int nc = (D + 1) * (D + 1);
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float4 *S = s_sh + wv * kWave * kShPitch;
+    const uint64_t need = __ballot(vis);
+    const int64_t row0 = (int64_t)blockIdx.x * blockDim.x + wv * kWave;
+    const int cols = (nc * 3 + 3) / 4;  // float4 per row that hold active coefficients
+    const float4 *src4 = reinterpret_cast<const float4 *>(shs) + row0 * kShRow;
+    float4 v[kShRow];
+#pragma unroll
+    for (int k = 0; k < kShRow; k++) {
+        const int f = k * kWave + lane, row = f / kShRow, col = f - row * kShRow;
+        v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (((need >> row) & 1ull) && col < cols) v[k] = src4[f];
+    }
+#pragma unroll
+    for (int k = 0; k < kShRow; k++) {
+        const int f = k * kWave + lane, row = f / kShRow, col = f - row * kShRow;
+        S[row * kShPitch + col] = v[k];
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS writes landed
+    __builtin_amdgcn_wave_barrier();
+    float sh[48];
+#pragma unroll
+    for (int c = 0; c < kShRow; c++) {
+        const float4 w = S[lane * kShPitch + c];
+        sh[4 * c] = w.x; sh[4 * c + 1] = w.y; sh[4 * c + 2] = w.z; sh[4 * c + 3] = w.w;
+    }
+    if (i >= P) return;
+    if (!vis) {
+        gs.clamped[i] = 0;
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < 48; k++) sh[k] = k < nc * 3 ? sh[k] : 0.f;  // tail of a partial float4
+    const float3 p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
+    float dir[3], dor[3];
+    sh_dir(p, make_float3(campos[0], campos[1], campos[2]), dir, dor);
+    uint8_t clamp_bits = 0;
+    float rgb[3];
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) {
+        const float val = sh_channel(D, sh + ch, dir[0], dir[1], dir[2]);
+        if (val < 0.f) clamp_bits |= (uint8_t)(1u << ch);
+        rgb[ch] = val < 0.f ? 0.f : val;
+    }
+    float4 *R = reinterpret_cast<float4 *>(gs.rec + i);
+    const float z = R[3].z;  // view depth, written by the preprocess
+    R[2] = make_float4(rgb[0], rgb[1], rgb[2], 1.f / z);
+    gs.clamped[i] = clamp_bits;
+}
+
+bool color_split_supported(const GaussianInputs &in) {
+    return in.shs && !in.colors_precomp && in.M == 16 && (reinterpret_cast<uintptr_t>(in.shs) % 16 == 0);
+}
+
 void launch_preprocess(const GaussianInputs &in, const Camera &cam, const GeomState &gs, int *radii,
-                       hipStream_t s) {
+                       hipStream_t s, bool split_color) {
     if (in.P == 0) return;
     const int blocks = (in.P + 255) / 256;
     const bool vec = in.shs && (in.M * 3) % 4 == 0 && (reinterpret_cast<uintptr_t>(in.shs) % 16 == 0) && in.M >= 16;
-    if (vec)
-        hipLaunchKernelGGL(preprocess_kernel<true>, dim3(blocks), dim3(256), 0, s, in.P, in.D, in.M, in.means3D,
-                           in.scales, in.scale_modifier, in.rotations, in.opacities, in.shs, in.colors_precomp,
-                           in.cov3D_precomp, cam.view, cam.proj, cam.campos, cam.W, cam.H, cam.tanx, cam.tany, cam.fx,
-                           cam.fy, cam.gx, cam.gy, gs, radii);
+#define GSR_PRE_ARGS                                                                                                 \
+    in.P, in.D, in.M, in.means3D, in.scales, in.scale_modifier, in.rotations, in.opacities, in.shs, in.colors_precomp, \
+        in.cov3D_precomp, cam.view, cam.proj, cam.campos, cam.W, cam.H, cam.tanx, cam.tany, cam.fx, cam.fy, cam.gx,   \
+        cam.gy, gs, radii
+    if (split_color)
+        hipLaunchKernelGGL((preprocess_kernel<true, true>), dim3(blocks), dim3(256), 0, s, GSR_PRE_ARGS);
+    else if (vec)
+        hipLaunchKernelGGL((preprocess_kernel<true, false>), dim3(blocks), dim3(256), 0, s, GSR_PRE_ARGS);
     else
-        hipLaunchKernelGGL(preprocess_kernel<false>, dim3(blocks), dim3(256), 0, s, in.P, in.D, in.M, in.means3D,
-                           in.scales, in.scale_modifier, in.rotations, in.opacities, in.shs, in.colors_precomp,
-                           in.cov3D_precomp, cam.view, cam.proj, cam.campos, cam.W, cam.H, cam.tanx, cam.tany, cam.fx,
-                           cam.fy, cam.gx, cam.gy, gs, radii);
+        hipLaunchKernelGGL((preprocess_kernel<false, false>), dim3(blocks), dim3(256), 0, s, GSR_PRE_ARGS);
+#undef GSR_PRE_ARGS
 }
 
-
+void launch_preprocess_color(const GaussianInputs &in, const Camera &cam, const GeomState &gs, const int *radii,
+                             hipStream_t s) {
+    if (in.P == 0) return;
+    hipLaunchKernelGGL(preprocess_color_kernel, dim3((in.P + kColorThreads - 1) / kColorThreads), dim3(kColorThreads),
+                       0, s, in.P, in.D, in.means3D, in.shs, cam.campos, radii, gs);
+}
 
 __global__ __launch_bounds__(256) void mark_visible_kernel(int P, const float *__restrict__ means3D,
                                                            const float *__restrict__ viewmatrix,

@@ -20,12 +20,50 @@ thread_local std::string g_err;
 thread_local uint32_t *g_pinned = nullptr;
 
 // Stage profiling is process-wide: torch runs the backward on its autograd device thread.
-constexpr int kStages = 8;
+constexpr int kStages = 9;
 std::mutex g_prof_mu;
 int g_profile = 0;
 bool g_ev_init = false;
 hipEvent_t g_ev_begin[kStages], g_ev_end[kStages];
 bool g_ev_recorded[kStages];
+
+// Side stream for work that overlaps the main stream's latency-bound stages (the SH colour
+// pass runs beside the depth sort and the binning); fork / join with events, so it also works
+// inside a captured HIP graph.  One per device, created on first use.
+constexpr int kMaxDevices = 64;
+std::mutex g_side_mu;
+hipStream_t g_side[kMaxDevices] = {};
+hipEvent_t g_fork[kMaxDevices] = {}, g_join[kMaxDevices] = {};
+
+#ifndef GSR_SIDE_STREAM
+#define GSR_SIDE_STREAM 1
+#endif
+bool side_stream(hipStream_t main, hipStream_t *side, hipEvent_t *fork, hipEvent_t *join) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return false;
+    std::lock_guard<std::mutex> lk(g_side_mu);
+    if (!g_side[dev]) {
+        if (hipStreamCreateWithFlags(&g_side[dev], hipStreamNonBlocking) != hipSuccess) return false;
+        if (hipEventCreateWithFlags(&g_fork[dev], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&g_join[dev], hipEventDisableTiming) != hipSuccess)
+            return false;
+    }
+    *side = GSR_SIDE_STREAM ? g_side[dev] : main;  // 0: the colour pass serialises (timing experiments)
+    *fork = g_fork[dev];
+    *join = g_join[dev];
+    return true;
+}
+
+// Joins the side stream into the main one when the forward leaves early (errors), so the
+// caller's buffers are never released under side-stream work.
+struct SideJoin {
+    hipStream_t s = nullptr;
+    hipEvent_t join = nullptr;
+    bool pending = false;
+    ~SideJoin() {
+        if (pending) (void)hipStreamWaitEvent(s, join, 0);
+    }
+};
 
 int fail(int code, const std::string &msg) {
     g_err = msg;
@@ -257,11 +295,33 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
 
     GaussianInputs in{P, D, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp,
                       scale_modifier};
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+    const bool split = P > 0 && color_split_supported(in) && side_stream(s, &side, &fork, &join);
+    SideJoin sj;
     {
         StageTimer st(0, s);
-        launch_preprocess(in, cam, gs, radii, s);
+        launch_preprocess(in, cam, gs, radii, s, split);
     }
     if ((rc = check("preprocess", debug, s))) return rc;
+#ifndef GSR_COLOR_FORK
+#define GSR_COLOR_FORK 0  // 0: beside the depth sort and the binning; 1: beside the binning only
+#endif
+    auto fork_color = [&]() -> int {
+        // fork: the SH colours stream in beside latency-bound main-stream stages; joined before render_fwd
+        if (hipEventRecord(fork, s) != hipSuccess || hipStreamWaitEvent(side, fork, 0) != hipSuccess)
+            return fail(GSR_ERR_DEVICE, "side stream fork failed");
+        {
+            StageTimer st(8, side);
+            launch_preprocess_color(in, cam, gs, radii, side);
+        }
+        if (hipEventRecord(join, side) != hipSuccess) return fail(GSR_ERR_DEVICE, "side stream join record failed");
+        sj.s = s;
+        sj.join = join;
+        sj.pending = true;
+        return check("preprocess colour", debug, side);
+    };
+    if (split && GSR_COLOR_FORK == 0 && (rc = fork_color())) return rc;
     {
         StageTimer st(1, s);
         if (depth_sort(gs.tmp, gs.tmp_bytes, gs.dkey, gs.dkey_sorted, gs.ids, gs.order, P, s) != hipSuccess)
@@ -282,6 +342,7 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
         if (hipStreamSynchronize(s) != hipSuccess) return fail(GSR_ERR_DEVICE, "stream sync failed");
         K = (int64_t)*g_pinned;
     }
+    if (split && GSR_COLOR_FORK == 1 && (rc = fork_color())) return rc;
     size_t bbytes = 0;
     carve_binning(nullptr, K, &bbytes);
     void *bbase = binning_buffer(resize_ctx, bbytes);
@@ -303,6 +364,10 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
         launch_tile_order(nullptr, is.ranges, T, 4, is.tile_ids, s);  // forward order: by list length
     }
     if ((rc = check("tile order", debug, s))) return rc;
+    if (split) {
+        sj.pending = false;
+        if (hipStreamWaitEvent(s, join, 0) != hipSuccess) return fail(GSR_ERR_DEVICE, "side stream join failed");
+    }
     {
         StageTimer st(5, s);
         launch_render_fwd(cam, gs, bs, is, background, out_color, out_invdepth, s);

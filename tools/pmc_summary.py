@@ -20,7 +20,8 @@ from collections import defaultdict
 
 STAGE_OF = [("render_bwd_kernel", "render_bwd"), ("render_fwd", "render_fwd"),
             ("preprocess_bwd_kernel", "preprocess_bwd"), ("record_sum_kernel", "record_sum"),
-            ("preprocess_kernel", "preprocess"), ("depth_gather_kernel", "depth_gather"),
+            ("preprocess_color_kernel", "sh_color"), ("preprocess_kernel", "preprocess"),
+            ("depth_gather_kernel", "depth_gather"),
             ("sb_count_kernel", "bin_superblocks:count"), ("sb_colscan_kernel", "bin_superblocks:colscan"),
             ("sb_base_kernel", "bin_superblocks:base"), ("sb_scatter_kernel", "bin_superblocks:scatter"),
             ("tile_bin_kernel", "bin_tiles"), ("tile_order_kernel", "tile_order"), ("mark_visible", "mark_visible"),
