@@ -15,9 +15,11 @@ constexpr uint32_t kRedSerial = 32;
 // zeroing gc).  dL/dsh[k][ch] = B_k gc[ch];  dL/ddir = sum_k dB_k/ddir * (sum_ch sh[k][ch] gc[ch]).
 // The basis and its gradient are evaluated once and shared by the three channels; with M = 16
 // the 192-B coefficient row is read and the gradient row written as 12 float4s.
-template <int D>
+template <int D, bool kRow = false>
 __device__ __forceinline__ void sh_backward(const float *__restrict__ sh, int M, bool vec, const float dir[3],
                                             const float gc[3], float *__restrict__ dsh, float gd[3]) {
+    // kRow: `sh` / `dsh` are this lane's 12-float4 rows of the wave's LDS tile (staged reads,
+    // staged coalesced writes; see preprocess_bwd_kernel)
     constexpr int NC = (D + 1) * (D + 1);
     const float x = dir[0], y = dir[1], z = dir[2];
     float B[16], Bx[16], By[16], Bz[16];
@@ -58,7 +60,7 @@ __device__ __forceinline__ void sh_backward(const float *__restrict__ sh, int M,
         }
     }
     float c[48];
-    if (vec) {
+    if (kRow || vec) {
         const float4 *s4 = reinterpret_cast<const float4 *>(sh);
 #pragma unroll
         for (int q = 0; q < 12; q++) {
@@ -81,7 +83,7 @@ __device__ __forceinline__ void sh_backward(const float *__restrict__ sh, int M,
         gd[1] = fmaf(By[k], vk, gd[1]);
         gd[2] = fmaf(Bz[k], vk, gd[2]);
     }
-    if (vec) {
+    if (kRow || vec) {
         float4 *d4 = reinterpret_cast<float4 *>(dsh);
 #pragma unroll
         for (int q = 0; q < 12; q++) {
@@ -189,6 +191,8 @@ __global__ __launch_bounds__(256) void record_sum_kernel(int P, int gx, const in
     sc.gsum[2 * (size_t)i + 1] = make_float4(g[6], g[7], g[8], 0.f);
 }
 
+constexpr int kShPitch = 13;  // padded LDS row pitch (float4) of the staged SH rows
+
 __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
     int P, int D, int M, const float *__restrict__ means3D, const int *__restrict__ radii,
     const float *__restrict__ shs, const uint8_t *__restrict__ clamped, const float *__restrict__ scales,
@@ -196,6 +200,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
     const float *__restrict__ viewmatrix, const float *__restrict__ projmatrix, const float *__restrict__ campos_p,
     float tanx, float tany, float fx, float fy, int gx, const uint32_t *__restrict__ tiles,
     const GRec *__restrict__ rec, const uint64_t *__restrict__ boundary, BwdScratch sc, GaussianGrads out) {
+    __shared__ float4 s_sh[4 * kWave * kShPitch];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & (kWave - 1);
     const bool valid = i < P;
@@ -205,10 +210,11 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
     const bool vec_sh = M == 16 && (reinterpret_cast<uintptr_t>(shs) % 16 == 0) &&
                         (reinterpret_cast<uintptr_t>(out.dsh) % 16 == 0);
 
-    if (!valid) return;
+    // lanes past P stay to the end of the SH staging (the wave loads and stores rows together)
+    const int iv = valid ? i : 0;
     float g[10];
     {
-        const float4 s0 = sc.gsum[2 * (size_t)i], s1 = sc.gsum[2 * (size_t)i + 1];
+        const float4 s0 = sc.gsum[2 * (size_t)iv], s1 = sc.gsum[2 * (size_t)iv + 1];
         g[0] = g[1] = g[5] = 0.f;  // screen-space mean and opacity: written by record_sum_kernel
         g[2] = s0.x; g[3] = s0.y; g[4] = s0.z; g[9] = s0.w;
         g[6] = s1.x; g[7] = s1.y; g[8] = s1.z;
@@ -221,7 +227,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
     float dm[3] = {0.f, 0.f, 0.f};
     float dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const Mat4 V = load_mat4(viewmatrix);
-    const float3 p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
+    const float3 p = make_float3(means3D[3 * iv], means3D[3 * iv + 1], means3D[3 * iv + 2]);
     float c3[6];
     float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
     float3 s_in = make_float3(0.f, 0.f, 0.f);
@@ -307,7 +313,75 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
     }
 
     // ---- colour ----
-    if (has_shs) {
+    if (has_shs && vec_sh) {
+        // Staged SH rows: the wave's 64 coefficient rows come in as 1 KiB contiguous loads (load k of
+        // lane l = float4 k*64 + l) into a tile with rows padded to 13 float4, each lane reads and
+        // overwrites its own row with dL/dsh, and the tile goes out with the same contiguous stores:
+        // one lane per row would put 64 rows, 192 B apart, under every load and store.
+        const int wv = threadIdx.x >> 6;
+        float4 *S = s_sh + wv * kWave * kShPitch;
+        const uint64_t need = __ballot(vis);
+        const int64_t row0 = (int64_t)blockIdx.x * blockDim.x + wv * kWave;
+        const int cols = ((D + 1) * (D + 1) * 3 + 3) / 4;
+        const float4 *src4 = reinterpret_cast<const float4 *>(shs) + row0 * 12;
+        float4 v[12];
+#pragma unroll
+        for (int k = 0; k < 12; k++) {
+            const int f = k * kWave + lane, row = f / 12;
+            v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (((need >> row) & 1ull) && f - row * 12 < cols) v[k] = src4[f];
+        }
+#pragma unroll
+        for (int k = 0; k < 12; k++) {
+            const int f = k * kWave + lane, row = f / 12;
+            S[row * kShPitch + (f - row * 12)] = v[k];
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+        __builtin_amdgcn_wave_barrier();
+        float4 *mine = S + lane * kShPitch;
+        if (vis) {
+            float dir[3], dor[3];
+            sh_dir(p, make_float3(campos_p[0], campos_p[1], campos_p[2]), dir, dor);
+            const uint8_t cl = clamped[i];
+            float gc[3];
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++) gc[ch] = (cl >> ch) & 1 ? 0.f : g[6 + ch];
+            float gd[3];
+            const float *row = reinterpret_cast<const float *>(mine);
+            float *drow = reinterpret_cast<float *>(mine);
+            switch (D) {
+                case 0: sh_backward<0, true>(row, M, true, dir, gc, drow, gd); break;
+                case 1: sh_backward<1, true>(row, M, true, dir, gc, drow, gd); break;
+                case 2: sh_backward<2, true>(row, M, true, dir, gc, drow, gd); break;
+                default: sh_backward<3, true>(row, M, true, dir, gc, drow, gd); break;
+            }
+            const float s2 = dor[0] * dor[0] + dor[1] * dor[1] + dor[2] * dor[2];
+            const float inv32 = 1.0f / sqrtf(s2 * s2 * s2);
+            dm[0] += ((s2 - dor[0] * dor[0]) * gd[0] - dor[1] * dor[0] * gd[1] - dor[2] * dor[0] * gd[2]) * inv32;
+            dm[1] += (-dor[0] * dor[1] * gd[0] + (s2 - dor[1] * dor[1]) * gd[1] - dor[2] * dor[1] * gd[2]) * inv32;
+            dm[2] += (-dor[0] * dor[2] * gd[0] - dor[1] * dor[2] * gd[1] + (s2 - dor[2] * dor[2]) * gd[2]) * inv32;
+        } else {
+#pragma unroll
+            for (int c = 0; c < 12; c++) mine[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        float4 *dst4 = reinterpret_cast<float4 *>(out.dsh) + row0 * 12;
+#pragma unroll
+        for (int k = 0; k < 12; k++) {
+            const int f = k * kWave + lane, row = f / 12;
+            if (row0 + row < P) dst4[f] = S[row * kShPitch + (f - row * 12)];
+        }
+        if (valid && out.dcolors) {
+            out.dcolors[3 * i + 0] = 0.f;
+            out.dcolors[3 * i + 1] = 0.f;
+            out.dcolors[3 * i + 2] = 0.f;
+        }
+    }
+    if (!valid) return;
+    if (has_shs && vec_sh) {
+        // done above
+    } else if (has_shs) {
         float *dsh = out.dsh + (size_t)i * M * 3;
         if (!vis) {
             if (vec_sh) {
