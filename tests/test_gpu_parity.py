@@ -30,6 +30,8 @@ CASES = [
     dict(name="behind_camera", P=1500, W=96, H=64, deg=3, seed=6, log_scale=-3.0, behind=0.3),
     dict(name="coarse_M4", P=1500, W=96, H=64, deg=1, seed=7, log_scale=-3.0, M=4),
     dict(name="config1_10k_256", P=10000, W=256, H=256, deg=3, seed=0, log_scale=-4.0),
+    # depth ties: 3000 Gaussians at one depth, ordered by id inside every tile
+    dict(name="equal_depths", P=3000, W=96, H=64, deg=1, seed=9, log_scale=-3.0, flat_z=6.0),
 ]
 
 
@@ -39,6 +41,10 @@ def make_scene(c):
                           primx=c.get("primx", 0.5), primy=c.get("primy", 0.5))
     if c.get("M", 16) != 16:
         s["shs"] = np.ascontiguousarray(s["shs"][:, :c["M"], :])
+    if c.get("flat_z"):
+        m = s["means3D"]
+        m[:, :2] *= c["flat_z"] / m[:, 2:3]  # same direction, one depth for every Gaussian
+        m[:, 2] = c["flat_z"]
     if c.get("behind"):
         rng = np.random.default_rng(c["seed"] + 100)
         idx = rng.random(c["P"]) < c["behind"]
@@ -97,6 +103,13 @@ def compare(c, st, g, h, check_grads=True):
     np.testing.assert_array_equal(S["keys"], st["keys"])
     np.testing.assert_array_equal(S["point_list"], st["point_list"])
     np.testing.assert_array_equal(S["ranges"], st["ranges"])
+    # the depth order itself: visible Gaussians by (depth bits, id), then the culled ones
+    vis = (h["radii"] > 0) & (S["tiles_touched"] > 0)
+    nv = int(vis.sum())
+    ids = np.nonzero(vis)[0]
+    want = ids[np.lexsort((ids, S["depths"].view(np.uint32)[ids]))]
+    np.testing.assert_array_equal(S["order"][:nv], want)
+    np.testing.assert_array_equal(np.sort(S["order"][nv:]), np.nonzero(~vis)[0])
     # the raw (superblock-major) ranges partition [0, K) exactly
     r = S["ranges_raw"].astype(np.int64)
     o = np.argsort(r[:, 0], kind="stable")
