@@ -287,16 +287,21 @@ void gso_ranges(unsigned long long K, const unsigned long long *keys, int T, uns
     }
 }
 
-/* Gaussian exponent at pixel offset d = mean2D - pixel, in the fixed FMA order the HIP kernels
- * use:  power = -0.5 (a dx^2 + c dy^2) - b dx dy.  G = exp(power) evaluated as exp2(power*log2e)
- * (the GPU's v_exp_f32 form). */
+/* Gaussian exponent at pixel offset d = mean2D - pixel.  Upstream: power = -0.5 (a dx^2 + c dy^2)
+ * - b dx dy, G = exp(power).  Restated in base 2 with the conic scaled per splat, in the exact
+ * operation order the HIP kernels use (gsr_device.h gauss_p2; the GPU's v_exp_f32 is exp2):
+ *   a_s = a (-0.5 log2e), b_s = b log2e, c_s = c (-0.5 log2e)
+ *   p2 = fma(-(b_s dx), dy, fma(c_s dy, dy, a_s dx dx)) = log2(G),  G = exp2(p2)
+ * p2 > 0 <=> power > 0 up to rounding: the same test upstream applies to power. */
 static const float GS_LOG2E = 1.4426950408889634f;
-static inline float gauss_power(const float *co, float dx, float dy) {
-    const float adxdx = co[0] * dx * dx;
-    const float t = fmaf(co[2] * dy, dy, adxdx);
-    return fmaf(-(co[1] * dx), dy, -0.5f * t);
+static const float GS_HALF_LOG2E = -0.5f * 1.4426950408889634f;
+static inline float gauss_p2(const float *co, float dx, float dy) {
+    const float as = co[0] * GS_HALF_LOG2E, bs = co[1] * GS_LOG2E, cs = co[2] * GS_HALF_LOG2E;
+    const float adxdx = as * dx * dx;
+    const float t = fmaf(cs * dy, dy, adxdx);
+    return fmaf(-(bs * dx), dy, t);
 }
-static inline float gexp(float power) { return exp2f(power * GS_LOG2E); }
+static inline float gexp2(float p2) { return exp2f(p2); }
 
 /* ------------------------------------------------------------------------------------------
  * Render forward (A9): per tile front-to-back alpha blending, colour + inverse depth.
@@ -322,9 +327,9 @@ void gso_render_fwd(int W, int H, const unsigned int *ranges, const unsigned int
                     unsigned g = point_list[s];
                     float dx = xy[2 * g] - pfx, dy = xy[2 * g + 1] - pfy;
                     const float *co = conic_opacity + 4 * g;
-                    float power = gauss_power(co, dx, dy);
-                    if (power > 0.0f) continue;
-                    float alpha = fminf_(0.99f, co[3] * gexp(power));
+                    float p2 = gauss_p2(co, dx, dy);
+                    if (p2 > 0.0f) continue;
+                    float alpha = fminf_(0.99f, co[3] * gexp2(p2));
                     if (alpha < 1.0f / 255.0f) continue;
                     float test_T = T * (1.f - alpha);
                     if (test_T < 0.0001f) break;
@@ -383,9 +388,9 @@ void gso_render_bwd(int W, int H, const unsigned int *ranges, const unsigned int
                     unsigned g = point_list[s];
                     float dx = xy[2 * g] - pfx, dy = xy[2 * g + 1] - pfy;
                     const float *co = conic_opacity + 4 * g;
-                    float power = gauss_power(co, dx, dy);
-                    if (power > 0.0f) continue;
-                    float G = gexp(power);
+                    float p2 = gauss_p2(co, dx, dy);
+                    if (p2 > 0.0f) continue;
+                    float G = gexp2(p2);
                     float alpha = fminf_(0.99f, co[3] * G);
                     if (alpha < 1.0f / 255.0f) continue;
                     float rc = 1.f / (1.f - alpha);

@@ -336,9 +336,15 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 // ------------------------------------------------------------------------------------------
 constexpr float kLog2e = 1.4426950408889634f;
 
-// power = -0.5 (a dx^2 + c dy^2) - b dx dy in the fixed FMA order the oracle restates
-__device__ __forceinline__ float gauss_power(float adxdx, float bdx, float c, float dy) {
-    return fmaf(-bdx, dy, -0.5f * fmaf(c * dy, dy, adxdx));
+// The Gaussian's exponent in base 2, p2 = log2(G) = log2(e) (-0.5 (a dx^2 + c dy^2) - b dx dy), from
+// the conic scaled once per instance: a_s = a (-0.5 log2e), b_s = b log2e, c_s = c (-0.5 log2e)
+// (render kernels scale it when they stage an instance in LDS).  Per pixel:
+//   p2 = fma(-(b_s dx), dy, fma(c_s dy, dy, a_s dx dx)),  G = exp2(p2)
+// -- two multiplies fewer than forming -0.5(...) and scaling by log2e per pixel.  The oracle
+// restates this order exactly (oracle/gs_oracle.c gauss_p2).
+constexpr float kHalfLog2e = -0.5f * 1.4426950408889634f;  // exact: a power-of-two scaling
+__device__ __forceinline__ float gauss_p2(float adxdx_s, float bdx_s, float c_s, float dy) {
+    return fmaf(-bdx_s, dy, fmaf(c_s * dy, dy, adxdx_s));
 }
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }

@@ -99,8 +99,9 @@ __global__ __launch_bounds__(64) void render_fwd_kernel(
         const uint32_t cnt = (uint32_t)__popcll(keep);
         if (m) {
             const uint32_t slot = lane_prefix(keep);
-            s_a[slot] = qa;
-            s_b[slot] = make_float4(qb.x, qb.y, __uint_as_float(base - rg.x + (uint32_t)lane + 1u), __uint_as_float(m));
+            s_a[slot] = make_float4(qa.x, qa.y, qa.z * kHalfLog2e, qa.w * kLog2e);  // scaled conic: gauss_p2
+            s_b[slot] = make_float4(qb.x * kHalfLog2e, qb.y, __uint_as_float(base - rg.x + (uint32_t)lane + 1u),
+                                    __uint_as_float(m));
             s_c[slot] = qc;
         }
         __syncthreads();
@@ -117,9 +118,9 @@ __global__ __launch_bounds__(64) void render_fwd_kernel(
             for (int k = 0; k < kPixPerLane; k++) {
                 if (!(mk & (1u << k))) continue;  // scalar branch: sub-block k culled
                 const float dy = a.y - pfy[k];
-                const float power = gauss_power(adxdx, bdx, b.x, dy);
-                const float alpha = fmin_(0.99f, b.y * gexp2(power * kLog2e));
-                const bool ok = alive[k] && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+                const float p2 = gauss_p2(adxdx, bdx, b.x, dy);
+                const float alpha = fminf(0.99f, b.y * gexp2(p2));
+                const bool ok = alive[k] && !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f);
                 const float test_T = T[k] * (1.f - alpha);
                 const bool stop = test_T < 0.0001f;
                 const bool acc = ok && !stop;
@@ -205,8 +206,8 @@ __global__ __launch_bounds__(256) void render_fwd_sb_kernel(
         const uint32_t cnt = (uint32_t)__popcll(keep);
         if (hit) {
             const uint32_t slot = lane_prefix(keep);
-            s_q[w][0][slot] = qa;
-            s_q[w][1][slot] = qb;
+            s_q[w][0][slot] = make_float4(qa.x, qa.y, qa.z * kHalfLog2e, qa.w * kLog2e);  // scaled conic: gauss_p2
+            s_q[w][1][slot] = make_float4(qb.x * kHalfLog2e, qb.y, qb.z, qb.w);
             s_q[w][2][slot] = qc;
         }
         // wave-private LDS slice: the wave's own writes are visible after its lgkmcnt drain
@@ -224,9 +225,9 @@ __global__ __launch_bounds__(256) void render_fwd_sb_kernel(
             rem &= rem - 1ull;
             const float dx = a.x - pfx;
             const float dy = a.y - pfy;
-            const float power = gauss_power(a.z * dx * dx, a.w * dx, b.x, dy);
-            const float alpha = fmin_(0.99f, b.y * gexp2(power * kLog2e));
-            const bool ok = alive && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+            const float p2 = gauss_p2(a.z * dx * dx, a.w * dx, b.x, dy);
+            const float alpha = fminf(0.99f, b.y * gexp2(p2));
+            const bool ok = alive && !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f);
             const float test_T = T * (1.f - alpha);
             const bool stop = test_T < 0.0001f;
             const bool acc = ok && !stop;
@@ -351,6 +352,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
     __shared__ float4 s_a[kWave];
     __shared__ float4 s_b[kWave];  // conic.c, opacity, list position, sub-block mask
     __shared__ float4 s_c[kWave];
+    __shared__ float4 s_d[kWave];  // scaled conic (gauss_p2); s_a / s_b keep the conic for the finalisation
     __shared__ uint32_t s_u[kWave];
     __shared__ float2 s_red[kWave * 2 * 5];  // per instance, per half wave: 10 partial sums
 
@@ -440,6 +442,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
             s_a[slot] = qa;
             s_b[slot] = make_float4(qb.x, qb.y, __uint_as_float(pos), __uint_as_float(m));
             s_c[slot] = qc;
+            s_d[slot] = make_float4(qa.z * kHalfLog2e, qa.w * kLog2e, qb.x * kHalfLog2e, 0.f);
             s_u[slot] = u;
         }
         __syncthreads();
@@ -447,11 +450,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
             const float4 a = s_a[j];
             const float4 b = s_b[j];
             const float4 c = s_c[j];
+            const float4 cs = s_d[j];
             const uint32_t mk = __builtin_amdgcn_readfirstlane(__float_as_uint(b.w));
             const uint32_t jpos = __builtin_amdgcn_readfirstlane(__float_as_uint(b.z));
             const float dx = a.x - pfx;
-            const float adxdx = a.z * dx * dx;
-            const float bdx = a.w * dx;
+            const float adxdx_s = cs.x * dx * dx;
+            const float bdx_s = cs.y * dx;
             float q[10];
 #pragma unroll
             for (int t = 0; t < 10; t++) q[t] = 0.f;
@@ -462,10 +466,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
                 if (!((mk >> k) & 1u)) continue;  // scalar branch: sub-block k culled for this instance
 #endif
                 const float dy = a.y - pfy[k];
-                const float power = gauss_power(adxdx, bdx, b.x, dy);
-                const float G = gexp2(power * kLog2e);
-                const float alpha = fmin_(0.99f, b.y * G);
-                const bool ok = ((mk >> k) & 1u) && jpos < last[k] && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+                const float p2 = gauss_p2(adxdx_s, bdx_s, cs.z, dy);
+                const float G = gexp2(p2);
+                const float alpha = fminf(0.99f, b.y * G);
+                const bool ok = ((mk >> k) & 1u) && jpos < last[k] && !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f);
                 any = any || ok;
                 const float ae = ok ? alpha : 0.f;
                 const float rc = __builtin_amdgcn_rcpf(1.f - ae);
