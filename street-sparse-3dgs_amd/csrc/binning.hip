@@ -2,7 +2,7 @@
 //
 // Upstream emits K (tile << 32 | depth) keys and radix-sorts them (6 passes over 24-B pairs at
 // 1080p), then scans the sorted keys for tile ranges.  Here the Gaussians are already in depth
-// order (one 32-bit sort of P keys, sort.hip), and the per-tile lists are built by two stable
+// order (one 32-bit sort of P keys, dsort.hip), and the per-tile lists are built by two stable
 // counting passes that exploit each splat's footprint being a rectangle of tiles:
 //
 //   level 1  Gaussian -> superblock (SB = 2^s x 2^s tiles, ~500 at 1080p).  Chunks of 2048
@@ -17,8 +17,7 @@
 //
 // The result is the upstream order inside every tile -- (depth bits, Gaussian id) -- with tiles
 // laid out SB-major instead of row-major; every consumer goes through `ranges`, so the layout of
-// whole tiles in point_list is free.  Also writes rec[g].off (the Gaussian-major instance offset
-// the backward records use).  Traffic ~ 8 B per SB instance + 4 B per tile instance written.
+// whole tiles in point_list is free.  Traffic ~ 8 B per SB instance + 4 B per tile instance written.
 #include "gsr_launch.h"
 
 namespace gsr {
@@ -41,33 +40,12 @@ __device__ __forceinline__ TileRect unpack_rect(uint2 d) {
 }
 
 // Depth-ordered rect / tile count of every Gaussian: the one random gather of the binning.
-__global__ __launch_bounds__(256) void depth_gather_kernel(int P, const GRec *__restrict__ rec,
-                                                           const uint32_t *__restrict__ order,
-                                                           const uint32_t *__restrict__ tiles, uint2 *__restrict__ drect,
-                                                           uint32_t *__restrict__ dtiles) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= P) return;
-    const uint32_t g = order[j];
-    const uint32_t area = tiles[g];
-    uint2 d = make_uint2(0u, 0u);
-    if (area > 0) {
-        const uint4 q3 = reinterpret_cast<const uint4 *>(rec + g)[3];
-        const uint32_t w = q3.y, x0 = q3.x & 0xFFFFu, y0 = q3.x >> 16;
-        d = make_uint2(q3.x, (x0 + w) | ((y0 + area / w) << 16));
-    }
-    drect[j] = d;
-    dtiles[j] = area;
-}
-
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
 // Level 1, pass 1: per chunk and SB, the number of Gaussians and of tile instances.
-__global__ __launch_bounds__(1024) void sb_count_kernel(int P, SBGrid sg, GRec *__restrict__ rec,
-                                                       const uint32_t *__restrict__ order,
-                                                       const uint2 *__restrict__ drect,
-                                                       const uint32_t *__restrict__ offsets,
+__global__ __launch_bounds__(1024) void sb_count_kernel(int P, SBGrid sg, const uint2 *__restrict__ drect,
                                                        uint32_t *__restrict__ cnt_g, uint32_t *__restrict__ cnt_i) {
     extern __shared__ uint32_t lds[];
     uint32_t *cg = lds, *ci = lds + sg.nsb;
@@ -78,7 +56,6 @@ __global__ __launch_bounds__(1024) void sb_count_kernel(int P, SBGrid sg, GRec *
     for (int j = j0 + (int)threadIdx.x; j < j1; j += 1024) {
         const TileRect r = unpack_rect(drect[j]);
         if (r.x1 < r.x0) continue;
-        rec[order[j]].off = j == 0 ? 0u : offsets[j - 1];
         const int side = 1 << sg.shift;
         for (int sy = r.y0 >> sg.shift; sy <= r.y1 >> sg.shift; sy++) {
             const int h = min(r.y1, sy * side + side - 1) - max(r.y0, sy * side) + 1;
@@ -425,12 +402,6 @@ __global__ __launch_bounds__(64 * kTBWaves) void tile_bin_kernel(SBGrid sg, int 
 
 }  // namespace
 
-void launch_depth_gather(int P, const GeomState &gs, hipStream_t s) {
-    if (P == 0) return;
-    hipLaunchKernelGGL(depth_gather_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, gs.rec, gs.order, gs.tiles,
-                       gs.drect, gs.dtiles);
-}
-
 SBGrid sb_grid(int gx, int gy, int P) {
     SBGrid g;
     g.shift = 2;
@@ -456,8 +427,8 @@ void launch_binning_superblocks(int P, const Camera &cam, const GeomState &gs, c
     if (P == 0 || cam.gx * cam.gy == 0) return;
     const size_t l1 = sizeof(uint32_t) * 2 * (size_t)sg.nsb;
     const size_t l3 = sizeof(uint32_t) * 3 * kScatterWaves * (size_t)sg.nsb;
-    hipLaunchKernelGGL(sb_count_kernel, dim3(sg.nchunks), dim3(1024), l1, s, P, sg, gs.rec, gs.order, gs.drect,
-                       gs.offsets, gs.sb_cnt_g, gs.sb_cnt_i);
+    hipLaunchKernelGGL(sb_count_kernel, dim3(sg.nchunks), dim3(1024), l1, s, P, sg, gs.drect, gs.sb_cnt_g,
+                       gs.sb_cnt_i);
     hipLaunchKernelGGL(sb_colscan_kernel, dim3(sg.nsb), dim3(256), 0, s, sg, gs.sb_cnt_g, gs.sb_cnt_i, gs.sb_base_g,
                        gs.sb_base_i);
     hipLaunchKernelGGL(sb_base_kernel, dim3(1), dim3(256), 0, s, sg.nsb, gs.sb_base_g, gs.sb_base_i);

@@ -374,14 +374,14 @@ struct SBGrid {
 struct GeomState {          // per Gaussian, written by preprocess
     GRec *rec;
     uint32_t *tiles;        // tiles_touched
-    uint32_t *dkey;         // depth sort key: depth bits, 0xFFFFFFFF when culled
-    uint32_t *dkey_sorted;
-    uint32_t *ids;          // 0..P-1
+    uint32_t *dkey;         // depth sort key: depth bits, 0xFFFFFFFF when culled (clobbered by the sort)
+    uint32_t *dkey_sorted;  // sort ping-pong buffer
+    uint32_t *ids;          // sort ping-pong buffer (values)
     uint32_t *order;        // Gaussian ids in (depth, id) order
-    uint32_t *offsets;      // inclusive scan of tiles_touched in depth order
+    uint32_t *offsets;      // unused (kept: the scratch layout the tests decode)
     uint8_t *clamped;       // bit c set: SH channel c clamped at 0
-    void *tmp;              // depth-sort / scan temp storage
-    size_t tmp_bytes;
+    uint32_t *ctrl;         // depth-sort control words (dsort.hip), zeroed by the preprocess
+    uint32_t ctrl_words;
     uint2 *drect;           // per depth-order slot: tile rect (x0 | y0 << 16, x1 | y1 << 16), 0/0 = none
     uint32_t *dtiles;       // per depth-order slot: tiles_touched (the scan input)
     SBGrid sb;              // level-1 binning counters: [nsb][nchunks] Gaussians / instances,

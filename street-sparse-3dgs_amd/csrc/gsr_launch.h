@@ -36,19 +36,21 @@ void launch_tile_order(const uint32_t *work, const uint2 *ranges, int T, int shi
 void launch_mark_visible(int P, const float *means3D, const float *view, uint8_t *present, hipStream_t s);
 
 // sort.hip (rocPRIM)
-size_t scan_temp_bytes(int P);
-hipError_t inclusive_scan(void *tmp, size_t tmp_bytes, const uint32_t *in, uint32_t *out, int P, hipStream_t s);
 // Stable LSD sort of n (key, value) pairs over key bits [0, end_bit) (kNN Morton order).
 size_t sort_pairs_temp_bytes(size_t n, int end_bit);
 hipError_t sort_pairs(void *tmp, size_t tmp_bytes, const uint32_t *kin, uint32_t *kout, const uint32_t *vin,
                       uint32_t *vout, size_t n, int end_bit, hipStream_t s);
-size_t depth_sort_temp_bytes(int P);
-hipError_t depth_sort(void *tmp, size_t tmp_bytes, const uint32_t *kin, uint32_t *kout, const uint32_t *vin,
-                      uint32_t *vout, int P, hipStream_t s);
+// dsort.hip: the stable (depth bits, id) order of the P Gaussians (gs.order), depth-ordered tile
+// rects / counts (gs.drect, gs.dtiles), the Gaussian-major record offsets (rec.off) and
+// K = sum of tiles_touched, stored to *dsort_K_word and, when host_K != NULL, to that pinned
+// host word; k_ready (optional) is recorded once K is final, before the sort passes run.
+int dsort_blocks(int P);
+size_t dsort_ctrl_words(int P);
+void launch_depth_sort(int P, const GeomState &gs, uint32_t *host_K, hipStream_t s, hipEvent_t k_ready);
+uint32_t *dsort_K_word(const GeomState &gs);
+uint32_t *dsort_err_word(const GeomState &gs);
 // binning.hip: per-tile lists from the depth-ordered Gaussians (two stable counting levels).
 SBGrid sb_grid(int gx, int gy, int P);
-// Depth-ordered copies of each Gaussian's tile rect and tile count (one gather pass after the sort).
-void launch_depth_gather(int P, const GeomState &gs, hipStream_t s);
 bool sb_grid_supported(const SBGrid &g);
 void launch_binning_superblocks(int P, const Camera &cam, const GeomState &gs, const BinningState &bs,
                                 const ImageState &is, hipStream_t s);

@@ -16,13 +16,14 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
     const float *__restrict__ viewmatrix, const float *__restrict__ projmatrix, const float *__restrict__ campos,
     int W, int H, float tanx, float tany, float fx, float fy, int gx, int gy, GeomState gs, int *__restrict__ radii) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    // the depth sort's control words (tickets, histograms, lookback status) start at zero
+    for (uint32_t c = (uint32_t)i; c < gs.ctrl_words; c += gridDim.x * blockDim.x) gs.ctrl[c] = 0u;
     if (i >= P) return;
     const Mat4 V = load_mat4(viewmatrix);
     const Mat4 Pm = load_mat4(projmatrix);
     radii[i] = 0;
     gs.tiles[i] = 0;
     gs.dkey[i] = 0xFFFFFFFFu;  // culled Gaussians sort behind every visible one
-    gs.ids[i] = (uint32_t)i;
     const float3 p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
     const float3 pv = xf_point43(p, V);
     if (pv.z <= 0.2f) return;  // in_frustum (prefiltered is treated as a plain cull)

@@ -1,8 +1,9 @@
 // rasterizer.hip -- the C ABI (include/gsr.h): buffer carving, stage orchestration, the one
 // device->host read of K (num_rendered), debug checking and per-stage HIP-event timing.
 //
-// Flow per frame:  preprocess -> inclusive scan -> [D2H K] ->
-// duplicate-with-keys -> radix sort (32 + bits(T) bits) -> tile ranges -> render fwd;
+// Flow per frame:  preprocess -> depth sort (histograms + tile scan ->
+// [K to the host] -> 4 radix passes, the last one gathering the depth-ordered tile rects) ->
+// two-level binning (tile lists + ranges) -> render fwd;
 // backward: render bwd (per-instance records) -> preprocess bwd (per-Gaussian sum + chain).
 #include <cstdio>
 #include <cstring>
@@ -17,7 +18,14 @@ using namespace gsr;
 namespace {
 
 thread_local std::string g_err;
+// K (num_rendered) arrives in pinned, host-coherent memory written by the depth sort's first
+// kernel; the host waits on an event recorded right after it, so the sort passes keep running
+// while the host sizes the binning buffer.
 thread_local uint32_t *g_pinned = nullptr;
+thread_local uint32_t *g_pinned_dev = nullptr;
+constexpr int kMaxDevicesK = 64;
+thread_local hipEvent_t g_k_ready[kMaxDevicesK] = {};
+constexpr uint32_t kKPending = 0xFFFFFFFFu;
 
 // Stage profiling is process-wide: torch runs the backward on its autograd device thread.
 constexpr int kStages = 9;
@@ -130,9 +138,8 @@ GeomState carve_geom(void *base, int P, int gx, int gy, size_t *bytes) {
     g.order = c.take<uint32_t>(P);
     g.offsets = c.take<uint32_t>(P);
     g.clamped = c.take<uint8_t>(P);
-    const size_t a = scan_temp_bytes(P), b = depth_sort_temp_bytes(P);
-    g.tmp_bytes = a > b ? a : b;
-    g.tmp = c.take<char>(g.tmp_bytes);
+    g.ctrl_words = (uint32_t)dsort_ctrl_words(P);
+    g.ctrl = c.take<uint32_t>(g.ctrl_words);
     g.drect = c.take<uint2>(P);
     g.dtiles = c.take<uint32_t>(P);
     g.sb = sb_grid(gx, gy, P);
@@ -221,8 +228,9 @@ int gsr_abi_version(void) { return GSR_ABI_VERSION; }
 const char *gsr_last_error(void) { return g_err.c_str(); }
 
 const char *gsr_build_info(void) {
-    return "gsr_hip gfx950: preprocess/duplicate/ranges (preprocess.hip), rocPRIM depth sort + tile sort (sort.hip), "
-           "wave-per-tile render fwd/bwd with DPP reductions (render.hip), per-Gaussian backward (backward.hip)";
+    return "gsr_hip gfx950: preprocess (preprocess.hip), onesweep depth sort with fused tile scan / gather "
+           "(dsort.hip), two-level counting binning (binning.hip), sub-block render fwd / wave-per-tile render bwd "
+           "with DPP reductions (render.hip), per-Gaussian backward (backward.hip)";
 }
 
 int gsr_set_profiling(int enable) {
@@ -322,25 +330,41 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
         return check("preprocess colour", debug, side);
     };
     if (split && GSR_COLOR_FORK == 0 && (rc = fork_color())) return rc;
-    {
-        StageTimer st(1, s);
-        if (depth_sort(gs.tmp, gs.tmp_bytes, gs.dkey, gs.dkey_sorted, gs.ids, gs.order, P, s) != hipSuccess)
-            return fail(GSR_ERR_DEVICE, "depth sort failed");
-        launch_depth_gather(P, gs, s);
-        if (inclusive_scan(gs.tmp, gs.tmp_bytes, gs.dtiles, gs.offsets, P, s) != hipSuccess)
-            return fail(GSR_ERR_DEVICE, "inclusive scan failed");
-    }
-    if ((rc = check("depth sort / scan", debug, s))) return rc;
-    int64_t K = 0;
+    hipEvent_t k_ready = nullptr;
     if (P > 0) {
         if (!g_pinned) {
-            if (hipHostMalloc(reinterpret_cast<void **>(&g_pinned), sizeof(uint32_t)) != hipSuccess)
+            if (hipHostMalloc(reinterpret_cast<void **>(&g_pinned), sizeof(uint32_t), hipHostMallocCoherent) !=
+                    hipSuccess ||
+                hipHostGetDevicePointer(reinterpret_cast<void **>(&g_pinned_dev), g_pinned, 0) != hipSuccess)
                 return fail(GSR_ERR_ALLOCATION, "pinned host allocation failed");
         }
-        if (hipMemcpyAsync(g_pinned, gs.offsets + (P - 1), sizeof(uint32_t), hipMemcpyDeviceToHost, s) != hipSuccess)
-            return fail(GSR_ERR_DEVICE, "num_rendered copy failed");
-        if (hipStreamSynchronize(s) != hipSuccess) return fail(GSR_ERR_DEVICE, "stream sync failed");
-        K = (int64_t)*g_pinned;
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevicesK)
+            return fail(GSR_ERR_DEVICE, "no current device");
+        if (!g_k_ready[dev] && hipEventCreateWithFlags(&g_k_ready[dev], hipEventDisableTiming) != hipSuccess)
+            return fail(GSR_ERR_DEVICE, "event creation failed");
+        k_ready = g_k_ready[dev];
+        __atomic_store_n(g_pinned, kKPending, __ATOMIC_SEQ_CST);
+    }
+    {
+        StageTimer st(1, s);
+        launch_depth_sort(P, gs, g_pinned_dev, s, k_ready);
+    }
+    if ((rc = check("depth sort", debug, s))) return rc;
+    int64_t K = 0;
+    if (P > 0) {
+        if (hipEventSynchronize(k_ready) != hipSuccess) return fail(GSR_ERR_DEVICE, "num_rendered wait failed");
+        uint32_t k = __atomic_load_n(g_pinned, __ATOMIC_SEQ_CST);
+        if (k == kKPending) {  // not expected: read the device copy instead
+            if (hipMemcpy(&k, dsort_K_word(gs), sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
+                return fail(GSR_ERR_DEVICE, "num_rendered copy failed");
+        }
+        if (debug) {
+            uint32_t err = 0;
+            if (hipMemcpy(&err, dsort_err_word(gs), sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess || err)
+                return fail(GSR_ERR_DEVICE, "depth sort: a lookback spin timed out");
+        }
+        K = (int64_t)k;
     }
     if (split && GSR_COLOR_FORK == 1 && (rc = fork_color())) return rc;
     size_t bbytes = 0;

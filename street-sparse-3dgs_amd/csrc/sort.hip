@@ -1,12 +1,6 @@
-// sort.hip -- the depth sort of the P Gaussians and the gathered scan of their tile counts, on
-// rocPRIM.
-//
-// Binning order.  Upstream sorts K (tile << 32 | depth bits) 64-bit keys over 32 + bits(T)
-// bits (6 LSD passes of 8 bits at 1080p).  Here only the P Gaussians are sorted, stably by their
-// 32-bit depth bits (ties by id, as upstream's key order breaks them); binning.hip then builds
-// every tile's list from this order with stable counting passes, which yields exactly the
-// upstream (tile, depth, id) order inside each tile.  Kept in its own translation unit:
-// rocPRIM's templates dominate compile time.
+// sort.hip -- rocPRIM pair sort for the kNN initialisation's Morton order (knn.hip).  The
+// rasterizer's depth sort is dsort.hip.  Kept in its own translation unit: rocPRIM's templates
+// dominate compile time.
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 #include "gsr_launch.h"
@@ -31,32 +25,6 @@ using OnesweepCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim:
 #endif
 
 }  // namespace
-
-size_t scan_temp_bytes(int P) {
-    size_t bytes = 0;
-    rocprim::inclusive_scan(nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)(P > 0 ? P : 1),
-                            rocprim::plus<uint32_t>());
-    return bytes;
-}
-
-hipError_t inclusive_scan(void *tmp, size_t tmp_bytes, const uint32_t *in, uint32_t *out, int P, hipStream_t s) {
-    if (P == 0) return hipSuccess;
-    return rocprim::inclusive_scan(tmp, tmp_bytes, in, out, (size_t)P, rocprim::plus<uint32_t>(), s);
-}
-
-size_t depth_sort_temp_bytes(int P) {
-    size_t bytes = 0;
-    rocprim::radix_sort_pairs<OnesweepCfg>(nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                                           (const uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)(P > 0 ? P : 1),
-                                           0, 32);
-    return bytes;
-}
-
-hipError_t depth_sort(void *tmp, size_t tmp_bytes, const uint32_t *kin, uint32_t *kout, const uint32_t *vin,
-                      uint32_t *vout, int P, hipStream_t s) {
-    if (P == 0) return hipSuccess;
-    return rocprim::radix_sort_pairs<OnesweepCfg>(tmp, tmp_bytes, kin, kout, vin, vout, (size_t)P, 0, 32, s);
-}
 
 size_t sort_pairs_temp_bytes(size_t n, int end_bit) {
     size_t bytes = 0;

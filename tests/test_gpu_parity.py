@@ -32,6 +32,8 @@ CASES = [
     dict(name="config1_10k_256", P=10000, W=256, H=256, deg=3, seed=0, log_scale=-4.0),
     # depth ties: 3000 Gaussians at one depth, ordered by id inside every tile
     dict(name="equal_depths", P=3000, W=96, H=64, deg=1, seed=9, log_scale=-3.0, flat_z=6.0),
+    # many depth-sort tiles (8192 keys each) with ties across tiles and culled Gaussians mixed in
+    dict(name="sort_tiles_ties", P=40000, W=128, H=96, deg=0, seed=14, log_scale=-3.5, behind=0.2, quant_z=0.25),
 ]
 
 
@@ -45,6 +47,11 @@ def make_scene(c):
         m = s["means3D"]
         m[:, :2] *= c["flat_z"] / m[:, 2:3]  # same direction, one depth for every Gaussian
         m[:, 2] = c["flat_z"]
+    if c.get("quant_z"):
+        m = s["means3D"]
+        z = np.maximum(np.round(m[:, 2] / c["quant_z"]), 1.0).astype(np.float32) * np.float32(c["quant_z"])
+        m[:, :2] *= z[:, None] / m[:, 2:3]
+        m[:, 2] = z
     if c.get("behind"):
         rng = np.random.default_rng(c["seed"] + 100)
         idx = rng.random(c["P"]) < c["behind"]
@@ -95,6 +102,18 @@ def run_hip(s, c, dcol, dinv, colors_precomp=None, cov3D_precomp=None):
                 radii=radii.cpu().numpy(), grads=grads)
 
 
+def check_record_offsets(S, vis, K):
+    """rec.off (the backward's Gaussian-major record base): the visible Gaussians' ranges
+    [off, off + tiles_touched) partition [0, K) exactly."""
+    off = S["rec"][:, 15].view(np.uint32)[vis].astype(np.int64)
+    n = S["tiles_touched"][vis].astype(np.int64)
+    o = np.argsort(off, kind="stable")
+    off, n = off[o], n[o]
+    if len(off):
+        assert off[0] == 0 and off[-1] + n[-1] == K
+        np.testing.assert_array_equal(off[1:], off[:-1] + n[:-1])
+
+
 def compare(c, st, g, h, check_grads=True):
     assert h["K"] == st["K"], f"K {h['K']} vs oracle {st['K']}"
     np.testing.assert_array_equal(h["radii"], st["radii"])
@@ -110,6 +129,7 @@ def compare(c, st, g, h, check_grads=True):
     want = ids[np.lexsort((ids, S["depths"].view(np.uint32)[ids]))]
     np.testing.assert_array_equal(S["order"][:nv], want)
     np.testing.assert_array_equal(np.sort(S["order"][nv:]), np.nonzero(~vis)[0])
+    check_record_offsets(S, vis, h["K"])
     # the raw (superblock-major) ranges partition [0, K) exactly
     r = S["ranges_raw"].astype(np.int64)
     o = np.argsort(r[:, 0], kind="stable")
@@ -278,6 +298,44 @@ def test_config2_full_size_vs_oracle():
     nz = r[:, 1] > r[:, 0]
     assert int((r[nz, 1] - r[nz, 0]).sum()) == h["K"]
     compare(c, st, g, h)
+
+
+@pytest.mark.gpu
+def test_depth_order_large():
+    """The depth sort at 3M Gaussians (367 sort tiles) with 25% culled: the order is the
+    stable (depth bits, id) order of the visible Gaussians, then the culled ones; the record
+    offsets partition [0, K); K is the sum of tiles_touched."""
+    import torch
+    from diff_gaussian_rasterization import _C
+    c = dict(name="large", P=3_000_000, W=1920, H=1080, deg=0, seed=21, log_scale=-4.0, behind=0.25)
+    s = make_scene(c)
+    dev = torch.device("cuda:0")
+    inp = torch_inputs(s, dev)
+    rs = settings(s, dev, 0)
+    e = torch.empty(0, device=dev)
+    with torch.no_grad():
+        raw = _C.rasterize_gaussians(rs.bg, inp["means3D"], e, inp["opacities"], inp["scales"], inp["rotations"], 1.0,
+                                     e, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height,
+                                     rs.image_width, inp["shs"], 0, rs.campos, False, False, rs.render_indices,
+                                     rs.parent_indices, rs.interpolation_weights, rs.num_node_kids, True)
+    torch.cuda.synchronize()
+    K = int(raw[0])
+    g = raw[4].cpu().numpy()
+    from helpers import geom_layout, view
+    gl = geom_layout(c["P"])
+    rec = view(g, gl, "rec", np.float32, (c["P"], 16))
+    tiles = view(g, gl, "tiles", np.uint32)
+    order = view(g, gl, "order", np.uint32)
+    radii = raw[3].cpu().numpy()
+    vis = (radii > 0) & (tiles > 0)
+    nv = int(vis.sum())
+    assert 0 < nv < c["P"]
+    assert K == int(tiles.astype(np.int64).sum())
+    ids = np.nonzero(vis)[0]
+    dbits = rec[:, 14].view(np.uint32)
+    np.testing.assert_array_equal(order[:nv], ids[np.lexsort((ids, dbits[ids]))])
+    np.testing.assert_array_equal(np.sort(order[nv:]), np.nonzero(~vis)[0])
+    check_record_offsets(dict(rec=rec, tiles_touched=tiles), vis, K)
 
 
 @pytest.mark.gpu
