@@ -10,6 +10,13 @@
 namespace gsr {
 
 constexpr uint32_t kRedSerial = 32;
+#ifndef GSR_REC_BATCH
+#define GSR_REC_BATCH 4
+#endif
+#ifndef GSR_LIVE_UNROLL
+#define GSR_LIVE_UNROLL 8
+#endif
+constexpr int kRecBatch = GSR_REC_BATCH;  // live records loaded together per Gaussian (record_sum)
 
 // SH backward for degree D: rgb_ch = sum_k B_k(dir) sh[k][ch] (+0.5, clamp handled by the caller
 // zeroing gc).  dL/dsh[k][ch] = B_k gc[ch];  dL/ddir = sum_k dB_k/ddir * (sum_ch sh[k][ch] gc[ch]).
@@ -113,6 +120,7 @@ __device__ __forceinline__ void sh_backward(const float *__restrict__ sh, int M,
 __global__ __launch_bounds__(256) void record_sum_kernel(int P, int gx, const int *__restrict__ radii,
                                                          const uint32_t *__restrict__ tiles,
                                                          const GRec *__restrict__ rec,
+                                                         const uint32_t *__restrict__ offsets,
                                                          const uint64_t *__restrict__ boundary, BwdScratch sc,
                                                          float *__restrict__ dmeans2D, float *__restrict__ dopacity) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -131,7 +139,7 @@ __global__ __launch_bounds__(256) void record_sum_kernel(int P, int gx, const in
         y0 = q3.x >> 16;
         w = q3.y;
         key = ((uint64_t)q3.z << 32) | (uint32_t)i;
-        off = q3.w;
+        off = offsets[i];
     }
     auto accumulate = [&](float *acc, uint32_t u) {
         const float4 a = sc.rec[4 * (size_t)u + 0];
@@ -144,7 +152,7 @@ __global__ __launch_bounds__(256) void record_sum_kernel(int P, int gx, const in
     if (n <= kRedSerial && n > 0) {
         uint32_t live = 0, x = x0, y = y0;
         const uint32_t xe = x0 + w;
-#pragma unroll 8
+#pragma unroll GSR_LIVE_UNROLL
         for (uint32_t k = 0; k < n; k++) {
             const uint64_t bk = boundary[y * (uint32_t)gx + x];
             live |= (uint32_t)(bk != 0 && key <= bk) << k;
@@ -153,10 +161,30 @@ __global__ __launch_bounds__(256) void record_sum_kernel(int P, int gx, const in
                 ++y;
             }
         }
+        // live records kRecBatch at a time: all their loads in flight before the adds
         while (live) {
-            const uint32_t k = (uint32_t)__ffs(live) - 1u;
-            live &= live - 1u;
-            accumulate(g, off + k);
+            uint32_t ks[kRecBatch];
+            bool has[kRecBatch];
+#pragma unroll
+            for (int q = 0; q < kRecBatch; q++) {
+                has[q] = live != 0u;
+                ks[q] = has[q] ? (uint32_t)__ffs(live) - 1u : 0u;
+                live &= live - 1u;
+            }
+            float4 ra[kRecBatch], rb[kRecBatch], rc[kRecBatch];
+#pragma unroll
+            for (int q = 0; q < kRecBatch; q++) {
+                const size_t u = 4 * (size_t)(off + ks[q]);
+                ra[q] = has[q] ? sc.rec[u + 0] : make_float4(0.f, 0.f, 0.f, 0.f);
+                rb[q] = has[q] ? sc.rec[u + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+                rc[q] = has[q] ? sc.rec[u + 2] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int q = 0; q < kRecBatch; q++) {
+                g[0] += ra[q].x; g[1] += ra[q].y; g[2] += ra[q].z; g[3] += ra[q].w;
+                g[4] += rb[q].x; g[5] += rb[q].y; g[6] += rb[q].z; g[7] += rb[q].w;
+                g[8] += rc[q].x; g[9] += rc[q].y;
+            }
         }
     }
     for (uint64_t big = __ballot(n > kRedSerial); big; big &= big - 1) {
@@ -478,7 +506,7 @@ void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const Ge
                            const int *radii, const BwdScratch &sc, const GaussianGrads &out, hipStream_t s) {
     if (in.P == 0) return;
     hipLaunchKernelGGL(record_sum_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, cam.gx, radii, gs.tiles,
-                       gs.rec, is.boundary, sc, out.dmeans2D, out.dopacity);
+                       gs.rec, gs.offsets, is.boundary, sc, out.dmeans2D, out.dopacity);
     hipLaunchKernelGGL(preprocess_bwd_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, in.D, in.M, in.means3D,
                        radii, in.shs, gs.clamped, in.scales, in.rotations, in.scale_modifier, in.cov3D_precomp,
                        cam.view, cam.proj, cam.campos, cam.tanx, cam.tany, cam.fx, cam.fy, cam.gx, gs.tiles, gs.rec,

@@ -3,30 +3,31 @@
 //
 // Upstream sorts K (tile << 32 | depth bits) keys; this build sorts only the P depth keys
 // (binning.hip derives every tile's (depth, id) list from this order) and does it with its own
-// onesweep-style kernels instead of a library sort, because at P ~ 1M the library's per-pass
-// launches, memsets and lookback resets cost more than the data movement (~0.17 ms vs ~8 MB
-// per pass):
+// onesweep-style kernels instead of a library sort: at P ~ 1M the library's per-pass launches,
+// memsets and lookback resets cost ~0.17 ms for ~8 MB of data movement per pass.
 //
-//   dsort_upsweep   one read of the keys and tile counts: the four 8-bit digit histograms
-//                   (global, for every pass) and the exclusive scan of tiles_touched in Gaussian
-//                   order (chained single-pass scan) -> rec[g].off, K = the total.  K is also
-//                   stored straight into pinned host memory, so the host can size the binning
+//   dsort_upsweep   one read of the keys and tile counts by <= 128 workgroups: each one's four
+//                   8-bit digit histograms (LDS, written out as one row -- no global atomics on a
+//                   few hot lines) and tiles_touched sums; the last workgroup to finish adds up K
+//                   and stores it straight into pinned host memory, so the host sizes the binning
 //                   buffer while the sort passes still run.
-//   dsort_pass x4   per 8192-key tile (1024 threads, 8 keys each, wave-striped so that wave,
-//                   item, lane order is the input order): match-mask ranking (8 ballots per key)
-//                   into per-wave LDS counters, block digit scan, decoupled lookback per digit
-//                   over the preceding tiles, the tile reordered through LDS by digit, coalesced
-//                   stores.  Pass 0 takes the Gaussian index as the value (no id array); the last
-//                   pass writes the order plus each slot's tile rect and count (the depth gather).
+//   dsort_pass x4   per 8192-key tile (1024 threads, 8 keys each, wave-striped so that wave, item,
+//                   lane order is the input order): the pass's global digit bases from the per-tile
+//                   histograms, match-mask ranking (8 ballots per key) into per-wave LDS counters,
+//                   block digit scan, decoupled lookback per digit over the preceding tiles (16
+//                   predecessors per round trip), the tile reordered through LDS by digit,
+//                   coalesced stores.  Pass 0 takes the Gaussian index as the value (no id array)
+//                   and writes the Gaussian-major record offsets (exclusive scan of tiles_touched
+//                   in index order, gs.offsets); the last pass writes the order and each slot's
+//                   tile rect gathered from the preprocess's compact rect array.
 //
 // Stability: every pass ranks equal digits in input order, so equal depth bits keep Gaussian-id
 // order -- upstream's key (depth bits, then the stable sort's index order).  Culled Gaussians
 // carry key 0xFFFFFFFF and end up behind every visible one.
 //
-// Control words (zeroed by the preprocess kernel, which runs first on the same stream):
-// tickets (one per kernel: tiles are numbered in start order, so a tile only ever waits for
-// tiles that are already running), the 4 x 256 histograms, K, the scan's per-tile status and
-// the per-pass, per-tile, per-digit lookback status (count | flag << 30).
+// Control words: [0, kCtlHead) tickets / counters, then the lookback status of every pass
+// (count | flag << 30) -- zeroed by the preprocess kernel, which runs first on the same stream --
+// then the upsweep's tile offsets, workgroup totals and histogram rows (fully written by it).
 #include "gsr_launch.h"
 
 namespace gsr {
@@ -39,15 +40,27 @@ constexpr int kDsItems = 8;
 constexpr int kDsTile = kDsThreads * kDsItems;
 constexpr int kRadix = 256;
 constexpr int kPasses = 4;
+constexpr int kLookWin = 16;
+constexpr int kMaxResident = 240;  // tiles numbered by blockIdx.x up to this many (< CUs)
 
 // control word offsets
-constexpr int kCtlTicket = 0;                  // [0] upsweep, [1 + p] pass p
-constexpr int kCtlHist = 8;                    // [kPasses][kRadix]
-constexpr int kCtlK = kCtlHist + kPasses * kRadix;
-constexpr int kCtlErr = kCtlK + 1;             // set when a bounded spin gave up (never expected)
-constexpr int kCtlScan = kCtlK + 8;            // [nb] u64 scan status (8-B aligned)
-constexpr int kSpinLimit = 1 << 20;            // ~1 s of polling: a predecessor tile can never take that long
-__host__ __device__ inline size_t ctl_pass(int nb, int p) { return kCtlScan + 2 * (size_t)nb + (size_t)p * nb * kRadix; }
+constexpr int kCtlTicket = 0;  // [p] pass p
+constexpr int kCtlDone = 4;    // upsweep tiles finished
+constexpr int kCtlK = 5;       // sum of tiles_touched
+constexpr int kCtlErr = 6;     // set when a bounded spin gave up (never expected)
+constexpr int kCtlHead = 8;
+// The upsweep runs at most kUpMax workgroups, each over tpb consecutive tiles, so that a pass
+// reduces at most kUpMax histogram rows (kUpMax / 4 loads per thread, all in flight at once).
+constexpr int kUpMax = 128;
+__host__ __device__ inline int up_tpb(int nb) { return (nb + kUpMax - 1) / kUpMax; }
+__host__ __device__ inline int up_blocks(int nb) { return (nb + up_tpb(nb) - 1) / up_tpb(nb); }
+__host__ __device__ inline size_t ctl_status(int nb, int p) { return kCtlHead + (size_t)p * nb * kRadix; }
+__host__ __device__ inline size_t ctl_zero_words(int nb) { return ctl_status(nb, kPasses); }
+__host__ __device__ inline size_t ctl_bex(int nb) { return ctl_zero_words(nb); }              // [nb]
+__host__ __device__ inline size_t ctl_btot(int nb) { return ctl_bex(nb) + nb; }               // [kUpMax]
+__host__ __device__ inline size_t ctl_blkhist(int nb) { return (ctl_btot(nb) + kUpMax + 63) / 64 * 64; }
+__host__ __device__ inline size_t ctl_words(int nb) { return ctl_blkhist(nb) + (size_t)kUpMax * kPasses * kRadix; }
+constexpr int kSpinLimit = 1 << 20;  // ~1 s of polling: a predecessor tile can never take that long
 
 // Diagnostic build only (tools/dsort_bench.hip): per-workgroup phase stamps of s_memrealtime
 // (100 MHz) into g_ds_trace[(kernel * 4096 + block) * 8 + slot].
@@ -66,6 +79,15 @@ __device__ uint64_t *g_ds_trace;
     do {                     \
     } while (0)
 #endif
+#ifdef GSR_DS_TRACE
+#define DS_STAMP_AFTER(kern, slot, x)            \
+    do {                                         \
+        asm volatile("s_waitcnt vmcnt(0)" ::"v"(x)); \
+        DS_STAMP(kern, slot);                    \
+    } while (0)
+#else
+#define DS_STAMP_AFTER(kern, slot, x) DS_STAMP(kern, slot)
+#endif
 
 constexpr uint32_t kFlagAgg = 1u << 30, kFlagInc = 2u << 30, kCountMask = (1u << 30) - 1u;
 
@@ -73,12 +95,6 @@ __device__ __forceinline__ uint32_t ld_agent(const uint32_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void st_agent(uint32_t *p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t ld_agent64(const uint64_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_agent64(uint64_t *p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -120,104 +136,77 @@ __device__ __forceinline__ uint32_t scan256_wave(uint32_t *a, int lane) {
     return (uint32_t)__shfl((int)incl, 63, 64);
 }
 
+// Per workgroup u: tiles [u tpb, (u + 1) tpb): the digit histograms of all passes over its tiles
+// (one LDS add per key and pass; conflicts only where a wave's digits coincide) -> histogram row
+// u; the tiles_touched sum of each tile -> its exclusive offset inside the workgroup (bex) and the
+// workgroup total (btot); K = the sum of the totals, stored by the last workgroup to finish.
 __global__ __launch_bounds__(kDsThreads) void dsort_upsweep_kernel(int P, int nb, const uint32_t *__restrict__ keys,
                                                                     const uint32_t *__restrict__ tiles,
-                                                                    GRec *__restrict__ rec, uint32_t *__restrict__ ctl,
+                                                                    uint32_t *__restrict__ ctl,
                                                                     uint32_t *__restrict__ host_K) {
+    // the top digit (sign + exponent + 1 mantissa bit) takes a handful of values: its counters are
+    // replicated 16x (lane & 15 picks the copy) so a wave's LDS adds collide at most 4 ways
+    constexpr int kTopCopies = 16;
     __shared__ uint32_t s_hist[kPasses * kRadix];
+    __shared__ uint32_t s_top[kTopCopies][kRadix];
     __shared__ uint32_t s_wsum[kDsWaves];
-    __shared__ uint32_t s_v, s_prefix;
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    const int u = blockIdx.x, tpb = up_tpb(nb);
     DS_STAMP(0, 0);
     s_hist[t] = 0u;
-    if (t == 0) s_v = atomicAdd(&ctl[kCtlTicket], 1u);
+#pragma unroll
+    for (int k = 0; k < kTopCopies * kRadix / kDsThreads; k++) (&s_top[0][0])[t + k * kDsThreads] = 0u;
     __syncthreads();
-    const uint32_t v = s_v;
-    if (v >= (uint32_t)nb) return;  // control words not zeroed: never index past P
-    const size_t base = (size_t)v * kDsTile + (size_t)w * kDsItems * kWave;
-    uint32_t key[kDsItems], tl[kDsItems];
+    uint32_t run = 0;  // thread 0: tiles_touched of the workgroup's earlier tiles
+    const int v1 = min(nb, (u + 1) * tpb);
+    for (int v = u * tpb; v < v1; v++) {
+        const size_t base = (size_t)v * kDsTile + (size_t)w * kDsItems * kWave;
+        uint32_t key[kDsItems], tl[kDsItems];
 #pragma unroll
-    for (int k = 0; k < kDsItems; k++) {
-        const size_t e = base + (size_t)k * kWave + lane;
-        key[k] = e < (size_t)P ? keys[e] : 0u;
-        tl[k] = e < (size_t)P ? tiles[e] : 0u;
-    }
-    // digit histograms of all passes: one LDS add per (wave, distinct digit)
-#pragma unroll
-    for (int k = 0; k < kDsItems; k++) {
-        const size_t e = base + (size_t)k * kWave + lane;
-        const bool valid = e < (size_t)P;
-        const uint64_t vm = __ballot(valid);
-        if (vm == 0ull) break;
-#pragma unroll
-        for (int p = 0; p < kPasses; p++) {
-            const uint32_t d = (key[k] >> (8 * p)) & 0xFFu;
-            const uint64_t m = match8(d, vm);
-            if (valid && below(m) == 0u) atomicAdd(&s_hist[p * kRadix + d], (uint32_t)__popcll(m));
+        for (int k = 0; k < kDsItems; k++) {
+            const size_t e = base + (size_t)k * kWave + lane;
+            key[k] = e < (size_t)P ? keys[e] : 0u;
+            tl[k] = e < (size_t)P ? tiles[e] : 0u;
         }
-    }
-    // tiles_touched: exclusive offsets inside the wave's 512 keys (wave-major, item, lane order)
-    uint32_t off[kDsItems], run = 0;
+        uint32_t sum = 0;
 #pragma unroll
-    for (int k = 0; k < kDsItems; k++) {
-        const uint32_t incl = wave_incl_scan(tl[k], lane);
-        off[k] = run + incl - tl[k];
-        run += (uint32_t)__shfl((int)incl, 63, 64);
+        for (int k = 0; k < kDsItems; k++) {
+            const size_t e = base + (size_t)k * kWave + lane;
+            if (e < (size_t)P) {
+#pragma unroll
+                for (int p = 0; p < kPasses - 1; p++) atomicAdd(&s_hist[p * kRadix + ((key[k] >> (8 * p)) & 0xFFu)], 1u);
+                atomicAdd(&s_top[lane & (kTopCopies - 1)][key[k] >> 24], 1u);
+            }
+            sum += tl[k];
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) sum += (uint32_t)__shfl_xor((int)sum, o, 64);
+        if (lane == 0) s_wsum[w] = sum;
+        __syncthreads();
+        if (t == 0) {
+            ctl[ctl_bex(nb) + v] = run;
+#pragma unroll
+            for (int k = 0; k < kDsWaves; k++) run += s_wsum[k];
+        }
+        __syncthreads();
     }
-    if (lane == 0) s_wsum[w] = run;
-    __syncthreads();
     DS_STAMP(0, 1);
-    {
-        const uint32_t c = s_hist[t];
-        if (c) atomicAdd(&ctl[kCtlHist + t], c);
+    uint32_t hv = s_hist[t];
+    if (t >= (kPasses - 1) * kRadix) {
+#pragma unroll
+        for (int c = 0; c < kTopCopies; c++) hv += s_top[c][t - (kPasses - 1) * kRadix];
     }
-    if (w == 0) {
-        const uint32_t x = lane < kDsWaves ? s_wsum[lane] : 0u;
-        const uint32_t incl = wave_incl_scan(x, lane);
-        if (lane < kDsWaves) s_wsum[lane] = incl - x;
-        const uint32_t total = (uint32_t)__shfl((int)incl, 63, 64);
-        if (lane == 0) {
-            // chained scan over tiles: publish the aggregate, walk back to an inclusive prefix
-            uint64_t *st = reinterpret_cast<uint64_t *>(ctl + kCtlScan);
-            uint32_t prefix = 0;
-            if (v == 0) {
-                st_agent64(&st[0], (2ull << 32) | total);
-            } else {
-                st_agent64(&st[v], (1ull << 32) | total);
-                int spins = 0;
-                for (int j = (int)v - 1; j >= 0;) {
-                    const uint64_t s = ld_agent64(&st[j]);
-                    const uint32_t f = (uint32_t)(s >> 32);
-                    if (f == 0u) {
-                        if (++spins > kSpinLimit) {
-                            ctl[kCtlErr] = 1u;
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(1);
-                        continue;
-                    }
-                    prefix += (uint32_t)s;
-                    if (f == 2u) break;
-                    j--;
-                }
-                st_agent64(&st[v], (2ull << 32) | (uint64_t)(prefix + total));
-            }
-            s_prefix = prefix;
-            if (v == (uint32_t)nb - 1u) {
-                ctl[kCtlK] = prefix + total;
-                if (host_K) __hip_atomic_store(host_K, prefix + total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
+    ctl[ctl_blkhist(nb) + (size_t)u * kPasses * kRadix + t] = hv;
+    if (t == 0) {
+        ctl[ctl_btot(nb) + u] = run;
+        __hip_atomic_fetch_add(&ctl[kCtlK], run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t done = __hip_atomic_fetch_add(&ctl[kCtlDone], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (done == (uint32_t)gridDim.x - 1u && host_K) {
+            const uint32_t K = ld_agent(&ctl[kCtlK]);
+            __hip_atomic_store(host_K, K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
-    __syncthreads();
     DS_STAMP(0, 2);
-    const uint32_t pre = s_prefix + s_wsum[w];
-#pragma unroll
-    for (int k = 0; k < kDsItems; k++) {
-        const size_t e = base + (size_t)k * kWave + lane;
-        if (e < (size_t)P && tl[k] > 0u) rec[e].off = pre + off[k];
-    }
-    DS_STAMP(0, 3);
 }
 
 template <int kPass>
@@ -225,55 +214,115 @@ __global__ __launch_bounds__(kDsThreads) void dsort_pass_kernel(int P, int nb, c
                                                                  uint32_t *__restrict__ kout,
                                                                  const uint32_t *__restrict__ vin,
                                                                  uint32_t *__restrict__ vout, uint32_t *__restrict__ ctl,
-                                                                 const GRec *__restrict__ rec,
+                                                                 uint32_t *__restrict__ offsets,
                                                                  const uint32_t *__restrict__ tiles,
-                                                                 uint2 *__restrict__ drect, uint32_t *__restrict__ dtiles) {
-    constexpr bool kLast = kPass == kPasses - 1;
+                                                                 const uint2 *__restrict__ rect8,
+                                                                 uint2 *__restrict__ drect) {
+    constexpr bool kFirst = kPass == 0, kLast = kPass == kPasses - 1;
     constexpr int kShift = 8 * kPass;
     __shared__ uint32_t s_key[kDsTile];
     __shared__ uint32_t s_val[kDsTile];
     __shared__ uint32_t s_wh[kDsWaves][kRadix];  // per-wave digit counts -> exclusive prefix over waves
-    __shared__ uint32_t s_gb[kRadix];            // global digit base
+    __shared__ uint32_t s_gb[4][kRadix];         // global digit base (4 partial sums, then [0] scanned)
     __shared__ uint32_t s_bex[kRadix];           // tile-local digit base
     __shared__ uint32_t s_dst[kRadix];           // global slot of tile-local position 0 of each digit
-    __shared__ uint32_t s_v;
+    __shared__ uint32_t s_wsum[kDsWaves];
+    __shared__ uint32_t s_v, s_pre;
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     DS_STAMP(1 + kPass, 0);
 #pragma unroll
     for (int k = 0; k < kDsWaves * kRadix / kDsThreads; k++) (&s_wh[0][0])[t + k * kDsThreads] = 0u;
-    if (t < kRadix) s_gb[t] = ctl[kCtlHist + kPass * kRadix + t];
-    if (t == 0) s_v = atomicAdd(&ctl[kCtlTicket + 1 + kPass], 1u);
-    __syncthreads();
-    const uint32_t v = s_v;
+    // Tile numbering: up to kMaxResident tiles every workgroup can be resident at once (one per CU;
+    // nothing else this build runs holds a CU indefinitely), so a tile waiting on lower-numbered
+    // ones can always be overtaken and blockIdx.x is the tile; above that, tiles are numbered in
+    // start order by a ticket, so a tile only ever waits on tiles that are already running.
+    // The histogram-row loads are issued first and summed after the ranking.
+    const int nbu = up_blocks(nb);
+    uint32_t h[kUpMax / 4];
+    {
+        const uint32_t *bh = ctl + ctl_blkhist(nb) + kPass * kRadix + (t & (kRadix - 1));
+#pragma unroll
+        for (int q = 0; q < kUpMax / 4; q++) {
+            const int j = (t >> 8) + 4 * q;
+            h[q] = j < nbu ? bh[(size_t)j * kPasses * kRadix] : 0u;
+        }
+    }
+    uint32_t v = blockIdx.x;
+    if (nb > kMaxResident) {
+        if (t == 0) s_v = atomicAdd(&ctl[kCtlTicket + kPass], 1u);
+        __syncthreads();
+        v = s_v;
+    } else {
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // s_wh zeroed: LDS only (the row loads stay in flight)
+        __builtin_amdgcn_s_barrier();
+    }
     if (v >= (uint32_t)nb) return;  // control words not zeroed: never index past P
+    DS_STAMP(1 + kPass, 5);
+    const int wbase = w * kDsItems * kWave;
     const size_t tile0 = (size_t)v * kDsTile;
     const int n = (int)min((size_t)kDsTile, (size_t)P - tile0);
-    const int wbase = w * kDsItems * kWave;
-    uint32_t key[kDsItems], val[kDsItems];
+    uint32_t key[kDsItems], val[kDsItems], tl[kDsItems];
 #pragma unroll
     for (int k = 0; k < kDsItems; k++) {
         const int i = wbase + k * kWave + lane;
         const bool valid = i < n;
         key[k] = valid ? kin[tile0 + i] : 0xFFFFFFFFu;
-        val[k] = kPass == 0 ? (uint32_t)(tile0 + i) : (valid ? vin[tile0 + i] : 0u);
+        val[k] = kFirst ? (uint32_t)(tile0 + i) : (valid ? vin[tile0 + i] : 0u);
+        tl[k] = (kFirst && valid) ? tiles[tile0 + i] : 0u;
     }
-    if (w == 0) (void)scan256_wave(s_gb, lane);
-    // ranks: within the wave, equal digits in (item, lane) order
+    DS_STAMP_AFTER(1 + kPass, 6, key[kDsItems - 1] + val[kDsItems - 1]);
+    uint32_t toff[kDsItems];
+    if (kFirst) {
+        // record offsets: the totals of the earlier upsweep workgroups + this tile's offset inside
+        // its workgroup, then the in-tile order
+        if (w == 0) {
+            const int u = (int)v / up_tpb(nb);
+            uint32_t c = 0;
+#pragma unroll
+            for (int q = 0; q < kUpMax / kWave; q++) c += lane + q * kWave < u ? ctl[ctl_btot(nb) + lane + q * kWave] : 0u;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o, 64);
+            if (lane == 0) s_pre = c + ctl[ctl_bex(nb) + v];
+        }
+        uint32_t run = 0;
+#pragma unroll
+        for (int k = 0; k < kDsItems; k++) {
+            const uint32_t incl = wave_incl_scan(tl[k], lane);
+            toff[k] = run + incl - tl[k];  // exclusive offset inside the wave's 512 keys
+            run += (uint32_t)__shfl((int)incl, 63, 64);
+        }
+        if (lane == 0) s_wsum[w] = run;
+    }
+    // ranks: within the wave, equal digits in (item, lane) order (8 ballots per key)
     uint32_t rk[kDsItems];
 #pragma unroll
     for (int k = 0; k < kDsItems; k++) {
-        const int i = wbase + k * kWave + lane;
-        const bool valid = i < n;
-        const uint64_t vm = __ballot(valid);
+        const bool valid = wbase + k * kWave + lane < n;
         const uint32_t d = (key[k] >> kShift) & 0xFFu;
-        const uint64_t m = match8(d, vm);
+        const uint64_t m = match8(d, __ballot(valid));
         const uint32_t b = below(m);
         const uint32_t old = s_wh[w][d];
         if (valid && b == 0u) s_wh[w][d] = old + (uint32_t)__popcll(m);
         rk[k] = old + b;
     }
+    {
+        // global digit base: column kPass of the upsweep's histogram rows, 4 strided partial sums
+        uint32_t c = 0;
+#pragma unroll
+        for (int q = 0; q < kUpMax / 4; q++) c += h[q];
+        s_gb[t >> 8][t & (kRadix - 1)] = c;
+    }
     __syncthreads();
     DS_STAMP(1 + kPass, 1);
+    if (kFirst) {
+        uint32_t pre = s_pre;
+        for (int k = 0; k < w; k++) pre += s_wsum[k];
+#pragma unroll
+        for (int k = 0; k < kDsItems; k++) {
+            const int i = wbase + k * kWave + lane;
+            if (i < n) offsets[tile0 + i] = pre + toff[k];
+        }
+    }
     uint32_t cnt = 0;
     if (t < kRadix) {
 #pragma unroll
@@ -282,12 +331,14 @@ __global__ __launch_bounds__(kDsThreads) void dsort_pass_kernel(int P, int nb, c
             s_wh[ww][t] = cnt;
             cnt += c;
         }
-        uint32_t *st = ctl + ctl_pass(nb, kPass);
+        uint32_t *st = ctl + ctl_status(nb, kPass);
         st_agent(&st[(size_t)v * kRadix + t], (v == 0 ? kFlagInc : kFlagAgg) | cnt);
         s_bex[t] = cnt;
+        s_gb[0][t] += s_gb[1][t] + s_gb[2][t] + s_gb[3][t];
     }
     __syncthreads();
     if (w == 0) (void)scan256_wave(s_bex, lane);
+    if (w == 1) (void)scan256_wave(s_gb[0], lane);
     __syncthreads();
     DS_STAMP(1 + kPass, 2);
     // the tile in digit order, through LDS
@@ -301,29 +352,42 @@ __global__ __launch_bounds__(kDsThreads) void dsort_pass_kernel(int P, int nb, c
             s_val[lp] = val[k];
         }
     }
+    DS_STAMP(1 + kPass, 7);
     if (t < kRadix) {
-        // decoupled lookback for digit t over the preceding tiles
-        uint32_t *st = ctl + ctl_pass(nb, kPass);
+        // decoupled lookback for digit t over the preceding tiles, kLookWin status words per round
+        // trip: add words from the nearest predecessor back until an inclusive one; a word not yet
+        // published ends the round (re-polled next round)
+        const uint32_t *st = ctl + ctl_status(nb, kPass);
         uint32_t excl = 0;
-        if (v > 0) {
-            int spins = 0;
-            for (int j = (int)v - 1; j >= 0;) {
-                const uint32_t s = ld_agent(&st[(size_t)j * kRadix + t]);
-                if ((s & ~kCountMask) == 0u) {
-                    if (++spins > kSpinLimit) {
-                        ctl[kCtlErr] = 1u;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
+        int spins = 0;
+        for (int j = (int)v - 1; j >= 0;) {
+            uint32_t s[kLookWin];
+#pragma unroll
+            for (int q = 0; q < kLookWin; q++)
+                s[q] = j - q >= 0 ? ld_agent(&st[(size_t)(j - q) * kRadix + t]) : kFlagInc;  // past tile 0: +0, stop
+            int q = 0;
+            bool inc = false;
+#pragma unroll
+            for (int qq = 0; qq < kLookWin; qq++) {
+                const uint32_t f = s[qq] & ~kCountMask;
+                if (q == qq && f != 0u && !inc) {
+                    excl += s[qq] & kCountMask;
+                    inc = f == kFlagInc;
+                    q = qq + 1;
                 }
-                excl += s & kCountMask;
-                if ((s & ~kCountMask) == kFlagInc) break;
-                j--;
             }
-            st_agent(&st[(size_t)v * kRadix + t], kFlagInc | (excl + cnt));
+            if (inc) break;
+            j -= q;
+            if (q < kLookWin) {
+                if (++spins > kSpinLimit) {
+                    ctl[kCtlErr] = 1u;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
         }
-        s_dst[t] = s_gb[t] + excl - s_bex[t];
+        if (v > 0) st_agent(&ctl[ctl_status(nb, kPass) + (size_t)v * kRadix + t], kFlagInc | (excl + cnt));
+        s_dst[t] = s_gb[0][t] + excl - s_bex[t];
     }
     __syncthreads();
     DS_STAMP(1 + kPass, 3);
@@ -333,15 +397,7 @@ __global__ __launch_bounds__(kDsThreads) void dsort_pass_kernel(int P, int nb, c
         const uint32_t g = s_val[i];
         if (kLast) {
             vout[j] = g;
-            const uint32_t area = tiles[g];
-            uint2 r = make_uint2(0u, 0u);
-            if (area > 0) {
-                const uint4 q3 = reinterpret_cast<const uint4 *>(rec + g)[3];
-                const uint32_t wd = q3.y, x0 = q3.x & 0xFFFFu, y0 = q3.x >> 16;
-                r = make_uint2(q3.x, (x0 + wd) | ((y0 + area / wd) << 16));
-            }
-            drect[j] = r;
-            dtiles[j] = area;
+            drect[j] = rect8[g];
         } else {
             kout[j] = k;
             vout[j] = g;
@@ -354,26 +410,24 @@ __global__ __launch_bounds__(kDsThreads) void dsort_pass_kernel(int P, int nb, c
 
 int dsort_blocks(int P) { return (P + kDsTile - 1) / kDsTile; }
 
-size_t dsort_ctrl_words(int P) {
-    const int nb = dsort_blocks(P) > 0 ? dsort_blocks(P) : 1;
-    return ctl_pass(nb, kPasses);
-}
+size_t dsort_ctrl_words(int P) { return ctl_words(dsort_blocks(P) > 0 ? dsort_blocks(P) : 1); }
+size_t dsort_ctrl_zero_words(int P) { return ctl_zero_words(dsort_blocks(P) > 0 ? dsort_blocks(P) : 1); }
 
 void launch_depth_sort(int P, const GeomState &gs, uint32_t *host_K, hipStream_t s, hipEvent_t k_ready) {
     if (P == 0) return;
     const int nb = dsort_blocks(P);
-    hipLaunchKernelGGL(dsort_upsweep_kernel, dim3(nb), dim3(kDsThreads), 0, s, P, nb, gs.dkey, gs.tiles, gs.rec, gs.ctrl,
-                       host_K);
+    hipLaunchKernelGGL(dsort_upsweep_kernel, dim3(up_blocks(nb)), dim3(kDsThreads), 0, s, P, nb, gs.dkey, gs.tiles,
+                       gs.ctrl, host_K);
     if (k_ready) (void)hipEventRecord(k_ready, s);
     // keys: dkey -> dkey_sorted -> dkey -> dkey_sorted -> (none); values: (index) -> ids -> order -> ids -> order
     hipLaunchKernelGGL(dsort_pass_kernel<0>, dim3(nb), dim3(kDsThreads), 0, s, P, nb, gs.dkey, gs.dkey_sorted,
-                       (const uint32_t *)nullptr, gs.ids, gs.ctrl, gs.rec, gs.tiles, gs.drect, gs.dtiles);
+                       (const uint32_t *)nullptr, gs.ids, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect);
     hipLaunchKernelGGL(dsort_pass_kernel<1>, dim3(nb), dim3(kDsThreads), 0, s, P, nb, gs.dkey_sorted, gs.dkey, gs.ids,
-                       gs.order, gs.ctrl, gs.rec, gs.tiles, gs.drect, gs.dtiles);
+                       gs.order, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect);
     hipLaunchKernelGGL(dsort_pass_kernel<2>, dim3(nb), dim3(kDsThreads), 0, s, P, nb, gs.dkey, gs.dkey_sorted, gs.order,
-                       gs.ids, gs.ctrl, gs.rec, gs.tiles, gs.drect, gs.dtiles);
+                       gs.ids, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect);
     hipLaunchKernelGGL(dsort_pass_kernel<3>, dim3(nb), dim3(kDsThreads), 0, s, P, nb, gs.dkey_sorted,
-                       (uint32_t *)nullptr, gs.ids, gs.order, gs.ctrl, gs.rec, gs.tiles, gs.drect, gs.dtiles);
+                       (uint32_t *)nullptr, gs.ids, gs.order, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect);
 }
 
 uint32_t *dsort_K_word(const GeomState &gs) { return gs.ctrl + kCtlK; }

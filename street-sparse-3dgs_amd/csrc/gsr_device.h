@@ -349,14 +349,14 @@ __device__ __forceinline__ float gauss_p2(float adxdx_s, float bdx_s, float c_s,
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-// One 64-B render record per Gaussian (written by preprocess, off by duplicate): everything a
+// One 64-B render record per Gaussian (written by the preprocess): everything a
 // tile instance needs sits in one cache line, so the render kernels gather 1 line per instance.
 struct alignas(16) GRec {
     float x, y, ca, cb;       // q0: pixel-space mean, conic (a, b)
     float cc, op, ex, ey;     // q1: conic c, opacity, half-extents of the alpha >= 1/255 ellipse
                               //     (ex < 0: can never reach alpha >= 1/255)
     float r, g, b, invd;      // q2: colour, 1 / view depth
-    uint32_t rect0, rectw, dbits, off;  // q3: tile rect x0 | y0 << 16, width; depth bits; scan offset
+    uint32_t rect0, rectw, dbits, off;  // q3: tile rect x0 | y0 << 16, width; depth bits; (unused)
 };
 static_assert(sizeof(GRec) == 64, "GRec must be one 64-B line");
 
@@ -378,12 +378,13 @@ struct GeomState {          // per Gaussian, written by preprocess
     uint32_t *dkey_sorted;  // sort ping-pong buffer
     uint32_t *ids;          // sort ping-pong buffer (values)
     uint32_t *order;        // Gaussian ids in (depth, id) order
-    uint32_t *offsets;      // unused (kept: the scratch layout the tests decode)
+    uint32_t *offsets;      // exclusive scan of tiles_touched in Gaussian order: each Gaussian's first
+                            // backward record (dsort.hip pass 0)
     uint8_t *clamped;       // bit c set: SH channel c clamped at 0
-    uint32_t *ctrl;         // depth-sort control words (dsort.hip), zeroed by the preprocess
-    uint32_t ctrl_words;
+    uint32_t *ctrl;         // depth-sort control words (dsort.hip); the first ctrl_zero are zeroed by
+    uint32_t ctrl_zero;     // the preprocess
     uint2 *drect;           // per depth-order slot: tile rect (x0 | y0 << 16, x1 | y1 << 16), 0/0 = none
-    uint32_t *dtiles;       // per depth-order slot: tiles_touched (the scan input)
+    uint2 *rect8;           // per Gaussian (index order): the same rect, written by the preprocess
     SBGrid sb;              // level-1 binning counters: [nsb][nchunks] Gaussians / instances,
     uint32_t *sb_cnt_g;     // per-SB bases (nsb + 1 each)
     uint32_t *sb_cnt_i;

@@ -41,11 +41,12 @@ size_t sort_pairs_temp_bytes(size_t n, int end_bit);
 hipError_t sort_pairs(void *tmp, size_t tmp_bytes, const uint32_t *kin, uint32_t *kout, const uint32_t *vin,
                       uint32_t *vout, size_t n, int end_bit, hipStream_t s);
 // dsort.hip: the stable (depth bits, id) order of the P Gaussians (gs.order), depth-ordered tile
-// rects / counts (gs.drect, gs.dtiles), the Gaussian-major record offsets (rec.off) and
+// rects (gs.drect, from gs.rect8), the Gaussian-major record offsets (rec.off) and
 // K = sum of tiles_touched, stored to *dsort_K_word and, when host_K != NULL, to that pinned
 // host word; k_ready (optional) is recorded once K is final, before the sort passes run.
 int dsort_blocks(int P);
 size_t dsort_ctrl_words(int P);
+size_t dsort_ctrl_zero_words(int P);
 void launch_depth_sort(int P, const GeomState &gs, uint32_t *host_K, hipStream_t s, hipEvent_t k_ready);
 uint32_t *dsort_K_word(const GeomState &gs);
 uint32_t *dsort_err_word(const GeomState &gs);

@@ -17,13 +17,14 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
     int W, int H, float tanx, float tany, float fx, float fy, int gx, int gy, GeomState gs, int *__restrict__ radii) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     // the depth sort's control words (tickets, histograms, lookback status) start at zero
-    for (uint32_t c = (uint32_t)i; c < gs.ctrl_words; c += gridDim.x * blockDim.x) gs.ctrl[c] = 0u;
+    for (uint32_t c = (uint32_t)i; c < gs.ctrl_zero; c += gridDim.x * blockDim.x) gs.ctrl[c] = 0u;
     if (i >= P) return;
     const Mat4 V = load_mat4(viewmatrix);
     const Mat4 Pm = load_mat4(projmatrix);
     radii[i] = 0;
     gs.tiles[i] = 0;
     gs.dkey[i] = 0xFFFFFFFFu;  // culled Gaussians sort behind every visible one
+    gs.rect8[i] = make_uint2(0u, 0u);
     const float3 p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
     const float3 pv = xf_point43(p, V);
     if (pv.z <= 0.2f) return;  // in_frustum (prefiltered is treated as a plain cull)
@@ -119,6 +120,7 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
                        __uint_as_float(__float_as_uint(pv.z)), 0.f);
     if (!kSplitColor) gs.clamped[i] = clamp_bits;
     gs.tiles[i] = (uint32_t)area;
+    gs.rect8[i] = make_uint2((uint32_t)r.x0 | ((uint32_t)r.y0 << 16), (uint32_t)r.x1 | ((uint32_t)r.y1 << 16));
     gs.dkey[i] = __float_as_uint(pv.z);
 }
 

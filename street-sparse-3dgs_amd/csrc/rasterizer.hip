@@ -138,10 +138,10 @@ GeomState carve_geom(void *base, int P, int gx, int gy, size_t *bytes) {
     g.order = c.take<uint32_t>(P);
     g.offsets = c.take<uint32_t>(P);
     g.clamped = c.take<uint8_t>(P);
-    g.ctrl_words = (uint32_t)dsort_ctrl_words(P);
-    g.ctrl = c.take<uint32_t>(g.ctrl_words);
+    g.ctrl_zero = (uint32_t)dsort_ctrl_zero_words(P);
+    g.ctrl = c.take<uint32_t>(dsort_ctrl_words(P));
     g.drect = c.take<uint2>(P);
-    g.dtiles = c.take<uint32_t>(P);
+    g.rect8 = c.take<uint2>(P);
     g.sb = sb_grid(gx, gy, P);
     g.sb_cnt_g = c.take<uint32_t>((size_t)g.sb.nsb * g.sb.nchunks);
     g.sb_cnt_i = c.take<uint32_t>((size_t)g.sb.nsb * g.sb.nchunks);
@@ -313,7 +313,7 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
     }
     if ((rc = check("preprocess", debug, s))) return rc;
 #ifndef GSR_COLOR_FORK
-#define GSR_COLOR_FORK 0  // 0: beside the depth sort and the binning; 1: beside the binning only
+#define GSR_COLOR_FORK 1  // 0: beside the depth sort and the binning; 1: beside the binning only
 #endif
     auto fork_color = [&]() -> int {
         // fork: the SH colours stream in beside latency-bound main-stream stages; joined before render_fwd

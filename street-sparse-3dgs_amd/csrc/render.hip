@@ -348,7 +348,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
     const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list, int W, int H, int gx,
     const GRec *__restrict__ rec, const float *__restrict__ bg, const float *__restrict__ final_Ts,
     const uint32_t *__restrict__ n_contrib, const float *__restrict__ dL_dpix, const float *__restrict__ dL_dinvd,
-    const uint32_t *__restrict__ tile_order, uint64_t *__restrict__ boundary, float4 *__restrict__ out) {
+    const uint32_t *__restrict__ tile_order, const uint32_t *__restrict__ goff, uint64_t *__restrict__ boundary,
+    float4 *__restrict__ out) {
     __shared__ float4 s_a[kWave];
     __shared__ float4 s_b[kWave];  // conic.c, opacity, list position, sub-block mask
     __shared__ float4 s_c[kWave];
@@ -422,7 +423,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
             qb = R[1];
             qc = R[2];
             const uint4 q3 = reinterpret_cast<const uint4 *>(rec + g)[3];
-            u = q3.w + (uint32_t)((ty - (int)(q3.x >> 16)) * (int)q3.y + (tx - (int)(q3.x & 0xFFFFu)));
+            u = goff[g] + (uint32_t)((ty - (int)(q3.x >> 16)) * (int)q3.y + (tx - (int)(q3.x & 0xFFFFu)));
             m = sub_block_mask(qa, qb, tx0, ty0);
 #pragma unroll
             for (int k = 0; k < kPixPerLane; k++)
@@ -586,11 +587,11 @@ void launch_render_bwd(const Camera &cam, const GeomState &gs, const BinningStat
     if (dL_dinvdepth)
         hipLaunchKernelGGL(render_bwd_kernel<true>, dim3(T), dim3(kWave), 0, s, is.ranges, bs.point_list, cam.W,
                            cam.H, cam.gx, gs.rec, bg, is.final_T, is.n_contrib, dL_dpix, dL_dinvdepth, is.tile_order,
-                           is.boundary, sc.rec);
+                           gs.offsets, is.boundary, sc.rec);
     else
         hipLaunchKernelGGL(render_bwd_kernel<false>, dim3(T), dim3(kWave), 0, s, is.ranges, bs.point_list, cam.W,
                            cam.H, cam.gx, gs.rec, bg, is.final_T, is.n_contrib, dL_dpix, dL_dinvdepth, is.tile_order,
-                           is.boundary, sc.rec);
+                           gs.offsets, is.boundary, sc.rec);
 }
 
 }  // namespace gsr

@@ -103,9 +103,9 @@ def run_hip(s, c, dcol, dinv, colors_precomp=None, cov3D_precomp=None):
 
 
 def check_record_offsets(S, vis, K):
-    """rec.off (the backward's Gaussian-major record base): the visible Gaussians' ranges
-    [off, off + tiles_touched) partition [0, K) exactly."""
-    off = S["rec"][:, 15].view(np.uint32)[vis].astype(np.int64)
+    """The backward's Gaussian-major record bases (exclusive scan of tiles_touched in Gaussian
+    order): the visible Gaussians' ranges [off, off + tiles_touched) partition [0, K) exactly."""
+    off = S["offsets"][vis].astype(np.int64)
     n = S["tiles_touched"][vis].astype(np.int64)
     o = np.argsort(off, kind="stable")
     off, n = off[o], n[o]
@@ -326,6 +326,7 @@ def test_depth_order_large():
     rec = view(g, gl, "rec", np.float32, (c["P"], 16))
     tiles = view(g, gl, "tiles", np.uint32)
     order = view(g, gl, "order", np.uint32)
+    offsets = view(g, gl, "offsets", np.uint32)
     radii = raw[3].cpu().numpy()
     vis = (radii > 0) & (tiles > 0)
     nv = int(vis.sum())
@@ -335,7 +336,7 @@ def test_depth_order_large():
     dbits = rec[:, 14].view(np.uint32)
     np.testing.assert_array_equal(order[:nv], ids[np.lexsort((ids, dbits[ids]))])
     np.testing.assert_array_equal(np.sort(order[nv:]), np.nonzero(~vis)[0])
-    check_record_offsets(dict(rec=rec, tiles_touched=tiles), vis, K)
+    check_record_offsets(dict(offsets=offsets, tiles_touched=tiles), vis, K)
 
 
 @pytest.mark.gpu
