@@ -21,7 +21,9 @@ from collections import defaultdict
 STAGE_OF = [("render_bwd_kernel", "render_bwd"), ("render_fwd", "render_fwd"),
             ("preprocess_bwd_kernel", "preprocess_bwd"), ("record_sum_kernel", "record_sum"),
             ("preprocess_color_kernel", "sh_color"), ("preprocess_kernel", "preprocess"),
-            ("depth_gather_kernel", "depth_gather"),
+            ("depth_gather_kernel", "depth_gather"), ("dsort_upsweep", "depth_sort:upsweep"),
+            ("dsort_pass_kernel<0>", "depth_sort:pass0"), ("dsort_pass_kernel<1>", "depth_sort:pass1"),
+            ("dsort_pass_kernel<2>", "depth_sort:pass2"), ("dsort_pass_kernel<3>", "depth_sort:pass3"),
             ("sb_count_kernel", "bin_superblocks:count"), ("sb_colscan_kernel", "bin_superblocks:colscan"),
             ("sb_base_kernel", "bin_superblocks:base"), ("sb_scatter_kernel", "bin_superblocks:scatter"),
             ("tile_bin_kernel", "bin_tiles"), ("tile_order_kernel", "tile_order"), ("mark_visible", "mark_visible"),
