@@ -9,7 +9,10 @@
 
 namespace gsr {
 
-constexpr uint32_t kRedSerial = 32;
+#ifndef GSR_RED_SERIAL
+#define GSR_RED_SERIAL 32
+#endif
+constexpr uint32_t kRedSerial = GSR_RED_SERIAL;  // splats up to this many tiles: summed by their own lane
 #ifndef GSR_REC_BATCH
 #define GSR_REC_BATCH 4
 #endif

@@ -74,8 +74,10 @@ __global__ __launch_bounds__(1024) void sb_count_kernel(int P, SBGrid sg, const 
     }
 }
 
-// Exclusive scan of 256 values held one per thread; returns the exclusive prefix and the total.
+// Exclusive scan of NT values held one per thread; returns the exclusive prefix and the total.
+template <int NT>
 __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t *wsum, uint32_t &total) {
+    constexpr int kW = NT / 64;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t incl = v;
 #pragma unroll
@@ -87,52 +89,65 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t *w
     if (lane == 63) wsum[w] = incl;
     __syncthreads();
     uint32_t before = 0;
-    for (int k = 0; k < w; k++) before += wsum[k];
-    total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    total = 0;
+#pragma unroll
+    for (int k = 0; k < kW; k++) {
+        before += k < w ? wsum[k] : 0u;
+        total += wsum[k];
+    }
     return before + incl - v;
 }
 
-// Level 1, pass 2a: per SB, exclusive scan of the Gaussian counts over chunks (in place) and the
-// SB totals of Gaussians and instances.
-__global__ __launch_bounds__(256) void sb_colscan_kernel(SBGrid sg, uint32_t *__restrict__ cnt_g,
-                                                         const uint32_t *__restrict__ cnt_i,
-                                                         uint32_t *__restrict__ base_g, uint32_t *__restrict__ base_i) {
-    __shared__ uint32_t wsum[4];
+// Level 1, pass 2: per SB, exclusive scan of the Gaussian counts over chunks (in place) and the
+// SB totals of Gaussians and instances; the last workgroup to finish (a per-frame counter in the
+// depth sort's zeroed control words) turns the totals into exclusive SB bases, base[nsb] = the
+// total -- one launch instead of a column scan plus a single-workgroup base scan.
+constexpr int kColThreads = 256;
+__global__ __launch_bounds__(kColThreads) void sb_colscan_kernel(SBGrid sg, uint32_t *__restrict__ cnt_g,
+                                                                 const uint32_t *__restrict__ cnt_i,
+                                                                 uint32_t *__restrict__ base_g,
+                                                                 uint32_t *__restrict__ base_i,
+                                                                 uint32_t *__restrict__ done) {
+    __shared__ uint32_t wsum[kColThreads / 64];
+    __shared__ uint32_t s_last;
     const int s = blockIdx.x;
     uint32_t *row = cnt_g + (size_t)s * sg.nchunks;
     const uint32_t *rowi = cnt_i + (size_t)s * sg.nchunks;
     uint32_t carry = 0, isum = 0;
-    for (int b = 0; b < sg.nchunks; b += 256) {
+    for (int b = 0; b < sg.nchunks; b += kColThreads) {
         const int c = b + (int)threadIdx.x;
         const uint32_t v = c < sg.nchunks ? row[c] : 0u;
         isum += c < sg.nchunks ? rowi[c] : 0u;
         uint32_t tot;
-        const uint32_t ex = block_exclusive_scan(v, wsum, tot);
+        const uint32_t ex = block_exclusive_scan<kColThreads>(v, wsum, tot);
         if (c < sg.nchunks) row[c] = carry + ex;
         carry += tot;
     }
     uint32_t itot;
-    (void)block_exclusive_scan(isum, wsum, itot);
+    (void)block_exclusive_scan<kColThreads>(isum, wsum, itot);
     if (threadIdx.x == 0) {
-        base_g[s] = carry;
-        base_i[s] = itot;
+        // publish the totals write-through (sc1), drain, then count this workgroup in; the last
+        // one reads them back with sc1 loads (MI355X_MICROARCH.md hand-off rules: no L2 fences)
+        __hip_atomic_store(&base_g[s], carry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&base_i[s], itot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = prev == gridDim.x - 1u;
     }
-}
-
-// Level 1, pass 2b: exclusive scans of the SB totals (one workgroup); base[nsb] = the total.
-__global__ __launch_bounds__(256) void sb_base_kernel(int nsb, uint32_t *__restrict__ base_g,
-                                                      uint32_t *__restrict__ base_i) {
-    __shared__ uint32_t wsum[4];
+    __syncthreads();
+    if (!s_last) return;
+    const int nsb = sg.nsb;
     uint32_t cg = 0, ci = 0;
-    for (int b = 0; b < nsb; b += 256) {
-        const int s = b + (int)threadIdx.x;
-        const uint32_t vg = s < nsb ? base_g[s] : 0u, vi = s < nsb ? base_i[s] : 0u;
+    for (int b = 0; b < nsb; b += kColThreads) {
+        const int k = b + (int)threadIdx.x;
+        const uint32_t vg = k < nsb ? __hip_atomic_load(&base_g[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        const uint32_t vi = k < nsb ? __hip_atomic_load(&base_i[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
         uint32_t tg, ti;
-        const uint32_t eg = block_exclusive_scan(vg, wsum, tg);
-        const uint32_t ei = block_exclusive_scan(vi, wsum, ti);
-        if (s < nsb) {
-            base_g[s] = cg + eg;
-            base_i[s] = ci + ei;
+        const uint32_t eg = block_exclusive_scan<kColThreads>(vg, wsum, tg);
+        const uint32_t ei = block_exclusive_scan<kColThreads>(vi, wsum, ti);
+        if (k < nsb) {
+            base_g[k] = cg + eg;
+            base_i[k] = ci + ei;
         }
         cg += tg;
         ci += ti;
@@ -429,9 +444,8 @@ void launch_binning_superblocks(int P, const Camera &cam, const GeomState &gs, c
     const size_t l3 = sizeof(uint32_t) * 3 * kScatterWaves * (size_t)sg.nsb;
     hipLaunchKernelGGL(sb_count_kernel, dim3(sg.nchunks), dim3(1024), l1, s, P, sg, gs.drect, gs.sb_cnt_g,
                        gs.sb_cnt_i);
-    hipLaunchKernelGGL(sb_colscan_kernel, dim3(sg.nsb), dim3(256), 0, s, sg, gs.sb_cnt_g, gs.sb_cnt_i, gs.sb_base_g,
-                       gs.sb_base_i);
-    hipLaunchKernelGGL(sb_base_kernel, dim3(1), dim3(256), 0, s, sg.nsb, gs.sb_base_g, gs.sb_base_i);
+    hipLaunchKernelGGL(sb_colscan_kernel, dim3(sg.nsb), dim3(kColThreads), 0, s, sg, gs.sb_cnt_g, gs.sb_cnt_i,
+                       gs.sb_base_g, gs.sb_base_i, dsort_aux_word(gs));
     hipLaunchKernelGGL(sb_scatter_kernel, dim3(sg.nchunks), dim3(64 * kScatterWaves), l3, s, P, sg, gs.order, gs.drect,
                        gs.sb_cnt_g, gs.sb_base_g, bs.sblist);
 }

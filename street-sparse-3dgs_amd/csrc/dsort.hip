@@ -48,6 +48,7 @@ constexpr int kCtlTicket = 0;  // [p] pass p
 constexpr int kCtlDone = 4;    // upsweep tiles finished
 constexpr int kCtlK = 5;       // sum of tiles_touched
 constexpr int kCtlErr = 6;     // set when a bounded spin gave up (never expected)
+constexpr int kCtlAux = 7;     // per-frame counter lent to the binning (sb_colscan's last-workgroup count)
 constexpr int kCtlHead = 8;
 // The upsweep runs at most kUpMax workgroups, each over tpb consecutive tiles, so that a pass
 // reduces at most kUpMax histogram rows (kUpMax / 4 loads per thread, all in flight at once).
@@ -432,5 +433,6 @@ void launch_depth_sort(int P, const GeomState &gs, uint32_t *host_K, hipStream_t
 
 uint32_t *dsort_K_word(const GeomState &gs) { return gs.ctrl + kCtlK; }
 uint32_t *dsort_err_word(const GeomState &gs) { return gs.ctrl + kCtlErr; }
+uint32_t *dsort_aux_word(const GeomState &gs) { return gs.ctrl + kCtlAux; }
 
 }  // namespace gsr

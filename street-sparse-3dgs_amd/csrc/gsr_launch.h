@@ -50,6 +50,8 @@ size_t dsort_ctrl_zero_words(int P);
 void launch_depth_sort(int P, const GeomState &gs, uint32_t *host_K, hipStream_t s, hipEvent_t k_ready);
 uint32_t *dsort_K_word(const GeomState &gs);
 uint32_t *dsort_err_word(const GeomState &gs);
+// a zeroed-per-frame control word the binning uses as a completion counter
+uint32_t *dsort_aux_word(const GeomState &gs);
 // binning.hip: per-tile lists from the depth-ordered Gaussians (two stable counting levels).
 SBGrid sb_grid(int gx, int gy, int P);
 bool sb_grid_supported(const SBGrid &g);

@@ -343,6 +343,9 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
 #ifndef GSR_BWD_FACTORED
 #define GSR_BWD_FACTORED 1
 #endif
+#ifndef GSR_BWD_ALWAYS_REDUCE
+#define GSR_BWD_ALWAYS_REDUCE 0
+#endif
 template <bool kDepth>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVES_PER_EU))) void render_bwd_kernel(
     const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list, int W, int H, int gx,
@@ -537,7 +540,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
 #endif
             // Half-wave sums only (5 DPP stages); lanes 16 and 48 park the two partials in LDS
             // and they are added once per batch below instead of per instance.
+#if GSR_BWD_ALWAYS_REDUCE
+            (void)any;
+            wave_halfsum<kDepth ? 10 : 9>(q);
+#else
             if (__any(any)) wave_halfsum<kDepth ? 10 : 9>(q);
+#endif
             if ((lane & 31) == 16) {
                 float2 *d = s_red + (j * 2 + (lane >> 5)) * 5;
 #pragma unroll
