@@ -346,6 +346,9 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
 #ifndef GSR_BWD_ALWAYS_REDUCE
 #define GSR_BWD_ALWAYS_REDUCE 0
 #endif
+#ifndef GSR_BWD_PREFETCH
+#define GSR_BWD_PREFETCH 0
+#endif
 template <bool kDepth>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVES_PER_EU))) void render_bwd_kernel(
     const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list, int W, int H, int gx,
@@ -353,11 +356,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
     const uint32_t *__restrict__ n_contrib, const float *__restrict__ dL_dpix, const float *__restrict__ dL_dinvd,
     const uint32_t *__restrict__ tile_order, const uint32_t *__restrict__ goff, uint64_t *__restrict__ boundary,
     float4 *__restrict__ out) {
+    // 8 KiB of LDS per wave (5 waves per SIMD fit): the scaled conic is formed per instance from
+    // s_a / s_b, and the record index rides in s_b.w next to (list position << 4 | sub-block mask)
     __shared__ float4 s_a[kWave];
-    __shared__ float4 s_b[kWave];  // conic.c, opacity, list position, sub-block mask
+    __shared__ float4 s_b[kWave];  // conic.c, opacity, list position << 4 | sub-block mask, record index
     __shared__ float4 s_c[kWave];
-    __shared__ float4 s_d[kWave];  // scaled conic (gauss_p2); s_a / s_b keep the conic for the finalisation
-    __shared__ uint32_t s_u[kWave];
     __shared__ float2 s_red[kWave * 2 * 5];  // per instance, per half wave: 10 partial sums
 
     // Tiles run heaviest first (longest-processing-time order from the forward's per-tile work):
@@ -444,19 +447,32 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
         if (m) {
             const uint32_t slot = lane_prefix(keep);
             s_a[slot] = qa;
-            s_b[slot] = make_float4(qb.x, qb.y, __uint_as_float(pos), __uint_as_float(m));
+            s_b[slot] = make_float4(qb.x, qb.y, __uint_as_float(pos << 4 | m), __uint_as_float(u));
             s_c[slot] = qc;
-            s_d[slot] = make_float4(qa.z * kHalfLog2e, qa.w * kLog2e, qb.x * kHalfLog2e, 0.f);
-            s_u[slot] = u;
         }
         __syncthreads();
+#if GSR_BWD_PREFETCH
+        // the next instance's LDS rows are read one iteration ahead (their latency overlaps the
+        // current instance's pixel work and reduction)
+        float4 na = s_a[0], nb = s_b[0], nc = s_c[0];
+#endif
         for (uint32_t j = 0; j < cnt; j++) {
+#if GSR_BWD_PREFETCH
+            const float4 a = na, b = nb, c = nc;
+            if (j + 1 < cnt) {
+                na = s_a[j + 1];
+                nb = s_b[j + 1];
+                nc = s_c[j + 1];
+            }
+#else
             const float4 a = s_a[j];
             const float4 b = s_b[j];
             const float4 c = s_c[j];
-            const float4 cs = s_d[j];
-            const uint32_t mk = __builtin_amdgcn_readfirstlane(__float_as_uint(b.w));
-            const uint32_t jpos = __builtin_amdgcn_readfirstlane(__float_as_uint(b.z));
+#endif
+            const float4 cs = make_float4(a.z * kHalfLog2e, a.w * kLog2e, b.x * kHalfLog2e, 0.f);  // gauss_p2
+            const uint32_t pm = __builtin_amdgcn_readfirstlane(__float_as_uint(b.z));
+            const uint32_t mk = pm & 0xFu;
+            const uint32_t jpos = pm >> 4;
             const float dx = a.x - pfx;
             const float adxdx_s = cs.x * dx * dx;
             const float bdx_s = cs.y * dx;
@@ -562,7 +578,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
                 r[2 * t] = p0.x + p1.x;
                 r[2 * t + 1] = p0.y + p1.y;
             }
-            const size_t o = 4 * (size_t)s_u[lane];
+            const size_t o = 4 * (size_t)__float_as_uint(s_b[lane].w);
 #if GSR_BWD_FACTORED
             {
                 // moments -> (dmean2D, dconic): dL/dG = opacity dL/dalpha, dG/d(dx) = -G (a dx + b dy), ...
