@@ -16,6 +16,7 @@
 // nonzero().  Here one launch walks all six groups' (param, grad, m, v) arrays once, testing
 // relevance (opacity grad != 0) per row on the device.
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <algorithm>
 #include <string>
@@ -379,6 +380,207 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_grad_kernel(const float 
     }
 }
 
+// Streaming form of l1_ssim_grad_kernel: a block owns a 64-column x kSegH-row strip of one plane
+// and walks it top to bottom kStep rows at a time.  Each step stages kStep input rows, and each
+// stage of the separable pipeline (horizontal moments -> vertical moments and dS/d(moment) ->
+// horizontal pass of a/b/c -> vertical pass to G) advances by kStep rows, the vertical passes
+// reading kRing-deep LDS rings.  Only the 2R-column side halo is recomputed (plus 4R rows per
+// strip instead of per 16-row tile), LDS is 43 KiB instead of 79 KiB, and the next step's input
+// rows are in flight while the current step computes.  Every value is formed with the same fmaf
+// order as l1_ssim_grad_kernel, so G and dx are bit-identical to it.
+constexpr int kStW = 64;
+#ifndef GSR_SSIM_SEG_H
+#define GSR_SSIM_SEG_H 64
+#endif
+constexpr int kSegH = GSR_SSIM_SEG_H;
+constexpr int kStep = 4;
+constexpr int kRing = 16;
+constexpr int kStIC = kStW + 4 * kR, kStMC = kStW + 2 * kR;  // 84 input, 74 SSIM-map columns
+constexpr int kStIP = odd_pitch(kStIC), kStMP = odd_pitch(kStMC), kStTP = odd_pitch(kStW);
+constexpr int kStInElems = kStep * kStIC;
+constexpr int kStInPer = (kStInElems + kLossThreads - 1) / kLossThreads;
+constexpr int kStHSeg = kStMC / 2;  // horizontal-moment tasks per row (two columns each)
+static_assert(kStMC % 2 == 0 && kStep * kStHSeg <= kLossThreads, "one horizontal-moment task per thread");
+static_assert(kStep * 64 == kLossThreads && kStep % 2 == 0 && 2 * kStMC <= kLossThreads, "one task per thread");
+static_assert(kRing >= 2 * kR + 1 + kStep - 1 && (kRing & (kRing - 1)) == 0, "ring holds a step's window rows");
+
+// Workgroup barrier for LDS hand-offs only: drains this wave's LDS operations but not its global
+// loads (__syncthreads waits for vmcnt(0) too), so the next step's rows stay in flight.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <bool kMap>
+__global__ __launch_bounds__(kLossThreads) void l1_ssim_stream_kernel(const float *__restrict__ x,
+                                                                       const float *__restrict__ y, int H, int W,
+                                                                       Window win, const float *__restrict__ dout,
+                                                                       float inv_n, float *__restrict__ dx,
+                                                                       float2 *__restrict__ partials) {
+    __shared__ float s_in[2][kStep][kStIP];
+    __shared__ float s_hm[5][kRing][kStMP];
+    __shared__ float s_abc[3][kStep][kStMP];
+    __shared__ float s_h3[3][kRing][kStTP];
+    __shared__ float s_red[8];
+    const size_t plane_off = (size_t)blockIdx.z * H * W;
+    x += plane_off;
+    y += plane_off;
+    dx += plane_off;
+    const int tid = threadIdx.x;
+    const int cx = blockIdx.x * kStW, r0 = blockIdx.y * kSegH, r1 = min(r0 + kSegH, H);
+    const float g_l1 = kMap ? 0.f : dout[0] * inv_n, g_ssim = kMap ? 0.f : dout[1] * inv_n;
+    const int nsteps = (r1 - r0 + 4 * kR + kStep - 1) / kStep;
+    float l1 = 0.f, ss = 0.f;
+
+    // Loads are unconditional (clamped coordinates) and the zero padding is applied when the
+    // values are staged: no branch around a load, so the compiler does not drain the loads early.
+    float px[kStInPer], py[kStInPer];
+    bool pin[kStInPer];
+    const auto fetch = [&](int p0) {
+#pragma unroll
+        for (int k = 0; k < kStInPer; k++) {
+            const int e = min(tid + k * kLossThreads, kStInElems - 1);
+            const int r = e / kStIC, c = e - r * kStIC;
+            const int gy = p0 + r, gx = cx - 2 * kR + c;
+            pin[k] = gy >= 0 && gy < H && gx >= 0 && gx < W;
+            const size_t o = (size_t)min(max(gy, 0), H - 1) * W + min(max(gx, 0), W - 1);
+            px[k] = x[o];
+            py[k] = y[o];
+        }
+    };
+    fetch(r0 - 2 * kR);
+
+    for (int st = 0; st < nsteps; st++) {
+        const int p0 = r0 - 2 * kR + kStep * st;  // first input row of this step
+        // (1) stage input rows p0 .. p0 + kStep - 1 and start loading the next step's
+#pragma unroll
+        for (int k = 0; k < kStInPer; k++) {
+            const int e = tid + k * kLossThreads;
+            if (e < kStInElems) {
+                const int r = e / kStIC, c = e - r * kStIC;
+                s_in[0][r][c] = pin[k] ? px[k] : 0.f;
+                s_in[1][r][c] = pin[k] ? py[k] : 0.f;
+            }
+        }
+        const int orow = p0 + (tid >> 6) - 2 * kR, ocol = cx + (tid & 63);  // (5)'s output pixel
+        const bool o_ok = orow >= r0 && orow < r1 && ocol < W;
+        const size_t oo = (size_t)min(max(orow, 0), H - 1) * W + min(ocol, W - 1);
+        const float xv = x[oo], yv = y[oo];
+        fetch(p0 + kStep);  // unconditional (clamped): a branch here would make every wait a full drain
+        lds_barrier();
+
+        // (2) horizontal moments of the staged rows at the 74 map columns, two per task
+        if (tid < kStep * kStHSeg) {
+            const int r = tid / kStHSeg, c0 = 2 * (tid - r * kStHSeg);
+            float u[2 + 2 * kR], v[2 + 2 * kR];
+#pragma unroll
+            for (int k = 0; k < 2 + 2 * kR; k++) {
+                u[k] = s_in[0][r][c0 + k];
+                v[k] = s_in[1][r][c0 + k];
+            }
+            const int ring = (p0 + r) & (kRing - 1);
+#pragma unroll
+            for (int o = 0; o < 2; o++) {
+                float m1 = 0.f, m2 = 0.f, a11 = 0.f, a22 = 0.f, a12 = 0.f;
+#pragma unroll
+                for (int j = 0; j < 2 * kR + 1; j++) {
+                    const float w = win.w[j];
+                    m1 = fmaf(w, u[o + j], m1);
+                    m2 = fmaf(w, v[o + j], m2);
+                    a11 = fmaf(w, u[o + j] * u[o + j], a11);
+                    a22 = fmaf(w, v[o + j] * v[o + j], a22);
+                    a12 = fmaf(w, u[o + j] * v[o + j], a12);
+                }
+                s_hm[0][ring][c0 + o] = m1;
+                s_hm[1][ring][c0 + o] = m2;
+                s_hm[2][ring][c0 + o] = a11;
+                s_hm[3][ring][c0 + o] = a22;
+                s_hm[4][ring][c0 + o] = a12;
+            }
+        }
+        lds_barrier();
+
+        // (3) vertical moments and dS/d(moment) at map rows p0 - R .. p0 + kStep - 1 - R, two rows
+        // per task.  Rows above r0 - R read ring rows never written; (5) never reads them.
+        if (tid < 2 * kStMC) {
+            const int pr = tid / kStMC, c = tid - pr * kStMC;
+            const int qa = p0 + 2 * pr - kR;
+            float m[5][2];
+#pragma unroll
+            for (int q = 0; q < 5; q++) {
+                m[q][0] = m[q][1] = 0.f;
+#pragma unroll
+                for (int t = 0; t < 2 * kR + 2; t++) {
+                    const float v = s_hm[q][(qa - kR + t) & (kRing - 1)][c];
+#pragma unroll
+                    for (int o = 0; o < 2; o++) {
+                        const int j = t - o;
+                        if (j >= 0 && j <= 2 * kR) m[q][o] = fmaf(win.w[j], v, m[q][o]);
+                    }
+                }
+            }
+            const int gx = cx - kR + c;
+            const bool col_in = gx >= 0 && gx < W;
+#pragma unroll
+            for (int o = 0; o < 2; o++) {
+                const int q = qa + o;
+                const Moments mo{m[0][o], m[1][o], m[2][o], m[3][o], m[4][o]};
+                float a, b, cc;
+                ssim_partials(mo, a, b, cc);
+                const bool in = col_in && q >= 0 && q < H;
+                if (kMap && in && q >= r0 && q < r1 && c >= kR && c < kR + kStW) ss += ssim_value(mo);
+                s_abc[0][2 * pr + o][c] = in ? a : 0.f;
+                s_abc[1][2 * pr + o][c] = in ? b : 0.f;
+                s_abc[2][2 * pr + o][c] = in ? cc : 0.f;
+            }
+        }
+        lds_barrier();
+
+        // (4) horizontal pass of a/b/c (symmetric window: the transposed convolution is the same
+        // correlation), one output column per lane
+        {
+            const int r = tid >> 6, c = tid & 63;
+            const int ring = (p0 + r - kR) & (kRing - 1);
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                float sum = 0.f;
+#pragma unroll
+                for (int j = 0; j < 2 * kR + 1; j++) sum = fmaf(win.w[j], s_abc[q][r][c + j], sum);
+                s_h3[q][ring][c] = sum;
+            }
+        }
+        lds_barrier();
+
+        // (5) vertical pass and the gradient at output row orow = p0 + r - 2R
+        if (o_ok) {
+            const int c = tid & 63;
+            float acc[3];
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                acc[q] = 0.f;
+#pragma unroll
+                for (int j = 0; j < 2 * kR + 1; j++)
+                    acc[q] = fmaf(win.w[j], s_h3[q][(orow - kR + j) & (kRing - 1)][c], acc[q]);
+            }
+            const size_t o = (size_t)orow * W + ocol;
+            const float d = xv - yv;
+            const float G = acc[0] + 2.f * xv * acc[1] + yv * acc[2];
+            if (kMap) {
+                dx[o] = G;
+                l1 += fabsf(d);
+            } else {
+                const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+                dx[o] = g_l1 * sgn + g_ssim * G;
+            }
+        }
+    }
+    if (kMap) {
+        l1 = block_sum(l1, s_red);
+        ss = block_sum(ss, s_red + 4);
+        if (tid == 0) {
+            const int b = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+            partials[b] = make_float2(l1, ss);
+        }
+    }
+}
+
 // dx = (dout[0] sign(x - y) + dout[1] G) / n from the field l1_ssim_grad_kernel<true> stored.
 __global__ __launch_bounds__(256) void l1_ssim_bwd_map_kernel(const float4 *__restrict__ x, const float4 *__restrict__ y,
                                                               const float4 *__restrict__ G, int64_t n4,
@@ -620,6 +822,14 @@ int exposure_blocks(int64_t n) {
 }
 
 dim3 loss_grid(int C, int H, int W) { return dim3((W + kTW - 1) / kTW, (H + kTH - 1) / kTH, C); }
+dim3 stream_grid(int C, int H, int W) { return dim3((W + kStW - 1) / kStW, (H + kSegH - 1) / kSegH, C); }
+
+// GSR_SSIM_TILED=1 selects the 64 x 16 tile gradient kernel instead of the streaming one (same
+// bits; kept for the A/B test and measurements).  Read per call so a test can switch it.
+bool ssim_tiled() {
+    const char *e = std::getenv("GSR_SSIM_TILED");
+    return e != nullptr && e[0] == '1';
+}
 
 bool g_lds_attr = false;
 
@@ -641,8 +851,8 @@ extern "C" {
 
 size_t gsr_l1_ssim_scratch_bytes(int C, int H, int W) {
     if (C <= 0 || H <= 0 || W <= 0) return 0;
-    const dim3 g = loss_grid(C, H, W);
-    return sizeof(float2) * (size_t)g.x * g.y * g.z;
+    const dim3 g = loss_grid(C, H, W), gs = stream_grid(C, H, W);
+    return sizeof(float2) * std::max<size_t>((size_t)g.x * g.y * g.z, (size_t)gs.x * gs.y * gs.z);
 }
 
 int gsr_l1_ssim_forward(const float *img, const float *gt, int C, int H, int W, void *scratch, float *out,
@@ -674,8 +884,13 @@ int gsr_l1_ssim_backward(const float *img, const float *gt, int C, int H, int W,
     }
     hipStream_t s = static_cast<hipStream_t>(stream);
     set_lds_attr();
-    hipLaunchKernelGGL(l1_ssim_grad_kernel<false>, loss_grid(C, H, W), dim3(kLossThreads), kBwdLds, s, img, gt, H, W,
-                       ssim_window(), dL_dout, (float)(1.0 / ((double)C * H * W)), dL_dimg, nullptr);
+    const float inv_n = (float)(1.0 / ((double)C * H * W));
+    if (ssim_tiled())
+        hipLaunchKernelGGL(l1_ssim_grad_kernel<false>, loss_grid(C, H, W), dim3(kLossThreads), kBwdLds, s, img, gt, H,
+                           W, ssim_window(), dL_dout, inv_n, dL_dimg, nullptr);
+    else
+        hipLaunchKernelGGL(l1_ssim_stream_kernel<false>, stream_grid(C, H, W), dim3(kLossThreads), 0, s, img, gt, H,
+                           W, ssim_window(), dL_dout, inv_n, dL_dimg, nullptr);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_last_error(std::string("gsr_l1_ssim_backward: ") + hipGetErrorString(e));
@@ -692,11 +907,16 @@ int gsr_l1_ssim_forward_with_map(const float *img, const float *gt, int C, int H
     }
     hipStream_t s = static_cast<hipStream_t>(stream);
     set_lds_attr();
-    const dim3 g = loss_grid(C, H, W);
+    const bool tiled = ssim_tiled();
+    const dim3 g = tiled ? loss_grid(C, H, W) : stream_grid(C, H, W);
     const int nb = (int)(g.x * g.y * g.z);
     float2 *part = static_cast<float2 *>(scratch);
-    hipLaunchKernelGGL(l1_ssim_grad_kernel<true>, g, dim3(kLossThreads), kBwdLds, s, img, gt, H, W, ssim_window(),
-                       nullptr, 0.f, ssim_grad_map, part);
+    if (tiled)
+        hipLaunchKernelGGL(l1_ssim_grad_kernel<true>, g, dim3(kLossThreads), kBwdLds, s, img, gt, H, W, ssim_window(),
+                           nullptr, 0.f, ssim_grad_map, part);
+    else
+        hipLaunchKernelGGL(l1_ssim_stream_kernel<true>, g, dim3(kLossThreads), 0, s, img, gt, H, W, ssim_window(),
+                           nullptr, 0.f, ssim_grad_map, part);
     hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(1024), 0, s, part, nb, 1.0 / ((double)C * H * W), out);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {

@@ -98,6 +98,35 @@ def test_l1_ssim_map_path_equals_direct_backward(shape):
     assert torch.equal(img.grad, direct)
 
 
+@pytest.mark.parametrize("shape", [(3, 1080, 1920), (3, 77, 131), (1, 200, 64), (2, 64, 63), (1, 5, 9)])
+def test_l1_ssim_streaming_equals_tiled(shape, monkeypatch):
+    """The streaming gradient kernel (64 x 64 strips, LDS rings) and the 64 x 16 tile kernel form
+    every value with the same fmaf order: G and dx must agree bit for bit (GSR_SSIM_TILED=1
+    selects the tile kernel)."""
+    from gs_train._native import lib, ptr, stream
+    g = torch.Generator().manual_seed(11)
+    img = torch.rand(shape, generator=g).to(DEV)
+    gt = torch.rand(shape, generator=g).to(DEV)
+    C, H, W = shape
+    up = torch.tensor([0.8, -0.2], device=DEV)
+    L = lib()
+    scratch = torch.empty(L.gsr_l1_ssim_scratch_bytes(C, H, W), dtype=torch.uint8, device=DEV)
+    res = {}
+    for tiled in ("0", "1"):
+        monkeypatch.setenv("GSR_SSIM_TILED", tiled)
+        dx = torch.empty_like(img)
+        gmap = torch.empty_like(img)
+        out = torch.empty(2, device=DEV)
+        s = stream(img.device)
+        assert L.gsr_l1_ssim_backward(ptr(img), ptr(gt), C, H, W, ptr(up), ptr(dx), s) == 0
+        assert L.gsr_l1_ssim_forward_with_map(ptr(img), ptr(gt), C, H, W, ptr(scratch), ptr(out), ptr(gmap), s) == 0
+        torch.cuda.synchronize()
+        res[tiled] = (dx, gmap, out)
+    assert torch.equal(res["0"][0], res["1"][0])
+    assert torch.equal(res["0"][1], res["1"][1])
+    assert torch.allclose(res["0"][2], res["1"][2], rtol=0, atol=1e-6)
+
+
 def _adam_from_fixture(use_index):
     from gs_train import Adam
     d = np.load(os.path.join(GOLD, "adam.npz"))
