@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--profile-steps", type=int, default=5, help="extra steps with per-stage HIP events")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--diag", action="store_true", help="print synced per-step fwd/bwd wall times to stderr")
-    ap.add_argument("--train-steps", type=int, default=10, help="timed train-step harness iterations (0 = skip)")
+    ap.add_argument("--train-steps", type=int, default=20, help="timed train-step harness iterations (0 = skip)")
     ap.add_argument("--config5", action="store_true",
                     help="also time config 5: hierarchy cut blend + forward render of the cut at 1080p")
     ap.add_argument("--c5-nodes", type=int, default=50_000_000)
@@ -336,12 +336,12 @@ def main():
                               if serial_ms > 0 else None},
     }
     if a.train_steps > 0:
-        tr = {"ms": round(train_step_ms(s, W, H, deg, a.train_steps, 3, True, dev), 4),
+        tr = {"ms": round(train_step_ms(s, W, H, deg, a.train_steps, 5, True, dev), 4),
               "workload": f"train_single.py iteration on the bench scene ({P} Gaussians, {W}x{H}): render, exposure, "
                           f"0.8 L1 + 0.2 (1 - SSIM), backward, densify stats, exposure Adam, sparse Adam, scale clamp",
               "steps": a.train_steps, "fused": True}
         if a.train_baseline:
-            tr["reference_structured_ms"] = round(train_step_ms(s, W, H, deg, a.train_steps, 3, False, dev), 4)
+            tr["reference_structured_ms"] = round(train_step_ms(s, W, H, deg, a.train_steps, 5, False, dev), 4)
         out["train_step"] = tr
     if a.config5:
         out["config5"] = config5(a, dev)
