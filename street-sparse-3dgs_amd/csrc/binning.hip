@@ -5,7 +5,7 @@
 // order (one 32-bit sort of P keys, dsort.hip), and the per-tile lists are built by two stable
 // counting passes that exploit each splat's footprint being a rectangle of tiles:
 //
-//   level 1  Gaussian -> superblock (SB = 2^s x 2^s tiles, ~500 at 1080p).  Chunks of 2048
+//   level 1  Gaussian -> superblock (SB = 2^s x 2^s tiles, ~500 at 1080p).  Chunks of 1024 (more when P is large)
 //            depth-ordered Gaussians count their SB footprints in LDS (sb_count), per-SB column
 //            scans over chunks give every chunk its offsets (sb_colscan, sb_base), and a second
 //            pass writes each SB's Gaussian list in depth order (sb_scatter): per batch of 64
@@ -44,6 +44,52 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+#ifndef GSR_SCATTER_WAVES
+#define GSR_SCATTER_WAVES 8
+#endif
+#ifndef GSR_SMALL_SB
+#define GSR_SMALL_SB 16
+#endif
+constexpr int kScatterWaves = GSR_SCATTER_WAVES;
+constexpr int kSmallSB = GSR_SMALL_SB;
+
+struct SBFoot {
+    int sx0, sy0, sw, n;
+};
+
+__device__ __forceinline__ SBFoot sb_foot(const TileRect &r, int shift) {
+    SBFoot f{0, 0, 1, 0};
+    if (r.x1 < r.x0) return f;
+    f.sx0 = r.x0 >> shift;
+    f.sy0 = r.y0 >> shift;
+    f.sw = (r.x1 >> shift) - f.sx0 + 1;
+    f.n = f.sw * ((r.y1 >> shift) - f.sy0 + 1);
+    return f;
+}
+
+__device__ __forceinline__ uint32_t sb_key(const SBFoot &f, int k, int nsbx) {
+    return (uint32_t)((f.sy0 + k / f.sw) * nsbx + f.sx0 + k % f.sw);
+}
+
+// footprint clipped to SB `key`, in SB-local tile coordinates (8 bits each)
+__device__ __forceinline__ uint32_t sb_local(const TileRect &r, uint32_t key, const SBGrid &sg) {
+    const int side = 1 << sg.shift;
+    const int ox = (int)(key % (uint32_t)sg.nsbx) * side, oy = (int)(key / (uint32_t)sg.nsbx) * side;
+    return (uint32_t)(max(r.x0, ox) - ox) | ((uint32_t)(max(r.y0, oy) - oy) << 8) |
+           ((uint32_t)(min(r.x1, ox + side - 1) - ox) << 16) | ((uint32_t)(min(r.y1, oy + side - 1) - oy) << 24);
+}
+
+// lane b's value; b is wave-uniform, so v_readlane (no LDS round trip as with __shfl)
+__device__ __forceinline__ int rl(int v, int b) { return __builtin_amdgcn_readlane(v, b); }
+
+__device__ __forceinline__ TileRect lane_rect(const TileRect &r, int b) {
+    return TileRect{rl(r.x0, b), rl(r.y0, b), rl(r.x1, b), rl(r.y1, b)};
+}
+
+__device__ __forceinline__ SBFoot lane_foot(const SBFoot &f, int b) {
+    return SBFoot{rl(f.sx0, b), rl(f.sy0, b), rl(f.sw, b), rl(f.n, b)};
+}
+
 // Level 1, pass 1: per chunk and SB, the number of Gaussians and of tile instances.
 __global__ __launch_bounds__(1024) void sb_count_kernel(int P, SBGrid sg, const uint2 *__restrict__ drect,
                                                        uint32_t *__restrict__ cnt_g, uint32_t *__restrict__ cnt_i) {
@@ -52,19 +98,29 @@ __global__ __launch_bounds__(1024) void sb_count_kernel(int P, SBGrid sg, const 
     for (int i = threadIdx.x; i < 2 * sg.nsb; i += 1024) lds[i] = 0u;
     __syncthreads();
     const int chunk = blockIdx.x;
-    const int j0 = chunk * kSBChunk, j1 = min(P, j0 + kSBChunk);
-    for (int j = j0 + (int)threadIdx.x; j < j1; j += 1024) {
-        const TileRect r = unpack_rect(drect[j]);
-        if (r.x1 < r.x0) continue;
-        const int side = 1 << sg.shift;
-        for (int sy = r.y0 >> sg.shift; sy <= r.y1 >> sg.shift; sy++) {
-            const int h = min(r.y1, sy * side + side - 1) - max(r.y0, sy * side) + 1;
-            for (int sx = r.x0 >> sg.shift; sx <= r.x1 >> sg.shift; sx++) {
-                const int w = min(r.x1, sx * side + side - 1) - max(r.x0, sx * side) + 1;
-                const int sb = sy * sg.nsbx + sx;
-                atomicAdd(&cg[sb], 1u);
-                atomicAdd(&ci[sb], (uint32_t)(w * h));
-            }
+    const int j0 = chunk * sg.chunk, j1 = min(P, j0 + sg.chunk);
+    const int side = 1 << sg.shift;
+    // instances of Gaussian footprint r in SB `key`
+    const auto count = [&](const TileRect &r, uint32_t key) {
+        const int sx = (int)(key % (uint32_t)sg.nsbx), sy = (int)(key / (uint32_t)sg.nsbx);
+        const int h = min(r.y1, sy * side + side - 1) - max(r.y0, sy * side) + 1;
+        const int w = min(r.x1, sx * side + side - 1) - max(r.x0, sx * side) + 1;
+        atomicAdd(&cg[key], 1u);
+        atomicAdd(&ci[key], (uint32_t)(w * h));
+    };
+    for (int jb = j0; jb < j1; jb += 1024) {
+        const int j = jb + (int)threadIdx.x;
+        const TileRect r = j < j1 ? unpack_rect(drect[j]) : TileRect{0, 0, -1, -1};
+        const SBFoot f = sb_foot(r, sg.shift);
+        // footprints over more than kSmallSB superblocks are counted by the whole wave, one SB per
+        // lane (a single lane would hold its wave for hundreds of iterations)
+        const bool small = f.n <= kSmallSB;
+        for (int k = 0; small && k < f.n; k++) count(r, sb_key(f, k, sg.nsbx));
+        for (uint64_t big = __ballot(!small); big; big &= big - 1) {
+            const int b = __ffsll((unsigned long long)big) - 1;
+            const SBFoot fb = lane_foot(f, b);
+            const TileRect rb = lane_rect(r, b);
+            for (int k = threadIdx.x & 63; k < fb.n; k += 64) count(rb, sb_key(fb, k, sg.nsbx));
         }
     }
     __syncthreads();
@@ -164,52 +220,6 @@ __global__ __launch_bounds__(kColThreads) void sb_colscan_kernel(SBGrid sg, uint
 // each mask advances the SB's position and clears the mask.  Footprints of up to kSmallSB SBs
 // are walked per lane; larger ones (rare, 3-sigma splats) by the whole wave, one at a time, so
 // one outlier does not serialise its batch.
-#ifndef GSR_SCATTER_WAVES
-#define GSR_SCATTER_WAVES 8
-#endif
-#ifndef GSR_SMALL_SB
-#define GSR_SMALL_SB 16
-#endif
-constexpr int kScatterWaves = GSR_SCATTER_WAVES;
-constexpr int kSmallSB = GSR_SMALL_SB;
-
-struct SBFoot {
-    int sx0, sy0, sw, n;
-};
-
-__device__ __forceinline__ SBFoot sb_foot(const TileRect &r, int shift) {
-    SBFoot f{0, 0, 1, 0};
-    if (r.x1 < r.x0) return f;
-    f.sx0 = r.x0 >> shift;
-    f.sy0 = r.y0 >> shift;
-    f.sw = (r.x1 >> shift) - f.sx0 + 1;
-    f.n = f.sw * ((r.y1 >> shift) - f.sy0 + 1);
-    return f;
-}
-
-__device__ __forceinline__ uint32_t sb_key(const SBFoot &f, int k, int nsbx) {
-    return (uint32_t)((f.sy0 + k / f.sw) * nsbx + f.sx0 + k % f.sw);
-}
-
-// footprint clipped to SB `key`, in SB-local tile coordinates (8 bits each)
-__device__ __forceinline__ uint32_t sb_local(const TileRect &r, uint32_t key, const SBGrid &sg) {
-    const int side = 1 << sg.shift;
-    const int ox = (int)(key % (uint32_t)sg.nsbx) * side, oy = (int)(key / (uint32_t)sg.nsbx) * side;
-    return (uint32_t)(max(r.x0, ox) - ox) | ((uint32_t)(max(r.y0, oy) - oy) << 8) |
-           ((uint32_t)(min(r.x1, ox + side - 1) - ox) << 16) | ((uint32_t)(min(r.y1, oy + side - 1) - oy) << 24);
-}
-
-// lane b's value; b is wave-uniform, so v_readlane (no LDS round trip as with __shfl)
-__device__ __forceinline__ int rl(int v, int b) { return __builtin_amdgcn_readlane(v, b); }
-
-__device__ __forceinline__ TileRect lane_rect(const TileRect &r, int b) {
-    return TileRect{rl(r.x0, b), rl(r.y0, b), rl(r.x1, b), rl(r.y1, b)};
-}
-
-__device__ __forceinline__ SBFoot lane_foot(const SBFoot &f, int b) {
-    return SBFoot{rl(f.sx0, b), rl(f.sy0, b), rl(f.sw, b), rl(f.n, b)};
-}
-
 __global__ __launch_bounds__(64 * kScatterWaves) void sb_scatter_kernel(int P, SBGrid sg,
                                                                          const uint32_t *__restrict__ order,
                                                                          const uint2 *__restrict__ drect,
@@ -222,8 +232,8 @@ __global__ __launch_bounds__(64 * kScatterWaves) void sb_scatter_kernel(int P, S
     for (int i = threadIdx.x; i < 3 * kScatterWaves * nsb; i += 64 * kScatterWaves) wc[i] = 0u;
     __syncthreads();
     const int chunk = blockIdx.x;
-    constexpr int kPerWave = kSBChunk / kScatterWaves;
-    const int jw0 = chunk * kSBChunk + w * kPerWave, jw1 = min(P, jw0 + kPerWave);
+    const int per_wave = sg.chunk / kScatterWaves;
+    const int jw0 = chunk * sg.chunk + w * per_wave, jw1 = min(P, jw0 + per_wave);
     uint32_t *run = wc + w * nsb;
     uint64_t *msk = reinterpret_cast<uint64_t *>(wc + kScatterWaves * nsb) + w * nsb;
     const uint64_t lt = (1ull << lane) - 1ull;
@@ -428,7 +438,12 @@ SBGrid sb_grid(int gx, int gy, int P) {
         if (g.nsb <= kMaxSB || (1 << (2 * (g.shift + 1))) > kMaxTilesPerSB) break;
         g.shift++;
     }
-    g.nchunks = (P + kSBChunk - 1) / kSBChunk;
+    // The per-(SB, chunk) counters are written column-major ([nsb][nchunks], one 4-B store per
+    // SB and chunk): past ~1.5K chunks they outgrow the caches and every store becomes a partial
+    // HBM line write (sb_count 282 us at 5.1M Gaussians), so large P takes bigger chunks.
+    g.chunk = kSBChunk;
+    while ((P + g.chunk - 1) / g.chunk > kMaxChunks) g.chunk *= 2;
+    g.nchunks = (P + g.chunk - 1) / g.chunk;
     if (g.nchunks < 1) g.nchunks = 1;
     return g;
 }

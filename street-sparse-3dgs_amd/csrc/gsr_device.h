@@ -364,11 +364,15 @@ static_assert(sizeof(GRec) == 64, "GRec must be one 64-B line");
 #ifndef GSR_SB_CHUNK
 #define GSR_SB_CHUNK 1024
 #endif
-constexpr int kSBChunk = GSR_SB_CHUNK;  // depth-ordered Gaussians per level-1 chunk
+constexpr int kSBChunk = GSR_SB_CHUNK;  // smallest level-1 chunk (SBGrid.chunk doubles for large P)
+#ifndef GSR_MAX_CHUNKS
+#define GSR_MAX_CHUNKS 1536
+#endif
+constexpr int kMaxChunks = GSR_MAX_CHUNKS;  // chunks before SBGrid.chunk doubles
 constexpr int kMaxSB = 1536;          // superblocks (3 x 8 waves x 4 B of LDS each in sb_scatter)
 constexpr int kMaxTilesPerSB = 256;   // up to 16 x 16 tiles per superblock
 struct SBGrid {
-    int shift, nsbx, nsby, nsb, nchunks;
+    int shift, nsbx, nsby, nsb, nchunks, chunk;  // chunk: depth-ordered Gaussians per level-1 chunk
 };
 
 struct GeomState {          // per Gaussian, written by preprocess

@@ -1,6 +1,6 @@
 // hier.hip -- fused hierarchy-cut interpolation of render_post (include/gsr_hier.h; SURVEY.md
-// 8(a) A14, 8(f) row 3).  Thread per output row; the 48-float SH row moves as 12 float4 when
-// M = 16 and the arrays are 16-B aligned.  Backward scatters with float atomics into the N-row
+// 8(a) A14, 8(f) row 3).  Thread per output row for the scalar fields; the 48-float SH rows are
+// moved 16 lanes per row (one float4 per lane) when M = 16.  Backward scatters with float atomics into the N-row
 // gradients: the same accumulate semantics as torch's index backward, which the reference relies
 // on when several rendered nodes share a parent.
 #include <string>
@@ -36,6 +36,10 @@ __device__ __forceinline__ CutRow cut_row(int64_t r, int64_t N, int64_t R, int64
 
 __device__ __forceinline__ float lerp_w(float t, float a, float b) { return t * a + (1.f - t) * b; }
 
+// Thread per output row for the 14 scalar fields.  The 192-B SH rows (M = 16, 16-B aligned) are
+// moved by the wave as a whole: 16 lanes per row (12 active, one float4 each), four rows per
+// instruction, so every load reads whole contiguous rows instead of one float4 from each of 64
+// rows 192 B apart.  The row's (child, parent, weight) come from its owner lane by shuffle.
 __global__ __launch_bounds__(256) void cut_fwd_kernel(int64_t N, int M, int64_t R, int64_t S, const int *ri,
                                                       const int *pi, const float *w, const float *__restrict__ means,
                                                       const float *__restrict__ scales, const float *__restrict__ rots,
@@ -44,46 +48,59 @@ __global__ __launch_bounds__(256) void cut_fwd_kernel(int64_t N, int M, int64_t 
                                                       float *__restrict__ orot, float *__restrict__ oop,
                                                       float *__restrict__ osh, bool vec) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= R + S) return;
-    const CutRow q = cut_row(r, N, R, S, ri, pi, w);
+    const int64_t rows = R + S;
+    const bool valid = r < rows;
+    CutRow q{0, 0, 1.f, true};
+    if (valid) q = cut_row(r, N, R, S, ri, pi, w);
     const float t = q.t;
-    if (q.copy) {
-        for (int k = 0; k < 3; k++) om[3 * r + k] = means[3 * q.c + k];
-        for (int k = 0; k < 3; k++) os[3 * r + k] = scales[3 * q.c + k];
-        for (int k = 0; k < 4; k++) orot[4 * r + k] = rots[4 * q.c + k];
-        oop[r] = opac[q.c];
-        if (vec) {
-            const float4 *src = reinterpret_cast<const float4 *>(shs) + 12 * q.c;
-            float4 *dst = reinterpret_cast<float4 *>(osh) + 12 * r;
-#pragma unroll
-            for (int k = 0; k < 12; k++) dst[k] = src[k];
+    if (valid) {
+        if (q.copy) {
+            for (int k = 0; k < 3; k++) om[3 * r + k] = means[3 * q.c + k];
+            for (int k = 0; k < 3; k++) os[3 * r + k] = scales[3 * q.c + k];
+            for (int k = 0; k < 4; k++) orot[4 * r + k] = rots[4 * q.c + k];
+            oop[r] = opac[q.c];
         } else {
-            for (int k = 0; k < 3 * M; k++) osh[(size_t)r * 3 * M + k] = shs[(size_t)q.c * 3 * M + k];
+            for (int k = 0; k < 3; k++) om[3 * r + k] = lerp_w(t, means[3 * q.c + k], means[3 * q.p + k]);
+            for (int k = 0; k < 3; k++) os[3 * r + k] = lerp_w(t, scales[3 * q.c + k], scales[3 * q.p + k]);
+            const float4 qc = reinterpret_cast<const float4 *>(rots)[q.c];
+            float4 qp = reinterpret_cast<const float4 *>(rots)[q.p];
+            // torch.bmm(rots (1x4), parents (4x1)): the dot in float, left to right
+            const float dot = qc.x * qp.x + qc.y * qp.y + qc.z * qp.z + qc.w * qp.w;
+            if (dot < 0.f) qp = make_float4(-qp.x, -qp.y, -qp.z, -qp.w);
+            reinterpret_cast<float4 *>(orot)[r] = make_float4(lerp_w(t, qc.x, qp.x), lerp_w(t, qc.y, qp.y),
+                                                              lerp_w(t, qc.z, qp.z), lerp_w(t, qc.w, qp.w));
+            oop[r] = lerp_w(t, opac[q.c], opac[q.p]);
         }
-        return;
     }
-    for (int k = 0; k < 3; k++) om[3 * r + k] = lerp_w(t, means[3 * q.c + k], means[3 * q.p + k]);
-    for (int k = 0; k < 3; k++) os[3 * r + k] = lerp_w(t, scales[3 * q.c + k], scales[3 * q.p + k]);
-    const float4 qc = reinterpret_cast<const float4 *>(rots)[q.c];
-    float4 qp = reinterpret_cast<const float4 *>(rots)[q.p];
-    // torch.bmm(rots (1x4), parents (4x1)): the dot in float, left to right
-    const float dot = qc.x * qp.x + qc.y * qp.y + qc.z * qp.z + qc.w * qp.w;
-    if (dot < 0.f) qp = make_float4(-qp.x, -qp.y, -qp.z, -qp.w);
-    reinterpret_cast<float4 *>(orot)[r] =
-        make_float4(lerp_w(t, qc.x, qp.x), lerp_w(t, qc.y, qp.y), lerp_w(t, qc.z, qp.z), lerp_w(t, qc.w, qp.w));
-    oop[r] = lerp_w(t, opac[q.c], opac[q.p]);
     if (vec) {
-        const float4 *a = reinterpret_cast<const float4 *>(shs) + 12 * q.c;
-        const float4 *b = reinterpret_cast<const float4 *>(shs) + 12 * q.p;
-        float4 *dst = reinterpret_cast<float4 *>(osh) + 12 * r;
-#pragma unroll
-        for (int k = 0; k < 12; k++) {
-            const float4 x = a[k], y = b[k];
-            dst[k] = make_float4(lerp_w(t, x.x, y.x), lerp_w(t, x.y, y.y), lerp_w(t, x.z, y.z), lerp_w(t, x.w, y.w));
+        const int lane = threadIdx.x & 63, col = lane & 15, sub = lane >> 4;
+        const int64_t wrow0 = r - lane;
+        if (wrow0 >= rows) return;  // wave-uniform
+        const float4 *sh4 = reinterpret_cast<const float4 *>(shs);
+        float4 *o4 = reinterpret_cast<float4 *>(osh);
+#pragma unroll 4
+        for (int k = 0; k < 16; k++) {
+            const int src = 4 * k + sub;
+            const int64_t rr = wrow0 + src;
+            const int64_t cc = __shfl((long long)q.c, src, 64), pp = __shfl((long long)q.p, src, 64);
+            const float tt = __shfl(t, src, 64);
+            const bool cp = __shfl((int)q.copy, src, 64) != 0;
+            if (rr < rows && col < 12) {
+                const float4 x = sh4[12 * cc + col];
+                float4 v = x;
+                if (!cp) {
+                    const float4 y = sh4[12 * pp + col];
+                    v = make_float4(lerp_w(tt, x.x, y.x), lerp_w(tt, x.y, y.y), lerp_w(tt, x.z, y.z), lerp_w(tt, x.w, y.w));
+                }
+                o4[12 * rr + col] = v;
+            }
         }
-    } else {
-        for (int k = 0; k < 3 * M; k++)
-            osh[(size_t)r * 3 * M + k] = lerp_w(t, shs[(size_t)q.c * 3 * M + k], shs[(size_t)q.p * 3 * M + k]);
+    } else if (valid) {
+        if (q.copy)
+            for (int k = 0; k < 3 * M; k++) osh[(size_t)r * 3 * M + k] = shs[(size_t)q.c * 3 * M + k];
+        else
+            for (int k = 0; k < 3 * M; k++)
+                osh[(size_t)r * 3 * M + k] = lerp_w(t, shs[(size_t)q.c * 3 * M + k], shs[(size_t)q.p * 3 * M + k]);
     }
 }
 
@@ -92,7 +109,7 @@ __global__ __launch_bounds__(256) void cut_bwd_kernel(int64_t N, int M, int64_t 
                                                       const float *__restrict__ gm, const float *__restrict__ gs,
                                                       const float *__restrict__ grot, const float *__restrict__ gop,
                                                       const float *__restrict__ gsh, float *dm, float *ds, float *drot,
-                                                      float *dop, float *dsh) {
+                                                      float *dop, float *dsh, bool vec) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= R + S) return;
     const CutRow q = cut_row(r, N, R, S, ri, pi, w);
@@ -102,7 +119,8 @@ __global__ __launch_bounds__(256) void cut_bwd_kernel(int64_t N, int M, int64_t 
         for (int k = 0; k < 3; k++) atomicAdd(&ds[3 * q.c + k], gs[3 * r + k]);
         for (int k = 0; k < 4; k++) atomicAdd(&drot[4 * q.c + k], grot[4 * r + k]);
         atomicAdd(&dop[q.c], gop[r]);
-        for (int k = 0; k < 3 * M; k++) atomicAdd(&dsh[(size_t)q.c * 3 * M + k], gsh[(size_t)r * 3 * M + k]);
+        if (!vec)
+            for (int k = 0; k < 3 * M; k++) atomicAdd(&dsh[(size_t)q.c * 3 * M + k], gsh[(size_t)r * 3 * M + k]);
         return;
     }
     for (int k = 0; k < 3; k++) {
@@ -121,11 +139,42 @@ __global__ __launch_bounds__(256) void cut_bwd_kernel(int64_t N, int M, int64_t 
     }
     atomicAdd(&dop[q.c], t * gop[r]);
     atomicAdd(&dop[q.p], u * gop[r]);
+    if (vec) return;
     for (int k = 0; k < 3 * M; k++) {
         const float g = gsh[(size_t)r * 3 * M + k];
         atomicAdd(&dsh[(size_t)q.c * 3 * M + k], t * g);
         atomicAdd(&dsh[(size_t)q.p * 3 * M + k], u * g);
     }
+}
+
+// SH part of the backward for M = 16: 16 lanes per row (12 active, 4 floats each), four rows per
+// wave instruction, so the atomics of one row hit one or two cache lines together.
+__global__ __launch_bounds__(256) void cut_bwd_sh_kernel(int64_t N, int64_t R, int64_t S, const int *ri, const int *pi,
+                                                         const float *w, const float *__restrict__ gsh,
+                                                         float *dsh) {
+    const int64_t rr = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+    const int col = threadIdx.x & 15;
+    if (rr >= R + S || col >= 12) return;
+    const CutRow q = cut_row(rr, N, R, S, ri, pi, w);
+    const float4 g = reinterpret_cast<const float4 *>(gsh)[12 * rr + col];
+    float *dc = dsh + 48 * q.c + 4 * col;
+    if (q.copy) {
+        atomicAdd(dc + 0, g.x);
+        atomicAdd(dc + 1, g.y);
+        atomicAdd(dc + 2, g.z);
+        atomicAdd(dc + 3, g.w);
+        return;
+    }
+    const float t = q.t, u = 1.f - q.t;
+    float *dp = dsh + 48 * q.p + 4 * col;
+    atomicAdd(dc + 0, t * g.x);
+    atomicAdd(dc + 1, t * g.y);
+    atomicAdd(dc + 2, t * g.z);
+    atomicAdd(dc + 3, t * g.w);
+    atomicAdd(dp + 0, u * g.x);
+    atomicAdd(dp + 1, u * g.y);
+    atomicAdd(dp + 2, u * g.z);
+    atomicAdd(dp + 3, u * g.w);
 }
 
 }  // namespace
@@ -182,11 +231,16 @@ int gsr_interpolate_cut_backward(int64_t N, int M, int64_t R, int64_t S, const i
         return GSR_ERR_INVALID_ARGUMENT;
     }
     const int64_t rows = R + S;
+    const bool vec = M == 16 && reinterpret_cast<uintptr_t>(dL_dout_shs) % 16 == 0;
     hipLaunchKernelGGL(cut_bwd_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0,
                        static_cast<hipStream_t>(stream), N, M, R, S, render_indices, parent_indices,
                        interpolation_weights, rotations, dL_dout_means3D, dL_dout_scales, dL_dout_rotations,
                        dL_dout_opacities, dL_dout_shs, dL_dmeans3D, dL_dscales, dL_drotations, dL_dopacities,
-                       dL_dshs);
+                       dL_dshs, vec);
+    if (vec)
+        hipLaunchKernelGGL(cut_bwd_sh_kernel, dim3((unsigned)((16 * rows + 255) / 256)), dim3(256), 0,
+                           static_cast<hipStream_t>(stream), N, R, S, render_indices, parent_indices,
+                           interpolation_weights, dL_dout_shs, dL_dshs);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_last_error(std::string("gsr_interpolate_cut_backward: ") + hipGetErrorString(e));

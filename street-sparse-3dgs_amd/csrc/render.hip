@@ -349,6 +349,9 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
 #ifndef GSR_BWD_PREFETCH
 #define GSR_BWD_PREFETCH 0
 #endif
+#ifndef GSR_REC_PAD
+#define GSR_REC_PAD 1  // write the unused 4th float4 of a 64-B record (full 64-B segments)
+#endif
 template <bool kDepth>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVES_PER_EU))) void render_bwd_kernel(
     const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list, int W, int H, int gx,
@@ -439,7 +442,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
                 out[4 * (size_t)u + 0] = z;
                 out[4 * (size_t)u + 1] = z;
                 out[4 * (size_t)u + 2] = z;
-                out[4 * (size_t)u + 3] = z;
+                if (GSR_REC_PAD) out[4 * (size_t)u + 3] = z;
             }
         }
         const uint64_t keep = __ballot(m != 0u);
@@ -596,7 +599,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
             out[o + 0] = make_float4(r[0] * sx, r[1] * sy, -0.5f * r[2], -0.5f * r[3]);
             out[o + 1] = make_float4(-0.5f * r[4], r[5], r[6], r[7]);
             out[o + 2] = make_float4(r[8], r[9], 0.f, 0.f);
-            out[o + 3] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (GSR_REC_PAD) out[o + 3] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
         __syncthreads();
     }

@@ -34,6 +34,8 @@ CASES = [
     dict(name="equal_depths", P=3000, W=96, H=64, deg=1, seed=9, log_scale=-3.0, flat_z=6.0),
     # many depth-sort tiles (8192 keys each) with ties across tiles and culled Gaussians mixed in
     dict(name="sort_tiles_ties", P=40000, W=128, H=96, deg=0, seed=14, log_scale=-3.5, behind=0.2, quant_z=0.25),
+    # footprints over tens of 4x4-tile superblocks next to small ones (the binning's wave-wide path)
+    dict(name="huge_splats_sb", P=300, W=640, H=480, deg=1, seed=15, log_scale=-0.5),
 ]
 
 
