@@ -1,4 +1,5 @@
-"""Host-vs-device split of the fused train step (diagnostic)."""
+"""Host-issue vs device time of the fused train step, plus a cProfile of 20 steps (run on the GPU box:
+`python tools/train_host_split.py`)."""
 import cProfile, pstats, sys, time, io
 sys.path.insert(0, "/root/repo"); sys.path.insert(0, "/root/repo/street-sparse-3dgs_amd")
 import torch
