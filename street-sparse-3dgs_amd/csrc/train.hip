@@ -674,6 +674,59 @@ __global__ __launch_bounds__(kAdamThreads) void sparse_adam_kernel(AdamArgs a, c
     }
 }
 
+// Row-block form: one wave per 64 consecutive rows.  The relevance of the 64 rows is one
+// coalesced load and a ballot; a block of irrelevant rows costs nothing more.  Narrow groups
+// (xyz, opacity, scaling, rotation, f_dc) are updated lane = row; a wide group (f_rest) row by
+// relevant row, lanes across its columns (one contiguous 180-B segment per row).  The per-element
+// arithmetic is adam_element's, so the result is bit-identical to sparse_adam_kernel's; the
+// element-per-thread form launched P x 59 threads that mostly only read rel[row].
+__device__ __forceinline__ void adam_at(const gsr_adam_group &G, int64_t e, float b1, float b2, float omb1,
+                                        float omb2, float eps) {
+    const float g = G.grad[e];
+    const float m = G.exp_avg[e] * b1 + omb1 * g;
+    const float v = G.exp_avg_sq[e] * b2 + omb2 * (g * g);
+    const float denom = sqrtf(v) / G.bias_correction2_sqrt + eps;
+    G.exp_avg[e] = m;
+    G.exp_avg_sq[e] = v;
+    G.param[e] = G.param[e] + (-G.step_size) * (m / denom);
+}
+
+constexpr int kAdamNarrow = 8;
+__global__ __launch_bounds__(kAdamThreads) void sparse_adam_rows_kernel(AdamArgs a, const float *__restrict__ rel,
+                                                                        int64_t P, float b1, float b2, float omb1,
+                                                                        float omb2, float eps,
+                                                                        const int *__restrict__ flag) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r0 = (((int64_t)blockIdx.x * kAdamThreads + threadIdx.x) >> 6) * 64;
+    if (r0 >= P) return;  // wave-uniform
+    const int64_t row = r0 + lane;
+    const bool dense = *flag == 0;
+    const bool relv = row < P && (dense || rel[row] != 0.f);
+    const uint64_t mask = __ballot(relv);
+    if (mask == 0) return;
+    for (int gi = 0; gi < a.n; gi++) {
+        const gsr_adam_group &G = a.g[gi];
+        const int w = G.width;
+        const int64_t rs = G.row_stride;
+        if (w <= kAdamNarrow) {
+            if (relv)
+                for (int c = 0; c < w; c++) adam_at(G, row * rs + c, b1, b2, omb1, omb2, eps);
+        } else {
+            for (uint64_t m = mask; m; m &= m - 1) {
+                const int64_t base = (r0 + __builtin_ctzll(m)) * rs;
+                for (int c = lane; c < w; c += 64) adam_at(G, base + c, b1, b2, omb1, omb2, eps);
+            }
+        }
+    }
+}
+
+// GSR_ADAM_ELEMENTWISE=1 selects the element-per-thread kernel (same bits; A/B test and
+// measurements).  Read per call so a test can switch it.
+bool adam_elementwise() {
+    const char *e = std::getenv("GSR_ADAM_ELEMENTWISE");
+    return e != nullptr && e[0] == '1';
+}
+
 __global__ __launch_bounds__(256) void densify_stats_kernel(int64_t P, const int *__restrict__ radii,
                                                             const float *__restrict__ g2d, float *__restrict__ maxr,
                                                             float *__restrict__ accum, float *__restrict__ denom) {
@@ -991,8 +1044,14 @@ int gsr_sparse_adam_step(int n_groups, const gsr_adam_group *groups, int64_t P, 
     hipLaunchKernelGGL(any_nonzero_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, relevance, P,
                        flag_scratch);
     // torch applies python-float hyper-parameters as fp32 scalars: b, (1 - b) rounded from double
-    hipLaunchKernelGGL(sparse_adam_kernel, dim3((unsigned)blocks), dim3(kAdamThreads), 0, s, a, relevance, P,
-                       (float)beta1, (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps, flag_scratch);
+    if (!adam_elementwise())
+        hipLaunchKernelGGL(sparse_adam_rows_kernel, dim3((unsigned)((P + kAdamThreads - 1) / kAdamThreads)),
+                           dim3(kAdamThreads), 0, s, a, relevance, P, (float)beta1, (float)beta2,
+                           (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps, flag_scratch);
+    else
+        hipLaunchKernelGGL(sparse_adam_kernel, dim3((unsigned)blocks), dim3(kAdamThreads), 0, s, a, relevance, P,
+                           (float)beta1, (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps,
+                           flag_scratch);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_last_error(std::string("gsr_sparse_adam_step: ") + hipGetErrorString(e));

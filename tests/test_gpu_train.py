@@ -304,3 +304,36 @@ def test_adam_column_blocks_equal_separate_groups():
     assert torch.equal(joined.detach()[:, :1], dc.detach())
     assert torch.equal(joined.detach()[:, 1:], rest.detach())
     assert torch.equal(oj.state[joined]["exp_avg_sq"][:, 1:], os_.state[rest]["exp_avg_sq"])
+
+
+@pytest.mark.parametrize("frac", [0.12, 0.9, 0.0])
+def test_sparse_adam_row_blocks_equal_elementwise(frac, monkeypatch):
+    """The row-block Adam kernel (one wave per 64 rows) and the element-per-thread kernel apply
+    the same per-element arithmetic: parameters and moments bit-identical, for sparse and dense
+    relevance (frac 0: no relevant row, the dense fallback) and joined (P,16,3) column blocks."""
+    from gs_train import Adam
+    P = 70_001
+    g = torch.Generator().manual_seed(5)
+    shapes = [(3,), (16, 3), (1,), (3,), (4,)]
+    init = [torch.randn((P,) + s, generator=g) for s in shapes]
+    grads = [[torch.randn((P,) + s, generator=g) for s in shapes] for _ in range(2)]
+    for gr in grads:
+        gr[2][torch.rand(P, generator=g) >= frac] = 0.0
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("GSR_ADAM_ELEMENTWISE", mode)
+        params = [torch.nn.Parameter(h.to(DEV)) for h in init]
+        groups = [{"params": [params[0]], "lr": 1.6e-4},
+                  {"params": [params[1]], "lr": 2.5e-3, "column_lrs": [(0, 3, 2.5e-3), (3, 48, 1.25e-4)]},
+                  {"params": [params[2]], "lr": 5e-2}, {"params": [params[3]], "lr": 5e-3},
+                  {"params": [params[4]], "lr": 1e-3}]
+        opt = Adam(groups, lr=0.0, eps=1e-15)
+        for gr in grads:
+            for p, x in zip(params, gr):
+                p.grad = x.to(DEV)
+            opt.step(relevance=params[2].grad)
+        torch.cuda.synchronize()
+        out[mode] = [t.detach().clone() for p in params
+                     for t in (p, opt.state[p]["exp_avg"], opt.state[p]["exp_avg_sq"])]
+    for a, b in zip(out["0"], out["1"]):
+        assert torch.equal(a, b)
