@@ -56,6 +56,18 @@ int gsr_l1_ssim_forward_with_map(const float *img, const float *gt, int C, int H
 int gsr_l1_ssim_backward_from_map(const float *img, const float *gt, const float *ssim_grad_map, int C, int H, int W,
                                   const float *dL_dout, float *dL_dimg, void *stream);
 
+/* The whole photometric loss of train_single.py:121-123,
+ *   loss = (1 - lambda_dssim) * L1 + lambda_dssim * (1 - SSIM),
+ * as one autograd node: _forward writes out3 = (L1, SSIM, loss) (the combination in torch's fp32
+ * op order) and the SSIM gradient field; _backward takes the scalar dL/dloss (device pointer) and
+ * forms the pair torch's backward of that expression would hand to gsr_l1_ssim_backward_from_map,
+ * bit for bit.  Replaces the ~10 one-element torch launches of the composed expression and its
+ * backward.  lambda_dssim in [0, 1]. */
+int gsr_photo_loss_forward(const float *img, const float *gt, int C, int H, int W, double lambda_dssim, void *scratch,
+                           float *out3, float *ssim_grad_map, void *stream);
+int gsr_photo_loss_backward(const float *img, const float *gt, const float *ssim_grad_map, int C, int H, int W,
+                            double lambda_dssim, const float *dL_dloss, float *dL_dimg, void *stream);
+
 /* One parameter group of the sparse Adam step: a (P, width) row-major parameter with its grad
  * and moment buffers.  step_size = lr / (1 - beta1^step) and bias_correction2_sqrt =
  * sqrt(1 - beta2^step) are computed by the host in double, exactly as OurAdam does. */
@@ -74,7 +86,8 @@ typedef struct {
 } gsr_adam_group;
 
 /* Rows r with relevance[r] != 0 are updated in every group; if no row is relevant, every row
- * is updated (OurAdam's _single_tensor_adam2 branch).  flag_scratch: one device int. */
+ * is updated (OurAdam's _single_tensor_adam2 branch).  flag_scratch: one device int.
+ * relevance NULL: a dense step over every row (one launch; flag_scratch unused). */
 int gsr_sparse_adam_step(int n_groups, const gsr_adam_group *groups, int64_t P, const float *relevance,
                          double beta1, double beta2, double eps, int *flag_scratch, void *stream);
 

@@ -224,7 +224,8 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_fwd_kernel(const float *
 }
 
 __global__ __launch_bounds__(1024) void loss_finalize_kernel(const float2 *__restrict__ partials, int n, double inv_n,
-                                                             float *__restrict__ out) {
+                                                             float *__restrict__ out, float w_l1,
+                                                             float w_ssim) {
     __shared__ double s1[1024], s2[1024];
     double a = 0.0, b = 0.0;
     for (int i = threadIdx.x; i < n; i += 1024) {
@@ -244,6 +245,9 @@ __global__ __launch_bounds__(1024) void loss_finalize_kernel(const float2 *__res
     if (threadIdx.x == 0) {
         out[0] = (float)(s1[0] * inv_n);
         out[1] = (float)(s2[0] * inv_n);
+        // photo loss (train_single.py:121-123) in torch's fp32 op order: (1-l) * L1 + l * (1 - SSIM)
+        if (w_l1 >= 0.f)
+            out[2] = __fadd_rn(__fmul_rn(w_l1, out[0]), __fmul_rn(w_ssim, __fsub_rn(1.f, out[1])));
     }
 }
 
@@ -582,11 +586,19 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_stream_kernel(const floa
 }
 
 // dx = (dout[0] sign(x - y) + dout[1] G) / n from the field l1_ssim_grad_kernel<true> stored.
+// Upstream (dL/dL1, dL/dSSIM) scaled by 1/n: from the 2-vector dout, or (photo loss, w_l1 >= 0)
+// from the scalar dL/dloss as torch's backward of (1-l) * L1 + l * (1 - SSIM) forms them.
+__device__ __forceinline__ float2 loss_upstream(const float *dout, float inv_n, float w_l1, float w_ssim) {
+    if (w_l1 >= 0.f) return make_float2((w_l1 * dout[0]) * inv_n, (-(w_ssim * dout[0])) * inv_n);
+    return make_float2(dout[0] * inv_n, dout[1] * inv_n);
+}
+
 __global__ __launch_bounds__(256) void l1_ssim_bwd_map_kernel(const float4 *__restrict__ x, const float4 *__restrict__ y,
                                                               const float4 *__restrict__ G, int64_t n4,
                                                               const float *__restrict__ dout, float inv_n,
-                                                              float4 *__restrict__ dx) {
-    const float g_l1 = dout[0] * inv_n, g_ssim = dout[1] * inv_n;
+                                                              float4 *__restrict__ dx, float w_l1, float w_ssim) {
+    const float2 up = loss_upstream(dout, inv_n, w_l1, w_ssim);
+    const float g_l1 = up.x, g_ssim = up.y;
     const auto one = [&](float xv, float yv, float gv) {
         const float d = xv - yv;
         const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
@@ -602,10 +614,12 @@ __global__ __launch_bounds__(256) void l1_ssim_bwd_map_tail_kernel(const float *
                                                                    const float *__restrict__ y,
                                                                    const float *__restrict__ G, int64_t begin,
                                                                    int64_t n, const float *__restrict__ dout,
-                                                                   float inv_n, float *__restrict__ dx) {
+                                                                   float inv_n, float *__restrict__ dx, float w_l1,
+                                                                   float w_ssim) {
     const int64_t i = begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const float g_l1 = dout[0] * inv_n, g_ssim = dout[1] * inv_n;
+    const float2 up = loss_upstream(dout, inv_n, w_l1, w_ssim);
+    const float g_l1 = up.x, g_ssim = up.y;
     const float d = x[i] - y[i];
     const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
     dx[i] = g_l1 * sgn + g_ssim * G[i];
@@ -664,7 +678,7 @@ __global__ __launch_bounds__(kAdamThreads) void sparse_adam_kernel(AdamArgs a, c
     const gsr_adam_group &G = a.g[gi];
     const int64_t e = ((int64_t)blockIdx.x - a.block_start[gi]) * kAdamThreads + threadIdx.x;
     if (e >= P * G.width) return;
-    const bool dense = *flag == 0;
+    const bool dense = flag == nullptr || *flag == 0;  // no relevance given, or no relevant row
     switch (G.width) {
         case 1: adam_element<1>(G, e, rel, dense, b1, b2, omb1, omb2, eps); break;
         case 3: adam_element<3>(G, e, rel, dense, b1, b2, omb1, omb2, eps); break;
@@ -700,7 +714,7 @@ __global__ __launch_bounds__(kAdamThreads) void sparse_adam_rows_kernel(AdamArgs
     const int64_t r0 = (((int64_t)blockIdx.x * kAdamThreads + threadIdx.x) >> 6) * 64;
     if (r0 >= P) return;  // wave-uniform
     const int64_t row = r0 + lane;
-    const bool dense = *flag == 0;
+    const bool dense = flag == nullptr || *flag == 0;  // no relevance given, or no relevant row
     const bool relv = row < P && (dense || rel[row] != 0.f);
     const uint64_t mask = __ballot(relv);
     if (mask == 0) return;
@@ -920,7 +934,8 @@ int gsr_l1_ssim_forward(const float *img, const float *gt, int C, int H, int W, 
     const int nb = (int)(g.x * g.y * g.z);
     float2 *part = static_cast<float2 *>(scratch);
     hipLaunchKernelGGL(l1_ssim_fwd_kernel, g, dim3(kLossThreads), kFwdLds, s, img, gt, H, W, ssim_window(), part);
-    hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(1024), 0, s, part, nb, 1.0 / ((double)C * H * W), out);
+    hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(1024), 0, s, part, nb, 1.0 / ((double)C * H * W), out,
+                       -1.f, 0.f);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_last_error(std::string("gsr_l1_ssim_forward: ") + hipGetErrorString(e));
@@ -952,10 +967,15 @@ int gsr_l1_ssim_backward(const float *img, const float *gt, int C, int H, int W,
     return GSR_OK;
 }
 
-int gsr_l1_ssim_forward_with_map(const float *img, const float *gt, int C, int H, int W, void *scratch, float *out,
-                                 float *ssim_grad_map, void *stream) {
+}  // extern "C"
+
+namespace {
+
+// w_l1 < 0: out = (L1, SSIM); else also out[2] = the photo loss with weights (w_l1, w_ssim)
+int forward_with_map(const char *who, const float *img, const float *gt, int C, int H, int W, void *scratch,
+                     float *out, float *ssim_grad_map, float w_l1, float w_ssim, void *stream) {
     if (C <= 0 || H <= 0 || W <= 0 || !img || !gt || !scratch || !out || !ssim_grad_map) {
-        set_last_error("gsr_l1_ssim_forward_with_map: empty image or NULL pointer");
+        set_last_error(std::string(who) + ": empty image or NULL pointer");
         return GSR_ERR_INVALID_ARGUMENT;
     }
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -970,19 +990,20 @@ int gsr_l1_ssim_forward_with_map(const float *img, const float *gt, int C, int H
     else
         hipLaunchKernelGGL(l1_ssim_stream_kernel<true>, g, dim3(kLossThreads), 0, s, img, gt, H, W, ssim_window(),
                            nullptr, 0.f, ssim_grad_map, part);
-    hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(1024), 0, s, part, nb, 1.0 / ((double)C * H * W), out);
+    hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(1024), 0, s, part, nb, 1.0 / ((double)C * H * W), out,
+                       w_l1, w_ssim);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
-        set_last_error(std::string("gsr_l1_ssim_forward_with_map: ") + hipGetErrorString(e));
+        set_last_error(std::string(who) + ": " + hipGetErrorString(e));
         return GSR_ERR_DEVICE;
     }
     return GSR_OK;
 }
 
-int gsr_l1_ssim_backward_from_map(const float *img, const float *gt, const float *ssim_grad_map, int C, int H, int W,
-                                  const float *dL_dout, float *dL_dimg, void *stream) {
+int backward_from_map(const char *who, const float *img, const float *gt, const float *ssim_grad_map, int C, int H,
+                      int W, const float *dL_dout, float w_l1, float w_ssim, float *dL_dimg, void *stream) {
     if (C <= 0 || H <= 0 || W <= 0 || !img || !gt || !ssim_grad_map || !dL_dout || !dL_dimg) {
-        set_last_error("gsr_l1_ssim_backward_from_map: empty image or NULL pointer");
+        set_last_error(std::string(who) + ": empty image or NULL pointer");
         return GSR_ERR_INVALID_ARGUMENT;
     }
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -996,24 +1017,63 @@ int gsr_l1_ssim_backward_from_map(const float *img, const float *gt, const float
         hipLaunchKernelGGL(l1_ssim_bwd_map_kernel, dim3(blocks), dim3(256), 0, s,
                            reinterpret_cast<const float4 *>(img), reinterpret_cast<const float4 *>(gt),
                            reinterpret_cast<const float4 *>(ssim_grad_map), n4, dL_dout, inv_n,
-                           reinterpret_cast<float4 *>(dL_dimg));
+                           reinterpret_cast<float4 *>(dL_dimg), w_l1, w_ssim);
     }
     if (4 * n4 < n) {
         const int64_t rest = n - 4 * n4;
         hipLaunchKernelGGL(l1_ssim_bwd_map_tail_kernel, dim3((unsigned)((rest + 255) / 256)), dim3(256), 0, s, img, gt,
-                           ssim_grad_map, 4 * n4, n, dL_dout, inv_n, dL_dimg);
+                           ssim_grad_map, 4 * n4, n, dL_dout, inv_n, dL_dimg, w_l1, w_ssim);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
-        set_last_error(std::string("gsr_l1_ssim_backward_from_map: ") + hipGetErrorString(e));
+        set_last_error(std::string(who) + ": " + hipGetErrorString(e));
         return GSR_ERR_DEVICE;
     }
     return GSR_OK;
 }
 
+bool bad_lambda(const char *who, double lambda_dssim) {
+    if (!(lambda_dssim >= 0.0 && lambda_dssim <= 1.0)) {
+        set_last_error(std::string(who) + ": lambda_dssim outside [0, 1]");
+        return true;
+    }
+    return false;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gsr_l1_ssim_forward_with_map(const float *img, const float *gt, int C, int H, int W, void *scratch, float *out,
+                                 float *ssim_grad_map, void *stream) {
+    return forward_with_map("gsr_l1_ssim_forward_with_map", img, gt, C, H, W, scratch, out, ssim_grad_map, -1.f, 0.f,
+                            stream);
+}
+
+int gsr_l1_ssim_backward_from_map(const float *img, const float *gt, const float *ssim_grad_map, int C, int H, int W,
+                                  const float *dL_dout, float *dL_dimg, void *stream) {
+    return backward_from_map("gsr_l1_ssim_backward_from_map", img, gt, ssim_grad_map, C, H, W, dL_dout, -1.f, 0.f,
+                             dL_dimg, stream);
+}
+
+int gsr_photo_loss_forward(const float *img, const float *gt, int C, int H, int W, double lambda_dssim, void *scratch,
+                           float *out3, float *ssim_grad_map, void *stream) {
+    if (bad_lambda("gsr_photo_loss_forward", lambda_dssim)) return GSR_ERR_INVALID_ARGUMENT;
+    // torch applies the python floats (1 - lambda) and lambda as fp32 scalars
+    return forward_with_map("gsr_photo_loss_forward", img, gt, C, H, W, scratch, out3, ssim_grad_map,
+                            (float)(1.0 - lambda_dssim), (float)lambda_dssim, stream);
+}
+
+int gsr_photo_loss_backward(const float *img, const float *gt, const float *ssim_grad_map, int C, int H, int W,
+                            double lambda_dssim, const float *dL_dloss, float *dL_dimg, void *stream) {
+    if (bad_lambda("gsr_photo_loss_backward", lambda_dssim)) return GSR_ERR_INVALID_ARGUMENT;
+    return backward_from_map("gsr_photo_loss_backward", img, gt, ssim_grad_map, C, H, W, dL_dloss,
+                             (float)(1.0 - lambda_dssim), (float)lambda_dssim, dL_dimg, stream);
+}
+
 int gsr_sparse_adam_step(int n_groups, const gsr_adam_group *groups, int64_t P, const float *relevance,
                          double beta1, double beta2, double eps, int *flag_scratch, void *stream) {
-    if (n_groups < 0 || n_groups > kMaxGroups || P < 0 || (P > 0 && (!groups || !relevance || !flag_scratch))) {
+    if (n_groups < 0 || n_groups > kMaxGroups || P < 0 || (P > 0 && (!groups || (relevance && !flag_scratch)))) {
         set_last_error("gsr_sparse_adam_step: bad group count or NULL pointer");
         return GSR_ERR_INVALID_ARGUMENT;
     }
@@ -1040,18 +1100,22 @@ int gsr_sparse_adam_step(int n_groups, const gsr_adam_group *groups, int64_t P, 
         set_last_error("gsr_sparse_adam_step: parameter set too large for one launch");
         return GSR_ERR_UNSUPPORTED;
     }
-    (void)hipMemsetAsync(flag_scratch, 0, sizeof(int), s);
-    hipLaunchKernelGGL(any_nonzero_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, relevance, P,
-                       flag_scratch);
+    // relevance NULL: a dense step (torch.optim.Adam over every row), one launch
+    int *flag = relevance ? flag_scratch : nullptr;
+    if (relevance) {
+        (void)hipMemsetAsync(flag_scratch, 0, sizeof(int), s);
+        hipLaunchKernelGGL(any_nonzero_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, relevance, P,
+                           flag_scratch);
+    }
     // torch applies python-float hyper-parameters as fp32 scalars: b, (1 - b) rounded from double
     if (!adam_elementwise())
         hipLaunchKernelGGL(sparse_adam_rows_kernel, dim3((unsigned)((P + kAdamThreads - 1) / kAdamThreads)),
                            dim3(kAdamThreads), 0, s, a, relevance, P, (float)beta1, (float)beta2,
-                           (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps, flag_scratch);
+                           (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps, flag);
     else
         hipLaunchKernelGGL(sparse_adam_kernel, dim3((unsigned)blocks), dim3(kAdamThreads), 0, s, a, relevance, P,
                            (float)beta1, (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps,
-                           flag_scratch);
+                           flag);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_last_error(std::string("gsr_sparse_adam_step: ") + hipGetErrorString(e));

@@ -140,6 +140,17 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     return int(K.value), out_color, out_invdepth, radii, res.get("geom"), res.get("binning"), res.get("image")
 
 
+_ZEROS = {}
+
+
+def _zero(dev):
+    """One cached zero per device: the source of the zero-stride gradient views below."""
+    z = _ZEROS.get(dev)
+    if z is None:
+        z = _ZEROS[dev] = torch.zeros(1, dtype=torch.float32, device=dev)
+    return z
+
+
 def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier,
                                  cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color,
                                  dL_dout_invdepth, sh, degree, campos, geomBuffer, R, binningBuffer, imageBuffer,
@@ -162,7 +173,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     e = lambda *shape: torch.empty(*shape, dtype=torch.float32, device=dev)
     # gradients of inputs that were not given are identically zero: returned as zero-stride views
     # (upstream's shapes, no memory traffic) and not computed by the kernels
-    z = lambda *shape: torch.zeros(1, dtype=torch.float32, device=dev).expand(*shape)
+    z = lambda *shape: _zero(dev).expand(*shape)
     dL_dmeans2D, dL_dopacity, dL_dmeans3D = e(P, 3), e(P, 1), e(P, 3)
     dL_dcolors = e(P, 3) if sh_c is None else z(P, 3)
     dL_dcov3D = e(P, 6) if cov_c is not None else z(P, 6)

@@ -62,6 +62,9 @@ class _RasterizeGaussians(torch.autograd.Function):
             num_rendered, color, invdepth, radii, geomBuffer, binningBuffer, imgBuffer = _C.rasterize_gaussians(*args)
 
         ctx.raster_settings = rs
+        # an output no loss uses (the inverse depth, in most training steps) arrives as None, not
+        # as a materialised zero image: no fill launch, and the backward skips its depth term
+        ctx.set_materialize_grads(False)
         ctx.num_rendered = num_rendered
         ctx.do_depth = do_depth
         ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer,

@@ -51,6 +51,8 @@ SIGNATURES = {
     "gsr_l1_ssim_backward": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp, _vp]),
     "gsr_l1_ssim_forward_with_map": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp]),
     "gsr_l1_ssim_backward_from_map": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp]),
+    "gsr_photo_loss_forward": (_i, [_vp, _vp, _i, _i, _i, ctypes.c_double, _vp, _vp, _vp, _vp]),
+    "gsr_photo_loss_backward": (_i, [_vp, _vp, _vp, _i, _i, _i, ctypes.c_double, _vp, _vp, _vp]),
     "gsr_sparse_adam_step": (_i, [_i, ctypes.POINTER(AdamGroup), _i64, _vp, ctypes.c_double, ctypes.c_double,
                                   ctypes.c_double, _vp, _vp]),
     "gsr_densify_stats": (_i, [_i64, _vp, _vp, _vp, _vp, _vp, _vp]),

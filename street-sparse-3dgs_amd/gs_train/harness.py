@@ -157,12 +157,18 @@ class TrainStep:
         groups = gaussians.param_groups()
         self.optimizer = Adam(groups, lr=0.0, eps=1e-15) if fused else baseline.OurAdamTorch(groups, lr=0.0,
                                                                                               eps=1e-15)
-        self.exposure_optimizer = torch.optim.Adam([gaussians._exposure])
+        # the reference's torch.optim.Adam on the exposures; fused: the same update as one dense
+        # launch of the fused kernel (OurAdam's arithmetic: exp_avg by mul + add where torch's
+        # foreach Adam lerps -- an ulp-level difference on 12 floats per image)
+        self.exposure_optimizer = (Adam([gaussians._exposure], lr=1e-3, eps=1e-8) if fused
+                                   else torch.optim.Adam([gaussians._exposure]))
         self.xyz_lr = lambda it: expon_lr(it, LR["position_lr_init"] * gaussians.spatial_lr_scale,
                                           LR["position_lr_final"] * gaussians.spatial_lr_scale,
                                           lr_delay_mult=LR["position_lr_delay_mult"],
                                           max_steps=LR["position_lr_max_steps"])
         self.iteration = 1
+        self._means2D = None
+        self._one = None
         self.empty_i = torch.empty(0, dtype=torch.int32)
         self.empty_f = torch.empty(0, device=dev)
         self.empty_id = torch.empty(0, dtype=torch.int32, device=dev)
@@ -175,9 +181,17 @@ class TrainStep:
             viewmatrix=c["view"], projmatrix=c["proj"], sh_degree=g.active_sh_degree, campos=c["campos"],
             prefiltered=False, debug=False, do_depth=True, render_indices=self.empty_i, parent_indices=self.empty_i,
             interpolation_weights=self.empty_f, num_node_kids=self.empty_id)
-        means2D = torch.zeros_like(g._xyz, requires_grad=True) + 0
-        if means2D.requires_grad:
-            means2D.retain_grad()
+        if self.fused:
+            # the rasterizer never reads means2D's values (it only carries dL/dmeans2D): one
+            # zero leaf per Gaussian count, its .grad reset each step, instead of zeros + 0
+            if self._means2D is None or self._means2D.shape != g._xyz.shape:
+                self._means2D = torch.zeros_like(g._xyz, requires_grad=True)
+            means2D = self._means2D
+            means2D.grad = None
+        else:
+            means2D = torch.zeros_like(g._xyz, requires_grad=True) + 0
+            if means2D.requires_grad:
+                means2D.retain_grad()
         if self.fused:
             scales, rotations, opacities = activate(g._scaling, g._rotation, g._opacity)
         else:
@@ -208,7 +222,12 @@ class TrainStep:
             loss = baseline.photo_loss(image, gt, LR["lambda_dssim"])
         if self.mono is not None and self.depth_w > 0:
             loss = loss + self.depth_w * torch.abs(invd - self.mono[k]).mean()
-        loss.backward()
+        if self.fused:
+            if self._one is None:
+                self._one = torch.ones((), device=loss.device)
+            loss.backward(self._one)  # = loss.backward() without the ones_like fill launch
+        else:
+            loss.backward()
         with torch.no_grad():
             if self.fused:
                 add_densification_stats(radii, means2D.grad, g.max_radii2D, g.xyz_gradient_accum, g.denom)

@@ -67,8 +67,53 @@ def l1_ssim(img: torch.Tensor, gt: torch.Tensor) -> torch.Tensor:
     return _L1SSIM.apply(img, gt)
 
 
+class _PhotoLoss(torch.autograd.Function):
+    """loss = (1 - lambda) L1 + lambda (1 - SSIM) as ONE node (include/gsr_train.h
+    gsr_photo_loss_*): the same values and gradient bits as composing l1_ssim with torch's scalar
+    ops, without their one-element launches.  L1 and SSIM come back as non-differentiable
+    by-products (the reference uses Ll1 only for its progress bar)."""
+
+    @staticmethod
+    def forward(ctx, img, gt, lambda_dssim):
+        require_gpu(img, gt)
+        if img.shape != gt.shape:
+            raise ValueError(f"image shapes differ: {tuple(img.shape)} vs {tuple(gt.shape)}")
+        img = img.detach().float().contiguous()
+        gt = gt.detach().float().contiguous()
+        C, H, W = _planes(img)
+        L = lib()
+        out = torch.empty(3, dtype=torch.float32, device=img.device)
+        scratch = torch.empty(max(1, L.gsr_l1_ssim_scratch_bytes(C, H, W)), dtype=torch.uint8, device=img.device)
+        gmap = torch.empty_like(img)
+        check(L.gsr_photo_loss_forward(ptr(img), ptr(gt), C, H, W, float(lambda_dssim), ptr(scratch), ptr(out),
+                                       ptr(gmap), stream(img.device)), "gsr_photo_loss_forward")
+        ctx.save_for_backward(img, gt, gmap)
+        ctx.dims = (C, H, W)
+        ctx.lambda_dssim = float(lambda_dssim)
+        ctx.set_materialize_grads(False)
+        loss, l1, s = out[2], out[0], out[1]
+        ctx.mark_non_differentiable(l1, s)
+        return loss, l1, s
+
+    @staticmethod
+    def backward(ctx, gloss, _gl1, _gs):
+        if gloss is None:
+            return None, None, None
+        img, gt, gmap = ctx.saved_tensors
+        C, H, W = ctx.dims
+        gloss = gloss.float().contiguous()
+        dimg = torch.empty_like(img)
+        check(lib().gsr_photo_loss_backward(ptr(img), ptr(gt), ptr(gmap), C, H, W, ctx.lambda_dssim, ptr(gloss),
+                                            ptr(dimg), stream(img.device)), "gsr_photo_loss_backward")
+        return dimg, None, None
+
+
 def photo_loss(img: torch.Tensor, gt: torch.Tensor, lambda_dssim: float = 0.2):
-    """(1 - lambda) L1 + lambda (1 - SSIM)  (train_single.py:121-123); returns (loss, l1, ssim)."""
+    """(1 - lambda) L1 + lambda (1 - SSIM)  (train_single.py:121-123); returns (loss, l1, ssim).
+    With a gradient wanted for img: one fused node (_PhotoLoss); otherwise l1_ssim's forward and
+    the same expression."""
+    if torch.is_grad_enabled() and img.requires_grad:
+        return _PhotoLoss.apply(img, gt, lambda_dssim)
     v = l1_ssim(img, gt)
     l1, s = v[0], v[1]
     return (1.0 - lambda_dssim) * l1 + lambda_dssim * (1.0 - s), l1, s

@@ -113,10 +113,11 @@ class Adam(torch.optim.Optimizer):
             if rel.numel() != P:
                 raise ValueError("relevance must have one value per row")
             rel = rel.float().contiguous()
-        else:
+        elif relevant is not None and relevant.numel() > 0:
             rel = torch.zeros(P, dtype=torch.float32, device=dev)
-            if relevant is not None and relevant.numel() > 0:
-                rel.index_fill_(0, relevant.to(dev).flatten().long(), 1.0)
+            rel.index_fill_(0, relevant.to(dev).flatten().long(), 1.0)
+        else:
+            rel = None  # no relevant row given: the dense update, as OurAdam's fallback branch
         check(lib().gsr_sparse_adam_step(len(entries), groups, P, ptr(rel), betas[0], betas[1], eps,
                                          ptr(self._flag_for(dev)), stream(dev)), "gsr_sparse_adam_step")
         return loss

@@ -337,3 +337,24 @@ def test_sparse_adam_row_blocks_equal_elementwise(frac, monkeypatch):
                      for t in (p, opt.state[p]["exp_avg"], opt.state[p]["exp_avg_sq"])]
     for a, b in zip(out["0"], out["1"]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("lam,scale", [(0.2, 1.0), (0.35, 2.5)])
+def test_photo_loss_fused_equals_composed(lam, scale):
+    """gsr_photo_loss_* (one autograd node) against l1_ssim composed with torch's scalar ops as
+    train_single.py:121-123 writes it: loss, L1, SSIM and the image gradient bit for bit, also
+    for an upstream dL/dloss != 1."""
+    from gs_train import l1_ssim, photo_loss
+    g = torch.Generator().manual_seed(17)
+    img = torch.rand(3, 211, 333, generator=g).to(DEV)
+    gt = torch.rand(3, 211, 333, generator=g).to(DEV)
+    x1 = img.clone().requires_grad_(True)
+    loss, l1, s = photo_loss(x1, gt, lam)
+    (scale * loss).backward()
+    x2 = img.clone().requires_grad_(True)
+    v = l1_ssim(x2, gt)
+    loss2 = (1.0 - lam) * v[0] + lam * (1.0 - v[1])
+    (scale * loss2).backward()
+    assert torch.equal(loss, loss2) and torch.equal(l1, v[0].detach()) and torch.equal(s, v[1].detach())
+    assert torch.equal(x1.grad, x2.grad)
+    assert not l1.requires_grad and not s.requires_grad
