@@ -349,6 +349,9 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
 #ifndef GSR_BWD_PREFETCH
 #define GSR_BWD_PREFETCH 0
 #endif
+#ifndef GSR_BWD_RS
+#define GSR_BWD_RS 1  // per-instance sums as a 16-lane reduce-scatter (wave_rs10)
+#endif
 #ifndef GSR_REC_PAD
 #define GSR_REC_PAD 1  // write the unused 4th float4 of a 64-B record (full 64-B segments)
 #endif
@@ -419,6 +422,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
         boundary[tile] = bkey;
     }
     const float sx = 0.5f * (float)W, sy = 0.5f * (float)H;
+    const int rs_slot = wave_rs10_slot(lane);
+    (void)rs_slot;
 
     for (int hi = (int)maxlast; hi > 0; hi -= kWave) {
         const int n = hi < kWave ? hi : kWave;
@@ -559,6 +564,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
 #endif
             // Half-wave sums only (5 DPP stages); lanes 16 and 48 park the two partials in LDS
             // and they are added once per batch below instead of per instance.
+#if GSR_BWD_RS
+            // reduce-scatter: lane `rs_slot` of rows 1 and 3 parks its half-wave partial
+            const float h = __any(any) ? wave_rs10(q, lane) : 0.f;
+            if ((lane & 16) && rs_slot >= 0)
+                reinterpret_cast<float *>(s_red)[(j * 2 + (lane >> 5)) * 10 + rs_slot] = h;
+#else
 #if GSR_BWD_ALWAYS_REDUCE
             (void)any;
             wave_halfsum<kDepth ? 10 : 9>(q);
@@ -570,6 +581,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
 #pragma unroll
                 for (int t = 0; t < 5; t++) d[t] = make_float2(q[2 * t], (kDepth || t < 4) ? q[2 * t + 1] : 0.f);
             }
+#endif
         }
         __syncthreads();
         if ((uint32_t)lane < cnt) {
