@@ -27,6 +27,14 @@ CFLAGS = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-ffp-contract
           "-Wno-unused-result", "-I", CSRC, "-I", os.path.join(REPO, "include")]
 
 
+# Per-file extra flags.  render.hip: the SLP vectoriser pairs the backward's per-pixel
+# accumulations into v_pk_fma/add_f32 fed by v_mov_b32 shuffles -- packed fp32 has no throughput
+# gain on gfx950, so the moves (4 per pixel, 16 per instance) are pure overhead.
+FILE_FLAGS = {"render.hip": ["-fno-slp-vectorize"]}
+for _f in filter(None, os.environ.get("GSR_NOSLP_FILES", "").split(",")):  # measurement variants
+    FILE_FLAGS[_f] = ["-fno-slp-vectorize"]
+
+
 def _headers():
     return glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(REPO, "include", "*.h"))
 
@@ -41,7 +49,8 @@ def _stale(target, deps):
 def _compile(src, force, objdir=OBJ, defines=()):
     obj = os.path.join(objdir, os.path.basename(src) + ".o")
     if force or _stale(obj, [src] + _headers()):
-        cmd = [HIPCC] + CFLAGS + ["-D" + d for d in defines] + ["-c", src, "-o", obj + ".tmp"]
+        cmd = [HIPCC] + CFLAGS + FILE_FLAGS.get(os.path.basename(src), []) + ["-D" + d for d in defines] + \
+            ["-c", src, "-o", obj + ".tmp"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
@@ -52,8 +61,10 @@ def _compile(src, force, objdir=OBJ, defines=()):
 def build(force: bool = False, jobs: int = 4, defines=(), lib: str = LIB) -> str:
     """Build the library; `defines` (NAME or NAME=VALUE) with a different `lib` path builds a
     measurement variant in its own object directory (load it with GSR_LIBRARY=path)."""
-    objdir = OBJ if not defines else os.path.join(PKG_ROOT, "build", "obj_" + "_".join(
-        d.replace("=", "-") for d in defines))
+    tag = [d.replace("=", "-") for d in defines]
+    if os.environ.get("GSR_NOSLP_FILES"):
+        tag.append("noslp-" + os.environ["GSR_NOSLP_FILES"].replace(",", "-"))
+    objdir = OBJ if not tag else os.path.join(PKG_ROOT, "build", "obj_" + "_".join(tag))
     os.makedirs(objdir, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
