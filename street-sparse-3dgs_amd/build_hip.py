@@ -29,8 +29,9 @@ CFLAGS = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-ffp-contract
 
 # Per-file extra flags.  render.hip: the SLP vectoriser pairs the backward's per-pixel
 # accumulations into v_pk_fma/add_f32 fed by v_mov_b32 shuffles -- packed fp32 has no throughput
-# gain on gfx950, so the moves (4 per pixel, 16 per instance) are pure overhead.
-FILE_FLAGS = {"render.hip": ["-fno-slp-vectorize"]}
+# gain on gfx950, so the moves (4 per pixel, 16 per instance) are pure overhead: render_bwd
+# 0.260 -> 0.246 ms.  train.hip (the SSIM passes): train step -1%.
+FILE_FLAGS = {"render.hip": ["-fno-slp-vectorize"], "train.hip": ["-fno-slp-vectorize"]}
 for _f in filter(None, os.environ.get("GSR_NOSLP_FILES", "").split(",")):  # measurement variants
     FILE_FLAGS[_f] = ["-fno-slp-vectorize"]
 
