@@ -34,6 +34,8 @@ CFLAGS = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-ffp-contract
 FILE_FLAGS = {"render.hip": ["-fno-slp-vectorize"], "train.hip": ["-fno-slp-vectorize"]}
 for _f in filter(None, os.environ.get("GSR_NOSLP_FILES", "").split(",")):  # measurement variants
     FILE_FLAGS[_f] = ["-fno-slp-vectorize"]
+if os.environ.get("GSR_RENDER_FLAGS"):  # measurement variants: extra flags for render.hip
+    FILE_FLAGS["render.hip"] = FILE_FLAGS["render.hip"] + os.environ["GSR_RENDER_FLAGS"].split()
 
 
 def _headers():
@@ -65,6 +67,8 @@ def build(force: bool = False, jobs: int = 4, defines=(), lib: str = LIB) -> str
     tag = [d.replace("=", "-") for d in defines]
     if os.environ.get("GSR_NOSLP_FILES"):
         tag.append("noslp-" + os.environ["GSR_NOSLP_FILES"].replace(",", "-"))
+    if os.environ.get("GSR_RENDER_FLAGS"):
+        tag.append("rf" + "".join(c for c in os.environ["GSR_RENDER_FLAGS"] if c.isalnum()))
     objdir = OBJ if not tag else os.path.join(PKG_ROOT, "build", "obj_" + "_".join(tag))
     os.makedirs(objdir, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
