@@ -225,7 +225,8 @@ __global__ __launch_bounds__(64 * kScatterWaves) void sb_scatter_kernel(int P, S
                                                                          const uint2 *__restrict__ drect,
                                                                          const uint32_t *__restrict__ col,
                                                                          const uint32_t *__restrict__ base_g,
-                                                                         uint2 *__restrict__ sblist) {
+                                                                         uint2 *__restrict__ sblist, uint32_t cap) {
+    if (base_g[sg.nsb] > cap) return;  // the point-list capacity is short: the host re-runs at K
     extern __shared__ uint32_t wc[];  // [W][nsb] per-wave running positions, then [W][nsb] u64 masks
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int nsb = sg.nsb;
@@ -346,7 +347,8 @@ __global__ __launch_bounds__(64 * kTBWaves) void tile_bin_kernel(SBGrid sg, int 
                                                                  const uint32_t *__restrict__ base_i,
                                                                  const uint2 *__restrict__ sblist,
                                                                  uint32_t *__restrict__ point_list,
-                                                                 uint2 *__restrict__ ranges) {
+                                                                 uint2 *__restrict__ ranges, uint32_t cap) {
+    if (base_i[sg.nsb] > cap) return;  // the point-list capacity is short: the host re-runs at K
     __shared__ uint32_t tc[kTBWaves][kMaxTilesPerSB];
     const int s = blockIdx.x;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -462,7 +464,7 @@ void launch_binning_superblocks(int P, const Camera &cam, const GeomState &gs, c
     hipLaunchKernelGGL(sb_colscan_kernel, dim3(sg.nsb), dim3(kColThreads), 0, s, sg, gs.sb_cnt_g, gs.sb_cnt_i,
                        gs.sb_base_g, gs.sb_base_i, dsort_aux_word(gs));
     hipLaunchKernelGGL(sb_scatter_kernel, dim3(sg.nchunks), dim3(64 * kScatterWaves), l3, s, P, sg, gs.order, gs.drect,
-                       gs.sb_cnt_g, gs.sb_base_g, bs.sblist);
+                       gs.sb_cnt_g, gs.sb_base_g, bs.sblist, bs.cap);
 }
 
 void launch_binning_tiles(int P, const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
@@ -475,7 +477,7 @@ void launch_binning_tiles(int P, const Camera &cam, const GeomState &gs, const B
         return;
     }
     hipLaunchKernelGGL(tile_bin_kernel, dim3(sg.nsb), dim3(64 * kTBWaves), 0, s, sg, cam.gx, cam.gy, gs.sb_base_g,
-                       gs.sb_base_i, bs.sblist, bs.point_list, is.ranges);
+                       gs.sb_base_i, bs.sblist, bs.point_list, is.ranges, bs.cap);
 }
 
 }  // namespace gsr

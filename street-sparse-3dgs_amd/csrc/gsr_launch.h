@@ -32,7 +32,8 @@ bool color_split_supported(const GaussianInputs &in);
 void launch_preprocess_color(const GaussianInputs &in, const Camera &cam, const GeomState &gs, const int *radii,
                              hipStream_t s);
 // render.hip: tiles ordered heaviest first by work[t] (or, with work == NULL, by list length).
-void launch_tile_order(const uint32_t *work, const uint2 *ranges, int T, int shift, uint32_t *order, hipStream_t s);
+void launch_tile_order(const uint32_t *work, const uint2 *ranges, int T, int shift, uint32_t *order, hipStream_t s,
+                       const uint32_t *kdev = nullptr, uint32_t cap = 0);
 void launch_mark_visible(int P, const float *means3D, const float *view, uint8_t *present, hipStream_t s);
 
 // sort.hip (rocPRIM)

@@ -25,6 +25,11 @@ thread_local uint32_t *g_pinned = nullptr;
 thread_local uint32_t *g_pinned_dev = nullptr;
 constexpr int kMaxDevicesK = 64;
 thread_local hipEvent_t g_k_ready[kMaxDevicesK] = {};
+// per device: capacity for the next frame's point list (last K + 1/8 + 4096), 0 = none yet
+thread_local int64_t g_khint[kMaxDevicesK] = {};
+#ifndef GSR_DEFER_K
+#define GSR_DEFER_K 1
+#endif
 constexpr uint32_t kKPending = 0xFFFFFFFFu;
 
 // Stage profiling is process-wide: torch runs the backward on its autograd device thread.
@@ -151,11 +156,15 @@ GeomState carve_geom(void *base, int P, int gx, int gy, size_t *bytes) {
     return g;
 }
 
+// point_list first: the backward re-carves this buffer with num_rendered, which may be smaller
+// than the capacity the forward carved it with.
 BinningState carve_binning(void *base, int64_t K, size_t *bytes) {
     Carver c(base);
     BinningState b;
-    b.sblist = c.take<uint2>(K);
     b.point_list = c.take<uint32_t>(K);
+    b.sblist = c.take<uint2>(K);
+    b.cap = (uint32_t)K;
+    b.kdev = nullptr;
     if (bytes) *bytes = align_up(c.off, 256);
     return b;
 }
@@ -351,8 +360,17 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
         launch_depth_sort(P, gs, g_pinned_dev, s, k_ready);
     }
     if ((rc = check("depth sort", debug, s))) return rc;
+    // K sizes the point list.  With a capacity hint from this device's previous frame the binning
+    // and the forward render are queued first and K is read afterwards (the GPU never waits on
+    // the host's hand-off); kernels that would overrun the capacity exit at once (they compare the
+    // device's K / instance totals with bs.cap) and the frame's binning and render are queued
+    // again at the real K.  Without a hint (first frame, debug) K is read before the binning.
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevicesK)
+        return fail(GSR_ERR_DEVICE, "no current device");
     int64_t K = 0;
-    if (P > 0) {
+    bool have_K = P == 0;
+    auto read_K = [&]() -> int {
         if (hipEventSynchronize(k_ready) != hipSuccess) return fail(GSR_ERR_DEVICE, "num_rendered wait failed");
         uint32_t k = __atomic_load_n(g_pinned, __ATOMIC_SEQ_CST);
         if (k == kKPending) {  // not expected: read the device copy instead
@@ -365,39 +383,59 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
                 return fail(GSR_ERR_DEVICE, "depth sort: a lookback spin timed out");
         }
         K = (int64_t)k;
-    }
+        have_K = true;
+        return GSR_OK;
+    };
+    const bool defer = GSR_DEFER_K && P > 0 && !debug && g_khint[dev] > 0;
+    if (P > 0 && !defer && (rc = read_K())) return rc;
     if (split && GSR_COLOR_FORK == 1 && (rc = fork_color())) return rc;
-    size_t bbytes = 0;
-    carve_binning(nullptr, K, &bbytes);
-    void *bbase = binning_buffer(resize_ctx, bbytes);
-    if (!bbase) return fail(GSR_ERR_ALLOCATION, "binning buffer allocation failed");
-    const BinningState bs = carve_binning(bbase, K, nullptr);
-
-    {
-        StageTimer st(2, s);
-        launch_binning_superblocks(P, cam, gs, bs, is, s);
+    bool joined = false;
+    auto bin_and_render = [&](int64_t cap) -> int {
+        size_t bbytes = 0;
+        carve_binning(nullptr, cap, &bbytes);
+        void *bbase = binning_buffer(resize_ctx, bbytes);
+        if (!bbase) return fail(GSR_ERR_ALLOCATION, "binning buffer allocation failed");
+        BinningState bs = carve_binning(bbase, cap, nullptr);
+        bs.kdev = dsort_K_word(gs);
+        int r;
+        {
+            StageTimer st(2, s);
+            launch_binning_superblocks(P, cam, gs, bs, is, s);
+        }
+        if ((r = check("binning (superblocks)", debug, s))) return r;
+        {
+            StageTimer st(3, s);
+            launch_binning_tiles(P, cam, gs, bs, is, s);
+        }
+        if ((r = check("binning (tiles)", debug, s))) return r;
+        {
+            StageTimer st(4, s);
+            launch_tile_order(nullptr, is.ranges, T, 4, is.tile_ids, s, bs.kdev, bs.cap);  // forward order: by list length
+        }
+        if ((r = check("tile order", debug, s))) return r;
+        if (split && !joined) {
+            sj.pending = false;
+            joined = true;
+            if (hipStreamWaitEvent(s, join, 0) != hipSuccess) return fail(GSR_ERR_DEVICE, "side stream join failed");
+        }
+        {
+            StageTimer st(5, s);
+            launch_render_fwd(cam, gs, bs, is, background, out_color, out_invdepth, s);
+            launch_tile_order(is.tile_work, is.ranges, T, 2, is.tile_order, s, bs.kdev, bs.cap);
+        }
+        return check("render", debug, s);
+    };
+    const int64_t cap0 = defer ? g_khint[dev] : K;
+    if ((rc = bin_and_render(cap0))) return rc;
+    if (!have_K && (rc = read_K())) return rc;
+    if (K > cap0) {  // the capacity was short: again at K
+        // sb_colscan's last-workgroup counter (a depth-sort control word the preprocess zeroes
+        // once per frame) must start from zero again
+        if (hipMemsetAsync(dsort_aux_word(gs), 0, sizeof(uint32_t), s) != hipSuccess)
+            return fail(GSR_ERR_DEVICE, "binning counter reset failed");
+        if ((rc = bin_and_render(K))) return rc;
     }
-    if ((rc = check("binning (superblocks)", debug, s))) return rc;
-    {
-        StageTimer st(3, s);
-        launch_binning_tiles(P, cam, gs, bs, is, s);
-    }
-    if ((rc = check("binning (tiles)", debug, s))) return rc;
-    {
-        StageTimer st(4, s);
-        launch_tile_order(nullptr, is.ranges, T, 4, is.tile_ids, s);  // forward order: by list length
-    }
-    if ((rc = check("tile order", debug, s))) return rc;
-    if (split) {
-        sj.pending = false;
-        if (hipStreamWaitEvent(s, join, 0) != hipSuccess) return fail(GSR_ERR_DEVICE, "side stream join failed");
-    }
-    {
-        StageTimer st(5, s);
-        launch_render_fwd(cam, gs, bs, is, background, out_color, out_invdepth, s);
-        launch_tile_order(is.tile_work, is.ranges, T, 2, is.tile_order, s);
-    }
-    if ((rc = check("render", debug, s))) return rc;
+    if (P > 0) g_khint[dev] = K + K / 8 + 4096;
     if (num_rendered) *num_rendered = K;
     return GSR_OK;
 }

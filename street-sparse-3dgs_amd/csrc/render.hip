@@ -59,7 +59,9 @@ __global__ __launch_bounds__(64) void render_fwd_kernel(
     const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list, int W, int H, int gx,
     const GRec *__restrict__ rec, const float *__restrict__ bg, float *__restrict__ out_color,
     float *__restrict__ out_invd, float *__restrict__ final_T, uint32_t *__restrict__ n_contrib,
-    uint32_t *__restrict__ tile_work, uint32_t *__restrict__ tile_ids) {
+    uint32_t *__restrict__ tile_work, uint32_t *__restrict__ tile_ids, const uint32_t *__restrict__ kdev,
+    uint32_t cap) {
+    if (kdev && *kdev > cap) return;  // the point-list capacity is short: the host re-runs at K
     __shared__ float4 s_a[kWave];  // x, y, conic.a, conic.b
     __shared__ float4 s_b[kWave];  // conic.c, opacity, contributor index, sub-block mask
     __shared__ float4 s_c[kWave];  // r, g, b, 1/depth
@@ -168,7 +170,9 @@ __global__ __launch_bounds__(256) void render_fwd_sb_kernel(
     const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list, int W, int H, int gx,
     const GRec *__restrict__ rec, const float *__restrict__ bg, float *__restrict__ out_color,
     float *__restrict__ out_invd, float *__restrict__ final_T, uint32_t *__restrict__ n_contrib,
-    uint32_t *__restrict__ tile_work, const uint32_t *__restrict__ fwd_order) {
+    uint32_t *__restrict__ tile_work, const uint32_t *__restrict__ fwd_order, const uint32_t *__restrict__ kdev,
+    uint32_t cap) {
+    if (kdev && *kdev > cap) return;  // the point-list capacity is short: the host re-runs at K
     // per wave, three 64-entry planes: {x, y, conic.a, conic.b}, {conic.c, opacity, -, -},
     // {r, g, b, 1/depth}; one base address serves all three (offsets 0 / 1 / 2 KiB)
     __shared__ float4 s_q[4][3][kWave];
@@ -270,7 +274,8 @@ __global__ __launch_bounds__(256) void render_fwd_sb_kernel(
 // 2^shift instances (LDS histogram, scan, scatter).  Order within a class is arbitrary; every
 // tile writes only its own outputs, so results do not depend on it.
 __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t *__restrict__ work, const uint2 *__restrict__ ranges,
-                                                          int T, int shift, uint32_t *__restrict__ order) {
+                                                          int T, int shift, uint32_t *__restrict__ order, const uint32_t *__restrict__ kdev, uint32_t cap) {
+    if (kdev && *kdev > cap) return;  // ranges / work were not written this pass (capacity re-run)
     __shared__ uint32_t hist[256];
     if (threadIdx.x < 256) hist[threadIdx.x] = 0u;
     __syncthreads();
@@ -300,9 +305,10 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t *__rest
     for (int t = threadIdx.x; t < T; t += 1024) order[atomicAdd(&hist[bucket(t)], 1u)] = (uint32_t)t;
 }
 
-void launch_tile_order(const uint32_t *work, const uint2 *ranges, int T, int shift, uint32_t *order, hipStream_t s) {
+void launch_tile_order(const uint32_t *work, const uint2 *ranges, int T, int shift, uint32_t *order, hipStream_t s,
+                       const uint32_t *kdev, uint32_t cap) {
     if (T == 0) return;
-    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, s, work, ranges, T, shift, order);
+    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, s, work, ranges, T, shift, order, kdev, cap);
 }
 
 void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
@@ -312,12 +318,12 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
     if (GSR_FWD_SUBBLOCK) {  // launch order: is.tile_ids (rasterizer.hip, by list length)
         hipLaunchKernelGGL(render_fwd_sb_kernel, dim3(T), dim3(4 * kWave), 0, s, is.ranges, bs.point_list, cam.W,
                            cam.H, cam.gx, gs.rec, bg, out_color, out_invdepth, is.final_T, is.n_contrib, is.tile_work,
-                           is.tile_ids);
+                           is.tile_ids, bs.kdev, bs.cap);
     }
     else
         hipLaunchKernelGGL(render_fwd_kernel, dim3(T), dim3(kWave), 0, s, is.ranges, bs.point_list, cam.W, cam.H,
                            cam.gx, gs.rec, bg, out_color, out_invdepth, is.final_T, is.n_contrib, is.tile_work,
-                           is.tile_ids);
+                           is.tile_ids, bs.kdev, bs.cap);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -30,7 +30,8 @@ def geom_layout(P):
 
 
 def binning_layout(K, T):
-    return carve([("sblist", 8 * K), ("point_list", 4 * K)])
+    # point_list first (csrc/rasterizer.hip carve_binning): the forward may carve a larger capacity
+    return carve([("point_list", 4 * K), ("sblist", 8 * K)])
 
 
 def image_layout(T, npix):
