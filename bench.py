@@ -113,7 +113,23 @@ def cpu_baseline(s, P, W, H, deg, min_seconds=10.0, max_frames=8):
     dt = time.perf_counter() - t0
     return {"value": round(frames * W * H / dt / 1e6, 4), "unit": "Mpix/s", "cores": O.num_threads(), "kind": "port",
             "sample": f"{frames} fwd+bwd frames of the bench workload ({P} Gaussians, {W}x{H}, SH deg {deg}) "
-                      f"through the C oracle, {dt:.2f} s"}
+                      f"through the C oracle, {dt:.2f} s"}, st
+
+
+def psnr_vs_oracle(gpu_color, gpu_invd, st):
+    """BASELINE.json metric part 3: PSNR of the bench frame rendered by the HIP path against the
+    same frame rendered by the CPU oracle (peak 1.0; colour and inverse depth), plus the fraction
+    of pixels off by more than 1e-4."""
+    import numpy as np
+    c = gpu_color.detach().float().cpu().numpy()
+    d = gpu_invd.detach().float().cpu().numpy()
+    mse = float(np.mean((c.astype(np.float64) - st["color"]) ** 2))
+    out = {"psnr_db": round(10 * np.log10(1.0 / mse), 2) if mse > 0 else None,  # None: bit-identical
+           "max_abs_err": float(np.max(np.abs(c - st["color"]))),
+           "frac_pixels_off_1e-4": float(np.mean(np.abs(c - st["color"]) > 1e-4)),
+           "invdepth_rel_l2": float(np.linalg.norm(d - st["invdepth"]) / max(np.linalg.norm(st["invdepth"]), 1e-30)),
+           "reference": "oracle/gs_oracle.c forward of the bench frame (fp32, upstream algorithm restated)"}
+    return out
 
 
 def train_step_ms(s, W, H, deg, steps, warmup, fused, dev):
@@ -346,7 +362,10 @@ def main():
     if a.config5:
         out["config5"] = config5(a, dev)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(s, P, W, H, deg)
+        out["cpu_baseline"], st = cpu_baseline(s, P, W, H, deg)
+        with torch.no_grad():
+            color, _, invd = raster(**inp)
+        out["psnr_vs_oracle"] = psnr_vs_oracle(color, invd, st)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

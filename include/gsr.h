@@ -108,6 +108,16 @@ int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const
 int gsr_set_profiling(int enable);
 int gsr_stage_times_ms(float *out, int max_stages);
 
+/* dL/dscales convention, process-wide.  0 (default): upstream's -- the gradient with respect to
+ * the modified scale scale_modifier * s, reported as dL/ds.  1: the exact derivative dL/ds
+ * (multiplied by scale_modifier; identical when scale_modifier == 1).  Returns the previous mode. */
+int gsr_set_true_scale_gradient(int enable);
+
+/* Forward statistics since load: out[0] = frames rasterized (P > 0), out[1] = frames whose
+ * binning ran twice because the capacity hint from the previous frame was short of K.
+ * Returns the number of values written (<= n). */
+int gsr_forward_stats(int64_t *out, int n);
+
 /* Version / diagnostics. */
 int gsr_abi_version(void);
 const char *gsr_last_error(void);

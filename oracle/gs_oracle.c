@@ -295,13 +295,21 @@ void gso_ranges(unsigned long long K, const unsigned long long *keys, int T, uns
  * p2 > 0 <=> power > 0 up to rounding: the same test upstream applies to power. */
 static const float GS_LOG2E = 1.4426950408889634f;
 static const float GS_HALF_LOG2E = -0.5f * 1.4426950408889634f;
+/* Upstream-formulation mode (gso_set_upstream_exponent(1)): the exponent as the published
+ * renderCUDA writes it, power = -0.5 (a dx^2 + c dy^2) - b dx dy, G = expf(power), with no
+ * base-2 rescaling (compiled with -ffp-contract=off: every product rounded).  The GPU tests bound
+ * the HIP kernels' drift from this formulation (n_contrib flips, image PSNR) -- the exp2 order
+ * above is this build's choice, this one is the reference's. */
+static int g_upstream_exp = 0;
+void gso_set_upstream_exponent(int on) { g_upstream_exp = on ? 1 : 0; }
 static inline float gauss_p2(const float *co, float dx, float dy) {
+    if (g_upstream_exp) return -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
     const float as = co[0] * GS_HALF_LOG2E, bs = co[1] * GS_LOG2E, cs = co[2] * GS_HALF_LOG2E;
     const float adxdx = as * dx * dx;
     const float t = fmaf(cs * dy, dy, adxdx);
     return fmaf(-(bs * dx), dy, t);
 }
-static inline float gexp2(float p2) { return exp2f(p2); }
+static inline float gexp2(float p2) { return g_upstream_exp ? expf(p2) : exp2f(p2); }
 
 /* ------------------------------------------------------------------------------------------
  * Render forward (A9): per tile front-to-back alpha blending, colour + inverse depth.
@@ -455,7 +463,7 @@ void gso_preprocess_bwd(int P, int D, int M, const float *means3D, const int *ra
                         const unsigned char *clamped, const float *scales, const float *rotations,
                         float mod, const float *cov3D /*P*6 as produced in fwd*/, const float *view,
                         const float *proj, const float *campos, int W, int H, float tanx, float tany,
-                        const float *g10, int has_shs, int has_scales,
+                        const float *g10, int has_shs, int has_scales, int true_scale_grad,
                         float *dL_dmeans3D, float *dL_dmeans2D, float *dL_dcolors, float *dL_dopacity,
                         float *dL_dcov3D, float *dL_dsh, float *dL_dscales, float *dL_drots) {
     const float fy = (float)H / (2.0f * tany);
@@ -645,7 +653,9 @@ void gso_preprocess_bwd(int P, int D, int M, const float *means3D, const int *ra
                 for (int cc = 0; cc < 3; cc++)
                     dLL[rr][cc] = 2.f * (G3[rr][0] * R[0][cc] * s[cc] + G3[rr][1] * R[1][cc] * s[cc] + G3[rr][2] * R[2][cc] * s[cc]);
             for (int k = 0; k < 3; k++)
-                dL_dscales[3 * i + k] = mod * (dLL[0][k] * R[0][k] + dLL[1][k] * R[1][k] + dLL[2][k] * R[2][k]);
+                /* upstream returns dL/d(mod s) as dL/ds (no factor mod); true_scale_grad applies it */
+                dL_dscales[3 * i + k] = (true_scale_grad ? mod : 1.0f) *
+                                        (dLL[0][k] * R[0][k] + dLL[1][k] * R[1][k] + dLL[2][k] * R[2][k]);
             float Gr[3][3];
             for (int rr = 0; rr < 3; rr++)
                 for (int cc = 0; cc < 3; cc++) Gr[rr][cc] = dLL[rr][cc] * s[cc];

@@ -129,8 +129,12 @@ def forward(means3D, opacities, view, proj, campos, bg, W, H, tanfovx, tanfovy, 
         n_contrib=n_contrib)
 
 
-def backward(st, dL_dcolor, dL_dinvdepth=None):
-    """Backward from a forward() state.  Returns grads named as the _C backward returns them."""
+def backward(st, dL_dcolor, dL_dinvdepth=None, true_scale_grad=False):
+    """Backward from a forward() state.  Returns grads named as the _C backward returns them.
+
+    dL/dscales follows upstream by default: the gradient with respect to the modified scale
+    (scale_modifier * s), reported as dL/ds.  true_scale_grad=True multiplies in scale_modifier
+    (the exact derivative; what fp64 autograd in dense_torch.py computes)."""
     L = lib()
     P, M, K, W, H = st["P"], st["M"], st["K"], st["W"], st["H"]
     dL_dcolor = _f32(dL_dcolor).reshape(3, H, W)
@@ -158,11 +162,24 @@ def backward(st, dL_dcolor, dL_dinvdepth=None):
                          ctypes.c_float(st["scale_modifier"]), _p(st["cov3D"]), _p(st["view"]), _p(st["proj"]),
                          _p(st["campos"]), ctypes.c_int(W), ctypes.c_int(H), ctypes.c_float(st["tanfovx"]),
                          ctypes.c_float(st["tanfovy"]), _p(g10), ctypes.c_int(int(has_shs)),
-                         ctypes.c_int(int(has_scales)), _p(dm3), _p(dm2), _p(dcol), _p(dop), _p(dcov), _p(dsh),
+                         ctypes.c_int(int(has_scales)), ctypes.c_int(int(true_scale_grad)), _p(dm3), _p(dm2), _p(dcol), _p(dop), _p(dcov), _p(dsh),
                          _p(dsc), _p(drot))
     return dict(dL_dmeans3D=dm3, dL_dmeans2D=dm2, dL_dcolors=dcol, dL_dopacity=dop, dL_dcov3D=dcov,
                 dL_dsh=dsh if has_shs else np.zeros((0,), np.float32), dL_dscales=dsc, dL_drotations=drot,
                 inst=inst[:K], g10=g10)
+
+
+class upstream_exponent:
+    """Context manager: the oracle's render fwd/bwd evaluate the Gaussian as upstream writes it
+    (power = -0.5 (a dx^2 + c dy^2) - b dx dy, expf) instead of the kernels' exp2 order."""
+
+    def __enter__(self):
+        lib().gso_set_upstream_exponent(ctypes.c_int(1))
+        return self
+
+    def __exit__(self, *exc):
+        lib().gso_set_upstream_exponent(ctypes.c_int(0))
+        return False
 
 
 def mark_visible(means3D, view, proj):

@@ -227,7 +227,7 @@ constexpr int kShPitch = 13;  // padded LDS row pitch (float4) of the staged SH 
 __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
     int P, int D, int M, const float *__restrict__ means3D, const int *__restrict__ radii,
     const float *__restrict__ shs, const uint8_t *__restrict__ clamped, const float *__restrict__ scales,
-    const float *__restrict__ rotations, float mod, const float *__restrict__ cov3D_precomp,
+    const float *__restrict__ rotations, float mod, float dscale_mod, const float *__restrict__ cov3D_precomp,
     const float *__restrict__ viewmatrix, const float *__restrict__ projmatrix, const float *__restrict__ campos_p,
     float tanx, float tany, float fx, float fy, int gx, const uint32_t *__restrict__ tiles,
     const GRec *__restrict__ rec, const uint64_t *__restrict__ boundary, BwdScratch sc, GaussianGrads out) {
@@ -478,7 +478,9 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
                                          G3[rr][2] * R.m[2][cc] * s[cc]);
 #pragma unroll
             for (int k = 0; k < 3; k++)
-                ds[k] = mod * (dLL[0][k] * R.m[0][k] + dLL[1][k] * R.m[1][k] + dLL[2][k] * R.m[2][k]);
+                // dscale_mod = 1 (upstream: dL/d(mod s) reported as dL/ds) or mod (the exact
+                // derivative, gsr_set_true_scale_gradient)
+                ds[k] = dscale_mod * (dLL[0][k] * R.m[0][k] + dLL[1][k] * R.m[1][k] + dLL[2][k] * R.m[2][k]);
             float Gr[3][3];
 #pragma unroll
             for (int rr = 0; rr < 3; rr++)
@@ -511,7 +513,8 @@ void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const Ge
     hipLaunchKernelGGL(record_sum_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, cam.gx, radii, gs.tiles,
                        gs.rec, gs.offsets, is.boundary, sc, out.dmeans2D, out.dopacity);
     hipLaunchKernelGGL(preprocess_bwd_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, in.D, in.M, in.means3D,
-                       radii, in.shs, gs.clamped, in.scales, in.rotations, in.scale_modifier, in.cov3D_precomp,
+                       radii, in.shs, gs.clamped, in.scales, in.rotations, in.scale_modifier,
+                       true_scale_gradient() ? in.scale_modifier : 1.0f, in.cov3D_precomp,
                        cam.view, cam.proj, cam.campos, cam.tanx, cam.tany, cam.fx, cam.fy, cam.gx, gs.tiles, gs.rec,
                        is.boundary, sc, out);
 }

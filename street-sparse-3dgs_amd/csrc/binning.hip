@@ -214,6 +214,22 @@ __global__ __launch_bounds__(kColThreads) void sb_colscan_kernel(SBGrid sg, uint
     }
 }
 
+// The lane masks are only ever touched through workgroup-scope atomics: the ORs of step 1 and the
+// reads of steps 2 and 3 address the same LDS words, and with a plain read after the atomic OR the
+// compiler may serve the read from the atomic's own result (that lane's OR alone, without the other
+// lanes' bits -- the hazard that once produced wrong ranks in the depth sort).  An atomic load
+// cannot be forwarded that way; the hardware keeps one wave's LDS operations in order, so it
+// costs no wait beyond the ds_read itself.
+__device__ __forceinline__ void mask_or(uint64_t *m, uint64_t bit) {
+    (void)__hip_atomic_fetch_or(m, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint64_t mask_load(uint64_t *m) {
+    return __hip_atomic_load(m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void mask_clear(uint64_t *m) {
+    __hip_atomic_store(m, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // Level 1, pass 3: stable scatter of (chunk, wave, batch, lane)-ordered Gaussians into the SB
 // lists.  Ranks come from LDS lane masks: every lane ORs its bit into the mask of each SB it
 // covers, its rank in that SB's list is the popcount of the lower lanes, and the highest lane of
@@ -225,8 +241,11 @@ __global__ __launch_bounds__(64 * kScatterWaves) void sb_scatter_kernel(int P, S
                                                                          const uint2 *__restrict__ drect,
                                                                          const uint32_t *__restrict__ col,
                                                                          const uint32_t *__restrict__ base_g,
-                                                                         uint2 *__restrict__ sblist, uint32_t cap) {
-    if (base_g[sg.nsb] > cap) return;  // the point-list capacity is short: the host re-runs at K
+                                                                         uint2 *__restrict__ sblist,
+                                                                         const uint32_t *__restrict__ kdev, uint32_t cap) {
+    // the point-list capacity is short: the host re-runs at K (SB instances <= K, so K <= cap
+    // bounds the level-1 lists too; the same test as every other binning / render kernel)
+    if (*kdev > cap) return;
     extern __shared__ uint32_t wc[];  // [W][nsb] per-wave running positions, then [W][nsb] u64 masks
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int nsb = sg.nsb;
@@ -279,19 +298,19 @@ __global__ __launch_bounds__(64 * kScatterWaves) void sb_scatter_kernel(int P, S
         // 1. masks
 #pragma unroll
         for (int k = 0; k < kSmallSB; k++)
-            if (small && k < f.n) atomicOr(reinterpret_cast<unsigned long long *>(&msk[sb_key(f, k, sg.nsbx)]), 1ull << lane);
+            if (small && k < f.n) mask_or(&msk[sb_key(f, k, sg.nsbx)], 1ull << lane);
         for (uint64_t big = bigs; big; big &= big - 1) {
             const int b = __ffsll((unsigned long long)big) - 1;
             const SBFoot fb = lane_foot(f, b);
             for (int k = lane; k < fb.n; k += 64)
-                atomicOr(reinterpret_cast<unsigned long long *>(&msk[sb_key(fb, k, sg.nsbx)]), 1ull << b);
+                mask_or(&msk[sb_key(fb, k, sg.nsbx)], 1ull << b);
         }
         // 2. ranked writes
 #pragma unroll
         for (int k = 0; k < kSmallSB; k++)
             if (small && k < f.n) {
                 const uint32_t key = sb_key(f, k, sg.nsbx);
-                sblist[run[key] + (uint32_t)__popcll(msk[key] & lt)] = make_uint2(g, sb_local(r, key, sg));
+                sblist[run[key] + (uint32_t)__popcll(mask_load(&msk[key]) & lt)] = make_uint2(g, sb_local(r, key, sg));
             }
         for (uint64_t big = bigs; big; big &= big - 1) {
             const int b = __ffsll((unsigned long long)big) - 1;
@@ -300,7 +319,7 @@ __global__ __launch_bounds__(64 * kScatterWaves) void sb_scatter_kernel(int P, S
             const uint32_t gb = (uint32_t)rl((int)g, b);
             for (int k = lane; k < fb.n; k += 64) {
                 const uint32_t key = sb_key(fb, k, sg.nsbx);
-                sblist[run[key] + (uint32_t)__popcll(msk[key] & ((1ull << b) - 1ull))] = make_uint2(gb, sb_local(rb, key, sg));
+                sblist[run[key] + (uint32_t)__popcll(mask_load(&msk[key]) & ((1ull << b) - 1ull))] = make_uint2(gb, sb_local(rb, key, sg));
             }
         }
         // 3. the highest lane of every mask advances the SB position and clears the mask
@@ -308,10 +327,10 @@ __global__ __launch_bounds__(64 * kScatterWaves) void sb_scatter_kernel(int P, S
         for (int k = 0; k < kSmallSB; k++)
             if (small && k < f.n) {
                 const uint32_t key = sb_key(f, k, sg.nsbx);
-                const uint64_t m = msk[key];
+                const uint64_t m = mask_load(&msk[key]);
                 if (m != 0 && 63 - __clzll((long long)m) == lane) {
                     run[key] += (uint32_t)__popcll(m);
-                    msk[key] = 0ull;
+                    mask_clear(&msk[key]);
                 }
             }
         for (uint64_t big = bigs; big; big &= big - 1) {
@@ -319,10 +338,10 @@ __global__ __launch_bounds__(64 * kScatterWaves) void sb_scatter_kernel(int P, S
             const SBFoot fb = lane_foot(f, b);
             for (int k = lane; k < fb.n; k += 64) {
                 const uint32_t key = sb_key(fb, k, sg.nsbx);
-                const uint64_t m = msk[key];
+                const uint64_t m = mask_load(&msk[key]);
                 if (m != 0 && 63 - __clzll((long long)m) == b) {
                     run[key] += (uint32_t)__popcll(m);
-                    msk[key] = 0ull;
+                    mask_clear(&msk[key]);
                 }
             }
         }
@@ -347,8 +366,9 @@ __global__ __launch_bounds__(64 * kTBWaves) void tile_bin_kernel(SBGrid sg, int 
                                                                  const uint32_t *__restrict__ base_i,
                                                                  const uint2 *__restrict__ sblist,
                                                                  uint32_t *__restrict__ point_list,
-                                                                 uint2 *__restrict__ ranges, uint32_t cap) {
-    if (base_i[sg.nsb] > cap) return;  // the point-list capacity is short: the host re-runs at K
+                                                                 uint2 *__restrict__ ranges,
+                                                                 const uint32_t *__restrict__ kdev, uint32_t cap) {
+    if (*kdev > cap) return;  // the point-list capacity is short: the host re-runs at K
     __shared__ uint32_t tc[kTBWaves][kMaxTilesPerSB];
     const int s = blockIdx.x;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -464,7 +484,7 @@ void launch_binning_superblocks(int P, const Camera &cam, const GeomState &gs, c
     hipLaunchKernelGGL(sb_colscan_kernel, dim3(sg.nsb), dim3(kColThreads), 0, s, sg, gs.sb_cnt_g, gs.sb_cnt_i,
                        gs.sb_base_g, gs.sb_base_i, dsort_aux_word(gs));
     hipLaunchKernelGGL(sb_scatter_kernel, dim3(sg.nchunks), dim3(64 * kScatterWaves), l3, s, P, sg, gs.order, gs.drect,
-                       gs.sb_cnt_g, gs.sb_base_g, bs.sblist, bs.cap);
+                       gs.sb_cnt_g, gs.sb_base_g, bs.sblist, bs.kdev, bs.cap);
 }
 
 void launch_binning_tiles(int P, const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
@@ -477,7 +497,7 @@ void launch_binning_tiles(int P, const Camera &cam, const GeomState &gs, const B
         return;
     }
     hipLaunchKernelGGL(tile_bin_kernel, dim3(sg.nsb), dim3(64 * kTBWaves), 0, s, sg, cam.gx, cam.gy, gs.sb_base_g,
-                       gs.sb_base_i, bs.sblist, bs.point_list, is.ranges, bs.cap);
+                       gs.sb_base_i, bs.sblist, bs.point_list, is.ranges, bs.kdev, bs.cap);
 }
 
 }  // namespace gsr

@@ -218,7 +218,8 @@ __global__ __launch_bounds__(kDsThreads) void dsort_pass_kernel(int P, int nb, c
                                                                  uint32_t *__restrict__ offsets,
                                                                  const uint32_t *__restrict__ tiles,
                                                                  const uint2 *__restrict__ rect8,
-                                                                 uint2 *__restrict__ drect) {
+                                                                 uint2 *__restrict__ drect,
+                                                                 uint32_t *__restrict__ host_err) {
     constexpr bool kFirst = kPass == 0, kLast = kPass == kPasses - 1;
     constexpr int kShift = 8 * kPass;
     __shared__ uint32_t s_key[kDsTile];
@@ -381,7 +382,10 @@ __global__ __launch_bounds__(kDsThreads) void dsort_pass_kernel(int P, int nb, c
             j -= q;
             if (q < kLookWin) {
                 if (++spins > kSpinLimit) {
+                    // never expected; made loud: render_fwd writes NaN pixels when this word is
+                    // set, and the sticky host word fails the next library call on this thread
                     ctl[kCtlErr] = 1u;
+                    if (host_err) __hip_atomic_store(host_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
@@ -414,7 +418,8 @@ int dsort_blocks(int P) { return (P + kDsTile - 1) / kDsTile; }
 size_t dsort_ctrl_words(int P) { return ctl_words(dsort_blocks(P) > 0 ? dsort_blocks(P) : 1); }
 size_t dsort_ctrl_zero_words(int P) { return ctl_zero_words(dsort_blocks(P) > 0 ? dsort_blocks(P) : 1); }
 
-void launch_depth_sort(int P, const GeomState &gs, uint32_t *host_K, hipStream_t s, hipEvent_t k_ready) {
+void launch_depth_sort(int P, const GeomState &gs, uint32_t *host_K, uint32_t *host_err, hipStream_t s,
+                       hipEvent_t k_ready) {
     if (P == 0) return;
     const int nb = dsort_blocks(P);
     hipLaunchKernelGGL(dsort_upsweep_kernel, dim3(up_blocks(nb)), dim3(kDsThreads), 0, s, P, nb, gs.dkey, gs.tiles,
@@ -422,13 +427,13 @@ void launch_depth_sort(int P, const GeomState &gs, uint32_t *host_K, hipStream_t
     if (k_ready) (void)hipEventRecord(k_ready, s);
     // keys: dkey -> dkey_sorted -> dkey -> dkey_sorted -> (none); values: (index) -> ids -> order -> ids -> order
     hipLaunchKernelGGL(dsort_pass_kernel<0>, dim3(nb), dim3(kDsThreads), 0, s, P, nb, gs.dkey, gs.dkey_sorted,
-                       (const uint32_t *)nullptr, gs.ids, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect);
+                       (const uint32_t *)nullptr, gs.ids, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect, host_err);
     hipLaunchKernelGGL(dsort_pass_kernel<1>, dim3(nb), dim3(kDsThreads), 0, s, P, nb, gs.dkey_sorted, gs.dkey, gs.ids,
-                       gs.order, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect);
+                       gs.order, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect, host_err);
     hipLaunchKernelGGL(dsort_pass_kernel<2>, dim3(nb), dim3(kDsThreads), 0, s, P, nb, gs.dkey, gs.dkey_sorted, gs.order,
-                       gs.ids, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect);
+                       gs.ids, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect, host_err);
     hipLaunchKernelGGL(dsort_pass_kernel<3>, dim3(nb), dim3(kDsThreads), 0, s, P, nb, gs.dkey_sorted,
-                       (uint32_t *)nullptr, gs.ids, gs.order, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect);
+                       (uint32_t *)nullptr, gs.ids, gs.order, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect, host_err);
 }
 
 uint32_t *dsort_K_word(const GeomState &gs) { return gs.ctrl + kCtlK; }

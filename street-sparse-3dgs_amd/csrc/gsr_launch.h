@@ -9,6 +9,8 @@ namespace gsr {
 
 // rasterizer.hip: message returned by gsr_last_error() for the calling thread.
 void set_last_error(const std::string &msg);
+// gsr_set_true_scale_gradient: dL/dscales including the scale_modifier factor (default off: upstream)
+bool true_scale_gradient();
 
 struct Camera {
     const float *view;  // device, 16
@@ -48,7 +50,9 @@ hipError_t sort_pairs(void *tmp, size_t tmp_bytes, const uint32_t *kin, uint32_t
 int dsort_blocks(int P);
 size_t dsort_ctrl_words(int P);
 size_t dsort_ctrl_zero_words(int P);
-void launch_depth_sort(int P, const GeomState &gs, uint32_t *host_K, hipStream_t s, hipEvent_t k_ready);
+// host_err (optional, pinned): set with a system-scope store when a lookback spin gives up.
+void launch_depth_sort(int P, const GeomState &gs, uint32_t *host_K, uint32_t *host_err, hipStream_t s,
+                       hipEvent_t k_ready);
 uint32_t *dsort_K_word(const GeomState &gs);
 uint32_t *dsort_err_word(const GeomState &gs);
 // a zeroed-per-frame control word the binning uses as a completion counter

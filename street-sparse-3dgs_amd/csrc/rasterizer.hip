@@ -7,8 +7,10 @@
 // backward: render bwd (per-instance records) -> preprocess bwd (per-Gaussian sum + chain).
 #include <cstdio>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <string>
+#include <algorithm>
 
 #include "../../include/gsr.h"
 #include "gsr_launch.h"
@@ -21,12 +23,20 @@ thread_local std::string g_err;
 // K (num_rendered) arrives in pinned, host-coherent memory written by the depth sort's first
 // kernel; the host waits on an event recorded right after it, so the sort passes keep running
 // while the host sizes the binning buffer.
+// g_pinned[0] = K, g_pinned[1] = sticky depth-sort error (a lookback spin gave up; never expected)
 thread_local uint32_t *g_pinned = nullptr;
 thread_local uint32_t *g_pinned_dev = nullptr;
+// forward statistics (gsr_forward_stats): frames, binning re-runs at K (capacity hint short)
+std::atomic<int64_t> g_frames{0}, g_reruns{0};
 constexpr int kMaxDevicesK = 64;
 thread_local hipEvent_t g_k_ready[kMaxDevicesK] = {};
-// per device: capacity for the next frame's point list (last K + 1/8 + 4096), 0 = none yet
+// per device: capacity for the next frame's point list, 0 = none yet.  It is the largest K of the
+// last kKHist frames + 1/8 + 4096, so a training loop cycling its cameras (whose K differs from
+// view to view) rarely comes up short and re-runs the binning (gsr_forward_stats counts re-runs).
+constexpr int kKHist = 8;
 thread_local int64_t g_khint[kMaxDevicesK] = {};
+thread_local int64_t g_khist[kMaxDevicesK][kKHist] = {};
+thread_local int g_khead[kMaxDevicesK] = {};
 #ifndef GSR_DEFER_K
 #define GSR_DEFER_K 1
 #endif
@@ -81,6 +91,14 @@ struct SideJoin {
 int fail(int code, const std::string &msg) {
     g_err = msg;
     return code;
+}
+
+// A lookback timeout of this or an earlier frame's depth sort (the pass kernels store the pinned
+// word; its frame's render_fwd already wrote NaN pixels): fail this call, once per occurrence.
+int sticky_sort_error() {
+    if (g_pinned && __atomic_exchange_n(&g_pinned[1], 0u, __ATOMIC_SEQ_CST) != 0u)
+        return fail(GSR_ERR_DEVICE, "depth sort: a lookback spin timed out (this or an earlier frame; its image is NaN)");
+    return GSR_OK;
 }
 
 void ensure_events() {
@@ -230,6 +248,11 @@ int validate_common(int P, int D, int M, const float *shs, const float *colors_p
 
 void gsr::set_last_error(const std::string &msg) { g_err = msg; }
 
+namespace {
+std::atomic<int> g_true_scale_grad{0};
+}
+bool gsr::true_scale_gradient() { return g_true_scale_grad.load(std::memory_order_relaxed) != 0; }
+
 extern "C" {
 
 int gsr_abi_version(void) { return GSR_ABI_VERSION; }
@@ -342,10 +365,11 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
     hipEvent_t k_ready = nullptr;
     if (P > 0) {
         if (!g_pinned) {
-            if (hipHostMalloc(reinterpret_cast<void **>(&g_pinned), sizeof(uint32_t), hipHostMallocCoherent) !=
+            if (hipHostMalloc(reinterpret_cast<void **>(&g_pinned), 2 * sizeof(uint32_t), hipHostMallocCoherent) !=
                     hipSuccess ||
                 hipHostGetDevicePointer(reinterpret_cast<void **>(&g_pinned_dev), g_pinned, 0) != hipSuccess)
                 return fail(GSR_ERR_ALLOCATION, "pinned host allocation failed");
+            g_pinned[1] = 0u;
         }
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevicesK)
@@ -357,7 +381,7 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
     }
     {
         StageTimer st(1, s);
-        launch_depth_sort(P, gs, g_pinned_dev, s, k_ready);
+        launch_depth_sort(P, gs, g_pinned_dev, g_pinned_dev + 1, s, k_ready);
     }
     if ((rc = check("depth sort", debug, s))) return rc;
     // K sizes the point list.  With a capacity hint from this device's previous frame the binning
@@ -377,11 +401,12 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
             if (hipMemcpy(&k, dsort_K_word(gs), sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
                 return fail(GSR_ERR_DEVICE, "num_rendered copy failed");
         }
-        if (debug) {
+        if (debug) {  // the sort passes are complete here (debug syncs after every stage)
             uint32_t err = 0;
             if (hipMemcpy(&err, dsort_err_word(gs), sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess || err)
                 return fail(GSR_ERR_DEVICE, "depth sort: a lookback spin timed out");
         }
+        if ((rc = sticky_sort_error())) return rc;
         K = (int64_t)k;
         have_K = true;
         return GSR_OK;
@@ -428,14 +453,30 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
     const int64_t cap0 = defer ? g_khint[dev] : K;
     if ((rc = bin_and_render(cap0))) return rc;
     if (!have_K && (rc = read_K())) return rc;
+    if (debug && P > 0) {  // the binning's instance total must be K (the kernels' capacity test is on K)
+        uint32_t bi = 0;
+        if (hipMemcpy(&bi, gs.sb_base_i + gs.sb.nsb, sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
+            return fail(GSR_ERR_DEVICE, "binning total copy failed");
+        if ((int64_t)bi != K) return fail(GSR_ERR_DEVICE, "binning: superblock instance total differs from K");
+    }
+    if (P > 0) g_frames.fetch_add(1, std::memory_order_relaxed);
     if (K > cap0) {  // the capacity was short: again at K
+        g_reruns.fetch_add(1, std::memory_order_relaxed);
         // sb_colscan's last-workgroup counter (a depth-sort control word the preprocess zeroes
         // once per frame) must start from zero again
         if (hipMemsetAsync(dsort_aux_word(gs), 0, sizeof(uint32_t), s) != hipSuccess)
             return fail(GSR_ERR_DEVICE, "binning counter reset failed");
         if ((rc = bin_and_render(K))) return rc;
     }
-    if (P > 0) g_khint[dev] = K + K / 8 + 4096;
+    // the kernels compare K with a 32-bit capacity: keep the hint representable
+    if (P > 0) {
+        g_khist[dev][g_khead[dev]] = K;
+        g_khead[dev] = (g_khead[dev] + 1) % kKHist;
+        int64_t kmax = 0;
+        for (int i = 0; i < kKHist; i++) kmax = std::max(kmax, g_khist[dev][i]);
+        // the kernels compare K with a 32-bit capacity: keep the hint representable
+        g_khint[dev] = std::min<int64_t>(kmax + kmax / 8 + 4096, (int64_t)UINT32_MAX);
+    }
     if (num_rendered) *num_rendered = K;
     return GSR_OK;
 }
@@ -464,6 +505,7 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
     if (P > 0 && shs && !dL_dsh) return fail(GSR_ERR_INVALID_ARGUMENT, "NULL dL_dsh");
     if (P > 0 && !cov3D_precomp && (!dL_dscales || !dL_drotations))
         return fail(GSR_ERR_INVALID_ARGUMENT, "NULL dL_dscales / dL_drotations");
+    if ((rc = sticky_sort_error())) return rc;
 
     const Camera cam = make_camera(viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, width, height);
     const int T = cam.gx * cam.gy;
@@ -491,6 +533,19 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
     }
     if ((rc = check("preprocess backward", debug, s))) return rc;
     return GSR_OK;
+}
+
+int gsr_set_true_scale_gradient(int enable) {
+    const int prev = g_true_scale_grad.exchange(enable ? 1 : 0);
+    return prev;
+}
+
+int gsr_forward_stats(int64_t *out, int n) {
+    if (!out || n < 0) return fail(GSR_ERR_INVALID_ARGUMENT, "NULL stats buffer");
+    const int64_t v[2] = {g_frames.load(), g_reruns.load()};
+    int k = 0;
+    for (; k < n && k < 2; k++) out[k] = v[k];
+    return k;
 }
 
 int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,

@@ -171,7 +171,7 @@ __global__ __launch_bounds__(256) void render_fwd_sb_kernel(
     const GRec *__restrict__ rec, const float *__restrict__ bg, float *__restrict__ out_color,
     float *__restrict__ out_invd, float *__restrict__ final_T, uint32_t *__restrict__ n_contrib,
     uint32_t *__restrict__ tile_work, const uint32_t *__restrict__ fwd_order, const uint32_t *__restrict__ kdev,
-    uint32_t cap) {
+    uint32_t cap, const uint32_t *__restrict__ sort_err) {
     if (kdev && *kdev > cap) return;  // the point-list capacity is short: the host re-runs at K
     // per wave, three 64-entry planes: {x, y, conic.a, conic.b}, {conic.c, opacity, -, -},
     // {r, g, b, 1/depth}; one base address serves all three (offsets 0 / 1 / 2 KiB)
@@ -248,6 +248,9 @@ __global__ __launch_bounds__(256) void render_fwd_sb_kernel(
     }
     const uint32_t wl = wave_max_u32(last);
     if (lane == 0) s_work[w] = wl;
+    if (*sort_err) {  // the depth sort gave up on a lookback: make the frame unmistakably invalid
+        C0 = C1 = C2 = ID = __builtin_nanf("");
+    }
     if (inside) {
         const int pix = py * W + px;
         final_T[pix] = T;
@@ -318,7 +321,7 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
     if (GSR_FWD_SUBBLOCK) {  // launch order: is.tile_ids (rasterizer.hip, by list length)
         hipLaunchKernelGGL(render_fwd_sb_kernel, dim3(T), dim3(4 * kWave), 0, s, is.ranges, bs.point_list, cam.W,
                            cam.H, cam.gx, gs.rec, bg, out_color, out_invdepth, is.final_T, is.n_contrib, is.tile_work,
-                           is.tile_ids, bs.kdev, bs.cap);
+                           is.tile_ids, bs.kdev, bs.cap, dsort_err_word(gs));
     }
     else
         hipLaunchKernelGGL(render_fwd_kernel, dim3(T), dim3(kWave), 0, s, is.ranges, bs.point_list, cam.W, cam.H,

@@ -26,6 +26,7 @@ torch caching allocator and are freed with the autograd graph, as upstream's are
 from __future__ import annotations
 
 import ctypes
+import threading
 
 import torch
 
@@ -57,32 +58,40 @@ def _stream(device):
 class _Resizer:
     """Holds the uint8 tensors the library asks for through gsr_resize_fn callbacks.
 
-    The callbacks close over `bufs` and `device` only (not over the resizer), and `release()`
-    drops the ctypes thunks after the call: no reference cycle, so every frame's scratch is
-    returned to the caching allocator as soon as autograd releases it instead of waiting for
-    Python's cyclic GC (which let ~10 frames of scratch pile up and forced fresh hipMallocs)."""
+    The ctypes thunks are built once per process (one per buffer name, module level) and find
+    the resizer of the call in progress through a thread-local slot, so a call builds no
+    CFUNCTYPE objects (three per frame cost measurable host time on slow hosts).  `release()`
+    empties the slot: the tensors are owned by `bufs` alone, and every frame's scratch returns
+    to the caching allocator as soon as autograd releases it."""
 
     def __init__(self, device):
         self.device = device
         self.bufs = {}
-        self.fns = {}
+        _TLS.current = self
 
     def fn(self, name):
-        bufs, device = self.bufs, self.device
-
-        def cb(_ctx, nbytes):
-            t = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
-            bufs[name] = t
-            return t.data_ptr()
-        f = _lib.RESIZE_FN(cb)
-        self.fns[name] = f
-        return f
+        return _THUNKS[name]
 
     def release(self):
-        self.fns.clear()
+        _TLS.current = None
 
     def get(self, name):
         return self.bufs.get(name, torch.empty(0, dtype=torch.uint8, device=self.device))
+
+
+_TLS = threading.local()
+
+
+def _make_thunk(name):
+    def cb(_ctx, nbytes):
+        r = _TLS.current
+        t = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=r.device)
+        r.bufs[name] = t
+        return t.data_ptr()
+    return _lib.RESIZE_FN(cb)
+
+
+_THUNKS = {n: _make_thunk(n) for n in ("geom", "binning", "image", "scratch")}
 
 
 def _check(rc, what):
@@ -210,6 +219,19 @@ def mark_visible(means3D, viewmatrix, projmatrix):
         rc = _L.gsr_mark_visible(P, _ptr(m), _ptr(v), _ptr(p), _ptr(present), _stream(dev))
     _check(rc, "mark_visible")
     return present.bool()
+
+
+def set_true_scale_gradient(enable: bool) -> bool:
+    """dL/dscales as the exact derivative (times scale_modifier) instead of upstream's dL/d(mod*s).
+    Process-wide; returns the previous setting.  Only differs when scale_modifier != 1."""
+    return bool(_L.gsr_set_true_scale_gradient(int(bool(enable))))
+
+
+def forward_stats() -> dict:
+    """Frames rasterized since load and how many re-ran their binning at K (gsr_forward_stats)."""
+    buf = (ctypes.c_int64 * 2)()
+    n = _L.gsr_forward_stats(buf, 2)
+    return {"frames": int(buf[0]) if n > 0 else 0, "reruns": int(buf[1]) if n > 1 else 0}
 
 
 def set_profiling(enable: bool) -> None:

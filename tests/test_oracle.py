@@ -76,8 +76,11 @@ def test_oracle_backward_matches_fp64_autograd(c):
     rng = np.random.default_rng(0)
     gc = rng.normal(size=(3, H, W))
     gd = rng.normal(size=(1, H, W))
-    b = O.backward(st, gc, gd)
+    b = O.backward(st, gc, gd, true_scale_grad=True)  # fp64 autograd gives the exact derivative
     d = DT.dense_grads(st, gc, gd)
+    # upstream's convention (the default): dL/d(mod * s) reported as dL/ds
+    bu = O.backward(st, gc, gd)
+    assert rel_l2(bu["dL_dscales"] * np.float32(c.get("mod", 1.0)), b["dL_dscales"]) < 1e-6
     assert rel_l2(st["color"], d["color"]) < 1e-5
     assert rel_l2(st["invdepth"], d["invdepth"]) < 1e-5
     for dk, ok in [("dL_dmeans3D", "dL_dmeans3D"), ("dL_dmeans2D", "dL_dmeans2D"), ("dL_dopacities", "dL_dopacity"),
