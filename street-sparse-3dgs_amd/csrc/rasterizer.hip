@@ -421,7 +421,8 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
         void *bbase = binning_buffer(resize_ctx, bbytes);
         if (!bbase) return fail(GSR_ERR_ALLOCATION, "binning buffer allocation failed");
         BinningState bs = carve_binning(bbase, cap, nullptr);
-        bs.kdev = dsort_K_word(gs);
+        // P == 0: no depth sort ran, its control words are not initialised (no capacity test)
+        bs.kdev = P > 0 ? dsort_K_word(gs) : nullptr;
         int r;
         {
             StageTimer st(2, s);

@@ -248,7 +248,7 @@ __global__ __launch_bounds__(256) void render_fwd_sb_kernel(
     }
     const uint32_t wl = wave_max_u32(last);
     if (lane == 0) s_work[w] = wl;
-    if (*sort_err) {  // the depth sort gave up on a lookback: make the frame unmistakably invalid
+    if (sort_err && *sort_err) {  // the depth sort gave up on a lookback: make the frame unmistakably invalid
         C0 = C1 = C2 = ID = __builtin_nanf("");
     }
     if (inside) {
@@ -321,7 +321,7 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
     if (GSR_FWD_SUBBLOCK) {  // launch order: is.tile_ids (rasterizer.hip, by list length)
         hipLaunchKernelGGL(render_fwd_sb_kernel, dim3(T), dim3(4 * kWave), 0, s, is.ranges, bs.point_list, cam.W,
                            cam.H, cam.gx, gs.rec, bg, out_color, out_invdepth, is.final_T, is.n_contrib, is.tile_work,
-                           is.tile_ids, bs.kdev, bs.cap, dsort_err_word(gs));
+                           is.tile_ids, bs.kdev, bs.cap, bs.kdev ? dsort_err_word(gs) : nullptr);
     }
     else
         hipLaunchKernelGGL(render_fwd_kernel, dim3(T), dim3(kWave), 0, s, is.ranges, bs.point_list, cam.W, cam.H,
