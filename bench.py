@@ -21,6 +21,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "street-sparse-3dgs_amd"))
 sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -43,8 +45,8 @@ def parse():
     ap.add_argument("--train-steps", type=int, default=20, help="timed train-step harness iterations (0 = skip)")
     ap.add_argument("--config5", action="store_true",
                     help="also time config 5: hierarchy cut blend + forward render of the cut at 1080p")
-    ap.add_argument("--c5-nodes", type=int, default=50_000_000)
-    ap.add_argument("--c5-cut", type=int, default=5_000_000)
+    ap.add_argument("--c5-leaves", type=int, default=37_500_000, help="leaves of the config-5 tree (~4/3 as many nodes)")
+    ap.add_argument("--c5-tau", type=float, default=3.0, help="render_hierarchy.py tau (pixels)")
     ap.add_argument("--train-baseline", action="store_true",
                     help="also time the reference-structured torch train step (conv2d SSIM, OurAdam gather/scatter)")
     return ap.parse_args()
@@ -159,45 +161,76 @@ def train_step_ms(s, W, H, deg, steps, warmup, fused, dev):
 
 def config5(a, dev):
     """render_hierarchy.py's per-frame work on a synthetic merged
-    hierarchy -- render_post's LOD blend of the cut (fused kernel) and the forward render of the
-    cut at 1920x1080 (no_grad, do_depth), timed together per frame."""
+    hierarchy (a real tree: Morton-grouped leaves, one Gaussian per node, ~50M nodes) --
+    expand_to_size at the tau threshold (render_hierarchy.py:61-72), get_interpolation_weights
+    (:76-85), render_post's LOD blend (fused kernel) and the forward render of the cut at 1080p
+    (no_grad, do_depth), timed together per frame."""
     import torch
     from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    from gaussian_hierarchy._C import expand_to_size, get_interpolation_weights
     from gs_train.hier import interpolate_cut
-    from gs_train.synthetic import synthetic_hierarchy
+    from gs_train.synthetic import synthetic_lod_hierarchy, tau_threshold
     W, H = a.width, a.height
-    h = synthetic_hierarchy(a.c5_nodes, a.c5_cut, 100_000, W, H, dev, seed=5)
+    h = synthetic_lod_hierarchy(a.c5_leaves, W, H, dev, seed=5, skybox=100_000)
+    N = h["nodes"].shape[0]
+    thr = tau_threshold(a.c5_tau, h["tanfovx"], W)
     t = lambda x: torch.tensor(x, dtype=torch.float32, device=dev)
+    ri, pi, ni = (torch.zeros(N, dtype=torch.int32, device=dev) for _ in range(3))
+    wts = torch.zeros(N, device=dev)
+    kids = torch.zeros(N, dtype=torch.int32, device=dev)
+    cam = t(h["campos"])
+    cam_cpu = cam.cpu()
+    zero3 = torch.zeros(3)
     rs = GaussianRasterizationSettings(
         image_height=H, image_width=W, tanfovx=float(h["tanfovx"]), tanfovy=float(h["tanfovy"]), bg=t([0, 0, 0]),
         scale_modifier=1.0, viewmatrix=t(h["view"]).reshape(4, 4), projmatrix=t(h["proj"]).reshape(4, 4),
-        sh_degree=3, campos=t(h["campos"]), prefiltered=False, debug=False, do_depth=True,
+        sh_degree=3, campos=cam, prefiltered=False, debug=False, do_depth=True,
         render_indices=torch.empty(0, dtype=torch.int32), parent_indices=torch.empty(0, dtype=torch.int32),
-        interpolation_weights=h["interpolation_weights"],
-        num_node_kids=torch.ones(a.c5_nodes, dtype=torch.int32, device=dev))
+        interpolation_weights=wts, num_node_kids=kids)
     raster = GaussianRasterizer(rs)
 
-    def frame():
+    def frame(split=None):
         with torch.no_grad():
+            n = expand_to_size(h["nodes"], h["boxes"], thr, cam, zero3, ri, pi, ni)
+            get_interpolation_weights(ni[:n], thr, h["nodes"], h["boxes"], cam_cpu, zero3, wts, kids)
+            if split is not None:
+                torch.cuda.synchronize()
+                split.append(time.perf_counter())
             m, sc, rot, op, sh = interpolate_cut(h["means3D"], h["scales"], h["rotations"], h["opacities"], h["shs"],
-                                                 h["render_indices"], h["parent_indices"],
-                                                 h["interpolation_weights"], h["skybox"])
-            return raster(means3D=m, means2D=torch.zeros_like(m), shs=sh, colors_precomp=None, opacities=op,
-                          scales=sc, rotations=rot, cov3D_precomp=None)
+                                                 ri[:n], pi, wts, h["skybox"])
+            if split is not None:
+                torch.cuda.synchronize()
+                split.append(time.perf_counter())
+            out = raster(means3D=m, means2D=torch.zeros_like(m), shs=sh, colors_precomp=None, opacities=op,
+                         scales=sc, rotations=rot, cov3D_precomp=None)
+            if split is not None:
+                torch.cuda.synchronize()
+                split.append(time.perf_counter())
+            return n, out
 
     for _ in range(3):
         frame()
     torch.cuda.synchronize()
-    n = 10
+    nf = 10
     t0 = time.perf_counter()
-    for _ in range(n):
-        color, radii, _ = frame()
+    for _ in range(nf):
+        n, (color, radii, _) = frame()
     torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) / n * 1e3
-    out = {"ms_per_frame": round(ms, 3), "fwd_mpix_s": round(W * H / ms / 1e3, 1), "nodes": a.c5_nodes,
-           "rendered": a.c5_cut + 100_000, "visible": int((radii > 0).sum().item()), "width": W, "height": H,
-           "workload": "render_post LOD blend (fused) + rasterizer forward of the cut, no_grad, do_depth",
-           "data": "synthetic hierarchy generated on the device (random cut; .hier / expand_to_size unavailable)"}
+    ms = (time.perf_counter() - t0) / nf * 1e3
+    parts = []
+    for _ in range(3):  # synced split, separate from the timed frames
+        sp = [time.perf_counter()]
+        frame(sp)
+        parts.append([1e3 * (sp[i + 1] - sp[i]) for i in range(3)])
+    parts = np.median(np.array(parts), 0)
+    out = {"ms_per_frame": round(ms, 3), "fwd_mpix_s": round(W * H / ms / 1e3, 1), "nodes": N,
+           "leaves": a.c5_leaves, "tau": a.c5_tau, "cut": n, "rendered": n + h["skybox"],
+           "visible": int((radii > 0).sum().item()), "width": W, "height": H,
+           "split_ms": {"cut_and_weights": round(float(parts[0]), 3), "blend": round(float(parts[1]), 3),
+                        "raster_fwd": round(float(parts[2]), 3)},
+           "workload": "expand_to_size + get_interpolation_weights + render_post LOD blend (fused) + rasterizer "
+                       "forward of the cut, no_grad, do_depth",
+           "data": "synthetic hierarchy generated on the device (Morton-grouped tree, branching 4, 100k skybox)"}
     del h, raster
     torch.cuda.empty_cache()
     return out

@@ -43,6 +43,31 @@ int gsr_interpolate_cut_backward(int64_t N, int M, int64_t R, int64_t S, const i
                                  const float *dL_dout_shs, float *dL_dmeans3D, float *dL_dscales,
                                  float *dL_drotations, float *dL_dopacities, float *dL_dshs, void *stream);
 
+/* ---- LOD cut (csrc/lod.hip) ------------------------------------------------------------
+ * Replace gaussian_hierarchy._C.expand_to_size / get_interpolation_weights (the gaussianhierarchy
+ * extension, un-vendored; called at render_hierarchy.py:63-85, train_post.py:91-113,
+ * render_hierarchy_final.py:222-245, render_position.py:105-130 of the reference).
+ *   nodes: (N, 7) int32 {depth, parent, start, count_leafs, count_merged, start_children,
+ *          count_children};  boxes: (N, 2, 4) float {minn.xyz, size, maxx.xyz, -}.
+ * expand_to_size writes the cut -- render_indices (Gaussian ids), parent_indices (the parent
+ * node's first Gaussian, -1 for roots) and nodes_for_render_indices (node ids), in node order --
+ * and returns its length in *to_render (the value the Python function returns; one host read, as
+ * upstream).  viewpoint is a DEVICE float[3] (the caller's camera_center on the GPU).
+ * Output arrays need room for the cut (N entries always suffice when every node holds at most one
+ * Gaussian; in general sum of count_leafs + count_merged).  scratch: a device buffer of
+ * gsr_expand_to_size_scratch_bytes(N) bytes. */
+size_t gsr_expand_to_size_scratch_bytes(int64_t N);
+int gsr_expand_to_size(int64_t N, const int *nodes, const float *boxes, float target_size, const float *viewpoint,
+                       int *render_indices, int *parent_indices, int *nodes_for_render_indices, void *scratch,
+                       size_t scratch_bytes, int64_t *to_render, void *stream);
+
+/* get_interpolation_weights: for the n rendered nodes node_indices[i], weights[i] = the blend
+ * weight t of the node with its parent and num_kids[i] = the parent's child count (1 for roots).
+ * The viewpoint is passed by value (the reference hands camera_center.cpu()). */
+int gsr_interpolation_weights(int64_t n, const int *node_indices, float target_size, const int *nodes,
+                              const float *boxes, float vx, float vy, float vz, float *weights, int *num_kids,
+                              void *stream);
+
 #ifdef __cplusplus
 }
 #endif

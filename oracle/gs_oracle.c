@@ -726,3 +726,65 @@ static void knn_one(long long N, const float *p, long long i, float *out) {
         *out = (b0 + b1 + b2) / 3.0f;
     }
 }
+
+/* ------------------------------------------------------------------------------------------
+ * Hierarchy LOD cut: gaussian_hierarchy._C.expand_to_size and
+ * get_interpolation_weights as render_hierarchy.py:61-85 / train_post.py:91-113 call them.
+ * gaussianhierarchy is not vendored, so this restates the published hierarchical-3DGS cut
+ * (Kerbl et al. 2024, sec. 4) -- PARITY UNPINNED against the extension itself.
+ * nodes (N,7) int32: depth, parent, start, count_leafs, count_merged, start_children,
+ * count_children; boxes (N,2,4) float: minn.xyz, size | maxx.xyz, -.
+ * ------------------------------------------------------------------------------------------ */
+static float lod_size(const float *b, const float *v) {
+    if (v[0] >= b[0] && v[0] <= b[4] && v[1] >= b[1] && v[1] <= b[5] && v[2] >= b[2] && v[2] <= b[6]) return FLT_MAX;
+    float cx = fmaxf(b[0], fminf(b[4], v[0]));
+    float cy = fmaxf(b[1], fminf(b[5], v[1]));
+    float cz = fmaxf(b[2], fminf(b[6], v[2]));
+    float dx = v[0] - cx, dy = v[1] - cy, dz = v[2] - cz;
+    float d = sqrtf(dx * dx + dy * dy + dz * dz);
+    return b[3] / d;
+}
+
+long long gso_expand_to_size(long long N, const int *nodes, const float *boxes, float target, const float *v,
+                             int *render_indices, int *parent_indices, int *nodes_for_render) {
+    long long out = 0;
+    for (long long i = 0; i < N; i++) {
+        const int *n = nodes + 7 * i;
+        float s = lod_size(boxes + 8 * i, v);
+        int c = 0;
+        if (s >= target) c = n[3];
+        else if (n[1] < 0 || lod_size(boxes + 8 * (long long)n[1], v) >= target) c = n[3] + n[4];
+        int pg = n[1] < 0 ? -1 : nodes[7 * (long long)n[1] + 2];
+        for (int k = 0; k < c; k++, out++) {
+            render_indices[out] = n[2] + k;
+            parent_indices[out] = pg;
+            nodes_for_render[out] = (int)i;
+        }
+    }
+    return out;
+}
+
+void gso_interpolation_weights(long long n, const int *node_indices, float target, const int *nodes,
+                               const float *boxes, const float *v, float *weights, int *num_kids) {
+    for (long long i = 0; i < n; i++) {
+        int id = node_indices[i];
+        int parent = nodes[7 * (long long)id + 1];
+        float t = 1.f;
+        int kids = 1;
+        if (parent >= 0) {
+            kids = nodes[7 * (long long)parent + 6];
+            float sp = lod_size(boxes + 8 * (long long)parent, v);
+            if (!(sp > 2.f * target)) {
+                float s = lod_size(boxes + 8 * (long long)id, v);
+                float s0 = fmaxf(0.5f * sp, s);
+                float diff = sp - s0;
+                if (diff > 0.f) {
+                    float tdiff = fmaxf(0.f, target - s0);
+                    t = fmaxf(1.f - tdiff / diff, 0.f);
+                }
+            }
+        }
+        weights[i] = t;
+        num_kids[i] = kids;
+    }
+}

@@ -169,6 +169,33 @@ def backward(st, dL_dcolor, dL_dinvdepth=None, true_scale_grad=False):
                 inst=inst[:K], g10=g10)
 
 
+def expand_to_size(nodes, boxes, target, viewpoint):
+    """C restatement of gaussian_hierarchy expand_to_size -> (render_indices, parent_indices,
+    nodes_for_render_indices), each int32 of the cut's length."""
+    nodes = np.ascontiguousarray(nodes, np.int32).reshape(-1, 7)
+    boxes = _f32(boxes).reshape(-1, 8)
+    N = nodes.shape[0]
+    cap = int(nodes[:, 3].astype(np.int64).sum() + nodes[:, 4].astype(np.int64).sum())
+    ri, pi, ni = (np.zeros(max(cap, 1), np.int32) for _ in range(3))
+    L = lib()
+    L.gso_expand_to_size.restype = ctypes.c_longlong
+    n = L.gso_expand_to_size(ctypes.c_longlong(N), _p(nodes), _p(boxes), ctypes.c_float(target),
+                             _p(_f32(viewpoint).reshape(3)), _p(ri), _p(pi), _p(ni))
+    return ri[:n].copy(), pi[:n].copy(), ni[:n].copy()
+
+
+def interpolation_weights(node_indices, target, nodes, boxes, viewpoint):
+    """C restatement of gaussian_hierarchy get_interpolation_weights -> (weights f32, num_kids i32)."""
+    node_indices = np.ascontiguousarray(node_indices, np.int32)
+    n = node_indices.shape[0]
+    w = np.zeros(max(n, 1), np.float32)
+    k = np.zeros(max(n, 1), np.int32)
+    lib().gso_interpolation_weights(ctypes.c_longlong(n), _p(node_indices), ctypes.c_float(target),
+                                    _p(np.ascontiguousarray(nodes, np.int32)), _p(_f32(boxes)),
+                                    _p(_f32(viewpoint).reshape(3)), _p(w), _p(k))
+    return w[:n], k[:n]
+
+
 class upstream_exponent:
     """Context manager: the oracle's render fwd/bwd evaluate the Gaussian as upstream writes it
     (power = -0.5 (a dx^2 + c dy^2) - b dx dy, expf) instead of the kernels' exp2 order."""

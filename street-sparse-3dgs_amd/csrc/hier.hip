@@ -24,6 +24,10 @@ __device__ __forceinline__ CutRow cut_row(int64_t r, int64_t N, int64_t R, int64
     if (r < R) {
         o.c = ri[r];
         o.p = pi[r];
+        // expand_to_size gives root nodes the parent -1; torch's gather in render_post reads that
+        // as the last row (weight 1 - t = 0 for a root), so do the same instead of reading before
+        // the array
+        if (o.p < 0) o.p += N;
         o.t = w[r];
         o.copy = false;
     } else {

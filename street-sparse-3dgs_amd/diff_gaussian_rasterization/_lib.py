@@ -67,6 +67,10 @@ SIGNATURES = {
     # include/gsr_hier.h
     "gsr_interpolate_cut_forward": (_i, [_i64, _i, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                          _vp, _vp, _vp]),
+    "gsr_expand_to_size_scratch_bytes": (ctypes.c_size_t, [_i64]),
+    "gsr_expand_to_size": (_i, [_i64, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t, ctypes.POINTER(_i64),
+                                _vp]),
+    "gsr_interpolation_weights": (_i, [_i64, _vp, _f, _vp, _vp, _f, _f, _f, _vp, _vp, _vp]),
     "gsr_densify_scratch_bytes": (ctypes.c_size_t, [_i64]),
     "gsr_densify_plan": (_i, [_i64, _i64, _vp, _vp, _vp, _vp, _f, _f, _f, _vp, _vp, _vp]),
     "gsr_densify_apply": (_i, [_i64, _i, ctypes.POINTER(RowGroup), ctypes.POINTER(RowGroup), _i, _i, _i, _vp, _i64,

@@ -1,0 +1,103 @@
+"""`gaussian_hierarchy._C` -- expand_to_size / get_interpolation_weights over the C ABI of
+include/gsr_hier.h (csrc/lod.hip), with the argument order and in-place outputs the reference's
+callers use:
+
+    to_render = expand_to_size(nodes, boxes, threshold, camera_center, viewdir,
+                               render_indices, parent_indices, nodes_for_render_indices)
+    get_interpolation_weights(node_indices, threshold, nodes, boxes, camera_center.cpu(), viewdir,
+                              interpolation_weights, num_siblings)
+
+(render_hierarchy.py:63-85, train_post.py:91-113).  nodes (N, 7) int32 and boxes (N, 2, 4) float32
+on the GPU, as the reference keeps them (scene/gaussian_model.py:424-425).  `viewdir` is accepted
+and unused, as in the published cut (the reference passes zeros).  The outputs are written in
+place; expand_to_size returns the cut length (one host read, as upstream).
+
+The .hier file I/O of the extension (load_hierarchy / write_hierarchy) is not part of the
+rasterizer's hot path and its binary format is not vendored here: both raise.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from diff_gaussian_rasterization import _lib
+
+_L = _lib.load()
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed ({rc}): {_lib.last_error()}")
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None and t.numel() > 0 else None
+
+
+def _stream(dev):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _need(t, name, dtype, dev):
+    if not t.is_cuda or t.device != dev:
+        raise RuntimeError(f"{name} must be on {dev}")
+    if t.dtype != dtype:
+        raise RuntimeError(f"{name} must be {dtype}")
+    if not t.is_contiguous():
+        raise RuntimeError(f"{name} must be contiguous (written in place)")
+    return t
+
+
+def expand_to_size(nodes, boxes, size, viewpoint, viewdir, render_indices, parent_indices,
+                   nodes_for_render_indices):
+    dev = nodes.device
+    if not nodes.is_cuda:
+        raise RuntimeError("expand_to_size: nodes must be on a ROCm GPU device")
+    N = nodes.shape[0]
+    nodes_c = nodes.to(torch.int32).contiguous()
+    boxes_c = boxes.to(torch.float32).contiguous()
+    if nodes_c.numel() != 7 * N or boxes_c.numel() != 8 * N:
+        raise RuntimeError("expand_to_size: nodes must be (N, 7) int32 and boxes (N, 2, 4) float32")
+    for t, n in ((render_indices, "render_indices"), (parent_indices, "parent_indices"),
+                 (nodes_for_render_indices, "nodes_for_render_indices")):
+        _need(t, n, torch.int32, dev)
+    cap = min(render_indices.numel(), parent_indices.numel(), nodes_for_render_indices.numel())
+    need = int(nodes_c[:, 3].sum().item() + nodes_c[:, 4].sum().item()) if cap < N else N
+    if cap < need:
+        raise RuntimeError(f"expand_to_size: output arrays hold {cap} entries, the cut may need {need}")
+    vp = viewpoint.to(device=dev, dtype=torch.float32).contiguous().reshape(3)
+    scratch = torch.empty(int(_L.gsr_expand_to_size_scratch_bytes(N)), dtype=torch.uint8, device=dev)
+    out = ctypes.c_int64(0)
+    with torch.cuda.device(dev):
+        rc = _L.gsr_expand_to_size(N, _p(nodes_c), _p(boxes_c), float(size), _p(vp), _p(render_indices),
+                                   _p(parent_indices), _p(nodes_for_render_indices), _p(scratch),
+                                   scratch.numel(), ctypes.byref(out), _stream(dev))
+    _check(rc, "expand_to_size")
+    return int(out.value)
+
+
+def get_interpolation_weights(node_indices, size, nodes, boxes, viewpoint, viewdir, out_weights, out_num_kids):
+    dev = nodes.device
+    n = node_indices.shape[0]
+    idx = node_indices.to(device=dev, dtype=torch.int32).contiguous()
+    nodes_c = nodes.to(torch.int32).contiguous()
+    boxes_c = boxes.to(torch.float32).contiguous()
+    _need(out_weights, "interpolation_weights", torch.float32, dev)
+    _need(out_num_kids, "num_node_kids", torch.int32, dev)
+    if out_weights.numel() < n or out_num_kids.numel() < n:
+        raise RuntimeError("get_interpolation_weights: output arrays shorter than node_indices")
+    vx, vy, vz = (float(v) for v in viewpoint.detach().reshape(3).cpu().tolist())
+    with torch.cuda.device(dev):
+        rc = _L.gsr_interpolation_weights(n, _p(idx), float(size), _p(nodes_c), _p(boxes_c), vx, vy, vz,
+                                          _p(out_weights), _p(out_num_kids), _stream(dev))
+    _check(rc, "get_interpolation_weights")
+
+
+def load_hierarchy(path):
+    raise NotImplementedError("gaussian_hierarchy.load_hierarchy: the .hier file format (gaussianhierarchy, not "
+                              "vendored in the reference) is outside the rasterizer hot path this package rebuilds")
+
+
+def write_hierarchy(*args, **kwargs):
+    raise NotImplementedError("gaussian_hierarchy.write_hierarchy: the .hier file format is not rebuilt here")
