@@ -46,7 +46,10 @@ def parse():
     ap.add_argument("--config5", action="store_true",
                     help="also time config 5: hierarchy cut blend + forward render of the cut at 1080p")
     ap.add_argument("--c5-leaves", type=int, default=37_500_000, help="leaves of the config-5 tree (~4/3 as many nodes)")
-    ap.add_argument("--c5-tau", type=float, default=3.0, help="render_hierarchy.py tau (pixels)")
+    ap.add_argument("--c5-tau", type=float, default=15.0,
+                    help="render_hierarchy.py tau in pixels (its default list: 0, 3, 6, 15)")
+    ap.add_argument("--c5-log-scale", type=float, default=-6.0,
+                    help="mean log leaf scale of the config-5 tree (-6: ~7.4M-node cut of 50M at tau 15)")
     ap.add_argument("--train-baseline", action="store_true",
                     help="also time the reference-structured torch train step (conv2d SSIM, OurAdam gather/scatter)")
     return ap.parse_args()
@@ -171,7 +174,7 @@ def config5(a, dev):
     from gs_train.hier import interpolate_cut
     from gs_train.synthetic import synthetic_lod_hierarchy, tau_threshold
     W, H = a.width, a.height
-    h = synthetic_lod_hierarchy(a.c5_leaves, W, H, dev, seed=5, skybox=100_000)
+    h = synthetic_lod_hierarchy(a.c5_leaves, W, H, dev, seed=5, skybox=100_000, log_scale_mean=a.c5_log_scale)
     N = h["nodes"].shape[0]
     thr = tau_threshold(a.c5_tau, h["tanfovx"], W)
     t = lambda x: torch.tensor(x, dtype=torch.float32, device=dev)
@@ -224,7 +227,7 @@ def config5(a, dev):
         parts.append([1e3 * (sp[i + 1] - sp[i]) for i in range(3)])
     parts = np.median(np.array(parts), 0)
     out = {"ms_per_frame": round(ms, 3), "fwd_mpix_s": round(W * H / ms / 1e3, 1), "nodes": N,
-           "leaves": a.c5_leaves, "tau": a.c5_tau, "cut": n, "rendered": n + h["skybox"],
+           "leaves": a.c5_leaves, "tau": a.c5_tau, "leaf_log_scale": a.c5_log_scale, "cut": n, "rendered": n + h["skybox"],
            "visible": int((radii > 0).sum().item()), "width": W, "height": H,
            "split_ms": {"cut_and_weights": round(float(parts[0]), 3), "blend": round(float(parts[1]), 3),
                         "raster_fwd": round(float(parts[2]), 3)},
