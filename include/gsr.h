@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 1
+#define GSR_ABI_VERSION 2
 
 typedef enum {
     GSR_OK = 0,
@@ -62,8 +62,14 @@ typedef void *(*gsr_resize_fn)(void *ctx, size_t bytes);
  *   M = shs.shape[1] (coefficient stride), D = active SH degree (0..3, (D+1)^2 <= M).
  *   out_color (3,H,W); out_invdepth (1,H,W) or NULL when do_depth is false; radii (P) int32.
  *   render_indices/parent_indices/interpolation_weights/num_node_kids: the hierarchy-cut
- *   fields.  num_render == 0 (every reference call path) means plain
- *   3DGS and the four pointers are never dereferenced (they may be host pointers).
+ *   fields.  num_render == 0 (every reference call path: render_post blends in Python and
+ *   passes empty ones) means plain 3DGS and the four pointers are never dereferenced (they may
+ *   be host pointers).  num_render = R > 0: the P input rows are a hierarchy's Gaussians and the
+ *   frame renders the R rows render_post's blend would produce (gaussian_renderer/__init__.py:
+ *   200-220; row r = t * x[render_indices[r]] + (1 - t) * x[parent_indices[r]], parent
+ *   quaternions sign-aligned, t = interpolation_weights[r], parent -1 = the last row); needs shs,
+ *   scales and rotations; the three arrays are device int32 / int32 / float32 of >= R entries;
+ *   radii then has R entries.  num_node_kids is accepted and not read (render_post ignores it).
  *   *num_rendered receives K, the number of tile instances. */
 int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffer, gsr_resize_fn image_buffer,
                           void *resize_ctx, int P, int D, int M, const float *background, int width, int height,
@@ -77,6 +83,9 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
                           int debug, void *stream, int64_t *num_rendered);
 
 /* Backward.  geom/binning/image are the pointers the forward's callbacks returned; R = K.
+ * The hierarchy-cut fields must be the forward's; with num_render > 0 the gradients of the P
+ * input rows are those of render_post's blend (shared parents summed) and dL_dmeans2D holds the
+ * rendered rows' screen-space gradient in rows [0, num_render), zero below.
  * dL_dpix (3,H,W); dL_dinvdepth (1,H,W) or NULL (no depth gradient).  `scratch` provides
  * the per-tile-instance gradient workspace.  Every output row is written (zeros where
  * radii == 0 and beyond the active SH degree), so outputs need no pre-zeroing:
@@ -94,7 +103,9 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
                            void *binning_buffer, void *image_buffer, const float *dL_dpix,
                            const float *dL_dinvdepth, float *dL_dmeans2D, float *dL_dcolors, float *dL_dopacity,
                            float *dL_dmeans3D, float *dL_dcov3D, float *dL_dsh, float *dL_dscales,
-                           float *dL_drotations, int debug, void *stream);
+                           float *dL_drotations, const int *render_indices, const int *parent_indices,
+                           const float *interpolation_weights, const int *num_node_kids, int num_render,
+                           int debug, void *stream);
 
 /* Frustum test (view-space z > 0.2), present[P] as bytes 0/1. */
 int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,

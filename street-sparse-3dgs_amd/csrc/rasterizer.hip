@@ -13,6 +13,7 @@
 #include <algorithm>
 
 #include "../../include/gsr.h"
+#include "../../include/gsr_hier.h"
 #include "gsr_launch.h"
 
 using namespace gsr;
@@ -210,6 +211,62 @@ BwdScratch carve_bwd(void *base, int64_t K, int P, size_t *bytes) {
     return s;
 }
 
+// Rows blended from the hierarchy cut when render_indices is non-empty (gsr.h): carved after the
+// geometry state, read back by the backward from the same buffer.
+struct CutRows {
+    float *means, *scales, *rots, *opac, *shs;
+};
+
+CutRows carve_cut(Carver &c, int R, int M) {
+    CutRows r;
+    r.means = c.take<float>(3 * (size_t)R);
+    r.scales = c.take<float>(3 * (size_t)R);
+    r.rots = c.take<float>(4 * (size_t)R);
+    r.opac = c.take<float>((size_t)R);
+    r.shs = c.take<float>(3 * (size_t)M * R);
+    return r;
+}
+
+size_t geom_bytes(int P, int gx, int gy, int R, int M) {
+    size_t b = 0;
+    carve_geom(nullptr, P, gx, gy, &b);
+    if (R > 0) {
+        Carver c(nullptr);
+        c.off = b;
+        carve_cut(c, R, M);
+        b = align_up(c.off, 256);
+    }
+    return b;
+}
+
+CutRows cut_rows_of(void *geom, int P, int gx, int gy, int M) {
+    size_t b = 0;
+    carve_geom(nullptr, P, gx, gy, &b);
+    Carver c(geom);
+    c.off = b;
+    return carve_cut(c, P, M);
+}
+
+int validate_cut(int R, int64_t N, const float *shs, const float *scales, const float *rotations,
+                 const int *render_indices, const int *parent_indices, const float *interpolation_weights) {
+    if (R < 0) return fail(GSR_ERR_INVALID_ARGUMENT, "num_render must be >= 0");
+    if (R == 0) return GSR_OK;
+    if (!shs || !scales || !rotations)
+        return fail(GSR_ERR_UNSUPPORTED,
+                    "render_indices needs shs, scales and rotations (render_post's blend is defined for them only)");
+    if (!render_indices || !parent_indices || !interpolation_weights)
+        return fail(GSR_ERR_INVALID_ARGUMENT, "render_indices given without parent_indices / interpolation_weights");
+    if (N <= 0) return fail(GSR_ERR_INVALID_ARGUMENT, "render_indices given with no Gaussians");
+    for (const void *p : {(const void *)render_indices, (const void *)parent_indices,
+                          (const void *)interpolation_weights}) {
+        hipPointerAttribute_t a;
+        if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeDevice)
+            return fail(GSR_ERR_INVALID_ARGUMENT, "render_indices / parent_indices / interpolation_weights must be "
+                                                  "device memory when non-empty");
+    }
+    return GSR_OK;
+}
+
 Camera make_camera(const float *view, const float *proj, const float *campos, float tanx, float tany, int W, int H) {
     Camera c;
     c.view = view;
@@ -299,18 +356,14 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
                           const float *interpolation_weights, const int *num_node_kids, int num_render,
                           int debug, void *stream, int64_t *num_rendered) {
     (void)prefiltered;
-    (void)render_indices;
-    (void)parent_indices;
-    (void)interpolation_weights;
-    (void)num_node_kids;
+    (void)num_node_kids;  // accepted; render_post's blend (which this reproduces) does not read it
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (num_rendered) *num_rendered = 0;
     int rc = validate_common(P, D, M, shs, colors_precomp, scales, rotations, cov3D_precomp, width, height);
     if (rc) return rc;
-    if (num_render != 0)
-        return fail(GSR_ERR_UNSUPPORTED,
-                    "in-kernel hierarchy interpolation (non-empty render_indices) is not implemented; every "
-                    "reference call path passes empty render_indices (SURVEY.md 0.6)");
+    if ((rc = validate_cut(num_render, P, shs, scales, rotations, render_indices, parent_indices,
+                           interpolation_weights)))
+        return rc;
     if (!geom_buffer || !binning_buffer || !image_buffer)
         return fail(GSR_ERR_INVALID_ARGUMENT, "resize callbacks must be non-NULL");
     if (!background || !out_color || !viewmatrix || !projmatrix || !cam_pos || (P > 0 && !radii))
@@ -318,20 +371,40 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
     if (P > 0 && (!means3D || !opacities))
         return fail(GSR_ERR_INVALID_ARGUMENT, "NULL means3D / opacities");
 
+    // Hierarchy cut: the rasterizer renders the num_render rows blended from (render_indices,
+    // parent_indices, interpolation_weights) over the P input rows -- render_post's LOD blend
+    // (gaussian_renderer/__init__.py:200-243) done here, into the geometry buffer.
+    const int64_t Nin = P;
+    const int R = num_render;
+    if (R > 0) P = R;
+
     const Camera cam = make_camera(viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, width, height);
     const int T = cam.gx * cam.gy;
     const int npix = width * height;
 
-    size_t gbytes = 0, ibytes = 0;
-    carve_geom(nullptr, P, cam.gx, cam.gy, &gbytes);
+    size_t ibytes = 0;
+    const size_t gbytes = geom_bytes(P, cam.gx, cam.gy, R, M);
     if (!sb_grid_supported(sb_grid(cam.gx, cam.gy, P)))
-        return fail(GSR_ERR_UNSUPPORTED, "image too large for the superblock grid (more than 2048 superblocks of 16x16 tiles)");
+        return fail(GSR_ERR_UNSUPPORTED, "image too large for the superblock grid");
     carve_image(nullptr, T, npix, &ibytes);
     void *gbase = geom_buffer(resize_ctx, gbytes);
     void *ibase = image_buffer(resize_ctx, ibytes);
     if (!gbase || !ibase) return fail(GSR_ERR_ALLOCATION, "geometry/image buffer allocation failed");
     const GeomState gs = carve_geom(gbase, P, cam.gx, cam.gy, nullptr);
     const ImageState is = carve_image(ibase, T, npix, nullptr);
+    if (R > 0) {
+        const CutRows cr = cut_rows_of(gbase, P, cam.gx, cam.gy, M);
+        if ((rc = gsr_interpolate_cut_forward(Nin, M, R, 0, render_indices, parent_indices, interpolation_weights,
+                                              means3D, scales, rotations, opacities, shs, cr.means, cr.scales,
+                                              cr.rots, cr.opac, cr.shs, stream)))
+            return rc;
+        means3D = cr.means;
+        scales = cr.scales;
+        rotations = cr.rots;
+        opacities = cr.opac;
+        shs = cr.shs;
+        if ((rc = check("hierarchy cut blend", debug, s))) return rc;
+    }
 
     GaussianInputs in{P, D, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp,
                       scale_modifier};
@@ -482,7 +555,7 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
     return GSR_OK;
 }
 
-int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D, int M, int64_t R,
+int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D, int M, int64_t R_inst,
                            const float *background, int width, int height, const float *means3D,
                            const float *shs, const float *colors_precomp, const float *scales,
                            float scale_modifier, const float *rotations, const float *cov3D_precomp,
@@ -491,11 +564,17 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
                            void *binning_buffer, void *image_buffer, const float *dL_dpix,
                            const float *dL_dinvdepth, float *dL_dmeans2D, float *dL_dcolors, float *dL_dopacity,
                            float *dL_dmeans3D, float *dL_dcov3D, float *dL_dsh, float *dL_dscales,
-                           float *dL_drotations, int debug, void *stream) {
+                           float *dL_drotations, const int *render_indices, const int *parent_indices,
+                           const float *interpolation_weights, const int *num_node_kids, int num_render,
+                           int debug, void *stream) {
+    (void)num_node_kids;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int rc = validate_common(P, D, M, shs, colors_precomp, scales, rotations, cov3D_precomp, width, height);
     if (rc) return rc;
-    if (R < 0) return fail(GSR_ERR_INVALID_ARGUMENT, "num_rendered must be >= 0");
+    if ((rc = validate_cut(num_render, P, shs, scales, rotations, render_indices, parent_indices,
+                           interpolation_weights)))
+        return rc;
+    if (R_inst < 0) return fail(GSR_ERR_INVALID_ARGUMENT, "num_rendered must be >= 0");
     if (!scratch) return fail(GSR_ERR_INVALID_ARGUMENT, "scratch callback must be non-NULL");
     if (!geom_buffer || !binning_buffer || !image_buffer || !dL_dpix)
         return fail(GSR_ERR_INVALID_ARGUMENT, "NULL state buffer / dL_dpix");
@@ -508,24 +587,58 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
         return fail(GSR_ERR_INVALID_ARGUMENT, "NULL dL_dscales / dL_drotations");
     if ((rc = sticky_sort_error())) return rc;
 
+    const int64_t Nin = P;
+    const int R = num_render;
+    const float *rotations_in = rotations;
+    if (R > 0) P = R;
     const Camera cam = make_camera(viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, width, height);
     const int T = cam.gx * cam.gy;
     const GeomState gs = carve_geom(geom_buffer, P, cam.gx, cam.gy, nullptr);
-    const BinningState bs = carve_binning(binning_buffer, R, nullptr);
+    const BinningState bs = carve_binning(binning_buffer, R_inst, nullptr);
     const ImageState is = carve_image(image_buffer, T, width * height, nullptr);
     size_t sbytes = 0;
-    carve_bwd(nullptr, R, P, &sbytes);
+    carve_bwd(nullptr, R_inst, P, &sbytes);
+    // hierarchy cut: gradients of the R blended rows first, then scattered to the input rows
+    size_t cut_off = 0;
+    if (R > 0) {
+        Carver c(nullptr);
+        c.off = sbytes;
+        carve_cut(c, R, M);
+        cut_off = sbytes;
+        sbytes = align_up(c.off, 256);
+    }
     void *sbase = scratch(resize_ctx, sbytes);
     if (!sbase) return fail(GSR_ERR_ALLOCATION, "backward scratch allocation failed");
-    const BwdScratch sc = carve_bwd(sbase, R, P, nullptr);
+    const BwdScratch sc = carve_bwd(sbase, R_inst, P, nullptr);
 
-    GaussianInputs in{P, D, M, means3D, shs, colors_precomp, nullptr, scales, rotations, cov3D_precomp,
-                      scale_modifier};
     GaussianGrads out{dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
                       dL_drotations};
+    CutRows rows{}, grows{};
+    if (R > 0) {
+        rows = cut_rows_of(geom_buffer, P, cam.gx, cam.gy, M);
+        Carver c(sbase);
+        c.off = cut_off;
+        grows = carve_cut(c, R, M);
+        means3D = rows.means;
+        scales = rows.scales;
+        rotations = rows.rots;
+        shs = rows.shs;
+        out.dmeans3D = grows.means;
+        out.dscales = grows.scales;
+        out.drots = grows.rots;
+        out.dopacity = grows.opac;
+        out.dsh = grows.shs;
+        // means2D: the rendered rows' screen-space gradient lands in rows [0, R) of the input's
+        // gradient (render_post slices means2D[:R + skybox] the same way); the rest is zero
+        if (Nin > R && hipMemsetAsync(dL_dmeans2D + 3 * (size_t)R, 0, sizeof(float) * 3 * (size_t)(Nin - R), s) !=
+                           hipSuccess)
+            return fail(GSR_ERR_DEVICE, "means2D gradient clear failed");
+    }
+    GaussianInputs in{P, D, M, means3D, shs, colors_precomp, nullptr, scales, rotations, cov3D_precomp,
+                      scale_modifier};
     {
         StageTimer st(6, s);
-        if (R > 0) launch_render_bwd(cam, gs, bs, is, radii, background, dL_dpix, dL_dinvdepth, sc, s);
+        if (R_inst > 0) launch_render_bwd(cam, gs, bs, is, radii, background, dL_dpix, dL_dinvdepth, sc, s);
     }
     if ((rc = check("render backward", debug, s))) return rc;
     {
@@ -533,6 +646,20 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
         launch_preprocess_bwd(in, cam, gs, is, radii, sc, out, s);
     }
     if ((rc = check("preprocess backward", debug, s))) return rc;
+    if (R > 0) {
+        const size_t n3 = sizeof(float) * 3 * (size_t)Nin;
+        if (hipMemsetAsync(dL_dmeans3D, 0, n3, s) != hipSuccess || hipMemsetAsync(dL_dscales, 0, n3, s) != hipSuccess ||
+            hipMemsetAsync(dL_drotations, 0, sizeof(float) * 4 * (size_t)Nin, s) != hipSuccess ||
+            hipMemsetAsync(dL_dopacity, 0, sizeof(float) * (size_t)Nin, s) != hipSuccess ||
+            hipMemsetAsync(dL_dsh, 0, sizeof(float) * 3 * (size_t)M * Nin, s) != hipSuccess)
+            return fail(GSR_ERR_DEVICE, "gradient clear failed");
+        if ((rc = gsr_interpolate_cut_backward(Nin, M, R, 0, render_indices, parent_indices, interpolation_weights,
+                                               rotations_in, grows.means,
+                                               grows.scales, grows.rots, grows.opac, grows.shs, dL_dmeans3D,
+                                               dL_dscales, dL_drotations, dL_dopacity, dL_dsh, stream)))
+            return rc;
+        if ((rc = check("hierarchy cut blend backward", debug, s))) return rc;
+    }
     return GSR_OK;
 }
 

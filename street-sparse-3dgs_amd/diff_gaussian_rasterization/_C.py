@@ -129,12 +129,13 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     bg_c = _dev_f32(background, "bg", dev)
     if P > 0 and opac_c is None:
         raise RuntimeError("opacities must be provided")
-    n_render = 0 if render_indices is None else int(render_indices.numel())
+    n_render, ri_c, pi_c, w_c, kids_c = _cut_args(render_indices, parent_indices, interpolation_weights,
+                                                  num_node_kids, dev)
 
     out_color = torch.empty(3, H, W, dtype=torch.float32, device=dev)
     # written for every pixel when do_depth; zeros otherwise (callers ignore it)
     out_invdepth = (torch.empty if do_depth else torch.zeros)(1, H, W, dtype=torch.float32, device=dev)
-    radii = torch.empty(P, dtype=torch.int32, device=dev)
+    radii = torch.empty(n_render if n_render > 0 else P, dtype=torch.int32, device=dev)
     res = _Resizer(dev)
     K = ctypes.c_int64(0)
     with torch.cuda.device(dev):
@@ -143,10 +144,27 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
             _ptr(means3D_c), _ptr(sh_c), _ptr(colors_c), _ptr(opac_c), _ptr(scales_c), float(scale_modifier),
             _ptr(rots_c), _ptr(cov_c), _ptr(view_c), _ptr(proj_c), _ptr(campos_c), float(tan_fovx),
             float(tan_fovy), int(bool(prefiltered)), _ptr(out_color), _ptr(out_invdepth) if do_depth else None,
-            _ptr(radii), None, None, None, None, n_render, int(bool(debug)), _stream(dev), ctypes.byref(K))
+            _ptr(radii), _ptr(ri_c), _ptr(pi_c), _ptr(w_c), _ptr(kids_c), n_render, int(bool(debug)), _stream(dev),
+            ctypes.byref(K))
     res.release()
     _check(rc, "rasterize_gaussians")
     return int(K.value), out_color, out_invdepth, radii, res.get("geom"), res.get("binning"), res.get("image")
+
+
+def _cut_args(render_indices, parent_indices, interpolation_weights, num_node_kids, dev):
+    """The hierarchy-cut fields: empty render_indices (every reference caller) -> nothing is
+    passed; non-empty ones must come with parent_indices / interpolation_weights of at least as
+    many entries, on the device (include/gsr.h)."""
+    n = 0 if render_indices is None else int(render_indices.numel())
+    if n == 0:
+        return 0, None, None, None, None
+    if parent_indices is None or interpolation_weights is None or parent_indices.numel() < n or \
+            interpolation_weights.numel() < n:
+        raise RuntimeError("render_indices needs parent_indices and interpolation_weights of at least as many entries")
+    i32 = lambda t: t.to(device=dev, dtype=torch.int32).contiguous()
+    kids = i32(num_node_kids) if num_node_kids is not None and num_node_kids.numel() else None
+    return n, i32(render_indices), i32(parent_indices), \
+        interpolation_weights.to(device=dev, dtype=torch.float32).contiguous(), kids
 
 
 _ZEROS = {}
@@ -178,6 +196,8 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     dpix = f(dL_dout_color, "dL_dout_color")
     dinv = f(dL_dout_invdepth, "dL_dout_invdepth") if dL_dout_invdepth is not None else None
     radii_c = radii.contiguous()
+    n_render, ri_c, pi_c, w_c, kids_c = _cut_args(render_indices, parent_indices, interpolation_weights,
+                                                  num_node_kids, dev)
 
     e = lambda *shape: torch.empty(*shape, dtype=torch.float32, device=dev)
     # gradients of inputs that were not given are identically zero: returned as zero-stride views
@@ -201,7 +221,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
             _ptr(dL_dcolors) if sh_c is None else None, _ptr(dL_dopacity), _ptr(dL_dmeans3D),
             _ptr(dL_dcov3D) if cov_c is not None else None, _ptr(dL_dsh) if sh_c is not None else None,
             _ptr(dL_dscales) if cov_c is None else None, _ptr(dL_drotations) if cov_c is None else None,
-            int(bool(debug)), _stream(dev))
+            _ptr(ri_c), _ptr(pi_c), _ptr(w_c), _ptr(kids_c), n_render, int(bool(debug)), _stream(dev))
     res.release()
     _check(rc, "rasterize_gaussians_backward")
     return dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations

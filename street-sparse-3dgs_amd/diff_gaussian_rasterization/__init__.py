@@ -23,8 +23,9 @@ from . import _C
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "_C"]
 
 
-def cpu_deep_copy_tuple(input_tuple):
-    return tuple(item.cpu().clone() if isinstance(item, torch.Tensor) else item for item in input_tuple)
+def _host_copy(args):
+    """Host copies of the call's tensors, kept so a failing debug-mode call can be replayed."""
+    return tuple(a.cpu().clone() if isinstance(a, torch.Tensor) else a for a in args)
 
 
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
@@ -50,14 +51,15 @@ class _RasterizeGaussians(torch.autograd.Function):
                 _hier(rs, "parent_indices"), _hier(rs, "interpolation_weights"), _hier(rs, "num_node_kids"),
                 do_depth)
         if rs.debug:
-            cpu_args = cpu_deep_copy_tuple(args)
+            saved = _host_copy(args)
             try:
                 num_rendered, color, invdepth, radii, geomBuffer, binningBuffer, imgBuffer = \
                     _C.rasterize_gaussians(*args)
-            except Exception as ex:
-                torch.save(cpu_args, "snapshot_fw.dump")
-                print("\nAn error occured in forward. Please forward snapshot_fw.dump for debugging.")
-                raise ex
+            except Exception:
+                torch.save(saved, "snapshot_fw.dump")
+                print("\n[diff_gaussian_rasterization] forward failed in debug mode; its inputs are in "
+                      "snapshot_fw.dump (torch.load it and call _C.rasterize_gaussians(*args) to replay)")
+                raise
         else:
             num_rendered, color, invdepth, radii, geomBuffer, binningBuffer, imgBuffer = _C.rasterize_gaussians(*args)
 
@@ -86,13 +88,14 @@ class _RasterizeGaussians(torch.autograd.Function):
                 ctx.num_rendered, binningBuffer, imgBuffer, _hier(rs, "render_indices"), _hier(rs, "parent_indices"),
                 _hier(rs, "interpolation_weights"), _hier(rs, "num_node_kids"), rs.debug)
         if rs.debug:
-            cpu_args = cpu_deep_copy_tuple(args)
+            saved = _host_copy(args)
             try:
                 grads = _C.rasterize_gaussians_backward(*args)
-            except Exception as ex:
-                torch.save(cpu_args, "snapshot_bw.dump")
-                print("\nAn error occured in backward. Writing snapshot_bw.dump for debugging.\n")
-                raise ex
+            except Exception:
+                torch.save(saved, "snapshot_bw.dump")
+                print("\n[diff_gaussian_rasterization] backward failed in debug mode; its inputs are in "
+                      "snapshot_bw.dump (replay with _C.rasterize_gaussians_backward(*args))")
+                raise
         else:
             grads = _C.rasterize_gaussians_backward(*args)
         (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_sh, grad_scales,
@@ -132,7 +135,7 @@ class GaussianRasterizer(nn.Module):
         self.raster_settings = raster_settings
 
     def markVisible(self, positions):
-        # Mark visible points (based on frustum culling for camera) with a boolean
+        """Boolean mask of the positions in front of the camera's near plane (view z > 0.2)."""
         with torch.no_grad():
             rs = self.raster_settings
             visible = _C.mark_visible(positions, rs.viewmatrix, rs.projmatrix)

@@ -38,7 +38,7 @@ SIGNATURES = {
                                    ctypes.POINTER(_i64)]),
     "gsr_rasterize_backward": (_i, [RESIZE_FN, _vp, _i, _i, _i, _i64, _vp, _i, _i, _vp, _vp, _vp, _vp, _f,
                                     _vp, _vp, _vp, _vp, _vp, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp,
-                                    _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
+                                    _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp]),
     "gsr_mark_visible": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
     "gsr_set_profiling": (_i, [_i]),
     "gsr_stage_times_ms": (_i, [ctypes.POINTER(_f), _i]),
@@ -81,7 +81,7 @@ SIGNATURES = {
                                           _vp, _vp, _vp, _vp, _vp]),
 }
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 _lib = None
 
 

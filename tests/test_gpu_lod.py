@@ -109,3 +109,58 @@ def test_config5_end_to_end_vs_oracle():
     p = psnr(cpu(color), st["color"])
     assert p >= 80.0, p
     assert float(np.mean(np.abs(cpu(color) - st["color"]) > 1e-4)) <= 1e-3
+
+
+def test_rasterizer_render_indices_equal_render_post_blend():
+    """Non-empty render_indices in the rasterizer (the blend done inside gsr_rasterize_forward)
+    against render_post's order of work (interpolate_cut, then the rasterizer on the R rows):
+    identical image / radii / K; gradients of the N hierarchy rows equal up to the order of the
+    float atomics that sum shared parents; means2D's gradient in rows [0, R)."""
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    from gs_train.hier import interpolate_cut
+    from gs_train.synthetic import synthetic_lod_hierarchy, tau_threshold
+    W, H = 640, 360
+    h = synthetic_lod_hierarchy(60_000, W, H, DEV, seed=9, zmin=1.0, zmax=12.0, log_scale_mean=-3.5)
+    thr = tau_threshold(20.0, h["tanfovx"], W)
+    n, ri, pi, ni, w, k = _cut_hip(h, thr)
+    N = h["means3D"].shape[0]
+    assert 0 < n < N
+    t = lambda x: torch.tensor(x, dtype=torch.float32, device=DEV)
+    g = torch.Generator(device=DEV).manual_seed(1)
+    gc = torch.randn(3, H, W, generator=g, device=DEV)
+    gd = torch.randn(1, H, W, generator=g, device=DEV)
+
+    def settings(ri_, pi_, w_):
+        return GaussianRasterizationSettings(
+            image_height=H, image_width=W, tanfovx=float(h["tanfovx"]), tanfovy=float(h["tanfovy"]),
+            bg=t([0.3, 0.2, 0.1]), scale_modifier=1.0, viewmatrix=t(h["view"]).reshape(4, 4),
+            projmatrix=t(h["proj"]).reshape(4, 4), sh_degree=3, campos=t(h["campos"]), prefiltered=False,
+            debug=False, do_depth=True, render_indices=ri_, parent_indices=pi_, interpolation_weights=w_,
+            num_node_kids=k)
+
+    def leaves():
+        return [h[x].detach().clone().requires_grad_(True) for x in ("means3D", "scales", "rotations", "opacities",
+                                                                      "shs")]
+
+    # (a) inside the rasterizer
+    m, sc, rot, op, sh = leaves()
+    m2a = torch.zeros(N, 3, device=DEV, requires_grad=True)
+    ca, ra, da = GaussianRasterizer(settings(ri[:n], pi, w))(means3D=m, means2D=m2a, shs=sh, opacities=op,
+                                                             scales=sc, rotations=rot)
+    ((ca * gc).sum() + (da * gd).sum()).backward()
+    ga = [x.grad for x in (m, sc, rot, op, sh)]
+    # (b) render_post's order: blend, then rasterize the R rows
+    m, sc, rot, op, sh = leaves()
+    bm, bs, br, bo, bsh = interpolate_cut(m, sc, rot, op, sh, ri[:n], pi, w, 0)
+    m2b = torch.zeros(n, 3, device=DEV, requires_grad=True)
+    e = torch.empty(0, dtype=torch.int32)
+    cb, rb, db = GaussianRasterizer(settings(e, e, torch.empty(0, device=DEV)))(
+        means3D=bm, means2D=m2b, shs=bsh, opacities=bo, scales=bs, rotations=br)
+    ((cb * gc).sum() + (db * gd).sum()).backward()
+    gb = [x.grad for x in (m, sc, rot, op, sh)]
+    assert torch.equal(ca, cb) and torch.equal(da, db) and torch.equal(ra, rb)
+    assert ra.shape[0] == n
+    for name, x, y in zip(("means3D", "scales", "rotations", "opacities", "shs"), ga, gb):
+        err = float((x - y).norm() / y.norm().clamp_min(1e-30))
+        assert err <= 1e-6, (name, err)
+    assert torch.equal(m2a.grad[:n], m2b.grad) and int(m2a.grad[n:].abs().sum()) == 0
