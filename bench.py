@@ -51,7 +51,8 @@ def parse():
     ap.add_argument("--c5-log-scale", type=float, default=-6.0,
                     help="mean log leaf scale of the config-5 tree (-6: ~7.4M-node cut of 50M at tau 15)")
     ap.add_argument("--train-baseline", action="store_true",
-                    help="also time the reference-structured torch train step (conv2d SSIM, OurAdam gather/scatter)")
+                    help="also time the reference-structured torch train step (oracle/train_torch_ref.py: conv2d "
+                         "SSIM, OurAdam gather/scatter) -- a baseline leg, like cpu_baseline")
     return ap.parse_args()
 
 
@@ -137,18 +138,21 @@ def psnr_vs_oracle(gpu_color, gpu_invd, st):
     return out
 
 
-def train_step_ms(s, W, H, deg, steps, warmup, fused, dev):
-    """one train_single.py iteration (render + exposure + L1/SSIM loss +
-    backward + densification stats + exposure Adam + sparse Adam + scale clamp) on the bench
-    scene; wall time per step between synchronisations (the harness itself never syncs when
-    fused)."""
+def train_step_ms(P, W, H, steps, warmup, dev, street=True, reference=False):
+    """one train_single.py iteration on the bench scene (1M Gaussians at
+    1080p, perturbed), wall time per step between synchronisations (the fused step never syncs).
+    street=True: the Street-sparse iteration -- 4 training views cycled, the masked inverse-depth
+    L1 (train_single.py:133-141, weight schedule 1.0 -> 0.01), the first 10k rows a locked skybox
+    (:217-223), exposure and xyz lr schedules.  street=False: photometric loss only, one fixed
+    view (round 1's number, kept as a labelled variant).  reference=True: the same step in the
+    reference's torch formulation (oracle/train_torch_ref.py, a baseline leg)."""
     import torch
-    from gs_train.harness import GaussianSet, TrainStep
-    g = GaussianSet(s["means3D"], s["shs"], s["opacities"], s["scales"], s["rotations"], n_images=1,
-                    sh_degree=deg, device=dev, joined_features=fused)
-    gen = torch.Generator(device=dev).manual_seed(123)
-    gt = torch.rand((3, H, W), device=dev, generator=gen)
-    ts = TrainStep(g, [(s["view"], s["proj"], s["campos"], s["tanfovx"], s["tanfovy"])], [gt], W, H, fused=fused)
+    from gs_train.harness import make_problem
+    step_cls = None
+    if reference:
+        from train_torch_ref import ReferenceTrainStep as step_cls
+    ts = make_problem(P, W, H, n_views=4 if street else 1, seed=0, step_cls=step_cls, depth=street,
+                      skybox_points=10_000 if street else 0)
     for _ in range(warmup):
         ts.step()
     torch.cuda.synchronize()
@@ -157,7 +161,7 @@ def train_step_ms(s, W, H, deg, steps, warmup, fused, dev):
         ts.step()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / steps * 1e3
-    del ts, g
+    del ts
     torch.cuda.empty_cache()
     return ms
 
@@ -388,12 +392,19 @@ def main():
                               if serial_ms > 0 else None},
     }
     if a.train_steps > 0:
-        tr = {"ms": round(train_step_ms(s, W, H, deg, a.train_steps, 5, True, dev), 4),
-              "workload": f"train_single.py iteration on the bench scene ({P} Gaussians, {W}x{H}): render, exposure, "
-                          f"0.8 L1 + 0.2 (1 - SSIM), backward, densify stats, exposure Adam, sparse Adam, scale clamp",
-              "steps": a.train_steps, "fused": True}
+        from diff_gaussian_rasterization import _C as _Cstats
+        r0 = _Cstats.forward_stats()
+        tr = {"ms": round(train_step_ms(P, W, H, a.train_steps, 5, dev), 4),
+              "workload": f"Street-sparse train_single.py iteration on the bench scene ({P} Gaussians, {W}x{H}, 4 views "
+                          f"cycled): render, exposure, 0.8 L1 + 0.2 (1 - SSIM) + masked inverse-depth L1, backward "
+                          f"(depth gradient on), densify stats, exposure Adam, skybox lock (10k rows), sparse Adam, "
+                          f"scale clamp",
+              "steps": a.train_steps}
+        r1 = _Cstats.forward_stats()
+        tr["binning_reruns"] = r1["reruns"] - r0["reruns"]
+        tr["photo_only_fixed_view_ms"] = round(train_step_ms(P, W, H, a.train_steps, 5, dev, street=False), 4)
         if a.train_baseline:
-            tr["reference_structured_ms"] = round(train_step_ms(s, W, H, deg, a.train_steps, 5, False, dev), 4)
+            tr["reference_structured_ms"] = round(train_step_ms(P, W, H, a.train_steps, 5, dev, reference=True), 4)
         out["train_step"] = tr
     if a.config5:
         out["config5"] = config5(a, dev)

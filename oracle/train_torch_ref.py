@@ -1,6 +1,8 @@
-"""The reference's own torch formulation of the train-step pieces, run on the GPU for the
-side-by-side "train-step ms" number (harness.TrainStep(fused=False)).  Not the product path and
-not a fallback: the fused kernels never route here.
+"""TEST INFRASTRUCTURE / BASELINE LEG ONLY -- the reference's own torch formulation of the
+train-step pieces, run on the GPU as the checker of the fused kernels (tests/) and for the bench's
+side-by-side "reference-structured train-step ms" (ReferenceTrainStep).  Not the product path and
+not a fallback: the fused kernels never route here, and nothing under street-sparse-3dgs_amd/
+imports this module.
 
   photo_loss           utils/loss_utils.py:17-63 (five depthwise 11x11 conv2d) as combined at
                        train_single.py:121-123
@@ -8,6 +10,9 @@ not a fallback: the fused kernels never route here.
                        update as separate torch ops, scatter back; dense when nothing is relevant
   densification_stats  train_single.py:193-194 + scene/gaussian_model.py:780-793 with the
                        nonzero()-built visibility filter of gaussian_renderer/__init__.py:124-135
+  ReferenceTrainStep   gs_train.harness.TrainStep with every hook in the reference's formulation
+                       (train_single.py:65-247)
+  densify_and_prune    scene/gaussian_model.py:560-778 (the checker of gs_train.densify)
 """
 from __future__ import annotations
 
@@ -192,3 +197,70 @@ def densify_and_prune(g, opt, max_grad, min_opacity, extent, percent_dense, firs
     prune[:first_row] = False
     _prune_points(g, opt, prune)
     g.max_radii2D = torch.zeros((g._xyz.shape[0]), device=dev)
+
+
+# ---- one train_single.py iteration in the reference's formulation ------------------------------
+def _reference_step_cls():
+    from gs_train.harness import LR, TrainStep
+
+    class ReferenceTrainStep(TrainStep):
+        """TrainStep with the reference's torch pieces: get_* activations, matmul exposure,
+        conv2d SSIM, the torch depth-L1 expression, nonzero()-built filters, OurAdam's per-group
+        gather/scatter, the six-gradient skybox zeroing, boolean-mask scale shrink."""
+        JOINED_FEATURES = False
+
+        def _make_optimizers(self, groups):
+            if self.g.joined:
+                raise ValueError("the reference-structured step needs the reference's split SH layout")
+            self.optimizer = OurAdamTorch(groups, lr=0.0, eps=1e-15)
+            self.exposure_optimizer = torch.optim.Adam([self.g._exposure])
+
+        def _means2D_leaf(self):
+            m = torch.zeros_like(self.g._xyz, requires_grad=True) + 0
+            m.retain_grad()
+            return m
+
+        def _activations(self):
+            g = self.g
+            return g.get_scaling, g.get_rotation, g.get_opacity
+
+        def _apply_exposure(self, color, E):
+            image = torch.matmul(color.permute(1, 2, 0), E[:3, :3]).permute(2, 0, 1) + E[:3, 3, None, None]
+            return image.clamp(0, 1)
+
+        def _photo_loss(self, image, gt):
+            return photo_loss(image, gt, LR["lambda_dssim"])
+
+        def _depth_loss(self, invd, mono, mask, w):
+            m = mask if mask is not None else torch.ones_like(invd)
+            return w * torch.abs((invd - mono) * m).mean()
+
+        def _backward(self, loss):
+            loss.backward()
+
+        def _densify_stats(self, radii, grad2d):
+            densification_stats(self.g, radii, grad2d)
+
+        def _lock_skybox(self):
+            g, S = self.g, self.skybox
+            for p in (g._xyz, g._rotation, g._features_dc, g._features_rest, g._opacity, g._scaling):
+                if p.grad is not None:
+                    p.grad[:S] = 0
+
+        def _sparse_step(self):
+            relevant = (self.g._opacity.grad.flatten() != 0).nonzero().flatten().long()
+            self.optimizer.step(relevant)
+
+        def _shrink(self):
+            g = self.g
+            sc = g.get_scaling
+            bad = sc.max(dim=1).values > self.extent * 0.02
+            g._scaling[bad] = torch.log(sc[bad] * 0.8)
+
+    return ReferenceTrainStep
+
+
+def __getattr__(name):
+    if name == "ReferenceTrainStep":
+        return _reference_step_cls()
+    raise AttributeError(name)

@@ -898,6 +898,79 @@ bool ssim_tiled() {
     return e != nullptr && e[0] == '1';
 }
 
+
+// ---- masked inverse-depth L1 (train_single.py:135-141) ----------------------------------------
+// forward: per-block partial sums of |(invd - mono) * mask| (fp32 per thread over a float4 stride,
+// fp64 across threads and blocks), then mean and weight; backward: torch's chain
+// w -> / N -> * sgn(d) -> * mask for d = (invd - mono) * mask, in that order (bit-identical to
+// autograd through the reference's expression).
+constexpr int kDepthThreads = 256;
+constexpr int kDepthPerBlock = 4 * kDepthThreads * 4;  // float4 per thread, 4 strides
+
+__device__ __forceinline__ float depth_term(float x, float y, float m) { return (x - y) * m; }
+
+__global__ __launch_bounds__(kDepthThreads) void depth_l1_fwd_kernel(const float *__restrict__ invd,
+                                                                    const float *__restrict__ mono,
+                                                                    const float *__restrict__ mask, int64_t n,
+                                                                    double *__restrict__ partials) {
+    __shared__ double red[kDepthThreads / 64];
+    const int64_t b0 = (int64_t)blockIdx.x * kDepthPerBlock;
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int64_t i = b0 + 4 * ((int64_t)k * kDepthThreads + threadIdx.x);
+        if (i + 3 < n) {
+            const float4 x = *reinterpret_cast<const float4 *>(invd + i);
+            const float4 y = *reinterpret_cast<const float4 *>(mono + i);
+            const float4 m = mask ? *reinterpret_cast<const float4 *>(mask + i) : make_float4(1.f, 1.f, 1.f, 1.f);
+            acc += fabsf(depth_term(x.x, y.x, m.x)) + fabsf(depth_term(x.y, y.y, m.y)) +
+                   fabsf(depth_term(x.z, y.z, m.z)) + fabsf(depth_term(x.w, y.w, m.w));
+        } else {
+            for (int64_t j = i; j < n && j < i + 4; j++) acc += fabsf(depth_term(invd[j], mono[j], mask ? mask[j] : 1.f));
+        }
+    }
+    double v = acc;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int k = 0; k < kDepthThreads / 64; k++) t += red[k];
+        partials[blockIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(1024) void depth_l1_finalize_kernel(const double *__restrict__ partials, int nb,
+                                                                 double inv_n, float w, float *__restrict__ out) {
+    __shared__ double red[1024];
+    double a = 0.0;
+    for (int i = threadIdx.x; i < nb; i += 1024) a += partials[i];
+    red[threadIdx.x] = a;
+    __syncthreads();
+    for (int k = 512; k > 0; k >>= 1) {
+        if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out[0] = (float)(red[0] * inv_n);       // Ll1depth_pure
+        out[1] = __fmul_rn(w, out[0]);          // depth_l1_weight(iteration) * Ll1depth_pure
+    }
+}
+
+__global__ __launch_bounds__(256) void depth_l1_bwd_kernel(const float *__restrict__ invd, const float *__restrict__ mono,
+                                                           const float *__restrict__ mask, int64_t n,
+                                                           const float *__restrict__ gout, float w, float count,
+                                                           float *__restrict__ dinvd) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float g = __fdiv_rn(__fmul_rn(gout[0], w), count);
+    const float m = mask ? mask[i] : 1.f;
+    const float d = depth_term(invd[i], mono[i], m);
+    const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+    dinvd[i] = __fmul_rn(__fmul_rn(g, sg), m);
+}
+
 bool g_lds_attr = false;
 
 void set_lds_attr() {
@@ -1237,6 +1310,58 @@ int gsr_shrink_scales(int64_t P, int64_t first_row, float *scaling_raw, float ma
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_last_error(std::string("gsr_shrink_scales: ") + hipGetErrorString(e));
+        return GSR_ERR_DEVICE;
+    }
+    return GSR_OK;
+}
+
+size_t gsr_depth_l1_scratch_bytes(int64_t n) {
+    return sizeof(double) * (size_t)std::max<int64_t>(1, (n + kDepthPerBlock - 1) / kDepthPerBlock);
+}
+
+int gsr_depth_l1_forward(const float *invdepth, const float *mono_invdepth, const float *mask, int64_t n,
+                         float weight, void *scratch, float *out2, void *stream) {
+    if (n < 0 || (n > 0 && (!invdepth || !mono_invdepth || !scratch)) || !out2) {
+        set_last_error("gsr_depth_l1_forward: bad size or NULL pointer");
+        return GSR_ERR_INVALID_ARGUMENT;
+    }
+    const bool aligned = (reinterpret_cast<uintptr_t>(invdepth) | reinterpret_cast<uintptr_t>(mono_invdepth) |
+                          reinterpret_cast<uintptr_t>(mask)) % 16 == 0;
+    if (!aligned) {
+        set_last_error("gsr_depth_l1_forward: arrays must be 16-byte aligned");
+        return GSR_ERR_INVALID_ARGUMENT;
+    }
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int nb = (int)std::max<int64_t>(1, (n + kDepthPerBlock - 1) / kDepthPerBlock);
+    double *part = static_cast<double *>(scratch);
+    if (n > 0)
+        hipLaunchKernelGGL(depth_l1_fwd_kernel, dim3(nb), dim3(kDepthThreads), 0, s, invdepth, mono_invdepth, mask, n,
+                           part);
+    else if (hipMemsetAsync(part, 0, sizeof(double), s) != hipSuccess)
+        return GSR_ERR_DEVICE;
+    hipLaunchKernelGGL(depth_l1_finalize_kernel, dim3(1), dim3(1024), 0, s, part, nb,
+                       n > 0 ? 1.0 / (double)n : 0.0, weight, out2);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_last_error(std::string("gsr_depth_l1_forward: ") + hipGetErrorString(e));
+        return GSR_ERR_DEVICE;
+    }
+    return GSR_OK;
+}
+
+int gsr_depth_l1_backward(const float *invdepth, const float *mono_invdepth, const float *mask, int64_t n,
+                          float weight, const float *dL_dloss, float *dL_dinvdepth, void *stream) {
+    if (n < 0 || (n > 0 && (!invdepth || !mono_invdepth || !dL_dloss || !dL_dinvdepth))) {
+        set_last_error("gsr_depth_l1_backward: bad size or NULL pointer");
+        return GSR_ERR_INVALID_ARGUMENT;
+    }
+    if (n == 0) return GSR_OK;
+    hipLaunchKernelGGL(depth_l1_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), invdepth, mono_invdepth, mask, n, dL_dloss, weight,
+                       (float)n, dL_dinvdepth);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_last_error(std::string("gsr_depth_l1_backward: ") + hipGetErrorString(e));
         return GSR_ERR_DEVICE;
     }
     return GSR_OK;

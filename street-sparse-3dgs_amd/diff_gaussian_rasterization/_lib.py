@@ -61,6 +61,9 @@ SIGNATURES = {
     "gsr_activate_forward": (_i, [_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gsr_activate_backward": (_i, [_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gsr_shrink_scales": (_i, [_i64, _i64, _vp, _f, _vp]),
+    "gsr_depth_l1_scratch_bytes": (ctypes.c_size_t, [_i64]),
+    "gsr_depth_l1_forward": (_i, [_vp, _vp, _vp, _i64, _f, _vp, _vp, _vp]),
+    "gsr_depth_l1_backward": (_i, [_vp, _vp, _vp, _i64, _f, _vp, _vp, _vp]),
     "gsr_exposure_forward": (_i, [_vp, _vp, _i64, _vp, _vp]),
     "gsr_exposure_scratch_bytes": (ctypes.c_size_t, [_i64]),
     "gsr_exposure_backward": (_i, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),

@@ -2,23 +2,29 @@
 (train_single.py:65-247) on the MI355X path, used for the "train-step ms" half of the metric.
 
 Per step, as the reference does it:
-  1. xyz learning-rate schedule (scene/gaussian_model.py:447-457, utils/general_utils.py:31-70)
+  1. learning-rate schedules: xyz and exposure (scene/gaussian_model.py:447-457,
+     utils/general_utils.py:31-70)
   2. render(): activations of the raw parameters (scene/gaussian_model.py:39-47,125-156),
      GaussianRasterizer (drop-in), per-image exposure affine and clamp
-     (gaussian_renderer/__init__.py:115-120)
-  3. photometric loss (1 - 0.2) L1 + 0.2 (1 - SSIM) (train_single.py:121-123), plus the
-     inverse-depth L1 when a mono depth map is given (train_single.py:128-137)
-  4. loss.backward()
-  5. densification statistics (train_single.py:193-194)
-  6. exposure Adam step, sparse Adam step on rows with nonzero opacity gradient
-     (train_single.py:212-233), zero_grad(set_to_none=True)
-  7. shrink over-large Gaussians (train_single.py:235-241)
+     (gaussian_renderer/__init__.py:115-120); cameras cycle over the training views
+  3. image *= alpha_mask when the view has one (train_single.py:117-119)
+  4. photometric loss (1 - 0.2) L1 + 0.2 (1 - SSIM) (train_single.py:121-123), plus the masked
+     inverse-depth L1 w(it) |(invDepth - mono_invdepth) * depth_mask|.mean() when the view has a
+     mono depth map (train_single.py:133-141, w = depth_l1_weight: 1.0 -> 0.01 log-linear)
+  5. loss.backward()
+  6. densification statistics (train_single.py:193-194)
+  7. exposure Adam step; the locked skybox rows' gradients zeroed (train_single.py:217-223);
+     sparse Adam on rows with nonzero opacity gradient (train_single.py:225-233);
+     zero_grad(set_to_none=True)
+  8. shrink over-large Gaussians (train_single.py:235-241)
 
-`fused=True` runs the activations, the exposure/clamp and steps 3, 5, 6 and 7 on the csrc/train.hip kernels and keeps the step free of host
-synchronisation; `fused=False` runs the same step with the reference's own torch formulation
-(gs_train.baseline) for the side-by-side number.  Densify/prune, opacity reset, SH degree
-increments and checkpointing run every few hundred/thousand iterations and are out of scope
-(SURVEY.md 8(f) row 4).
+Every piece runs on the csrc/train.hip kernels and the step is free of host synchronisation (the
+reference's .item() calls feed only its progress bar).  The reference-structured formulation of
+the same step (conv2d SSIM, OurAdam gather/scatter, ...) lives in oracle/train_torch_ref.py
+(ReferenceTrainStep, test infrastructure and the bench's baseline leg) and overrides the hook
+methods below.  Densify/prune, opacity reset, SH degree increments and checkpointing run every
+few hundred/thousand iterations and are out of scope (gs_train.densify
+has the densify/prune kernels).  Depth-only views (additional_depth_maps) are not modelled.
 """
 from __future__ import annotations
 
@@ -29,16 +35,17 @@ import torch
 
 from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
 
-from . import baseline
 from .activations import activate, shrink_scales
 from .densify import add_densification_stats
 from .exposure import apply_exposure
-from .loss import photo_loss
+from .loss import depth_l1_loss, photo_loss
 from .optim import Adam
 
 # arguments/__init__.py:89-109 (OptimizationParams defaults)
 LR = dict(position_lr_init=0.00002, position_lr_final=0.0000002, position_lr_delay_mult=0.01,
           position_lr_max_steps=30_000, feature_lr=0.0025, opacity_lr=0.05, scaling_lr=0.005, rotation_lr=0.001,
+          exposure_lr_init=0.001, exposure_lr_final=0.0001, exposure_lr_delay_steps=5000,
+          exposure_lr_delay_mult=0.001, depth_l1_weight_init=1.0, depth_l1_weight_final=0.01, iterations=30_000,
           lambda_dssim=0.2)
 
 
@@ -137,41 +144,95 @@ class GaussianSet:
 
 class TrainStep:
     """cameras: list of (view, proj, campos, tanfovx, tanfovy) numpy tuples (synthetic.camera);
-    gts: list of (3, H, W) device tensors; mono_invdepths: optional list of (1, H, W)."""
+    gts: list of (3, H, W) device tensors.  Optional per view: mono_invdepths (1, H, W),
+    depth_masks (1, H, W) float 0/1 (None entries = no depth supervision for that view) and
+    alpha_masks (1, H, W).  skybox_points: the first rows are the locked skybox
+    (scene/gaussian_model.py:73-74,182-187)."""
 
-    def __init__(self, gaussians: GaussianSet, cameras, gts, W, H, fused=True, cameras_extent=10.0,
-                 mono_invdepths=None, depth_l1_weight=0.0):
+    def __init__(self, gaussians: GaussianSet, cameras, gts, W, H, cameras_extent=10.0, mono_invdepths=None,
+                 depth_masks=None, alpha_masks=None, skybox_points=0, iterations=LR["iterations"]):
         self.g = gaussians
         self.W, self.H = W, H
-        self.fused = fused
         self.extent = cameras_extent
         self.gts = gts
-        self.mono = mono_invdepths
-        self.depth_w = depth_l1_weight
+        n = len(cameras)
+        self.mono = mono_invdepths if mono_invdepths is not None else [None] * n
+        self.dmask = depth_masks if depth_masks is not None else [None] * n
+        self.amask = alpha_masks if alpha_masks is not None else [None] * n
+        self.skybox = int(skybox_points)
         dev = gaussians._xyz.device
         f = lambda a: torch.as_tensor(np.asarray(a), dtype=torch.float32, device=dev)
         self.cams = [dict(view=f(v).reshape(4, 4), proj=f(p).reshape(4, 4), campos=f(c), tx=float(tx), ty=float(ty))
                      for (v, p, c, tx, ty) in cameras]
-        if gaussians.joined and not fused:
-            raise ValueError("the reference-structured step needs the reference's split SH layout")
-        groups = gaussians.param_groups()
-        self.optimizer = Adam(groups, lr=0.0, eps=1e-15) if fused else baseline.OurAdamTorch(groups, lr=0.0,
-                                                                                              eps=1e-15)
-        # the reference's torch.optim.Adam on the exposures; fused: the same update as one dense
-        # launch of the fused kernel (OurAdam's arithmetic: exp_avg by mul + add where torch's
-        # foreach Adam lerps -- an ulp-level difference on 12 floats per image)
-        self.exposure_optimizer = (Adam([gaussians._exposure], lr=1e-3, eps=1e-8) if fused
-                                   else torch.optim.Adam([gaussians._exposure]))
-        self.xyz_lr = lambda it: expon_lr(it, LR["position_lr_init"] * gaussians.spatial_lr_scale,
-                                          LR["position_lr_final"] * gaussians.spatial_lr_scale,
+        self._make_optimizers(gaussians.param_groups())
+        s = gaussians.spatial_lr_scale
+        self.xyz_lr = lambda it: expon_lr(it, LR["position_lr_init"] * s, LR["position_lr_final"] * s,
                                           lr_delay_mult=LR["position_lr_delay_mult"],
                                           max_steps=LR["position_lr_max_steps"])
+        self.exposure_lr = lambda it: expon_lr(it, LR["exposure_lr_init"], LR["exposure_lr_final"],
+                                               lr_delay_steps=LR["exposure_lr_delay_steps"],
+                                               lr_delay_mult=LR["exposure_lr_delay_mult"], max_steps=iterations)
+        self.depth_weight = lambda it: expon_lr(it, LR["depth_l1_weight_init"], LR["depth_l1_weight_final"],
+                                                max_steps=iterations)
         self.iteration = 1
         self._means2D = None
         self._one = None
         self.empty_i = torch.empty(0, dtype=torch.int32)
         self.empty_f = torch.empty(0, device=dev)
         self.empty_id = torch.empty(0, dtype=torch.int32, device=dev)
+
+    # ---- the pieces (fused kernels here; oracle/train_torch_ref.py restates them in torch) ----
+    def _make_optimizers(self, groups):
+        if not self.g.joined:
+            raise ValueError("the fused step keeps the SH coefficients as one (P, 16, 3) parameter")
+        self.optimizer = Adam(groups, lr=0.0, eps=1e-15)
+        # the reference's torch.optim.Adam on the exposures, as one dense launch of the fused kernel
+        # (OurAdam's arithmetic: exp_avg by mul + add where torch's foreach Adam lerps -- an
+        # ulp-level difference on 12 floats per image)
+        self.exposure_optimizer = Adam([self.g._exposure], lr=LR["exposure_lr_init"], eps=1e-8)
+
+    def _means2D_leaf(self):
+        # the rasterizer never reads means2D's values (it only carries dL/dmeans2D): one zero leaf
+        # per Gaussian count, its .grad reset each step
+        g = self.g
+        if self._means2D is None or self._means2D.shape != g._xyz.shape:
+            self._means2D = torch.zeros_like(g._xyz, requires_grad=True)
+        self._means2D.grad = None
+        return self._means2D
+
+    def _activations(self):
+        g = self.g
+        return activate(g._scaling, g._rotation, g._opacity)
+
+    def _apply_exposure(self, color, E):
+        return apply_exposure(color, E)
+
+    def _photo_loss(self, image, gt):
+        return photo_loss(image, gt, LR["lambda_dssim"])[0]
+
+    def _depth_loss(self, invd, mono, mask, w):
+        return depth_l1_loss(invd, mono, mask, w)
+
+    def _backward(self, loss):
+        if self._one is None:
+            self._one = torch.ones((), device=loss.device)
+        loss.backward(self._one)  # = loss.backward() without the ones_like fill launch
+
+    def _densify_stats(self, radii, grad2d):
+        g = self.g
+        add_densification_stats(radii, grad2d, g.max_radii2D, g.xyz_gradient_accum, g.denom)
+
+    def _lock_skybox(self):
+        # train_single.py:217-223 zeroes all six gradients of the skybox rows; the rows then have a
+        # zero opacity gradient, so the sparse step skips them -- zeroing that one gradient is the
+        # whole effect (the others are discarded by zero_grad)
+        self.g._opacity.grad[:self.skybox] = 0
+
+    def _sparse_step(self):
+        self.optimizer.step(relevance=self.g._opacity.grad)
+
+    def _shrink(self):
+        shrink_scales(self.g._scaling, self.extent * 0.02)
 
     def render(self, cam_idx, bg):
         c = self.cams[cam_idx]
@@ -181,91 +242,69 @@ class TrainStep:
             viewmatrix=c["view"], projmatrix=c["proj"], sh_degree=g.active_sh_degree, campos=c["campos"],
             prefiltered=False, debug=False, do_depth=True, render_indices=self.empty_i, parent_indices=self.empty_i,
             interpolation_weights=self.empty_f, num_node_kids=self.empty_id)
-        if self.fused:
-            # the rasterizer never reads means2D's values (it only carries dL/dmeans2D): one
-            # zero leaf per Gaussian count, its .grad reset each step, instead of zeros + 0
-            if self._means2D is None or self._means2D.shape != g._xyz.shape:
-                self._means2D = torch.zeros_like(g._xyz, requires_grad=True)
-            means2D = self._means2D
-            means2D.grad = None
-        else:
-            means2D = torch.zeros_like(g._xyz, requires_grad=True) + 0
-            if means2D.requires_grad:
-                means2D.retain_grad()
-        if self.fused:
-            scales, rotations, opacities = activate(g._scaling, g._rotation, g._opacity)
-        else:
-            scales, rotations, opacities = g.get_scaling, g.get_rotation, g.get_opacity
+        means2D = self._means2D_leaf()
+        scales, rotations, opacities = self._activations()
         color, radii, invd = GaussianRasterizer(rs)(means3D=g.get_xyz, means2D=means2D, shs=g.get_features,
                                                     colors_precomp=None, opacities=opacities, scales=scales,
                                                     rotations=rotations, cov3D_precomp=None)
-        E = g._exposure[cam_idx]
-        if self.fused:
-            return apply_exposure(color, E), invd, means2D, radii
-        image = torch.matmul(color.permute(1, 2, 0), E[:3, :3]).permute(2, 0, 1) + E[:3, 3, None, None]
-        return image.clamp(0, 1), invd, means2D, radii
+        return self._apply_exposure(color, g._exposure[cam_idx]), invd, means2D, radii
 
     def step(self, cam_idx=None):
-        """One iteration; returns the loss tensor (no host synchronisation when fused)."""
+        """One iteration; returns the loss tensor (no host synchronisation on the fused path)."""
         g = self.g
         it = self.iteration
         k = (it - 1) % len(self.cams) if cam_idx is None else cam_idx
         for pg in self.optimizer.param_groups:
             if pg["name"] == "xyz":
                 pg["lr"] = self.xyz_lr(it)
+        for pg in self.exposure_optimizer.param_groups:
+            pg["lr"] = self.exposure_lr(it)
         bg = torch.rand(3, device=g._xyz.device)
         image, invd, means2D, radii = self.render(k, bg)
-        gt = self.gts[k]
-        if self.fused:
-            loss, l1, s = photo_loss(image, gt, LR["lambda_dssim"])
-        else:
-            loss = baseline.photo_loss(image, gt, LR["lambda_dssim"])
-        if self.mono is not None and self.depth_w > 0:
-            loss = loss + self.depth_w * torch.abs(invd - self.mono[k]).mean()
-        if self.fused:
-            if self._one is None:
-                self._one = torch.ones((), device=loss.device)
-            loss.backward(self._one)  # = loss.backward() without the ones_like fill launch
-        else:
-            loss.backward()
+        if self.amask[k] is not None:
+            image = image * self.amask[k]
+        loss = self._photo_loss(image, self.gts[k])
+        w = self.depth_weight(it)
+        if self.mono[k] is not None and w > 0:
+            loss = loss + self._depth_loss(invd, self.mono[k], self.dmask[k], w)
+        self._backward(loss)
         with torch.no_grad():
-            if self.fused:
-                add_densification_stats(radii, means2D.grad, g.max_radii2D, g.xyz_gradient_accum, g.denom)
-            else:
-                baseline.densification_stats(g, radii, means2D.grad)
+            self._densify_stats(radii, means2D.grad)
             self.exposure_optimizer.step()
             self.exposure_optimizer.zero_grad(set_to_none=True)
-            if self.fused:
-                self.optimizer.step(relevance=g._opacity.grad)
-            else:
-                relevant = (g._opacity.grad.flatten() != 0).nonzero().flatten().long()
-                self.optimizer.step(relevant)
+            if self.skybox > 0 and g._opacity.grad is not None:
+                self._lock_skybox()
+            self._sparse_step()
             self.optimizer.zero_grad(set_to_none=True)
-            # train_single.py:235-241: shrink Gaussians larger than 2% of the scene extent
-            if self.fused:
-                shrink_scales(g._scaling, self.extent * 0.02)
-            else:
-                sc = g.get_scaling
-                bad = sc.max(dim=1).values > self.extent * 0.02
-                g._scaling[bad] = torch.log(sc[bad] * 0.8)
+            self._shrink()  # train_single.py:235-241: shrink Gaussians larger than 2% of the extent
         self.iteration += 1
         return loss.detach()
 
 
-def make_problem(P, W, H, n_views=4, seed=0, sh_degree=3, device="cuda", fused=True, perturb=0.02):
-    """A synthetic training problem: ground-truth views rendered from a seeded scene, and a
-    TrainStep that starts from a perturbed copy of it."""
+def make_problem(P, W, H, n_views=4, seed=0, sh_degree=3, device="cuda", step_cls=None, perturb=0.02,
+                 depth=True, depth_mask_frac=0.85, alpha=False, skybox_points=0):
+    """A synthetic Street-sparse training problem: ground-truth views and inverse-depth maps
+    rendered from a seeded scene over `n_views` orbit cameras, depth masks (a random ~85% of each
+    map valid, as the reference's depth_mask), optional alpha masks, and a step (TrainStep, or
+    `step_cls`, e.g. oracle/train_torch_ref.ReferenceTrainStep) that starts from a perturbed copy.
+    The mono depth maps are the true inverse depth with 5% multiplicative noise."""
     from .synthetic import orbit_cameras, synthetic_scene
+    step_cls = step_cls or TrainStep
     s = synthetic_scene(P, W, H, seed=seed, sh_degree=sh_degree)
     cams = orbit_cameras(n_views, W, H)
     truth = GaussianSet(s["means3D"], s["shs"], s["opacities"], s["scales"], s["rotations"], n_images=n_views,
-                        sh_degree=sh_degree, device=device)
-    tmp = TrainStep(truth, cams, [None] * n_views, W, H, fused=fused)
-    gts = []
+                        sh_degree=sh_degree, device=device, joined_features=True)
+    tmp = TrainStep(truth, cams, [None] * n_views, W, H)
+    gen = torch.Generator(device=device).manual_seed(seed + 7)
+    gts, monos, dmasks, amasks = [], [], [], []
     with torch.no_grad():
         for k in range(n_views):
-            img, _, _, _ = tmp.render(k, torch.zeros(3, device=device))
+            img, invd, _, _ = tmp.render(k, torch.zeros(3, device=device))
             gts.append(img.contiguous())
+            noise = 1.0 + 0.05 * torch.randn(invd.shape, generator=gen, device=device)
+            monos.append((invd * noise).contiguous())
+            dmasks.append((torch.rand(invd.shape, generator=gen, device=device) < depth_mask_frac).float())
+            amasks.append((torch.rand(invd.shape, generator=gen, device=device) < 0.97).float())
     rng = np.random.default_rng(seed + 99)
     noisy = dict(means3D=s["means3D"] + perturb * rng.normal(size=s["means3D"].shape).astype(np.float32),
                  shs=s["shs"] + perturb * rng.normal(size=s["shs"].shape).astype(np.float32),
@@ -273,5 +312,7 @@ def make_problem(P, W, H, n_views=4, seed=0, sh_degree=3, device="cuda", fused=T
                  rotations=s["rotations"])
     model = GaussianSet(noisy["means3D"], noisy["shs"], noisy["opacities"], noisy["scales"].astype(np.float32),
                         noisy["rotations"], n_images=n_views, sh_degree=sh_degree, device=device,
-                        joined_features=fused)
-    return TrainStep(model, cams, gts, W, H, fused=fused)
+                        joined_features=getattr(step_cls, "JOINED_FEATURES", True))
+    return step_cls(model, cams, gts, W, H, mono_invdepths=monos if depth else None,
+                    depth_masks=dmasks if depth else None, alpha_masks=amasks if alpha else None,
+                    skybox_points=skybox_points)

@@ -117,3 +117,48 @@ def photo_loss(img: torch.Tensor, gt: torch.Tensor, lambda_dssim: float = 0.2):
     v = l1_ssim(img, gt)
     l1, s = v[0], v[1]
     return (1.0 - lambda_dssim) * l1 + lambda_dssim * (1.0 - s), l1, s
+
+
+class _DepthL1(torch.autograd.Function):
+    """w * mean(|(invdepth - mono) * mask|) as one node (include/gsr_train.h gsr_depth_l1_*):
+    train_single.py:138-140's Ll1depth.  The gradient w.r.t. invdepth is bit-identical to torch's
+    autograd through the reference's expression; the value is the fp64-accumulated mean (torch
+    sums in fp32: they agree to fp32 rounding)."""
+
+    @staticmethod
+    def forward(ctx, invd, mono, mask, weight):
+        require_gpu(invd, mono, mask)
+        if invd.shape != mono.shape or (mask is not None and mask.shape != invd.shape):
+            raise ValueError("invdepth, mono_invdepth and depth_mask must have one shape")
+        x = invd.detach().float().contiguous()
+        y = mono.detach().float().contiguous()
+        m = mask.detach().float().contiguous() if mask is not None else None
+        n = x.numel()
+        L = lib()
+        out = torch.empty(2, dtype=torch.float32, device=x.device)
+        scratch = torch.empty(max(8, int(L.gsr_depth_l1_scratch_bytes(n))), dtype=torch.uint8, device=x.device)
+        check(L.gsr_depth_l1_forward(ptr(x), ptr(y), ptr(m), n, float(weight), ptr(scratch), ptr(out),
+                                     stream(x.device)), "gsr_depth_l1_forward")
+        ctx.save_for_backward(x, y, m)
+        ctx.weight = float(weight)
+        ctx.set_materialize_grads(False)
+        loss, pure = out[1], out[0]
+        ctx.mark_non_differentiable(pure)
+        return loss, pure
+
+    @staticmethod
+    def backward(ctx, gloss, _gpure):
+        if gloss is None:
+            return None, None, None, None
+        x, y, m = ctx.saved_tensors
+        d = torch.empty_like(x)
+        check(lib().gsr_depth_l1_backward(ptr(x), ptr(y), ptr(m), x.numel(), ctx.weight,
+                                          ptr(gloss.float().contiguous()), ptr(d), stream(x.device)),
+              "gsr_depth_l1_backward")
+        return d, None, None, None
+
+
+def depth_l1_loss(invd: torch.Tensor, mono: torch.Tensor, mask: torch.Tensor | None, weight: float):
+    """depth_l1_weight * |(invDepth - mono_invdepth) * depth_mask|.mean()  (train_single.py:138-140),
+    differentiable w.r.t. invd.  Returns the weighted loss (a 0-dim tensor)."""
+    return _DepthL1.apply(invd, mono, mask, weight)[0]

@@ -1,5 +1,5 @@
 """GPU parity of the fused densify-and-prune (csrc/densify.hip, include/gsr_densify.h) with the
-reference's own formulation (gs_train.baseline.densify_and_prune, a transcription of
+reference's own formulation (oracle/train_torch_ref.densify_and_prune, a transcription of
 scene/gaussian_model.py:560-778) on the same state and the same generator stream: row order,
 counts, every parameter and both Adam moments bit-exact, except the split children's xyz, which
 the reference forms with torch.bmm (library summation order; 1e-6 relative)."""
@@ -34,7 +34,7 @@ def _state(P, seed):
 
 def _optimizers(a, b, rng):
     from gs_train import Adam
-    from gs_train.baseline import OurAdamTorch
+    from train_torch_ref import OurAdamTorch
     oa = Adam(a.param_groups(), lr=0.0, eps=1e-15)
     ob = OurAdamTorch(b.param_groups(), lr=0.0, eps=1e-15)
     mom = {}
@@ -57,7 +57,7 @@ def _optimizers(a, b, rng):
 
 @pytest.mark.parametrize("P,first_row", [(50_000, 0), (20_011, 300)])
 def test_densify_and_prune_matches_reference(P, first_row):
-    from gs_train.baseline import densify_and_prune as ref
+    from train_torch_ref import densify_and_prune as ref
     from gs_train.densify import densify_and_prune
     a, b, rng = _state(P, 3)
     oa, ob = _optimizers(a, b, rng)
@@ -89,7 +89,7 @@ def test_densify_then_train_step_runs():
     """The densified set keeps training: the optimizer's groups point at the new parameters."""
     from gs_train.densify import densify_and_prune
     from gs_train.harness import make_problem
-    ts = make_problem(20_000, 256, 192, n_views=2, seed=4, fused=True)
+    ts = make_problem(20_000, 256, 192, n_views=2, seed=4)
     for _ in range(3):
         ts.step()
     g = ts.g

@@ -190,19 +190,24 @@ def test_densify_stats_matches_reference():
     np.testing.assert_array_equal(den.cpu().numpy(), d["denom_after"])
 
 
-def test_train_step_fused_matches_reference_structured_step():
+@pytest.mark.parametrize("depth,alpha,skybox", [(False, False, 0), (True, True, 500)])
+def test_train_step_fused_matches_reference_structured_step(depth, alpha, skybox):
+    """The fused Street-sparse iteration against the reference's torch formulation of it
+    (oracle/train_torch_ref.ReferenceTrainStep): with and without the masked inverse-depth L1,
+    the alpha mask and a locked skybox."""
     from gs_train.harness import make_problem
+    from train_torch_ref import ReferenceTrainStep
+    names = ("_xyz", "_features_dc", "_opacity", "_scaling", "_rotation")
     steps = {}
     for fused in (True, False):
         torch.manual_seed(0)
-        ts = make_problem(20_000, 256, 192, n_views=3, seed=1, fused=fused)
-        losses = []
-        for _ in range(3):
-            losses.append(ts.step().item())
-        steps[fused] = (losses, [p.detach().clone() for p in (ts.g._xyz, ts.g._features_dc, ts.g._opacity,
-                                                                  ts.g._scaling, ts.g._rotation)],
-                        ts.g.xyz_gradient_accum.clone(), ts.g.denom.clone())
-    (la, pa, aa, da), (lb, pb, ab, db) = steps[True], steps[False]
+        ts = make_problem(20_000, 256, 192, n_views=3, seed=1, step_cls=None if fused else ReferenceTrainStep,
+                          depth=depth, alpha=alpha, skybox_points=skybox)
+        init = [getattr(ts.g, n).detach().clone() for n in names]
+        losses = [ts.step().item() for _ in range(3)]
+        steps[fused] = (losses, [getattr(ts.g, n).detach().clone() for n in names], ts.g.xyz_gradient_accum.clone(),
+                        ts.g.denom.clone(), init)
+    (la, pa, aa, da, ia), (lb, pb, ab, db, _) = steps[True], steps[False]
     np.testing.assert_allclose(la, lb, rtol=1e-5, atol=1e-6)
     # Adam's first steps move each element by ~lr * sign(grad): an element whose gradient is
     # fp32 noise around zero may legitimately go the other way, so compare the bulk.
@@ -211,12 +216,43 @@ def test_train_step_fused_matches_reference_structured_step():
         assert close >= 0.999, close
     assert torch.equal(da, db)
     assert torch.isclose(aa, ab, rtol=1e-3, atol=1e-9).float().mean().item() >= 0.999
+    if skybox:  # the locked rows never move (the scale shrink aside, which the reference applies to them too)
+        for x, x0, name in zip(pa, ia, names):
+            if name != "_scaling":
+                assert torch.equal(x[:skybox], x0[:skybox]), name
+
+
+def test_depth_l1_node_matches_torch_expression():
+    """gs_train.loss.depth_l1_loss vs train_single.py:138-140 through torch autograd: value to fp32
+    rounding (fp64 accumulation here), dL/dinvdepth bit-identical (including sgn(0) = 0 where the
+    mask or the difference is zero)."""
+    from gs_train.loss import depth_l1_loss
+    g = torch.Generator(device=DEV).manual_seed(5)
+    for H, W in ((1080, 1920), (37, 53)):
+        invd = torch.rand(1, H, W, generator=g, device=DEV)
+        mono = invd * (1 + 0.1 * torch.randn(1, H, W, generator=g, device=DEV))
+        mono[:, :3] = invd[:, :3]  # exact zeros of the difference
+        mask = (torch.rand(1, H, W, generator=g, device=DEV) < 0.8).float()
+        w = 0.73
+        a = invd.clone().requires_grad_(True)
+        la = depth_l1_loss(a, mono, mask, w)
+        la.backward()
+        b = invd.clone().requires_grad_(True)
+        lb = w * torch.abs((b - mono) * mask).mean()
+        lb.backward()
+        assert abs(la.item() - lb.item()) <= 2e-6 * abs(lb.item())
+        assert torch.equal(a.grad, b.grad)
+        c = invd.clone().requires_grad_(True)
+        depth_l1_loss(c, mono, None, w).backward()
+        d = invd.clone().requires_grad_(True)
+        (w * torch.abs(d - mono).mean()).backward()
+        assert torch.equal(c.grad, d.grad)
 
 
 def test_train_step_reduces_loss():
     from gs_train.harness import make_problem
     torch.manual_seed(0)
-    ts = make_problem(20_000, 256, 192, n_views=2, seed=2, fused=True, perturb=0.05)
+    ts = make_problem(20_000, 256, 192, n_views=2, seed=2, perturb=0.05)
     first = [ts.step().item() for _ in range(2)]
     for _ in range(40):
         ts.step()

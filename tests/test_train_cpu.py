@@ -1,5 +1,5 @@
 """CPU tests of the train-step row: the oracle
-(oracle/train_ref.py) and the reference-structured baseline (gs_train.baseline) are pinned to
+(oracle/train_ref.py) and the reference-structured baseline (oracle/train_torch_ref.py) are pinned to
 the fixtures the reference's own loss_utils / OurAdam / get_expon_lr_func produced
 (tests/golden/make_train_golden.py); host logic of gs_train is checked without a GPU."""
 from __future__ import annotations
@@ -22,7 +22,7 @@ def _gold(name):
 
 @pytest.mark.parametrize("mod", ["oracle", "baseline"])
 def test_loss_matches_reference_fixtures(mod):
-    from gs_train import baseline
+    import train_torch_ref as baseline
     d = _gold("loss.npz")
     for k in range(int(d["n"])):
         img = torch.tensor(d[f"img_{k}"], requires_grad=True)
@@ -61,7 +61,7 @@ def test_oracle_sparse_adam_matches_reference_ouradam():
 
 
 def test_baseline_ouradam_matches_reference_ouradam():
-    from gs_train import baseline
+    import train_torch_ref as baseline
     d = _gold("adam.npz")
     params = [torch.nn.Parameter(torch.tensor(d[f"init_{n}"])) for n in NAMES]
     opt = baseline.OurAdamTorch([{"params": [p], "lr": float(lr), "name": n}

@@ -3,15 +3,9 @@
 import cProfile, pstats, sys, time, io
 sys.path.insert(0, "/root/repo"); sys.path.insert(0, "/root/repo/street-sparse-3dgs_amd")
 import torch
-import bench
-from gs_train.harness import GaussianSet, TrainStep
-dev = torch.device("cuda", 0)
-P, W, H, deg = 1_000_000, 1920, 1080, 3
-s, inp, gcol, ginv = bench.make_inputs(P, W, H, deg, seed=0, device=dev)
-g = GaussianSet(s["means3D"], s["shs"], s["opacities"], s["scales"], s["rotations"], n_images=1, sh_degree=deg,
-                device=dev, joined_features=True)
-gt = torch.rand((3, H, W), device=dev, generator=torch.Generator(device=dev).manual_seed(123))
-ts = TrainStep(g, [(s["view"], s["proj"], s["campos"], s["tanfovx"], s["tanfovy"])], [gt], W, H, fused=True)
+from gs_train.harness import make_problem
+P, W, H = 1_000_000, 1920, 1080
+ts = make_problem(P, W, H, n_views=4, seed=0, skybox_points=10_000)  # the bench's Street-sparse iteration
 for _ in range(5):
     ts.step()
 torch.cuda.synchronize()

@@ -26,15 +26,12 @@ def main():
     ap.add_argument("--baseline", action="store_true")
     a = ap.parse_args()
     import torch
-    from gs_train.harness import GaussianSet, TrainStep
-    from gs_train.synthetic import synthetic_scene
-    dev = torch.device("cuda", 0)
-    s = synthetic_scene(a.gaussians, a.width, a.height, seed=0)
-    g = GaussianSet(s["means3D"], s["shs"], s["opacities"], s["scales"], s["rotations"], device=dev,
-                    joined_features=not a.baseline)
-    gt = torch.rand((3, a.height, a.width), device=dev)
-    ts = TrainStep(g, [(s["view"], s["proj"], s["campos"], s["tanfovx"], s["tanfovy"])], [gt], a.width, a.height,
-                   fused=not a.baseline)
+    from gs_train.harness import make_problem
+    step_cls = None
+    if a.baseline:
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "oracle"))
+        from train_torch_ref import ReferenceTrainStep as step_cls
+    ts = make_problem(a.gaussians, a.width, a.height, n_views=4, seed=0, step_cls=step_cls, skybox_points=10_000)
     for _ in range(a.warmup):
         ts.step()
     torch.cuda.synchronize()
