@@ -129,7 +129,7 @@ int gsr_shrink_scales(int64_t P, int64_t first_row, float *scaling_raw, float ma
  *   out2[0] = mean(|(invdepth - mono_invdepth) * mask|)   (Ll1depth_pure; mask NULL = all ones)
  *   out2[1] = weight * out2[0]                            (Ll1depth, weight = depth_l1_weight(it))
  * n = H * W elements, 16-byte aligned arrays; scratch of gsr_depth_l1_scratch_bytes(n).  The
- * backward writes dL/dinvdepth = ((dL/dout2[1] * weight) / n) * sgn(d) * mask, d = (invdepth -
+ * backward writes dL/dinvdepth = ((dL/dout2[1] * weight) * (1/n)) * sgn(d) * mask, d = (invdepth -
  * mono) * mask: torch's autograd chain through the reference's expression, bit for bit. */
 size_t gsr_depth_l1_scratch_bytes(int64_t n);
 int gsr_depth_l1_forward(const float *invdepth, const float *mono_invdepth, const float *mask, int64_t n,

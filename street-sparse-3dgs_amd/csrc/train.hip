@@ -902,7 +902,7 @@ bool ssim_tiled() {
 // ---- masked inverse-depth L1 (train_single.py:135-141) ----------------------------------------
 // forward: per-block partial sums of |(invd - mono) * mask| (fp32 per thread over a float4 stride,
 // fp64 across threads and blocks), then mean and weight; backward: torch's chain
-// w -> / N -> * sgn(d) -> * mask for d = (invd - mono) * mask, in that order (bit-identical to
+// * w -> * (1/N) -> * sgn(d) -> * mask for d = (invd - mono) * mask, in that order (bit-identical to
 // autograd through the reference's expression).
 constexpr int kDepthThreads = 256;
 constexpr int kDepthPerBlock = 4 * kDepthThreads * 4;  // float4 per thread, 4 strides
@@ -960,11 +960,13 @@ __global__ __launch_bounds__(1024) void depth_l1_finalize_kernel(const double *_
 
 __global__ __launch_bounds__(256) void depth_l1_bwd_kernel(const float *__restrict__ invd, const float *__restrict__ mono,
                                                            const float *__restrict__ mask, int64_t n,
-                                                           const float *__restrict__ gout, float w, float count,
+                                                           const float *__restrict__ gout, float w, float inv_count,
                                                            float *__restrict__ dinvd) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const float g = __fdiv_rn(__fmul_rn(gout[0], w), count);
+    // MeanBackward divides by the element count as a CPU scalar, which ATen turns into a
+    // multiply by its fp32 reciprocal
+    const float g = __fmul_rn(__fmul_rn(gout[0], w), inv_count);
     const float m = mask ? mask[i] : 1.f;
     const float d = depth_term(invd[i], mono[i], m);
     const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
@@ -1358,7 +1360,7 @@ int gsr_depth_l1_backward(const float *invdepth, const float *mono_invdepth, con
     if (n == 0) return GSR_OK;
     hipLaunchKernelGGL(depth_l1_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                        static_cast<hipStream_t>(stream), invdepth, mono_invdepth, mask, n, dL_dloss, weight,
-                       (float)n, dL_dinvdepth);
+                       1.0f / (float)n, dL_dinvdepth);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_last_error(std::string("gsr_depth_l1_backward: ") + hipGetErrorString(e));

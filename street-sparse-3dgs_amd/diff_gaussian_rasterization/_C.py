@@ -167,6 +167,16 @@ def _cut_args(render_indices, parent_indices, interpolation_weights, num_node_ki
         interpolation_weights.to(device=dev, dtype=torch.float32).contiguous(), kids
 
 
+def _leaf_grad(t, shape, dev):
+    """Output for the gradient of input `t`: a view of the capturing gsr_dist.GradBucket when
+    one owns t (data-parallel training: the all-reduce then needs no cat / copy), else new."""
+    try:
+        import gsr_dist
+    except ImportError:  # the package used without the repo's multi-GPU helpers
+        return torch.empty(shape, dtype=torch.float32, device=dev)
+    return gsr_dist.grad_out(t.data_ptr() if t is not None else None, shape, dev)
+
+
 _ZEROS = {}
 
 
@@ -203,10 +213,11 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     # gradients of inputs that were not given are identically zero: returned as zero-stride views
     # (upstream's shapes, no memory traffic) and not computed by the kernels
     z = lambda *shape: _zero(dev).expand(*shape)
-    dL_dmeans2D, dL_dopacity, dL_dmeans3D = e(P, 3), e(P, 1), e(P, 3)
+    dL_dmeans2D, dL_dopacity = e(P, 3), e(P, 1)
+    dL_dmeans3D = _leaf_grad(means3D, (P, 3), dev)
     dL_dcolors = e(P, 3) if sh_c is None else z(P, 3)
     dL_dcov3D = e(P, 6) if cov_c is not None else z(P, 6)
-    dL_dsh = e(P, M, 3) if sh_c is not None else torch.zeros(P, 0, 3, device=dev)
+    dL_dsh = _leaf_grad(sh, (P, M, 3), dev) if sh_c is not None else torch.zeros(P, 0, 3, device=dev)
     if cov_c is None:
         dL_dscales, dL_drotations = e(P, 3), e(P, 4)
     else:

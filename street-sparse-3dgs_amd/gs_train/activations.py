@@ -33,6 +33,7 @@ class _Activate(torch.autograd.Function):
         check(lib().gsr_activate_forward(P, ptr(s), ptr(q), ptr(o), ptr(scales), ptr(rots), ptr(opac),
                                          stream(s.device)), "gsr_activate_forward")
         ctx.save_for_backward(q, scales, opac)
+        ctx.keys = (scaling.data_ptr(), rotation.data_ptr(), opacity.data_ptr())  # gsr_dist.GradBucket views
         return scales, rots, opac
 
     @staticmethod
@@ -41,7 +42,10 @@ class _Activate(torch.autograd.Function):
         P = q.shape[0]
         z = lambda g, like: torch.zeros_like(like) if g is None else g.float().contiguous()
         g_s, g_q, g_o = z(g_s, scales), z(g_q, q), z(g_o, opac)
-        d_s, d_q, d_o = torch.empty_like(scales), torch.empty_like(q), torch.empty_like(opac)
+        from gsr_dist import grad_out
+        ks, kq, ko = ctx.keys
+        d_s, d_q, d_o = (grad_out(ks, scales.shape, q.device), grad_out(kq, q.shape, q.device),
+                         grad_out(ko, opac.shape, q.device))
         check(lib().gsr_activate_backward(P, ptr(q), ptr(scales), ptr(opac), ptr(g_s), ptr(g_q), ptr(g_o),
                                           ptr(d_s), ptr(d_q), ptr(d_o), stream(q.device)), "gsr_activate_backward")
         return d_s, d_q, d_o

@@ -394,3 +394,36 @@ def test_photo_loss_fused_equals_composed(lam, scale):
     assert torch.equal(loss, loss2) and torch.equal(l1, v[0].detach()) and torch.equal(s, v[1].detach())
     assert torch.equal(x1.grad, x2.grad)
     assert not l1.requires_grad and not s.requires_grad
+
+
+def test_grad_bucket_captures_rasterizer_gradients():
+    """Data-parallel flat bucket (gsr_dist.GradBucket) on the real kernels: inside a capture the
+    rasterizer's dL/dmeans3D, dL/dshs and the activations' raw gradients are written straight into
+    the bucket (the parameters' .grad are views of it) and equal the gradients of an uncaptured
+    backward bit for bit; the world-size-1 all-reduce keeps them in place."""
+    import gsr_dist
+    from gs_train.harness import make_problem
+    ts = make_problem(20_000, 256, 192, n_views=1, seed=3)
+    g = ts.g
+    params = {"xyz": g._xyz, "features": g._features, "opacity": g._opacity, "scaling": g._scaling,
+              "rotation": g._rotation}
+    bg = torch.zeros(3, device=DEV)
+
+    def backward():
+        for p in params.values():
+            p.grad = None
+        image, invd, _, _ = ts.render(0, bg)
+        loss = ts._photo_loss(image, ts.gts[0]) + ts._depth_loss(invd, ts.mono[0], ts.dmask[0], 0.5)
+        loss.backward()
+
+    backward()
+    ref = {k: p.grad.clone() for k, p in params.items()}
+    bucket = gsr_dist.GradBucket(params)
+    with bucket.capture():
+        backward()
+    for k, p in params.items():
+        assert bucket.owns(p), k
+        assert torch.equal(p.grad, ref[k]), k
+    bucket.allreduce()
+    for k, p in params.items():
+        assert bucket.owns(p) and torch.equal(p.grad, ref[k]), k
