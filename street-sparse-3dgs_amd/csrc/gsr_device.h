@@ -179,26 +179,27 @@ __device__ __forceinline__ float sh_channel(int deg, const float *sh, float x, f
 // True if some pixel centre of the box [x0, x1] x [y0, y1] may reach alpha >= 1/255, i.e. the
 // conic form Q(d) = a dx^2 + 2 b dx dy + c dy^2 (power = -Q/2) gets down to tau = 2 ln(255 op)
 // somewhere on the box.  The minimum of the convex Q over a box not containing the centre lies on
-// a face turned towards the centre; each face is a 1-D quadratic minimised in closed form.  A
-// relative + absolute margin on tau keeps the test conservative against the kernels' float
-// evaluation of power and exp, so culling with it never changes an output.
-__device__ __forceinline__ bool ellipse_meets_box(float cx, float cy, float a, float b, float c, float op, float x0,
+// a face turned towards the centre; each face is a 1-D quadratic minimised in closed form.  `tm`
+// is tau with a relative + absolute margin (formed once by the preprocess, GRec.cull_tm) that
+// keeps the test conservative against the kernels' float evaluation of power and exp, so culling
+// with it never changes an output.  The face minimiser comes from an approximate reciprocal: any
+// point of the face bounds the face minimum from above, here by O(ulp^2) of Q -- far inside the
+// margin.
+__device__ __forceinline__ bool ellipse_meets_box(float cx, float cy, float a, float b, float c, float tm, float x0,
                                                   float x1, float y0, float y1) {
     if (!(a > 0.f && c > 0.f)) return true;
     const float X0 = x0 - cx, X1 = x1 - cx, Y0 = y0 - cy, Y1 = y1 - cy;
     const bool outx = X0 > 0.f || X1 < 0.f, outy = Y0 > 0.f || Y1 < 0.f;
     if (!outx && !outy) return true;
-    const float tau = 2.f * 0.6931471805599453f * __builtin_amdgcn_logf(255.f * op);  // v_log_f32 = log2
-    const float tm = fmaf(fabsf(tau), 1.0e-3f, tau) + 1.0e-2f;
     float q = 3.0e38f;
     if (outx) {
         const float xe = X0 > 0.f ? X0 : X1;
-        const float ys = fminf(fmaxf(-b * xe / c, Y0), Y1);
+        const float ys = fminf(fmaxf(-b * xe * __builtin_amdgcn_rcpf(c), Y0), Y1);
         q = fminf(q, fmaf(a * xe, xe, fmaf(2.f * b * xe, ys, c * ys * ys)));
     }
     if (outy) {
         const float ye = Y0 > 0.f ? Y0 : Y1;
-        const float xs = fminf(fmaxf(-b * ye / a, X0), X1);
+        const float xs = fminf(fmaxf(-b * ye * __builtin_amdgcn_rcpf(a), X0), X1);
         q = fminf(q, fmaf(a * xs, xs, fmaf(2.f * b * xs, ye, c * ye * ye)));
     }
     return q <= tm;
@@ -399,7 +400,8 @@ struct alignas(16) GRec {
     float cc, op, ex, ey;     // q1: conic c, opacity, half-extents of the alpha >= 1/255 ellipse
                               //     (ex < 0: can never reach alpha >= 1/255)
     float r, g, b, invd;      // q2: colour, 1 / view depth
-    uint32_t rect0, rectw, dbits, off;  // q3: tile rect x0 | y0 << 16, width; depth bits; (unused)
+    uint32_t rect0, rectw, dbits;       // q3: tile rect x0 | y0 << 16, width; depth bits;
+    float cull_tm;                      //     the cull threshold of ellipse_meets_box
 };
 static_assert(sizeof(GRec) == 64, "GRec must be one 64-B line");
 

@@ -30,7 +30,8 @@ __device__ __forceinline__ float gexp2(float x) { return __builtin_amdgcn_exp2f(
 #define GSR_EXACT_CULL 3  // bit 0: forward, bit 1: backward
 #endif
 
-__device__ __forceinline__ uint32_t sub_block_mask(const float4 &qa, const float4 &qb, float tx0, float ty0) {
+__device__ __forceinline__ uint32_t sub_block_mask(const float4 &qa, const float4 &qb, float tm, float tx0,
+                                                   float ty0) {
     // bit k: the alpha >= 1/255 ellipse of the instance (its box, then the ellipse itself) meets
     // pixel rows ty0+4k..ty0+4k+3
     const float X = qa.x, Y = qa.y, ex = qb.z, ey = qb.w;
@@ -40,7 +41,7 @@ __device__ __forceinline__ uint32_t sub_block_mask(const float4 &qa, const float
     for (int k = 0; k < kPixPerLane; k++) {
         const float y0 = ty0 + (float)(4 * k);
         if (Y + ey >= y0 && Y - ey <= y0 + 3.f &&
-            (!(GSR_EXACT_CULL & 2) || ellipse_meets_box(X, Y, qa.z, qa.w, qb.x, qb.y, tx0, tx0 + 15.f, y0, y0 + 3.f)))
+            (!(GSR_EXACT_CULL & 2) || ellipse_meets_box(X, Y, qa.z, qa.w, qb.x, tm, tx0, tx0 + 15.f, y0, y0 + 3.f)))
             m |= 1u << k;
     }
     return m;
@@ -53,119 +54,30 @@ __device__ __forceinline__ uint32_t lane_prefix(uint64_t mask) {
 // ------------------------------------------------------------------------------------------
 // Forward
 // ------------------------------------------------------------------------------------------
-// Culled 16x4 sub-blocks are skipped with a scalar branch.  Measured on MI355X (1M Gaussians,
-// 1080p): 0.34 ms vs 0.39-0.40 ms for the predicated / LDS-prefetched forms.
-__global__ __launch_bounds__(64) void render_fwd_kernel(
-    const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list, int W, int H, int gx,
-    const GRec *__restrict__ rec, const float *__restrict__ bg, float *__restrict__ out_color,
-    float *__restrict__ out_invd, float *__restrict__ final_T, uint32_t *__restrict__ n_contrib,
-    uint32_t *__restrict__ tile_work, uint32_t *__restrict__ tile_ids, const uint32_t *__restrict__ kdev,
-    uint32_t cap) {
-    if (kdev && *kdev > cap) return;  // the point-list capacity is short: the host re-runs at K
-    __shared__ float4 s_a[kWave];  // x, y, conic.a, conic.b
-    __shared__ float4 s_b[kWave];  // conic.c, opacity, contributor index, sub-block mask
-    __shared__ float4 s_c[kWave];  // r, g, b, 1/depth
+// A 256-thread workgroup per tile, wave w owning the 16x4 sub-block w with one pixel per lane.
+// Each wave walks the tile's list on its own (gather, cull to its sub-block with the exact
+// ellipse-vs-box test, ballot-compact into its own LDS slice) and stops when its own 64 pixels
+// saturate, so a heavy tile is spread over four waves and culled sub-blocks cost nothing.
+//
+// The gather is software-pipelined: while batch b blends, the GRec lines of batch b+1 and the
+// point-list ids of batch b+2 are in flight (two dependent round trips per batch -- id, then the
+// line -- that were otherwise exposed once per batch per wave).
+struct FwdBatch {
+    float4 a, b, c;  // GRec q0..q2
+    float tm;        // GRec.cull_tm
+};
 
-    const int tile = blockIdx.x;
-    const int tx = tile % gx, ty = tile / gx;
-    const int lane = threadIdx.x;
-    const int px = tx * kTile + (lane & 15);
-    const int py0 = ty * kTile + (lane >> 4);
-    const float pfx = (float)px;
-    const float tx0 = (float)(tx * kTile), ty0 = (float)(ty * kTile);
-
-    float T[kPixPerLane], C0[kPixPerLane], C1[kPixPerLane], C2[kPixPerLane], ID[kPixPerLane], pfy[kPixPerLane];
-    uint32_t last[kPixPerLane];
-    bool alive[kPixPerLane];
-#pragma unroll
-    for (int k = 0; k < kPixPerLane; k++) {
-        T[k] = 1.f; C0[k] = C1[k] = C2[k] = ID[k] = 0.f; last[k] = 0;
-        alive[k] = px < W && py0 + 4 * k < H;
-        pfy[k] = (float)(py0 + 4 * k);
-    }
-    const uint2 rg = ranges[tile];
-    for (uint32_t base = rg.x; base < rg.y; base += kWave) {
-        if (!__any(alive[0] || alive[1] || alive[2] || alive[3])) break;
-        const uint32_t n = min((uint32_t)kWave, rg.y - base);
-        uint32_t m = 0;
-        float4 qa, qb, qc;
-        if ((uint32_t)lane < n) {
-            const uint32_t g = point_list[base + lane];
-            const float4 *R = reinterpret_cast<const float4 *>(rec + g);
-            qa = R[0];
-            qb = R[1];
-            qc = R[2];
-            m = sub_block_mask(qa, qb, tx0, ty0);
-        }
-        const uint64_t keep = __ballot(m != 0u);
-        const uint32_t cnt = (uint32_t)__popcll(keep);
-        if (m) {
-            const uint32_t slot = lane_prefix(keep);
-            s_a[slot] = make_float4(qa.x, qa.y, qa.z * kHalfLog2e, qa.w * kLog2e);  // scaled conic: gauss_p2
-            s_b[slot] = make_float4(qb.x * kHalfLog2e, qb.y, __uint_as_float(base - rg.x + (uint32_t)lane + 1u),
-                                    __uint_as_float(m));
-            s_c[slot] = qc;
-        }
-        __syncthreads();
-        for (uint32_t j = 0; j < cnt; j++) {
-            const float4 a = s_a[j];
-            const float4 b = s_b[j];
-            const float4 c = s_c[j];
-            const uint32_t mk = __builtin_amdgcn_readfirstlane(__float_as_uint(b.w));
-            const uint32_t contributor = __builtin_amdgcn_readfirstlane(__float_as_uint(b.z));
-            const float dx = a.x - pfx;
-            const float adxdx = a.z * dx * dx;
-            const float bdx = a.w * dx;
-#pragma unroll
-            for (int k = 0; k < kPixPerLane; k++) {
-                if (!(mk & (1u << k))) continue;  // scalar branch: sub-block k culled
-                const float dy = a.y - pfy[k];
-                const float p2 = gauss_p2(adxdx, bdx, b.x, dy);
-                const float alpha = fminf(0.99f, b.y * gexp2(p2));
-                const bool ok = alive[k] && !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f);
-                const float test_T = T[k] * (1.f - alpha);
-                const bool stop = test_T < 0.0001f;
-                const bool acc = ok && !stop;
-                alive[k] = alive[k] && !(ok && stop);
-                const float w = acc ? alpha * T[k] : 0.f;
-                C0[k] = fmaf(c.x, w, C0[k]);
-                C1[k] = fmaf(c.y, w, C1[k]);
-                C2[k] = fmaf(c.z, w, C2[k]);
-                ID[k] = fmaf(c.w, w, ID[k]);
-                T[k] = acc ? test_T : T[k];
-                last[k] = acc ? contributor : last[k];
-            }
-        }
-        __syncthreads();
-    }
-    // backward work estimate for the launch order of render_bwd: its last contributor position
-    uint32_t wl = last[0];
-#pragma unroll
-    for (int k = 1; k < kPixPerLane; k++) wl = last[k] > wl ? last[k] : wl;
-    wl = wave_max_u32(wl);
-    if (lane == 0) tile_work[tile] = wl;
-    (void)tile_ids;
-    const float b0 = bg[0], b1 = bg[1], b2 = bg[2];
-#pragma unroll
-    for (int k = 0; k < kPixPerLane; k++) {
-        const int py = py0 + 4 * k;
-        if (px < W && py < H) {
-            const int pix = py * W + px;
-            final_T[pix] = T[k];
-            n_contrib[pix] = last[k];
-            out_color[pix] = C0[k] + T[k] * b0;
-            out_color[H * W + pix] = C1[k] + T[k] * b1;
-            out_color[2 * H * W + pix] = C2[k] + T[k] * b2;
-            if (out_invd) out_invd[pix] = ID[k];
-        }
-    }
+// Unconditional loads (lanes past the list end re-read the last entry; their hit test is false):
+// a load under a lane mask would make the compiler join the old and new register values at the
+// end of the branch, which waits for the load right there -- no overlap.
+__device__ __forceinline__ void fwd_gather(const GRec *__restrict__ rec, uint32_t g, FwdBatch &o) {
+    const float4 *R = reinterpret_cast<const float4 *>(rec + g);
+    o.a = R[0];
+    o.b = R[1];
+    o.c = R[2];
+    o.tm = rec[g].cull_tm;
 }
 
-// Sub-block forward: a 256-thread workgroup per tile, wave w owning the 16x4 sub-block w with one
-// pixel per lane.  Each wave walks the tile's list on its own (gather, cull to its sub-block,
-// ballot-compact into its own LDS slice) and stops when its own 64 pixels saturate, so a heavy
-// tile is spread over four waves and culled sub-blocks cost nothing.  The per-pixel blend is the
-// same as render_fwd_kernel's (bit-identical outputs).
 __global__ __launch_bounds__(256) void render_fwd_sb_kernel(
     const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list, int W, int H, int gx,
     const GRec *__restrict__ rec, const float *__restrict__ bg, float *__restrict__ out_color,
@@ -191,21 +103,25 @@ __global__ __launch_bounds__(256) void render_fwd_sb_kernel(
     uint32_t last = 0;
     bool alive = inside;
     const uint2 rg = ranges[tile];
+    // pipeline prologue: batch 0's lines, batch 1's ids (indices clamped to the list)
+    FwdBatch cur;
+    uint32_t gnext = 0;
+    const uint32_t lastpos = rg.y > rg.x ? rg.y - 1u : rg.x;
+    if (rg.y > rg.x) {
+        fwd_gather(rec, point_list[min(rg.x + (uint32_t)lane, lastpos)], cur);
+        gnext = point_list[min(rg.x + kWave + (uint32_t)lane, lastpos)];
+    }
     for (uint32_t base = rg.x; base < rg.y; base += kWave) {
         if (!__any(alive)) break;
-        const uint32_t n = min((uint32_t)kWave, rg.y - base);
-        bool hit = false;
-        float4 qa, qb, qc;
-        if ((uint32_t)lane < n) {
-            const uint32_t g = point_list[base + lane];
-            const float4 *R = reinterpret_cast<const float4 *>(rec + g);
-            qa = R[0];
-            qb = R[1];
-            qc = R[2];
-            hit = qa.x + qb.z >= tx0 && qa.x - qb.z <= tx0 + 15.f && qa.y + qb.w >= sy0 && qa.y - qb.w <= sy0 + 3.f &&
-                  (!(GSR_EXACT_CULL & 1) ||
-                   ellipse_meets_box(qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, tx0, tx0 + 15.f, sy0, sy0 + 3.f));
-        }
+        const bool valid = base + (uint32_t)lane < rg.y;
+        const float4 qa = cur.a, qb = cur.b, qc = cur.c;
+        const bool hit = valid && qa.x + qb.z >= tx0 && qa.x - qb.z <= tx0 + 15.f && qa.y + qb.w >= sy0 &&
+                         qa.y - qb.w <= sy0 + 3.f &&
+                         (!(GSR_EXACT_CULL & 1) ||
+                          ellipse_meets_box(qa.x, qa.y, qa.z, qa.w, qb.x, cur.tm, tx0, tx0 + 15.f, sy0, sy0 + 3.f));
+        // next batch in flight while this one blends
+        fwd_gather(rec, gnext, cur);
+        gnext = point_list[min(base + 2 * kWave + (uint32_t)lane, lastpos)];
         const uint64_t keep = __ballot(hit);
         const uint32_t cnt = (uint32_t)__popcll(keep);
         if (hit) {
@@ -268,10 +184,6 @@ __global__ __launch_bounds__(256) void render_fwd_sb_kernel(
     }
 }
 
-#ifndef GSR_FWD_SUBBLOCK
-#define GSR_FWD_SUBBLOCK 1
-#endif
-
 // Launch order for a tile pass, heaviest first (longest-processing-time-first list scheduling):
 // one 1024-thread workgroup buckets the T work estimates into 256 descending classes of
 // 2^shift instances (LDS histogram, scan, scatter).  Order within a class is arbitrary; every
@@ -318,15 +230,10 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
                        const float *bg, float *out_color, float *out_invdepth, hipStream_t s) {
     const int T = cam.gx * cam.gy;
     if (T == 0) return;
-    if (GSR_FWD_SUBBLOCK) {  // launch order: is.tile_ids (rasterizer.hip, by list length)
-        hipLaunchKernelGGL(render_fwd_sb_kernel, dim3(T), dim3(4 * kWave), 0, s, is.ranges, bs.point_list, cam.W,
-                           cam.H, cam.gx, gs.rec, bg, out_color, out_invdepth, is.final_T, is.n_contrib, is.tile_work,
-                           is.tile_ids, bs.kdev, bs.cap, bs.kdev ? dsort_err_word(gs) : nullptr);
-    }
-    else
-        hipLaunchKernelGGL(render_fwd_kernel, dim3(T), dim3(kWave), 0, s, is.ranges, bs.point_list, cam.W, cam.H,
-                           cam.gx, gs.rec, bg, out_color, out_invdepth, is.final_T, is.n_contrib, is.tile_work,
-                           is.tile_ids, bs.kdev, bs.cap);
+    // launch order: is.tile_ids (rasterizer.hip, by list length)
+    hipLaunchKernelGGL(render_fwd_sb_kernel, dim3(T), dim3(4 * kWave), 0, s, is.ranges, bs.point_list, cam.W, cam.H,
+                       cam.gx, gs.rec, bg, out_color, out_invdepth, is.final_T, is.n_contrib, is.tile_work,
+                       is.tile_ids, bs.kdev, bs.cap, bs.kdev ? dsort_err_word(gs) : nullptr);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -364,6 +271,22 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
 #ifndef GSR_REC_PAD
 #define GSR_REC_PAD 1  // write the unused 4th float4 of a 64-B record (full 64-B segments)
 #endif
+struct BwdBatch {
+    float4 a, b, c;  // GRec q0..q2
+    uint4 q3;        // tile rect, depth bits, cull threshold
+    uint32_t goff;   // the Gaussian's first backward record
+};
+
+__device__ __forceinline__ void bwd_gather(const GRec *__restrict__ rec, const uint32_t *__restrict__ goff, uint32_t g,
+                                           BwdBatch &o) {
+    const float4 *R = reinterpret_cast<const float4 *>(rec + g);
+    o.a = R[0];
+    o.b = R[1];
+    o.c = R[2];
+    o.q3 = reinterpret_cast<const uint4 *>(rec + g)[3];
+    o.goff = goff[g];
+}
+
 template <bool kDepth>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVES_PER_EU))) void render_bwd_kernel(
     const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list, int W, int H, int gx,
@@ -399,18 +322,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
 #endif
     uint32_t last[kPixPerLane], lastk[kPixPerLane];
     uint32_t maxlast = 0;
+    // every per-pixel input load first (clamped to the image, zeroed outside it), so the 24 loads
+    // of a lane are in flight together instead of one round trip per pixel row
 #pragma unroll
     for (int k = 0; k < kPixPerLane; k++) {
         const int py = py0 + 4 * k;
-        const bool inside = px < W && py < H;
-        const int pix = py * W + px;
+        const int pix = min(py, H - 1) * W + min(px, W - 1);
         pfy[k] = (float)py;
-        T[k] = inside ? final_Ts[pix] : 0.f;
-        last[k] = inside ? n_contrib[pix] : 0u;
-        dp0[k] = inside ? dL_dpix[pix] : 0.f;
-        dp1[k] = inside ? dL_dpix[H * W + pix] : 0.f;
-        dp2[k] = inside ? dL_dpix[2 * H * W + pix] : 0.f;
-        did[k] = (kDepth && inside) ? dL_dinvd[pix] : 0.f;
+        T[k] = final_Ts[pix];
+        last[k] = n_contrib[pix];
+        dp0[k] = dL_dpix[pix];
+        dp1[k] = dL_dpix[H * W + pix];
+        dp2[k] = dL_dpix[2 * H * W + pix];
+        did[k] = kDepth ? dL_dinvd[pix] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < kPixPerLane; k++) {
+        const bool inside = px < W && py0 + 4 * k < H;
+        T[k] = inside ? T[k] : 0.f;
+        last[k] = inside ? last[k] : 0u;
+        dp0[k] = inside ? dp0[k] : 0.f;
+        dp1[k] = inside ? dp1[k] : 0.f;
+        dp2[k] = inside ? dp2[k] : 0.f;
+        did[k] = inside ? did[k] : 0.f;
 #if GSR_BWD_FACTORED
         S[k] = 0.f;
 #else
@@ -422,42 +356,46 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
         maxlast = lastk[k] > maxlast ? lastk[k] : maxlast;
     }
     const uint2 rg = ranges[tile];
-    if (lane == 0) {
-        uint64_t bkey = 0;
-        if (maxlast > 0) {
-            const uint32_t gb = point_list[rg.x + maxlast - 1];
-            bkey = ((uint64_t)rec[gb].dbits << 32) | gb;
-        }
-        boundary[tile] = bkey;
-    }
     const float sx = 0.5f * (float)W, sy = 0.5f * (float)H;
     const int rs_slot = wave_rs10_slot(lane);
     (void)rs_slot;
 
+    // The gather is software-pipelined as in the forward: batch b-1's GRec lines and record bases
+    // and batch b-2's ids are in flight while batch b replays (unconditional loads at clamped list
+    // positions -- a masked load would be waited for at the end of its branch).
+    BwdBatch cur;
+    uint32_t gnext = 0;
+    if (maxlast > 0) {
+        const uint32_t g0 = point_list[rg.x + (uint32_t)max((int)maxlast - 1 - lane, 0)];
+        bwd_gather(rec, goff, g0, cur);
+        gnext = point_list[rg.x + (uint32_t)max((int)maxlast - 1 - kWave - lane, 0)];
+        // the tile's boundary key: lane 0 holds the last instance any pixel uses
+        if (lane == 0) boundary[tile] = ((uint64_t)cur.q3.z << 32) | g0;
+    } else if (lane == 0) {
+        boundary[tile] = 0ull;
+    }
     for (int hi = (int)maxlast; hi > 0; hi -= kWave) {
         const int n = hi < kWave ? hi : kWave;
         uint32_t m = 0, u = 0, pos = 0;
-        float4 qa, qb, qc;
+        const float4 qa = cur.a, qb = cur.b, qc = cur.c;
         if (lane < n) {
             pos = (uint32_t)(hi - 1 - lane);
-            const uint32_t g = point_list[rg.x + pos];
-            const float4 *R = reinterpret_cast<const float4 *>(rec + g);
-            qa = R[0];
-            qb = R[1];
-            qc = R[2];
-            const uint4 q3 = reinterpret_cast<const uint4 *>(rec + g)[3];
-            u = goff[g] + (uint32_t)((ty - (int)(q3.x >> 16)) * (int)q3.y + (tx - (int)(q3.x & 0xFFFFu)));
-            m = sub_block_mask(qa, qb, tx0, ty0);
+            const uint4 q3 = cur.q3;
+            u = cur.goff + (uint32_t)((ty - (int)(q3.x >> 16)) * (int)q3.y + (tx - (int)(q3.x & 0xFFFFu)));
+            m = sub_block_mask(qa, qb, __uint_as_float(q3.w), tx0, ty0);
 #pragma unroll
             for (int k = 0; k < kPixPerLane; k++)
                 if (pos >= lastk[k]) m &= ~(1u << k);
-            if (m == 0u) {  // in the live range but touches no pixel that needs it: zero record
-                const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-                out[4 * (size_t)u + 0] = z;
-                out[4 * (size_t)u + 1] = z;
-                out[4 * (size_t)u + 2] = z;
-                if (GSR_REC_PAD) out[4 * (size_t)u + 3] = z;
-            }
+        }
+        // next batch in flight while this one replays
+        bwd_gather(rec, goff, gnext, cur);
+        gnext = point_list[rg.x + (uint32_t)max(hi - 1 - 2 * kWave - lane, 0)];
+        if (lane < n && m == 0u) {  // in the live range but touches no pixel that needs it: zero record
+            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+            out[4 * (size_t)u + 0] = z;
+            out[4 * (size_t)u + 1] = z;
+            out[4 * (size_t)u + 2] = z;
+            if (GSR_REC_PAD) out[4 * (size_t)u + 3] = z;
         }
         const uint64_t keep = __ballot(m != 0u);
         const uint32_t cnt = (uint32_t)__popcll(keep);
