@@ -79,6 +79,7 @@ def algorithmic_bytes(P, Pv, K, T, npix, M=16):
         "bin_superblocks": 2 * 24 * Pv + 8 * Pv + 4 * P1,
         "bin_tiles": 2 * 24 * P1 + 4 * K + 8 * T,
         "tile_order": 16 * T,
+        "tile_order_bwd": 12 * T,
         "render_fwd": 44 * K + 24 * npix,
         "render_bwd": 44 * K + 24 * npix + 40 * Pv,
         "preprocess_bwd": (356 + sh - 192) * P + (260 + sh - 192) * P,
@@ -243,17 +244,43 @@ def config5(a, dev):
     return out
 
 
-def latest_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/*pmc*.json)."""
+def latest_profile_entry(kernel, field):
+    """`field` of `kernel` (a stage name: render_bwd is the depth-gradient variant the bench runs)
+    from the newest committed PMC summary (profiles/r<round><letter>_pmc.json) that has it."""
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")))  # named r<round><letter>_...
     for f in reversed(files):
         try:
             d = json.load(open(f))
-            if kernel in d.get("kernels", {}):
-                return d["kernels"][kernel].get("hbm_bytes_per_launch"), os.path.basename(f)
+            e = d.get("kernels", {}).get(kernel, {})
+            v = e.get(field) if "." not in field else e.get(field.split(".")[0], {}).get(field.split(".")[1])
+            if v is not None:
+                return v, os.path.basename(f)
         except Exception:
             continue
     return None, None
+
+
+def latest_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary."""
+    return latest_profile_entry(kernel, "hbm_bytes_per_launch")
+
+
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD every 2 cycles at the
+# 2.4 GHz engine clock (MI355X_MICROARCH.md, v_fma_f32 row)
+VALU_PEAK_INSTR_S = 256 * 4 * 2.4e9 / 2
+
+
+def valu_roofline(kernel, ms):
+    """Second roofline for the blend kernels, which are VALU-issue bound: wave-level VALU
+    instructions per launch (SQ_INSTS_VALU from the committed rocprofv3 summary of the same
+    kernel variant) over the live-measured launch time, against the issue peak."""
+    instr, src = latest_profile_entry(kernel, "sq.SQ_INSTS_VALU")
+    if not instr or not ms:
+        return None
+    ach = instr / (ms * 1e-3)
+    return {"kernel": kernel, "bound": "valu-issue", "achieved": round(ach / 1e9, 2), "peak": VALU_PEAK_INSTR_S / 1e9,
+            "unit": "G wave-instr/s", "frac": round(ach / VALU_PEAK_INSTR_S, 4), "valu_instr_per_launch": instr,
+            "avg_ms": round(ms, 5), "instr_source": src}
 
 
 def main():
@@ -385,6 +412,7 @@ def main():
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "algorithmic_bytes": abytes[dom], "avg_ms": round(dom_ms, 5),
                      "traffic_source": traffic_src},
+        "valu_roofline": [r for r in (valu_roofline(k, stages.get(k)) for k in ("render_bwd", "render_fwd")) if r],
         "stages_ms": {k: round(v, 5) for k, v in stages.items()},
         # stages on the main stream (sh_color overlaps the sort / binning on a side stream)
         "pipeline_roofline": {"algorithmic_bytes": sum(abytes.values()),

@@ -114,8 +114,9 @@ int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const
 /* Per-stage device time of the last forward/backward on this thread, filled only when
  * gsr_set_profiling(1) was called (HIP events; for bench.py's roofline).  Stage order:
  * 0 preprocess, 1 depth sort + scan, 2 binning level 1 (superblocks), 3 binning level 2 (tiles and
- * ranges), 4 forward tile order, 5 render_fwd (+ backward tile order), 6 render_bwd, 7 preprocess_bwd,
- * 8 SH colour (on an internal side stream, overlapping stages 1-4; joined before stage 5).  Returns the number of stages written. */
+ * ranges), 4 forward tile order, 5 render_fwd, 6 render_bwd, 7 preprocess_bwd, 8 SH colour (on an
+ * internal side stream, overlapping stages 1-4; joined before stage 5), 9 backward tile order.
+ * Returns the number of stages written. */
 int gsr_set_profiling(int enable);
 int gsr_stage_times_ms(float *out, int max_stages);
 

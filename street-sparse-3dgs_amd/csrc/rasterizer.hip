@@ -44,7 +44,7 @@ thread_local int g_khead[kMaxDevicesK] = {};
 constexpr uint32_t kKPending = 0xFFFFFFFFu;
 
 // Stage profiling is process-wide: torch runs the backward on its autograd device thread.
-constexpr int kStages = 9;
+constexpr int kStages = 10;
 std::mutex g_prof_mu;
 int g_profile = 0;
 bool g_ev_init = false;
@@ -520,6 +520,9 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
         {
             StageTimer st(5, s);
             launch_render_fwd(cam, gs, bs, is, background, out_color, out_invdepth, s);
+        }
+        {
+            StageTimer st(9, s);  // backward launch order, from the forward's per-tile work
             launch_tile_order(is.tile_work, is.ranges, T, 2, is.tile_order, s, bs.kdev, bs.cap);
         }
         return check("render", debug, s);

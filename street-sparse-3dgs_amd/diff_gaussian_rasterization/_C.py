@@ -270,7 +270,7 @@ def set_profiling(enable: bool) -> None:
 
 
 STAGES = ("preprocess", "depth_sort_scan", "bin_superblocks", "bin_tiles", "tile_order", "render_fwd", "render_bwd",
-          "preprocess_bwd", "sh_color")
+          "preprocess_bwd", "sh_color", "tile_order_bwd")
 
 
 def stage_times_ms() -> dict:

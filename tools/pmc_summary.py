@@ -18,7 +18,8 @@ import os
 import re
 from collections import defaultdict
 
-STAGE_OF = [("render_bwd_kernel", "render_bwd"), ("render_fwd", "render_fwd"),
+STAGE_OF = [("render_bwd_kernel<true>", "render_bwd"), ("render_bwd_kernel<false>", "render_bwd:nodepth"),
+            ("render_bwd_kernel", "render_bwd"), ("render_fwd", "render_fwd"),
             ("preprocess_bwd_kernel", "preprocess_bwd"), ("record_sum_kernel", "record_sum"),
             ("preprocess_color_kernel", "sh_color"), ("preprocess_kernel", "preprocess"),
             ("depth_gather_kernel", "depth_gather"), ("dsort_upsweep", "depth_sort:upsweep"),
@@ -62,6 +63,22 @@ def read_pmc(d, counter):
     return vals
 
 
+SQ_COUNTERS = ("SQ_INSTS_VALU", "SQ_INSTS_VALU_TRANS_F32", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM",
+               "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_ANY",
+               "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_LDS_BANK_CONFLICT", "SQ_WAIT_INST_LDS", "GRBM_GUI_ACTIVE",
+               "SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_ADD_F32")
+
+
+def read_sq(dirs):
+    """Per-launch averages of the SQ / GRBM counters of every stage (several --pmc passes)."""
+    out = defaultdict(dict)
+    for d in dirs:
+        for c in SQ_COUNTERS:
+            for s, v in read_pmc(d, c).items():
+                out[s][c] = sum(v) / len(v)
+    return out
+
+
 def read_stats(d):
     out = {}
     for f in glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True):
@@ -81,13 +98,15 @@ def main():
     ap.add_argument("--fetch")
     ap.add_argument("--write")
     ap.add_argument("--out", required=True)
+    ap.add_argument("--sq", action="append", default=[], help="rocprofv3 --pmc SQ_* pass directories")
     ap.add_argument("--note", default="")
     a = ap.parse_args()
     res = {"note": a.note, "kernels": {}}
     stats = read_stats(a.trace) if a.trace else {}
     fetch = read_pmc(a.fetch, "FETCH_SIZE") if a.fetch else {}
     write = read_pmc(a.write, "WRITE_SIZE") if a.write else {}
-    for s in sorted(set(stats) | set(fetch) | set(write)):
+    sq = read_sq(a.sq)
+    for s in sorted(set(stats) | set(fetch) | set(write) | set(sq)):
         e = dict(stats.get(s, {}))
         if s in fetch:
             f = sum(fetch[s]) / len(fetch[s])
@@ -99,6 +118,14 @@ def main():
             e["write_bytes"] = w * 1024
         if "read_bytes_corrected" in e and "write_bytes" in e:
             e["hbm_bytes_per_launch"] = e["read_bytes_corrected"] + e["write_bytes"]
+        if s in sq:
+            e["sq"] = sq[s]
+            # VALU issue: a wave64 VALU instruction holds its SIMD for 2 cycles (MI355X_MICROARCH.md,
+            # v_fma_f32 row); GRBM_GUI_ACTIVE is summed over the 8 XCDs
+            g = sq[s].get("GRBM_GUI_ACTIVE")
+            v = sq[s].get("SQ_INSTS_VALU")
+            if g and v:
+                e["valu_issue_frac"] = v * 2.0 / (1024 * g / 8.0)
         res["kernels"][s] = e
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     json.dump(res, open(a.out, "w"), indent=1)
