@@ -356,7 +356,10 @@ __device__ __forceinline__ float wave_rs10(const float *v, int lane) {
     float e0 = b0 ? d1 : d0;
     const float w0 = b0 ? d0 : d1;
     asm volatile("s_nop 1\n" GSR_DPP_RS("quad_perm:[1,0,3,2]", 0, 1) : "+v"(e0) : "v"(w0));
-    return e0 + __shfl_xor(e0, 16, 64);  // rows 0+1 and 2+3 (both rows of a pair hold the sum)
+    // rows 0+1 and 2+3 (both rows of a pair hold the sum): v_permlane16_swap hands every lane its
+    // partner row's value without the LDS round trip of a ds_bpermute (same sum, same bits)
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(e0), __float_as_uint(e0), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 #undef GSR_DPP_RS
 
@@ -366,13 +369,21 @@ __device__ __forceinline__ int wave_rs10_slot(int lane) {
     return (c == 3 || (b2 && c == 2)) ? -1 : 5 * b3 + 3 * b2 + c;
 }
 
+// Max over the 64 lanes, in every lane: DPP within the 16-lane rows, then gfx950's row and half
+// swaps (no LDS round trips, unlike a __shfl_xor butterfly).
+template <int kCtrl>
+__device__ __forceinline__ uint32_t dpp_u(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, 0xF, 0xF, false);
+}
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-        const uint32_t o = (uint32_t)__shfl_xor((int)v, m, 64);
-        v = o > v ? o : v;
-    }
-    return v;
+    v = max(v, dpp_u<0xB1>(v));   // quad_perm [1,0,3,2]
+    v = max(v, dpp_u<0x4E>(v));   // quad_perm [2,3,0,1]
+    v = max(v, dpp_u<0x124>(v));  // row_ror:4
+    v = max(v, dpp_u<0x128>(v));  // row_ror:8 -> every lane holds its row's max
+    const auto r16 = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    v = max(r16[0], r16[1]);
+    const auto r32 = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return max(r32[0], r32[1]);
 }
 
 // ------------------------------------------------------------------------------------------
