@@ -326,27 +326,34 @@ __device__ __forceinline__ void wave_rowsum<9>(float *v) {
 // Reduce-scatter of 10 values over every 16-lane row, then rows 0+1 and 2+3 added: each lane
 // ends with ONE half-wave partial, of value index wave_rs10_slot(lane) (-1: a padding slot).
 // Four exchange stages (partners l^8, l^7, l^2, l^1 -- row_ror:8, row_half_mirror and two
-// quad_perms; after each, a lane keeps half of its values, chosen by one bit of its index)
-// cost 15 + 9 + 6 + 3 VALU instead of the 40 of four all-reduce stages over 10 values, and the
-// result is parked with one masked store instead of five from one lane.
+// quad_perms; after each, a lane keeps half of its values, chosen by one bit of its index).  In
+// the first two stages that bit is a DPP bank bit (bank = 4-lane group: bit 3 splits banks {0,1}
+// from {2,3}, bit 2 banks {0,2} from {1,3}), so each kept value is ONE bank-masked DPP add per
+// half -- own + partner's copy of the SAME value -- with no selects (10 + 5 VALU instead of
+// 15 + 9); the last two stages select within a bank (6 + 3).  Sums are formed in the same order
+// as before (partner + own), so the bits do not change.
 #define GSR_DPP_RS(CTRL, I, N) "v_add_f32_dpp %" #I ", %" #N ", %" #I " " CTRL " row_mask:0xf bank_mask:0xf\n"
+#define GSR_DPP_KEEP(CTRL, BANKS, D, S) "v_add_f32_dpp %" #D ", %" #S ", %" #S " " CTRL " row_mask:0xf bank_mask:" BANKS "\n"
 __device__ __forceinline__ float wave_rs10(const float *v, int lane) {
-    const bool b3 = (lane >> 3) & 1, b2 = (lane >> 2) & 1, b1 = (lane >> 1) & 1, b0 = lane & 1;
-    float k0 = b3 ? v[5] : v[0], k1 = b3 ? v[6] : v[1], k2 = b3 ? v[7] : v[2], k3 = b3 ? v[8] : v[3],
-          k4 = b3 ? v[9] : v[4];
-    float s0 = b3 ? v[0] : v[5], s1 = b3 ? v[1] : v[6], s2 = b3 ? v[2] : v[7], s3 = b3 ? v[3] : v[8],
-          s4 = b3 ? v[4] : v[9];
-    asm volatile("s_nop 1\n" GSR_DPP_RS("row_ror:8", 0, 5) GSR_DPP_RS("row_ror:8", 1, 6)
-                     GSR_DPP_RS("row_ror:8", 2, 7) GSR_DPP_RS("row_ror:8", 3, 8) GSR_DPP_RS("row_ror:8", 4, 9)
-                 : "+v"(k0), "+v"(k1), "+v"(k2), "+v"(k3), "+v"(k4)
-                 : "v"(s0), "v"(s1), "v"(s2), "v"(s3), "v"(s4));
-    // values a0..a4 (+ a5 = 0): bit 2 keeps a0..a2 or a3..a5
-    float c0 = b2 ? k3 : k0, c1 = b2 ? k4 : k1, c2 = b2 ? 0.f : k2;
-    float t0 = b2 ? k0 : k3, t1 = b2 ? k1 : k4, t2 = b2 ? k2 : 0.f;
-    asm volatile("s_nop 1\n" GSR_DPP_RS("row_half_mirror", 0, 3) GSR_DPP_RS("row_half_mirror", 1, 4)
-                     GSR_DPP_RS("row_half_mirror", 2, 5)
-                 : "+v"(c0), "+v"(c1), "+v"(c2)
-                 : "v"(t0), "v"(t1), "v"(t2));
+    const bool b1 = (lane >> 1) & 1, b0 = lane & 1;
+    // stage 1 (l^8): banks 0,1 keep values 0..4, banks 2,3 values 5..9
+    float k0, k1, k2, k3, k4;
+    asm volatile("s_nop 1\n" GSR_DPP_KEEP("row_ror:8", "0x3", 0, 5) GSR_DPP_KEEP("row_ror:8", "0xc", 0, 10)
+                     GSR_DPP_KEEP("row_ror:8", "0x3", 1, 6) GSR_DPP_KEEP("row_ror:8", "0xc", 1, 11)
+                         GSR_DPP_KEEP("row_ror:8", "0x3", 2, 7) GSR_DPP_KEEP("row_ror:8", "0xc", 2, 12)
+                             GSR_DPP_KEEP("row_ror:8", "0x3", 3, 8) GSR_DPP_KEEP("row_ror:8", "0xc", 3, 13)
+                                 GSR_DPP_KEEP("row_ror:8", "0x3", 4, 9) GSR_DPP_KEEP("row_ror:8", "0xc", 4, 14)
+                 : "=&v"(k0), "=&v"(k1), "=&v"(k2), "=&v"(k3), "=&v"(k4)
+                 : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]),
+                   "v"(v[8]), "v"(v[9]));
+    // stage 2 (l^7, row_half_mirror): values a0..a4 (+ a5 = pad): banks 0,2 keep a0..a2, banks 1,3
+    // a3, a4 and the pad (left unwritten: it only ever reaches padding slots)
+    float c0, c1, c2;
+    asm volatile("s_nop 1\n" GSR_DPP_KEEP("row_half_mirror", "0x5", 0, 3) GSR_DPP_KEEP("row_half_mirror", "0xa", 0, 6)
+                     GSR_DPP_KEEP("row_half_mirror", "0x5", 1, 4) GSR_DPP_KEEP("row_half_mirror", "0xa", 1, 7)
+                         GSR_DPP_KEEP("row_half_mirror", "0x5", 2, 5)
+                 : "=&v"(c0), "=&v"(c1), "=&v"(c2)
+                 : "v"(k0), "v"(k1), "v"(k2), "v"(k3), "v"(k4));
     // b0..b2 (+ b3 = 0): bit 1 keeps b0, b1 or b2, b3
     float d0 = b1 ? c2 : c0, d1 = b1 ? 0.f : c1;
     float u0 = b1 ? c0 : c2, u1 = b1 ? c1 : 0.f;
@@ -362,6 +369,7 @@ __device__ __forceinline__ float wave_rs10(const float *v, int lane) {
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 #undef GSR_DPP_RS
+#undef GSR_DPP_KEEP
 
 // Value index of lane's wave_rs10 result: 5 b3 + 3 b2 + (2 b1 + b0), or -1 for a padding slot.
 __device__ __forceinline__ int wave_rs10_slot(int lane) {
