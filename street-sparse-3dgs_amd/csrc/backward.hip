@@ -19,6 +19,9 @@ constexpr uint32_t kRedSerial = GSR_RED_SERIAL;  // splats up to this many tiles
 #ifndef GSR_LIVE_UNROLL
 #define GSR_LIVE_UNROLL 8
 #endif
+#ifndef GSR_BIG_BLOCK
+#define GSR_BIG_BLOCK 2
+#endif
 constexpr int kRecBatch = GSR_REC_BATCH;  // live records loaded together per Gaussian (record_sum)
 
 // SH backward for degree D: rgb_ch = sum_k B_k(dir) sh[k][ch] (+0.5, clamp handled by the caller
@@ -190,6 +193,10 @@ __global__ __launch_bounds__(256) void record_sum_kernel(int P, int gx, const in
             }
         }
     }
+    // Splats over more than kRedSerial tiles (the near, large ones -- a few per wave) are summed by
+    // the whole wave, one at a time, in blocks of 2 x 64 tiles whose boundary keys are all loaded
+    // before any is tested and whose live records are all loaded before any is added: two memory
+    // round trips per block instead of two per 64 tiles.
     for (uint64_t big = __ballot(n > kRedSerial); big; big &= big - 1) {
         const int bl = __ffsll((unsigned long long)big) - 1;
         const uint32_t boff = (uint32_t)__builtin_amdgcn_readlane((int)off, bl);
@@ -202,10 +209,32 @@ __global__ __launch_bounds__(256) void record_sum_kernel(int P, int gx, const in
         float q[10];
 #pragma unroll
         for (int k = 0; k < 10; k++) q[k] = 0.f;
-        for (uint32_t idx = lane; idx < bn; idx += kWave) {
-            const uint32_t t = (by0 + idx / bw) * (uint32_t)gx + bx0 + idx % bw;
-            const uint64_t bk = boundary[t];
-            if (bk != 0 && bkey <= bk) accumulate(q, boff + idx);
+        constexpr int kBigBlock = GSR_BIG_BLOCK;
+        for (uint32_t b0 = 0; b0 < bn; b0 += kBigBlock * kWave) {
+            uint64_t bk[kBigBlock];
+#pragma unroll
+            for (int j = 0; j < kBigBlock; j++) {
+                const uint32_t idx = min(b0 + (uint32_t)(j * kWave + lane), bn - 1u);  // clamped: always a tile of the splat
+                bk[j] = boundary[(by0 + idx / bw) * (uint32_t)gx + bx0 + idx % bw];
+            }
+            float4 ra[kBigBlock], rb[kBigBlock], rc[kBigBlock];
+#pragma unroll
+            for (int j = 0; j < kBigBlock; j++) {
+                const uint32_t idx = b0 + (uint32_t)(j * kWave + lane);
+                ra[j] = rb[j] = rc[j] = make_float4(0.f, 0.f, 0.f, 0.f);  // set before the masked loads
+                if (idx < bn && bk[j] != 0 && bkey <= bk[j]) {
+                    const size_t u = 4 * (size_t)(boff + idx);
+                    ra[j] = sc.rec[u + 0];
+                    rb[j] = sc.rec[u + 1];
+                    rc[j] = sc.rec[u + 2];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < kBigBlock; j++) {
+                q[0] += ra[j].x; q[1] += ra[j].y; q[2] += ra[j].z; q[3] += ra[j].w;
+                q[4] += rb[j].x; q[5] += rb[j].y; q[6] += rb[j].z; q[7] += rb[j].w;
+                q[8] += rc[j].x; q[9] += rc[j].y;
+            }
         }
 #pragma unroll
         for (int k = 0; k < 10; k++) {
