@@ -9,8 +9,9 @@ via torch.distributed.run): one process per GPU, each rank rasterizes its own sy
 
 Prints ONE JSON line on rank 0.  Extras: "roofline" for the dominant kernel (algorithmic bytes
 per launch from SURVEY.md 8(d) / its HIP-event-measured average duration on the rasterizer's
-stream), "stages_ms" for every kernel, and "cpu_baseline" (the C oracle, timed on the host cores
-on one full-size fwd+bwd frame, rank 0 at N=1 only).
+stream), "stages_ms" for every kernel, "cpu_baseline" (the C oracle, timed on the host cores on
+full-size fwd+bwd frames, rank 0 at N=1 only) and "cpu_baseline_torch" (the naive PyTorch-CPU
+splat of SURVEY.md 8(d) on config 1).
 """
 from __future__ import annotations
 
@@ -121,6 +122,24 @@ def cpu_baseline(s, P, W, H, deg, min_seconds=10.0, max_frames=8):
     return {"value": round(frames * W * H / dt / 1e6, 4), "unit": "Mpix/s", "cores": O.num_threads(), "kind": "port",
             "sample": f"{frames} fwd+bwd frames of the bench workload ({P} Gaussians, {W}x{H}, SH deg {deg}) "
                       f"through the C oracle, {dt:.2f} s"}, st
+
+
+def cpu_baseline_torch(min_seconds=3.0):
+    """SURVEY.md 8(d) / north_star: the naive vectorised PyTorch-CPU splat (oracle/torch_splat.py:
+    tensor-op preprocess, key sort, per-tile alpha matrices with cumprod transmittance, autograd
+    backward) timed on the host cores on config 1 (10k Gaussians at 256x256, SH degree 3), in full."""
+    import numpy as np
+    import gs_oracle as O
+    import torch_splat as TS
+    W = H = 256
+    s = O.synthetic_scene(10_000, W, H, seed=0, sh_degree=3)
+    rng = np.random.default_rng(7)
+    dcol = (rng.normal(size=(3, H, W)) / (W * H)).astype(np.float32)
+    dinv = (rng.normal(size=(1, H, W)) / (W * H)).astype(np.float32)
+    v, frames, dt, threads = TS.time_fwd_bwd(s, dcol, dinv, min_seconds=min_seconds)
+    return {"value": round(v, 5), "unit": "Mpix/s", "cores": threads, "kind": "port",
+            "sample": f"config 1 in full: {frames} fwd+bwd frames of 10000 Gaussians at {W}x{H} (SH deg 3) through the "
+                      f"naive PyTorch-CPU splat (oracle/torch_splat.py, torch.autograd backward), {dt:.2f} s"}
 
 
 def psnr_vs_oracle(gpu_color, gpu_invd, st):
@@ -438,6 +457,7 @@ def main():
         out["config5"] = config5(a, dev)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"], st = cpu_baseline(s, P, W, H, deg)
+        out["cpu_baseline_torch"] = cpu_baseline_torch()
         with torch.no_grad():
             color, _, invd = raster(**inp)
         out["psnr_vs_oracle"] = psnr_vs_oracle(color, invd, st)

@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes
 import os
 
-LIB_PATH = os.environ.get("GSR_LIBRARY", os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgsr_hip.so"))
+LIB_PATH = os.environ.get("GSR_LIBRARY") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgsr_hip.so")
 
 RESIZE_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
 
