@@ -123,28 +123,33 @@ __device__ __forceinline__ void sh_backward(const float *__restrict__ sh, int M,
 // issued back to back; larger splats are summed by the whole wave (coalesced loads + DPP).  Kept
 // apart from the chain rule below: this half is memory-latency bound and wants occupancy
 // (few VGPRs), the other half is arithmetic with ~130 VGPRs.
-__global__ __launch_bounds__(256) void record_sum_kernel(int P, int gx, const int *__restrict__ radii,
-                                                         const uint32_t *__restrict__ tiles,
-                                                         const GRec *__restrict__ rec,
+// The splat's tile rect comes from the compact per-Gaussian rect array (8 B; an empty rect marks
+// a culled Gaussian) and its depth bits are recomputed from the mean exactly as the preprocess
+// forms them -- reading them from the GRec line fetched a whole 64-B line per Gaussian.
+__global__ __launch_bounds__(256) void record_sum_kernel(int P, int gx, const float *__restrict__ means3D,
+                                                         const float *__restrict__ viewmatrix,
+                                                         const uint2 *__restrict__ rect8,
                                                          const uint32_t *__restrict__ offsets,
                                                          const uint64_t *__restrict__ boundary, BwdScratch sc,
                                                          float *__restrict__ dmeans2D, float *__restrict__ dopacity) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & (kWave - 1);
     const bool valid = i < P;
-    const bool vis = valid && radii[i] > 0;
+    const uint2 rr = valid ? rect8[i] : make_uint2(0u, 0u);
+    const bool vis = rr.y != 0u;  // x1 | y1 << 16 with x1 > x0 >= 0: zero only when culled
     float g[10];
 #pragma unroll
     for (int k = 0; k < 10; k++) g[k] = 0.f;
     uint32_t n = 0, x0 = 0, y0 = 0, w = 1, off = 0;
     uint64_t key = 0;
     if (vis) {
-        n = tiles[i];
-        const uint4 q3 = reinterpret_cast<const uint4 *>(rec + i)[3];
-        x0 = q3.x & 0xFFFFu;
-        y0 = q3.x >> 16;
-        w = q3.y;
-        key = ((uint64_t)q3.z << 32) | (uint32_t)i;
+        x0 = rr.x & 0xFFFFu;
+        y0 = rr.x >> 16;
+        w = (rr.y & 0xFFFFu) - x0;
+        n = w * ((rr.y >> 16) - y0);
+        const float3 p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
+        const float z = xf_point43(p, load_mat4(viewmatrix)).z;
+        key = ((uint64_t)__float_as_uint(z) << 32) | (uint32_t)i;
         off = offsets[i];
     }
     auto accumulate = [&](float *acc, uint32_t u) {
@@ -539,8 +544,8 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
 void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const GeomState &gs, const ImageState &is,
                            const int *radii, const BwdScratch &sc, const GaussianGrads &out, hipStream_t s) {
     if (in.P == 0) return;
-    hipLaunchKernelGGL(record_sum_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, cam.gx, radii, gs.tiles,
-                       gs.rec, gs.offsets, is.boundary, sc, out.dmeans2D, out.dopacity);
+    hipLaunchKernelGGL(record_sum_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, cam.gx, in.means3D,
+                       cam.view, gs.rect8, gs.offsets, is.boundary, sc, out.dmeans2D, out.dopacity);
     hipLaunchKernelGGL(preprocess_bwd_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, in.D, in.M, in.means3D,
                        radii, in.shs, gs.clamped, in.scales, in.rotations, in.scale_modifier,
                        true_scale_gradient() ? in.scale_modifier : 1.0f, in.cov3D_precomp,

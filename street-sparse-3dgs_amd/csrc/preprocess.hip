@@ -144,6 +144,7 @@ constexpr int kColorThreads = kColorWaves * kWave;
 __global__ __launch_bounds__(kColorThreads) void preprocess_color_kernel(int P, int D, const float *__restrict__ means3D,
                                                                          const float *__restrict__ shs,
                                                                          const float *__restrict__ campos,
+                                                                         const float *__restrict__ viewmatrix,
                                                                          const int *__restrict__ radii, GeomState gs) {
     __shared__ float4 s_sh[kColorWaves * kWave * kShPitch];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -193,9 +194,10 @@ __global__ __launch_bounds__(kColorThreads) void preprocess_color_kernel(int P, 
         if (val < 0.f) clamp_bits |= (uint8_t)(1u << ch);
         rgb[ch] = val < 0.f ? 0.f : val;
     }
-    float4 *R = reinterpret_cast<float4 *>(gs.rec + i);
-    const float z = R[3].z;  // view depth, written by the preprocess
-    R[2] = make_float4(rgb[0], rgb[1], rgb[2], 1.f / z);
+    // view depth recomputed exactly as the preprocess forms it (same operations, same order)
+    // instead of read back from the GRec line: that read fetched a whole 64-B line per Gaussian
+    const float z = xf_point43(p, load_mat4(viewmatrix)).z;
+    reinterpret_cast<float4 *>(gs.rec + i)[2] = make_float4(rgb[0], rgb[1], rgb[2], 1.f / z);
     gs.clamped[i] = clamp_bits;
 }
 
@@ -225,7 +227,7 @@ void launch_preprocess_color(const GaussianInputs &in, const Camera &cam, const 
                              hipStream_t s) {
     if (in.P == 0) return;
     hipLaunchKernelGGL(preprocess_color_kernel, dim3((in.P + kColorThreads - 1) / kColorThreads), dim3(kColorThreads),
-                       0, s, in.P, in.D, in.means3D, in.shs, cam.campos, radii, gs);
+                       0, s, in.P, in.D, in.means3D, in.shs, cam.campos, cam.view, radii, gs);
 }
 
 __global__ __launch_bounds__(256) void mark_visible_kernel(int P, const float *__restrict__ means3D,
