@@ -125,6 +125,13 @@ int gsr_stage_times_ms(float *out, int max_stages);
  * (multiplied by scale_modifier; identical when scale_modifier == 1).  Returns the previous mode. */
 int gsr_set_true_scale_gradient(int enable);
 
+/* Backward accumulation mode, process-wide.  0 (default): render_bwd adds every tile instance's
+ * ten per-Gaussian gradient sums into a per-Gaussian row with hardware float atomics (like
+ * upstream's atomicAdd accumulation: results vary in the last bits from run to run).  1: each
+ * instance writes a record and a second pass sums every Gaussian's records in a fixed order --
+ * forward + backward bitwise reproducible, slower.  Returns the previous mode. */
+int gsr_set_deterministic(int enable);
+
 /* Forward statistics since load: out[0] = frames rasterized (P > 0), out[1] = frames whose
  * binning ran twice because the capacity hint from the previous frame was short of K.
  * Returns the number of values written (<= n). */

@@ -278,7 +278,23 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
     // lanes past P stay to the end of the SH staging (the wave loads and stores rows together)
     const int iv = valid ? i : 0;
     float g[10];
-    {
+    if (sc.atomic) {
+        // render_bwd's atomic accumulator row (zeroed by render_fwd; untouched rows stay zero)
+        const float4 a0 = sc.acc[4 * (size_t)iv], a1 = sc.acc[4 * (size_t)iv + 1], a2 = sc.acc[4 * (size_t)iv + 2];
+        g[0] = a0.x; g[1] = a0.y; g[2] = a0.z; g[3] = a0.w;
+        g[4] = a1.x; g[5] = a1.y; g[6] = a1.z; g[7] = a1.w;
+        g[8] = a2.x; g[9] = a2.y;
+        if (!vis) {
+#pragma unroll
+            for (int k = 0; k < 10; k++) g[k] = 0.f;
+        }
+        if (valid) {
+            out.dmeans2D[3 * i + 0] = g[0];
+            out.dmeans2D[3 * i + 1] = g[1];
+            out.dmeans2D[3 * i + 2] = 0.f;
+            out.dopacity[i] = g[5];
+        }
+    } else {
         const float4 s0 = sc.gsum[2 * (size_t)iv], s1 = sc.gsum[2 * (size_t)iv + 1];
         g[0] = g[1] = g[5] = 0.f;  // screen-space mean and opacity: written by record_sum_kernel
         g[2] = s0.x; g[3] = s0.y; g[4] = s0.z; g[9] = s0.w;
@@ -544,7 +560,8 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
 void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const GeomState &gs, const ImageState &is,
                            const int *radii, const BwdScratch &sc, const GaussianGrads &out, hipStream_t s) {
     if (in.P == 0) return;
-    hipLaunchKernelGGL(record_sum_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, cam.gx, in.means3D,
+    if (!sc.atomic)  // atomic mode: the sums are already in GeomState.acc
+        hipLaunchKernelGGL(record_sum_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, cam.gx, in.means3D,
                        cam.view, gs.rect8, gs.offsets, is.boundary, sc, out.dmeans2D, out.dopacity);
     hipLaunchKernelGGL(preprocess_bwd_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, in.D, in.M, in.means3D,
                        radii, in.shs, gs.clamped, in.scales, in.rotations, in.scale_modifier,

@@ -458,6 +458,8 @@ struct GeomState {          // per Gaussian, written by preprocess
     uint32_t *sb_cnt_i;
     uint32_t *sb_base_g;
     uint32_t *sb_base_i;
+    float4 *acc;            // backward accumulators, 4 float4 (64 B) per Gaussian, zeroed by render_fwd
+    int nacc;               // rows of acc (P)
 };
 
 struct BinningState {       // per tile instance
@@ -481,9 +483,15 @@ struct ImageState {
 // (Gaussian-major) position u:  q0 = dmean2D.x, dmean2D.y, dconic.a, dconic.b;
 // q1 = dconic.c, dopacity, drgb.r, drgb.g;  q2 = drgb.b, dinvdepth, 0, 0;  q3 = 0.
 // Only instances at list positions below their tile's boundary are written.
+//
+// Default (atomic) mode: no records; render_bwd adds each live instance's ten values (same order:
+// dmean2D x, y, dconic a, b, c, dopacity, drgb r, g, b, dinvdepth) into the Gaussian's 64-B
+// accumulator row GeomState.acc with no-return float atomics, one 40-B segment per instance.
 struct BwdScratch {
     float4 *rec;
     float4 *gsum;  // per Gaussian: {dconic a, b, c, dinvdepth}, {drgb r, g, b, 0} (record_sum -> preprocess_bwd)
+    float4 *acc;   // atomic mode: GeomState.acc (rec / gsum unused)
+    int atomic;
 };
 
 }  // namespace gsr

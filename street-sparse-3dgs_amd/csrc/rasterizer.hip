@@ -171,6 +171,8 @@ GeomState carve_geom(void *base, int P, int gx, int gy, size_t *bytes) {
     g.sb_cnt_i = c.take<uint32_t>((size_t)g.sb.nsb * g.sb.nchunks);
     g.sb_base_g = c.take<uint32_t>((size_t)g.sb.nsb + 1);
     g.sb_base_i = c.take<uint32_t>((size_t)g.sb.nsb + 1);
+    g.acc = c.take<float4>(4 * (size_t)P);
+    g.nacc = P;
     if (bytes) *bytes = align_up(c.off, 256);
     return g;
 }
@@ -202,11 +204,15 @@ ImageState carve_image(void *base, int T, int npix, size_t *bytes) {
     return s;
 }
 
-BwdScratch carve_bwd(void *base, int64_t K, int P, size_t *bytes) {
+// atomic mode needs no scratch (the accumulators live in the geometry buffer, GeomState.acc)
+BwdScratch carve_bwd(void *base, int64_t K, int P, bool atomic, size_t *bytes) {
     Carver c(base);
-    BwdScratch s;
-    s.rec = c.take<float4>(4 * (size_t)K);
-    s.gsum = c.take<float4>(2 * (size_t)P);
+    BwdScratch s{};
+    s.atomic = atomic ? 1 : 0;
+    if (!atomic) {
+        s.rec = c.take<float4>(4 * (size_t)K);
+        s.gsum = c.take<float4>(2 * (size_t)P);
+    }
     if (bytes) *bytes = align_up(c.off, 256);
     return s;
 }
@@ -307,6 +313,10 @@ void gsr::set_last_error(const std::string &msg) { g_err = msg; }
 
 namespace {
 std::atomic<int> g_true_scale_grad{0};
+#ifndef GSR_DETERMINISTIC_DEFAULT
+#define GSR_DETERMINISTIC_DEFAULT 0  // backward accumulation: 0 float atomics, 1 records + ordered sums
+#endif
+std::atomic<int> g_deterministic{GSR_DETERMINISTIC_DEFAULT};
 }
 bool gsr::true_scale_gradient() { return g_true_scale_grad.load(std::memory_order_relaxed) != 0; }
 
@@ -599,8 +609,9 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
     const GeomState gs = carve_geom(geom_buffer, P, cam.gx, cam.gy, nullptr);
     const BinningState bs = carve_binning(binning_buffer, R_inst, nullptr);
     const ImageState is = carve_image(image_buffer, T, width * height, nullptr);
+    const bool atomic = g_deterministic.load(std::memory_order_relaxed) == 0;
     size_t sbytes = 0;
-    carve_bwd(nullptr, R_inst, P, &sbytes);
+    carve_bwd(nullptr, R_inst, P, atomic, &sbytes);
     // hierarchy cut: gradients of the R blended rows first, then scattered to the input rows
     size_t cut_off = 0;
     if (R > 0) {
@@ -610,9 +621,10 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
         cut_off = sbytes;
         sbytes = align_up(c.off, 256);
     }
-    void *sbase = scratch(resize_ctx, sbytes);
+    void *sbase = scratch(resize_ctx, std::max<size_t>(sbytes, 256));  // atomic mode: nothing carved
     if (!sbase) return fail(GSR_ERR_ALLOCATION, "backward scratch allocation failed");
-    const BwdScratch sc = carve_bwd(sbase, R_inst, P, nullptr);
+    BwdScratch sc = carve_bwd(sbase, R_inst, P, atomic, nullptr);
+    sc.acc = gs.acc;
 
     GaussianGrads out{dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
                       dL_drotations};
@@ -670,6 +682,8 @@ int gsr_set_true_scale_gradient(int enable) {
     const int prev = g_true_scale_grad.exchange(enable ? 1 : 0);
     return prev;
 }
+
+int gsr_set_deterministic(int enable) { return g_deterministic.exchange(enable ? 1 : 0); }
 
 int gsr_forward_stats(int64_t *out, int n) {
     if (!out || n < 0) return fail(GSR_ERR_INVALID_ARGUMENT, "NULL stats buffer");

@@ -83,8 +83,17 @@ __global__ __launch_bounds__(256) void render_fwd_sb_kernel(
     const GRec *__restrict__ rec, const float *__restrict__ bg, float *__restrict__ out_color,
     float *__restrict__ out_invd, float *__restrict__ final_T, uint32_t *__restrict__ n_contrib,
     uint32_t *__restrict__ tile_work, const uint32_t *__restrict__ fwd_order, const uint32_t *__restrict__ kdev,
-    uint32_t cap, const uint32_t *__restrict__ sort_err) {
+    uint32_t cap, const uint32_t *__restrict__ sort_err, float4 *__restrict__ acc, uint32_t acc_n4) {
     if (kdev && *kdev > cap) return;  // the point-list capacity is short: the host re-runs at K
+    {
+        // the backward's per-Gaussian accumulator rows (atomic mode) start at zero: every
+        // workgroup clears one slice with streaming stores that drain while it blends (the
+        // blend is VALU-bound; HBM is nearly idle here)
+        const uint32_t per = (acc_n4 + gridDim.x - 1) / gridDim.x;
+        const uint32_t a0 = blockIdx.x * per, a1 = min(acc_n4, a0 + per);
+        for (uint32_t k = a0 + threadIdx.x; k < a1; k += blockDim.x)
+            acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     // per wave, three 64-entry planes: {x, y, conic.a, conic.b}, {conic.c, opacity, -, -},
     // {r, g, b, 1/depth}; one base address serves all three (offsets 0 / 1 / 2 KiB)
     __shared__ float4 s_q[4][3][kWave];
@@ -233,7 +242,8 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
     // launch order: is.tile_ids (rasterizer.hip, by list length)
     hipLaunchKernelGGL(render_fwd_sb_kernel, dim3(T), dim3(4 * kWave), 0, s, is.ranges, bs.point_list, cam.W, cam.H,
                        cam.gx, gs.rec, bg, out_color, out_invdepth, is.final_T, is.n_contrib, is.tile_work,
-                       is.tile_ids, bs.kdev, bs.cap, bs.kdev ? dsort_err_word(gs) : nullptr);
+                       is.tile_ids, bs.kdev, bs.cap, bs.kdev ? dsort_err_word(gs) : nullptr, gs.acc,
+                       (uint32_t)(4 * (size_t)gs.nacc));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -274,9 +284,10 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
 struct BwdBatch {
     float4 a, b, c;  // GRec q0..q2
     uint4 q3;        // tile rect, depth bits, cull threshold
-    uint32_t goff;   // the Gaussian's first backward record
+    uint32_t goff;   // record mode: the Gaussian's first backward record; atomic mode: its id
 };
 
+template <bool kAtomic>
 __device__ __forceinline__ void bwd_gather(const GRec *__restrict__ rec, const uint32_t *__restrict__ goff, uint32_t g,
                                            BwdBatch &o) {
     const float4 *R = reinterpret_cast<const float4 *>(rec + g);
@@ -284,10 +295,16 @@ __device__ __forceinline__ void bwd_gather(const GRec *__restrict__ rec, const u
     o.b = R[1];
     o.c = R[2];
     o.q3 = reinterpret_cast<const uint4 *>(rec + g)[3];
-    o.goff = goff[g];
+    o.goff = kAtomic ? g : goff[g];
 }
 
-template <bool kDepth>
+// kAtomic (default): every live instance's ten sums are added into its Gaussian's accumulator row
+// (GeomState.acc) with no-return float atomics once per batch -- ten wave-wide atomic instructions,
+// lanes = (instance, value) pairs, so each instance is ONE contiguous 40-B segment of a 64-B row
+// (one memory-side request; MI355X_MICROARCH.md, Global float atomics).  Otherwise each instance
+// writes a 64-B record at its Gaussian-major index and the tile's boundary key, and
+// backward.hip's record_sum adds them up in a fixed order (bitwise reproducible).
+template <bool kDepth, bool kAtomic>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVES_PER_EU))) void render_bwd_kernel(
     const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list, int W, int H, int gx,
     const GRec *__restrict__ rec, const float *__restrict__ bg, const float *__restrict__ final_Ts,
@@ -367,11 +384,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
     uint32_t gnext = 0;
     if (maxlast > 0) {
         const uint32_t g0 = point_list[rg.x + (uint32_t)max((int)maxlast - 1 - lane, 0)];
-        bwd_gather(rec, goff, g0, cur);
+        bwd_gather<kAtomic>(rec, goff, g0, cur);
         gnext = point_list[rg.x + (uint32_t)max((int)maxlast - 1 - kWave - lane, 0)];
         // the tile's boundary key: lane 0 holds the last instance any pixel uses
-        if (lane == 0) boundary[tile] = ((uint64_t)cur.q3.z << 32) | g0;
-    } else if (lane == 0) {
+        if (!kAtomic && lane == 0) boundary[tile] = ((uint64_t)cur.q3.z << 32) | g0;
+    } else if (!kAtomic && lane == 0) {
         boundary[tile] = 0ull;
     }
     for (int hi = (int)maxlast; hi > 0; hi -= kWave) {
@@ -381,16 +398,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
         if (lane < n) {
             pos = (uint32_t)(hi - 1 - lane);
             const uint4 q3 = cur.q3;
-            u = cur.goff + (uint32_t)((ty - (int)(q3.x >> 16)) * (int)q3.y + (tx - (int)(q3.x & 0xFFFFu)));
+            u = kAtomic ? cur.goff  // the Gaussian id
+                        : cur.goff + (uint32_t)((ty - (int)(q3.x >> 16)) * (int)q3.y + (tx - (int)(q3.x & 0xFFFFu)));
             m = sub_block_mask(qa, qb, __uint_as_float(q3.w), tx0, ty0);
 #pragma unroll
             for (int k = 0; k < kPixPerLane; k++)
                 if (pos >= lastk[k]) m &= ~(1u << k);
         }
         // next batch in flight while this one replays
-        bwd_gather(rec, goff, gnext, cur);
+        bwd_gather<kAtomic>(rec, goff, gnext, cur);
         gnext = point_list[rg.x + (uint32_t)max(hi - 1 - 2 * kWave - lane, 0)];
-        if (lane < n && m == 0u) {  // in the live range but touches no pixel that needs it: zero record
+        if (!kAtomic && lane < n && m == 0u) {  // in the live range but touches no pixel that needs it: zero record
             const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
             out[4 * (size_t)u + 0] = z;
             out[4 * (size_t)u + 1] = z;
@@ -531,9 +549,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
 #endif
         }
         __syncthreads();
+        float r[10];
         if ((uint32_t)lane < cnt) {
             const float2 *d = s_red + lane * 10;
-            float r[10];
 #pragma unroll
             for (int t = 0; t < 5; t++) {
                 const float2 p0 = d[t], p1 = d[5 + t];
@@ -555,10 +573,37 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
                 r[4] = op * myy;
             }
 #endif
-            out[o + 0] = make_float4(r[0] * sx, r[1] * sy, -0.5f * r[2], -0.5f * r[3]);
-            out[o + 1] = make_float4(-0.5f * r[4], r[5], r[6], r[7]);
-            out[o + 2] = make_float4(r[8], r[9], 0.f, 0.f);
-            if (GSR_REC_PAD) out[o + 3] = make_float4(0.f, 0.f, 0.f, 0.f);
+            r[0] *= sx;
+            r[1] *= sy;
+            r[2] *= -0.5f;
+            r[3] *= -0.5f;
+            r[4] *= -0.5f;
+            if (!kAtomic) {
+                out[o + 0] = make_float4(r[0], r[1], r[2], r[3]);
+                out[o + 1] = make_float4(r[4], r[5], r[6], r[7]);
+                out[o + 2] = make_float4(r[8], r[9], 0.f, 0.f);
+                if (GSR_REC_PAD) out[o + 3] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+        if (kAtomic) {
+            // the batch's sums, instance-major, through LDS (s_red is free again: every lane has
+            // read its halves), then ten atomic instructions: lane l of round k adds value
+            // (64k + l) % 10 of instance (64k + l) / 10 -- consecutive lanes, consecutive floats
+            // of one Gaussian's row
+            __syncthreads();
+            float *st = reinterpret_cast<float *>(s_red);
+            if ((uint32_t)lane < cnt) {
+#pragma unroll
+                for (int t = 0; t < 10; t++) st[lane * 10 + t] = r[t];
+            }
+            __syncthreads();
+#pragma unroll 1
+            for (uint32_t pidx = (uint32_t)lane; pidx < 10u * cnt; pidx += (uint32_t)kWave) {
+                const uint32_t j = pidx / 10u, v = pidx - 10u * j;
+                const float val = st[pidx];
+                const uint32_t g = __float_as_uint(s_b[j].w);
+                if (val != 0.f) unsafeAtomicAdd(reinterpret_cast<float *>(out + 4 * (size_t)g) + v, val);
+            }
         }
         __syncthreads();
     }
@@ -570,14 +615,18 @@ void launch_render_bwd(const Camera &cam, const GeomState &gs, const BinningStat
     (void)radii;
     const int T = cam.gx * cam.gy;
     if (T == 0) return;
-    if (dL_dinvdepth)
-        hipLaunchKernelGGL(render_bwd_kernel<true>, dim3(T), dim3(kWave), 0, s, is.ranges, bs.point_list, cam.W,
-                           cam.H, cam.gx, gs.rec, bg, is.final_T, is.n_contrib, dL_dpix, dL_dinvdepth, is.tile_order,
-                           gs.offsets, is.boundary, sc.rec);
-    else
-        hipLaunchKernelGGL(render_bwd_kernel<false>, dim3(T), dim3(kWave), 0, s, is.ranges, bs.point_list, cam.W,
-                           cam.H, cam.gx, gs.rec, bg, is.final_T, is.n_contrib, dL_dpix, dL_dinvdepth, is.tile_order,
-                           gs.offsets, is.boundary, sc.rec);
+#define GSR_BWD_LAUNCH(D, A)                                                                                       \
+    hipLaunchKernelGGL((render_bwd_kernel<D, A>), dim3(T), dim3(kWave), 0, s, is.ranges, bs.point_list, cam.W, cam.H, \
+                       cam.gx, gs.rec, bg, is.final_T, is.n_contrib, dL_dpix, dL_dinvdepth, is.tile_order, gs.offsets, \
+                       is.boundary, A ? sc.acc : sc.rec)
+    if (dL_dinvdepth) {
+        if (sc.atomic) GSR_BWD_LAUNCH(true, true);
+        else GSR_BWD_LAUNCH(true, false);
+    } else {
+        if (sc.atomic) GSR_BWD_LAUNCH(false, true);
+        else GSR_BWD_LAUNCH(false, false);
+    }
+#undef GSR_BWD_LAUNCH
 }
 
 }  // namespace gsr

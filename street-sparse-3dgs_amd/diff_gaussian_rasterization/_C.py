@@ -258,6 +258,13 @@ def set_true_scale_gradient(enable: bool) -> bool:
     return bool(_L.gsr_set_true_scale_gradient(int(bool(enable))))
 
 
+def set_deterministic(enable: bool) -> bool:
+    """Backward accumulation: False (default) = hardware float atomics into per-Gaussian rows
+    (upstream's scheme, last-bit run-to-run variation); True = per-instance records summed in a
+    fixed order (bitwise reproducible, slower).  Process-wide; returns the previous setting."""
+    return bool(_L.gsr_set_deterministic(int(bool(enable))))
+
+
 def forward_stats() -> dict:
     """Frames rasterized since load and how many re-ran their binning at K (gsr_forward_stats)."""
     buf = (ctypes.c_int64 * 2)()

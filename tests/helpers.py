@@ -3,6 +3,8 @@ decoding the scratch buffers (GeomState / BinningState / ImageState carve order 
 csrc/rasterizer.hip) so integer intermediates can be compared bit-exactly with the oracle."""
 from __future__ import annotations
 
+import contextlib
+
 import math
 
 import numpy as np
@@ -126,3 +128,15 @@ def settings(scene, device, sh_degree, scale_modifier=1.0, do_depth=True, debug=
         render_indices=torch.empty(0, dtype=torch.int32), parent_indices=torch.empty(0, dtype=torch.int32),
         interpolation_weights=torch.empty(0, dtype=torch.float32, device=device),
         num_node_kids=torch.empty(0, dtype=torch.int32, device=device))
+
+
+@contextlib.contextmanager
+def deterministic():
+    """Backward in the record mode (gsr_set_deterministic(1)): bitwise reproducible gradients, for
+    tests that compare two runs bit for bit; the default atomic mode differs in summation order."""
+    from diff_gaussian_rasterization import _C
+    prev = _C.set_deterministic(True)
+    try:
+        yield
+    finally:
+        _C.set_deterministic(prev)

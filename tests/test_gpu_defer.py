@@ -27,6 +27,12 @@ def _frame(scene, deg=3, debug=False):
 
 
 def test_capacity_overflow_rerun_matches():
+    from helpers import deterministic
+    with deterministic():
+        _capacity_overflow_rerun_matches()
+
+
+def _capacity_overflow_rerun_matches():
     import gs_oracle as O
     small = O.synthetic_scene(200, 160, 120, seed=31, sh_degree=3, log_scale_mean=-3.0)
     big = O.synthetic_scene(20000, 480, 320, seed=32, sh_degree=3, log_scale_mean=-2.0)

@@ -116,6 +116,12 @@ def test_rasterizer_render_indices_equal_render_post_blend():
     against render_post's order of work (interpolate_cut, then the rasterizer on the R rows):
     identical image / radii / K; gradients of the N hierarchy rows equal up to the order of the
     float atomics that sum shared parents; means2D's gradient in rows [0, R)."""
+    from helpers import deterministic
+    with deterministic():
+        _render_indices_equal_render_post_blend()
+
+
+def _render_indices_equal_render_post_blend():
     from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
     from gs_train.hier import interpolate_cut
     from gs_train.synthetic import synthetic_lod_hierarchy, tau_threshold

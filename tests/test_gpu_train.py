@@ -416,13 +416,15 @@ def test_grad_bucket_captures_rasterizer_gradients():
         loss = ts._photo_loss(image, ts.gts[0]) + ts._depth_loss(invd, ts.mono[0], ts.dmask[0], 0.5)
         loss.backward()
 
-    backward()
-    ref = {k: p.grad.clone() for k, p in params.items()}
-    bucket = gsr_dist.GradBucket(params)
-    for p in params.values():
-        p.grad = None
-    with bucket.capture():
+    from helpers import deterministic
+    with deterministic():  # two backward passes compared bit for bit
         backward()
+        ref = {k: p.grad.clone() for k, p in params.items()}
+        bucket = gsr_dist.GradBucket(params)
+        for p in params.values():
+            p.grad = None
+        with bucket.capture():
+            backward()
     for k, p in params.items():
         assert bucket.owns(p), k
         assert torch.equal(p.grad, ref[k]), k
