@@ -287,6 +287,12 @@ def latest_traffic(kernel):
 # VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD every 2 cycles at the
 # 2.4 GHz engine clock (MI355X_MICROARCH.md, v_fma_f32 row)
 VALU_PEAK_INSTR_S = 256 * 4 * 2.4e9 / 2
+# Sustained issue rate of independent v_fma_f32 on the box, 8 waves per SIMD
+# (tools/valu_bench.hip, profiles/r02e_valu_bench.txt): 947 G wave-instr/s -- the clock under full
+# VALU load sits near 1.85 GHz, so 77% of the nominal figure above is the practical ceiling
+# (v_exp_f32 / v_rcp_f32 issue at about a quarter of that rate; v_pk_fma_f32 adds only ~10% of
+# fp32 throughput, so packed math is no lever)
+VALU_SUSTAINED_INSTR_S = 947e9
 
 
 def valu_roofline(kernel, ms):
@@ -298,8 +304,9 @@ def valu_roofline(kernel, ms):
         return None
     ach = instr / (ms * 1e-3)
     return {"kernel": kernel, "bound": "valu-issue", "achieved": round(ach / 1e9, 2), "peak": VALU_PEAK_INSTR_S / 1e9,
-            "unit": "G wave-instr/s", "frac": round(ach / VALU_PEAK_INSTR_S, 4), "valu_instr_per_launch": instr,
-            "avg_ms": round(ms, 5), "instr_source": src}
+            "unit": "G wave-instr/s", "frac": round(ach / VALU_PEAK_INSTR_S, 4),
+            "sustained_peak": VALU_SUSTAINED_INSTR_S / 1e9, "frac_of_sustained": round(ach / VALU_SUSTAINED_INSTR_S, 4),
+            "valu_instr_per_launch": instr, "avg_ms": round(ms, 5), "instr_source": src}
 
 
 def main():
