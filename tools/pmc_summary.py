@@ -18,7 +18,10 @@ import os
 import re
 from collections import defaultdict
 
-STAGE_OF = [("render_bwd_kernel<true>", "render_bwd"), ("render_bwd_kernel<false>", "render_bwd:nodepth"),
+STAGE_OF = [("render_bwd_kernel<true, true>", "render_bwd"), ("render_bwd_kernel<true, false>", "render_bwd:records"),
+            ("render_bwd_kernel<false, true>", "render_bwd:nodepth"),
+            ("render_bwd_kernel<false, false>", "render_bwd:nodepth_records"),
+            ("render_bwd_kernel<true>", "render_bwd"), ("render_bwd_kernel<false>", "render_bwd:nodepth"),
             ("render_bwd_kernel", "render_bwd"), ("render_fwd", "render_fwd"),
             ("preprocess_bwd_kernel", "preprocess_bwd"), ("record_sum_kernel", "record_sum"),
             ("preprocess_color_kernel", "sh_color"), ("preprocess_kernel", "preprocess"),
