@@ -13,13 +13,14 @@
 //
 // Backward: upstream accumulates ~10 float atomics per (pixel, Gaussian) pair.  On gfx950 float
 // atomics execute at the memory side (MI355X_MICROARCH.md, Global float atomics) and 64 lanes
-// adding into one address serialise, so each wave instead reduces every instance's 10 gradient
-// terms over its 256 pixels: per instance a 5-stage DPP sum over each half wave
-// (gsr_device.h wave_halfsum) whose 2 partials go to LDS; once per batch of 64 instances each
-// lane adds its instance's halves and stores one 64-B record with plain stores at the instance's unsorted
-// (Gaussian-major) index.  Only instances in front of the tile's last contributor are visited
-// (13% of them on the 1M-Gaussian bench scene); the tile's boundary key tells backward.hip
-// which records exist.  No atomics: fwd+bwd is bitwise reproducible.
+// adding into one address serialise, so each wave first reduces every instance's 10 gradient
+// terms over its 256 pixels in registers (a DPP reduce-scatter, gsr_device.h wave_rs10, whose
+// half-wave partials go to LDS and are combined once per batch of 64 instances).  The per-batch
+// sums then leave either as ten wave-wide float-atomic instructions into per-Gaussian rows (the
+// default: one contiguous 40-B segment per instance, one memory-side request) or, in
+// deterministic mode, as one 64-B record per instance at its Gaussian-major index, summed by
+// backward.hip in a fixed order (bitwise reproducible).  Only instances in front of the tile's
+// last contributor are visited (13% of them on the 1M-Gaussian bench scene).
 #include "gsr_launch.h"
 
 namespace gsr {
