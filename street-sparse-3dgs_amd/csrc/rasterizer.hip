@@ -11,6 +11,7 @@
 #include <mutex>
 #include <string>
 #include <algorithm>
+#include <thread>
 
 #include "../../include/gsr.h"
 #include "../../include/gsr_hier.h"
@@ -61,6 +62,12 @@ hipEvent_t g_fork[kMaxDevices] = {}, g_join[kMaxDevices] = {};
 
 #ifndef GSR_SIDE_STREAM
 #define GSR_SIDE_STREAM 1
+#endif
+#ifndef GSR_COLOR_SERIAL
+#define GSR_COLOR_SERIAL 0  // 1: SH colour pass on the main stream after the preprocess (measured: no faster)
+#endif
+#ifndef GSR_K_POLL
+#define GSR_K_POLL 1  // deferred K read by polling the pinned word (0: an event after the upsweep)
 #endif
 bool side_stream(hipStream_t main, hipStream_t *side, hipEvent_t *fork, hipEvent_t *join) {
     int dev = 0;
@@ -420,13 +427,25 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
                       scale_modifier};
     hipStream_t side = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
-    const bool split = P > 0 && color_split_supported(in) && side_stream(s, &side, &fork, &join);
+    // GSR_COLOR_SERIAL=1 runs the SH colour pass on the main stream right after the preprocess:
+    // beside the binning on the side stream it slows the binning by about its own length (both
+    // want the CUs), but run serially it costs the same (2490-2498 vs 2540 Mpix/s), so the side
+    // stream stays the default.
+    const bool split = P > 0 && color_split_supported(in) &&
+                       (GSR_COLOR_SERIAL || side_stream(s, &side, &fork, &join));
     SideJoin sj;
     {
         StageTimer st(0, s);
         launch_preprocess(in, cam, gs, radii, s, split);
     }
     if ((rc = check("preprocess", debug, s))) return rc;
+    if (split && GSR_COLOR_SERIAL) {
+        {
+            StageTimer st(8, s);
+            launch_preprocess_color(in, cam, gs, radii, s);
+        }
+        if ((rc = check("preprocess colour", debug, s))) return rc;
+    }
 #ifndef GSR_COLOR_FORK
 #define GSR_COLOR_FORK 1  // 0: beside the depth sort and the binning; 1: beside the binning only
 #endif
@@ -444,7 +463,16 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
         sj.pending = true;
         return check("preprocess colour", debug, side);
     };
-    if (split && GSR_COLOR_FORK == 0 && (rc = fork_color())) return rc;
+    if (split && !GSR_COLOR_SERIAL && GSR_COLOR_FORK == 0 && (rc = fork_color())) return rc;
+    // K sizes the point list.  With a capacity hint from this device's previous frame the binning
+    // and the forward render are queued first and K is read afterwards (the GPU never waits on
+    // the host's hand-off); kernels that would overrun the capacity exit at once (they compare the
+    // device's K / instance totals with bs.cap) and the frame's binning and render are queued
+    // again at the real K.  Without a hint (first frame, debug) K is read before the binning.
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevicesK)
+        return fail(GSR_ERR_DEVICE, "no current device");
+    const bool defer = GSR_DEFER_K && P > 0 && !debug && g_khint[dev] > 0;
     hipEvent_t k_ready = nullptr;
     if (P > 0) {
         if (!g_pinned) {
@@ -459,7 +487,9 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
             return fail(GSR_ERR_DEVICE, "no current device");
         if (!g_k_ready[dev] && hipEventCreateWithFlags(&g_k_ready[dev], hipEventDisableTiming) != hipSuccess)
             return fail(GSR_ERR_DEVICE, "event creation failed");
-        k_ready = g_k_ready[dev];
+        // deferred K: no event -- its marker packet cost a ~7 us gap before the first sort pass;
+        // the host polls the pinned word the upsweep stores instead (read_K)
+        k_ready = (defer && GSR_K_POLL) ? nullptr : g_k_ready[dev];
         __atomic_store_n(g_pinned, kKPending, __ATOMIC_SEQ_CST);
     }
     {
@@ -467,18 +497,22 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
         launch_depth_sort(P, gs, g_pinned_dev, g_pinned_dev + 1, s, k_ready);
     }
     if ((rc = check("depth sort", debug, s))) return rc;
-    // K sizes the point list.  With a capacity hint from this device's previous frame the binning
-    // and the forward render are queued first and K is read afterwards (the GPU never waits on
-    // the host's hand-off); kernels that would overrun the capacity exit at once (they compare the
-    // device's K / instance totals with bs.cap) and the frame's binning and render are queued
-    // again at the real K.  Without a hint (first frame, debug) K is read before the binning.
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevicesK)
-        return fail(GSR_ERR_DEVICE, "no current device");
     int64_t K = 0;
     bool have_K = P == 0;
     auto read_K = [&]() -> int {
-        if (hipEventSynchronize(k_ready) != hipSuccess) return fail(GSR_ERR_DEVICE, "num_rendered wait failed");
+        if (k_ready) {
+            if (hipEventSynchronize(k_ready) != hipSuccess) return fail(GSR_ERR_DEVICE, "num_rendered wait failed");
+        } else {
+            // the frame is queued; the upsweep's last workgroup stores K into the pinned word (it is
+            // normally there already: the host runs ahead of the GPU).  A drained stream with the
+            // word still pending falls through to the device copy below.
+            while (__atomic_load_n(g_pinned, __ATOMIC_SEQ_CST) == kKPending) {
+                const hipError_t q = hipStreamQuery(s);
+                if (q == hipSuccess) break;
+                if (q != hipErrorNotReady) return fail(GSR_ERR_DEVICE, "num_rendered wait failed");
+                std::this_thread::yield();
+            }
+        }
         uint32_t k = __atomic_load_n(g_pinned, __ATOMIC_SEQ_CST);
         if (k == kKPending) {  // not expected: read the device copy instead
             if (hipMemcpy(&k, dsort_K_word(gs), sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
@@ -494,9 +528,8 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
         have_K = true;
         return GSR_OK;
     };
-    const bool defer = GSR_DEFER_K && P > 0 && !debug && g_khint[dev] > 0;
     if (P > 0 && !defer && (rc = read_K())) return rc;
-    if (split && GSR_COLOR_FORK == 1 && (rc = fork_color())) return rc;
+    if (split && !GSR_COLOR_SERIAL && GSR_COLOR_FORK == 1 && (rc = fork_color())) return rc;
     bool joined = false;
     auto bin_and_render = [&](int64_t cap) -> int {
         size_t bbytes = 0;
@@ -522,7 +555,7 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
             launch_tile_order(nullptr, is.ranges, T, 4, is.tile_ids, s, bs.kdev, bs.cap);  // forward order: by list length
         }
         if ((r = check("tile order", debug, s))) return r;
-        if (split && !joined) {
+        if (split && !GSR_COLOR_SERIAL && !joined) {
             sj.pending = false;
             joined = true;
             if (hipStreamWaitEvent(s, join, 0) != hipSuccess) return fail(GSR_ERR_DEVICE, "side stream join failed");
