@@ -257,6 +257,9 @@ __global__ __launch_bounds__(256) void record_sum_kernel(int P, int gx, const fl
 }
 
 constexpr int kShPitch = 13;  // padded LDS row pitch (float4) of the staged SH rows
+#ifndef GSR_BWD_SKIP_DEAD
+#define GSR_BWD_SKIP_DEAD 1
+#endif
 
 __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
     int P, int D, int M, const float *__restrict__ means3D, const int *__restrict__ radii,
@@ -304,15 +307,28 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
             g[1] = out.dmeans2D[3 * i + 1];
         }
     }
+    // A visible Gaussian in front of no tile's last contributor (occluded, or outside every
+    // pixel's reach) has ten zero sums, so every gradient below is zero: its coefficient and
+    // parameter rows are not read (88% of the bench scene's Gaussians; only its zero rows are
+    // written)
+    bool live = vis;
+    if (GSR_BWD_SKIP_DEAD) {
+        bool nz = false;
+#pragma unroll
+        for (int t = 0; t < 10; t++) nz = nz || g[t] != 0.f;
+        if (!sc.atomic && vis) nz = nz || out.dopacity[i] != 0.f;  // record mode: summed by record_sum
+        live = vis && nz;
+    }
 
     float dm[3] = {0.f, 0.f, 0.f};
     float dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const Mat4 V = load_mat4(viewmatrix);
-    const float3 p = make_float3(means3D[3 * iv], means3D[3 * iv + 1], means3D[3 * iv + 2]);
+    const int ip = live ? i : 0;
+    const float3 p = make_float3(means3D[3 * ip], means3D[3 * ip + 1], means3D[3 * ip + 2]);
     float c3[6];
     float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
     float3 s_in = make_float3(0.f, 0.f, 0.f);
-    if (vis) {
+    if (live) {
         // ---- conic -> cov2D -> cov3D and mean ----
         if (has_scales) {
             s_in = make_float3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
@@ -401,7 +417,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
         // one lane per row would put 64 rows, 192 B apart, under every load and store.
         const int wv = threadIdx.x >> 6;
         float4 *S = s_sh + wv * kWave * kShPitch;
-        const uint64_t need = __ballot(vis);
+        const uint64_t need = __ballot(live);
         const int64_t row0 = (int64_t)blockIdx.x * blockDim.x + wv * kWave;
         const int cols = ((D + 1) * (D + 1) * 3 + 3) / 4;
         const float4 *src4 = reinterpret_cast<const float4 *>(shs) + row0 * 12;
@@ -420,7 +436,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
         __builtin_amdgcn_wave_barrier();
         float4 *mine = S + lane * kShPitch;
-        if (vis) {
+        if (live) {
             float dir[3], dor[3];
             sh_dir(p, make_float3(campos_p[0], campos_p[1], campos_p[2]), dir, dor);
             const uint8_t cl = clamped[i];
@@ -464,7 +480,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
         // done above
     } else if (has_shs) {
         float *dsh = out.dsh + (size_t)i * M * 3;
-        if (!vis) {
+        if (!live) {
             if (vec_sh) {
                 float4 *d4 = reinterpret_cast<float4 *>(dsh);
 #pragma unroll
@@ -512,7 +528,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
     if (has_scales) {
         float ds[3] = {0.f, 0.f, 0.f};
         float dq[4] = {0.f, 0.f, 0.f, 0.f};
-        if (vis) {
+        if (live) {
             const float r = q.x, x = q.y, y = q.z, z = q.w;
             const float s[3] = {mod * s_in.x, mod * s_in.y, mod * s_in.z};
             const Rot3 R = quat_to_rot(q);
