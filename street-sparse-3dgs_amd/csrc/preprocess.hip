@@ -138,7 +138,10 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
 // degree are not fetched.
 constexpr int kShRow = 12;                 // float4 per row (M = 16)
 constexpr int kShPitch = 13;               // padded LDS row pitch, in float4
-constexpr int kColorWaves = 2;             // 2 waves per block: 26 KiB of LDS
+#ifndef GSR_COLOR_WAVES
+#define GSR_COLOR_WAVES 8  // 104 KiB per block, one block per CU: it interferes less with the binning beside it
+#endif
+constexpr int kColorWaves = GSR_COLOR_WAVES;  // waves per block (13 KiB of LDS each)
 constexpr int kColorThreads = kColorWaves * kWave;
 
 __global__ __launch_bounds__(kColorThreads) void preprocess_color_kernel(int P, int D, const float *__restrict__ means3D,
