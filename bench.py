@@ -317,10 +317,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # GSR_BENCH_SHARE_GPU=1 (rehearsal of the multi-rank path on a one-GPU box): every rank on
+    # device 0 and gloo for the barriers / timing reduction (RCCL refuses two ranks on one device).
+    # The driver's runs use one GPU per rank and RCCL.
+    share = os.environ.get("GSR_BENCH_SHARE_GPU") == "1"
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else 0)
+        torch.cuda.set_device(0 if share else local)
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", 0 if share or world == 1 else local)
 
     from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer, _C
 
@@ -384,7 +391,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        e = torch.tensor([elapsed], device="cpu" if share else dev, dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
 
