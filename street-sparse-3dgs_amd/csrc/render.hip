@@ -21,6 +21,8 @@
 // deterministic mode, as one 64-B record per instance at its Gaussian-major index, summed by
 // backward.hip in a fixed order (bitwise reproducible).  Only instances in front of the tile's
 // last contributor are visited (13% of them on the 1M-Gaussian bench scene).
+#include <type_traits>
+
 #include "gsr_launch.h"
 
 namespace gsr {
@@ -264,21 +266,6 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
 #ifndef GSR_TILE_REVERSE
 #define GSR_TILE_REVERSE 0
 #endif
-#ifndef GSR_BWD_BRANCH
-#define GSR_BWD_BRANCH 1
-#endif
-#ifndef GSR_BWD_FACTORED
-#define GSR_BWD_FACTORED 1
-#endif
-#ifndef GSR_BWD_ALWAYS_REDUCE
-#define GSR_BWD_ALWAYS_REDUCE 0
-#endif
-#ifndef GSR_BWD_PREFETCH
-#define GSR_BWD_PREFETCH 0
-#endif
-#ifndef GSR_BWD_RS
-#define GSR_BWD_RS 1  // per-instance sums as a 16-lane reduce-scatter (wave_rs10)
-#endif
 #ifndef GSR_REC_PAD
 #define GSR_REC_PAD 1  // write the unused 4th float4 of a 64-B record (full 64-B segments)
 #endif
@@ -312,11 +299,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
     const uint32_t *__restrict__ n_contrib, const float *__restrict__ dL_dpix, const float *__restrict__ dL_dinvd,
     const uint32_t *__restrict__ tile_order, const uint32_t *__restrict__ goff, uint64_t *__restrict__ boundary,
     float4 *__restrict__ out) {
-    // 8 KiB of LDS per wave (5 waves per SIMD fit): the scaled conic is formed per instance from
-    // s_a / s_b, and the record index rides in s_b.w next to (list position << 4 | sub-block mask)
-    __shared__ float4 s_a[kWave];
-    __shared__ float4 s_b[kWave];  // conic.c, opacity, list position << 4 | sub-block mask, record index
-    __shared__ float4 s_c[kWave];
+    // 9 KiB of LDS per wave: each compacted instance's mean and conic (scaled for gauss_p2 by the
+    // lane that stages it, once per instance instead of by the whole wave), opacity, list position
+    // << 4 | sub-block mask, Gaussian id (atomic mode) or record index, colour, and the unscaled
+    // conic for the batch epilogue
+    __shared__ float4 s_a[kWave];  // x, y, a_s, b_s
+    __shared__ float4 s_b[kWave];  // c_s, opacity, list position << 4 | sub-block mask, id / record index
+    __shared__ float4 s_c[kWave];  // r, g, b, 1 / depth
+    __shared__ float4 s_d[kWave];  // conic a, b, c
     __shared__ float2 s_red[kWave * 2 * 5];  // per instance, per half wave: 10 partial sums
 
     // Tiles run heaviest first (longest-processing-time order from the forward's per-tile work):
@@ -331,13 +321,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
     const float b0 = bg[0], b1 = bg[1], b2 = bg[2];
 
     float T[kPixPerLane], TfB[kPixPerLane], dp0[kPixPerLane], dp1[kPixPerLane], dp2[kPixPerLane], did[kPixPerLane];
-#if GSR_BWD_FACTORED
     // S = sum_c A_c dL/dpix_c: the colour (and inverse depth) accumulated behind the current
     // instance, already dotted with the pixel's upstream gradient -- the only form dL/dalpha needs
     float S[kPixPerLane], pfy[kPixPerLane];
-#else
-    float A0[kPixPerLane], A1[kPixPerLane], A2[kPixPerLane], Ai[kPixPerLane], pfy[kPixPerLane];
-#endif
     uint32_t last[kPixPerLane], lastk[kPixPerLane];
     uint32_t maxlast = 0;
     // every per-pixel input load first (clamped to the image, zeroed outside it), so the 24 loads
@@ -363,11 +349,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
         dp1[k] = inside ? dp1[k] : 0.f;
         dp2[k] = inside ? dp2[k] : 0.f;
         did[k] = inside ? did[k] : 0.f;
-#if GSR_BWD_FACTORED
         S[k] = 0.f;
-#else
-        A0[k] = A1[k] = A2[k] = Ai[k] = 0.f;
-#endif
         // background term of dL/dalpha: -T_final / (1 - alpha) * (bg . dL/dpix)
         TfB[k] = -T[k] * (b0 * dp0[k] + b1 * dp1[k] + b2 * dp2[k]);
         lastk[k] = wave_max_u32(last[k]);  // sub-block k needs list positions < lastk[k]
@@ -420,134 +402,106 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
         const uint32_t cnt = (uint32_t)__popcll(keep);
         if (m) {
             const uint32_t slot = lane_prefix(keep);
-            s_a[slot] = qa;
-            s_b[slot] = make_float4(qb.x, qb.y, __uint_as_float(pos << 4 | m), __uint_as_float(u));
+            s_a[slot] = make_float4(qa.x, qa.y, qa.z * kHalfLog2e, qa.w * kLog2e);  // scaled conic: gauss_p2
+            s_b[slot] = make_float4(qb.x * kHalfLog2e, qb.y, __uint_as_float(pos << 4 | m), __uint_as_float(u));
             s_c[slot] = qc;
+            s_d[slot] = make_float4(qa.z, qa.w, qb.x, 0.f);
         }
         __syncthreads();
-#if GSR_BWD_PREFETCH
-        // the next instance's LDS rows are read one iteration ahead (their latency overlaps the
-        // current instance's pixel work and reduction)
-        float4 na = s_a[0], nb = s_b[0], nc = s_c[0];
-#endif
         for (uint32_t j = 0; j < cnt; j++) {
-#if GSR_BWD_PREFETCH
-            const float4 a = na, b = nb, c = nc;
-            if (j + 1 < cnt) {
-                na = s_a[j + 1];
-                nb = s_b[j + 1];
-                nc = s_c[j + 1];
-            }
-#else
             const float4 a = s_a[j];
             const float4 b = s_b[j];
             const float4 c = s_c[j];
-#endif
-            const float4 cs = make_float4(a.z * kHalfLog2e, a.w * kLog2e, b.x * kHalfLog2e, 0.f);  // gauss_p2
             const uint32_t pm = __builtin_amdgcn_readfirstlane(__float_as_uint(b.z));
-            const uint32_t mk = pm & 0xFu;
+            const uint32_t mk = pm & 0xFu;  // != 0: compacted instances touch a sub-block
             const uint32_t jpos = pm >> 4;
             const float dx = a.x - pfx;
-            const float adxdx_s = cs.x * dx * dx;
-            const float bdx_s = cs.y * dx;
+            const float adxdx_s = a.z * dx * dx;
+            const float bdx_s = a.w * dx;
             float q[10];
-#pragma unroll
-            for (int t = 0; t < 10; t++) q[t] = 0.f;
             bool any = false;
-#pragma unroll
-            for (int k = 0; k < kPixPerLane; k++) {
-#if GSR_BWD_BRANCH
-                if (!((mk >> k) & 1u)) continue;  // scalar branch: sub-block k culled for this instance
-#endif
+            // Sub-block k's replay.  The first active sub-block sets the ten lane sums, later ones
+            // add to them, so a culled sub-block 0 costs no zero moves (the compiler had peeled
+            // k = 0 and materialised the zeros on that path).
+            const auto pix = [&](auto kk, auto ff) {
+                constexpr int k = decltype(kk)::value;
+                constexpr bool first = decltype(ff)::value;
                 const float dy = a.y - pfy[k];
-                const float p2 = gauss_p2(adxdx_s, bdx_s, cs.z, dy);
+                const float p2 = gauss_p2(adxdx_s, bdx_s, b.x, dy);
                 const float G = gexp2(p2);
                 const float alpha = fminf(0.99f, b.y * G);
-                const bool ok = ((mk >> k) & 1u) && jpos < last[k] && !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f);
-                any = any || ok;
+                const bool ok = jpos < last[k] && !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f);
+                any = first ? ok : (any || ok);
                 const float ae = ok ? alpha : 0.f;
                 const float rc = __builtin_amdgcn_rcpf(1.f - ae);
                 T[k] = T[k] * rc;
                 const float dch = ae * T[k];
-#if GSR_BWD_FACTORED
                 // dL/dalpha colour part: sum_c (c_c - A_c) dp_c = (c . dp) - S;  S += alpha (c . dp - S)
                 float cd = fmaf(c.z, dp2[k], fmaf(c.y, dp1[k], c.x * dp0[k]));
                 if (kDepth) cd = fmaf(c.w, did[k], cd);
                 const float dlac = cd - S[k];
                 S[k] = fmaf(ae, dlac, S[k]);
-                q[6] = fmaf(dch, dp0[k], q[6]);
-                q[7] = fmaf(dch, dp1[k], q[7]);
-                q[8] = fmaf(dch, dp2[k], q[8]);
-                if (kDepth) q[9] = fmaf(dch, did[k], q[9]);
-                float dla = fmaf(TfB[k], rc, dlac * T[k]);
+                const float dla = fmaf(TfB[k], rc, dlac * T[k]);
                 // u = G dL/dalpha: the conic / mean terms are opacity * u times (dx, dy) moments,
                 // summed here as sum u, sum u dy, sum u dy^2 (dx is the lane's column: applied
                 // once per instance below; opacity and the conic after the wave sum)
                 const float u = ok ? G * dla : 0.f;
-                q[5] += u;
                 const float uy = u * dy;
-                q[1] += uy;
-                q[4] = fmaf(uy, dy, q[4]);
-#else
-                const float Ge = ok ? G : 0.f;
-                const float d0 = c.x - A0[k];
-                float dla = d0 * dp0[k];
-                A0[k] = fmaf(ae, d0, A0[k]);
-                q[6] = fmaf(dch, dp0[k], q[6]);
-                const float d1 = c.y - A1[k];
-                dla = fmaf(d1, dp1[k], dla);
-                A1[k] = fmaf(ae, d1, A1[k]);
-                q[7] = fmaf(dch, dp1[k], q[7]);
-                const float d2 = c.z - A2[k];
-                dla = fmaf(d2, dp2[k], dla);
-                A2[k] = fmaf(ae, d2, A2[k]);
-                q[8] = fmaf(dch, dp2[k], q[8]);
-                if (kDepth) {
-                    const float di = c.w - Ai[k];
-                    dla = fmaf(di, did[k], dla);
-                    Ai[k] = fmaf(ae, di, Ai[k]);
-                    q[9] = fmaf(dch, did[k], q[9]);
+                if constexpr (first) {
+                    q[6] = dch * dp0[k];
+                    q[7] = dch * dp1[k];
+                    q[8] = dch * dp2[k];
+                    q[9] = kDepth ? dch * did[k] : 0.f;
+                    q[5] = u;
+                    q[1] = uy;
+                    q[4] = uy * dy;
+                } else {
+                    q[6] = fmaf(dch, dp0[k], q[6]);
+                    q[7] = fmaf(dch, dp1[k], q[7]);
+                    q[8] = fmaf(dch, dp2[k], q[8]);
+                    if (kDepth) q[9] = fmaf(dch, did[k], q[9]);
+                    q[5] += u;
+                    q[1] += uy;
+                    q[4] = fmaf(uy, dy, q[4]);
                 }
-                dla = fmaf(TfB[k], rc, dla * T[k]);
-                dla = ok ? dla : 0.f;
-                const float dLdG = b.y * dla;
-                const float gdx = Ge * dx, gdy = Ge * dy;
-                q[0] = fmaf(dLdG, fmaf(-gdy, a.w, -gdx * a.z), q[0]);
-                q[1] = fmaf(dLdG, fmaf(-gdx, a.w, -gdy * b.x), q[1]);
-                const float tg = dLdG * gdx;
-                q[2] = fmaf(tg, dx, q[2]);
-                q[3] = fmaf(tg, dy, q[3]);
-                q[4] = fmaf(dLdG * gdy, dy, q[4]);
-                q[5] = fmaf(Ge, dla, q[5]);
-#endif
+            };
+            using I0 = std::integral_constant<int, 0>;
+            using I1 = std::integral_constant<int, 1>;
+            using I2 = std::integral_constant<int, 2>;
+            using I3 = std::integral_constant<int, 3>;
+            using First = std::true_type;
+            using Next = std::false_type;
+            // scalar branches on the wave-uniform mask: sub-blocks the instance cannot touch are skipped
+            switch (__builtin_ctz(mk)) {
+                case 0:
+                    pix(I0{}, First{});
+                    if (mk & 2u) pix(I1{}, Next{});
+                    if (mk & 4u) pix(I2{}, Next{});
+                    if (mk & 8u) pix(I3{}, Next{});
+                    break;
+                case 1:
+                    pix(I1{}, First{});
+                    if (mk & 4u) pix(I2{}, Next{});
+                    if (mk & 8u) pix(I3{}, Next{});
+                    break;
+                case 2:
+                    pix(I2{}, First{});
+                    if (mk & 8u) pix(I3{}, Next{});
+                    break;
+                default:
+                    pix(I3{}, First{});
+                    break;
             }
-#if GSR_BWD_FACTORED
             // lane moments in dx: q0 = sum u dx, q2 = sum u dx^2, q3 = sum u dx dy (q1 = sum u dy,
             // q4 = sum u dy^2, q5 = sum u)
             q[0] = dx * q[5];
             q[2] = dx * q[0];
             q[3] = dx * q[1];
-#endif
-            // Half-wave sums only (5 DPP stages); lanes 16 and 48 park the two partials in LDS
-            // and they are added once per batch below instead of per instance.
-#if GSR_BWD_RS
-            // reduce-scatter: lane `rs_slot` of rows 1 and 3 parks its half-wave partial
+            // reduce-scatter: lane `rs_slot` of rows 1 and 3 parks its half-wave partial; the two
+            // halves are added once per batch below instead of per instance
             const float h = __any(any) ? wave_rs10(q, lane) : 0.f;
             if ((lane & 16) && rs_slot >= 0)
                 reinterpret_cast<float *>(s_red)[(j * 2 + (lane >> 5)) * 10 + rs_slot] = h;
-#else
-#if GSR_BWD_ALWAYS_REDUCE
-            (void)any;
-            wave_halfsum<kDepth ? 10 : 9>(q);
-#else
-            if (__any(any)) wave_halfsum<kDepth ? 10 : 9>(q);
-#endif
-            if ((lane & 31) == 16) {
-                float2 *d = s_red + (j * 2 + (lane >> 5)) * 5;
-#pragma unroll
-                for (int t = 0; t < 5; t++) d[t] = make_float2(q[2 * t], (kDepth || t < 4) ? q[2 * t + 1] : 0.f);
-            }
-#endif
         }
         __syncthreads();
         float r[10];
@@ -560,12 +514,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
                 r[2 * t + 1] = p0.y + p1.y;
             }
             const size_t o = 4 * (size_t)__float_as_uint(s_b[lane].w);
-#if GSR_BWD_FACTORED
             {
                 // moments -> (dmean2D, dconic): dL/dG = opacity dL/dalpha, dG/d(dx) = -G (a dx + b dy), ...
-                const float4 ia = s_a[lane];
-                const float4 ib = s_b[lane];
-                const float op = ib.y, ca = ia.z, cb = ia.w, cc = ib.x;
+                const float4 id = s_d[lane];
+                const float op = s_b[lane].y, ca = id.x, cb = id.y, cc = id.z;
                 const float m0 = r[0], m1 = r[1], mxx = r[2], mxy = r[3], myy = r[4];
                 r[0] = -op * fmaf(cb, m1, ca * m0);
                 r[1] = -op * fmaf(cb, m0, cc * m1);
@@ -573,7 +525,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
                 r[3] = op * mxy;
                 r[4] = op * myy;
             }
-#endif
             r[0] *= sx;
             r[1] *= sy;
             r[2] *= -0.5f;
