@@ -31,8 +31,9 @@ void launch_preprocess(const GaussianInputs &in, const Camera &cam, const GeomSt
                        hipStream_t s, bool split_color);
 // SH colour of the visible Gaussians (rec.col, clamped) after a split_color preprocess
 bool color_split_supported(const GaussianInputs &in);
+// blocks > 0: a persistent grid of that many blocks (the pass held to part of the chip)
 void launch_preprocess_color(const GaussianInputs &in, const Camera &cam, const GeomState &gs, const int *radii,
-                             hipStream_t s);
+                             hipStream_t s, int blocks = 0);
 // render.hip: tiles ordered heaviest first by work[t] (or, with work == NULL, by list length).
 void launch_tile_order(const uint32_t *work, const uint2 *ranges, int T, int shift, uint32_t *order, hipStream_t s,
                        const uint32_t *kdev = nullptr, uint32_t cap = 0);

@@ -4,6 +4,8 @@
 // Layout: inputs are the caller's AoS tensors (means (P,3), scales (P,3), rotations (P,4),
 // shs (P,M,3)); the output is one 64-B GRec per Gaussian (gsr_device.h) so that every tile
 // instance the render kernels touch is a single cache-line gather.
+#include <algorithm>
+
 #include "gsr_launch.h"
 
 namespace gsr {
@@ -142,21 +144,22 @@ constexpr int kShPitch = 13;               // padded LDS row pitch, in float4
 #define GSR_COLOR_WAVES 8  // 104 KiB per block, one block per CU: it interferes less with the binning beside it
 #endif
 constexpr int kColorWaves = GSR_COLOR_WAVES;  // waves per block (13 KiB of LDS each)
+#ifndef GSR_COLOR_BLOCKS
+#define GSR_COLOR_BLOCKS 0
+#endif
 constexpr int kColorThreads = kColorWaves * kWave;
 
-__global__ __launch_bounds__(kColorThreads) void preprocess_color_kernel(int P, int D, const float *__restrict__ means3D,
-                                                                         const float *__restrict__ shs,
-                                                                         const float *__restrict__ campos,
-                                                                         const float *__restrict__ viewmatrix,
-                                                                         const int *__restrict__ radii, GeomState gs) {
-    __shared__ float4 s_sh[kColorWaves * kWave * kShPitch];
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void color_block(int vb, float4 *s_sh, int P, int D, const float *__restrict__ means3D,
+                                            const float *__restrict__ shs, const float *__restrict__ campos,
+                                            const float *__restrict__ viewmatrix, const int *__restrict__ radii,
+                                            const GeomState &gs) {
+    const int i = vb * blockDim.x + threadIdx.x;
     const bool vis = i < P && radii[i] > 0;
     const int nc = (D + 1) * (D + 1);
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     float4 *S = s_sh + wv * kWave * kShPitch;
     const uint64_t need = __ballot(vis);
-    const int64_t row0 = (int64_t)blockIdx.x * blockDim.x + wv * kWave;
+    const int64_t row0 = (int64_t)vb * blockDim.x + wv * kWave;
     const int cols = (nc * 3 + 3) / 4;  // float4 per row that hold active coefficients
     const float4 *src4 = reinterpret_cast<const float4 *>(shs) + row0 * kShRow;
     float4 v[kShRow];
@@ -204,6 +207,21 @@ __global__ __launch_bounds__(kColorThreads) void preprocess_color_kernel(int P, 
     gs.clamped[i] = clamp_bits;
 }
 
+// GSR_COLOR_BLOCKS > 0: a persistent grid of that many blocks walks the row blocks (so the pass
+// can be held to part of the chip while latency-bound work runs beside it)
+__global__ __launch_bounds__(kColorThreads) void preprocess_color_kernel(int P, int D, const float *__restrict__ means3D,
+                                                                         const float *__restrict__ shs,
+                                                                         const float *__restrict__ campos,
+                                                                         const float *__restrict__ viewmatrix,
+                                                                         const int *__restrict__ radii, GeomState gs,
+                                                                         int nvb) {
+    __shared__ float4 s_sh[kColorWaves * kWave * kShPitch];
+    for (int vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
+        color_block(vb, s_sh, P, D, means3D, shs, campos, viewmatrix, radii, gs);
+        __syncthreads();  // the next row block's staging reuses s_sh
+    }
+}
+
 bool color_split_supported(const GaussianInputs &in) {
     return in.shs && !in.colors_precomp && in.M == 16 && (reinterpret_cast<uintptr_t>(in.shs) % 16 == 0);
 }
@@ -227,10 +245,13 @@ void launch_preprocess(const GaussianInputs &in, const Camera &cam, const GeomSt
 }
 
 void launch_preprocess_color(const GaussianInputs &in, const Camera &cam, const GeomState &gs, const int *radii,
-                             hipStream_t s) {
+                             hipStream_t s, int blocks) {
     if (in.P == 0) return;
-    hipLaunchKernelGGL(preprocess_color_kernel, dim3((in.P + kColorThreads - 1) / kColorThreads), dim3(kColorThreads),
-                       0, s, in.P, in.D, in.means3D, in.shs, cam.campos, cam.view, radii, gs);
+    const int nvb = (in.P + kColorThreads - 1) / kColorThreads;
+    const int cap = blocks > 0 ? blocks : GSR_COLOR_BLOCKS;
+    const int grid = cap > 0 ? std::min(nvb, cap) : nvb;
+    hipLaunchKernelGGL(preprocess_color_kernel, dim3(grid), dim3(kColorThreads), 0, s, in.P, in.D, in.means3D, in.shs,
+                       cam.campos, cam.view, radii, gs, nvb);
 }
 
 __global__ __launch_bounds__(256) void mark_visible_kernel(int P, const float *__restrict__ means3D,

@@ -96,6 +96,18 @@ struct SideJoin {
     }
 };
 
+// compute units of the current device (cached per device)
+int device_cus() {
+    static int cache[kMaxDevices] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return 256;
+    if (!cache[dev]) {
+        int n = 0;
+        cache[dev] = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
+    }
+    return cache[dev];
+}
+
 int fail(int code, const std::string &msg) {
     g_err = msg;
     return code;
@@ -447,15 +459,32 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
         if ((rc = check("preprocess colour", debug, s))) return rc;
     }
 #ifndef GSR_COLOR_FORK
-#define GSR_COLOR_FORK 1  // 0: beside the depth sort and the binning; 1: beside the binning only
+#define GSR_COLOR_FORK 2  // 0: beside the sort and the binning; 1: beside the binning only; 2: chosen per frame
 #endif
+    // The depth sort runs one 1024-thread workgroup per 8192 keys (dsort_blocks) and leaves the
+    // other CUs idle: when it leaves a good share of them, the SH colour pass forks right after the
+    // preprocess as a persistent grid on those CUs (1M Gaussians: 123 sort workgroups, 128 colour
+    // blocks; 2640 -> 2696 Mpix/s, 133 blocks already slowed the sort); otherwise it forks after the sort, beside the
+    // binning, at full width.
+    int color_blocks = 0;
+    bool color_early = GSR_COLOR_FORK == 0;
+    if (GSR_COLOR_FORK == 2 && split && !GSR_COLOR_SERIAL) {
+        // workgroups are dealt round-robin over the 8 XCDs: leave every XCD room for its share
+        // of the sort's workgroups (123 of them -> 16 per XCD -> 8 x (32 - 16) = 128 colour blocks)
+        const int per_xcd = device_cus() / 8;
+        const int free_cus = 8 * (per_xcd - (dsort_blocks(P) + 7) / 8);
+        if (free_cus >= 2 * per_xcd) {
+            color_early = true;
+            color_blocks = free_cus;
+        }
+    }
     auto fork_color = [&]() -> int {
         // fork: the SH colours stream in beside latency-bound main-stream stages; joined before render_fwd
         if (hipEventRecord(fork, s) != hipSuccess || hipStreamWaitEvent(side, fork, 0) != hipSuccess)
             return fail(GSR_ERR_DEVICE, "side stream fork failed");
         {
             StageTimer st(8, side);
-            launch_preprocess_color(in, cam, gs, radii, side);
+            launch_preprocess_color(in, cam, gs, radii, side, color_blocks);
         }
         if (hipEventRecord(join, side) != hipSuccess) return fail(GSR_ERR_DEVICE, "side stream join record failed");
         sj.s = s;
@@ -463,7 +492,7 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
         sj.pending = true;
         return check("preprocess colour", debug, side);
     };
-    if (split && !GSR_COLOR_SERIAL && GSR_COLOR_FORK == 0 && (rc = fork_color())) return rc;
+    if (split && !GSR_COLOR_SERIAL && color_early && (rc = fork_color())) return rc;
     // K sizes the point list.  With a capacity hint from this device's previous frame the binning
     // and the forward render are queued first and K is read afterwards (the GPU never waits on
     // the host's hand-off); kernels that would overrun the capacity exit at once (they compare the
@@ -529,7 +558,7 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
         return GSR_OK;
     };
     if (P > 0 && !defer && (rc = read_K())) return rc;
-    if (split && !GSR_COLOR_SERIAL && GSR_COLOR_FORK == 1 && (rc = fork_color())) return rc;
+    if (split && !GSR_COLOR_SERIAL && !color_early && (rc = fork_color())) return rc;
     bool joined = false;
     auto bin_and_render = [&](int64_t cap) -> int {
         size_t bbytes = 0;
