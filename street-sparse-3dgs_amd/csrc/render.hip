@@ -65,6 +65,9 @@ __device__ __forceinline__ uint32_t lane_prefix(uint64_t mask) {
 // The gather is software-pipelined: while batch b blends, the GRec lines of batch b+1 and the
 // point-list ids of batch b+2 are in flight (two dependent round trips per batch -- id, then the
 // line -- that were otherwise exposed once per batch per wave).
+#ifndef GSR_FWD_SUB
+#define GSR_FWD_SUB 1  // 16x4 sub-blocks per wave (measured: 1 -> 0.139 ms, 2 -> 0.176, 4 -> 0.242)
+#endif
 struct FwdBatch {
     float4 a, b, c;  // GRec q0..q2
     float tm;        // GRec.cull_tm
@@ -81,12 +84,50 @@ __device__ __forceinline__ void fwd_gather(const GRec *__restrict__ rec, uint32_
     o.tm = rec[g].cull_tm;
 }
 
-__global__ __launch_bounds__(256) void render_fwd_sb_kernel(
+// kSub sub-blocks per wave (4 / kSub waves per tile): lane l holds pixels (l & 15, (l >> 4) + 4k) of
+// its wave's sub-blocks k = 0..kSub-1, and the instance's dx terms, LDS reads and list position
+// are shared by the lane's kSub rows.  Fewer waves per tile are slower despite the shared work
+// (kSub 2: 0.176 ms, 4: 0.242 ms vs 0.139 ms for kSub 1 on the bench frame): 4% of the pixels never
+// saturate, so their waves walk the whole list (1700 instances on average), and that walk is
+// serial per wave.  The wave's walk stops when all its pixels have saturated; saturated
+// sub-blocks drop out of the cull mask at the next batch and an instance's culled sub-blocks are
+// skipped with scalar branches.  The list position comes from LDS with the instance (no scalar
+// bit scan and no SGPR->VGPR move per pixel).  Per-pixel arithmetic in the oracle's order.
+#ifndef GSR_FWD_MASKSEL
+#define GSR_FWD_MASKSEL 1
+#endif
+constexpr int kFcmpUGE = 11, kFcmpULE = 13;  // llvm::CmpInst unordered-or predicates: !(x < y), !(x > y)
+// per-lane select by a wave mask held in SGPRs (mask bit set: t)
+__device__ __forceinline__ float lane_select(uint64_t mask, float t, float f) {
+    float r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(mask));
+    return r;
+}
+
+template <int kSub>
+__device__ __forceinline__ uint32_t sub_block_mask_n(const float4 &qa, const float4 &qb, float tm, float tx0,
+                                                     float ty0) {
+    const float X = qa.x, Y = qa.y, ex = qb.z, ey = qb.w;
+    if (!(X + ex >= tx0 && X - ex <= tx0 + 15.f)) return 0u;
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < kSub; k++) {
+        const float y0 = ty0 + (float)(4 * k);
+        if (Y + ey >= y0 && Y - ey <= y0 + 3.f &&
+            (!(GSR_EXACT_CULL & 1) || ellipse_meets_box(X, Y, qa.z, qa.w, qb.x, tm, tx0, tx0 + 15.f, y0, y0 + 3.f)))
+            m |= 1u << k;
+    }
+    return m;
+}
+
+template <int kSub>
+__global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kernel(
     const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list, int W, int H, int gx,
     const GRec *__restrict__ rec, const float *__restrict__ bg, float *__restrict__ out_color,
     float *__restrict__ out_invd, float *__restrict__ final_T, uint32_t *__restrict__ n_contrib,
     uint32_t *__restrict__ tile_work, const uint32_t *__restrict__ fwd_order, const uint32_t *__restrict__ kdev,
     uint32_t cap, const uint32_t *__restrict__ sort_err, float4 *__restrict__ acc, uint32_t acc_n4) {
+    constexpr int kWaves = kPixPerLane / kSub;
     if (kdev && *kdev > cap) return;  // the point-list capacity is short: the host re-runs at K
     {
         // the backward's per-Gaussian accumulator rows (atomic mode) start at zero: every
@@ -97,25 +138,36 @@ __global__ __launch_bounds__(256) void render_fwd_sb_kernel(
         for (uint32_t k = a0 + threadIdx.x; k < a1; k += blockDim.x)
             acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    // per wave, three 64-entry planes: {x, y, conic.a, conic.b}, {conic.c, opacity, -, -},
-    // {r, g, b, 1/depth}; one base address serves all three (offsets 0 / 1 / 2 KiB)
-    __shared__ float4 s_q[4][3][kWave];
-    __shared__ uint32_t s_work[4];
+    __shared__ float4 s_a[kWaves][kWave];  // x, y, a_s, b_s (conic scaled for gauss_p2)
+    __shared__ float4 s_b[kWaves][kWave];  // c_s, opacity, sub-block mask, list position + 1
+    __shared__ float4 s_c[kWaves][kWave];  // r, g, b, 1 / depth
+    __shared__ uint32_t s_work[kWaves];
 
     const int tile = (int)fwd_order[blockIdx.x];
     const int tx = tile % gx, ty = tile / gx;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int px = tx * kTile + (lane & 15);
-    const int py = ty * kTile + 4 * w + (lane >> 4);
-    const float pfx = (float)px, pfy = (float)py;
-    const float tx0 = (float)(tx * kTile), sy0 = (float)(ty * kTile + 4 * w);
-    const bool inside = px < W && py < H;
+    const int sy = ty * kTile + 4 * kSub * w;  // the wave's first pixel row
+    const float pfx = (float)px;
+    const float tx0 = (float)(tx * kTile), sy0 = (float)sy;
 
-    float T = 1.f, C0 = 0.f, C1 = 0.f, C2 = 0.f, ID = 0.f;
-    uint32_t last = 0;
-    bool alive = inside;
+    // liveness: kSub == 1 keeps a lane mask (no branches in the blend); otherwise a dead pixel's
+    // alpha threshold is 2 (above any alpha)
+    float T[kSub], C0[kSub], C1[kSub], C2[kSub], ID[kSub], pfy[kSub], amin[kSub];
+    uint32_t last[kSub];
+    bool alive[kSub];
+#pragma unroll
+    for (int k = 0; k < kSub; k++) {
+        const int py = sy + (lane >> 4) + 4 * k;
+        pfy[k] = (float)py;
+        T[k] = 1.f;
+        C0[k] = C1[k] = C2[k] = ID[k] = 0.f;
+        last[k] = 0u;
+        alive[k] = px < W && py < H;
+        amin[k] = alive[k] ? 1.0f / 255.0f : 2.f;
+    }
+    uint64_t livem = __ballot(alive[0]);  // GSR_FWD_MASKSEL: the live pixels as a wave mask
     const uint2 rg = ranges[tile];
-    // pipeline prologue: batch 0's lines, batch 1's ids (indices clamped to the list)
     FwdBatch cur;
     uint32_t gnext = 0;
     const uint32_t lastpos = rg.y > rg.x ? rg.y - 1u : rg.x;
@@ -124,75 +176,119 @@ __global__ __launch_bounds__(256) void render_fwd_sb_kernel(
         gnext = point_list[min(rg.x + kWave + (uint32_t)lane, lastpos)];
     }
     for (uint32_t base = rg.x; base < rg.y; base += kWave) {
-        if (!__any(alive)) break;
+        uint32_t live = 0;  // sub-blocks with a pixel still accumulating (wave-uniform)
+#pragma unroll
+        for (int k = 0; k < kSub; k++)
+            live |= (kSub == 1 && GSR_FWD_MASKSEL ? livem != 0 : __ballot(kSub == 1 ? alive[k] : amin[k] < 1.f) != 0)
+                        ? 1u << k
+                        : 0u;
+        if (!live) break;
         const bool valid = base + (uint32_t)lane < rg.y;
         const float4 qa = cur.a, qb = cur.b, qc = cur.c;
-        const bool hit = valid && qa.x + qb.z >= tx0 && qa.x - qb.z <= tx0 + 15.f && qa.y + qb.w >= sy0 &&
-                         qa.y - qb.w <= sy0 + 3.f &&
-                         (!(GSR_EXACT_CULL & 1) ||
-                          ellipse_meets_box(qa.x, qa.y, qa.z, qa.w, qb.x, cur.tm, tx0, tx0 + 15.f, sy0, sy0 + 3.f));
+        const uint32_t m = valid ? sub_block_mask_n<kSub>(qa, qb, cur.tm, tx0, sy0) & live : 0u;
         // next batch in flight while this one blends
         fwd_gather(rec, gnext, cur);
         gnext = point_list[min(base + 2 * kWave + (uint32_t)lane, lastpos)];
-        const uint64_t keep = __ballot(hit);
+        const uint64_t keep = __ballot(m != 0u);
         const uint32_t cnt = (uint32_t)__popcll(keep);
-        if (hit) {
+        if (m) {
             const uint32_t slot = lane_prefix(keep);
-            s_q[w][0][slot] = make_float4(qa.x, qa.y, qa.z * kHalfLog2e, qa.w * kLog2e);  // scaled conic: gauss_p2
-            s_q[w][1][slot] = make_float4(qb.x * kHalfLog2e, qb.y, qb.z, qb.w);
-            s_q[w][2][slot] = qc;
+            const uint32_t pos1 = base - rg.x + (uint32_t)lane + 1u;  // n_contrib counts list positions from 1
+            s_a[w][slot] = make_float4(qa.x, qa.y, qa.z * kHalfLog2e, qa.w * kLog2e);
+            s_b[w][slot] = make_float4(qb.x * kHalfLog2e, qb.y, __uint_as_float(m), __uint_as_float(pos1));
+            s_c[w][slot] = qc;
         }
         // wave-private LDS slice: the wave's own writes are visible after its lgkmcnt drain
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
-        // the j-th compacted entry is the j-th set bit of `keep`: its list position comes from a
-        // scalar bit scan, not from LDS
-        uint64_t rem = keep;
-        const uint32_t pos0 = base - rg.x + 1u;
-        for (uint32_t j = 0; j < cnt; j++) {
-            const float4 a = s_q[w][0][j];
-            const float4 b = s_q[w][1][j];
-            const float4 c = s_q[w][2][j];
-            const uint32_t contributor = pos0 + (uint32_t)__builtin_ctzll(rem);
-            rem &= rem - 1ull;
+        const auto blend = [&](uint32_t j) {
+            const float4 a = s_a[w][j];
+            const float4 b = s_b[w][j];
+            const float4 c = s_c[w][j];
+            const uint32_t mk = kSub > 1 ? __builtin_amdgcn_readfirstlane(__float_as_uint(b.z)) : 1u;
+            const uint32_t pos = __float_as_uint(b.w);
             const float dx = a.x - pfx;
-            const float dy = a.y - pfy;
-            const float p2 = gauss_p2(a.z * dx * dx, a.w * dx, b.x, dy);
-            const float alpha = fminf(0.99f, b.y * gexp2(p2));
-            const bool ok = alive && !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f);
-            const float test_T = T * (1.f - alpha);
-            const bool stop = test_T < 0.0001f;
-            const bool acc = ok && !stop;
-            alive = alive && !(ok && stop);
-            const float wgt = acc ? alpha * T : 0.f;
-            C0 = fmaf(c.x, wgt, C0);
-            C1 = fmaf(c.y, wgt, C1);
-            C2 = fmaf(c.z, wgt, C2);
-            ID = fmaf(c.w, wgt, ID);
-            T = acc ? test_T : T;
-            last = acc ? contributor : last;
+            const float adxdx_s = a.z * dx * dx;
+            const float bdx_s = a.w * dx;
+#pragma unroll
+            for (int k = 0; k < kSub; k++) {
+                if (kSub > 1 && !(mk & (1u << k))) continue;
+                const float dy = a.y - pfy[k];
+                const float p2 = gauss_p2(adxdx_s, bdx_s, b.x, dy);
+                const float alpha = fminf(0.99f, b.y * gexp2(p2));
+                if (kSub == 1 && GSR_FWD_MASKSEL) {
+                    // the three tests as wave masks, combined on the scalar unit, and the three
+                    // selects from one mask: one compare of test_T instead of two (the compiler
+                    // materialises both the stop test and its negation)
+                    const float test_T = T[k] * (1.f - alpha);
+                    const uint64_t okm = livem & __builtin_amdgcn_fcmpf(p2, 0.0f, kFcmpULE) &
+                                         __builtin_amdgcn_fcmpf(alpha, 1.0f / 255.0f, kFcmpUGE);
+                    const uint64_t contm = __builtin_amdgcn_fcmpf(test_T, 0.0001f, kFcmpUGE);
+                    const uint64_t accm = okm & contm;
+                    livem &= ~okm | contm;
+                    const float wgt = lane_select(accm, alpha * T[k], 0.f);
+                    C0[k] = fmaf(c.x, wgt, C0[k]);
+                    C1[k] = fmaf(c.y, wgt, C1[k]);
+                    C2[k] = fmaf(c.z, wgt, C2[k]);
+                    ID[k] = fmaf(c.w, wgt, ID[k]);
+                    T[k] = lane_select(accm, test_T, T[k]);
+                    last[k] = __float_as_uint(lane_select(accm, b.w, __uint_as_float(last[k])));
+                    continue;
+                }
+                const bool ok = kSub == 1 ? alive[k] && !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f)
+                                          : !(p2 > 0.0f) && !(alpha < amin[k]);
+                const float test_T = T[k] * (1.f - alpha);
+                const bool cont = !(test_T < 0.0001f);
+                const bool accept = ok && cont;
+                if (kSub == 1) alive[k] = alive[k] && !(ok && !cont);
+                else amin[k] = ok && !cont ? 2.f : amin[k];
+                const float wgt = accept ? alpha * T[k] : 0.f;
+                C0[k] = fmaf(c.x, wgt, C0[k]);
+                C1[k] = fmaf(c.y, wgt, C1[k]);
+                C2[k] = fmaf(c.z, wgt, C2[k]);
+                ID[k] = fmaf(c.w, wgt, ID[k]);
+                T[k] = accept ? test_T : T[k];
+                last[k] = accept ? pos : last[k];
+            }
+        };
+        // two instances per iteration (by hand: the wave-mask compares are convergent, which
+        // blocks the compiler's runtime unrolling) so their independent chains interleave
+        uint32_t j = 0;
+        for (; j + 1 < cnt; j += 2) {
+            blend(j);
+            blend(j + 1);
         }
+        if (j < cnt) blend(j);
         __builtin_amdgcn_wave_barrier();
     }
-    const uint32_t wl = wave_max_u32(last);
-    if (lane == 0) s_work[w] = wl;
-    if (sort_err && *sort_err) {  // the depth sort gave up on a lookback: make the frame unmistakably invalid
-        C0 = C1 = C2 = ID = __builtin_nanf("");
+    const bool bad = sort_err && *sort_err;  // the depth sort gave up on a lookback: NaN frame
+    uint32_t wl = 0;
+#pragma unroll
+    for (int k = 0; k < kSub; k++) {
+        wl = last[k] > wl ? last[k] : wl;
+        const int py = sy + (lane >> 4) + 4 * k;
+        if (px < W && py < H) {
+            const int pix = py * W + px;
+            const float nan = __builtin_nanf("");
+            final_T[pix] = T[k];
+            n_contrib[pix] = last[k];
+            out_color[pix] = bad ? nan : C0[k] + T[k] * bg[0];
+            out_color[H * W + pix] = bad ? nan : C1[k] + T[k] * bg[1];
+            out_color[2 * H * W + pix] = bad ? nan : C2[k] + T[k] * bg[2];
+            if (out_invd) out_invd[pix] = bad ? nan : ID[k];
+        }
     }
-    if (inside) {
-        const int pix = py * W + px;
-        final_T[pix] = T;
-        n_contrib[pix] = last;
-        out_color[pix] = C0 + T * bg[0];
-        out_color[H * W + pix] = C1 + T * bg[1];
-        out_color[2 * H * W + pix] = C2 + T * bg[2];
-        if (out_invd) out_invd[pix] = ID;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t m = s_work[0];
-        for (int k = 1; k < 4; k++) m = s_work[k] > m ? s_work[k] : m;
-        tile_work[tile] = m;
+    wl = wave_max_u32(wl);
+    if (kWaves == 1) {
+        if (lane == 0) tile_work[tile] = wl;
+    } else {
+        if (lane == 0) s_work[w] = wl;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t mx = s_work[0];
+            for (int k = 1; k < kWaves; k++) mx = s_work[k] > mx ? s_work[k] : mx;
+            tile_work[tile] = mx;
+        }
     }
 }
 
@@ -243,10 +339,13 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
     const int T = cam.gx * cam.gy;
     if (T == 0) return;
     // launch order: is.tile_ids (rasterizer.hip, by list length)
-    hipLaunchKernelGGL(render_fwd_sb_kernel, dim3(T), dim3(4 * kWave), 0, s, is.ranges, bs.point_list, cam.W, cam.H,
-                       cam.gx, gs.rec, bg, out_color, out_invdepth, is.final_T, is.n_contrib, is.tile_work,
-                       is.tile_ids, bs.kdev, bs.cap, bs.kdev ? dsort_err_word(gs) : nullptr, gs.acc,
-                       (uint32_t)(4 * (size_t)gs.nacc));
+#define GSR_FWD_LAUNCH(K, NT)                                                                                       \
+    hipLaunchKernelGGL(K, dim3(T), dim3(NT), 0, s, is.ranges, bs.point_list, cam.W, cam.H, cam.gx, gs.rec, bg,      \
+                       out_color, out_invdepth, is.final_T, is.n_contrib, is.tile_work, is.tile_ids, bs.kdev, bs.cap, \
+                       bs.kdev ? dsort_err_word(gs) : nullptr, gs.acc, (uint32_t)(4 * (size_t)gs.nacc))
+    static_assert(GSR_FWD_SUB == 1 || GSR_FWD_SUB == 2 || GSR_FWD_SUB == 4, "GSR_FWD_SUB: 1, 2 or 4");
+    GSR_FWD_LAUNCH(render_fwd_kernel<GSR_FWD_SUB>, kWave * (kPixPerLane / GSR_FWD_SUB));
+#undef GSR_FWD_LAUNCH
 }
 
 // ------------------------------------------------------------------------------------------
