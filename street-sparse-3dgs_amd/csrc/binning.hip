@@ -353,12 +353,33 @@ __global__ __launch_bounds__(64 * kScatterWaves) void sb_scatter_kernel(int P, S
 // entries and each of the SB's tiles (16 at a time), a ballot of "footprint contains the tile"
 // gives the tile's count (pass A) or, after the tile scan, the stable rank of every covering
 // entry (pass B).  Counters and positions are wave-uniform registers: no LDS in the loops.
-constexpr int kTBWaves = 8;
+#ifndef GSR_TB_WAVES
+#define GSR_TB_WAVES 8
+#endif
+constexpr int kTBWaves = GSR_TB_WAVES;
 constexpr int kTileGroup = 16;
 
-__device__ __forceinline__ bool rect_has(uint32_t r, int lx, int ly) {
-    return lx >= (int)(r & 0xFFu) && ly >= (int)((r >> 8) & 0xFFu) && lx <= (int)((r >> 16) & 0xFFu) &&
-           ly <= (int)(r >> 24);
+#ifndef GSR_TB_DEPTH
+#define GSR_TB_DEPTH 2  // list batches in flight per wave (loads issued one group ahead)
+#endif
+constexpr int kTBDepth = GSR_TB_DEPTH;
+
+// Footprint of SB-clipped rect r over tile group [tg, tg + 16) (SB-local row-major), one bit per
+// tile: the column range as a bit run, replicated over the group's rows inside the row range.
+__device__ __forceinline__ uint32_t group_mask(uint32_t r, int tg, int shift) {
+    const int side = 1 << shift;
+    const int x0 = (int)(r & 0xFFu), y0 = (int)((r >> 8) & 0xFFu), x1 = (int)((r >> 16) & 0xFFu),
+              y1 = (int)(r >> 24);
+    if (x1 < x0) return 0u;  // padding entry (0xFF) or empty
+    const uint32_t cols = ((2u << x1) - 1u) & ~((1u << x0) - 1u);  // x1 <= 15
+    const int row0 = tg >> shift, rows = kTileGroup >> shift;     // side <= 16: rows >= 1
+    uint32_t m = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int ry = row0 + q;
+        if (q < rows && ry >= y0 && ry <= y1) m |= cols << (q * side);
+    }
+    return m;
 }
 
 __global__ __launch_bounds__(64 * kTBWaves) void tile_bin_kernel(SBGrid sg, int gx, int gy,
@@ -377,20 +398,34 @@ __global__ __launch_bounds__(64 * kTBWaves) void tile_bin_kernel(SBGrid sg, int 
     const uint32_t L0 = base_g[s], L = base_g[s + 1] - L0;
     const uint32_t seg0 = (uint32_t)(((uint64_t)L * w) / kTBWaves), seg1 = (uint32_t)(((uint64_t)L * (w + 1)) / kTBWaves);
     const uint64_t lt = (1ull << lane) - 1ull;
+    // the wave's list segment in groups of kTBDepth batches: group n + 1's entries are loaded
+    // while group n is ranked (one dependent load latency per group instead of one per batch)
+    const auto load = [&](uint32_t gb, uint2 *e) {
+#pragma unroll
+        for (int d = 0; d < kTBDepth; d++) {
+            const uint32_t i = gb + (uint32_t)(d * 64 + lane);
+            e[d] = i < seg1 ? sblist[L0 + i] : make_uint2(0u, 0xFFu);
+        }
+    };
+    constexpr uint32_t kGroup = 64 * kTBDepth;
 
     // pass A: per-wave tile counts
     for (int tg = 0; tg < tps; tg += kTileGroup) {
         uint32_t cnt[kTileGroup];
 #pragma unroll
         for (int k = 0; k < kTileGroup; k++) cnt[k] = 0u;
-        for (uint32_t ib = seg0; ib < seg1; ib += 64) {
-            const uint32_t i = ib + lane;
-            const uint32_t r = i < seg1 ? sblist[L0 + i].y : 0xFFu;
+        uint2 cur[kTBDepth], nxt[kTBDepth];
+        load(seg0, cur);
+        for (uint32_t gb = seg0; gb < seg1; gb += kGroup) {
+            load(gb + kGroup, nxt);
 #pragma unroll
-            for (int k = 0; k < kTileGroup; k++) {
-                const int t = tg + k;
-                cnt[k] += (uint32_t)__popcll(__ballot(rect_has(r, t & (side - 1), t >> sg.shift)));
+            for (int d = 0; d < kTBDepth; d++) {
+                const uint32_t m = group_mask(cur[d].y, tg, sg.shift);
+#pragma unroll
+                for (int k = 0; k < kTileGroup; k++) cnt[k] += (uint32_t)__popcll(__ballot((m >> k) & 1u));
             }
+#pragma unroll
+            for (int d = 0; d < kTBDepth; d++) cur[d] = nxt[d];
         }
         if (lane == 0)
 #pragma unroll
@@ -431,18 +466,23 @@ __global__ __launch_bounds__(64 * kTBWaves) void tile_bin_kernel(SBGrid sg, int 
         uint32_t pos[kTileGroup];
 #pragma unroll
         for (int k = 0; k < kTileGroup; k++) pos[k] = tg + k < tps ? tc[w][tg + k] : 0u;
-        for (uint32_t ib = seg0; ib < seg1; ib += 64) {
-            const uint32_t i = ib + lane;
-            uint2 e = make_uint2(0u, 0xFFu);
-            if (i < seg1) e = sblist[L0 + i];
+        uint2 cur[kTBDepth], nxt[kTBDepth];
+        load(seg0, cur);
+        for (uint32_t gb = seg0; gb < seg1; gb += kGroup) {
+            load(gb + kGroup, nxt);
 #pragma unroll
-            for (int k = 0; k < kTileGroup; k++) {
-                const int t = tg + k;
-                const bool hit = rect_has(e.y, t & (side - 1), t >> sg.shift);
-                const uint64_t m = __ballot(hit);
-                if (hit) point_list[pos[k] + (uint32_t)__popcll(m & lt)] = e.x;
-                pos[k] += (uint32_t)__popcll(m);
+            for (int d = 0; d < kTBDepth; d++) {
+                const uint32_t m = group_mask(cur[d].y, tg, sg.shift);
+#pragma unroll
+                for (int k = 0; k < kTileGroup; k++) {
+                    const bool hit = (m >> k) & 1u;
+                    const uint64_t bm = __ballot(hit);
+                    if (hit) point_list[pos[k] + (uint32_t)__popcll(bm & lt)] = cur[d].x;
+                    pos[k] += (uint32_t)__popcll(bm);
+                }
             }
+#pragma unroll
+            for (int d = 0; d < kTBDepth; d++) cur[d] = nxt[d];
         }
     }
 }
