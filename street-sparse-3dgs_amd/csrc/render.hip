@@ -359,6 +359,9 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
 // Sub-blocks an instance cannot touch (ellipse box, or past the sub-block's last contributor) are
 // skipped with a scalar branch on the wave-uniform mask: 0.479 vs 0.502 ms for the predicated
 // form on the 1M-Gaussian 1080p bench scene once tiles run heaviest-first.
+#ifndef GSR_BWD_BG_IN_S
+#define GSR_BWD_BG_IN_S 1  // 0: upstream's separate background term (one more FMA per pixel)
+#endif
 #ifndef GSR_BWD_WAVES_PER_EU
 #define GSR_BWD_WAVES_PER_EU 1
 #endif
@@ -419,10 +422,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
     const float tx0 = (float)(tx * kTile), ty0 = (float)(ty * kTile);
     const float b0 = bg[0], b1 = bg[1], b2 = bg[2];
 
-    float T[kPixPerLane], TfB[kPixPerLane], dp0[kPixPerLane], dp1[kPixPerLane], dp2[kPixPerLane], did[kPixPerLane];
+    float T[kPixPerLane], dp0[kPixPerLane], dp1[kPixPerLane], dp2[kPixPerLane], did[kPixPerLane];
     // S = sum_c A_c dL/dpix_c: the colour (and inverse depth) accumulated behind the current
-    // instance, already dotted with the pixel's upstream gradient -- the only form dL/dalpha needs
-    float S[kPixPerLane], pfy[kPixPerLane];
+    // instance, already dotted with the pixel's upstream gradient -- the only form dL/dalpha needs.
+    // The background is the layer behind the last contributor (alpha 1, colour bg): S starts at
+    // bg . dL/dpix, which folds upstream's -T_final (bg . dL/dpix) / (1 - alpha) term into
+    // T (cd - S) -- T_i S_i then carries T_final bg / (1 - alpha_i) by the same recurrence.
+    float S[kPixPerLane], pfy[kPixPerLane], TfB[kPixPerLane];
     uint32_t last[kPixPerLane], lastk[kPixPerLane];
     uint32_t maxlast = 0;
     // every per-pixel input load first (clamped to the image, zeroed outside it), so the 24 loads
@@ -448,9 +454,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
         dp1[k] = inside ? dp1[k] : 0.f;
         dp2[k] = inside ? dp2[k] : 0.f;
         did[k] = inside ? did[k] : 0.f;
-        S[k] = 0.f;
-        // background term of dL/dalpha: -T_final / (1 - alpha) * (bg . dL/dpix)
-        TfB[k] = -T[k] * (b0 * dp0[k] + b1 * dp1[k] + b2 * dp2[k]);
+        S[k] = GSR_BWD_BG_IN_S ? fmaf(b2, dp2[k], fmaf(b1, dp1[k], b0 * dp0[k])) : 0.f;
+        TfB[k] = GSR_BWD_BG_IN_S ? 0.f : -T[k] * (b0 * dp0[k] + b1 * dp1[k] + b2 * dp2[k]);
         lastk[k] = wave_max_u32(last[k]);  // sub-block k needs list positions < lastk[k]
         maxlast = lastk[k] > maxlast ? lastk[k] : maxlast;
     }
@@ -540,7 +545,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
                 if (kDepth) cd = fmaf(c.w, did[k], cd);
                 const float dlac = cd - S[k];
                 S[k] = fmaf(ae, dlac, S[k]);
-                const float dla = fmaf(TfB[k], rc, dlac * T[k]);
+                const float dla = GSR_BWD_BG_IN_S ? dlac * T[k] : fmaf(TfB[k], rc, dlac * T[k]);
                 // u = G dL/dalpha: the conic / mean terms are opacity * u times (dx, dy) moments,
                 // summed here as sum u, sum u dy, sum u dy^2 (dx is the lane's column: applied
                 // once per instance below; opacity and the conic after the wave sum)
