@@ -34,6 +34,9 @@ CASES = [
     dict(name="equal_depths", P=3000, W=96, H=64, deg=1, seed=9, log_scale=-3.0, flat_z=6.0),
     # many depth-sort tiles (8192 keys each) with ties across tiles and culled Gaussians mixed in
     dict(name="sort_tiles_ties", P=40000, W=128, H=96, deg=0, seed=14, log_scale=-3.5, behind=0.2, quant_z=0.25),
+    # depth keys spanning more than 2^27 float steps (z 0.25 .. 1e5): the depth sort's 4 x 8-bit
+    # layout (every other case fits the 3 x 9-bit one); culled Gaussians mixed in
+    dict(name="wide_depth_4pass", P=4000, W=96, H=64, deg=1, seed=16, log_scale=-3.0, far=0.3, behind=0.1),
     # footprints over tens of 4x4-tile superblocks next to small ones (the binning's wave-wide path)
     dict(name="huge_splats_sb", P=300, W=640, H=480, deg=1, seed=15, log_scale=-0.5),
 ]
@@ -54,6 +57,19 @@ def make_scene(c):
         z = np.maximum(np.round(m[:, 2] / c["quant_z"]), 1.0).astype(np.float32) * np.float32(c["quant_z"])
         m[:, :2] *= z[:, None] / m[:, 2:3]
         m[:, 2] = z
+    if c.get("far"):
+        # a fraction moved along its ray to z in [1e3, 1e5] (log-uniform), scaled to stay visible,
+        # and one Gaussian pulled in to z = 0.25
+        rng = np.random.default_rng(c["seed"] + 200)
+        idx = np.nonzero(rng.random(c["P"]) < c["far"])[0]
+        m = s["means3D"]
+        znew = np.exp(rng.uniform(np.log(1e3), np.log(1e5), len(idx))).astype(np.float32)
+        f = znew / m[idx, 2]
+        m[idx] *= f[:, None]
+        s["scales"][idx] *= f[:, None]
+        f0 = np.float32(0.25) / m[0, 2]
+        m[0] *= f0
+        s["scales"][0] *= f0
     if c.get("behind"):
         rng = np.random.default_rng(c["seed"] + 100)
         idx = rng.random(c["P"]) < c["behind"]

@@ -83,16 +83,16 @@ int main(int argc, char **argv) {
                            (uint32_t *)nullptr);
         CK(hipEventRecord(ev[1], s));
         hipLaunchKernelGGL(dsort_pass_kernel<0>, dim3(nb), dim3(kDsThreads), 0, s, P, nb, gs.dkey, gs.dkey_sorted,
-                           (const uint32_t *)nullptr, gs.ids, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect);
+                           (const uint32_t *)nullptr, gs.ids, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect, (uint32_t *)nullptr);
         CK(hipEventRecord(ev[2], s));
         hipLaunchKernelGGL(dsort_pass_kernel<1>, dim3(nb), dim3(kDsThreads), 0, s, P, nb, gs.dkey_sorted, gs.dkey,
-                           gs.ids, gs.order, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect);
+                           gs.ids, gs.order, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect, (uint32_t *)nullptr);
         CK(hipEventRecord(ev[3], s));
         hipLaunchKernelGGL(dsort_pass_kernel<2>, dim3(nb), dim3(kDsThreads), 0, s, P, nb, gs.dkey, gs.dkey_sorted,
-                           gs.order, gs.ids, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect);
+                           gs.order, gs.ids, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect, (uint32_t *)nullptr);
         CK(hipEventRecord(ev[4], s));
         hipLaunchKernelGGL(dsort_pass_kernel<3>, dim3(nb), dim3(kDsThreads), 0, s, P, nb, gs.dkey_sorted,
-                           (uint32_t *)nullptr, gs.ids, gs.order, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect);
+                           (uint32_t *)nullptr, gs.ids, gs.order, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect, (uint32_t *)nullptr);
         CK(hipEventRecord(ev[5], s));
         CK(hipStreamSynchronize(s));
         if (it >= 2)
