@@ -93,6 +93,9 @@ __device__ __forceinline__ void fwd_gather(const GRec *__restrict__ rec, uint32_
 // sub-blocks drop out of the cull mask at the next batch and an instance's culled sub-blocks are
 // skipped with scalar branches.  The list position comes from LDS with the instance (no scalar
 // bit scan and no SGPR->VGPR move per pixel).  Per-pixel arithmetic in the oracle's order.
+#ifndef GSR_FWD_POLY
+#define GSR_FWD_POLY 1  // exponent as a quadratic in the sub-block-local pixel offset (5 FMAs)
+#endif
 #ifndef GSR_FWD_MASKSEL
 #define GSR_FWD_MASKSEL 1
 #endif
@@ -149,6 +152,10 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kerne
     const int px = tx * kTile + (lane & 15);
     const int sy = ty * kTile + 4 * kSub * w;  // the wave's first pixel row
     const float pfx = (float)px;
+    // kPoly: the lane's offset from its sub-block's centre and its products (exact in fp32)
+    constexpr bool kPoly = GSR_FWD_POLY && kSub == 1;
+    const float lx = (float)(lane & 15) - 7.5f, ly = (float)(lane >> 4) - 1.5f;
+    const float lxx = lx * lx, lxy = lx * ly, lyy = ly * ly;
     const float tx0 = (float)(tx * kTile), sy0 = (float)sy;
 
     // liveness: kSub == 1 keeps a lane mask (no branches in the blend); otherwise a dead pixel's
@@ -194,8 +201,20 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kerne
         if (m) {
             const uint32_t slot = lane_prefix(keep);
             const uint32_t pos1 = base - rg.x + (uint32_t)lane + 1u;  // n_contrib counts list positions from 1
-            s_a[w][slot] = make_float4(qa.x, qa.y, qa.z * kHalfLog2e, qa.w * kLog2e);
-            s_b[w][slot] = make_float4(qb.x * kHalfLog2e, qb.y, __uint_as_float(m), __uint_as_float(pos1));
+            const float as = qa.z * kHalfLog2e, bs = qa.w * kLog2e, cs = qb.x * kHalfLog2e;
+            if (kPoly) {
+                // the exponent as a quadratic in the pixel's offset (lx, ly) from the sub-block
+                // centre: p2 = F + D lx + E ly + a lx^2 - b lx ly + c ly^2
+                const float X = qa.x - (tx0 + 7.5f), Y = qa.y - (sy0 + 1.5f);
+                const float F = fmaf(-(bs * X), Y, fmaf(cs * Y, Y, (as * X) * X));
+                const float D = fmaf(bs, Y, (-2.f * as) * X);
+                const float E = fmaf(bs, X, (-2.f * cs) * Y);
+                s_a[w][slot] = make_float4(F, D, E, as);
+                s_b[w][slot] = make_float4(-bs, qb.y, cs, __uint_as_float(pos1));
+            } else {
+                s_a[w][slot] = make_float4(qa.x, qa.y, as, bs);
+                s_b[w][slot] = make_float4(cs, qb.y, __uint_as_float(m), __uint_as_float(pos1));
+            }
             s_c[w][slot] = qc;
         }
         // wave-private LDS slice: the wave's own writes are visible after its lgkmcnt drain
@@ -206,15 +225,17 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kerne
             const float4 b = s_b[w][j];
             const float4 c = s_c[w][j];
             const uint32_t mk = kSub > 1 ? __builtin_amdgcn_readfirstlane(__float_as_uint(b.z)) : 1u;
+            // kPoly: a = (F, D, E, a_s), b = (-b_s, opacity, c_s, position)
             const uint32_t pos = __float_as_uint(b.w);
-            const float dx = a.x - pfx;
+            const float dx = kPoly ? 0.f : a.x - pfx;
             const float adxdx_s = a.z * dx * dx;
             const float bdx_s = a.w * dx;
 #pragma unroll
             for (int k = 0; k < kSub; k++) {
                 if (kSub > 1 && !(mk & (1u << k))) continue;
                 const float dy = a.y - pfy[k];
-                const float p2 = gauss_p2(adxdx_s, bdx_s, b.x, dy);
+                const float p2 = kPoly ? fmaf(a.w, lxx, fmaf(b.x, lxy, fmaf(b.z, lyy, fmaf(a.y, lx, fmaf(a.z, ly, a.x)))))
+                                       : gauss_p2(adxdx_s, bdx_s, b.x, dy);
                 const float alpha = fminf(0.99f, b.y * gexp2(p2));
                 if (kSub == 1 && GSR_FWD_MASKSEL) {
                     // the three tests as wave masks, combined on the scalar unit, and the three
