@@ -257,11 +257,22 @@ __global__ __launch_bounds__(64 * kScatterWaves) void sb_scatter_kernel(int P, S
     uint32_t *run = wc + w * nsb;
     uint64_t *msk = reinterpret_cast<uint64_t *>(wc + kScatterWaves * nsb) + w * nsb;
     const uint64_t lt = (1ull << lane) - 1ull;
+    // the SB bases of this chunk (read after the counting): loads issued now
+    constexpr int kSBPerThread = (kMaxSB + 64 * kScatterWaves - 1) / (64 * kScatterWaves);
+    uint32_t sbase[kSBPerThread];
+#pragma unroll
+    for (int q = 0; q < kSBPerThread; q++) {
+        const int sq = (int)threadIdx.x + q * 64 * kScatterWaves;
+        sbase[q] = sq < nsb ? base_g[sq] + col[(size_t)sq * sg.nchunks + chunk] : 0u;
+    }
+    // list loads one batch ahead of their use
+    const auto rect_at = [&](int j) { return j < jw1 ? drect[j] : make_uint2(0u, 0u); };
 
     // per-wave SB counts
+    uint2 rnext = rect_at(jw0 + lane);
     for (int jb = jw0; jb < jw1; jb += 64) {
-        const int j = jb + lane;
-        const TileRect r = j < jw1 ? unpack_rect(drect[j]) : TileRect{0, 0, -1, -1};
+        const TileRect r = unpack_rect(rnext);
+        rnext = rect_at(jb + 64 + lane);
         const SBFoot f = sb_foot(r, sg.shift);
         const bool small = f.n <= kSmallSB;
 #pragma unroll
@@ -274,8 +285,11 @@ __global__ __launch_bounds__(64 * kScatterWaves) void sb_scatter_kernel(int P, S
         }
     }
     __syncthreads();
-    for (int s = threadIdx.x; s < nsb; s += 64 * kScatterWaves) {
-        uint32_t b = base_g[s] + col[(size_t)s * sg.nchunks + chunk];
+#pragma unroll
+    for (int q = 0; q < kSBPerThread; q++) {
+        const int s = (int)threadIdx.x + q * 64 * kScatterWaves;
+        if (s >= nsb) break;
+        uint32_t b = sbase[q];
         for (int k = 0; k < kScatterWaves; k++) {
             const uint32_t c = wc[k * nsb + s];
             wc[k * nsb + s] = b;
@@ -284,14 +298,14 @@ __global__ __launch_bounds__(64 * kScatterWaves) void sb_scatter_kernel(int P, S
     }
     __syncthreads();
 
+    const auto id_at = [&](int j) { return j < jw1 ? order[j] : 0u; };
+    uint32_t gnext = id_at(jw0 + lane);
+    rnext = rect_at(jw0 + lane);
     for (int jb = jw0; jb < jw1; jb += 64) {
-        const int j = jb + lane;
-        uint32_t g = 0;
-        TileRect r{0, 0, -1, -1};
-        if (j < jw1) {
-            g = order[j];
-            r = unpack_rect(drect[j]);
-        }
+        const uint32_t g = gnext;
+        const TileRect r = unpack_rect(rnext);  // (0, 0) past the end: no tiles
+        gnext = id_at(jb + 64 + lane);
+        rnext = rect_at(jb + 64 + lane);
         const SBFoot f = sb_foot(r, sg.shift);
         const bool small = f.n <= kSmallSB;
         const uint64_t bigs = __ballot(!small);
