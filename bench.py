@@ -250,7 +250,13 @@ def config5(a, dev):
         frame(sp)
         parts.append([1e3 * (sp[i + 1] - sp[i]) for i in range(3)])
     parts = np.median(np.array(parts), 0)
-    out = {"ms_per_frame": round(ms, 3), "fwd_mpix_s": round(W * H / ms / 1e3, 1), "nodes": N,
+    # the rasterizer's own stages for one more frame (HIP events on its stream)
+    from diff_gaussian_rasterization import _C
+    _C.set_profiling(True)
+    frame()
+    stages = {k: round(v, 4) for k, v in _C.stage_times_ms().items()}
+    _C.set_profiling(False)
+    out = {"ms_per_frame": round(ms, 3), "raster_stages_ms": stages, "fwd_mpix_s": round(W * H / ms / 1e3, 1), "nodes": N,
            "leaves": a.c5_leaves, "tau": a.c5_tau, "leaf_log_scale": a.c5_log_scale, "cut": n, "rendered": n + h["skybox"],
            "visible": int((radii > 0).sum().item()), "width": W, "height": H,
            "split_ms": {"cut_and_weights": round(float(parts[0]), 3), "blend": round(float(parts[1]), 3),
