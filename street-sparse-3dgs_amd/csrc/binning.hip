@@ -368,9 +368,14 @@ __global__ __launch_bounds__(64 * kScatterWaves) void sb_scatter_kernel(int P, S
 // gives the tile's count (pass A) or, after the tile scan, the stable rank of every covering
 // entry (pass B).  Counters and positions are wave-uniform registers: no LDS in the loops.
 #ifndef GSR_TB_WAVES
-#define GSR_TB_WAVES 8
+#define GSR_TB_WAVES 8  // waves per superblock for short lists (1M Gaussians: 8 > 16 > 4)
 #endif
-constexpr int kTBWaves = GSR_TB_WAVES;
+#ifndef GSR_TB_WAVES_LONG
+#define GSR_TB_WAVES_LONG 16  // ... and for long ones (more than GSR_TB_LONG Gaussians per SB on average)
+#endif
+#ifndef GSR_TB_LONG
+#define GSR_TB_LONG 4096
+#endif
 constexpr int kTileGroup = 16;
 
 #ifndef GSR_TB_DEPTH
@@ -396,6 +401,7 @@ __device__ __forceinline__ uint32_t group_mask(uint32_t r, int tg, int shift) {
     return m;
 }
 
+template <int kTBWaves>
 __global__ __launch_bounds__(64 * kTBWaves) void tile_bin_kernel(SBGrid sg, int gx, int gy,
                                                                  const uint32_t *__restrict__ base_g,
                                                                  const uint32_t *__restrict__ base_i,
@@ -550,7 +556,13 @@ void launch_binning_tiles(int P, const Camera &cam, const GeomState &gs, const B
         (void)hipMemsetAsync(is.ranges, 0, sizeof(uint2) * (size_t)T, s);
         return;
     }
-    hipLaunchKernelGGL(tile_bin_kernel, dim3(sg.nsb), dim3(64 * kTBWaves), 0, s, sg, cam.gx, cam.gy, gs.sb_base_g,
+    // long superblock lists (large P): more waves per superblock, the 510-ish workgroups of a
+    // 1080p frame are too few to hide the list walk's latency otherwise
+    if ((int64_t)P > (int64_t)GSR_TB_LONG * sg.nsb)
+        hipLaunchKernelGGL(tile_bin_kernel<GSR_TB_WAVES_LONG>, dim3(sg.nsb), dim3(64 * GSR_TB_WAVES_LONG), 0, s, sg, cam.gx, cam.gy, gs.sb_base_g,
+                       gs.sb_base_i, bs.sblist, bs.point_list, is.ranges, bs.kdev, bs.cap);
+    else
+        hipLaunchKernelGGL(tile_bin_kernel<GSR_TB_WAVES>, dim3(sg.nsb), dim3(64 * GSR_TB_WAVES), 0, s, sg, cam.gx, cam.gy, gs.sb_base_g,
                        gs.sb_base_i, bs.sblist, bs.point_list, is.ranges, bs.kdev, bs.cap);
 }
 
