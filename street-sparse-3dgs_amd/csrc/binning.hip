@@ -521,8 +521,10 @@ SBGrid sb_grid(int gx, int gy, int P) {
         g.shift++;
     }
     // The per-(SB, chunk) counters are written column-major ([nsb][nchunks], one 4-B store per
-    // SB and chunk): past ~1.5K chunks they outgrow the caches and every store becomes a partial
-    // HBM line write (sb_count 282 us at 5.1M Gaussians), so large P takes bigger chunks.
+    // SB and chunk): with too many chunks they outgrow the caches and every store becomes a partial
+    // HBM line write (sb_count 282 us at 5.1M Gaussians and 1K-Gaussian chunks), so large P takes
+    // bigger chunks (at most GSR_MAX_CHUNKS of them; too few, and sb_scatter's per-wave walks get
+    // long).
     g.chunk = kSBChunk;
     while ((P + g.chunk - 1) / g.chunk > kMaxChunks) g.chunk *= 2;
     g.nchunks = (P + g.chunk - 1) / g.chunk;

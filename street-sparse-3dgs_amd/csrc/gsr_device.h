@@ -430,7 +430,7 @@ static_assert(sizeof(GRec) == 64, "GRec must be one 64-B line");
 #endif
 constexpr int kSBChunk = GSR_SB_CHUNK;  // smallest level-1 chunk (SBGrid.chunk doubles for large P)
 #ifndef GSR_MAX_CHUNKS
-#define GSR_MAX_CHUNKS 1536
+#define GSR_MAX_CHUNKS 3072  // config 5 (7.4M): 3072 -> bin_superblocks 0.40 ms, 1536 -> 0.43, 768 -> 0.51
 #endif
 constexpr int kMaxChunks = GSR_MAX_CHUNKS;  // chunks before SBGrid.chunk doubles
 constexpr int kMaxSB = 1536;          // superblocks (3 x 8 waves x 4 B of LDS each in sb_scatter)
