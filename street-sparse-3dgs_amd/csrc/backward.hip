@@ -257,6 +257,18 @@ __global__ __launch_bounds__(256) void record_sum_kernel(int P, int gx, const fl
 }
 
 constexpr int kShPitch = 13;  // padded LDS row pitch (float4) of the staged SH rows
+#ifndef GSR_BWD_NT
+#define GSR_BWD_NT 1  // gradient rows written with non-temporal stores (streamed once, never re-read here)
+#endif
+__device__ __forceinline__ void st_out(float *p, float v) {
+    if (GSR_BWD_NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+__device__ __forceinline__ void st_out(float4 *p, float4 v) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    if (GSR_BWD_NT) __builtin_nontemporal_store(f4{v.x, v.y, v.z, v.w}, reinterpret_cast<f4 *>(p));
+    else *p = v;
+}
 #ifndef GSR_BWD_SKIP_DEAD
 #define GSR_BWD_SKIP_DEAD 1
 #endif
@@ -292,10 +304,10 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
             for (int k = 0; k < 10; k++) g[k] = 0.f;
         }
         if (valid) {
-            out.dmeans2D[3 * i + 0] = g[0];
-            out.dmeans2D[3 * i + 1] = g[1];
-            out.dmeans2D[3 * i + 2] = 0.f;
-            out.dopacity[i] = g[5];
+            st_out(&out.dmeans2D[3 * i + 0], g[0]);
+            st_out(&out.dmeans2D[3 * i + 1], g[1]);
+            st_out(&out.dmeans2D[3 * i + 2], 0.f);
+            st_out(&out.dopacity[i], g[5]);
         }
     } else {
         const float4 s0 = sc.gsum[2 * (size_t)iv], s1 = sc.gsum[2 * (size_t)iv + 1];
@@ -467,7 +479,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
 #pragma unroll
         for (int k = 0; k < 12; k++) {
             const int f = k * kWave + lane, row = f / 12;
-            if (row0 + row < P) dst4[f] = S[row * kShPitch + (f - row * 12)];
+            if (row0 + row < P) st_out(&dst4[f], S[row * kShPitch + (f - row * 12)]);
         }
         if (valid && out.dcolors) {
             out.dcolors[3 * i + 0] = 0.f;
@@ -520,9 +532,9 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
         out.dcolors[3 * i + 1] = g[7];
         out.dcolors[3 * i + 2] = g[8];
     }
-    out.dmeans3D[3 * i + 0] = dm[0];
-    out.dmeans3D[3 * i + 1] = dm[1];
-    out.dmeans3D[3 * i + 2] = dm[2];
+    st_out(&out.dmeans3D[3 * i + 0], dm[0]);
+    st_out(&out.dmeans3D[3 * i + 1], dm[1]);
+    st_out(&out.dmeans3D[3 * i + 2], dm[2]);
 
     // ---- cov3D -> scale / rotation ----
     if (has_scales) {
@@ -560,10 +572,10 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
             dq[3] = 2.f * (-2.f * z * Gr[0][0] - r * Gr[0][1] + x * Gr[0][2] + r * Gr[1][0] - 2.f * z * Gr[1][1] +
                            y * Gr[1][2] + x * Gr[2][0] + y * Gr[2][1]);
         }
-        out.dscales[3 * i + 0] = ds[0];
-        out.dscales[3 * i + 1] = ds[1];
-        out.dscales[3 * i + 2] = ds[2];
-        reinterpret_cast<float4 *>(out.drots)[i] = make_float4(dq[0], dq[1], dq[2], dq[3]);
+        st_out(&out.dscales[3 * i + 0], ds[0]);
+        st_out(&out.dscales[3 * i + 1], ds[1]);
+        st_out(&out.dscales[3 * i + 2], ds[2]);
+        st_out(&reinterpret_cast<float4 *>(out.drots)[i], make_float4(dq[0], dq[1], dq[2], dq[3]));
         if (out.dcov3D)  // optional with scales/rotations (no cov3D_precomp input)
 #pragma unroll
             for (int k = 0; k < 6; k++) out.dcov3D[6 * i + k] = 0.f;
