@@ -8,6 +8,10 @@
 
 #include "gsr_launch.h"
 
+#ifndef GSR_SH_NT
+#define GSR_SH_NT 0  // SH coefficient rows read with non-temporal loads in the colour pass
+#endif
+
 namespace gsr {
 
 template <bool kVecSH, bool kSplitColor>
@@ -167,7 +171,15 @@ __device__ __forceinline__ void color_block(int vb, float4 *s_sh, int P, int D, 
     for (int k = 0; k < kShRow; k++) {
         const int f = k * kWave + lane, row = f / kShRow, col = f - row * kShRow;
         v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (((need >> row) & 1ull) && col < cols) v[k] = src4[f];
+        if (((need >> row) & 1ull) && col < cols) {
+            if (GSR_SH_NT) {
+                typedef float f4 __attribute__((ext_vector_type(4)));
+                const f4 t = __builtin_nontemporal_load(reinterpret_cast<const f4 *>(src4 + f));
+                v[k] = make_float4(t.x, t.y, t.z, t.w);
+            } else {
+                v[k] = src4[f];
+            }
+        }
     }
 #pragma unroll
     for (int k = 0; k < kShRow; k++) {

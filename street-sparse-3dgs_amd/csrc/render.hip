@@ -65,6 +65,9 @@ __device__ __forceinline__ uint32_t lane_prefix(uint64_t mask) {
 // The gather is software-pipelined: while batch b blends, the GRec lines of batch b+1 and the
 // point-list ids of batch b+2 are in flight (two dependent round trips per batch -- id, then the
 // line -- that were otherwise exposed once per batch per wave).
+#ifndef GSR_ACC_NT
+#define GSR_ACC_NT 1
+#endif
 #ifndef GSR_FWD_SUB
 #define GSR_FWD_SUB 1  // 16x4 sub-blocks per wave (measured: 1 -> 0.139 ms, 2 -> 0.176, 4 -> 0.242)
 #endif
@@ -139,7 +142,11 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kerne
         const uint32_t per = (acc_n4 + gridDim.x - 1) / gridDim.x;
         const uint32_t a0 = blockIdx.x * per, a1 = min(acc_n4, a0 + per);
         for (uint32_t k = a0 + threadIdx.x; k < a1; k += blockDim.x)
-            acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        {
+            typedef float f4 __attribute__((ext_vector_type(4)));
+            if (GSR_ACC_NT) __builtin_nontemporal_store(f4{0.f, 0.f, 0.f, 0.f}, reinterpret_cast<f4 *>(acc + k));
+            else acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
     }
     __shared__ float4 s_a[kWaves][kWave];  // x, y, a_s, b_s (conic scaled for gauss_p2)
     __shared__ float4 s_b[kWaves][kWave];  // c_s, opacity, sub-block mask, list position + 1
