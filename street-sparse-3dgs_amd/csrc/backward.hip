@@ -260,6 +260,15 @@ constexpr int kShPitch = 13;  // padded LDS row pitch (float4) of the staged SH 
 #ifndef GSR_BWD_NT
 #define GSR_BWD_NT 1  // gradient rows written with non-temporal stores (streamed once, never re-read here)
 #endif
+#ifndef GSR_ACC_LD_NT
+#define GSR_ACC_LD_NT 0  // measured: non-temporal accumulator loads slow preprocess_bwd (82 -> 85 us)
+#endif
+__device__ __forceinline__ float4 ld_acc(const float4 *p) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    if (!GSR_ACC_LD_NT) return *p;
+    const f4 t = __builtin_nontemporal_load(reinterpret_cast<const f4 *>(p));
+    return make_float4(t.x, t.y, t.z, t.w);
+}
 __device__ __forceinline__ void st_out(float *p, float v) {
     if (GSR_BWD_NT) __builtin_nontemporal_store(v, p);
     else *p = v;
@@ -295,7 +304,9 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
     float g[10];
     if (sc.atomic) {
         // render_bwd's atomic accumulator row (zeroed by render_fwd; untouched rows stay zero)
-        const float4 a0 = sc.acc[4 * (size_t)iv], a1 = sc.acc[4 * (size_t)iv + 1], a2 = sc.acc[4 * (size_t)iv + 2];
+        // the rows are dead after this read: non-temporal loads keep them out of the caches
+        const float4 a0 = ld_acc(sc.acc + 4 * (size_t)iv), a1 = ld_acc(sc.acc + 4 * (size_t)iv + 1),
+                     a2 = ld_acc(sc.acc + 4 * (size_t)iv + 2);
         g[0] = a0.x; g[1] = a0.y; g[2] = a0.z; g[3] = a0.w;
         g[4] = a1.x; g[5] = a1.y; g[6] = a1.z; g[7] = a1.w;
         g[8] = a2.x; g[9] = a2.y;

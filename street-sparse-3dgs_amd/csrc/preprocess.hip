@@ -14,6 +14,11 @@
 
 namespace gsr {
 
+#ifndef GSR_PARAM_NT
+#define GSR_PARAM_NT 1  // parameter rows read with non-temporal loads in the preprocess (read once per frame)
+#endif
+__device__ __forceinline__ float ldp(const float *p) { return GSR_PARAM_NT ? __builtin_nontemporal_load(p) : *p; }
+
 template <bool kVecSH, bool kSplitColor>
 __global__ __launch_bounds__(256) void preprocess_kernel(
     int P, int D, int M, const float *__restrict__ means3D, const float *__restrict__ scales, float mod,
@@ -31,7 +36,7 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
     gs.tiles[i] = 0;
     gs.dkey[i] = 0xFFFFFFFFu;  // culled Gaussians sort behind every visible one
     gs.rect8[i] = make_uint2(0u, 0u);
-    const float3 p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
+    const float3 p = make_float3(ldp(means3D + 3 * i), ldp(means3D + 3 * i + 1), ldp(means3D + 3 * i + 2));
     const float3 pv = xf_point43(p, V);
     if (pv.z <= 0.2f) return;  // in_frustum (prefiltered is treated as a plain cull)
     const float4 ph = xf_point44(p, Pm);
@@ -43,8 +48,9 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
 #pragma unroll
         for (int k = 0; k < 6; k++) c3[k] = cov3D_precomp[6 * i + k];
     } else {
-        const float3 s = make_float3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
-        const float4 q = reinterpret_cast<const float4 *>(rotations)[i];
+        const float3 s = make_float3(ldp(scales + 3 * i), ldp(scales + 3 * i + 1), ldp(scales + 3 * i + 2));
+        const float4 q = make_float4(ldp(rotations + 4 * i), ldp(rotations + 4 * i + 1), ldp(rotations + 4 * i + 2),
+                                     ldp(rotations + 4 * i + 3));
         cov3d_from_scale_rot(s, mod, q, c3);
     }
     const Ewa e = ewa_rows(p, V, fx, fy, tanx, tany);
@@ -99,7 +105,7 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
         col = make_float4(rgb[0], rgb[1], rgb[2], 0.f);
     }
     if (!kSplitColor) col.w = 1.f / pv.z;
-    const float op = opacities[i];
+    const float op = ldp(opacities + i);
     const float ca_ = cc * det_inv, cb_ = -cb * det_inv, cc_ = ca * det_inv;
     // Half-extents of the region where alpha = op * exp(power) can reach 1/255:
     // power >= -t, t = ln(255 op)  <=>  d^T Q d <= 2t  ->  |dx| <= sqrt(2t (Q^-1)_xx).  Evaluated
