@@ -110,6 +110,9 @@ __device__ __forceinline__ float lane_select(uint64_t mask, float t, float f) {
     return r;
 }
 
+#ifndef GSR_FWD_EARLY_EXIT
+#define GSR_FWD_EARLY_EXIT 1  // leave a batch once every pixel of the sub-block has saturated
+#endif
 template <int kSub>
 __device__ __forceinline__ uint32_t sub_block_mask_n(const float4 &qa, const float4 &qb, float tm, float tx0,
                                                      float ty0) {
@@ -285,8 +288,9 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kerne
         for (; j + 1 < cnt; j += 2) {
             blend(j);
             blend(j + 1);
+            if (GSR_FWD_EARLY_EXIT && !livem) break;  // every pixel of the sub-block has saturated
         }
-        if (j < cnt) blend(j);
+        if (j < cnt && (!GSR_FWD_EARLY_EXIT || livem)) blend(j);
         __builtin_amdgcn_wave_barrier();
     }
     const bool bad = sort_err && *sort_err;  // the depth sort gave up on a lookback: NaN frame
