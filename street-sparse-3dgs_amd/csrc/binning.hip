@@ -125,8 +125,8 @@ __global__ __launch_bounds__(1024) void sb_count_kernel(int P, SBGrid sg, const 
     }
     __syncthreads();
     for (int s = threadIdx.x; s < sg.nsb; s += 1024) {
-        cnt_g[(size_t)s * sg.nchunks + chunk] = cg[s];
-        cnt_i[(size_t)s * sg.nchunks + chunk] = ci[s];
+        cnt_g[(size_t)s * sg.ccols + cnt_col(sg, chunk)] = cg[s];
+        cnt_i[(size_t)s * sg.ccols + cnt_col(sg, chunk)] = ci[s];
     }
 }
 
@@ -167,16 +167,16 @@ __global__ __launch_bounds__(kColThreads) void sb_colscan_kernel(SBGrid sg, uint
     __shared__ uint32_t wsum[kColThreads / 64];
     __shared__ uint32_t s_last;
     const int s = blockIdx.x;
-    uint32_t *row = cnt_g + (size_t)s * sg.nchunks;
-    const uint32_t *rowi = cnt_i + (size_t)s * sg.nchunks;
+    uint32_t *row = cnt_g + (size_t)s * sg.ccols;
+    const uint32_t *rowi = cnt_i + (size_t)s * sg.ccols;
     uint32_t carry = 0, isum = 0;
     for (int b = 0; b < sg.nchunks; b += kColThreads) {
         const int c = b + (int)threadIdx.x;
-        const uint32_t v = c < sg.nchunks ? row[c] : 0u;
-        isum += c < sg.nchunks ? rowi[c] : 0u;
+        const uint32_t v = c < sg.nchunks ? row[cnt_col(sg, c)] : 0u;
+        isum += c < sg.nchunks ? rowi[cnt_col(sg, c)] : 0u;
         uint32_t tot;
         const uint32_t ex = block_exclusive_scan<kColThreads>(v, wsum, tot);
-        if (c < sg.nchunks) row[c] = carry + ex;
+        if (c < sg.nchunks) row[cnt_col(sg, c)] = carry + ex;
         carry += tot;
     }
     uint32_t itot;
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(64 * kScatterWaves) void sb_scatter_kernel(int P, S
 #pragma unroll
     for (int q = 0; q < kSBPerThread; q++) {
         const int sq = (int)threadIdx.x + q * 64 * kScatterWaves;
-        sbase[q] = sq < nsb ? base_g[sq] + col[(size_t)sq * sg.nchunks + chunk] : 0u;
+        sbase[q] = sq < nsb ? base_g[sq] + col[(size_t)sq * sg.ccols + cnt_col(sg, chunk)] : 0u;
     }
     // list loads one batch ahead of their use
     const auto rect_at = [&](int j) { return j < jw1 ? drect[j] : make_uint2(0u, 0u); };
@@ -529,6 +529,8 @@ SBGrid sb_grid(int gx, int gy, int P) {
     while ((P + g.chunk - 1) / g.chunk > kMaxChunks) g.chunk *= 2;
     g.nchunks = (P + g.chunk - 1) / g.chunk;
     if (g.nchunks < 1) g.nchunks = 1;
+    g.cper = (g.nchunks + 7) / 8;
+    g.ccols = GSR_CNT_XCD ? 8 * g.cper : g.nchunks;
     return g;
 }
 

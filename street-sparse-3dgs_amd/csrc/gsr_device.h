@@ -437,7 +437,17 @@ constexpr int kMaxSB = 1536;          // superblocks (3 x 8 waves x 4 B of LDS e
 constexpr int kMaxTilesPerSB = 256;   // up to 16 x 16 tiles per superblock
 struct SBGrid {
     int shift, nsbx, nsby, nsb, nchunks, chunk;  // chunk: depth-ordered Gaussians per level-1 chunk
+    int cper, ccols;                             // counter columns per XCD, row stride of the counters
 };
+#ifndef GSR_CNT_XCD
+#define GSR_CNT_XCD 1
+#endif
+// Counter column of a level-1 chunk.  Chunk c runs as workgroup c, and workgroups are dealt to
+// the 8 XCDs round-robin, so the columns of one XCD's chunks are made adjacent: its 4-B counter
+// stores then fill whole lines in its own L2 instead of sharing every line with the 7 other XCDs.
+__host__ __device__ __forceinline__ int cnt_col(const SBGrid &g, int chunk) {
+    return GSR_CNT_XCD ? (chunk & 7) * g.cper + (chunk >> 3) : chunk;
+}
 
 struct GeomState {          // per Gaussian, written by preprocess
     GRec *rec;
@@ -453,7 +463,7 @@ struct GeomState {          // per Gaussian, written by preprocess
     uint32_t ctrl_zero;     // the preprocess
     uint2 *drect;           // per depth-order slot: tile rect (x0 | y0 << 16, x1 | y1 << 16), 0/0 = none
     uint2 *rect8;           // per Gaussian (index order): the same rect, written by the preprocess
-    SBGrid sb;              // level-1 binning counters: [nsb][nchunks] Gaussians / instances,
+    SBGrid sb;              // level-1 binning counters: [nsb][ccols] Gaussians / instances (cnt_col),
     uint32_t *sb_cnt_g;     // per-SB bases (nsb + 1 each)
     uint32_t *sb_cnt_i;
     uint32_t *sb_base_g;

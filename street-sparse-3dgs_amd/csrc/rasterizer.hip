@@ -186,8 +186,8 @@ GeomState carve_geom(void *base, int P, int gx, int gy, size_t *bytes) {
     g.drect = c.take<uint2>(P);
     g.rect8 = c.take<uint2>(P);
     g.sb = sb_grid(gx, gy, P);
-    g.sb_cnt_g = c.take<uint32_t>((size_t)g.sb.nsb * g.sb.nchunks);
-    g.sb_cnt_i = c.take<uint32_t>((size_t)g.sb.nsb * g.sb.nchunks);
+    g.sb_cnt_g = c.take<uint32_t>((size_t)g.sb.nsb * g.sb.ccols);
+    g.sb_cnt_i = c.take<uint32_t>((size_t)g.sb.nsb * g.sb.ccols);
     g.sb_base_g = c.take<uint32_t>((size_t)g.sb.nsb + 1);
     g.sb_base_i = c.take<uint32_t>((size_t)g.sb.nsb + 1);
     g.acc = c.take<float4>(4 * (size_t)P);
