@@ -123,19 +123,20 @@ __device__ __forceinline__ void sh_backward(const float *__restrict__ sh, int M,
 // issued back to back; larger splats are summed by the whole wave (coalesced loads + DPP).  Kept
 // apart from the chain rule below: this half is memory-latency bound and wants occupancy
 // (few VGPRs), the other half is arithmetic with ~130 VGPRs.
-// The splat's tile rect comes from the compact per-Gaussian rect array (8 B; an empty rect marks
+// The splat's tile rect comes from the compact per-Gaussian rect array (4 or 8 B; an empty rect marks
 // a culled Gaussian) and its depth bits are recomputed from the mean exactly as the preprocess
 // forms them -- reading them from the GRec line fetched a whole 64-B line per Gaussian.
 __global__ __launch_bounds__(256) void record_sum_kernel(int P, int gx, const float *__restrict__ means3D,
                                                          const float *__restrict__ viewmatrix,
                                                          const uint2 *__restrict__ rect8,
+                                                         const uint32_t *__restrict__ rect4,
                                                          const uint32_t *__restrict__ offsets,
                                                          const uint64_t *__restrict__ boundary, BwdScratch sc,
                                                          float *__restrict__ dmeans2D, float *__restrict__ dopacity) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & (kWave - 1);
     const bool valid = i < P;
-    const uint2 rr = valid ? rect8[i] : make_uint2(0u, 0u);
+    const uint2 rr = !valid ? make_uint2(0u, 0u) : rect4 ? unpack_rect4(rect4[i]) : rect8[i];
     const bool vis = rr.y != 0u;  // x1 | y1 << 16 with x1 > x0 >= 0: zero only when culled
     float g[10];
 #pragma unroll
@@ -601,7 +602,7 @@ void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const Ge
     if (in.P == 0) return;
     if (!sc.atomic)  // atomic mode: the sums are already in GeomState.acc
         hipLaunchKernelGGL(record_sum_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, cam.gx, in.means3D,
-                       cam.view, gs.rect8, gs.offsets, is.boundary, sc, out.dmeans2D, out.dopacity);
+                       cam.view, gs.rect8, gs.rect4, gs.offsets, is.boundary, sc, out.dmeans2D, out.dopacity);
     hipLaunchKernelGGL(preprocess_bwd_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, in.D, in.M, in.means3D,
                        radii, in.shs, gs.clamped, in.scales, in.rotations, in.scale_modifier,
                        true_scale_gradient() ? in.scale_modifier : 1.0f, in.cov3D_precomp,

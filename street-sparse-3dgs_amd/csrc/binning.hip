@@ -39,6 +39,11 @@ __device__ __forceinline__ TileRect unpack_rect(uint2 d) {
     return r;
 }
 
+// A depth-ordered rect: 8-bit fields (gs.rect4 layout) when drect4 is set, else the uint2 form.
+__device__ __forceinline__ uint2 load_drect(const uint2 *__restrict__ drect, const uint32_t *__restrict__ drect4, int j) {
+    return drect4 ? unpack_rect4(drect4[j]) : drect[j];
+}
+
 // Depth-ordered rect / tile count of every Gaussian: the one random gather of the binning.
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -91,7 +96,7 @@ __device__ __forceinline__ SBFoot lane_foot(const SBFoot &f, int b) {
 }
 
 // Level 1, pass 1: per chunk and SB, the number of Gaussians and of tile instances.
-__global__ __launch_bounds__(1024) void sb_count_kernel(int P, SBGrid sg, const uint2 *__restrict__ drect,
+__global__ __launch_bounds__(1024) void sb_count_kernel(int P, SBGrid sg, const uint2 *__restrict__ drect, const uint32_t *__restrict__ drect4,
                                                        uint32_t *__restrict__ cnt_g, uint32_t *__restrict__ cnt_i) {
     extern __shared__ uint32_t lds[];
     uint32_t *cg = lds, *ci = lds + sg.nsb;
@@ -110,7 +115,7 @@ __global__ __launch_bounds__(1024) void sb_count_kernel(int P, SBGrid sg, const 
     };
     for (int jb = j0; jb < j1; jb += 1024) {
         const int j = jb + (int)threadIdx.x;
-        const TileRect r = j < j1 ? unpack_rect(drect[j]) : TileRect{0, 0, -1, -1};
+        const TileRect r = j < j1 ? unpack_rect(load_drect(drect, drect4, j)) : TileRect{0, 0, -1, -1};
         const SBFoot f = sb_foot(r, sg.shift);
         // footprints over more than kSmallSB superblocks are counted by the whole wave, one SB per
         // lane (a single lane would hold its wave for hundreds of iterations)
@@ -239,6 +244,7 @@ __device__ __forceinline__ void mask_clear(uint64_t *m) {
 __global__ __launch_bounds__(64 * kScatterWaves) void sb_scatter_kernel(int P, SBGrid sg,
                                                                          const uint32_t *__restrict__ order,
                                                                          const uint2 *__restrict__ drect,
+                                                                         const uint32_t *__restrict__ drect4,
                                                                          const uint32_t *__restrict__ col,
                                                                          const uint32_t *__restrict__ base_g,
                                                                          uint2 *__restrict__ sblist,
@@ -266,7 +272,7 @@ __global__ __launch_bounds__(64 * kScatterWaves) void sb_scatter_kernel(int P, S
         sbase[q] = sq < nsb ? base_g[sq] + col[(size_t)sq * sg.ccols + cnt_col(sg, chunk)] : 0u;
     }
     // list loads one batch ahead of their use
-    const auto rect_at = [&](int j) { return j < jw1 ? drect[j] : make_uint2(0u, 0u); };
+    const auto rect_at = [&](int j) { return j < jw1 ? load_drect(drect, drect4, j) : make_uint2(0u, 0u); };
 
     // per-wave SB counts
     uint2 rnext = rect_at(jw0 + lane);
@@ -543,11 +549,11 @@ void launch_binning_superblocks(int P, const Camera &cam, const GeomState &gs, c
     if (P == 0 || cam.gx * cam.gy == 0) return;
     const size_t l1 = sizeof(uint32_t) * 2 * (size_t)sg.nsb;
     const size_t l3 = sizeof(uint32_t) * 3 * kScatterWaves * (size_t)sg.nsb;
-    hipLaunchKernelGGL(sb_count_kernel, dim3(sg.nchunks), dim3(1024), l1, s, P, sg, gs.drect, gs.sb_cnt_g,
+    hipLaunchKernelGGL(sb_count_kernel, dim3(sg.nchunks), dim3(1024), l1, s, P, sg, gs.drect, drect4_of(gs), gs.sb_cnt_g,
                        gs.sb_cnt_i);
     hipLaunchKernelGGL(sb_colscan_kernel, dim3(sg.nsb), dim3(kColThreads), 0, s, sg, gs.sb_cnt_g, gs.sb_cnt_i,
                        gs.sb_base_g, gs.sb_base_i, dsort_aux_word(gs));
-    hipLaunchKernelGGL(sb_scatter_kernel, dim3(sg.nchunks), dim3(64 * kScatterWaves), l3, s, P, sg, gs.order, gs.drect,
+    hipLaunchKernelGGL(sb_scatter_kernel, dim3(sg.nchunks), dim3(64 * kScatterWaves), l3, s, P, sg, gs.order, gs.drect, drect4_of(gs),
                        gs.sb_cnt_g, gs.sb_base_g, bs.sblist, bs.kdev, bs.cap);
 }
 

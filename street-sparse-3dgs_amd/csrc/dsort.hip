@@ -218,6 +218,7 @@ __global__ __launch_bounds__(kDsThreads) void dsort_pass_kernel(int P, int nb, c
                                                                  uint32_t *__restrict__ offsets,
                                                                  const uint32_t *__restrict__ tiles,
                                                                  const uint2 *__restrict__ rect8,
+                                                                 const uint32_t *__restrict__ rect4,
                                                                  uint2 *__restrict__ drect,
                                                                  uint32_t *__restrict__ host_err) {
     constexpr bool kFirst = kPass == 0, kLast = kPass == kPasses - 1;
@@ -402,7 +403,11 @@ __global__ __launch_bounds__(kDsThreads) void dsort_pass_kernel(int P, int nb, c
         const uint32_t g = s_val[i];
         if (kLast) {
             vout[j] = g;
-            drect[j] = rect8[g];
+            if (rect4) {
+                reinterpret_cast<uint32_t *>(drect)[j] = rect4[g];  // drect4_of(gs)
+            } else {
+                drect[j] = rect8[g];
+            }
         } else {
             kout[j] = k;
             vout[j] = g;
@@ -427,13 +432,13 @@ void launch_depth_sort(int P, const GeomState &gs, uint32_t *host_K, uint32_t *h
     if (k_ready) (void)hipEventRecord(k_ready, s);
     // keys: dkey -> dkey_sorted -> dkey -> dkey_sorted -> (none); values: (index) -> ids -> order -> ids -> order
     hipLaunchKernelGGL(dsort_pass_kernel<0>, dim3(nb), dim3(kDsThreads), 0, s, P, nb, gs.dkey, gs.dkey_sorted,
-                       (const uint32_t *)nullptr, gs.ids, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect, host_err);
+                       (const uint32_t *)nullptr, gs.ids, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.rect4, gs.drect, host_err);
     hipLaunchKernelGGL(dsort_pass_kernel<1>, dim3(nb), dim3(kDsThreads), 0, s, P, nb, gs.dkey_sorted, gs.dkey, gs.ids,
-                       gs.order, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect, host_err);
+                       gs.order, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.rect4, gs.drect, host_err);
     hipLaunchKernelGGL(dsort_pass_kernel<2>, dim3(nb), dim3(kDsThreads), 0, s, P, nb, gs.dkey, gs.dkey_sorted, gs.order,
-                       gs.ids, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect, host_err);
+                       gs.ids, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.rect4, gs.drect, host_err);
     hipLaunchKernelGGL(dsort_pass_kernel<3>, dim3(nb), dim3(kDsThreads), 0, s, P, nb, gs.dkey_sorted,
-                       (uint32_t *)nullptr, gs.ids, gs.order, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect, host_err);
+                       (uint32_t *)nullptr, gs.ids, gs.order, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.rect4, gs.drect, host_err);
 }
 
 uint32_t *dsort_K_word(const GeomState &gs) { return gs.ctrl + kCtlK; }

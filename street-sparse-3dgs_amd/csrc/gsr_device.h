@@ -439,6 +439,9 @@ struct SBGrid {
     int shift, nsbx, nsby, nsb, nchunks, chunk;  // chunk: depth-ordered Gaussians per level-1 chunk
     int cper, ccols;                             // counter columns per XCD, row stride of the counters
 };
+#ifndef GSR_RECT4
+#define GSR_RECT4 1
+#endif
 #ifndef GSR_CNT_XCD
 #define GSR_CNT_XCD 1
 #endif
@@ -463,6 +466,10 @@ struct GeomState {          // per Gaussian, written by preprocess
     uint32_t ctrl_zero;     // the preprocess
     uint2 *drect;           // per depth-order slot: tile rect (x0 | y0 << 16, x1 | y1 << 16), 0/0 = none
     uint2 *rect8;           // per Gaussian (index order): the same rect, written by the preprocess
+                            // unless rect4 is set
+    uint32_t *rect4;        // the same rect in 8-bit fields when the tile grid is <= 255 x 255 (else
+                            // nullptr), then written instead of rect8: the depth sort's last pass
+                            // gathers these 4 B, and drect holds them in that form too (drect4_of)
     SBGrid sb;              // level-1 binning counters: [nsb][ccols] Gaussians / instances (cnt_col),
     uint32_t *sb_cnt_g;     // per-SB bases (nsb + 1 each)
     uint32_t *sb_cnt_i;
@@ -471,6 +478,14 @@ struct GeomState {          // per Gaussian, written by preprocess
     float4 *acc;            // backward accumulators, 4 float4 (64 B) per Gaussian, zeroed by render_fwd
     int nacc;               // rows of acc (P)
 };
+// a 4-B packed rect (x0 | y0 << 8 | x1 << 16 | y1 << 24) in the 8-B form (x0 | y0 << 16, x1 | y1 << 16)
+__host__ __device__ __forceinline__ uint2 unpack_rect4(uint32_t q) {
+    return make_uint2((q & 0xFFu) | ((q << 8) & 0xFF0000u), ((q >> 16) & 0xFFu) | ((q >> 8) & 0xFF0000u));
+}
+// drect as 4-B packed rects (the depth sort's last pass wrote rect4's form), or nullptr
+__host__ __device__ __forceinline__ const uint32_t *drect4_of(const GeomState &g) {
+    return g.rect4 ? reinterpret_cast<const uint32_t *>(g.drect) : nullptr;
+}
 
 struct BinningState {       // per tile instance
     uint2 *sblist;          // level 1: (Gaussian id, footprint in SB-local tiles) per superblock, depth order

@@ -35,7 +35,10 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
     radii[i] = 0;
     gs.tiles[i] = 0;
     gs.dkey[i] = 0xFFFFFFFFu;  // culled Gaussians sort behind every visible one
-    gs.rect8[i] = make_uint2(0u, 0u);
+    if (gs.rect4)
+        gs.rect4[i] = 0u;
+    else
+        gs.rect8[i] = make_uint2(0u, 0u);
     const float3 p = make_float3(ldp(means3D + 3 * i), ldp(means3D + 3 * i + 1), ldp(means3D + 3 * i + 2));
     const float3 pv = xf_point43(p, V);
     if (pv.z <= 0.2f) return;  // in_frustum (prefiltered is treated as a plain cull)
@@ -136,7 +139,10 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
                        __uint_as_float(__float_as_uint(pv.z)), tm);
     if (!kSplitColor) gs.clamped[i] = clamp_bits;
     gs.tiles[i] = (uint32_t)area;
-    gs.rect8[i] = make_uint2((uint32_t)r.x0 | ((uint32_t)r.y0 << 16), (uint32_t)r.x1 | ((uint32_t)r.y1 << 16));
+    if (gs.rect4)
+        gs.rect4[i] = (uint32_t)r.x0 | ((uint32_t)r.y0 << 8) | ((uint32_t)r.x1 << 16) | ((uint32_t)r.y1 << 24);
+    else
+        gs.rect8[i] = make_uint2((uint32_t)r.x0 | ((uint32_t)r.y0 << 16), (uint32_t)r.x1 | ((uint32_t)r.y1 << 16));
     gs.dkey[i] = __float_as_uint(pv.z);
 }
 

@@ -185,6 +185,8 @@ GeomState carve_geom(void *base, int P, int gx, int gy, size_t *bytes) {
     g.ctrl = c.take<uint32_t>(dsort_ctrl_words(P));
     g.drect = c.take<uint2>(P);
     g.rect8 = c.take<uint2>(P);
+    g.rect4 = c.take<uint32_t>(P);
+    if (!GSR_RECT4 || gx > 255 || gy > 255) g.rect4 = nullptr;
     g.sb = sb_grid(gx, gy, P);
     g.sb_cnt_g = c.take<uint32_t>((size_t)g.sb.nsb * g.sb.ccols);
     g.sb_cnt_i = c.take<uint32_t>((size_t)g.sb.nsb * g.sb.ccols);

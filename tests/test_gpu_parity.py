@@ -39,6 +39,8 @@ CASES = [
     dict(name="wide_depth_4pass", P=4000, W=96, H=64, deg=1, seed=16, log_scale=-3.0, far=0.3, behind=0.1),
     # footprints over tens of 4x4-tile superblocks next to small ones (the binning's wave-wide path)
     dict(name="huge_splats_sb", P=300, W=640, H=480, deg=1, seed=15, log_scale=-0.5),
+    # more than 255 tiles across: the 8-B tile rects (every other case packs them into 4 B)
+    dict(name="wide_frame_rect8", P=3000, W=4200, H=64, deg=1, seed=17, log_scale=-3.0),
 ]
 
 
