@@ -44,8 +44,16 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--diag", action="store_true", help="print synced per-step fwd/bwd wall times to stderr")
     ap.add_argument("--train-steps", type=int, default=20, help="timed train-step harness iterations (0 = skip)")
-    ap.add_argument("--config5", action="store_true",
-                    help="also time config 5: hierarchy cut blend + forward render of the cut at 1080p")
+    ap.add_argument("--no-config5", action="store_true",
+                    help="skip config 5 (hierarchy cut + blend + forward render of the cut at 1080p; on by default)")
+    ap.add_argument("--config5", action="store_true", help=argparse.SUPPRESS)  # round-2 spelling: now the default
+    ap.add_argument("--no-street", action="store_true",
+                    help="skip the street-frame point (1536x1536 cube face, 90 deg fov: fwd+bwd and train step)")
+    ap.add_argument("--no-config4", action="store_true",
+                    help="skip config 4 (500k-Gaussian chunk per rank, seed = chunk id: fwd+bwd and train step)")
+    ap.add_argument("--metric-only", action="store_true",
+                    help="only the metric line's own work (profiling runs): no train step, configs 4/5, street "
+                         "frame or CPU baselines")
     ap.add_argument("--c5-leaves", type=int, default=37_500_000, help="leaves of the config-5 tree (~4/3 as many nodes)")
     ap.add_argument("--c5-tau", type=float, default=15.0,
                     help="render_hierarchy.py tau in pixels (its default list: 0, 3, 6, 15)")
@@ -60,16 +68,15 @@ def parse():
 OVERLAPPED_STAGES = ("sh_color",)
 
 
-def algorithmic_bytes(P, Pv, K, T, npix, M=16):
+def algorithmic_bytes(P, Pv, K, T, npix, P1, M=16):
     """Per-launch algorithmic bytes per stage.  SURVEY.md 8(d) figures (M=16 constants; the SH
     term scales with M) for the stages it defines; the binning stages follow this build's
     algorithm: a 32-bit depth sort of P ids (4 LSD passes, 16 B/elem/pass) + the
     gathered scan; level-1 binning reads (order, tiles, rect) twice per Gaussian and writes the
-    superblock lists (P1 ~ 1.5 P entries, not measured here); level 2 re-reads them with the
-    rects twice and writes the K-entry point list + ranges.  Upstream's 64-bit 6-pass key sort
-    alone would be 24*K*6."""
+    superblock lists (P1 entries of 8 B, measured per frame: gsr_frame_stats); level 2 re-reads
+    them with the rects twice and writes the K-entry point list + ranges.  Upstream's 64-bit
+    6-pass key sort alone would be 24*K*6."""
     sh = 12 * M
-    P1 = 1.5 * P
     return {
         # geometry: 44 B of inputs, the GRec minus its colour (48 B) and 4 x 4 B of per-Gaussian
         # outputs; the SH colour pass (side stream, overlapped): SH rows + means + radii in,
@@ -77,8 +84,12 @@ def algorithmic_bytes(P, Pv, K, T, npix, M=16):
         "preprocess": 44 * P + 64 * P,
         "sh_color": (sh + 12 + 4) * P + 17 * P,
         "depth_sort_scan": 16 * P * 4 + 12 * P,
-        "bin_superblocks": 2 * 24 * Pv + 8 * Pv + 4 * P1,
-        "bin_tiles": 2 * 24 * P1 + 4 * K + 8 * T,
+        # sb_count reads each visible Gaussian's 4-B depth-ordered tile rect; sb_scatter its order
+        # entry and rect again and writes the P1 8-B list entries (id, SB-local footprint)
+        "bin_superblocks": 4 * Pv + 8 * Pv + 8 * P1,
+        # tile_bin reads the level-1 lists (once, ideally: its second pass should hit L2) and
+        # writes the K-entry point list and the ranges
+        "bin_tiles": 8 * P1 + 4 * K + 8 * T,
         "tile_order": 16 * T,
         "tile_order_bwd": 12 * T,
         "render_fwd": 44 * K + 24 * npix,
@@ -87,11 +98,11 @@ def algorithmic_bytes(P, Pv, K, T, npix, M=16):
     }
 
 
-def make_inputs(P, W, H, deg, seed, device):
+def make_inputs(P, W, H, deg, seed, device, fovx_deg=60.0):
     import numpy as np
     import torch
     from gs_train.synthetic import synthetic_scene
-    s = synthetic_scene(P, W, H, seed=seed, sh_degree=deg)
+    s = synthetic_scene(P, W, H, seed=seed, sh_degree=deg, fovx_deg=fovx_deg)
     t = lambda a: torch.tensor(np.asarray(a), dtype=torch.float32, device=device)
     inp = dict(means3D=t(s["means3D"]), means2D=torch.zeros(P, 3, device=device), opacities=t(s["opacities"]),
                shs=t(s["shs"]), scales=t(s["scales"]), rotations=t(s["rotations"]))
@@ -158,7 +169,7 @@ def psnr_vs_oracle(gpu_color, gpu_invd, st):
     return out
 
 
-def train_step_ms(P, W, H, steps, warmup, dev, street=True, reference=False):
+def train_step_ms(P, W, H, steps, warmup, dev, street=True, reference=False, seed=0, fovx_deg=60.0):
     """one train_single.py iteration on the bench scene (1M Gaussians at
     1080p, perturbed), wall time per step between synchronisations (the fused step never syncs).
     street=True: the Street-sparse iteration -- 4 training views cycled, the masked inverse-depth
@@ -171,8 +182,8 @@ def train_step_ms(P, W, H, steps, warmup, dev, street=True, reference=False):
     step_cls = None
     if reference:
         from train_torch_ref import ReferenceTrainStep as step_cls
-    ts = make_problem(P, W, H, n_views=4 if street else 1, seed=0, step_cls=step_cls, depth=street,
-                      skybox_points=10_000 if street else 0)
+    ts = make_problem(P, W, H, n_views=4 if street else 1, seed=seed, step_cls=step_cls, depth=street,
+                      skybox_points=10_000 if street else 0, fovx_deg=fovx_deg)
     for _ in range(warmup):
         ts.step()
     torch.cuda.synchronize()
@@ -269,25 +280,62 @@ def config5(a, dev):
     return out
 
 
+def kernel_source_sha():
+    """Content hash of the kernel sources (csrc/, include/, the build flags): profiles/*_pmc.json
+    record it (tools/pmc_summary.py), so a profile taken before the kernels changed is flagged
+    stale instead of being reported as if it described the code that ran."""
+    import hashlib
+    h = hashlib.sha256()
+    pkg = os.path.join(REPO, "street-sparse-3dgs_amd")
+    files = sorted(glob.glob(os.path.join(pkg, "csrc", "*.hip")) + glob.glob(os.path.join(pkg, "csrc", "*.h")) +
+                   glob.glob(os.path.join(REPO, "include", "*.h"))) + [os.path.join(pkg, "build_hip.py")]
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
+_PROFILES = None
+
+
+def _profiles():
+    """Committed PMC summaries, newest first (profiles/r<round><letter>_pmc.json), each with
+    whether it was taken from the kernel sources in this tree."""
+    global _PROFILES
+    if _PROFILES is None:
+        sha = kernel_source_sha()
+        _PROFILES = []
+        for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")), reverse=True):
+            try:
+                d = json.load(open(f))
+            except Exception:
+                continue
+            _PROFILES.append((os.path.basename(f), d, d.get("source_sha") == sha))
+    return _PROFILES
+
+
 def latest_profile_entry(kernel, field):
     """`field` of `kernel` (a stage name: render_bwd is the depth-gradient variant the bench runs)
-    from the newest committed PMC summary (profiles/r<round><letter>_pmc.json) that has it."""
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")))  # named r<round><letter>_...
-    for f in reversed(files):
-        try:
-            d = json.load(open(f))
-            e = d.get("kernels", {}).get(kernel, {})
-            v = e.get(field) if "." not in field else e.get(field.split(".")[0], {}).get(field.split(".")[1])
-            if v is not None:
-                return v, os.path.basename(f)
-        except Exception:
+    from the newest committed PMC summary that has it -- one taken from the current kernel
+    sources if any -- as (value, file, current)."""
+    found = None
+    for name, d, cur in _profiles():
+        e = d.get("kernels", {}).get(kernel, {})
+        v = e.get(field) if "." not in field else e.get(field.split(".")[0], {}).get(field.split(".")[1])
+        if v is None:
             continue
-    return None, None
+        if cur:
+            return v, name, True
+        if found is None:
+            found = (v, name, False)
+    return found if found else (None, None, False)
 
 
 def latest_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary."""
-    return latest_profile_entry(kernel, "hbm_bytes_per_launch")
+    """HBM bytes per launch of `kernel` from the committed PMC summary of the current sources
+    (None when only a profile of older kernels exists)."""
+    v, src, cur = latest_profile_entry(kernel, "hbm_bytes_per_launch")
+    return (v if cur else None), src, cur
 
 
 # VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD every 2 cycles at the
@@ -305,8 +353,8 @@ def valu_roofline(kernel, ms):
     """Second roofline for the blend kernels, which are VALU-issue bound: wave-level VALU
     instructions per launch (SQ_INSTS_VALU from the committed rocprofv3 summary of the same
     kernel variant) over the live-measured launch time, against the issue peak."""
-    instr, src = latest_profile_entry(kernel, "sq.SQ_INSTS_VALU")
-    if not instr or not ms:
+    instr, src, cur = latest_profile_entry(kernel, "sq.SQ_INSTS_VALU")
+    if not instr or not ms or not cur:  # an instruction count of other kernel code says nothing
         return None
     ach = instr / (ms * 1e-3)
     return {"kernel": kernel, "bound": "valu-issue", "achieved": round(ach / 1e9, 2), "peak": VALU_PEAK_INSTR_S / 1e9,
@@ -321,12 +369,178 @@ def rocprof_ms(kernel):
     --profile-steps).  The VALU-bound blend kernels run ~8% longer under the profiler than the
     same launches timed with HIP events here; the memory-bound kernels agree within ~2%
     (DESIGN.md section 4)."""
-    us, _ = latest_profile_entry(kernel, "avg_us")
-    return round(us / 1e3, 5) if us else None
+    us, _, cur = latest_profile_entry(kernel, "avg_us")
+    return round(us / 1e3, 5) if us and cur else None
+
+
+def spawn_ranks(a):
+    """bench.py --gpus N run directly (no WORLD_SIZE): start N fresh rank processes through
+    torch.distributed.run -- one process per GPU, as the driver launches it -- before this process
+    touches the GPU, and exit with their status.  Mirrors the reference's one-process-per-chunk
+    fan-out (scripts/full_train.py:171-232, scripts/train_chunk.slurm:5-7)."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+class Ranks:
+    """Process-group helpers: barrier, MAX / gather of host floats (gloo on CPU tensors when the
+    ranks share one GPU, RCCL otherwise)."""
+
+    def __init__(self, world, rank, share, dev):
+        self.world, self.rank, self.share, self.dev = world, rank, share, dev
+
+    def barrier(self):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    def gather(self, x):
+        if self.world == 1:
+            return [float(x)]
+        import torch
+        import torch.distributed as dist
+        d = "cpu" if self.share else self.dev
+        t = torch.zeros(self.world, dtype=torch.float64, device=d)
+        t[self.rank] = float(x)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return [float(v) for v in t.cpu()]
+
+    def max(self, x):
+        return max(self.gather(x))
+
+
+def rasterizer_for(s, W, H, deg, dev):
+    import torch
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    t = lambda x: torch.tensor(x, dtype=torch.float32, device=dev)
+    rs = GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=float(s["tanfovx"]), tanfovy=float(s["tanfovy"]), bg=t(s["bg"]),
+        scale_modifier=1.0, viewmatrix=t(s["view"]).reshape(4, 4), projmatrix=t(s["proj"]).reshape(4, 4),
+        sh_degree=deg, campos=t(s["campos"]), prefiltered=False, debug=False, do_depth=True,
+        render_indices=torch.empty(0, dtype=torch.int32), parent_indices=torch.empty(0, dtype=torch.int32),
+        interpolation_weights=torch.empty(0, device=dev), num_node_kids=torch.empty(0, dtype=torch.int32, device=dev))
+    return rs, GaussianRasterizer(rs)
+
+
+def fwd_bwd_step(raster, inp, gcol, ginv):
+    import torch
+    leaves = list(inp.values())
+
+    def step():
+        for v in leaves:
+            v.grad = None
+        color, radii, invd = raster(**inp)
+        torch.autograd.backward([color, invd], [gcol, ginv])
+        return radii
+    return step
+
+
+def timed(step, steps, warmup, ranks):
+    """W untimed steps, then exactly `steps` steps bracketed by barrier + synchronize on both sides;
+    the MAX over ranks of the elapsed seconds."""
+    import torch
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    ranks.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    ranks.barrier()
+    torch.cuda.synchronize()
+    return ranks.max(time.perf_counter() - t0)
+
+
+def stage_profile(step, n):
+    """Per-stage device time (HIP events on the rasterizer's stream) averaged over n extra steps."""
+    from diff_gaussian_rasterization import _C
+    _C.set_profiling(True)
+    acc = {}
+    for _ in range(max(1, n)):
+        step()
+        for k, v in _C.stage_times_ms().items():
+            acc[k] = acc.get(k, 0.0) + v
+    _C.set_profiling(False)
+    return {k: v / max(1, n) for k, v in acc.items()}
+
+
+def frame_workload(rs, inp, W, H, deg, dev):
+    """Pv, K and the level-1 entry count P1 of the frame (one raw forward, no_grad)."""
+    import torch
+    from diff_gaussian_rasterization import _C
+    with torch.no_grad():
+        raw = _C.rasterize_gaussians(rs.bg, inp["means3D"], torch.empty(0, device=dev), inp["opacities"],
+                                     inp["scales"], inp["rotations"], 1.0, torch.empty(0, device=dev), rs.viewmatrix,
+                                     rs.projmatrix, rs.tanfovx, rs.tanfovy, H, W, inp["shs"], deg, rs.campos, False,
+                                     False, rs.render_indices, rs.parent_indices, rs.interpolation_weights,
+                                     rs.num_node_kids, True)
+        fs = _C.frame_stats(raw[4], inp["means3D"].shape[0], H, W)
+    return dict(K=int(raw[0]), Pv=int((raw[3] > 0).sum().item()), P1=fs["level1_entries"])
+
+
+def config4(a, ranks, dev):
+    """one synthetic 500k-Gaussian chunk per rank (seed = chunk id =
+    rank), rasterized at 1080p -- the product's one-chunk-per-GPU sharding, no data-path
+    collective -- and the Street-sparse train step on that chunk.  Aggregate Mpix/s over all ranks
+    and every rank's train-step ms (at N = 1 this is config 2's train step)."""
+    import torch
+    P4, W, H, deg = 500_000, a.width, a.height, a.sh_degree
+    s, inp, gcol, ginv = make_inputs(P4, W, H, deg, seed=ranks.rank, device=dev)
+    rs, raster = rasterizer_for(s, W, H, deg, dev)
+    el = timed(fwd_bwd_step(raster, inp, gcol, ginv), a.steps, a.warmup, ranks)
+    wl = frame_workload(rs, inp, W, H, deg, dev)
+    del inp, raster
+    torch.cuda.empty_cache()
+    tr = train_step_ms(P4, W, H, a.train_steps, 5, dev, seed=ranks.rank) if a.train_steps > 0 else None
+    per_rank = ranks.gather(tr) if tr is not None else None
+    return {"workload": f"{ranks.world} chunk(s) of {P4} Gaussians (seed = chunk id), one per rank, fwd+bwd at "
+                        f"{W}x{H} SH degree {deg} do_depth; train step = the Street-sparse iteration on the chunk",
+            "value": round(ranks.world * W * H * a.steps / el / 1e6, 3), "unit": "Mpix/s", "n_gpus": ranks.world,
+            "ms_per_step": round(el / a.steps * 1e3, 4), "visible_rank0": wl["Pv"], "tile_instances_rank0": wl["K"],
+            "train_step_ms_per_rank": [round(v, 4) for v in per_rank] if per_rank else None,
+            "train_step_ms_max": round(max(per_rank), 4) if per_rank else None,
+            "scaling": "weak", "collectives": "none on the data path (barrier + MAX of the elapsed time only)"}
+
+
+def street_frame(a, dev):
+    """The Street-sparse training frame: a 1536x1536 cube face with a 90 deg field of view
+    (ss_utils/generate_colmap_calibration.py:306-308,476-479,572: SIMPLE_PINHOLE, f = size / 2;
+    below the 1600-px rescale of utils/camera_utils.py:64-81), 1M synthetic Gaussians: fwd+bwd
+    Mpix/s with its stage split, and the train step with 4 cycled views of that size."""
+    import torch
+    W = H = 1536
+    P, deg = a.gaussians, a.sh_degree
+    s, inp, gcol, ginv = make_inputs(P, W, H, deg, seed=0, device=dev, fovx_deg=90.0)
+    rs, raster = rasterizer_for(s, W, H, deg, dev)
+    step = fwd_bwd_step(raster, inp, gcol, ginv)
+    el = timed(step, a.steps, a.warmup, Ranks(1, 0, False, dev))
+    stages = stage_profile(step, 3)
+    wl = frame_workload(rs, inp, W, H, deg, dev)
+    del inp, raster
+    torch.cuda.empty_cache()
+    out = {"workload": f"rasterizer fwd+bwd, {P} Gaussians, SH degree {deg}, {W}x{H} (90 deg fov), do_depth",
+           "value": round(W * H * a.steps / el / 1e6, 3), "unit": "Mpix/s", "ms_per_step": round(el / a.steps * 1e3, 4),
+           "visible": wl["Pv"], "tile_instances": wl["K"], "level1_entries": wl["P1"],
+           "tiles": ((W + 15) // 16) * ((H + 15) // 16), "stages_ms": {k: round(v, 5) for k, v in stages.items()}}
+    if a.train_steps > 0:
+        out["train_step_ms"] = round(train_step_ms(P, W, H, a.train_steps, 5, dev, fovx_deg=90.0), 4)
+    return out
 
 
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(a))
+    if a.metric_only:
+        a.train_steps, a.no_config5, a.no_street, a.no_config4, a.no_cpu_baseline = 0, True, True, True, True
     import torch
     import torch.distributed as dist
 
@@ -344,32 +558,17 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", 0 if share or world == 1 else local)
-
-    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer, _C
+    ranks = Ranks(world, rank, share, dev)
 
     P, W, H, deg = a.gaussians, a.width, a.height, a.sh_degree
     s, inp, gcol, ginv = make_inputs(P, W, H, deg, seed=rank, device=dev)
-    t = lambda x: torch.tensor(x, dtype=torch.float32, device=dev)
-    rs = GaussianRasterizationSettings(
-        image_height=H, image_width=W, tanfovx=float(s["tanfovx"]), tanfovy=float(s["tanfovy"]), bg=t(s["bg"]),
-        scale_modifier=1.0, viewmatrix=t(s["view"]).reshape(4, 4), projmatrix=t(s["proj"]).reshape(4, 4),
-        sh_degree=deg, campos=t(s["campos"]), prefiltered=False, debug=False, do_depth=True,
-        render_indices=torch.empty(0, dtype=torch.int32), parent_indices=torch.empty(0, dtype=torch.int32),
-        interpolation_weights=torch.empty(0, device=dev), num_node_kids=torch.empty(0, dtype=torch.int32, device=dev))
-    raster = GaussianRasterizer(rs)
+    rs, raster = rasterizer_for(s, W, H, deg, dev)
+    step = fwd_bwd_step(raster, inp, gcol, ginv)
     leaves = list(inp.values())
 
-    def step():
-        for v in leaves:
-            v.grad = None
-        color, radii, invd = raster(**inp)
-        torch.autograd.backward([color, invd], [gcol, ginv])
-        return radii
-
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
     if a.diag:
+        for _ in range(a.warmup):
+            step()
         for it in range(5):
             for v in leaves:
                 v.grad = None
@@ -395,49 +594,23 @@ def main():
         torch.cuda.synchronize()
         pr.disable()
         pstats.Stats(pr, stream=sys.stderr).sort_stats("cumulative").print_stats(18)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        radii = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        e = torch.tensor([elapsed], device="cpu" if share else dev, dtype=torch.float64)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
+    elapsed = timed(step, a.steps, a.warmup, ranks)
 
     # per-stage device time with HIP events on the rasterizer's stream (separate, untimed steps)
-    _C.set_profiling(True)
-    acc = {}
-    for _ in range(max(1, a.profile_steps)):
-        radii = step()
-        for k, v in _C.stage_times_ms().items():
-            acc[k] = acc.get(k, 0.0) + v
-    _C.set_profiling(False)
-    stages = {k: v / max(1, a.profile_steps) for k, v in acc.items()}
+    stages = stage_profile(step, a.profile_steps)
 
-    # workload statistics for the algorithmic-bytes model
-    with torch.no_grad():
-        raw = _C.rasterize_gaussians(rs.bg, inp["means3D"], torch.empty(0, device=dev), inp["opacities"],
-                                     inp["scales"], inp["rotations"], 1.0, torch.empty(0, device=dev), rs.viewmatrix,
-                                     rs.projmatrix, rs.tanfovx, rs.tanfovy, H, W, inp["shs"], deg, rs.campos, False,
-                                     False, rs.render_indices, rs.parent_indices, rs.interpolation_weights,
-                                     rs.num_node_kids, True)
-    K = int(raw[0])
-    Pv = int((raw[3] > 0).sum().item())
+    # workload statistics for the algorithmic-bytes model (P1 measured: gsr_frame_stats)
+    wl = frame_workload(rs, inp, W, H, deg, dev)
+    K, Pv, P1 = wl["K"], wl["Pv"], wl["P1"]
     T = ((W + 15) // 16) * ((H + 15) // 16)
     npix = W * H
-    abytes = algorithmic_bytes(P, Pv, K, T, npix, M=inp["shs"].shape[1])
+    abytes = algorithmic_bytes(P, Pv, K, T, npix, P1, M=inp["shs"].shape[1])
     serial_ms = sum(v for k, v in stages.items() if k not in OVERLAPPED_STAGES)
     dom = max(stages, key=lambda k: stages[k]) if stages else "render_bwd"
     dom_ms = stages.get(dom, 0.0)
     achieved = abytes[dom] / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
-    traffic, traffic_src = latest_traffic(dom)
+    traffic, traffic_src, traffic_cur = latest_traffic(dom)
+    rp_ms = rocprof_ms(dom)
 
     ms_per_step = elapsed / a.steps * 1e3
     value = world * npix * a.steps / elapsed / 1e6
@@ -456,22 +629,29 @@ def main():
         "data": "synthetic (seeded Gaussians in the frustum, SURVEY.md 8(d); one chunk per rank, seed = rank)",
         "config": {"workload": f"rasterizer fwd+bwd, {P} Gaussians, SH degree {deg}, {W}x{H}, do_depth",
                    "gaussians": P, "width": W, "height": H, "sh_degree": deg, "visible": Pv, "tile_instances": K,
-                   "tiles": T, "parallelism": f"chunk-per-gpu x{world}"},
+                   "level1_entries": P1, "tiles": T, "parallelism": f"chunk-per-gpu x{world}"},
+        # frac: algorithmic bytes / the kernel's HIP-event time measured here; frac_rocprof: the same
+        # bytes / the average duration in the committed rocprofv3 summary of these kernel sources
+        # (profiles/, null when no summary of the current sources is committed)
         "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "algorithmic_bytes": abytes[dom], "avg_ms": round(dom_ms, 5),
-                     "traffic_source": traffic_src, "rocprof_avg_ms": rocprof_ms(dom)},
+                     "traffic_source": traffic_src, "profile_is_current": traffic_cur, "rocprof_avg_ms": rp_ms,
+                     "frac_rocprof": round(abytes[dom] / (rp_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if rp_ms else None,
+                     "kernel_source_sha": kernel_source_sha()},
         "valu_roofline": [r for r in (valu_roofline(k, stages.get(k)) for k in ("render_bwd", "render_fwd")) if r],
         "stages_ms": {k: round(v, 5) for k, v in stages.items()},
+        "stage_bytes": {k: int(v) for k, v in abytes.items()},
         # stages on the main stream (sh_color overlaps the sort / binning on a side stream)
         "pipeline_roofline": {"algorithmic_bytes": sum(abytes.values()),
                               "frac": round(sum(abytes.values()) / (serial_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
                               if serial_ms > 0 else None},
     }
+    del step, raster
     if a.train_steps > 0:
         from diff_gaussian_rasterization import _C as _Cstats
         r0 = _Cstats.forward_stats()
-        tr = {"ms": round(train_step_ms(P, W, H, a.train_steps, 5, dev), 4),
+        tr = {"ms": round(train_step_ms(P, W, H, a.train_steps, 5, dev, seed=rank), 4),
               "workload": f"Street-sparse train_single.py iteration on the bench scene ({P} Gaussians, {W}x{H}, 4 views "
                           f"cycled): render, exposure, 0.8 L1 + 0.2 (1 - SSIM) + masked inverse-depth L1, backward "
                           f"(depth gradient on), densify stats, exposure Adam, skybox lock (10k rows), sparse Adam, "
@@ -483,19 +663,30 @@ def main():
         if a.train_baseline:
             tr["reference_structured_ms"] = round(train_step_ms(P, W, H, a.train_steps, 5, dev, reference=True), 4)
         out["train_step"] = tr
-    if a.config5:
+    if not a.no_config4:
+        out["config4"] = config4(a, ranks, dev)
+        if world == 1 and out["config4"]["train_step_ms_max"] is not None and "train_step" in out:
+            out["train_step"]["config2_500k_ms"] = out["config4"]["train_step_ms_max"]
+    if world == 1 and not a.no_street:
+        out["street_frame"] = street_frame(a, dev)
+    if world == 1 and not a.no_config5:
         out["config5"] = config5(a, dev)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"], st = cpu_baseline(s, P, W, H, deg)
         out["cpu_baseline_torch"] = cpu_baseline_torch()
         with torch.no_grad():
-            color, _, invd = raster(**inp)
+            color, _, invd = raster_again(s, inp, W, H, deg, dev)
         out["psnr_vs_oracle"] = psnr_vs_oracle(color, invd, st)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def raster_again(s, inp, W, H, deg, dev):
+    _, raster = rasterizer_for(s, W, H, deg, dev)
+    return raster(**inp)
 
 
 if __name__ == "__main__":

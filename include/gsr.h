@@ -82,12 +82,31 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
                           const float *interpolation_weights, const int *num_node_kids, int num_render,
                           int debug, void *stream, int64_t *num_rendered);
 
+/* gsr_rasterize_forward with flags (same arguments, then `flags`; gsr_rasterize_forward passes 0).
+ *   GSR_FWD_NO_BACKWARD: no backward will follow (the Python host sets it when autograd records
+ *   no graph: torch.no_grad() frames such as render_hierarchy.py's evaluation loop, SURVEY.md
+ *   3.3).  The frame skips clearing the backward's per-Gaussian accumulator rows (64 B per
+ *   Gaussian) and building the backward's tile order; gsr_rasterize_backward on its buffers fails
+ *   with GSR_ERR_INVALID_ARGUMENT. */
+#define GSR_FWD_NO_BACKWARD 1u
+int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffer, gsr_resize_fn image_buffer,
+                             void *resize_ctx, int P, int D, int M, const float *background, int width, int height,
+                             const float *means3D, const float *shs, const float *colors_precomp,
+                             const float *opacities, const float *scales, float scale_modifier,
+                             const float *rotations, const float *cov3D_precomp, const float *viewmatrix,
+                             const float *projmatrix, const float *cam_pos, float tan_fovx, float tan_fovy,
+                             int prefiltered, float *out_color, float *out_invdepth, int *radii,
+                             const int *render_indices, const int *parent_indices,
+                             const float *interpolation_weights, const int *num_node_kids, int num_render,
+                             int debug, void *stream, int64_t *num_rendered, unsigned flags);
+
 /* Backward.  geom/binning/image are the pointers the forward's callbacks returned; R = K.
  * The hierarchy-cut fields must be the forward's; with num_render > 0 the gradients of the P
  * input rows are those of render_post's blend (shared parents summed) and dL_dmeans2D holds the
  * rendered rows' screen-space gradient in rows [0, num_render), zero below.
  * dL_dpix (3,H,W); dL_dinvdepth (1,H,W) or NULL (no depth gradient).  `scratch` provides
- * the per-tile-instance gradient workspace.  Every output row is written (zeros where
+ * the per-tile-instance gradient workspace.  The call is repeatable: a second backward through
+ * the same buffers (retain_graph) returns the same gradients.  Every output row is written (zeros where
  * radii == 0 and beyond the active SH degree), so outputs need no pre-zeroing:
  *   dL_dmeans2D (P,3)  dL_dcolors (P,3) [may be NULL when shs != NULL]  dL_dopacity (P,1)
  *   dL_dmeans3D (P,3)  dL_dcov3D (P,6) [may be NULL when cov3D_precomp == NULL]
@@ -136,6 +155,12 @@ int gsr_set_deterministic(int enable);
  * binning ran twice because the capacity hint from the previous frame was short of K.
  * Returns the number of values written (<= n). */
 int gsr_forward_stats(int64_t *out, int n);
+
+/* Statistics of one forward frame, read from its geometry buffer (synchronises the device):
+ * out[0] = level-1 binning entries (Gaussian x superblock pairs, "P1" of DESIGN.md), out[1] = tile
+ * instances (K).  P = the frame's rendered rows (num_render when non-zero).  Returns the number of
+ * values written (<= n).  For bench.py's algorithmic-bytes model. */
+int gsr_frame_stats(const void *geom_buffer, int P, int width, int height, int64_t *out, int n);
 
 /* Version / diagnostics. */
 int gsr_abi_version(void);

@@ -53,13 +53,14 @@ int gsr_interpolate_cut_backward(int64_t N, int M, int64_t R, int64_t S, const i
  * node's first Gaussian, -1 for roots) and nodes_for_render_indices (node ids), in node order --
  * and returns its length in *to_render (the value the Python function returns; one host read, as
  * upstream).  viewpoint is a DEVICE float[3] (the caller's camera_center on the GPU).
- * Output arrays need room for the cut (N entries always suffice when every node holds at most one
- * Gaussian; in general sum of count_leafs + count_merged).  scratch: a device buffer of
- * gsr_expand_to_size_scratch_bytes(N) bytes. */
+ * `capacity` = the entries each output array holds: the write pass never stores past it, and a
+ * cut longer than it (possible when nodes hold several Gaussians: the cut can reach the sum of
+ * count_leafs + count_merged, more than N) fails with GSR_ERR_INVALID_ARGUMENT, *to_render set to
+ * the length it needs.  scratch: a device buffer of gsr_expand_to_size_scratch_bytes(N) bytes. */
 size_t gsr_expand_to_size_scratch_bytes(int64_t N);
 int gsr_expand_to_size(int64_t N, const int *nodes, const float *boxes, float target_size, const float *viewpoint,
-                       int *render_indices, int *parent_indices, int *nodes_for_render_indices, void *scratch,
-                       size_t scratch_bytes, int64_t *to_render, void *stream);
+                       int *render_indices, int *parent_indices, int *nodes_for_render_indices, int64_t capacity,
+                       void *scratch, size_t scratch_bytes, int64_t *to_render, void *stream);
 
 /* get_interpolation_weights: for the n rendered nodes node_indices[i], weights[i] = the blend
  * weight t of the node with its parent and num_kids[i] = the parent's child count (1 for roots).

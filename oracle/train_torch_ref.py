@@ -255,6 +255,7 @@ def _reference_step_cls():
             g = self.g
             sc = g.get_scaling
             bad = sc.max(dim=1).values > self.extent * 0.02
+            bad[:self.scaffold] = False  # train_single.py:239-240
             g._scaling[bad] = torch.log(sc[bad] * 0.8)
 
     return ReferenceTrainStep

@@ -336,12 +336,24 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
     // parameter rows are not read (88% of the bench scene's Gaussians; only its zero rows are
     // written)
     bool live = vis;
-    if (GSR_BWD_SKIP_DEAD) {
+    {
         bool nz = false;
 #pragma unroll
         for (int t = 0; t < 10; t++) nz = nz || g[t] != 0.f;
-        if (!sc.atomic && vis) nz = nz || out.dopacity[i] != 0.f;  // record mode: summed by record_sum
-        live = vis && nz;
+        if (sc.atomic && vis && nz) {
+            // the row is consumed: clear it, so a second backward through the same saved buffers
+            // (retain_graph, torch.autograd.grad twice, gradcheck) sums from zero again, as
+            // upstream's stateless backward does.  Only the ~12% of rows render_bwd added into
+            // are written (48 B each).
+            float4 *a = sc.acc + 4 * (size_t)i;
+            a[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+            a[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+            a[2] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        if (GSR_BWD_SKIP_DEAD) {
+            if (!sc.atomic && vis) nz = nz || out.dopacity[i] != 0.f;  // record mode: summed by record_sum
+            live = vis && nz;
+        }
     }
 
     float dm[3] = {0.f, 0.f, 0.f};

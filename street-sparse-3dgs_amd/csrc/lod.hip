@@ -91,9 +91,11 @@ __global__ __launch_bounds__(256) void lod_count_kernel(int64_t N, const int *__
 __global__ __launch_bounds__(256) void lod_put_kernel(int64_t N, const int *__restrict__ nodes,
                                                       const int *__restrict__ counts, const int *__restrict__ incl,
                                                       int *__restrict__ render_indices, int *__restrict__ parent_indices,
-                                                      int *__restrict__ nodes_for_render) {
+                                                      int *__restrict__ nodes_for_render, int64_t capacity) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N) return;
+    // a cut longer than the output arrays writes nothing (the host reports the length it needs)
+    if ((int64_t)incl[N - 1] > capacity) return;
     const int c = counts[i];
     if (c == 0) return;
     const int off = incl[i] - c;
@@ -154,8 +156,8 @@ size_t gsr_expand_to_size_scratch_bytes(int64_t N) {
 }
 
 int gsr_expand_to_size(int64_t N, const int *nodes, const float *boxes, float target_size, const float *viewpoint,
-                       int *render_indices, int *parent_indices, int *nodes_for_render_indices, void *scratch,
-                       size_t scratch_bytes, int64_t *to_render, void *stream) {
+                       int *render_indices, int *parent_indices, int *nodes_for_render_indices, int64_t capacity,
+                       void *scratch, size_t scratch_bytes, int64_t *to_render, void *stream) {
     if (to_render) *to_render = 0;
     if (N < 0 || N > INT32_MAX) return fail_lod(GSR_ERR_INVALID_ARGUMENT, "gsr_expand_to_size: N out of range");
     if (N == 0) return GSR_OK;
@@ -176,13 +178,16 @@ int gsr_expand_to_size(int64_t N, const int *nodes, const float *boxes, float ta
     if (rocprim::inclusive_scan(tmp, tmp_bytes, counts, incl, (size_t)N, rocprim::plus<int>(), s) != hipSuccess)
         return fail_lod(GSR_ERR_DEVICE, "gsr_expand_to_size: scan failed");
     hipLaunchKernelGGL(lod_put_kernel, dim3(blocks), dim3(256), 0, s, N, nodes, counts, incl, render_indices,
-                       parent_indices, nodes_for_render_indices);
+                       parent_indices, nodes_for_render_indices, capacity < 0 ? (int64_t)0 : capacity);
     int total = 0;
     hipError_t e = hipMemcpyAsync(&total, incl + (N - 1), sizeof(int), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e == hipSuccess) e = hipGetLastError();
     if (e != hipSuccess) return fail_lod(GSR_ERR_DEVICE, std::string("gsr_expand_to_size: ") + hipGetErrorString(e));
     *to_render = total;
+    if ((int64_t)total > capacity)
+        return fail_lod(GSR_ERR_INVALID_ARGUMENT, "gsr_expand_to_size: the cut needs " + std::to_string(total) +
+                                                      " entries, the output arrays hold " + std::to_string(capacity));
     return GSR_OK;
 }
 

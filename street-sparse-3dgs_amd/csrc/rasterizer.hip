@@ -12,6 +12,7 @@
 #include <string>
 #include <algorithm>
 #include <thread>
+#include <unordered_map>
 
 #include "../../include/gsr.h"
 #include "../../include/gsr_hier.h"
@@ -341,6 +342,34 @@ std::atomic<int> g_deterministic{GSR_DETERMINISTIC_DEFAULT};
 }
 bool gsr::true_scale_gradient() { return g_true_scale_grad.load(std::memory_order_relaxed) != 0; }
 
+namespace {
+// Geometry buffers whose accumulator rows the forward did not clear: forwards made with
+// GSR_FWD_NO_BACKWARD (a backward handed one fails loudly) and forwards made in deterministic
+// mode (their backward uses the record path even if the mode was switched in between).  Every
+// forward first removes its own buffer, so an address the caching allocator hands out again is
+// judged by the forward that carved it last.  Bounded: past kUnclearedMax entries the map is
+// cleared (those forwards lose the check; their buffers are normally long released by then).
+enum Uncleared : uint8_t { kNoBackward = 1, kDeterministicFwd = 2 };
+std::mutex g_unclr_mu;
+std::unordered_map<const void *, uint8_t> g_unclr;
+constexpr size_t kUnclearedMax = 4096;
+void note_forward_geom(const void *geom, bool need_bwd, bool cleared) {
+    std::lock_guard<std::mutex> lk(g_unclr_mu);
+    if (cleared) {
+        if (!g_unclr.empty()) g_unclr.erase(geom);
+        return;
+    }
+    if (g_unclr.size() >= kUnclearedMax) g_unclr.clear();
+    g_unclr[geom] = need_bwd ? kDeterministicFwd : kNoBackward;
+}
+uint8_t forward_uncleared(const void *geom) {
+    std::lock_guard<std::mutex> lk(g_unclr_mu);
+    if (g_unclr.empty()) return 0;
+    const auto it = g_unclr.find(geom);
+    return it == g_unclr.end() ? 0 : it->second;
+}
+}  // namespace
+
 extern "C" {
 
 int gsr_abi_version(void) { return GSR_ABI_VERSION; }
@@ -386,9 +415,31 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
                           const int *render_indices, const int *parent_indices,
                           const float *interpolation_weights, const int *num_node_kids, int num_render,
                           int debug, void *stream, int64_t *num_rendered) {
+    return gsr_rasterize_forward_ex(geom_buffer, binning_buffer, image_buffer, resize_ctx, P, D, M, background, width,
+                                    height, means3D, shs, colors_precomp, opacities, scales, scale_modifier, rotations,
+                                    cov3D_precomp, viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered,
+                                    out_color, out_invdepth, radii, render_indices, parent_indices,
+                                    interpolation_weights, num_node_kids, num_render, debug, stream, num_rendered, 0u);
+}
+
+int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffer, gsr_resize_fn image_buffer,
+                             void *resize_ctx, int P, int D, int M, const float *background, int width, int height,
+                             const float *means3D, const float *shs, const float *colors_precomp,
+                             const float *opacities, const float *scales, float scale_modifier,
+                             const float *rotations, const float *cov3D_precomp, const float *viewmatrix,
+                             const float *projmatrix, const float *cam_pos, float tan_fovx, float tan_fovy,
+                             int prefiltered, float *out_color, float *out_invdepth, int *radii,
+                             const int *render_indices, const int *parent_indices,
+                             const float *interpolation_weights, const int *num_node_kids, int num_render,
+                             int debug, void *stream, int64_t *num_rendered, unsigned flags) {
     (void)prefiltered;
     (void)num_node_kids;  // accepted; render_post's blend (which this reproduces) does not read it
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (flags & ~(unsigned)GSR_FWD_NO_BACKWARD) return fail(GSR_ERR_INVALID_ARGUMENT, "unknown forward flags");
+    // the backward's accumulator rows are cleared (and its launch order built) only for a frame a
+    // backward may follow: atomic mode, GSR_FWD_NO_BACKWARD not set
+    const bool need_bwd = !(flags & GSR_FWD_NO_BACKWARD);
+    const bool clear_acc = need_bwd && g_deterministic.load(std::memory_order_relaxed) == 0;
     if (num_rendered) *num_rendered = 0;
     int rc = validate_common(P, D, M, shs, colors_precomp, scales, rotations, cov3D_precomp, width, height);
     if (rc) return rc;
@@ -421,7 +472,9 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
     void *gbase = geom_buffer(resize_ctx, gbytes);
     void *ibase = image_buffer(resize_ctx, ibytes);
     if (!gbase || !ibase) return fail(GSR_ERR_ALLOCATION, "geometry/image buffer allocation failed");
-    const GeomState gs = carve_geom(gbase, P, cam.gx, cam.gy, nullptr);
+    GeomState gs = carve_geom(gbase, P, cam.gx, cam.gy, nullptr);
+    if (!clear_acc) gs.nacc = 0;
+    note_forward_geom(gbase, need_bwd, clear_acc);
     const ImageState is = carve_image(ibase, T, npix, nullptr);
     if (R > 0) {
         const CutRows cr = cut_rows_of(gbase, P, cam.gx, cam.gy, M);
@@ -595,7 +648,7 @@ int gsr_rasterize_forward(gsr_resize_fn geom_buffer, gsr_resize_fn binning_buffe
             StageTimer st(5, s);
             launch_render_fwd(cam, gs, bs, is, background, out_color, out_invdepth, s);
         }
-        {
+        if (need_bwd) {
             StageTimer st(9, s);  // backward launch order, from the forward's per-tile work
             launch_tile_order(is.tile_work, is.ranges, T, 2, is.tile_order, s, bs.kdev, bs.cap);
         }
@@ -663,6 +716,10 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
     if (P > 0 && !cov3D_precomp && (!dL_dscales || !dL_drotations))
         return fail(GSR_ERR_INVALID_ARGUMENT, "NULL dL_dscales / dL_drotations");
     if ((rc = sticky_sort_error())) return rc;
+    const uint8_t uncleared = forward_uncleared(geom_buffer);
+    if (uncleared == kNoBackward)
+        return fail(GSR_ERR_INVALID_ARGUMENT, "backward of a forward made with GSR_FWD_NO_BACKWARD (its accumulator "
+                                              "rows were not cleared); run the forward without the flag");
 
     const int64_t Nin = P;
     const int R = num_render;
@@ -673,7 +730,9 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
     const GeomState gs = carve_geom(geom_buffer, P, cam.gx, cam.gy, nullptr);
     const BinningState bs = carve_binning(binning_buffer, R_inst, nullptr);
     const ImageState is = carve_image(image_buffer, T, width * height, nullptr);
-    const bool atomic = g_deterministic.load(std::memory_order_relaxed) == 0;
+    // a frame forwarded in deterministic mode has no cleared accumulators: its backward takes
+    // the record path whatever the mode is now
+    const bool atomic = g_deterministic.load(std::memory_order_relaxed) == 0 && uncleared != kDeterministicFwd;
     size_t sbytes = 0;
     carve_bwd(nullptr, R_inst, P, atomic, &sbytes);
     // hierarchy cut: gradients of the R blended rows first, then scattered to the input rows
@@ -754,6 +813,25 @@ int gsr_forward_stats(int64_t *out, int n) {
     const int64_t v[2] = {g_frames.load(), g_reruns.load()};
     int k = 0;
     for (; k < n && k < 2; k++) out[k] = v[k];
+    return k;
+}
+
+int gsr_frame_stats(const void *geom_buffer, int P, int width, int height, int64_t *out, int n) {
+    if (!out || n < 0 || P < 0 || width <= 0 || height <= 0)
+        return fail(GSR_ERR_INVALID_ARGUMENT, "gsr_frame_stats: bad arguments");
+    if (P == 0 || n == 0) {
+        for (int k = 0; k < n && k < 2; k++) out[k] = 0;
+        return n < 2 ? n : 2;
+    }
+    if (!geom_buffer) return fail(GSR_ERR_INVALID_ARGUMENT, "gsr_frame_stats: NULL geometry buffer");
+    const int gx = (width + kTile - 1) / kTile, gy = (height + kTile - 1) / kTile;
+    const GeomState gs = carve_geom(const_cast<void *>(geom_buffer), P, gx, gy, nullptr);
+    uint32_t v[2] = {0u, 0u};
+    if (hipMemcpy(&v[0], gs.sb_base_g + gs.sb.nsb, sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(&v[1], gs.sb_base_i + gs.sb.nsb, sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(GSR_ERR_DEVICE, "gsr_frame_stats: copy failed");
+    int k = 0;
+    for (; k < n && k < 2; k++) out[k] = (int64_t)v[k];
     return k;
 }
 

@@ -33,6 +33,7 @@ import torch
 from . import _lib
 
 _L = _lib.load()
+_FWD_NO_BACKWARD = 1  # GSR_FWD_NO_BACKWARD (include/gsr.h)
 
 
 def _ptr(t):
@@ -108,7 +109,11 @@ def _require_gpu(t):
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
                         viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
                         prefiltered, debug, render_indices=None, parent_indices=None, interpolation_weights=None,
-                        num_node_kids=None, do_depth=True):
+                        num_node_kids=None, do_depth=True, need_backward=True):
+    """need_backward=False (an extension; upstream has no such argument): no backward will use
+    this frame's buffers -- the autograd Function passes it for frames autograd does not record
+    (torch.no_grad evaluation), which then skip the backward's accumulator clear
+    (GSR_FWD_NO_BACKWARD, include/gsr.h)."""
     if means3D.ndimension() != 2 or means3D.size(1) != 3:
         raise RuntimeError("means3D must have dimensions (num_points, 3)")
     _require_gpu(means3D)
@@ -139,13 +144,13 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     res = _Resizer(dev)
     K = ctypes.c_int64(0)
     with torch.cuda.device(dev):
-        rc = _L.gsr_rasterize_forward(
+        rc = _L.gsr_rasterize_forward_ex(
             res.fn("geom"), res.fn("binning"), res.fn("image"), None, P, int(degree), M, _ptr(bg_c), W, H,
             _ptr(means3D_c), _ptr(sh_c), _ptr(colors_c), _ptr(opac_c), _ptr(scales_c), float(scale_modifier),
             _ptr(rots_c), _ptr(cov_c), _ptr(view_c), _ptr(proj_c), _ptr(campos_c), float(tan_fovx),
             float(tan_fovy), int(bool(prefiltered)), _ptr(out_color), _ptr(out_invdepth) if do_depth else None,
             _ptr(radii), _ptr(ri_c), _ptr(pi_c), _ptr(w_c), _ptr(kids_c), n_render, int(bool(debug)), _stream(dev),
-            ctypes.byref(K))
+            ctypes.byref(K), 0 if need_backward else _FWD_NO_BACKWARD)
     res.release()
     _check(rc, "rasterize_gaussians")
     return int(K.value), out_color, out_invdepth, radii, res.get("geom"), res.get("binning"), res.get("image")
@@ -270,6 +275,17 @@ def forward_stats() -> dict:
     buf = (ctypes.c_int64 * 2)()
     n = _L.gsr_forward_stats(buf, 2)
     return {"frames": int(buf[0]) if n > 0 else 0, "reruns": int(buf[1]) if n > 1 else 0}
+
+
+def frame_stats(geomBuffer, P, image_height, image_width) -> dict:
+    """Level-1 binning entries and tile instances of the frame whose geometry buffer this is
+    (gsr_frame_stats; one device sync)."""
+    buf = (ctypes.c_int64 * 2)()
+    with torch.cuda.device(geomBuffer.device):
+        n = _L.gsr_frame_stats(_ptr(geomBuffer), int(P), int(image_width), int(image_height), buf, 2)
+    if n < 0:
+        _check(n, "frame_stats")
+    return {"level1_entries": int(buf[0]), "tile_instances": int(buf[1])}
 
 
 def set_profiling(enable: bool) -> None:

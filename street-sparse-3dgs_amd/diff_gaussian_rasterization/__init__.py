@@ -30,8 +30,13 @@ def _host_copy(args):
 
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
                         raster_settings):
+    # a frame autograd will not record (torch.no_grad evaluation, or no input that requires grad)
+    # can never reach the backward: it skips the backward's accumulator clear
+    need_backward = torch.is_grad_enabled() and any(
+        t is not None and t.requires_grad
+        for t in (means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp))
     return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
-                                     cov3Ds_precomp, raster_settings)
+                                     cov3Ds_precomp, raster_settings, need_backward)
 
 
 def _hier(rs, name):
@@ -42,7 +47,7 @@ def _hier(rs, name):
 class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
-                raster_settings):
+                raster_settings, need_backward=True):
         rs = raster_settings
         do_depth = bool(getattr(rs, "do_depth", True))
         args = (rs.bg, means3D, colors_precomp, opacities, scales, rotations, rs.scale_modifier, cov3Ds_precomp,
@@ -54,14 +59,15 @@ class _RasterizeGaussians(torch.autograd.Function):
             saved = _host_copy(args)
             try:
                 num_rendered, color, invdepth, radii, geomBuffer, binningBuffer, imgBuffer = \
-                    _C.rasterize_gaussians(*args)
+                    _C.rasterize_gaussians(*args, need_backward=need_backward)
             except Exception:
                 torch.save(saved, "snapshot_fw.dump")
                 print("\n[diff_gaussian_rasterization] forward failed in debug mode; its inputs are in "
                       "snapshot_fw.dump (torch.load it and call _C.rasterize_gaussians(*args) to replay)")
                 raise
         else:
-            num_rendered, color, invdepth, radii, geomBuffer, binningBuffer, imgBuffer = _C.rasterize_gaussians(*args)
+            num_rendered, color, invdepth, radii, geomBuffer, binningBuffer, imgBuffer = \
+                _C.rasterize_gaussians(*args, need_backward=need_backward)
 
         ctx.raster_settings = rs
         # an output no loss uses (the inverse depth, in most training steps) arrives as None, not
@@ -106,7 +112,7 @@ class _RasterizeGaussians(torch.autograd.Function):
 
         return (grad_means3D, grad_means2D, keep(grad_sh, sh), keep(grad_colors_precomp, colors_precomp),
                 grad_opacities, keep(grad_scales, scales), keep(grad_rotations, rotations),
-                keep(grad_cov3Ds_precomp, cov3Ds_precomp), None)
+                keep(grad_cov3Ds_precomp, cov3Ds_precomp), None, None)
 
 
 class GaussianRasterizationSettings(NamedTuple):

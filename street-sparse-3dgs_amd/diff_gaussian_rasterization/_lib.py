@@ -36,6 +36,10 @@ SIGNATURES = {
                                    _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _f, _f,
                                    _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp,
                                    ctypes.POINTER(_i64)]),
+    "gsr_rasterize_forward_ex": (_i, [RESIZE_FN, RESIZE_FN, RESIZE_FN, _vp, _i, _i, _i, _vp, _i, _i,
+                                      _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _f, _f,
+                                      _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp,
+                                      ctypes.POINTER(_i64), ctypes.c_uint]),
     "gsr_rasterize_backward": (_i, [RESIZE_FN, _vp, _i, _i, _i, _i64, _vp, _i, _i, _vp, _vp, _vp, _vp, _f,
                                     _vp, _vp, _vp, _vp, _vp, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp,
                                     _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp]),
@@ -43,6 +47,7 @@ SIGNATURES = {
     "gsr_set_profiling": (_i, [_i]),
     "gsr_stage_times_ms": (_i, [ctypes.POINTER(_f), _i]),
     "gsr_forward_stats": (_i, [ctypes.POINTER(_i64), _i]),
+    "gsr_frame_stats": (_i, [_vp, _i, _i, _i, ctypes.POINTER(_i64), _i]),
     "gsr_set_true_scale_gradient": (_i, [_i]),
     "gsr_set_deterministic": (_i, [_i]),
     "gsr_abi_version": (_i, []),
@@ -72,8 +77,8 @@ SIGNATURES = {
     "gsr_interpolate_cut_forward": (_i, [_i64, _i, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                          _vp, _vp, _vp]),
     "gsr_expand_to_size_scratch_bytes": (ctypes.c_size_t, [_i64]),
-    "gsr_expand_to_size": (_i, [_i64, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t, ctypes.POINTER(_i64),
-                                _vp]),
+    "gsr_expand_to_size": (_i, [_i64, _vp, _vp, _f, _vp, _vp, _vp, _vp, _i64, _vp, ctypes.c_size_t,
+                                ctypes.POINTER(_i64), _vp]),
     "gsr_interpolation_weights": (_i, [_i64, _vp, _f, _vp, _vp, _f, _f, _f, _vp, _vp, _vp]),
     "gsr_densify_scratch_bytes": (ctypes.c_size_t, [_i64]),
     "gsr_densify_plan": (_i, [_i64, _i64, _vp, _vp, _vp, _vp, _f, _f, _f, _vp, _vp, _vp]),

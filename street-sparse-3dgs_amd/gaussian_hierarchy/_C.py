@@ -62,16 +62,15 @@ def expand_to_size(nodes, boxes, size, viewpoint, viewdir, render_indices, paren
     for t, n in ((render_indices, "render_indices"), (parent_indices, "parent_indices"),
                  (nodes_for_render_indices, "nodes_for_render_indices")):
         _need(t, n, torch.int32, dev)
+    # the device writes at most `cap` entries and the call fails when the cut is longer (a node can
+    # hold several Gaussians, so the cut can exceed N)
     cap = min(render_indices.numel(), parent_indices.numel(), nodes_for_render_indices.numel())
-    need = int(nodes_c[:, 3].sum().item() + nodes_c[:, 4].sum().item()) if cap < N else N
-    if cap < need:
-        raise RuntimeError(f"expand_to_size: output arrays hold {cap} entries, the cut may need {need}")
     vp = viewpoint.to(device=dev, dtype=torch.float32).contiguous().reshape(3)
     scratch = torch.empty(int(_L.gsr_expand_to_size_scratch_bytes(N)), dtype=torch.uint8, device=dev)
     out = ctypes.c_int64(0)
     with torch.cuda.device(dev):
         rc = _L.gsr_expand_to_size(N, _p(nodes_c), _p(boxes_c), float(size), _p(vp), _p(render_indices),
-                                   _p(parent_indices), _p(nodes_for_render_indices), _p(scratch),
+                                   _p(parent_indices), _p(nodes_for_render_indices), cap, _p(scratch),
                                    scratch.numel(), ctypes.byref(out), _stream(dev))
     _check(rc, "expand_to_size")
     return int(out.value)

@@ -33,10 +33,13 @@ def add_densification_stats(radii: torch.Tensor, means2D_grad: torch.Tensor, max
 
 
 def densify_and_prune(g, optimizer, max_grad: float, min_opacity: float, extent: float, percent_dense: float,
-                      first_row: int = 0) -> dict:
+                      first_row: int = 0, normals: torch.Tensor = None) -> dict:
     """g: a joined-layout gs_train.harness.GaussianSet; optimizer: its gs_train.optim.Adam.  Replaces
     the parameters (and their optimizer state) with the densified / pruned rows and resets the
-    densification statistics, as the reference does.  Returns the plan's counts."""
+    densification statistics, as the reference does.  first_row: scaffold_points (rows never
+    densified or pruned).  normals: the (2 n_split, 3) standard-normal draws behind the split
+    samples, if given (parity tests inject the reference's own); drawn here otherwise.  Returns the
+    plan's counts."""
     from diff_gaussian_rasterization._lib import RowGroup
     if not getattr(g, "joined", False):
         raise ValueError("densify_and_prune works on the joined (P,16,3) SH layout")
@@ -56,7 +59,12 @@ def densify_and_prune(g, optimizer, max_grad: float, min_opacity: float, extent:
     n_old, n_clone, n_split, total = (int(v) for v in counts.cpu())
     # the reference's torch.normal(mean=zeros, std=stds) draws normal_(0, 1) on a (2 n_split, 3)
     # tensor and scales it: the same generator stream
-    normals = torch.empty((2 * n_split, 3), device=dev).normal_() if n_split else None
+    if normals is None:
+        normals = torch.empty((2 * n_split, 3), device=dev).normal_() if n_split else None
+    else:
+        if tuple(normals.shape) != (2 * n_split, 3):
+            raise ValueError(f"normals: expected shape {(2 * n_split, 3)}, got {tuple(normals.shape)}")
+        normals = normals.to(device=dev, dtype=torch.float32).contiguous() if n_split else None
     src = (RowGroup * len(names))()
     dst = (RowGroup * len(names))()
     new = []

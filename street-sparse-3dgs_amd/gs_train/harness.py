@@ -147,10 +147,13 @@ class TrainStep:
     gts: list of (3, H, W) device tensors.  Optional per view: mono_invdepths (1, H, W),
     depth_masks (1, H, W) float 0/1 (None entries = no depth supervision for that view) and
     alpha_masks (1, H, W).  skybox_points: the first rows are the locked skybox
-    (scene/gaussian_model.py:73-74,182-187)."""
+    (scene/gaussian_model.py:73-74,182-187).  scaffold_points: the first rows are the coarse
+    scaffold (scene/gaussian_model.py:224-262, loaded with a scaffold_file), which the scale shrink
+    leaves alone (train_single.py:239-240: violators[:scaffold_points] = False)."""
 
     def __init__(self, gaussians: GaussianSet, cameras, gts, W, H, cameras_extent=10.0, mono_invdepths=None,
-                 depth_masks=None, alpha_masks=None, skybox_points=0, iterations=LR["iterations"]):
+                 depth_masks=None, alpha_masks=None, skybox_points=0, scaffold_points=0,
+                 iterations=LR["iterations"]):
         self.g = gaussians
         self.W, self.H = W, H
         self.extent = cameras_extent
@@ -160,6 +163,7 @@ class TrainStep:
         self.dmask = depth_masks if depth_masks is not None else [None] * n
         self.amask = alpha_masks if alpha_masks is not None else [None] * n
         self.skybox = int(skybox_points)
+        self.scaffold = int(scaffold_points)
         dev = gaussians._xyz.device
         f = lambda a: torch.as_tensor(np.asarray(a), dtype=torch.float32, device=dev)
         self.cams = [dict(view=f(v).reshape(4, 4), proj=f(p).reshape(4, 4), campos=f(c), tx=float(tx), ty=float(ty))
@@ -232,7 +236,7 @@ class TrainStep:
         self.optimizer.step(relevance=self.g._opacity.grad)
 
     def _shrink(self):
-        shrink_scales(self.g._scaling, self.extent * 0.02)
+        shrink_scales(self.g._scaling, self.extent * 0.02, first_row=self.scaffold)
 
     def render(self, cam_idx, bg):
         c = self.cams[cam_idx]
@@ -282,16 +286,17 @@ class TrainStep:
 
 
 def make_problem(P, W, H, n_views=4, seed=0, sh_degree=3, device="cuda", step_cls=None, perturb=0.02,
-                 depth=True, depth_mask_frac=0.85, alpha=False, skybox_points=0):
+                 depth=True, depth_mask_frac=0.85, alpha=False, skybox_points=0, scaffold_points=0, fovx_deg=60.0):
     """A synthetic Street-sparse training problem: ground-truth views and inverse-depth maps
     rendered from a seeded scene over `n_views` orbit cameras, depth masks (a random ~85% of each
     map valid, as the reference's depth_mask), optional alpha masks, and a step (TrainStep, or
     `step_cls`, e.g. oracle/train_torch_ref.ReferenceTrainStep) that starts from a perturbed copy.
-    The mono depth maps are the true inverse depth with 5% multiplicative noise."""
+    The mono depth maps are the true inverse depth with 5% multiplicative noise.  fovx_deg: 90 for
+    Street-sparse's cube faces (ss_utils/generate_colmap_calibration.py:476-479: f = size / 2)."""
     from .synthetic import orbit_cameras, synthetic_scene
     step_cls = step_cls or TrainStep
-    s = synthetic_scene(P, W, H, seed=seed, sh_degree=sh_degree)
-    cams = orbit_cameras(n_views, W, H)
+    s = synthetic_scene(P, W, H, seed=seed, sh_degree=sh_degree, fovx_deg=fovx_deg)
+    cams = orbit_cameras(n_views, W, H, fovx_deg=fovx_deg)
     truth = GaussianSet(s["means3D"], s["shs"], s["opacities"], s["scales"], s["rotations"], n_images=n_views,
                         sh_degree=sh_degree, device=device, joined_features=True)
     tmp = TrainStep(truth, cams, [None] * n_views, W, H)
@@ -315,4 +320,4 @@ def make_problem(P, W, H, n_views=4, seed=0, sh_degree=3, device="cuda", step_cl
                         joined_features=getattr(step_cls, "JOINED_FEATURES", True))
     return step_cls(model, cams, gts, W, H, mono_invdepths=monos if depth else None,
                     depth_masks=dmasks if depth else None, alpha_masks=amasks if alpha else None,
-                    skybox_points=skybox_points)
+                    skybox_points=skybox_points, scaffold_points=scaffold_points)

@@ -12,6 +12,14 @@
                  schedules of scene/gaussian_model.py:301-305 (arguments/__init__.py:89-100)
   densify.npz    scene/gaussian_model.py:780-793 add_densification_stats + the max_radii2D update
                  of train_single.py:193
+  densify_prune_<case>.npz
+                 the reference's own GaussianModel.densify_and_prune (scene/gaussian_model.py:
+                 672-778: clone, split, opacity prune; gt_point_cloud_constraints off), imported with
+                 its native dependencies stubbed and a CPU device shim, run on a seeded model with
+                 OurAdam moments: inputs, the standard-normal draws behind its torch.normal split
+                 samples (checked bit for bit against the samples it drew), and every parameter,
+                 moment and statistic it leaves (case "plain": no scaffold; "scaffold": the first
+                 rows a scaffold, scaffold_points set)
 
 Nothing from the reference is copied; only numbers are kept.
 Usage:  python tests/golden/make_train_golden.py [--ref /root/reference]
@@ -116,6 +124,95 @@ def make_densify():
     np.savez_compressed(os.path.join(OUT, "densify.npz"), **out)
 
 
+def _import_gaussian_model(ref):
+    """scene.gaussian_model with its native / optional imports stubbed (plyfile, simple_knn._C,
+    gaussian_hierarchy._C, faiss): the module's Python runs as written."""
+    import importlib
+    import types
+    stubs = {"plyfile": dict(PlyData=object, PlyElement=object), "simple_knn": {}, "simple_knn._C": dict(distCUDA2=None),
+             "gaussian_hierarchy": {}, "gaussian_hierarchy._C": dict(load_hierarchy=None, write_hierarchy=None),
+             "faiss": {}}
+    for name, attrs in stubs.items():
+        m = types.ModuleType(name)
+        m.__dict__.update(attrs)
+        sys.modules[name] = m
+    pkg = types.ModuleType("scene")  # the package __init__ pulls in dataset readers (PIL, plyfile)
+    pkg.__path__ = [os.path.join(ref, "scene")]
+    sys.modules["scene"] = pkg
+    return importlib.import_module("scene.gaussian_model")
+
+
+def make_densify_prune(ref):
+    from make_golden import _NoCuda
+    gm = _import_gaussian_model(ref)
+    our_adam = sys.modules["scene.OurAdam"]
+    for case, scaffold in (("plain", None), ("scaffold", 150)):
+        g = torch.Generator().manual_seed(21 if scaffold is None else 22)
+        P = 1200
+        m = gm.GaussianModel.__new__(gm.GaussianModel)
+        m.setup_functions()
+        q = torch.randn((P, 4), generator=g)
+        init = {"xyz": torch.randn((P, 3), generator=g) * 5, "f_dc": torch.randn((P, 1, 3), generator=g),
+                "f_rest": torch.randn((P, 15, 3), generator=g), "opacity": torch.randn((P, 1), generator=g) * 2,
+                "scaling": torch.randn((P, 3), generator=g) * 0.7 - 4.0, "rotation": q}
+        for k, v in init.items():
+            setattr(m, "_" + ("features_dc" if k == "f_dc" else "features_rest" if k == "f_rest" else k),
+                    torch.nn.Parameter(v.clone()))
+        acc = torch.rand((P, 1), generator=g) * 0.001
+        acc[::97] = float("nan")  # NaN accumulators are zeroed first (gaussian_model.py:735)
+        maxr = torch.rand(P, generator=g) * 20
+        m.xyz_gradient_accum = acc.clone()
+        m.xyz_gradient_accum_depth = torch.zeros((P, 1))
+        m.denom = torch.randint(0, 5, (P, 1), generator=g).float()
+        m.max_radii2D = maxr.clone()
+        m.percent_dense = 0.0001
+        m.scaffold_points = scaffold
+        attr = {"xyz": m._xyz, "f_dc": m._features_dc, "f_rest": m._features_rest, "opacity": m._opacity,
+                "scaling": m._scaling, "rotation": m._rotation}
+        m.optimizer = our_adam.Adam([{"params": [attr[n]], "lr": 0.0, "name": n} for n in attr], lr=0.0, eps=1e-15)
+        out = {"in_" + n: v.numpy() for n, v in init.items()}
+        for n, p_ in attr.items():
+            mom, var = torch.randn(p_.shape, generator=g), torch.rand(p_.shape, generator=g)
+            m.optimizer.state[p_] = {"step": torch.tensor(7.0), "exp_avg": mom.clone(), "exp_avg_sq": var.clone()}
+            out["in_m_" + n], out["in_v_" + n] = mom.numpy(), var.numpy()
+        out.update(in_accum=acc.numpy(), in_max_radii2D=maxr.numpy(), in_denom=m.denom.numpy())
+        args = dict(max_grad=0.0002, min_opacity=0.05, extent=200.0)
+        # record the split samples torch.normal draws, and the standard normals behind them
+        real_normal, rec = torch.normal, {}
+
+        def normal(*a, **k):
+            r = real_normal(*a, **k)
+            rec["samples"], rec["std"] = r.clone(), k["std"].clone()
+            return r
+        torch.manual_seed(1234)
+        state = torch.get_rng_state()
+        torch.normal = normal
+        try:
+            with _NoCuda():
+                m.densify_and_prune(args["max_grad"], args["min_opacity"], args["extent"], False)
+        finally:
+            torch.normal = real_normal
+        torch.set_rng_state(state)
+        z = torch.empty(rec["samples"].shape).normal_()
+        assert torch.equal(z * rec["std"], rec["samples"]), "torch.normal is not normal_() * std here"
+        out["normals"] = z.numpy()
+        out.update(max_grad=np.float32(args["max_grad"]), min_opacity=np.float32(args["min_opacity"]),
+                   extent=np.float32(args["extent"]), percent_dense=np.float32(m.percent_dense),
+                   scaffold=np.int32(scaffold or 0))
+        final = {"xyz": m._xyz, "f_dc": m._features_dc, "f_rest": m._features_rest, "opacity": m._opacity,
+                 "scaling": m._scaling, "rotation": m._rotation}
+        grp = {pg["name"]: pg["params"][0] for pg in m.optimizer.param_groups}
+        for n, p_ in final.items():
+            assert grp[n] is p_
+            st = m.optimizer.state[p_]
+            out["out_" + n] = p_.detach().numpy()
+            out["out_m_" + n], out["out_v_" + n] = st["exp_avg"].numpy(), st["exp_avg_sq"].numpy()
+        out.update(out_accum=m.xyz_gradient_accum.numpy(), out_denom=m.denom.numpy(),
+                   out_max_radii2D=m.max_radii2D.numpy())
+        np.savez_compressed(os.path.join(OUT, f"densify_prune_{case}.npz"), **out)
+        print(case, "P", P, "->", m._xyz.shape[0], "split samples", tuple(rec["samples"].shape))
+
+
 def make_lr(ref):
     gu = load_by_path("ref_general_utils", os.path.join(ref, "utils", "general_utils.py"))
     steps = np.array([0, 1, 2, 10, 100, 999, 1000, 5000, 12345, 29999, 30000, 40000], np.int64)
@@ -134,4 +231,6 @@ if __name__ == "__main__":
     make_adam(ARGS.ref)
     make_densify()
     make_lr(ARGS.ref)
-    print("wrote loss.npz adam.npz densify.npz lr.npz")
+    sys.path.insert(0, OUT)
+    make_densify_prune(ARGS.ref)
+    print("wrote loss.npz adam.npz densify.npz lr.npz densify_prune_*.npz")

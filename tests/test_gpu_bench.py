@@ -1,0 +1,35 @@
+"""bench.py's multi-rank path as the driver uses it: `bench.py --gpus N`
+run directly spawns N rank processes itself (torch.distributed.run, one process per GPU, before
+the parent touches the GPU) and rank 0 prints ONE JSON line with n_gpus == N and config 4's
+per-chunk workload.  On the one-GPU box the ranks share device 0 (GSR_BENCH_SHARE_GPU=1: gloo for
+the barriers and the MAX of the elapsed time; the driver's 8-GPU runs use RCCL)."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_bench_gpus2_spawns_two_ranks():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+    env["GSR_BENCH_SHARE_GPU"] = "1"
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--gaussians", "200000", "--profile-steps", "1", "--train-steps", "2", "--no-config5", "--no-street",
+           "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=380, env=env, cwd=REPO)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert len(lines) == 1, r.stdout[-3000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["steps"] == 3 and d["warmup"] == 1
+    c4 = d["config4"]
+    assert c4["n_gpus"] == 2 and c4["value"] > 0 and len(c4["train_step_ms_per_rank"]) == 2
+    assert all(v > 0 for v in c4["train_step_ms_per_rank"])

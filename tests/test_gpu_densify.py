@@ -1,9 +1,16 @@
-"""GPU parity of the fused densify-and-prune (csrc/densify.hip, include/gsr_densify.h) with the
-reference's own formulation (oracle/train_torch_ref.densify_and_prune, a transcription of
-scene/gaussian_model.py:560-778) on the same state and the same generator stream: row order,
-counts, every parameter and both Adam moments bit-exact, except the split children's xyz, which
-the reference forms with torch.bmm (library summation order; 1e-6 relative)."""
+"""GPU parity of the fused densify-and-prune (csrc/densify.hip, include/gsr_densify.h):
+
+* against the reference itself: tests/golden/densify_prune_*.npz hold the inputs and outputs of
+  the reference's own GaussianModel.densify_and_prune (scene/gaussian_model.py:672-778, run by
+  tests/golden/make_train_golden.py in the build container) and the standard-normal draws behind
+  its split samples, which are injected here -- row order, counts, every parameter, both Adam
+  moments and the statistics bit-exact, except the split children's xyz, which the reference
+  forms with torch.bmm (library summation order; 1e-6);
+* at larger sizes against the torch restatement (oracle/train_torch_ref.densify_and_prune) on the
+  same generator stream."""
 from __future__ import annotations
+
+import os
 
 import numpy as np
 import pytest
@@ -53,6 +60,58 @@ def _optimizers(a, b, rng):
     ob.state[b._features_rest] = {"step": torch.tensor(7.0), "exp_avg": m[:, 1:].clone(),
                                   "exp_avg_sq": v[:, 1:].clone()}
     return oa, ob
+
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.mark.parametrize("case", ["plain", "scaffold"])
+def test_densify_and_prune_matches_reference_run(case):
+    from gs_train import Adam
+    from gs_train.densify import densify_and_prune
+    from gs_train.harness import GaussianSet
+    d = np.load(os.path.join(GOLD, f"densify_prune_{case}.npz"))
+    t = lambda k: torch.tensor(d[k], device=DEV).contiguous()
+    P = d["in_xyz"].shape[0]
+    g = GaussianSet(means3D=np.zeros((P, 3), np.float32), shs=np.zeros((P, 16, 3), np.float32),
+                    opacities=np.full((P, 1), 0.5, np.float32), scales=np.ones((P, 3), np.float32),
+                    rotations=np.zeros((P, 4), np.float32), device=DEV, joined_features=True)
+    with torch.no_grad():  # the raw parameters exactly as the reference held them
+        g._xyz.copy_(t("in_xyz"))
+        g._features.copy_(torch.cat((t("in_f_dc"), t("in_f_rest")), 1))
+        g._opacity.copy_(t("in_opacity"))
+        g._scaling.copy_(t("in_scaling"))
+        g._rotation.copy_(t("in_rotation"))
+    g.xyz_gradient_accum, g.max_radii2D, g.denom = t("in_accum"), t("in_max_radii2D"), t("in_denom")
+    opt = Adam(g.param_groups(), lr=0.0, eps=1e-15)
+    mom = {"_xyz": ("xyz",), "_features": ("f_dc", "f_rest"), "_opacity": ("opacity",), "_scaling": ("scaling",),
+           "_rotation": ("rotation",)}
+    for name, keys in mom.items():
+        opt.state[getattr(g, name)] = {"step": torch.tensor(7.0),
+                                       "exp_avg": torch.cat([t("in_m_" + k) for k in keys], 1),
+                                       "exp_avg_sq": torch.cat([t("in_v_" + k) for k in keys], 1)}
+    c = densify_and_prune(g, opt, float(d["max_grad"]), float(d["min_opacity"]), float(d["extent"]),
+                          float(d["percent_dense"]), first_row=int(d["scaffold"]), normals=t("normals"))
+    n = d["out_xyz"].shape[0]
+    assert c["total"] == n and c["cloned"] > 0 and c["split"] > 0 and c["kept"] < P
+    assert 2 * c["split"] == d["normals"].shape[0]
+    got = {"f_dc": g._features[:, :1], "f_rest": g._features[:, 1:], "opacity": g._opacity, "scaling": g._scaling,
+           "rotation": g._rotation}
+    for k, v in got.items():
+        np.testing.assert_array_equal(v.detach().cpu().numpy(), d["out_" + k], err_msg=k)
+    old = c["kept"] + c["cloned"]  # rows before the split children: copied xyz
+    xyz = g._xyz.detach().cpu().numpy()
+    np.testing.assert_array_equal(xyz[:old], d["out_xyz"][:old])
+    np.testing.assert_allclose(xyz, d["out_xyz"], rtol=1e-6, atol=1e-6)
+    for name, keys in mom.items():
+        st = opt.state[getattr(g, name)]
+        for sk, pre in (("exp_avg", "out_m_"), ("exp_avg_sq", "out_v_")):
+            want = np.concatenate([d[pre + k] for k in keys], 1)
+            np.testing.assert_array_equal(st[sk].cpu().numpy(), want, err_msg=f"{name} {sk}")
+        assert float(st["step"]) == 7.0
+    np.testing.assert_array_equal(g.xyz_gradient_accum.cpu().numpy(), d["out_accum"])
+    np.testing.assert_array_equal(g.denom.cpu().numpy(), d["out_denom"])
+    np.testing.assert_array_equal(g.max_radii2D.cpu().numpy(), d["out_max_radii2D"])
 
 
 @pytest.mark.parametrize("P,first_row", [(50_000, 0), (20_011, 300)])

@@ -50,25 +50,55 @@ def test_lod_cut_matches_oracle(tau, vp):
     assert int(ri[n:].abs().sum()) == 0 and float(w[n:].abs().sum()) == 0.0
 
 
-def test_config5_end_to_end_vs_oracle():
-    """Config 5: a 10M-node hierarchy (7.5M leaves), the cut at tau = 3 px seen from the camera,
-    blended with the parents and rendered at 1920x1080 (forward, do_depth), against the oracle."""
+def _covered_once(h, ri, n):
+    """Every leaf of the tree is rendered exactly once: by itself or through exactly one ancestor
+    in the cut (each node holds one Gaussian, Gaussian i = node i).  Level by level on the device:
+    cover[i] = rendered[i] + cover[parent[i]]."""
+    nodes = h["nodes"]
+    N = nodes.shape[0]
+    rendered = torch.zeros(N, dtype=torch.int32, device=DEV)
+    rendered[ri[:n].long()] = 1
+    assert int(rendered.sum()) == n  # no node twice
+    cover = rendered.clone()
+    depth, parent = nodes[:, 0], nodes[:, 1].long()
+    for d in range(1, int(depth.max()) + 1):
+        lv = torch.nonzero(depth == d).flatten()
+        cover[lv] += cover[parent[lv]]
+    leaf = nodes[:, 3] > 0
+    assert bool(torch.all(cover[leaf] == 1)), int((cover[leaf] != 1).sum())
+
+
+@pytest.mark.parametrize("leaves,tau,log_scale,skybox", [(7_500_000, 3.0, -4.5, 20_000),
+                                                         (37_500_000, 15.0, -6.0, 100_000)],
+                         ids=["10M_tau3", "50M_tau15_bench"])
+def test_config5_end_to_end_vs_oracle(leaves, tau, log_scale, skybox):
+    """Config 5 (render_hierarchy.py:61-99): a synthetic merged hierarchy (10M nodes, tau = 3 px;
+    and bench.py's full size: ~50M nodes, tau = 15 px, a ~7.4M-row cut), the cut seen from the
+    camera -- bit-exact cut, parents, weights and child counts vs the oracle, every leaf covered
+    once -- blended with the parents and rendered at 1920x1080 (forward, do_depth, no_grad)
+    against the oracle's forward of the same rows (radii bit-exact, PSNR >= 80 dB)."""
     import gs_oracle as O
     from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
     from gs_train.hier import interpolate_cut
     from gs_train.synthetic import synthetic_lod_hierarchy, tau_threshold
     W, H = 1920, 1080
-    h = synthetic_lod_hierarchy(7_500_000, W, H, DEV, seed=5, skybox=20_000)
+    h = synthetic_lod_hierarchy(leaves, W, H, DEV, seed=5, skybox=skybox, log_scale_mean=log_scale)
     N = h["nodes"].shape[0]
-    assert N >= 10_000_000
-    thr = float(np.float32(tau_threshold(3.0, h["tanfovx"], W)))
+    assert N >= leaves * 4 // 3
+    thr = float(np.float32(tau_threshold(tau, h["tanfovx"], W)))
     n, ri, pi, ni, w, k = _cut_hip(h, thr)
     assert 1_000_000 < n < N
     # the cut against the oracle
-    ori, opi, oni = O.expand_to_size(h["nodes"].cpu().numpy(), h["boxes"].cpu().numpy(), np.float32(thr),
-                                     h["campos"])
+    nodes_np, boxes_np = h["nodes"].cpu().numpy(), h["boxes"].cpu().numpy()
+    ori, opi, oni = O.expand_to_size(nodes_np, boxes_np, np.float32(thr), h["campos"])
     np.testing.assert_array_equal(ri[:n].cpu().numpy(), ori)
     np.testing.assert_array_equal(pi[:n].cpu().numpy(), opi)
+    np.testing.assert_array_equal(ni[:n].cpu().numpy(), oni)
+    ow, ok = O.interpolation_weights(oni, np.float32(thr), nodes_np, boxes_np, np.asarray(h["campos"], np.float32))
+    np.testing.assert_array_equal(w[:n].cpu().numpy(), ow)
+    np.testing.assert_array_equal(k[:n].cpu().numpy(), ok)
+    del nodes_np, boxes_np
+    _covered_once(h, ri, n)
     S = h["skybox"]
     with torch.no_grad():
         m, sc, rot, op, sh = interpolate_cut(h["means3D"], h["scales"], h["rotations"], h["opacities"], h["shs"],
@@ -170,3 +200,28 @@ def _render_indices_equal_render_post_blend():
         err = float((x - y).norm() / y.norm().clamp_min(1e-30))
         assert err <= 1e-6, (name, err)
     assert torch.equal(m2a.grad[:n], m2b.grad) and int(m2a.grad[n:].abs().sum()) == 0
+
+
+def test_expand_to_size_capacity_with_multi_gaussian_nodes():
+    """A node can hold several Gaussians (count_leafs + count_merged > 1), so the cut can be longer
+    than the node count N: output arrays of N entries are refused (nothing written past them), and
+    arrays of the needed length get the full cut."""
+    from gaussian_hierarchy._C import expand_to_size
+    # root (1 merged Gaussian) with three leaf nodes of 3 Gaussians each; every box contains the
+    # viewpoint, so every node is "too big" and renders its leaf Gaussians: 9 entries from 4 nodes
+    nodes = torch.tensor([[0, -1, 0, 0, 1, 1, 3], [1, 0, 1, 3, 0, -1, 0], [1, 0, 4, 3, 0, -1, 0],
+                          [1, 0, 7, 3, 0, -1, 0]], dtype=torch.int32, device=DEV)
+    boxes = torch.zeros(4, 2, 4, device=DEV)
+    boxes[:, 0, :3], boxes[:, 0, 3], boxes[:, 1, :3] = -10.0, 20.0, 10.0
+    cam = torch.zeros(3, device=DEV)
+    small = [torch.full((4,), -7, dtype=torch.int32, device=DEV) for _ in range(3)]
+    with pytest.raises(RuntimeError, match="needs 9 entries"):
+        expand_to_size(nodes, boxes, 0.01, cam, torch.zeros(3), *small)
+    assert all(bool(torch.all(t == -7)) for t in small)
+    big = [torch.full((12,), -7, dtype=torch.int32, device=DEV) for _ in range(3)]
+    n = expand_to_size(nodes, boxes, 0.01, cam, torch.zeros(3), *big)
+    assert n == 9
+    assert big[0][:9].tolist() == [1, 2, 3, 4, 5, 6, 7, 8, 9]
+    assert big[1][:9].tolist() == [0] * 9  # the parent's first Gaussian
+    assert big[2][:9].tolist() == [1, 1, 1, 2, 2, 2, 3, 3, 3]
+    assert all(bool(torch.all(t[9:] == -7)) for t in big)

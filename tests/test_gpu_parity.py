@@ -47,7 +47,7 @@ CASES = [
 def make_scene(c):
     import gs_oracle as O
     s = O.synthetic_scene(c["P"], c["W"], c["H"], seed=c["seed"], sh_degree=3, log_scale_mean=c["log_scale"],
-                          primx=c.get("primx", 0.5), primy=c.get("primy", 0.5))
+                          primx=c.get("primx", 0.5), primy=c.get("primy", 0.5), fovx_deg=c.get("fovx", 60.0))
     if c.get("M", 16) != 16:
         s["shs"] = np.ascontiguousarray(s["shs"][:, :c["M"], :])
     if c.get("flat_z"):
@@ -338,6 +338,24 @@ def test_config2_full_size_vs_oracle():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("deg,seed", [(3, 3), (1, 4)])
+def test_street_frame_1536_vs_oracle(deg, seed):
+    """The Street-sparse training frame: a 1536x1536 cube face with a 90 deg field of view
+    (ss_utils/generate_colmap_calibration.py:306-308,476-479,572 -- SIMPLE_PINHOLE, f = size / 2 --
+    below the 1600-px rescale of utils/camera_utils.py:64-81): 96 x 96 tiles, 576 superblocks,
+    1M Gaussians.  Bit-exact binning (keys, point list, ranges), image PSNR and gradients vs the
+    oracle; SH degree 1 is the coarse model's (train_coarse.py:31)."""
+    c = dict(name=f"street1536_deg{deg}", P=1_000_000, W=1536, H=1536, deg=deg, seed=seed, log_scale=-4.0,
+             fovx=90.0)
+    s = make_scene(c)
+    dcol, dinv = upstream_grads(c)
+    st, g = run_oracle(s, c, dcol, dinv)
+    h = run_hip(s, c, dcol, dinv)
+    assert h["K"] > 2_000_000
+    compare(c, st, g, h)
+
+
+@pytest.mark.gpu
 def test_depth_order_large():
     """The depth sort at 3M Gaussians (367 sort tiles) with 25% culled: the order is the
     stable (depth bits, id) order of the visible Gaussians, then the culled ones; the record
@@ -401,3 +419,67 @@ def test_scratch_is_released_every_frame():
         step()
     torch.cuda.synchronize()
     assert torch.cuda.memory_allocated(dev) <= base + (1 << 20)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("deterministic", [False, True])
+def test_backward_twice_through_saved_buffers(deterministic):
+    """A second backward through the same forward (loss.backward(retain_graph=True) twice,
+    torch.autograd.grad twice, gradcheck-style reuse) returns the same gradients: upstream's
+    backward keeps no state between calls, and render_bwd's accumulator rows are cleared by the
+    pass that consumes them."""
+    import torch
+    from diff_gaussian_rasterization import GaussianRasterizer, _C
+    c = dict(name="twice", P=4000, W=128, H=96, deg=3, seed=31, log_scale=-3.2)
+    s = make_scene(c)
+    dev = torch.device("cuda:0")
+    dcol, dinv = upstream_grads(c)
+    prev = _C.set_deterministic(deterministic)
+    try:
+        inp = torch_inputs(s, dev)
+        color, radii, invd = GaussianRasterizer(settings(s, dev, 3))(**inp)
+        loss = (color * torch.tensor(dcol, device=dev)).sum() + (invd * torch.tensor(dinv, device=dev)).sum()
+        leaves = list(inp.values())
+        g1 = torch.autograd.grad(loss, leaves, retain_graph=True)
+        g2 = torch.autograd.grad(loss, leaves, retain_graph=True)
+        loss.backward(retain_graph=True)
+        g3 = [v.grad.clone() for v in leaves]
+    finally:
+        _C.set_deterministic(prev)
+    for a, b, d in zip(g1, g2, g3):
+        if deterministic:
+            assert torch.equal(a, b) and torch.equal(a, d)
+        else:
+            for x in (b, d):
+                assert float((a - x).norm() / max(float(a.norm()), 1e-30)) < 1e-5
+    assert float(g1[0].norm()) > 0
+
+
+@pytest.mark.gpu
+def test_no_grad_forward_skips_backward_state():
+    """A frame autograd does not record (torch.no_grad) renders the same image, and its buffers
+    are refused by the backward (GSR_FWD_NO_BACKWARD: accumulators not cleared)."""
+    import torch
+    from diff_gaussian_rasterization import GaussianRasterizer, _C
+    c = dict(name="nograd", P=3000, W=96, H=64, deg=3, seed=32, log_scale=-3.0)
+    s = make_scene(c)
+    dev = torch.device("cuda:0")
+    inp = torch_inputs(s, dev)
+    rs = settings(s, dev, 3)
+    color, radii, invd = GaussianRasterizer(rs)(**inp)
+    with torch.no_grad():
+        color2, radii2, invd2 = GaussianRasterizer(rs)(**inp)
+    assert torch.equal(color, color2) and torch.equal(radii, radii2) and torch.equal(invd, invd2)
+    e = torch.empty(0, device=dev)
+    d = {k: v.detach() for k, v in inp.items()}
+    raw = _C.rasterize_gaussians(rs.bg, d["means3D"], e, d["opacities"], d["scales"], d["rotations"], 1.0, e,
+                                 rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width,
+                                 d["shs"], 3, rs.campos, False, False, rs.render_indices, rs.parent_indices,
+                                 rs.interpolation_weights, rs.num_node_kids, True, need_backward=False)
+    assert torch.equal(raw[1], color2)
+    with pytest.raises(RuntimeError, match="GSR_FWD_NO_BACKWARD"):
+        _C.rasterize_gaussians_backward(rs.bg, d["means3D"], raw[3], e, d["scales"], d["rotations"], 1.0, e,
+                                        rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy,
+                                        torch.ones_like(raw[1]), None, d["shs"], 3, rs.campos, raw[4], raw[0], raw[5],
+                                        raw[6], rs.render_indices, rs.parent_indices, rs.interpolation_weights,
+                                        rs.num_node_kids, False)

@@ -190,8 +190,9 @@ def test_densify_stats_matches_reference():
     np.testing.assert_array_equal(den.cpu().numpy(), d["denom_after"])
 
 
-@pytest.mark.parametrize("depth,alpha,skybox", [(False, False, 0), (True, True, 500)])
-def test_train_step_fused_matches_reference_structured_step(depth, alpha, skybox):
+@pytest.mark.parametrize("depth,alpha,skybox,scaffold", [(False, False, 0, 0), (True, True, 500, 0),
+                                                          (True, False, 300, 2000)])
+def test_train_step_fused_matches_reference_structured_step(depth, alpha, skybox, scaffold):
     """The fused Street-sparse iteration against the reference's torch formulation of it
     (oracle/train_torch_ref.ReferenceTrainStep): with and without the masked inverse-depth L1,
     the alpha mask and a locked skybox."""
@@ -202,7 +203,10 @@ def test_train_step_fused_matches_reference_structured_step(depth, alpha, skybox
     for fused in (True, False):
         torch.manual_seed(0)
         ts = make_problem(20_000, 256, 192, n_views=3, seed=1, step_cls=None if fused else ReferenceTrainStep,
-                          depth=depth, alpha=alpha, skybox_points=skybox)
+                          depth=depth, alpha=alpha, skybox_points=skybox, scaffold_points=scaffold)
+        if scaffold:  # some over-large Gaussians on both sides of the scaffold boundary: the shrink runs
+            with torch.no_grad():
+                ts.g._scaling[scaffold - 50:scaffold + 50] += 3.0
         init = [getattr(ts.g, n).detach().clone() for n in names]
         losses = [ts.step().item() for _ in range(3)]
         steps[fused] = (losses, [getattr(ts.g, n).detach().clone() for n in names], ts.g.xyz_gradient_accum.clone(),
@@ -216,6 +220,10 @@ def test_train_step_fused_matches_reference_structured_step(depth, alpha, skybox
         assert close >= 0.999, close
     assert torch.equal(da, db)
     assert torch.isclose(aa, ab, rtol=1e-3, atol=1e-9).float().mean().item() >= 0.999
+    if scaffold:  # the scaffold rows are never shrunk; the big rows after them are
+        s0, s1 = ia[names.index("_scaling")], pa[names.index("_scaling")]
+        assert torch.all(s1[scaffold - 50:scaffold] > s0[scaffold - 50:scaffold] - 0.05)
+        assert torch.all(s1[scaffold:scaffold + 50] < s0[scaffold:scaffold + 50] - 0.2)
     if skybox:  # the locked rows never move (the scale shrink aside, which the reference applies to them too)
         for x, x0, name in zip(pa, ia, names):
             if name != "_scaling":

@@ -127,3 +127,44 @@ def test_fused_adam_validation_on_host():
     p.grad = torch.zeros(4, 3)
     with pytest.raises(RuntimeError, match="ROCm GPU"):
         opt.step(relevance=torch.zeros(4))
+
+
+@pytest.mark.parametrize("case", ["plain", "scaffold"])
+def test_torch_ref_densify_matches_reference_run(case):
+    """oracle/train_torch_ref.densify_and_prune (the larger-size checker of test_gpu_densify.py) on
+    CPU against the reference's own densify_and_prune run (tests/golden/densify_prune_*.npz), with
+    the reference's standard-normal split draws injected: bit-exact."""
+    import train_torch_ref as R
+    from gs_train.harness import GaussianSet
+    d = _gold(f"densify_prune_{case}.npz")
+    P = d["in_xyz"].shape[0]
+    g = GaussianSet(means3D=d["in_xyz"], shs=np.concatenate([d["in_f_dc"], d["in_f_rest"]], 1),
+                    opacities=np.full((P, 1), 0.5, np.float32), scales=np.ones((P, 3), np.float32),
+                    rotations=d["in_rotation"], device="cpu", joined_features=False)
+    with torch.no_grad():
+        g._opacity.copy_(torch.tensor(d["in_opacity"]))
+        g._scaling.copy_(torch.tensor(d["in_scaling"]))
+    g.xyz_gradient_accum = torch.tensor(d["in_accum"])
+    g.max_radii2D = torch.tensor(d["in_max_radii2D"])
+    g.denom = torch.tensor(d["in_denom"])
+    opt = R.OurAdamTorch(g.param_groups(), lr=0.0, eps=1e-15)
+    keys = {"_xyz": "xyz", "_features_dc": "f_dc", "_features_rest": "f_rest", "_opacity": "opacity",
+            "_scaling": "scaling", "_rotation": "rotation"}
+    for attr, k in keys.items():
+        opt.state[getattr(g, attr)] = {"step": torch.tensor(7.0), "exp_avg": torch.tensor(d["in_m_" + k]),
+                                       "exp_avg_sq": torch.tensor(d["in_v_" + k])}
+    z = torch.tensor(d["normals"])
+    real = torch.normal
+    torch.normal = lambda mean, std: z * std
+    try:
+        R.densify_and_prune(g, opt, float(d["max_grad"]), float(d["min_opacity"]), float(d["extent"]),
+                            float(d["percent_dense"]), first_row=int(d["scaffold"]))
+    finally:
+        torch.normal = real
+    for attr, k in keys.items():
+        p = getattr(g, attr)
+        np.testing.assert_array_equal(p.detach().numpy(), d["out_" + k], err_msg=k)
+        np.testing.assert_array_equal(opt.state[p]["exp_avg"].numpy(), d["out_m_" + k])
+        np.testing.assert_array_equal(opt.state[p]["exp_avg_sq"].numpy(), d["out_v_" + k])
+    np.testing.assert_array_equal(g.denom.numpy(), d["out_denom"])
+    np.testing.assert_array_equal(g.max_radii2D.numpy(), d["out_max_radii2D"])

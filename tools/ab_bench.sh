@@ -4,7 +4,7 @@
 set -uo pipefail
 TAG=${1:-ab}; ROUNDS=${2:-2}
 OUT=gpurun_out/ab_$TAG; mkdir -p "$OUT"
-ARGS="--steps 50 --warmup 10 --no-cpu-baseline --train-steps 0"
+ARGS="--steps 50 --warmup 10 --metric-only"
 for r in $(seq 1 "$ROUNDS"); do
   timeout -k 10 120 python3 bench.py $ARGS > "$OUT/base_$r.json" 2>/dev/null || exit 1
   for lib in vlibs/*.so; do

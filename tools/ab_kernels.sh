@@ -6,7 +6,7 @@ set -uo pipefail
 TAG=${1:-abk}
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/abk_$TAG; mkdir -p "$OUT"
-ARGS="--steps 20 --warmup 5 --profile-steps 1 --no-cpu-baseline --train-steps 0"
+ARGS="--steps 20 --warmup 5 --profile-steps 1 --metric-only"
 export TMPDIR=/tmp
 run() {  # name, library ("" = in-tree)
   ( cd /tmp && GSR_LIBRARY="$2" timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv \

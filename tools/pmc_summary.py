@@ -16,6 +16,7 @@ import glob
 import json
 import os
 import re
+import sys
 from collections import defaultdict
 
 STAGE_OF = [("render_bwd_kernel<true, true>", "render_bwd"), ("render_bwd_kernel<true, false>", "render_bwd:records"),
@@ -104,7 +105,11 @@ def main():
     ap.add_argument("--sq", action="append", default=[], help="rocprofv3 --pmc SQ_* pass directories")
     ap.add_argument("--note", default="")
     a = ap.parse_args()
-    res = {"note": a.note, "kernels": {}}
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import kernel_source_sha
+    # the kernel sources this profile describes (bench.py reports traffic / rocprof times only from
+    # a profile of the sources that run)
+    res = {"note": a.note, "source_sha": kernel_source_sha(), "kernels": {}}
     stats = read_stats(a.trace) if a.trace else {}
     fetch = read_pmc(a.fetch, "FETCH_SIZE") if a.fetch else {}
     write = read_pmc(a.write, "WRITE_SIZE") if a.write else {}

@@ -7,7 +7,7 @@ TAG=${1:-r01}; shift || true
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
-ARGS="--steps 3 --warmup 2 --profile-steps 1 --no-cpu-baseline --train-steps 0 $*"
+ARGS="--steps 3 --warmup 2 --profile-steps 1 --metric-only $*"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 "$ROOT/bench.py" $ARGS > "$OUT/trace.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 "$ROOT/bench.py" $ARGS > "$OUT/fetch.log" 2>&1

@@ -8,7 +8,7 @@ ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/sq_$TAG
 mkdir -p "$OUT"
 PROG="$ROOT/bench.py"
-ARGS="--steps 2 --warmup 1 --profile-steps 1 --no-cpu-baseline --train-steps 0"
+ARGS="--steps 2 --warmup 1 --profile-steps 1 --metric-only"
 if [ "${2:-}" = "train" ]; then
   PROG="$ROOT/tools/train_step_profile.py"
   ARGS="--steps 2 --warmup 1"
