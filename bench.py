@@ -373,6 +373,11 @@ def rocprof_ms(kernel):
     return round(us / 1e3, 5) if us and cur else None
 
 
+def log(msg):
+    """Progress on stderr (a long default run keeps writing while it works)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def spawn_ranks(a):
     """bench.py --gpus N run directly (no WORLD_SIZE): start N fresh rank processes through
     torch.distributed.run -- one process per GPU, as the driver launches it -- before this process
@@ -594,6 +599,7 @@ def main():
         torch.cuda.synchronize()
         pr.disable()
         pstats.Stats(pr, stream=sys.stderr).sort_stats("cumulative").print_stats(18)
+    log("metric: timing")
     elapsed = timed(step, a.steps, a.warmup, ranks)
 
     # per-stage device time with HIP events on the rasterizer's stream (separate, untimed steps)
@@ -649,6 +655,7 @@ def main():
     }
     del step, raster
     if a.train_steps > 0:
+        log("train step")
         from diff_gaussian_rasterization import _C as _Cstats
         r0 = _Cstats.forward_stats()
         tr = {"ms": round(train_step_ms(P, W, H, a.train_steps, 5, dev, seed=rank), 4),
@@ -664,14 +671,18 @@ def main():
             tr["reference_structured_ms"] = round(train_step_ms(P, W, H, a.train_steps, 5, dev, reference=True), 4)
         out["train_step"] = tr
     if not a.no_config4:
+        log("config 4")
         out["config4"] = config4(a, ranks, dev)
         if world == 1 and out["config4"]["train_step_ms_max"] is not None and "train_step" in out:
             out["train_step"]["config2_500k_ms"] = out["config4"]["train_step_ms_max"]
     if world == 1 and not a.no_street:
+        log("street frame")
         out["street_frame"] = street_frame(a, dev)
     if world == 1 and not a.no_config5:
+        log("config 5")
         out["config5"] = config5(a, dev)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        log("cpu baselines")
         out["cpu_baseline"], st = cpu_baseline(s, P, W, H, deg)
         out["cpu_baseline_torch"] = cpu_baseline_torch()
         with torch.no_grad():
