@@ -162,6 +162,13 @@ int gsr_forward_stats(int64_t *out, int n);
  * values written (<= n).  For bench.py's algorithmic-bytes model. */
 int gsr_frame_stats(const void *geom_buffer, int P, int width, int height, int64_t *out, int n);
 
+/* Measurement builds only (a variant library compiled with -DGSR_BLEND_STATS=1; zeros otherwise):
+ * lane-liveness counters of the blend kernels since the last reset, out[0..13] = backward
+ * {(instance, sub-block) pairs, live lanes, live 8x4 halves, live 16x1 rows, live 4x4 quads,
+ * staged instances, batches}, forward {pairs, alpha-passing lanes, halves, rows, quads, accepted
+ * lanes}, backward tiles.  reset != 0 zeroes them after the read.  Returns the count written. */
+int gsr_blend_stats(int64_t *out, int n, int reset);
+
 /* Version / diagnostics. */
 int gsr_abi_version(void);
 const char *gsr_last_error(void);

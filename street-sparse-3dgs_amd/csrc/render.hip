@@ -29,6 +29,35 @@ namespace gsr {
 
 __device__ __forceinline__ float gexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// Measurement builds only (GSR_BLEND_STATS=1, a variant library): lane-liveness statistics of the
+// blend kernels, read back with gsr_blend_stats.  Per evaluated (instance, 16x4 sub-block) pair:
+// the lanes whose pixel passes the alpha / position tests, and how many finer cells (8x4 halves,
+// 16x1 rows, 4x4 quads) hold at least one such lane -- what a finer cull could skip.
+#ifndef GSR_BLEND_STATS
+#define GSR_BLEND_STATS 0
+#endif
+__device__ unsigned long long g_blend_stats[16];
+// StatAcc::flush writes (pairs, live lanes, live halves, live rows, live quads) at its base index
+enum BlendStat { kBwdPairs, kBwdLive, kBwdHalves, kBwdRows, kBwdQuads, kBwdInst, kBwdBatches, kFwdPairs, kFwdLive,
+                 kFwdHalves, kFwdRows, kFwdQuads, kFwdAcc, kBwdTiles };
+struct StatAcc {
+    uint64_t v[5] = {0, 0, 0, 0, 0};
+    __device__ __forceinline__ void add(uint64_t live) {
+        constexpr uint64_t kLeft = 0x00FF00FF00FF00FFull;
+        v[0] += 1;
+        v[1] += (uint64_t)__popcll(live);
+        v[2] += (uint64_t)((live & kLeft) != 0) + (uint64_t)((live & ~kLeft) != 0);
+#pragma unroll
+        for (int r = 0; r < 4; r++) v[3] += (uint64_t)(((live >> (16 * r)) & 0xFFFFull) != 0);
+#pragma unroll
+        for (int q = 0; q < 4; q++) v[4] += (uint64_t)((live & (0x000F000F000F000Full << (4 * q))) != 0);
+    }
+    __device__ __forceinline__ void flush(int base) {
+        if ((threadIdx.x & 63) == 0)
+            for (int k = 0; k < 5; k++) atomicAdd(&g_blend_stats[base + k], (unsigned long long)v[k]);
+    }
+};
+
 #ifndef GSR_EXACT_CULL
 #define GSR_EXACT_CULL 3  // bit 0: forward, bit 1: backward
 #endif
@@ -184,6 +213,8 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kerne
         amin[k] = alive[k] ? 1.0f / 255.0f : 2.f;
     }
     uint64_t livem = __ballot(alive[0]);  // GSR_FWD_MASKSEL: the live pixels as a wave mask
+    StatAcc fst;
+    uint64_t fwd_acc = 0;
     const uint2 rg = ranges[tile];
     FwdBatch cur;
     uint32_t gnext = 0;
@@ -256,6 +287,10 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kerne
                                          __builtin_amdgcn_fcmpf(alpha, 1.0f / 255.0f, kFcmpUGE);
                     const uint64_t contm = __builtin_amdgcn_fcmpf(test_T, 0.0001f, kFcmpUGE);
                     const uint64_t accm = okm & contm;
+                    if (GSR_BLEND_STATS) {
+                        fst.add(okm);
+                        fwd_acc += (uint64_t)__popcll(accm);
+                    }
                     livem &= ~okm | contm;
                     const float wgt = lane_select(accm, alpha * T[k], 0.f);
                     C0[k] = fmaf(c.x, wgt, C0[k]);
@@ -292,6 +327,10 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kerne
         }
         if (j < cnt && (!GSR_FWD_EARLY_EXIT || livem)) blend(j);
         __builtin_amdgcn_wave_barrier();
+    }
+    if (GSR_BLEND_STATS) {
+        fst.flush(kFwdPairs);
+        if (lane == 0) atomicAdd(&g_blend_stats[kFwdAcc], (unsigned long long)fwd_acc);
     }
     const bool bad = sort_err && *sort_err;  // the depth sort gave up on a lookback: NaN frame
     uint32_t wl = 0;
@@ -495,6 +534,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
     const float sx = 0.5f * (float)W, sy = 0.5f * (float)H;
     const int rs_slot = wave_rs10_slot(lane);
     (void)rs_slot;
+    StatAcc bst;
+    uint64_t b_inst = 0, b_batches = 0;
 
     // The gather is software-pipelined as in the forward: batch b-1's GRec lines and record bases
     // and batch b-2's ids are in flight while batch b replays (unconditional loads at clamped list
@@ -536,6 +577,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
         }
         const uint64_t keep = __ballot(m != 0u);
         const uint32_t cnt = (uint32_t)__popcll(keep);
+        if (GSR_BLEND_STATS) {
+            b_inst += cnt;
+            b_batches += 1;
+        }
         if (m) {
             const uint32_t slot = lane_prefix(keep);
             s_a[slot] = make_float4(qa.x, qa.y, qa.z * kHalfLog2e, qa.w * kLog2e);  // scaled conic: gauss_p2
@@ -567,6 +612,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
                 const float G = gexp2(p2);
                 const float alpha = fminf(0.99f, b.y * G);
                 const bool ok = jpos < last[k] && !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f);
+                if (GSR_BLEND_STATS) bst.add(__ballot(ok));
                 any = first ? ok : (any || ok);
                 const float ae = ok ? alpha : 0.f;
                 const float rc = __builtin_amdgcn_rcpf(1.f - ae);
@@ -695,6 +741,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
         }
         __syncthreads();
     }
+    if (GSR_BLEND_STATS) {
+        bst.flush(kBwdPairs);
+        if (lane == 0) {
+            atomicAdd(&g_blend_stats[kBwdInst], (unsigned long long)b_inst);
+            atomicAdd(&g_blend_stats[kBwdBatches], (unsigned long long)b_batches);
+            atomicAdd(&g_blend_stats[kBwdTiles], 1ull);
+        }
+    }
 }
 
 void launch_render_bwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
@@ -718,3 +772,16 @@ void launch_render_bwd(const Camera &cam, const GeomState &gs, const BinningStat
 }
 
 }  // namespace gsr
+
+extern "C" int gsr_blend_stats(int64_t *out, int n, int reset) {
+    unsigned long long v[16] = {};
+    if (!out || n < 0) return -1;
+    if (hipMemcpyFromSymbol(v, HIP_SYMBOL(gsr::g_blend_stats), sizeof(v)) != hipSuccess) return -3;
+    if (reset) {
+        const unsigned long long z[16] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(gsr::g_blend_stats), z, sizeof(z)) != hipSuccess) return -3;
+    }
+    int k = 0;
+    for (; k < n && k < 16; k++) out[k] = (int64_t)v[k];
+    return k;
+}
