@@ -344,11 +344,10 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
             // the row is consumed: clear it, so a second backward through the same saved buffers
             // (retain_graph, torch.autograd.grad twice, gradcheck) sums from zero again, as
             // upstream's stateless backward does.  Only the ~12% of rows render_bwd added into
-            // are written (48 B each).
+            // are written, as whole 64-B lines (no partial-line read-modify-write).
             float4 *a = sc.acc + 4 * (size_t)i;
-            a[0] = make_float4(0.f, 0.f, 0.f, 0.f);
-            a[1] = make_float4(0.f, 0.f, 0.f, 0.f);
-            a[2] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int q = 0; q < 4; q++) a[q] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
         if (GSR_BWD_SKIP_DEAD) {
             if (!sc.atomic && vis) nz = nz || out.dopacity[i] != 0.f;  // record mode: summed by record_sum

@@ -5,7 +5,8 @@
   tests/golden/make_train_golden.py in the build container) and the standard-normal draws behind
   its split samples, which are injected here -- row order, counts, every parameter, both Adam
   moments and the statistics bit-exact, except the split children's xyz, which the reference
-  forms with torch.bmm (library summation order; 1e-6);
+  forms with torch.bmm (library summation order; 1e-6), and their scaling log(exp(s) / 1.6)
+  (CPU exp / log / true division in the fixture run; a few ulps);
 * at larger sizes against the torch restatement (oracle/train_torch_ref.densify_and_prune) on the
   same generator stream."""
 from __future__ import annotations
@@ -95,11 +96,16 @@ def test_densify_and_prune_matches_reference_run(case):
     n = d["out_xyz"].shape[0]
     assert c["total"] == n and c["cloned"] > 0 and c["split"] > 0 and c["kept"] < P
     assert 2 * c["split"] == d["normals"].shape[0]
-    got = {"f_dc": g._features[:, :1], "f_rest": g._features[:, 1:], "opacity": g._opacity, "scaling": g._scaling,
-           "rotation": g._rotation}
+    got = {"f_dc": g._features[:, :1], "f_rest": g._features[:, 1:], "opacity": g._opacity, "rotation": g._rotation}
     for k, v in got.items():
         np.testing.assert_array_equal(v.detach().cpu().numpy(), d["out_" + k], err_msg=k)
-    old = c["kept"] + c["cloned"]  # rows before the split children: copied xyz
+    old = c["kept"] + c["cloned"]  # rows before the split children: copies
+    # the split children's log(exp(s) / 1.6): the reference ran on the CPU here (true division and
+    # CPU exp / log); on its own CUDA device torch divides by a scalar as a multiply by its
+    # reciprocal, as the kernel does -- an ulp apart at most
+    sc = g._scaling.detach().cpu().numpy()
+    np.testing.assert_array_equal(sc[:old], d["out_scaling"][:old])
+    np.testing.assert_allclose(sc, d["out_scaling"], rtol=4e-7, atol=0)
     xyz = g._xyz.detach().cpu().numpy()
     np.testing.assert_array_equal(xyz[:old], d["out_xyz"][:old])
     np.testing.assert_allclose(xyz, d["out_xyz"], rtol=1e-6, atol=1e-6)
