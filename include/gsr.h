@@ -148,12 +148,21 @@ int gsr_set_true_scale_gradient(int enable);
  * ten per-Gaussian gradient sums into a per-Gaussian row with hardware float atomics (like
  * upstream's atomicAdd accumulation: results vary in the last bits from run to run).  1: each
  * instance writes a record and a second pass sums every Gaussian's records in a fixed order --
- * forward + backward bitwise reproducible, slower.  Returns the previous mode. */
+ * forward + backward bitwise reproducible, slower.  A frame's backward uses the mode that was in
+ * force at its forward.  Returns the previous mode. */
 int gsr_set_deterministic(int enable);
 
+/* Depth-order strategy of the binning, process-wide.  0 (default): the local sort -- level 1 in
+ * Gaussian index order, each superblock list sorted by depth in LDS -- except for frames forwarded
+ * in deterministic mode and frames with a superblock list longer than the LDS sort holds, which
+ * take the global sort.  1: always the global depth sort of all P Gaussians (dsort.hip).  Both give
+ * the same per-tile lists.  Returns the previous mode (or GSR_ERR_INVALID_ARGUMENT). */
+int gsr_set_binning(int mode);
+
 /* Forward statistics since load: out[0] = frames rasterized (P > 0), out[1] = frames whose
- * binning ran twice because the capacity hint from the previous frame was short of K.
- * Returns the number of values written (<= n). */
+ * binning ran twice because the capacity hint from the previous frame was short of K,
+ * out[2] = frames binned by the local sort, out[3] = local frames re-run through the global sort
+ * (a superblock list too long for LDS).  Returns the number of values written (<= n). */
 int gsr_forward_stats(int64_t *out, int n);
 
 /* Statistics of one forward frame, read from its geometry buffer (synchronises the device):

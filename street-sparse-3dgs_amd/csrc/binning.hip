@@ -18,6 +18,17 @@
 // The result is the upstream order inside every tile -- (depth bits, Gaussian id) -- with tiles
 // laid out SB-major instead of row-major; every consumer goes through `ranges`, so the layout of
 // whole tiles in point_list is free.  Traffic ~ 8 B per SB instance + 4 B per tile instance written.
+//
+// Two ways to reach depth order (rasterizer.hip picks per frame):
+//   local sort (default)  level 1 runs over the Gaussians in INDEX order (no global depth sort), so
+//                         every SB list is in id order; sb_sort_bin then sorts each SB's list by
+//                         depth inside LDS (stable LSD radix over the list's own key range: equal
+//                         depths keep id order) and bins it into the SB's tiles from LDS.  The
+//                         column scan publishes K and the longest SB list.
+//   global sort           dsort.hip's depth order of all P Gaussians, level 1 over it, and
+//                         tile_bin over the (already depth-ordered) SB lists: frames with an SB
+//                         list longer than the LDS sort holds (kSortCap), and deterministic mode
+//                         (whose backward needs dsort's Gaussian-major record offsets).
 #include "gsr_launch.h"
 
 namespace gsr {
@@ -168,7 +179,7 @@ __global__ __launch_bounds__(kColThreads) void sb_colscan_kernel(SBGrid sg, uint
                                                                  const uint32_t *__restrict__ cnt_i,
                                                                  uint32_t *__restrict__ base_g,
                                                                  uint32_t *__restrict__ base_i,
-                                                                 uint32_t *__restrict__ done) {
+                                                                 uint32_t *__restrict__ done, FrameWords fw) {
     __shared__ uint32_t wsum[kColThreads / 64];
     __shared__ uint32_t s_last;
     const int s = blockIdx.x;
@@ -198,11 +209,12 @@ __global__ __launch_bounds__(kColThreads) void sb_colscan_kernel(SBGrid sg, uint
     __syncthreads();
     if (!s_last) return;
     const int nsb = sg.nsb;
-    uint32_t cg = 0, ci = 0;
+    uint32_t cg = 0, ci = 0, mg = 0;
     for (int b = 0; b < nsb; b += kColThreads) {
         const int k = b + (int)threadIdx.x;
         const uint32_t vg = k < nsb ? __hip_atomic_load(&base_g[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
         const uint32_t vi = k < nsb ? __hip_atomic_load(&base_i[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        mg = max(mg, vg);
         uint32_t tg, ti;
         const uint32_t eg = block_exclusive_scan<kColThreads>(vg, wsum, tg);
         const uint32_t ei = block_exclusive_scan<kColThreads>(vi, wsum, ti);
@@ -216,6 +228,25 @@ __global__ __launch_bounds__(kColThreads) void sb_colscan_kernel(SBGrid sg, uint
     if (threadIdx.x == 0) {
         base_g[nsb] = cg;
         base_i[nsb] = ci;
+    }
+    if (fw.dev_K) {
+        // local-sort frames: K (= the instance total) and the longest SB list for the kernels and
+        // the host.  The host's K word is stored last (the host reads the others once it is set).
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mg = max(mg, (uint32_t)__shfl_xor((int)mg, o, 64));
+        __syncthreads();
+        if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = mg;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int k = 1; k < kColThreads / 64; k++) mg = max(mg, wsum[k]);
+            *fw.dev_K = ci;
+            *fw.dev_maxsb = mg;
+            if (fw.host) {
+                __hip_atomic_store(&fw.host[kHostMaxSB], mg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&fw.host[kHostP1], cg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&fw.host[kHostK], ci, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
     }
 }
 
@@ -304,7 +335,7 @@ __global__ __launch_bounds__(64 * kScatterWaves) void sb_scatter_kernel(int P, S
     }
     __syncthreads();
 
-    const auto id_at = [&](int j) { return j < jw1 ? order[j] : 0u; };
+    const auto id_at = [&](int j) { return j < jw1 ? (order ? order[j] : (uint32_t)j) : 0u; };
     uint32_t gnext = id_at(jw0 + lane);
     rnext = rect_at(jw0 + lane);
     for (int jb = jw0; jb < jw1; jb += 64) {
@@ -513,7 +544,266 @@ __global__ __launch_bounds__(64 * kTBWaves) void tile_bin_kernel(SBGrid sg, int 
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Local sort: one workgroup per SB sorts its list (id order, from an index-order level 1) by depth
+// in LDS and bins it into the SB's tiles -- the global depth sort's job, per SB and without a pass
+// over global memory per digit.
+//
+// 1. Load: entry e's depth key (a gather of the Gaussian's key, dsort's key array) into registers,
+//    wave-striped so that (wave, item, lane) order is list order; the list's key range by a block
+//    min / max.
+// 2. Stable LSD radix over (key - min) in 8-bit digits, only as many passes as the range needs
+//    (equal depths: none): match-mask ranking (8 ballots per key) into per-wave LDS counters, a
+//    digit scan, the reorder through LDS (keys and 16-bit list positions ping-pong).  Stability
+//    keeps id order among equal depths: the (depth bits, id) order of upstream's keys.
+// 3. The sorted (id, footprint) pairs, gathered once from the SB list into LDS, then tile_bin's
+//    two ballot passes (per-wave tile counts, tile bases and ranges, stable placement) over them.
+// ---------------------------------------------------------------------------------------------
+#ifndef GSR_SORT_CAP
+#define GSR_SORT_CAP 8192
+#endif
+constexpr int kSBThreads = 1024;
+constexpr int kSBWaves = kSBThreads / 64;
+constexpr int kSortCap = GSR_SORT_CAP;            // longest SB list sorted in LDS
+constexpr int kSBItems = kSortCap / kSBThreads;   // keys per thread
+static_assert(kSortCap % kSBThreads == 0 && kSortCap <= 65536, "kSortCap: a multiple of 1024, 16-bit positions");
+
+__device__ __forceinline__ uint32_t lanes_with_digit(uint32_t d, uint64_t valid) {
+    uint64_t m = valid;
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+        const bool bit = (d >> b) & 1u;
+        const uint64_t bb = __ballot(bit);
+        m &= bit ? bb : ~bb;
+    }
+    return m;
+}
+
+__global__ __launch_bounds__(kSBThreads) void sb_sort_bin_kernel(SBGrid sg, int gx, int gy,
+                                                                const uint32_t *__restrict__ base_g,
+                                                                const uint32_t *__restrict__ base_i,
+                                                                const uint2 *__restrict__ sblist,
+                                                                const uint32_t *__restrict__ dkey,
+                                                                uint32_t *__restrict__ point_list,
+                                                                uint2 *__restrict__ ranges,
+                                                                const uint32_t *__restrict__ kdev, uint32_t cap,
+                                                                const uint32_t *__restrict__ maxsb) {
+    // capacity short (the host re-runs at K) or an SB list the LDS cannot hold (the host re-runs
+    // the frame through the global depth sort): nothing is written
+    if (*kdev > cap || *maxsb > (uint32_t)kSortCap) return;
+    __shared__ uint32_t s_key[2][kSortCap];
+    __shared__ uint16_t s_pos[2][kSortCap];
+    __shared__ uint32_t s_wh[kSBWaves][256];  // per-wave digit counts; later the per-wave tile counters
+    __shared__ uint32_t s_bex[256];
+    __shared__ uint32_t s_lo, s_hi;
+    const int s = blockIdx.x;
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    const int side = 1 << sg.shift, tps = side * side;
+    const int ox = (s % sg.nsbx) * side, oy = (s / sg.nsbx) * side;
+    const uint32_t L0 = base_g[s], n = base_g[s + 1] - L0;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const int wb = w * kSBItems * 64;  // the wave's first list position
+
+    // 1. keys and their range
+    if (t == 0) {
+        s_lo = 0xFFFFFFFFu;
+        s_hi = 0u;
+    }
+    for (int i = t; i < kSBWaves * 256; i += kSBThreads) (&s_wh[0][0])[i] = 0u;
+    uint32_t key[kSBItems];
+    uint16_t pos[kSBItems];
+    {
+        uint32_t id[kSBItems];
+#pragma unroll
+        for (int k = 0; k < kSBItems; k++) {
+            const uint32_t e = (uint32_t)(wb + k * 64 + lane);
+            id[k] = e < n ? sblist[L0 + e].x : 0u;
+        }
+        uint32_t lo = 0xFFFFFFFFu, hi = 0u;
+#pragma unroll
+        for (int k = 0; k < kSBItems; k++) {
+            const uint32_t e = (uint32_t)(wb + k * 64 + lane);
+            key[k] = e < n ? dkey[id[k]] : 0u;
+            pos[k] = (uint16_t)e;
+            if (e < n) {
+                lo = min(lo, key[k]);
+                hi = max(hi, key[k]);
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            lo = min(lo, (uint32_t)__shfl_xor((int)lo, o, 64));
+            hi = max(hi, (uint32_t)__shfl_xor((int)hi, o, 64));
+        }
+        __syncthreads();
+        if (lane == 0 && lo <= hi) {
+            atomicMin(&s_lo, lo);
+            atomicMax(&s_hi, hi);
+        }
+    }
+    __syncthreads();
+    const uint32_t klo = s_lo, range = s_lo <= s_hi ? s_hi - s_lo : 0u;
+    const int passes = range ? (32 - __clz((int)range) + 7) / 8 : 0;
+#pragma unroll
+    for (int k = 0; k < kSBItems; k++) key[k] -= klo;  // padding keys wrap: never ranked (valid mask)
+
+    // 2. stable LSD passes; the sorted positions end in s_pos[cur]
+    int cur = 0;
+    for (int p = 0; p < passes; p++) {
+        const int shift = 8 * p;
+        uint32_t rk[kSBItems];
+#pragma unroll
+        for (int k = 0; k < kSBItems; k++) {
+            if (wb + k * 64 >= (int)n) {  // wave-uniform: nothing of this item in the list
+                rk[k] = 0u;
+                continue;
+            }
+            const bool valid = (uint32_t)(wb + k * 64 + lane) < n;
+            const uint32_t d = (key[k] >> shift) & 0xFFu;
+            const uint64_t m = lanes_with_digit(d, __ballot(valid));
+            const uint32_t b = lanes_below(m);
+            const uint32_t old = s_wh[w][d];
+            if (valid && b == 0u) s_wh[w][d] = old + (uint32_t)__popcll(m);
+            rk[k] = old + b;
+        }
+        __syncthreads();
+        if (t < 256) {
+            uint32_t c = 0;
+#pragma unroll
+            for (int ww = 0; ww < kSBWaves; ww++) {
+                const uint32_t v = s_wh[ww][t];
+                s_wh[ww][t] = c;
+                c += v;
+            }
+            s_bex[t] = c;
+        }
+        __syncthreads();
+        if (w == 0) {
+            uint32_t *a = s_bex;
+            const uint32_t x0 = a[4 * lane], x1 = a[4 * lane + 1], x2 = a[4 * lane + 2], x3 = a[4 * lane + 3];
+            const uint32_t sum = x0 + x1 + x2 + x3;
+            uint32_t incl = sum;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t v = (uint32_t)__shfl_up((int)incl, o, 64);
+                if (lane >= o) incl += v;
+            }
+            const uint32_t e = incl - sum;
+            a[4 * lane] = e;
+            a[4 * lane + 1] = e + x0;
+            a[4 * lane + 2] = e + x0 + x1;
+            a[4 * lane + 3] = e + x0 + x1 + x2;
+        }
+        __syncthreads();
+        const int nxt = cur ^ 1;
+#pragma unroll
+        for (int k = 0; k < kSBItems; k++) {
+            if ((uint32_t)(wb + k * 64 + lane) < n) {
+                const uint32_t d = (key[k] >> shift) & 0xFFu;
+                const uint32_t dst = s_bex[d] + s_wh[w][d] + rk[k];
+                s_key[nxt][dst] = key[k];
+                s_pos[nxt][dst] = pos[k];
+            }
+        }
+        __syncthreads();
+        for (int i = t; i < kSBWaves * 256; i += kSBThreads) (&s_wh[0][0])[i] = 0u;
+#pragma unroll
+        for (int k = 0; k < kSBItems; k++) {
+            const uint32_t e = (uint32_t)(wb + k * 64 + lane);
+            if (e < n) {
+                key[k] = s_key[nxt][e];
+                pos[k] = s_pos[nxt][e];
+            }
+        }
+        cur = nxt;
+        // s_wh cleared and this pass's reads done before the next pass ranks and scatters
+        __syncthreads();
+    }
+
+    // 3. the sorted (id, footprint) pairs into LDS (the key buffers are free): sorted position e
+    // is held by the thread that owns e in the striped layout -- its pos[] after the last pass
+    uint32_t *s_id = s_key[0], *s_fp = s_key[1];
+#pragma unroll
+    for (int k = 0; k < kSBItems; k++) {
+        const uint32_t e = (uint32_t)(wb + k * 64 + lane);
+        if (e < n) {
+            const uint2 v = sblist[L0 + pos[k]];
+            s_id[e] = v.x;
+            s_fp[e] = v.y;
+        }
+    }
+    __syncthreads();
+
+    // tile binning over the sorted list (tile_bin's passes, entries from LDS): wave w owns the
+    // contiguous segment [seg0, seg1)
+    uint32_t(*tc)[256] = s_wh;
+    const uint32_t seg0 = (uint32_t)(((uint64_t)n * w) / kSBWaves), seg1 = (uint32_t)(((uint64_t)n * (w + 1)) / kSBWaves);
+    for (int tg = 0; tg < tps; tg += kTileGroup) {
+        uint32_t cnt[kTileGroup];
+#pragma unroll
+        for (int k = 0; k < kTileGroup; k++) cnt[k] = 0u;
+        for (uint32_t gb = seg0; gb < seg1; gb += 64) {
+            const uint32_t i = gb + (uint32_t)lane;
+            const uint32_t m = i < seg1 ? group_mask(s_fp[i], tg, sg.shift) : 0u;
+#pragma unroll
+            for (int k = 0; k < kTileGroup; k++) cnt[k] += (uint32_t)__popcll(__ballot((m >> k) & 1u));
+        }
+        if (lane == 0)
+#pragma unroll
+            for (int k = 0; k < kTileGroup; k++)
+                if (tg + k < tps) tc[w][tg + k] = cnt[k];
+    }
+    __syncthreads();
+    if (w == 0) {
+        uint32_t carry = 0;
+        for (int t0 = 0; t0 < tps; t0 += 64) {
+            const int tt = t0 + lane;
+            uint32_t c = 0;
+            if (tt < tps)
+                for (int k = 0; k < kSBWaves; k++) c += tc[k][tt];
+            uint32_t incl = c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t v = (uint32_t)__shfl_up((int)incl, o, 64);
+                if (lane >= o) incl += v;
+            }
+            if (tt < tps) {
+                uint32_t b = base_i[s] + carry + incl - c;
+                const int x = ox + (tt & (side - 1)), y = oy + (tt >> sg.shift);
+                if (x < gx && y < gy) ranges[y * gx + x] = make_uint2(b, b + c);
+                for (int k = 0; k < kSBWaves; k++) {
+                    const uint32_t ck = tc[k][tt];
+                    tc[k][tt] = b;
+                    b += ck;
+                }
+            }
+            carry += (uint32_t)__shfl((int)incl, 63, 64);
+        }
+    }
+    __syncthreads();
+    for (int tg = 0; tg < tps; tg += kTileGroup) {
+        uint32_t pk[kTileGroup];
+#pragma unroll
+        for (int k = 0; k < kTileGroup; k++) pk[k] = tg + k < tps ? tc[w][tg + k] : 0u;
+        for (uint32_t gb = seg0; gb < seg1; gb += 64) {
+            const uint32_t i = gb + (uint32_t)lane;
+            const bool in = i < seg1;
+            const uint32_t m = in ? group_mask(s_fp[i], tg, sg.shift) : 0u;
+            const uint32_t g = in ? s_id[i] : 0u;
+#pragma unroll
+            for (int k = 0; k < kTileGroup; k++) {
+                const bool hit = (m >> k) & 1u;
+                const uint64_t bm = __ballot(hit);
+                if (hit) point_list[pk[k] + (uint32_t)__popcll(bm & lt)] = g;
+                pk[k] += (uint32_t)__popcll(bm);
+            }
+        }
+    }
+}
+
 }  // namespace
+
+int sort_cap() { return kSortCap; }
 
 SBGrid sb_grid(int gx, int gy, int P) {
     SBGrid g;
@@ -542,28 +832,43 @@ SBGrid sb_grid(int gx, int gy, int P) {
 
 bool sb_grid_supported(const SBGrid &g) { return g.nsb <= kMaxSB; }
 
-void launch_binning_superblocks(int P, const Camera &cam, const GeomState &gs, const BinningState &bs,
-                                const ImageState &is, hipStream_t s) {
-    (void)is;
+void launch_binning_count(int P, const Camera &cam, const GeomState &gs, bool index_order, const FrameWords &fw,
+                          hipStream_t s) {
     const SBGrid &sg = gs.sb;
     if (P == 0 || cam.gx * cam.gy == 0) return;
     const size_t l1 = sizeof(uint32_t) * 2 * (size_t)sg.nsb;
-    const size_t l3 = sizeof(uint32_t) * 3 * kScatterWaves * (size_t)sg.nsb;
-    hipLaunchKernelGGL(sb_count_kernel, dim3(sg.nchunks), dim3(1024), l1, s, P, sg, gs.drect, drect4_of(gs), gs.sb_cnt_g,
+    const uint2 *rects = index_order ? gs.rect8 : gs.drect;
+    const uint32_t *rects4 = index_order ? gs.rect4 : drect4_of(gs);
+    hipLaunchKernelGGL(sb_count_kernel, dim3(sg.nchunks), dim3(1024), l1, s, P, sg, rects, rects4, gs.sb_cnt_g,
                        gs.sb_cnt_i);
     hipLaunchKernelGGL(sb_colscan_kernel, dim3(sg.nsb), dim3(kColThreads), 0, s, sg, gs.sb_cnt_g, gs.sb_cnt_i,
-                       gs.sb_base_g, gs.sb_base_i, dsort_aux_word(gs));
-    hipLaunchKernelGGL(sb_scatter_kernel, dim3(sg.nchunks), dim3(64 * kScatterWaves), l3, s, P, sg, gs.order, gs.drect, drect4_of(gs),
-                       gs.sb_cnt_g, gs.sb_base_g, bs.sblist, bs.kdev, bs.cap);
+                       gs.sb_base_g, gs.sb_base_i, dsort_aux_word(gs), fw);
+}
+
+void launch_binning_scatter(int P, const Camera &cam, const GeomState &gs, const BinningState &bs, bool index_order,
+                            hipStream_t s) {
+    const SBGrid &sg = gs.sb;
+    if (P == 0 || cam.gx * cam.gy == 0) return;
+    const size_t l3 = sizeof(uint32_t) * 3 * kScatterWaves * (size_t)sg.nsb;
+    const uint2 *rects = index_order ? gs.rect8 : gs.drect;
+    const uint32_t *rects4 = index_order ? gs.rect4 : drect4_of(gs);
+    hipLaunchKernelGGL(sb_scatter_kernel, dim3(sg.nchunks), dim3(64 * kScatterWaves), l3, s, P, sg,
+                       index_order ? (const uint32_t *)nullptr : gs.order, rects, rects4, gs.sb_cnt_g, gs.sb_base_g,
+                       bs.sblist, bs.kdev, bs.cap);
 }
 
 void launch_binning_tiles(int P, const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
-                          hipStream_t s) {
+                          bool local_sort, const uint32_t *maxsb, hipStream_t s) {
     const SBGrid &sg = gs.sb;
     const int T = cam.gx * cam.gy;
     if (T == 0) return;
     if (P == 0) {
         (void)hipMemsetAsync(is.ranges, 0, sizeof(uint2) * (size_t)T, s);
+        return;
+    }
+    if (local_sort) {
+        hipLaunchKernelGGL(sb_sort_bin_kernel, dim3(sg.nsb), dim3(kSBThreads), 0, s, sg, cam.gx, cam.gy, gs.sb_base_g,
+                           gs.sb_base_i, bs.sblist, gs.dkey, bs.point_list, is.ranges, bs.kdev, bs.cap, maxsb);
         return;
     }
     // long superblock lists (large P): more waves per superblock, the 510-ish workgroups of a

@@ -49,7 +49,8 @@ constexpr int kCtlDone = 4;    // upsweep tiles finished
 constexpr int kCtlK = 5;       // sum of tiles_touched
 constexpr int kCtlErr = 6;     // set when a bounded spin gave up (never expected)
 constexpr int kCtlAux = 7;     // per-frame counter lent to the binning (sb_colscan's last-workgroup count)
-constexpr int kCtlHead = 8;
+constexpr int kCtlMaxSB = 8;   // local-sort frames: the longest SB list (sb_colscan)
+constexpr int kCtlHead = 16;
 // The upsweep runs at most kUpMax workgroups, each over tpb consecutive tiles, so that a pass
 // reduces at most kUpMax histogram rows (kUpMax / 4 loads per thread, all in flight at once).
 constexpr int kUpMax = 128;
@@ -444,5 +445,7 @@ void launch_depth_sort(int P, const GeomState &gs, uint32_t *host_K, uint32_t *h
 uint32_t *dsort_K_word(const GeomState &gs) { return gs.ctrl + kCtlK; }
 uint32_t *dsort_err_word(const GeomState &gs) { return gs.ctrl + kCtlErr; }
 uint32_t *dsort_aux_word(const GeomState &gs) { return gs.ctrl + kCtlAux; }
+uint32_t *dsort_maxsb_word(const GeomState &gs) { return gs.ctrl + kCtlMaxSB; }
+int dsort_head_words() { return kCtlHead; }
 
 }  // namespace gsr

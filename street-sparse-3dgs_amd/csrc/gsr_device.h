@@ -487,6 +487,16 @@ __host__ __device__ __forceinline__ const uint32_t *drect4_of(const GeomState &g
     return g.rect4 ? reinterpret_cast<const uint32_t *>(g.drect) : nullptr;
 }
 
+// Frame words a local-sort frame's column scan publishes (binning.hip): device copies for the
+// kernels (dev_K = the depth sort's K word, which every capacity test reads) and, when host is set,
+// the pinned host words the host waits on.  host[kHostK] is stored last.
+enum HostWord { kHostK = 0, kHostErr = 1, kHostMaxSB = 2, kHostP1 = 3, kHostWords = 4 };
+struct FrameWords {
+    uint32_t *dev_K;      // nullptr: global-sort frame (dsort publishes K)
+    uint32_t *dev_maxsb;  // longest SB list
+    uint32_t *host;       // pinned host words (HostWord indices) or nullptr
+};
+
 struct BinningState {       // per tile instance
     uint2 *sblist;          // level 1: (Gaussian id, footprint in SB-local tiles) per superblock, depth order
     uint32_t *point_list;   // Gaussian ids, per tile contiguous in (depth, id) order; tiles SB-major

@@ -58,13 +58,25 @@ uint32_t *dsort_K_word(const GeomState &gs);
 uint32_t *dsort_err_word(const GeomState &gs);
 // a zeroed-per-frame control word the binning uses as a completion counter
 uint32_t *dsort_aux_word(const GeomState &gs);
-// binning.hip: per-tile lists from the depth-ordered Gaussians (two stable counting levels).
+// local-sort frames: the longest SB list (sb_colscan); the head words (tickets, counters, K, ...)
+// a frame re-run through the global sort must zero again
+uint32_t *dsort_maxsb_word(const GeomState &gs);
+int dsort_head_words();
+// binning.hip: per-tile lists (two stable counting levels).  index_order: level 1 over the
+// Gaussians in index order (local sort: sb_sort_bin orders each SB list by depth in LDS); else over
+// dsort's depth order (gs.order / gs.drect; tile_bin).
 SBGrid sb_grid(int gx, int gy, int P);
 bool sb_grid_supported(const SBGrid &g);
-void launch_binning_superblocks(int P, const Camera &cam, const GeomState &gs, const BinningState &bs,
-                                const ImageState &is, hipStream_t s);
-void launch_binning_tiles(int P, const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
+int sort_cap();  // the longest SB list the local sort holds
+// level-1 counts and SB bases; with fw.dev_K set (local sort) the column scan also stores K, the
+// longest SB list and the level-1 total (FrameWords)
+void launch_binning_count(int P, const Camera &cam, const GeomState &gs, bool index_order, const FrameWords &fw,
                           hipStream_t s);
+void launch_binning_scatter(int P, const Camera &cam, const GeomState &gs, const BinningState &bs, bool index_order,
+                            hipStream_t s);
+// local_sort: sb_sort_bin (exits when *maxsb > sort_cap()); else tile_bin over depth-ordered lists
+void launch_binning_tiles(int P, const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
+                          bool local_sort, const uint32_t *maxsb, hipStream_t s);
 
 // render.hip
 void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,

@@ -26,11 +26,14 @@ thread_local std::string g_err;
 // K (num_rendered) arrives in pinned, host-coherent memory written by the depth sort's first
 // kernel; the host waits on an event recorded right after it, so the sort passes keep running
 // while the host sizes the binning buffer.
-// g_pinned[0] = K, g_pinned[1] = sticky depth-sort error (a lookback spin gave up; never expected)
+// g_pinned[kHostK] = K, [kHostErr] = sticky depth-sort error (a lookback spin gave up; never
+// expected), [kHostMaxSB] / [kHostP1] = a local-sort frame's longest SB list / level-1 total
 thread_local uint32_t *g_pinned = nullptr;
 thread_local uint32_t *g_pinned_dev = nullptr;
 // forward statistics (gsr_forward_stats): frames, binning re-runs at K (capacity hint short)
-std::atomic<int64_t> g_frames{0}, g_reruns{0};
+std::atomic<int64_t> g_frames{0}, g_reruns{0}, g_local_frames{0}, g_fallbacks{0};
+// binning mode (gsr_set_binning): 0 = local sort where it applies, 1 = always the global depth sort
+std::atomic<int> g_binning_mode{0};
 constexpr int kMaxDevicesK = 64;
 thread_local hipEvent_t g_k_ready[kMaxDevicesK] = {};
 // per device: capacity for the next frame's point list, 0 = none yet.  It is the largest K of the
@@ -117,7 +120,7 @@ int fail(int code, const std::string &msg) {
 // A lookback timeout of this or an earlier frame's depth sort (the pass kernels store the pinned
 // word; its frame's render_fwd already wrote NaN pixels): fail this call, once per occurrence.
 int sticky_sort_error() {
-    if (g_pinned && __atomic_exchange_n(&g_pinned[1], 0u, __ATOMIC_SEQ_CST) != 0u)
+    if (g_pinned && __atomic_exchange_n(&g_pinned[kHostErr], 0u, __ATOMIC_SEQ_CST) != 0u)
         return fail(GSR_ERR_DEVICE, "depth sort: a lookback spin timed out (this or an earlier frame; its image is NaN)");
     return GSR_OK;
 }
@@ -439,7 +442,8 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
     // the backward's accumulator rows are cleared (and its launch order built) only for a frame a
     // backward may follow: atomic mode, GSR_FWD_NO_BACKWARD not set
     const bool need_bwd = !(flags & GSR_FWD_NO_BACKWARD);
-    const bool clear_acc = need_bwd && g_deterministic.load(std::memory_order_relaxed) == 0;
+    const bool det_fwd = g_deterministic.load(std::memory_order_relaxed) != 0;
+    const bool clear_acc = need_bwd && !det_fwd;
     if (num_rendered) *num_rendered = 0;
     int rc = validate_common(P, D, M, shs, colors_precomp, scales, rotations, cov3D_precomp, width, height);
     if (rc) return rc;
@@ -516,21 +520,35 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
 #ifndef GSR_COLOR_FORK
 #define GSR_COLOR_FORK 2  // 0: beside the sort and the binning; 1: beside the binning only; 2: chosen per frame
 #endif
+#ifndef GSR_COLOR_LOCAL_BLOCKS
+#define GSR_COLOR_LOCAL_BLOCKS 128  // local-sort frames: the colour pass's persistent grid beside the binning
+#endif
+    // Depth order (binning.hip): the local sort (level 1 in index order, each superblock list sorted
+    // in LDS) unless the frame is in deterministic mode (its backward needs the global sort's
+    // record offsets) or the global sort is forced; a local frame whose longest SB list exceeds
+    // what the LDS sort holds is re-run through the global sort.
+    bool local = P > 0 && g_binning_mode.load(std::memory_order_relaxed) == 0 && !det_fwd;
     // The depth sort runs one 1024-thread workgroup per 8192 keys (dsort_blocks) and leaves the
     // other CUs idle: when it leaves a good share of them, the SH colour pass forks right after the
     // preprocess as a persistent grid on those CUs (1M Gaussians: 123 sort workgroups, 128 colour
     // blocks; 2640 -> 2696 Mpix/s, 133 blocks already slowed the sort); otherwise it forks after the sort, beside the
-    // binning, at full width.
+    // binning, at full width.  Local-sort frames fork it right after the preprocess too, as a
+    // persistent grid of GSR_COLOR_LOCAL_BLOCKS blocks beside the binning.
     int color_blocks = 0;
     bool color_early = GSR_COLOR_FORK == 0;
     if (GSR_COLOR_FORK == 2 && split && !GSR_COLOR_SERIAL) {
-        // workgroups are dealt round-robin over the 8 XCDs: leave every XCD room for its share
-        // of the sort's workgroups (123 of them -> 16 per XCD -> 8 x (32 - 16) = 128 colour blocks)
-        const int per_xcd = device_cus() / 8;
-        const int free_cus = 8 * (per_xcd - (dsort_blocks(P) + 7) / 8);
-        if (free_cus >= 2 * per_xcd) {
+        if (local) {
             color_early = true;
-            color_blocks = free_cus;
+            color_blocks = GSR_COLOR_LOCAL_BLOCKS;
+        } else {
+            // workgroups are dealt round-robin over the 8 XCDs: leave every XCD room for its share
+            // of the sort's workgroups (123 of them -> 16 per XCD -> 8 x (32 - 16) = 128 colour blocks)
+            const int per_xcd = device_cus() / 8;
+            const int free_cus = 8 * (per_xcd - (dsort_blocks(P) + 7) / 8);
+            if (free_cus >= 2 * per_xcd) {
+                color_early = true;
+                color_blocks = free_cus;
+            }
         }
     }
     auto fork_color = [&]() -> int {
@@ -560,62 +578,91 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
     hipEvent_t k_ready = nullptr;
     if (P > 0) {
         if (!g_pinned) {
-            if (hipHostMalloc(reinterpret_cast<void **>(&g_pinned), 2 * sizeof(uint32_t), hipHostMallocCoherent) !=
-                    hipSuccess ||
+            if (hipHostMalloc(reinterpret_cast<void **>(&g_pinned), kHostWords * sizeof(uint32_t),
+                              hipHostMallocCoherent) != hipSuccess ||
                 hipHostGetDevicePointer(reinterpret_cast<void **>(&g_pinned_dev), g_pinned, 0) != hipSuccess)
                 return fail(GSR_ERR_ALLOCATION, "pinned host allocation failed");
-            g_pinned[1] = 0u;
+            for (int k = 0; k < kHostWords; k++) g_pinned[k] = 0u;
         }
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevicesK)
-            return fail(GSR_ERR_DEVICE, "no current device");
         if (!g_k_ready[dev] && hipEventCreateWithFlags(&g_k_ready[dev], hipEventDisableTiming) != hipSuccess)
             return fail(GSR_ERR_DEVICE, "event creation failed");
         // deferred K: no event -- its marker packet cost a ~7 us gap before the first sort pass;
-        // the host polls the pinned word the upsweep stores instead (read_K)
+        // the host polls the pinned word the upsweep / column scan stores instead (read_K)
         k_ready = (defer && GSR_K_POLL) ? nullptr : g_k_ready[dev];
-        __atomic_store_n(g_pinned, kKPending, __ATOMIC_SEQ_CST);
+        __atomic_store_n(&g_pinned[kHostK], kKPending, __ATOMIC_SEQ_CST);
     }
-    {
-        StageTimer st(1, s);
-        launch_depth_sort(P, gs, g_pinned_dev, g_pinned_dev + 1, s, k_ready);
+    const FrameWords fw_local{dsort_K_word(gs), dsort_maxsb_word(gs), g_pinned_dev};
+    const FrameWords fw_none{nullptr, nullptr, nullptr};
+    if (local) {
+        {
+            StageTimer st(1, s);  // level-1 counts, SB bases, K
+            launch_binning_count(P, cam, gs, true, fw_local, s);
+            if (k_ready) (void)hipEventRecord(k_ready, s);
+        }
+        if ((rc = check("binning (counts)", debug, s))) return rc;
+    } else if (P > 0) {
+        {
+            StageTimer st(1, s);
+            launch_depth_sort(P, gs, g_pinned_dev + kHostK, g_pinned_dev + kHostErr, s, k_ready);
+        }
+        if ((rc = check("depth sort", debug, s))) return rc;
     }
-    if ((rc = check("depth sort", debug, s))) return rc;
     int64_t K = 0;
+    uint32_t maxsb = 0;
     bool have_K = P == 0;
     auto read_K = [&]() -> int {
         if (k_ready) {
             if (hipEventSynchronize(k_ready) != hipSuccess) return fail(GSR_ERR_DEVICE, "num_rendered wait failed");
         } else {
-            // the frame is queued; the upsweep's last workgroup stores K into the pinned word (it is
-            // normally there already: the host runs ahead of the GPU).  A drained stream with the
-            // word still pending falls through to the device copy below.
-            while (__atomic_load_n(g_pinned, __ATOMIC_SEQ_CST) == kKPending) {
+            // the frame is queued; the upsweep's (column scan's) last workgroup stores K into the
+            // pinned word (it is normally there already: the host runs ahead of the GPU).  A drained
+            // stream with the word still pending falls through to the device copy below.
+            while (__atomic_load_n(&g_pinned[kHostK], __ATOMIC_SEQ_CST) == kKPending) {
                 const hipError_t q = hipStreamQuery(s);
                 if (q == hipSuccess) break;
                 if (q != hipErrorNotReady) return fail(GSR_ERR_DEVICE, "num_rendered wait failed");
                 std::this_thread::yield();
             }
         }
-        uint32_t k = __atomic_load_n(g_pinned, __ATOMIC_SEQ_CST);
-        if (k == kKPending) {  // not expected: read the device copy instead
-            if (hipMemcpy(&k, dsort_K_word(gs), sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
+        uint32_t k = __atomic_load_n(&g_pinned[kHostK], __ATOMIC_ACQUIRE);
+        uint32_t m = __atomic_load_n(&g_pinned[kHostMaxSB], __ATOMIC_ACQUIRE);
+        if (k == kKPending) {  // not expected: read the device copies instead
+            if (hipMemcpy(&k, dsort_K_word(gs), sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess ||
+                hipMemcpy(&m, dsort_maxsb_word(gs), sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
                 return fail(GSR_ERR_DEVICE, "num_rendered copy failed");
         }
-        if (debug) {  // the sort passes are complete here (debug syncs after every stage)
+        if (debug && !local) {  // the sort passes are complete here (debug syncs after every stage)
             uint32_t err = 0;
             if (hipMemcpy(&err, dsort_err_word(gs), sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess || err)
                 return fail(GSR_ERR_DEVICE, "depth sort: a lookback spin timed out");
         }
         if ((rc = sticky_sort_error())) return rc;
         K = (int64_t)k;
+        maxsb = local ? m : 0u;
         have_K = true;
         return GSR_OK;
     };
-    if (P > 0 && !defer && (rc = read_K())) return rc;
+    // a local frame re-run through the global sort: the head control words (tickets, counters, K)
+    // start from zero again, the lookback status words are still zero (the local path never
+    // touches them)
+    auto to_global = [&]() -> int {
+        local = false;
+        g_fallbacks.fetch_add(1, std::memory_order_relaxed);
+        if (hipMemsetAsync(gs.ctrl, 0, sizeof(uint32_t) * (size_t)dsort_head_words(), s) != hipSuccess)
+            return fail(GSR_ERR_DEVICE, "depth sort control reset failed");
+        {
+            StageTimer st(1, s);
+            launch_depth_sort(P, gs, nullptr, g_pinned_dev + kHostErr, s, nullptr);
+        }
+        return check("depth sort", debug, s);
+    };
+    if (P > 0 && !defer) {
+        if ((rc = read_K())) return rc;
+        if (local && maxsb > (uint32_t)sort_cap() && (rc = to_global())) return rc;
+    }
     if (split && !GSR_COLOR_SERIAL && !color_early && (rc = fork_color())) return rc;
     bool joined = false;
-    auto bin_and_render = [&](int64_t cap) -> int {
+    auto bin_and_render = [&](int64_t cap, bool counted) -> int {
         size_t bbytes = 0;
         carve_binning(nullptr, cap, &bbytes);
         void *bbase = binning_buffer(resize_ctx, bbytes);
@@ -626,12 +673,13 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
         int r;
         {
             StageTimer st(2, s);
-            launch_binning_superblocks(P, cam, gs, bs, is, s);
+            if (!local && !counted) launch_binning_count(P, cam, gs, false, fw_none, s);
+            launch_binning_scatter(P, cam, gs, bs, local, s);
         }
         if ((r = check("binning (superblocks)", debug, s))) return r;
         {
             StageTimer st(3, s);
-            launch_binning_tiles(P, cam, gs, bs, is, s);
+            launch_binning_tiles(P, cam, gs, bs, is, local, dsort_maxsb_word(gs), s);
         }
         if ((r = check("binning (tiles)", debug, s))) return r;
         {
@@ -655,7 +703,7 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
         return check("render", debug, s);
     };
     const int64_t cap0 = defer ? g_khint[dev] : K;
-    if ((rc = bin_and_render(cap0))) return rc;
+    if ((rc = bin_and_render(cap0, false))) return rc;
     if (!have_K && (rc = read_K())) return rc;
     if (debug && P > 0) {  // the binning's instance total must be K (the kernels' capacity test is on K)
         uint32_t bi = 0;
@@ -664,14 +712,21 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
         if ((int64_t)bi != K) return fail(GSR_ERR_DEVICE, "binning: superblock instance total differs from K");
     }
     if (P > 0) g_frames.fetch_add(1, std::memory_order_relaxed);
-    if (K > cap0) {  // the capacity was short: again at K
+    if (local && maxsb > (uint32_t)sort_cap()) {
+        // an SB list too long for the LDS sort (the sort kernel wrote nothing): the frame again
+        // through the global depth sort, at the capacity it needs
+        if ((rc = to_global())) return rc;
+        if ((rc = bin_and_render(std::max(K, cap0), false))) return rc;
+    } else if (K > cap0) {  // the capacity was short: again at K
         g_reruns.fetch_add(1, std::memory_order_relaxed);
-        // sb_colscan's last-workgroup counter (a depth-sort control word the preprocess zeroes
-        // once per frame) must start from zero again
-        if (hipMemsetAsync(dsort_aux_word(gs), 0, sizeof(uint32_t), s) != hipSuccess)
+        // global sort: sb_colscan's last-workgroup counter (a depth-sort control word the
+        // preprocess zeroes once per frame) must start from zero again; local sort: the counts and
+        // SB bases stand, only the scatter and the LDS sort re-run
+        if (!local && hipMemsetAsync(dsort_aux_word(gs), 0, sizeof(uint32_t), s) != hipSuccess)
             return fail(GSR_ERR_DEVICE, "binning counter reset failed");
-        if ((rc = bin_and_render(K))) return rc;
+        if ((rc = bin_and_render(K, local))) return rc;
     }
+    if (P > 0 && local) g_local_frames.fetch_add(1, std::memory_order_relaxed);
     // the kernels compare K with a 32-bit capacity: keep the hint representable
     if (P > 0) {
         g_khist[dev][g_khead[dev]] = K;
@@ -730,9 +785,10 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
     const GeomState gs = carve_geom(geom_buffer, P, cam.gx, cam.gy, nullptr);
     const BinningState bs = carve_binning(binning_buffer, R_inst, nullptr);
     const ImageState is = carve_image(image_buffer, T, width * height, nullptr);
-    // a frame forwarded in deterministic mode has no cleared accumulators: its backward takes
-    // the record path whatever the mode is now
-    const bool atomic = g_deterministic.load(std::memory_order_relaxed) == 0 && uncleared != kDeterministicFwd;
+    // a frame's accumulation mode is the one in force at its forward: one forwarded in
+    // deterministic mode has no cleared accumulators (record path), one forwarded in atomic mode
+    // may have no record offsets (the local sort computes none)
+    const bool atomic = uncleared != kDeterministicFwd;
     size_t sbytes = 0;
     carve_bwd(nullptr, R_inst, P, atomic, &sbytes);
     // hierarchy cut: gradients of the R blended rows first, then scattered to the input rows
@@ -808,11 +864,16 @@ int gsr_set_true_scale_gradient(int enable) {
 
 int gsr_set_deterministic(int enable) { return g_deterministic.exchange(enable ? 1 : 0); }
 
+int gsr_set_binning(int mode) {
+    if (mode < 0 || mode > 1) return fail(GSR_ERR_INVALID_ARGUMENT, "gsr_set_binning: mode 0 or 1");
+    return g_binning_mode.exchange(mode);
+}
+
 int gsr_forward_stats(int64_t *out, int n) {
     if (!out || n < 0) return fail(GSR_ERR_INVALID_ARGUMENT, "NULL stats buffer");
-    const int64_t v[2] = {g_frames.load(), g_reruns.load()};
+    const int64_t v[4] = {g_frames.load(), g_reruns.load(), g_local_frames.load(), g_fallbacks.load()};
     int k = 0;
-    for (; k < n && k < 2; k++) out[k] = v[k];
+    for (; k < n && k < 4; k++) out[k] = v[k];
     return k;
 }
 

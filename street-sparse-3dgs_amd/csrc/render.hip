@@ -125,8 +125,14 @@ __device__ __forceinline__ void fwd_gather(const GRec *__restrict__ rec, uint32_
 // sub-blocks drop out of the cull mask at the next batch and an instance's culled sub-blocks are
 // skipped with scalar branches.  The list position comes from LDS with the instance (no scalar
 // bit scan and no SGPR->VGPR move per pixel).  Per-pixel arithmetic in the oracle's order.
+// GSR_FWD_POLY=1 evaluates the exponent as a quadratic in the pixel's offset from its sub-block's
+// centre (5 FMAs; ~3 us faster on the bench frame) -- off: its p2 differs from the backward's
+// replay (and the oracle's) by up to 3e-5, and the backward reconstructs T from final_T by
+// dividing out (1 - alpha) of every instance, so the forward and the replay must agree on alpha
+// bit for bit.  With the quadratic, near Gaussians clamped at alpha = 0.99 amplified the mismatch
+// into 1e-3 relative gradient errors (1536x1536 street frame, SH degree 1: means3D 3.5e-4 rel L2).
 #ifndef GSR_FWD_POLY
-#define GSR_FWD_POLY 1  // exponent as a quadratic in the sub-block-local pixel offset (5 FMAs)
+#define GSR_FWD_POLY 0
 #endif
 #ifndef GSR_FWD_MASKSEL
 #define GSR_FWD_MASKSEL 1

@@ -270,11 +270,21 @@ def set_deterministic(enable: bool) -> bool:
     return bool(_L.gsr_set_deterministic(int(bool(enable))))
 
 
+def set_binning(mode: int) -> int:
+    """Depth-order strategy (gsr_set_binning): 0 = local per-superblock sort where it applies
+    (default), 1 = always the global depth sort.  Process-wide; returns the previous mode."""
+    r = _L.gsr_set_binning(int(mode))
+    _check(0 if r >= 0 else r, "set_binning")
+    return r
+
+
 def forward_stats() -> dict:
-    """Frames rasterized since load and how many re-ran their binning at K (gsr_forward_stats)."""
-    buf = (ctypes.c_int64 * 2)()
-    n = _L.gsr_forward_stats(buf, 2)
-    return {"frames": int(buf[0]) if n > 0 else 0, "reruns": int(buf[1]) if n > 1 else 0}
+    """Frames rasterized since load, how many re-ran their binning at K, how many were binned by
+    the local sort and how many of those fell back to the global sort (gsr_forward_stats)."""
+    buf = (ctypes.c_int64 * 4)()
+    n = _L.gsr_forward_stats(buf, 4)
+    keys = ("frames", "reruns", "local_sort", "fallbacks")
+    return {k: (int(buf[i]) if n > i else 0) for i, k in enumerate(keys)}
 
 
 def frame_stats(geomBuffer, P, image_height, image_width) -> dict:

@@ -51,6 +51,7 @@ SIGNATURES = {
     "gsr_blend_stats": (_i, [ctypes.POINTER(_i64), _i, _i]),
     "gsr_set_true_scale_gradient": (_i, [_i]),
     "gsr_set_deterministic": (_i, [_i]),
+    "gsr_set_binning": (_i, [_i]),
     "gsr_abi_version": (_i, []),
     "gsr_last_error": (ctypes.c_char_p, []),
     "gsr_build_info": (ctypes.c_char_p, []),

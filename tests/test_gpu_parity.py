@@ -13,6 +13,8 @@ Bars (stated here, SURVEY.md 8 / BASELINE.json north_star):
 """
 from __future__ import annotations
 
+import contextlib
+
 import numpy as np
 import pytest
 
@@ -134,7 +136,7 @@ def check_record_offsets(S, vis, K):
         np.testing.assert_array_equal(off[1:], off[:-1] + n[:-1])
 
 
-def compare(c, st, g, h, check_grads=True):
+def compare(c, st, g, h, check_grads=True, global_sort=False):
     assert h["K"] == st["K"], f"K {h['K']} vs oracle {st['K']}"
     np.testing.assert_array_equal(h["radii"], st["radii"])
     S = h["state"]
@@ -142,14 +144,16 @@ def compare(c, st, g, h, check_grads=True):
     np.testing.assert_array_equal(S["keys"], st["keys"])
     np.testing.assert_array_equal(S["point_list"], st["point_list"])
     np.testing.assert_array_equal(S["ranges"], st["ranges"])
-    # the depth order itself: visible Gaussians by (depth bits, id), then the culled ones
     vis = (h["radii"] > 0) & (S["tiles_touched"] > 0)
-    nv = int(vis.sum())
-    ids = np.nonzero(vis)[0]
-    want = ids[np.lexsort((ids, S["depths"].view(np.uint32)[ids]))]
-    np.testing.assert_array_equal(S["order"][:nv], want)
-    np.testing.assert_array_equal(np.sort(S["order"][nv:]), np.nonzero(~vis)[0])
-    check_record_offsets(S, vis, h["K"])
+    if global_sort:
+        # the global depth order itself: visible Gaussians by (depth bits, id), then the culled
+        # ones; and the Gaussian-major record offsets its first pass writes
+        nv = int(vis.sum())
+        ids = np.nonzero(vis)[0]
+        want = ids[np.lexsort((ids, S["depths"].view(np.uint32)[ids]))]
+        np.testing.assert_array_equal(S["order"][:nv], want)
+        np.testing.assert_array_equal(np.sort(S["order"][nv:]), np.nonzero(~vis)[0])
+        check_record_offsets(S, vis, h["K"])
     # the raw (superblock-major) ranges partition [0, K) exactly
     r = S["ranges_raw"].astype(np.int64)
     o = np.argsort(r[:, 0], kind="stable")
@@ -187,14 +191,67 @@ def upstream_grads(c, seed=99):
             (rng.normal(size=(1, c["H"], c["W"])) / n * 1e3).astype(np.float32))
 
 
+@contextlib.contextmanager
+def binning_mode(mode):
+    """gsr_set_binning for the duration: 0 = local per-superblock sort (default), 1 = global sort."""
+    from diff_gaussian_rasterization import _C
+    prev = _C.set_binning(mode)
+    try:
+        yield
+    finally:
+        _C.set_binning(prev)
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1], ids=["local_sort", "global_sort"])
 @pytest.mark.parametrize("c", CASES, ids=[c["name"] for c in CASES])
-def test_parity_vs_oracle(c):
+def test_parity_vs_oracle(c, mode):
     s = make_scene(c)
     dcol, dinv = upstream_grads(c)
     st, g = run_oracle(s, c, dcol, dinv)
-    h = run_hip(s, c, dcol, dinv)
-    compare(c, st, g, h)
+    with binning_mode(mode):
+        h = run_hip(s, c, dcol, dinv)
+    compare(c, st, g, h, global_sort=mode == 1)
+
+
+@pytest.mark.gpu
+def test_local_sort_paths_and_fallback():
+    """The binning's two depth-order strategies give identical frames: a sparse frame is binned by
+    the local (per-superblock LDS) sort, a frame with a superblock list longer than the LDS sort
+    holds falls back to the global sort (gsr_forward_stats counts both), and both equal the forced
+    global sort bit for bit (image, inverse depth, radii, tile lists)."""
+    import torch
+    from diff_gaussian_rasterization import GaussianRasterizer, _C
+    dev = torch.device("cuda:0")
+    for c, expect_fallback in ((dict(name="sparse", P=20000, W=320, H=240, deg=3, seed=41, log_scale=-3.5), False),
+                               (dict(name="dense_sb", P=60000, W=160, H=96, deg=1, seed=42, log_scale=-3.5), True)):
+        s = make_scene(c)
+        outs = []
+        for mode in (0, 1):
+            with binning_mode(mode), torch.no_grad():
+                inp = torch_inputs(s, dev, requires_grad=False)
+                rs = settings(s, dev, c["deg"])
+                f0 = _C.forward_stats()
+                color, radii, invd = GaussianRasterizer(rs)(**inp)
+                e = torch.empty(0, device=dev)
+                raw = _C.rasterize_gaussians(rs.bg, inp["means3D"], e, inp["opacities"], inp["scales"],
+                                             inp["rotations"], 1.0, e, rs.viewmatrix, rs.projmatrix, rs.tanfovx,
+                                             rs.tanfovy, rs.image_height, rs.image_width, inp["shs"], c["deg"],
+                                             rs.campos, False, False, rs.render_indices, rs.parent_indices,
+                                             rs.interpolation_weights, rs.num_node_kids, True)
+                torch.cuda.synchronize()
+                f1 = _C.forward_stats()
+                st = decode_state(raw[4], raw[5], raw[6], c["P"], raw[0], s["W"], s["H"])
+                outs.append((color.cpu(), invd.cpu(), radii.cpu(), st["point_list"], st["ranges"]))
+                if mode == 0:
+                    assert f1["local_sort"] - f0["local_sort"] == (0 if expect_fallback else 2), (c["name"], f0, f1)
+                    assert f1["fallbacks"] - f0["fallbacks"] == (2 if expect_fallback else 0), (c["name"], f0, f1)
+                else:
+                    assert f1["local_sort"] == f0["local_sort"] and f1["fallbacks"] == f0["fallbacks"]
+        (a, b) = outs
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+        np.testing.assert_array_equal(a[3], b[3])
+        np.testing.assert_array_equal(a[4], b[4])
 
 
 @pytest.mark.gpu
@@ -357,7 +414,7 @@ def test_street_frame_1536_vs_oracle(deg, seed):
 
 @pytest.mark.gpu
 def test_depth_order_large():
-    """The depth sort at 3M Gaussians (367 sort tiles) with 25% culled: the order is the
+    """The global depth sort at 3M Gaussians (367 sort tiles) with 25% culled: the order is the
     stable (depth bits, id) order of the visible Gaussians, then the culled ones; the record
     offsets partition [0, K); K is the sum of tiles_touched."""
     import torch
@@ -368,7 +425,7 @@ def test_depth_order_large():
     inp = torch_inputs(s, dev)
     rs = settings(s, dev, 0)
     e = torch.empty(0, device=dev)
-    with torch.no_grad():
+    with torch.no_grad(), binning_mode(1):  # the global depth sort's own outputs (order, offsets)
         raw = _C.rasterize_gaussians(rs.bg, inp["means3D"], e, inp["opacities"], inp["scales"], inp["rotations"], 1.0,
                                      e, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height,
                                      rs.image_width, inp["shs"], 0, rs.campos, False, False, rs.render_indices,
