@@ -170,6 +170,15 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t *w
     return before + incl - v;
 }
 
+#ifndef GSR_SORT_CAP
+#define GSR_SORT_CAP 8192
+#endif
+constexpr int kSBThreads = 1024;
+constexpr int kSBWaves = kSBThreads / 64;
+constexpr int kSortCap = GSR_SORT_CAP;            // longest SB list the local sort holds in LDS
+constexpr int kSBItems = kSortCap / kSBThreads;   // keys per thread
+static_assert(kSortCap % kSBThreads == 0 && kSortCap <= 65536, "kSortCap: a multiple of 1024, 16-bit positions");
+
 // Level 1, pass 2: per SB, exclusive scan of the Gaussian counts over chunks (in place) and the
 // SB totals of Gaussians and instances; the last workgroup to finish (a per-frame counter in the
 // depth sort's zeroed control words) turns the totals into exclusive SB bases, base[nsb] = the
@@ -239,7 +248,10 @@ __global__ __launch_bounds__(kColThreads) void sb_colscan_kernel(SBGrid sg, uint
         __syncthreads();
         if (threadIdx.x == 0) {
             for (int k = 1; k < kColThreads / 64; k++) mg = max(mg, wsum[k]);
-            *fw.dev_K = ci;
+            // an SB list too long for the local sort: the device K word reads "capacity short" to
+            // every later kernel of the frame (they exit at once; the host re-runs the frame
+            // through the global sort, which stores the real K there again)
+            *fw.dev_K = mg > (uint32_t)kSortCap ? 0xFFFFFFFFu : ci;
             *fw.dev_maxsb = mg;
             if (fw.host) {
                 __hip_atomic_store(&fw.host[kHostMaxSB], mg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -559,14 +571,6 @@ __global__ __launch_bounds__(64 * kTBWaves) void tile_bin_kernel(SBGrid sg, int 
 // 3. The sorted (id, footprint) pairs, gathered once from the SB list into LDS, then tile_bin's
 //    two ballot passes (per-wave tile counts, tile bases and ranges, stable placement) over them.
 // ---------------------------------------------------------------------------------------------
-#ifndef GSR_SORT_CAP
-#define GSR_SORT_CAP 8192
-#endif
-constexpr int kSBThreads = 1024;
-constexpr int kSBWaves = kSBThreads / 64;
-constexpr int kSortCap = GSR_SORT_CAP;            // longest SB list sorted in LDS
-constexpr int kSBItems = kSortCap / kSBThreads;   // keys per thread
-static_assert(kSortCap % kSBThreads == 0 && kSortCap <= 65536, "kSortCap: a multiple of 1024, 16-bit positions");
 
 __device__ __forceinline__ uint32_t lanes_with_digit(uint32_t d, uint64_t valid) {
     uint64_t m = valid;

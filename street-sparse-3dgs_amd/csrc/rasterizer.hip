@@ -626,8 +626,10 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
         }
         uint32_t k = __atomic_load_n(&g_pinned[kHostK], __ATOMIC_ACQUIRE);
         uint32_t m = __atomic_load_n(&g_pinned[kHostMaxSB], __ATOMIC_ACQUIRE);
-        if (k == kKPending) {  // not expected: read the device copies instead
-            if (hipMemcpy(&k, dsort_K_word(gs), sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess ||
+        if (k == kKPending) {  // not expected: read the device copies instead (a local frame's K
+                               // word may read "capacity short": its instance total is K)
+            const uint32_t *kw = local ? gs.sb_base_i + gs.sb.nsb : dsort_K_word(gs);
+            if (hipMemcpy(&k, kw, sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess ||
                 hipMemcpy(&m, dsort_maxsb_word(gs), sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
                 return fail(GSR_ERR_DEVICE, "num_rendered copy failed");
         }
