@@ -572,7 +572,7 @@ __global__ __launch_bounds__(64 * kTBWaves) void tile_bin_kernel(SBGrid sg, int 
 //    two ballot passes (per-wave tile counts, tile bases and ranges, stable placement) over them.
 // ---------------------------------------------------------------------------------------------
 
-__device__ __forceinline__ uint32_t lanes_with_digit(uint32_t d, uint64_t valid) {
+__device__ __forceinline__ uint64_t lanes_with_digit(uint32_t d, uint64_t valid) {
     uint64_t m = valid;
 #pragma unroll
     for (int b = 0; b < 8; b++) {
