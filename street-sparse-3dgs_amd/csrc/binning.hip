@@ -731,7 +731,7 @@ __global__ __launch_bounds__(kSBThreads) void sb_sort_bin_kernel(SBGrid sg, int 
     for (int k = 0; k < kSBItems; k++) {
         const uint32_t e = (uint32_t)(wb + k * 64 + lane);
         if (e < n) {
-            const uint2 v = sblist[L0 + pos[k]];
+            const uint2 v = sblist[L0 + min((uint32_t)pos[k], n - 1u)];  // (a permutation of [0, n))
             s_id[e] = v.x;
             s_fp[e] = v.y;
         }
