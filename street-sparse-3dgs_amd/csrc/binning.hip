@@ -291,6 +291,8 @@ __global__ __launch_bounds__(64 * kScatterWaves) void sb_scatter_kernel(int P, S
                                                                          const uint32_t *__restrict__ col,
                                                                          const uint32_t *__restrict__ base_g,
                                                                          uint2 *__restrict__ sblist,
+                                                                         uint4 *__restrict__ sblist4,
+                                                                         const uint32_t *__restrict__ dkey,
                                                                          const uint32_t *__restrict__ kdev, uint32_t cap) {
     // the point-list capacity is short: the host re-runs at K (SB instances <= K, so K <= cap
     // bounds the level-1 lists too; the same test as every other binning / render kernel)
@@ -347,13 +349,17 @@ __global__ __launch_bounds__(64 * kScatterWaves) void sb_scatter_kernel(int P, S
     }
     __syncthreads();
 
+    // local sort (sblist4): index order, and each entry carries the Gaussian's depth key (read
+    // here in index order, coalesced -- the sort kernel would otherwise gather it per entry)
     const auto id_at = [&](int j) { return j < jw1 ? (order ? order[j] : (uint32_t)j) : 0u; };
-    uint32_t gnext = id_at(jw0 + lane);
+    const auto key_at = [&](int j) { return (sblist4 && j < jw1) ? dkey[j] : 0u; };
+    uint32_t gnext = id_at(jw0 + lane), knext = key_at(jw0 + lane);
     rnext = rect_at(jw0 + lane);
     for (int jb = jw0; jb < jw1; jb += 64) {
-        const uint32_t g = gnext;
+        const uint32_t g = gnext, gk = knext;
         const TileRect r = unpack_rect(rnext);  // (0, 0) past the end: no tiles
         gnext = id_at(jb + 64 + lane);
+        knext = key_at(jb + 64 + lane);
         rnext = rect_at(jb + 64 + lane);
         const SBFoot f = sb_foot(r, sg.shift);
         const bool small = f.n <= kSmallSB;
@@ -373,16 +379,24 @@ __global__ __launch_bounds__(64 * kScatterWaves) void sb_scatter_kernel(int P, S
         for (int k = 0; k < kSmallSB; k++)
             if (small && k < f.n) {
                 const uint32_t key = sb_key(f, k, sg.nsbx);
-                sblist[run[key] + (uint32_t)__popcll(mask_load(&msk[key]) & lt)] = make_uint2(g, sb_local(r, key, sg));
+                const uint32_t at = run[key] + (uint32_t)__popcll(mask_load(&msk[key]) & lt);
+                if (sblist4)
+                    sblist4[at] = make_uint4(g, sb_local(r, key, sg), gk, 0u);
+                else
+                    sblist[at] = make_uint2(g, sb_local(r, key, sg));
             }
         for (uint64_t big = bigs; big; big &= big - 1) {
             const int b = __ffsll((unsigned long long)big) - 1;
             const SBFoot fb = lane_foot(f, b);
             const TileRect rb = lane_rect(r, b);
-            const uint32_t gb = (uint32_t)rl((int)g, b);
+            const uint32_t gb = (uint32_t)rl((int)g, b), gkb = (uint32_t)rl((int)gk, b);
             for (int k = lane; k < fb.n; k += 64) {
                 const uint32_t key = sb_key(fb, k, sg.nsbx);
-                sblist[run[key] + (uint32_t)__popcll(mask_load(&msk[key]) & ((1ull << b) - 1ull))] = make_uint2(gb, sb_local(rb, key, sg));
+                const uint32_t at = run[key] + (uint32_t)__popcll(mask_load(&msk[key]) & ((1ull << b) - 1ull));
+                if (sblist4)
+                    sblist4[at] = make_uint4(gb, sb_local(rb, key, sg), gkb, 0u);
+                else
+                    sblist[at] = make_uint2(gb, sb_local(rb, key, sg));
             }
         }
         // 3. the highest lane of every mask advances the SB position and clears the mask
@@ -561,7 +575,7 @@ __global__ __launch_bounds__(64 * kTBWaves) void tile_bin_kernel(SBGrid sg, int 
 // in LDS and bins it into the SB's tiles -- the global depth sort's job, per SB and without a pass
 // over global memory per digit.
 //
-// 1. Load: entry e's depth key (a gather of the Gaussian's key, dsort's key array) into registers,
+// 1. Load: entry e's depth key (stored with the entry by the index-order scatter) into registers,
 //    wave-striped so that (wave, item, lane) order is list order; the list's key range by a block
 //    min / max.
 // 2. Stable LSD radix over (key - min) in 8-bit digits, only as many passes as the range needs
@@ -586,8 +600,7 @@ __device__ __forceinline__ uint64_t lanes_with_digit(uint32_t d, uint64_t valid)
 __global__ __launch_bounds__(kSBThreads) void sb_sort_bin_kernel(SBGrid sg, int gx, int gy,
                                                                 const uint32_t *__restrict__ base_g,
                                                                 const uint32_t *__restrict__ base_i,
-                                                                const uint2 *__restrict__ sblist,
-                                                                const uint32_t *__restrict__ dkey,
+                                                                const uint4 *__restrict__ sblist,
                                                                 uint32_t *__restrict__ point_list,
                                                                 uint2 *__restrict__ ranges,
                                                                 const uint32_t *__restrict__ kdev, uint32_t cap,
@@ -617,17 +630,11 @@ __global__ __launch_bounds__(kSBThreads) void sb_sort_bin_kernel(SBGrid sg, int 
     uint32_t key[kSBItems];
     uint16_t pos[kSBItems];
     {
-        uint32_t id[kSBItems];
-#pragma unroll
-        for (int k = 0; k < kSBItems; k++) {
-            const uint32_t e = (uint32_t)(wb + k * 64 + lane);
-            id[k] = e < n ? sblist[L0 + e].x : 0u;
-        }
         uint32_t lo = 0xFFFFFFFFu, hi = 0u;
 #pragma unroll
         for (int k = 0; k < kSBItems; k++) {
             const uint32_t e = (uint32_t)(wb + k * 64 + lane);
-            key[k] = e < n ? dkey[id[k]] : 0u;
+            key[k] = e < n ? sblist[L0 + e].z : 0u;  // the depth key the scatter stored with the entry
             pos[k] = (uint16_t)e;
             if (e < n) {
                 lo = min(lo, key[k]);
@@ -731,8 +738,8 @@ __global__ __launch_bounds__(kSBThreads) void sb_sort_bin_kernel(SBGrid sg, int 
     for (int k = 0; k < kSBItems; k++) {
         const uint32_t e = (uint32_t)(wb + k * 64 + lane);
         if (e < n) {
-            const uint2 v = sblist[L0 + min((uint32_t)pos[k], n - 1u)];  // (a permutation of [0, n))
-            s_id[e] = v.x;
+            const uint2 v = reinterpret_cast<const uint2 *>(sblist + L0 + min((uint32_t)pos[k], n - 1u))[0];
+            s_id[e] = v.x;  // (pos: a permutation of [0, n))
             s_fp[e] = v.y;
         }
     }
@@ -858,7 +865,7 @@ void launch_binning_scatter(int P, const Camera &cam, const GeomState &gs, const
     const uint32_t *rects4 = index_order ? gs.rect4 : drect4_of(gs);
     hipLaunchKernelGGL(sb_scatter_kernel, dim3(sg.nchunks), dim3(64 * kScatterWaves), l3, s, P, sg,
                        index_order ? (const uint32_t *)nullptr : gs.order, rects, rects4, gs.sb_cnt_g, gs.sb_base_g,
-                       bs.sblist, bs.kdev, bs.cap);
+                       bs.sblist, index_order ? bs.sblist4 : (uint4 *)nullptr, gs.dkey, bs.kdev, bs.cap);
 }
 
 void launch_binning_tiles(int P, const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
@@ -872,7 +879,7 @@ void launch_binning_tiles(int P, const Camera &cam, const GeomState &gs, const B
     }
     if (local_sort) {
         hipLaunchKernelGGL(sb_sort_bin_kernel, dim3(sg.nsb), dim3(kSBThreads), 0, s, sg, cam.gx, cam.gy, gs.sb_base_g,
-                           gs.sb_base_i, bs.sblist, gs.dkey, bs.point_list, is.ranges, bs.kdev, bs.cap, maxsb);
+                           gs.sb_base_i, bs.sblist4, bs.point_list, is.ranges, bs.kdev, bs.cap, maxsb);
         return;
     }
     // long superblock lists (large P): more waves per superblock, the 510-ish workgroups of a

@@ -499,6 +499,7 @@ struct FrameWords {
 
 struct BinningState {       // per tile instance
     uint2 *sblist;          // level 1: (Gaussian id, footprint in SB-local tiles) per superblock, depth order
+    uint4 *sblist4;         // the same memory on the local-sort path: (id, footprint, depth key, 0), id order
     uint32_t *point_list;   // Gaussian ids, per tile contiguous in (depth, id) order; tiles SB-major
     uint32_t cap;           // entries carved for sblist and point_list
     const uint32_t *kdev;   // the frame's K on the device (forward): kernels exit if K > cap

@@ -208,7 +208,10 @@ BinningState carve_binning(void *base, int64_t K, size_t *bytes) {
     Carver c(base);
     BinningState b;
     b.point_list = c.take<uint32_t>(K);
-    b.sblist = c.take<uint2>(K);
+    // level-1 entries: 8 B (id, footprint) on the global-sort path, 16 B (id, footprint, depth key,
+    // -) on the local-sort path -- carved for the larger
+    b.sblist4 = c.take<uint4>(K);
+    b.sblist = reinterpret_cast<uint2 *>(b.sblist4);
     b.cap = (uint32_t)K;
     b.kdev = nullptr;
     if (bytes) *bytes = align_up(c.off, 256);
@@ -536,11 +539,11 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
     // persistent grid of GSR_COLOR_LOCAL_BLOCKS blocks beside the binning.
     int color_blocks = 0;
     bool color_early = GSR_COLOR_FORK == 0;
-    if (GSR_COLOR_FORK == 2 && split && !GSR_COLOR_SERIAL) {
-        if (local) {
-            color_early = true;
-            color_blocks = GSR_COLOR_LOCAL_BLOCKS;
-        } else {
+    if (local && split && !GSR_COLOR_SERIAL) {
+        color_early = GSR_COLOR_FORK != 1;  // 1: after the level-1 counts, beside the scatter and the sort
+        color_blocks = GSR_COLOR_LOCAL_BLOCKS;
+    } else if (GSR_COLOR_FORK == 2 && split && !GSR_COLOR_SERIAL) {
+        {
             // workgroups are dealt round-robin over the 8 XCDs: leave every XCD room for its share
             // of the sort's workgroups (123 of them -> 16 per XCD -> 8 x (32 - 16) = 128 colour blocks)
             const int per_xcd = device_cus() / 8;

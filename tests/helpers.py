@@ -33,7 +33,7 @@ def geom_layout(P):
 
 def binning_layout(K, T):
     # point_list first (csrc/rasterizer.hip carve_binning): the forward may carve a larger capacity
-    return carve([("point_list", 4 * K), ("sblist", 8 * K)])
+    return carve([("point_list", 4 * K), ("sblist", 16 * K)])
 
 
 def image_layout(T, npix):
