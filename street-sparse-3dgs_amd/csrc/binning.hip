@@ -608,8 +608,10 @@ __global__ __launch_bounds__(kSBThreads) void sb_sort_bin_kernel(SBGrid sg, int 
     // capacity short (the host re-runs at K) or an SB list the LDS cannot hold (the host re-runs
     // the frame through the global depth sort): nothing is written
     if (*kdev > cap || *maxsb > (uint32_t)kSortCap) return;
-    __shared__ uint32_t s_key[2][kSortCap];
-    __shared__ uint16_t s_pos[2][kSortCap];
+    // one key / position buffer: each pass scatters into it after every thread has its elements in
+    // registers (65 KiB of LDS in all: two workgroups per CU)
+    __shared__ uint32_t s_key[kSortCap];
+    __shared__ uint16_t s_pos[kSortCap];
     __shared__ uint32_t s_wh[kSBWaves][256];  // per-wave digit counts; later the per-wave tile counters
     __shared__ uint32_t s_bex[256];
     __shared__ uint32_t s_lo, s_hi;
@@ -658,8 +660,7 @@ __global__ __launch_bounds__(kSBThreads) void sb_sort_bin_kernel(SBGrid sg, int 
 #pragma unroll
     for (int k = 0; k < kSBItems; k++) key[k] -= klo;  // padding keys wrap: never ranked (valid mask)
 
-    // 2. stable LSD passes; the sorted positions end in s_pos[cur]
-    int cur = 0;
+    // 2. stable LSD passes; the sorted list positions end in s_pos (and in pos[] by striped slot)
     for (int p = 0; p < passes; p++) {
         const int shift = 8 * p;
         uint32_t rk[kSBItems];
@@ -705,15 +706,14 @@ __global__ __launch_bounds__(kSBThreads) void sb_sort_bin_kernel(SBGrid sg, int 
             a[4 * lane + 2] = e + x0 + x1;
             a[4 * lane + 3] = e + x0 + x1 + x2;
         }
-        __syncthreads();
-        const int nxt = cur ^ 1;
+        __syncthreads();  // (every element of the last pass is back in registers: the buffer is free)
 #pragma unroll
         for (int k = 0; k < kSBItems; k++) {
             if ((uint32_t)(wb + k * 64 + lane) < n) {
                 const uint32_t d = (key[k] >> shift) & 0xFFu;
                 const uint32_t dst = s_bex[d] + s_wh[w][d] + rk[k];
-                s_key[nxt][dst] = key[k];
-                s_pos[nxt][dst] = pos[k];
+                s_key[dst] = key[k];
+                s_pos[dst] = pos[k];
             }
         }
         __syncthreads();
@@ -722,25 +722,25 @@ __global__ __launch_bounds__(kSBThreads) void sb_sort_bin_kernel(SBGrid sg, int 
         for (int k = 0; k < kSBItems; k++) {
             const uint32_t e = (uint32_t)(wb + k * 64 + lane);
             if (e < n) {
-                key[k] = s_key[nxt][e];
-                pos[k] = s_pos[nxt][e];
+                key[k] = s_key[e];
+                pos[k] = s_pos[e];
             }
         }
-        cur = nxt;
         // s_wh cleared and this pass's reads done before the next pass ranks and scatters
         __syncthreads();
     }
 
-    // 3. the sorted (id, footprint) pairs into LDS (the key buffers are free): sorted position e
-    // is held by the thread that owns e in the striped layout -- its pos[] after the last pass
-    uint32_t *s_id = s_key[0], *s_fp = s_key[1];
+    // 3. the sorted footprints into LDS (the key buffer is free) and the sorted list positions (in
+    // s_pos already after a pass): sorted position e is held by the thread that owns e in the
+    // striped layout -- its pos[] after the last pass.  Pass B gathers the ids through s_pos.
+    uint32_t *s_fp = s_key;
 #pragma unroll
     for (int k = 0; k < kSBItems; k++) {
         const uint32_t e = (uint32_t)(wb + k * 64 + lane);
         if (e < n) {
-            const uint2 v = reinterpret_cast<const uint2 *>(sblist + L0 + min((uint32_t)pos[k], n - 1u))[0];
-            s_id[e] = v.x;  // (pos: a permutation of [0, n))
-            s_fp[e] = v.y;
+            const uint32_t pk = min((uint32_t)pos[k], n - 1u);  // (pos: a permutation of [0, n))
+            s_fp[e] = sblist[L0 + pk].y;
+            if (passes == 0) s_pos[e] = (uint16_t)pk;
         }
     }
     __syncthreads();
@@ -800,7 +800,7 @@ __global__ __launch_bounds__(kSBThreads) void sb_sort_bin_kernel(SBGrid sg, int 
             const uint32_t i = gb + (uint32_t)lane;
             const bool in = i < seg1;
             const uint32_t m = in ? group_mask(s_fp[i], tg, sg.shift) : 0u;
-            const uint32_t g = in ? s_id[i] : 0u;
+            const uint32_t g = m ? sblist[L0 + s_pos[i]].x : 0u;
 #pragma unroll
             for (int k = 0; k < kTileGroup; k++) {
                 const bool hit = (m >> k) & 1u;
