@@ -178,6 +178,11 @@ int gsr_frame_stats(const void *geom_buffer, int P, int width, int height, int64
  * lanes}, backward tiles.  reset != 0 zeroes them after the read.  Returns the count written. */
 int gsr_blend_stats(int64_t *out, int n, int reset);
 
+/* Measurement builds only (-DGSR_SB_TRACE=1; zeros otherwise): per-workgroup phase stamps of the
+ * local sort kernel, 8 words per superblock (s_memrealtime at 100 MHz; word 7 = list length).
+ * reset != 0 zeroes them after the read.  Returns the count written. */
+int gsr_debug_trace(int64_t *out, int n, int reset);
+
 /* Version / diagnostics. */
 int gsr_abi_version(void);
 const char *gsr_last_error(void);

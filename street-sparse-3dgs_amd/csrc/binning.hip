@@ -597,6 +597,20 @@ __device__ __forceinline__ uint64_t lanes_with_digit(uint32_t d, uint64_t valid)
     return m;
 }
 
+// Measurement builds only (GSR_SB_TRACE=1): per-workgroup phase stamps (s_memrealtime, 100 MHz)
+// of sb_sort_bin, read back with gsr_debug_trace.
+#ifndef GSR_SB_TRACE
+#define GSR_SB_TRACE 0
+#endif
+__device__ unsigned long long g_sb_trace[2048 * 8];
+#define SB_STAMP(slot)                                                                         \
+    do {                                                                                       \
+        if (GSR_SB_TRACE && threadIdx.x == 0 && blockIdx.x < 2048) {                           \
+            __builtin_amdgcn_s_waitcnt(0);                                                     \
+            g_sb_trace[blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime();            \
+        }                                                                                      \
+    } while (0)
+
 __global__ __launch_bounds__(kSBThreads) void sb_sort_bin_kernel(SBGrid sg, int gx, int gy,
                                                                 const uint32_t *__restrict__ base_g,
                                                                 const uint32_t *__restrict__ base_i,
@@ -622,6 +636,8 @@ __global__ __launch_bounds__(kSBThreads) void sb_sort_bin_kernel(SBGrid sg, int 
     const uint32_t L0 = base_g[s], n = base_g[s + 1] - L0;
     const uint64_t lt = (1ull << lane) - 1ull;
     const int wb = w * kSBItems * 64;  // the wave's first list position
+    SB_STAMP(0);
+    if (GSR_SB_TRACE && t == 0) g_sb_trace[min(blockIdx.x, 2047u) * 8 + 7] = n;
 
     // 1. keys and their range
     if (t == 0) {
@@ -657,6 +673,7 @@ __global__ __launch_bounds__(kSBThreads) void sb_sort_bin_kernel(SBGrid sg, int 
     __syncthreads();
     const uint32_t klo = s_lo, range = s_lo <= s_hi ? s_hi - s_lo : 0u;
     const int passes = range ? (32 - __clz((int)range) + 7) / 8 : 0;
+    SB_STAMP(1);
 #pragma unroll
     for (int k = 0; k < kSBItems; k++) key[k] -= klo;  // padding keys wrap: never ranked (valid mask)
 
@@ -730,6 +747,7 @@ __global__ __launch_bounds__(kSBThreads) void sb_sort_bin_kernel(SBGrid sg, int 
         __syncthreads();
     }
 
+    SB_STAMP(2);
     // 3. the sorted footprints into LDS (the key buffer is free) and the sorted list positions (in
     // s_pos already after a pass): sorted position e is held by the thread that owns e in the
     // striped layout -- its pos[] after the last pass.  Pass B gathers the ids through s_pos.
@@ -745,6 +763,7 @@ __global__ __launch_bounds__(kSBThreads) void sb_sort_bin_kernel(SBGrid sg, int 
     }
     __syncthreads();
 
+    SB_STAMP(3);
     // tile binning over the sorted list (tile_bin's passes, entries from LDS): wave w owns the
     // contiguous segment [seg0, seg1)
     uint32_t(*tc)[256] = s_wh;
@@ -792,6 +811,7 @@ __global__ __launch_bounds__(kSBThreads) void sb_sort_bin_kernel(SBGrid sg, int 
         }
     }
     __syncthreads();
+    SB_STAMP(4);
     for (int tg = 0; tg < tps; tg += kTileGroup) {
         uint32_t pk[kTileGroup];
 #pragma unroll
@@ -810,11 +830,26 @@ __global__ __launch_bounds__(kSBThreads) void sb_sort_bin_kernel(SBGrid sg, int 
             }
         }
     }
+    __syncthreads();
+    SB_STAMP(5);
 }
 
 }  // namespace
 
 int sort_cap() { return kSortCap; }
+
+int debug_trace(int64_t *out, int n, int reset) {
+    static unsigned long long v[2048 * 8];
+    if (!out || n < 0) return -1;
+    if (hipMemcpyFromSymbol(v, HIP_SYMBOL(g_sb_trace), sizeof(v)) != hipSuccess) return -3;
+    if (reset) {
+        static const unsigned long long z[2048 * 8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_sb_trace), z, sizeof(z)) != hipSuccess) return -3;
+    }
+    int k = 0;
+    for (; k < n && k < 2048 * 8; k++) out[k] = (int64_t)v[k];
+    return k;
+}
 
 SBGrid sb_grid(int gx, int gy, int P) {
     SBGrid g;

@@ -68,6 +68,7 @@ int dsort_head_words();
 SBGrid sb_grid(int gx, int gy, int P);
 bool sb_grid_supported(const SBGrid &g);
 int sort_cap();  // the longest SB list the local sort holds
+int debug_trace(int64_t *out, int n, int reset);  // GSR_SB_TRACE builds: sb_sort_bin phase stamps
 // level-1 counts and SB bases; with fw.dev_K set (local sort) the column scan also stores K, the
 // longest SB list and the level-1 total (FrameWords)
 void launch_binning_count(int P, const Camera &cam, const GeomState &gs, bool index_order, const FrameWords &fw,

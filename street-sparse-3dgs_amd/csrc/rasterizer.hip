@@ -901,6 +901,8 @@ int gsr_frame_stats(const void *geom_buffer, int P, int width, int height, int64
     return k;
 }
 
+int gsr_debug_trace(int64_t *out, int n, int reset) { return gsr::debug_trace(out, n, reset); }
+
 int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,
                      uint8_t *present, void *stream) {
     (void)projmatrix;

@@ -49,6 +49,7 @@ SIGNATURES = {
     "gsr_forward_stats": (_i, [ctypes.POINTER(_i64), _i]),
     "gsr_frame_stats": (_i, [_vp, _i, _i, _i, ctypes.POINTER(_i64), _i]),
     "gsr_blend_stats": (_i, [ctypes.POINTER(_i64), _i, _i]),
+    "gsr_debug_trace": (_i, [ctypes.POINTER(_i64), _i, _i]),
     "gsr_set_true_scale_gradient": (_i, [_i]),
     "gsr_set_deterministic": (_i, [_i]),
     "gsr_set_binning": (_i, [_i]),
