@@ -611,7 +611,10 @@ __device__ unsigned long long g_sb_trace[2048 * 8];
         }                                                                                      \
     } while (0)
 
-__global__ __launch_bounds__(kSBThreads) void sb_sort_bin_kernel(SBGrid sg, int gx, int gy,
+// __launch_bounds__(1024, 8): registers budgeted for 8 waves per SIMD -- two 1024-thread
+// workgroups per CU (66 KiB of LDS each); at the compiler's default (7 waves per SIMD, 104 SGPRs)
+// only one fit and the 510 superblocks of a 1080p frame ran in two rounds
+__global__ __launch_bounds__(kSBThreads, 8) void sb_sort_bin_kernel(SBGrid sg, int gx, int gy,
                                                                 const uint32_t *__restrict__ base_g,
                                                                 const uint32_t *__restrict__ base_i,
                                                                 const uint4 *__restrict__ sblist,
@@ -748,33 +751,34 @@ __global__ __launch_bounds__(kSBThreads) void sb_sort_bin_kernel(SBGrid sg, int 
     }
 
     SB_STAMP(2);
-    // 3. the sorted footprints into LDS (the key buffer is free) and the sorted list positions (in
-    // s_pos already after a pass): sorted position e is held by the thread that owns e in the
-    // striped layout -- its pos[] after the last pass.  Pass B gathers the ids through s_pos.
-    uint32_t *s_fp = s_key;
+    // 3. the sorted (id, footprint) pairs into registers: sorted position e = wb + 64 k + lane is
+    // held by that lane as item k (pos[] after the last pass), so the wave's tile binning below runs
+    // over its own 512 consecutive sorted positions with no LDS and no further gathers
+    uint32_t gid[kSBItems], gfp[kSBItems];
 #pragma unroll
     for (int k = 0; k < kSBItems; k++) {
         const uint32_t e = (uint32_t)(wb + k * 64 + lane);
+        gid[k] = 0u;
+        gfp[k] = 0xFFu;  // padding: an empty footprint (x1 < x0)
         if (e < n) {
-            const uint32_t pk = min((uint32_t)pos[k], n - 1u);  // (pos: a permutation of [0, n))
-            s_fp[e] = sblist[L0 + pk].y;
-            if (passes == 0) s_pos[e] = (uint16_t)pk;
+            const uint2 v = reinterpret_cast<const uint2 *>(sblist + L0 + min((uint32_t)pos[k], n - 1u))[0];
+            gid[k] = v.x;  // (pos: a permutation of [0, n))
+            gfp[k] = v.y;
         }
     }
-    __syncthreads();
-
     SB_STAMP(3);
-    // tile binning over the sorted list (tile_bin's passes, entries from LDS): wave w owns the
-    // contiguous segment [seg0, seg1)
+    // tile binning over the sorted list (tile_bin's two ballot passes): wave w owns sorted
+    // positions [wb, wb + 512), batch k = its item k
     uint32_t(*tc)[256] = s_wh;
-    const uint32_t seg0 = (uint32_t)(((uint64_t)n * w) / kSBWaves), seg1 = (uint32_t)(((uint64_t)n * (w + 1)) / kSBWaves);
+    const int kmax = wb >= (int)n ? 0 : min(kSBItems, ((int)n - wb + 63) / 64);  // the wave's non-empty items
     for (int tg = 0; tg < tps; tg += kTileGroup) {
         uint32_t cnt[kTileGroup];
 #pragma unroll
         for (int k = 0; k < kTileGroup; k++) cnt[k] = 0u;
-        for (uint32_t gb = seg0; gb < seg1; gb += 64) {
-            const uint32_t i = gb + (uint32_t)lane;
-            const uint32_t m = i < seg1 ? group_mask(s_fp[i], tg, sg.shift) : 0u;
+#pragma unroll
+        for (int b = 0; b < kSBItems; b++) {
+            if (b >= kmax) break;
+            const uint32_t m = group_mask(gfp[b], tg, sg.shift);
 #pragma unroll
             for (int k = 0; k < kTileGroup; k++) cnt[k] += (uint32_t)__popcll(__ballot((m >> k) & 1u));
         }
@@ -816,16 +820,15 @@ __global__ __launch_bounds__(kSBThreads) void sb_sort_bin_kernel(SBGrid sg, int 
         uint32_t pk[kTileGroup];
 #pragma unroll
         for (int k = 0; k < kTileGroup; k++) pk[k] = tg + k < tps ? tc[w][tg + k] : 0u;
-        for (uint32_t gb = seg0; gb < seg1; gb += 64) {
-            const uint32_t i = gb + (uint32_t)lane;
-            const bool in = i < seg1;
-            const uint32_t m = in ? group_mask(s_fp[i], tg, sg.shift) : 0u;
-            const uint32_t g = m ? sblist[L0 + s_pos[i]].x : 0u;
+#pragma unroll
+        for (int b = 0; b < kSBItems; b++) {
+            if (b >= kmax) break;
+            const uint32_t m = group_mask(gfp[b], tg, sg.shift);
 #pragma unroll
             for (int k = 0; k < kTileGroup; k++) {
                 const bool hit = (m >> k) & 1u;
                 const uint64_t bm = __ballot(hit);
-                if (hit) point_list[pk[k] + (uint32_t)__popcll(bm & lt)] = g;
+                if (hit) point_list[pk[k] + (uint32_t)__popcll(bm & lt)] = gid[b];
                 pk[k] += (uint32_t)__popcll(bm);
             }
         }
