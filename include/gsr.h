@@ -152,11 +152,11 @@ int gsr_set_true_scale_gradient(int enable);
  * force at its forward.  Returns the previous mode. */
 int gsr_set_deterministic(int enable);
 
-/* Depth-order strategy of the binning, process-wide.  0 (default): the local sort -- level 1 in
- * Gaussian index order, each superblock list sorted by depth in LDS -- except for frames forwarded
- * in deterministic mode and frames with a superblock list longer than the LDS sort holds, which
- * take the global sort.  1: always the global depth sort of all P Gaussians (dsort.hip).  Both give
- * the same per-tile lists.  Returns the previous mode (or GSR_ERR_INVALID_ARGUMENT). */
+/* Depth-order strategy of the binning, process-wide.  0: the local sort -- level 1 in Gaussian
+ * index order, each superblock list sorted by depth in LDS -- except for frames forwarded in
+ * deterministic mode and frames with a superblock list longer than the LDS sort holds, which take
+ * the global sort.  1 (default): always the global depth sort of all P Gaussians (dsort.hip).  Both
+ * give the same per-tile lists.  Returns the previous mode (or GSR_ERR_INVALID_ARGUMENT). */
 int gsr_set_binning(int mode);
 
 /* Forward statistics since load: out[0] = frames rasterized (P > 0), out[1] = frames whose

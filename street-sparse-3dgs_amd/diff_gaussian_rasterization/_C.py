@@ -271,8 +271,8 @@ def set_deterministic(enable: bool) -> bool:
 
 
 def set_binning(mode: int) -> int:
-    """Depth-order strategy (gsr_set_binning): 0 = local per-superblock sort where it applies
-    (default), 1 = always the global depth sort.  Process-wide; returns the previous mode."""
+    """Depth-order strategy (gsr_set_binning): 0 = local per-superblock sort where it applies,
+    1 = always the global depth sort (default).  Process-wide; returns the previous mode."""
     r = _L.gsr_set_binning(int(mode))
     _check(0 if r >= 0 else r, "set_binning")
     return r

@@ -193,7 +193,7 @@ def upstream_grads(c, seed=99):
 
 @contextlib.contextmanager
 def binning_mode(mode):
-    """gsr_set_binning for the duration: 0 = local per-superblock sort (default), 1 = global sort."""
+    """gsr_set_binning for the duration: 0 = local per-superblock sort, 1 = global sort (default)."""
     from diff_gaussian_rasterization import _C
     prev = _C.set_binning(mode)
     try:
