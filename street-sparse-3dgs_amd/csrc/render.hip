@@ -659,7 +659,33 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
             using I3 = std::integral_constant<int, 3>;
             using First = std::true_type;
             using Next = std::false_type;
-            // scalar branches on the wave-uniform mask: sub-blocks the instance cannot touch are skipped
+#ifndef GSR_BWD_FULLSWITCH
+#define GSR_BWD_FULLSWITCH 1
+#endif
+            // scalar branches on the wave-uniform mask: sub-blocks the instance cannot touch are
+            // skipped.  GSR_BWD_FULLSWITCH: one case per mask, so all of an instance's active
+            // sub-blocks are one basic block and their independent p2 -> exp -> alpha -> rcp -> T
+            // chains interleave (nested ifs put every sub-block in a block of its own: each chain's
+            // latency was exposed)
+            if (GSR_BWD_FULLSWITCH) {
+                switch (mk) {
+                    case 1: pix(I0{}, First{}); break;
+                    case 2: pix(I1{}, First{}); break;
+                    case 3: pix(I0{}, First{}); pix(I1{}, Next{}); break;
+                    case 4: pix(I2{}, First{}); break;
+                    case 5: pix(I0{}, First{}); pix(I2{}, Next{}); break;
+                    case 6: pix(I1{}, First{}); pix(I2{}, Next{}); break;
+                    case 7: pix(I0{}, First{}); pix(I1{}, Next{}); pix(I2{}, Next{}); break;
+                    case 8: pix(I3{}, First{}); break;
+                    case 9: pix(I0{}, First{}); pix(I3{}, Next{}); break;
+                    case 10: pix(I1{}, First{}); pix(I3{}, Next{}); break;
+                    case 11: pix(I0{}, First{}); pix(I1{}, Next{}); pix(I3{}, Next{}); break;
+                    case 12: pix(I2{}, First{}); pix(I3{}, Next{}); break;
+                    case 13: pix(I0{}, First{}); pix(I2{}, Next{}); pix(I3{}, Next{}); break;
+                    case 14: pix(I1{}, First{}); pix(I2{}, Next{}); pix(I3{}, Next{}); break;
+                    default: pix(I0{}, First{}); pix(I1{}, Next{}); pix(I2{}, Next{}); pix(I3{}, Next{}); break;
+                }
+            } else
             switch (__builtin_ctz(mk)) {
                 case 0:
                     pix(I0{}, First{});
