@@ -660,7 +660,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
             using First = std::true_type;
             using Next = std::false_type;
 #ifndef GSR_BWD_FULLSWITCH
-#define GSR_BWD_FULLSWITCH 1
+#define GSR_BWD_FULLSWITCH 0  // measured: 0.2257 -> 0.249 ms (r03j A/B), the larger basic blocks did not pay
 #endif
             // scalar branches on the wave-uniform mask: sub-blocks the instance cannot touch are
             // skipped.  GSR_BWD_FULLSWITCH: one case per mask, so all of an instance's active
