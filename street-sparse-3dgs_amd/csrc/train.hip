@@ -400,7 +400,10 @@ constexpr int kSegH = GSR_SSIM_SEG_H;
 constexpr int kStep = 4;
 constexpr int kRing = 16;
 constexpr int kStIC = kStW + 4 * kR, kStMC = kStW + 2 * kR;  // 84 input, 74 SSIM-map columns
-constexpr int kStIP = odd_pitch(kStIC), kStMP = odd_pitch(kStMC), kStTP = odd_pitch(kStW);
+// Even pitches: the row-pair passes (2) and (4) move two adjacent columns per LDS instruction
+// (8-B aligned float2), lanes on consecutive pairs, so they are conflict-free without padding.
+constexpr int kStIP = kStIC, kStMP = kStMC, kStTP = kStW;
+static_assert(kStIP % 2 == 0 && kStMP % 2 == 0 && kStTP % 2 == 0, "float2 rows");
 constexpr int kStInElems = kStep * kStIC;
 constexpr int kStInPer = (kStInElems + kLossThreads - 1) / kLossThreads;
 constexpr int kStHSeg = kStMC / 2;  // horizontal-moment tasks per row (two columns each)
@@ -418,10 +421,17 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_stream_kernel(const floa
                                                                        Window win, const float *__restrict__ dout,
                                                                        float inv_n, float *__restrict__ dx,
                                                                        float2 *__restrict__ partials) {
-    __shared__ float s_in[2][kStep][kStIP];
-    __shared__ float s_hm[5][kRing][kStMP];
-    __shared__ float s_abc[3][kStep][kStMP];
-    __shared__ float s_h3[3][kRing][kStTP];
+    // The staged input rows (read by (2)) and the a/b/c rows ((3) -> (4)) share one buffer: (3)
+    // writes after the barrier that ends (2), and the next step's (1) writes after the barrier
+    // that ends (4).  40.1 KiB in all, so four workgroups fit a CU.
+    __shared__ __attribute__((aligned(16))) union {
+        float in[2][kStep][kStIP];
+        float abc[3][kStep][kStMP];
+    } s_u;
+    __shared__ __attribute__((aligned(16))) float s_hm[5][kRing][kStMP];
+    __shared__ __attribute__((aligned(16))) float s_h3[3][kRing][kStTP];
+    auto &s_in = s_u.in;
+    auto &s_abc = s_u.abc;
     __shared__ float s_red[8];
     const size_t plane_off = (size_t)blockIdx.z * H * W;
     x += plane_off;
@@ -463,10 +473,15 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_stream_kernel(const floa
                 s_in[1][r][c] = pin[k] ? py[k] : 0.f;
             }
         }
-        const int orow = p0 + (tid >> 6) - 2 * kR, ocol = cx + (tid & 63);  // (5)'s output pixel
-        const bool o_ok = orow >= r0 && orow < r1 && ocol < W;
-        const size_t oo = (size_t)min(max(orow, 0), H - 1) * W + min(ocol, W - 1);
-        const float xv = x[oo], yv = y[oo];
+        // (5)'s output pixels: rows orow, orow + 1 of column ocol (tasks tid < 128)
+        const int orow = p0 + 2 * ((tid >> 6) & 1) - 2 * kR, ocol = cx + (tid & 63);
+        float xv[2], yv[2];
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const size_t oo = (size_t)min(max(orow + k, 0), H - 1) * W + min(ocol, W - 1);
+            xv[k] = x[oo];
+            yv[k] = y[oo];
+        }
         fetch(p0 + kStep);  // unconditional (clamped): a branch here would make every wait a full drain
         lds_barrier();
 
@@ -475,11 +490,16 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_stream_kernel(const floa
             const int r = tid / kStHSeg, c0 = 2 * (tid - r * kStHSeg);
             float u[2 + 2 * kR], v[2 + 2 * kR];
 #pragma unroll
-            for (int k = 0; k < 2 + 2 * kR; k++) {
-                u[k] = s_in[0][r][c0 + k];
-                v[k] = s_in[1][r][c0 + k];
+            for (int k = 0; k < 2 + 2 * kR; k += 2) {
+                const float2 a = *reinterpret_cast<const float2 *>(&s_in[0][r][c0 + k]);
+                const float2 b = *reinterpret_cast<const float2 *>(&s_in[1][r][c0 + k]);
+                u[k] = a.x;
+                u[k + 1] = a.y;
+                v[k] = b.x;
+                v[k + 1] = b.y;
             }
             const int ring = (p0 + r) & (kRing - 1);
+            float m[5][2];
 #pragma unroll
             for (int o = 0; o < 2; o++) {
                 float m1 = 0.f, m2 = 0.f, a11 = 0.f, a22 = 0.f, a12 = 0.f;
@@ -492,12 +512,15 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_stream_kernel(const floa
                     a22 = fmaf(w, v[o + j] * v[o + j], a22);
                     a12 = fmaf(w, u[o + j] * v[o + j], a12);
                 }
-                s_hm[0][ring][c0 + o] = m1;
-                s_hm[1][ring][c0 + o] = m2;
-                s_hm[2][ring][c0 + o] = a11;
-                s_hm[3][ring][c0 + o] = a22;
-                s_hm[4][ring][c0 + o] = a12;
+                m[0][o] = m1;
+                m[1][o] = m2;
+                m[2][o] = a11;
+                m[3][o] = a22;
+                m[4][o] = a12;
             }
+#pragma unroll
+            for (int q = 0; q < 5; q++)
+                *reinterpret_cast<float2 *>(&s_hm[q][ring][c0]) = make_float2(m[q][0], m[q][1]);
         }
         lds_barrier();
 
@@ -538,40 +561,62 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_stream_kernel(const floa
         lds_barrier();
 
         // (4) horizontal pass of a/b/c (symmetric window: the transposed convolution is the same
-        // correlation), one output column per lane
-        {
-            const int r = tid >> 6, c = tid & 63;
+        // correlation), two adjacent output columns per task: 128 tasks, two waves
+        if (tid < kStep * kStW / 2) {
+            const int r = tid / (kStW / 2), c0 = 2 * (tid - r * (kStW / 2));
             const int ring = (p0 + r - kR) & (kRing - 1);
 #pragma unroll
             for (int q = 0; q < 3; q++) {
-                float sum = 0.f;
+                float a[2 + 2 * kR];
 #pragma unroll
-                for (int j = 0; j < 2 * kR + 1; j++) sum = fmaf(win.w[j], s_abc[q][r][c + j], sum);
-                s_h3[q][ring][c] = sum;
+                for (int k = 0; k < 2 + 2 * kR; k += 2) {
+                    const float2 t = *reinterpret_cast<const float2 *>(&s_abc[q][r][c0 + k]);
+                    a[k] = t.x;
+                    a[k + 1] = t.y;
+                }
+                float sum0 = 0.f, sum1 = 0.f;
+#pragma unroll
+                for (int j = 0; j < 2 * kR + 1; j++) {
+                    sum0 = fmaf(win.w[j], a[j], sum0);
+                    sum1 = fmaf(win.w[j], a[j + 1], sum1);
+                }
+                *reinterpret_cast<float2 *>(&s_h3[q][ring][c0]) = make_float2(sum0, sum1);
             }
         }
         lds_barrier();
 
-        // (5) vertical pass and the gradient at output row orow = p0 + r - 2R
-        if (o_ok) {
+        // (5) vertical pass and the gradient at output rows orow, orow + 1 (p0 + r - 2R), two rows
+        // per task from 12 ring rows: 128 tasks, two waves
+        if (tid < kStep * 64 / 2) {
             const int c = tid & 63;
-            float acc[3];
+            float acc[3][2];
 #pragma unroll
             for (int q = 0; q < 3; q++) {
-                acc[q] = 0.f;
+                acc[q][0] = acc[q][1] = 0.f;
 #pragma unroll
-                for (int j = 0; j < 2 * kR + 1; j++)
-                    acc[q] = fmaf(win.w[j], s_h3[q][(orow - kR + j) & (kRing - 1)][c], acc[q]);
+                for (int t = 0; t < 2 * kR + 2; t++) {
+                    const float v = s_h3[q][(orow - kR + t) & (kRing - 1)][c];
+#pragma unroll
+                    for (int k = 0; k < 2; k++) {
+                        const int j = t - k;
+                        if (j >= 0 && j <= 2 * kR) acc[q][k] = fmaf(win.w[j], v, acc[q][k]);
+                    }
+                }
             }
-            const size_t o = (size_t)orow * W + ocol;
-            const float d = xv - yv;
-            const float G = acc[0] + 2.f * xv * acc[1] + yv * acc[2];
-            if (kMap) {
-                dx[o] = G;
-                l1 += fabsf(d);
-            } else {
-                const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
-                dx[o] = g_l1 * sgn + g_ssim * G;
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const int row = orow + k;
+                if (row < r0 || row >= r1 || ocol >= W) continue;
+                const size_t o = (size_t)row * W + ocol;
+                const float d = xv[k] - yv[k];
+                const float G = acc[0][k] + 2.f * xv[k] * acc[1][k] + yv[k] * acc[2][k];
+                if (kMap) {
+                    dx[o] = G;
+                    l1 += fabsf(d);
+                } else {
+                    const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+                    dx[o] = g_l1 * sgn + g_ssim * G;
+                }
             }
         }
     }

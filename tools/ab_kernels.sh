@@ -7,10 +7,13 @@ TAG=${1:-abk}
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/abk_$TAG; mkdir -p "$OUT"
 ARGS="--steps 20 --warmup 5 --profile-steps 1 --metric-only"
+# AB_SCRIPT / AB_ARGS: profile another program (e.g. tools/train_step_profile.py --steps 20)
+SCRIPT=${AB_SCRIPT:-bench.py}
+[ -n "${AB_ARGS:-}" ] && ARGS=$AB_ARGS
 export TMPDIR=/tmp
 run() {  # name, library ("" = in-tree)
   ( cd /tmp && GSR_LIBRARY="$2" timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv \
-      -d "$OUT/$1" -o run -- python3 "$ROOT/bench.py" $ARGS > "$OUT/$1.log" 2>&1 )
+      -d "$OUT/$1" -o run -- python3 "$ROOT/$SCRIPT" $ARGS > "$OUT/$1.log" 2>&1 )
 }
 run base "" || exit 1
 for lib in vlibs/*.so; do
