@@ -169,17 +169,21 @@ def psnr_vs_oracle(gpu_color, gpu_invd, st):
     return out
 
 
-def train_step_ms(P, W, H, steps, warmup, dev, street=True, reference=False, seed=0, fovx_deg=60.0):
+def train_step_ms(P, W, H, steps, warmup, dev, street=True, reference=False, seed=0, fovx_deg=60.0, native=True):
     """one train_single.py iteration on the bench scene (1M Gaussians at
     1080p, perturbed), wall time per step between synchronisations (the fused step never syncs).
     street=True: the Street-sparse iteration -- 4 training views cycled, the masked inverse-depth
     L1 (train_single.py:133-141, weight schedule 1.0 -> 0.01), the first 10k rows a locked skybox
     (:217-223), exposure and xyz lr schedules.  street=False: photometric loss only, one fixed
     view (round 1's number, kept as a labelled variant).  reference=True: the same step in the
-    reference's torch formulation (oracle/train_torch_ref.py, a baseline leg)."""
+    reference's torch formulation (oracle/train_torch_ref.py, a baseline leg).  native=True: the
+    step as one gsr_train_step call (gs_train.native_step); False: issued from Python through the
+    autograd API (gs_train.harness.TrainStep) -- the same kernels in the same order."""
     import torch
     from gs_train.harness import make_problem
     step_cls = None
+    if native and not reference:
+        from gs_train.native_step import NativeTrainStep as step_cls
     if reference:
         from train_torch_ref import ReferenceTrainStep as step_cls
     ts = make_problem(P, W, H, n_views=4 if street else 1, seed=seed, step_cls=step_cls, depth=street,
@@ -662,10 +666,12 @@ def main():
               "workload": f"Street-sparse train_single.py iteration on the bench scene ({P} Gaussians, {W}x{H}, 4 views "
                           f"cycled): render, exposure, 0.8 L1 + 0.2 (1 - SSIM) + masked inverse-depth L1, backward "
                           f"(depth gradient on), densify stats, exposure Adam, skybox lock (10k rows), sparse Adam, "
-                          f"scale clamp",
+                          f"scale clamp; one native gsr_train_step call per step (python_driven_ms: the same step "
+                          f"issued from Python through the autograd API)",
               "steps": a.train_steps}
         r1 = _Cstats.forward_stats()
         tr["binning_reruns"] = r1["reruns"] - r0["reruns"]
+        tr["python_driven_ms"] = round(train_step_ms(P, W, H, a.train_steps, 5, dev, seed=rank, native=False), 4)
         tr["photo_only_fixed_view_ms"] = round(train_step_ms(P, W, H, a.train_steps, 5, dev, street=False), 4)
         if a.train_baseline:
             tr["reference_structured_ms"] = round(train_step_ms(P, W, H, a.train_steps, 5, dev, reference=True), 4)

@@ -137,6 +137,61 @@ int gsr_depth_l1_forward(const float *invdepth, const float *mono_invdepth, cons
 int gsr_depth_l1_backward(const float *invdepth, const float *mono_invdepth, const float *mask, int64_t n,
                           float weight, const float *dL_dloss, float *dL_dinvdepth, void *stream);
 
+/* ---- Native train-step executor ------------------------------------------------------------
+ * gsr_train_step runs one whole Street-sparse iteration (train_single.py:65-247: render with
+ * the exposure of the view, photometric loss + masked inverse-depth L1, backward, densification
+ * statistics, exposure Adam, skybox lock, sparse Adam, scale shrink) as ONE host call, through
+ * the entry points above and gsr_rasterize_forward_ex / _backward in the order
+ * gs_train/harness.py TrainStep.step issues them, so its results are those of the Python step
+ * (bit for bit in the deterministic backward mode).  The context owns every per-step
+ * intermediate (rasterizer buffers, images, activated values and their gradients) in grow-only
+ * device allocations reused across steps; the caller owns the parameters, their gradients
+ * (overwritten each step), the Adam moments and the densification statistics.
+ * Replaces the Python-driven step; none of the reference's files has a native executor. */
+typedef struct gsr_train_ctx gsr_train_ctx;
+gsr_train_ctx *gsr_train_ctx_create(void);
+/* Waits for the last step's stream, then frees the context's device buffers. */
+void gsr_train_ctx_destroy(gsr_train_ctx *ctx);
+
+typedef struct {
+    int64_t P;   /* Gaussians */
+    int D, M;    /* active SH degree, coefficients per Gaussian (features is (P, M, 3)) */
+    int width, height;
+    /* parameters (updated in place) and their gradients (overwritten) */
+    float *xyz, *features, *opacity, *scaling, *rotation;           /* raw: (P,3) (P,M,3) (P,1) (P,3) (P,4) */
+    float *xyz_grad, *features_grad, *opacity_grad, *scaling_grad, *rotation_grad;
+    float *exposure, *exposure_grad; /* (n_images, 3, 4); the gradient is zero outside image_index */
+    int n_images, image_index;
+    /* the view */
+    const float *viewmatrix, *projmatrix, *campos; /* device: 16, 16, 3 */
+    float tan_fovx, tan_fovy;
+    const float *background;                        /* device: 3 */
+    const float *gt;                                /* (3, H, W) */
+    const float *alpha_mask;                        /* (H, W) or NULL */
+    const float *mono_invdepth, *depth_mask;        /* (H, W) or NULL (no depth term); mask NULL = ones */
+    float depth_weight;                             /* depth_l1_weight(iteration); <= 0: no depth term */
+    double lambda_dssim;
+    /* densification statistics (P) */
+    float *max_radii2D, *xyz_gradient_accum, *denom;
+    /* optimizers: the Gaussian groups (their grad pointers are the gradients above) and the
+     * exposure's one dense group (n_images rows of 12) */
+    int n_groups;
+    const gsr_adam_group *groups;
+    double beta1, beta2, eps;
+    const gsr_adam_group *exposure_group;
+    double exposure_beta1, exposure_beta2, exposure_eps;
+    int64_t skybox_rows;   /* the first rows: their opacity gradient is zeroed before the sparse step */
+    int64_t scaffold_rows; /* the first rows: left alone by the scale shrink */
+    float max_scale;       /* shrink rows whose largest scale exceeds this (extent * 0.02) */
+    /* out (device, 5 floats): L1, SSIM, photometric loss, then (depth term only) the unweighted
+     * and weighted depth L1; the step's loss is [2] + [4] */
+    float *losses;
+    void *stream;
+} gsr_train_step_args;
+
+/* *num_rendered receives the frame's K. */
+int gsr_train_step(gsr_train_ctx *ctx, const gsr_train_step_args *args, int64_t *num_rendered);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,240 @@
+// train_step.hip -- the native train-step executor (include/gsr_train.h gsr_train_step): one host
+// call runs a whole Street-sparse iteration (train_single.py:65-247, as gs_train/harness.py
+// TrainStep.step drives it from Python) through the same C-ABI entry points, in the same order:
+//
+//   activations -> rasterizer forward -> exposure -> [alpha mask] -> photometric loss (+ SSIM
+//   gradient field) -> [masked inverse-depth L1] -> loss backward -> [alpha mask] -> exposure
+//   backward -> rasterizer backward -> activation backward -> densification statistics ->
+//   exposure Adam -> skybox lock -> sparse Adam -> scale shrink
+//
+// The Python step spends about as long issuing its ~45 launches (autograd nodes, tensor
+// allocation, ctypes marshalling) as the GPU spends running them, so the GPU idles between
+// launches; here the host issues the step in a small fraction of the GPU time and the step is
+// bound by the kernels.  Every per-step intermediate lives in grow-only device buffers owned by
+// the context and reused across steps (no allocation in steady state).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "../../include/gsr.h"
+#include "../../include/gsr_train.h"
+#include "gsr_launch.h"
+
+namespace gsr {
+namespace {
+
+enum Slot {
+    kGeom, kBinning, kImage, kBwdScratch,                                  // rasterizer buffers
+    kColor, kInvDepth, kExposed, kGradMap, kDImage, kDColor, kDInvDepth,   // image-sized
+    kScales, kRots, kOpac, kDScales, kDRots, kDOpac, kDMeans2D, kRadii,    // per-Gaussian
+    kLossScratch, kExpScratch, kDepthScratch, kWords,                      // small
+    kSlots
+};
+
+__global__ void mask_multiply_kernel(float *__restrict__ x, const float *__restrict__ mask, int C, int64_t npix) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npix) return;
+    const float m = mask[i];
+    for (int c = 0; c < C; c++) x[(int64_t)c * npix + i] = x[(int64_t)c * npix + i] * m;
+}
+
+}  // namespace
+}  // namespace gsr
+
+using namespace gsr;
+
+struct gsr_train_ctx {
+    struct Buf {
+        void *p = nullptr;
+        size_t cap = 0;
+    } buf[kSlots];
+    hipStream_t stream = nullptr;
+    bool failed_alloc = false;
+    bool one_written = false;
+
+    // grow-only: a larger request waits for the stream (queued kernels may still use the old
+    // allocation), frees it and allocates 1/8 more than asked (rasterizer buffers follow K)
+    void *get(int slot, size_t bytes) {
+        Buf &b = buf[slot];
+        if (bytes <= b.cap && b.p) return b.p;
+        if (b.p) {
+            if (hipStreamSynchronize(stream) != hipSuccess) return nullptr;
+            (void)hipFree(b.p);
+            b.p = nullptr;
+            b.cap = 0;
+        }
+        const size_t want = std::max<size_t>(256, bytes + bytes / 8);
+        if (hipMalloc(&b.p, want) != hipSuccess) {
+            b.p = nullptr;
+            failed_alloc = true;
+            return nullptr;
+        }
+        b.cap = want;
+        return b.p;
+    }
+    float *f32(int slot, size_t n) { return static_cast<float *>(get(slot, n * sizeof(float))); }
+
+    ~gsr_train_ctx() {
+        for (auto &b : buf)
+            if (b.p) (void)hipFree(b.p);
+    }
+};
+
+namespace {
+
+void *buf_ptr(gsr_train_ctx *c, int slot) { return c->buf[slot].p; }
+void *resize_geom(void *c, size_t n) { return static_cast<gsr_train_ctx *>(c)->get(kGeom, n); }
+void *resize_binning(void *c, size_t n) { return static_cast<gsr_train_ctx *>(c)->get(kBinning, n); }
+void *resize_image(void *c, size_t n) { return static_cast<gsr_train_ctx *>(c)->get(kImage, n); }
+void *resize_scratch(void *c, size_t n) { return static_cast<gsr_train_ctx *>(c)->get(kBwdScratch, n); }
+
+int fail_step(int rc, const char *what) {
+    if (rc == GSR_OK) return rc;
+    set_last_error(std::string("gsr_train_step: ") + what + ": " + gsr_last_error());
+    return rc;
+}
+
+int invalid(const char *msg) {
+    set_last_error(std::string("gsr_train_step: ") + msg);
+    return GSR_ERR_INVALID_ARGUMENT;
+}
+
+}  // namespace
+
+extern "C" {
+
+gsr_train_ctx *gsr_train_ctx_create(void) { return new (std::nothrow) gsr_train_ctx(); }
+
+void gsr_train_ctx_destroy(gsr_train_ctx *ctx) {
+    if (!ctx) return;
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    delete ctx;
+}
+
+int gsr_train_step(gsr_train_ctx *ctx, const gsr_train_step_args *a, int64_t *num_rendered) {
+    if (num_rendered) *num_rendered = 0;
+    if (!ctx || !a) return invalid("NULL context or arguments");
+    const int64_t P = a->P;
+    const int W = a->width, H = a->height;
+    if (P <= 0 || P > 0x7fffffff || W <= 0 || H <= 0 || a->M <= 0 || a->D < 0 || (a->D + 1) * (a->D + 1) > a->M)
+        return invalid("bad sizes");
+    if (!a->xyz || !a->features || !a->opacity || !a->scaling || !a->rotation || !a->xyz_grad ||
+        !a->features_grad || !a->opacity_grad || !a->scaling_grad || !a->rotation_grad)
+        return invalid("NULL parameter or gradient");
+    if (!a->exposure || !a->exposure_grad || a->n_images <= 0 || a->image_index < 0 || a->image_index >= a->n_images)
+        return invalid("bad exposure arguments");
+    if (!a->viewmatrix || !a->projmatrix || !a->campos || !a->background || !a->gt || !a->losses)
+        return invalid("NULL camera, background, target or loss output");
+    if (!a->max_radii2D || !a->xyz_gradient_accum || !a->denom) return invalid("NULL densification statistics");
+    if (a->n_groups <= 0 || !a->groups || !a->exposure_group) return invalid("no optimizer groups");
+    if (a->skybox_rows < 0 || a->skybox_rows > P || a->scaffold_rows < 0)
+        return invalid("skybox / scaffold rows outside [0, P]");
+    if (!(a->lambda_dssim >= 0.0 && a->lambda_dssim <= 1.0)) return invalid("lambda_dssim outside [0, 1]");
+
+    hipStream_t s = static_cast<hipStream_t>(a->stream);
+    ctx->stream = s;
+    void *sv = a->stream;
+    const int64_t npix = (int64_t)W * H;
+    const bool depth = a->mono_invdepth != nullptr && a->depth_weight > 0.f;
+
+    float *scales = ctx->f32(kScales, 3 * P), *rots = ctx->f32(kRots, 4 * P), *opac = ctx->f32(kOpac, P);
+    float *d_scales = ctx->f32(kDScales, 3 * P), *d_rots = ctx->f32(kDRots, 4 * P), *d_opac = ctx->f32(kDOpac, P);
+    float *d_means2D = ctx->f32(kDMeans2D, 3 * P);
+    int *radii = static_cast<int *>(ctx->get(kRadii, sizeof(int) * P));
+    float *color = ctx->f32(kColor, 3 * npix), *invd = ctx->f32(kInvDepth, npix);
+    float *image = ctx->f32(kExposed, 3 * npix), *gmap = ctx->f32(kGradMap, 3 * npix);
+    float *d_image = ctx->f32(kDImage, 3 * npix), *d_color = ctx->f32(kDColor, 3 * npix);
+    float *d_invd = ctx->f32(kDInvDepth, npix);
+    void *loss_scratch = ctx->get(kLossScratch, gsr_l1_ssim_scratch_bytes(3, H, W));
+    void *exp_scratch = ctx->get(kExpScratch, gsr_exposure_scratch_bytes(npix));
+    void *depth_scratch = ctx->get(kDepthScratch, gsr_depth_l1_scratch_bytes(npix));
+    // words: [0] the Adam relevance flag, [1] dL/dloss = 1 (the upstream of loss.backward())
+    void *words = ctx->get(kWords, 64);
+    if (ctx->failed_alloc || !scales || !rots || !opac || !d_scales || !d_rots || !d_opac || !d_means2D || !radii ||
+        !color || !invd || !image || !gmap || !d_image || !d_color || !d_invd || !loss_scratch || !exp_scratch ||
+        !depth_scratch || !words) {
+        ctx->failed_alloc = false;
+        set_last_error("gsr_train_step: device allocation failed");
+        return GSR_ERR_ALLOCATION;
+    }
+    int *flag = static_cast<int *>(words);
+    float *one = static_cast<float *>(words) + 1;
+    if (!ctx->one_written) {  // once per context (the words slot is never re-allocated: 64 B)
+        const float one_h = 1.f;
+        if (hipMemcpy(one, &one_h, sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
+            return fail_step(GSR_ERR_DEVICE, "upstream gradient");
+        ctx->one_written = true;
+    }
+    int rc;
+
+    // render(): activations, rasterizer, exposure of this view (harness.py TrainStep.render)
+    if ((rc = gsr_activate_forward(P, a->scaling, a->rotation, a->opacity, scales, rots, opac, sv)))
+        return fail_step(rc, "activations");
+    int64_t K = 0;
+    if ((rc = gsr_rasterize_forward_ex(resize_geom, resize_binning, resize_image, ctx, (int)P, a->D, a->M,
+                                       a->background, W, H, a->xyz, a->features, nullptr, opac, scales, 1.0f, rots,
+                                       nullptr, a->viewmatrix, a->projmatrix, a->campos, a->tan_fovx, a->tan_fovy, 0,
+                                       color, invd, radii, nullptr, nullptr, nullptr, nullptr, 0, 0, sv, &K, 0)))
+        return fail_step(rc, "rasterizer forward");
+    const float *E = a->exposure + 12 * (int64_t)a->image_index;
+    if ((rc = gsr_exposure_forward(color, E, npix, image, sv))) return fail_step(rc, "exposure");
+    const unsigned mblocks = (unsigned)((npix + 255) / 256);
+    if (a->alpha_mask) hipLaunchKernelGGL(mask_multiply_kernel, dim3(mblocks), dim3(256), 0, s, image, a->alpha_mask, 3, npix);
+
+    // losses (train_single.py:121-141)
+    if ((rc = gsr_photo_loss_forward(image, a->gt, 3, H, W, a->lambda_dssim, loss_scratch, a->losses, gmap, sv)))
+        return fail_step(rc, "photometric loss");
+    if (depth && (rc = gsr_depth_l1_forward(invd, a->mono_invdepth, a->depth_mask, npix, a->depth_weight,
+                                            depth_scratch, a->losses + 3, sv)))
+        return fail_step(rc, "depth loss");
+
+    // loss.backward()
+    if (depth && (rc = gsr_depth_l1_backward(invd, a->mono_invdepth, a->depth_mask, npix, a->depth_weight, one, d_invd,
+                                             sv)))
+        return fail_step(rc, "depth loss backward");
+    if ((rc = gsr_photo_loss_backward(image, a->gt, gmap, 3, H, W, a->lambda_dssim, one, d_image, sv)))
+        return fail_step(rc, "photometric loss backward");
+    if (a->alpha_mask)
+        hipLaunchKernelGGL(mask_multiply_kernel, dim3(mblocks), dim3(256), 0, s, d_image, a->alpha_mask, 3, npix);
+    // the exposure gradient is the indexed row of a zero (n_images, 3, 4) tensor, as autograd forms it
+    if (hipMemsetAsync(a->exposure_grad, 0, sizeof(float) * 12 * (size_t)a->n_images, s) != hipSuccess)
+        return fail_step(GSR_ERR_DEVICE, "exposure gradient clear");
+    if ((rc = gsr_exposure_backward(color, E, npix, d_image, d_color, a->exposure_grad + 12 * (int64_t)a->image_index,
+                                    exp_scratch, sv)))
+        return fail_step(rc, "exposure backward");
+    if ((rc = gsr_rasterize_backward(resize_scratch, ctx, (int)P, a->D, a->M, K, a->background, W, H, a->xyz,
+                                     a->features, nullptr, scales, 1.0f, rots, nullptr, a->viewmatrix, a->projmatrix,
+                                     a->campos, a->tan_fovx, a->tan_fovy, radii, buf_ptr(ctx, kGeom),
+                                     buf_ptr(ctx, kBinning), buf_ptr(ctx, kImage), d_color, depth ? d_invd : nullptr,
+                                     d_means2D, nullptr, d_opac, a->xyz_grad, nullptr, a->features_grad, d_scales,
+                                     d_rots, nullptr, nullptr, nullptr, nullptr, 0, 0, sv)))
+        return fail_step(rc, "rasterizer backward");
+    if ((rc = gsr_activate_backward(P, a->rotation, scales, opac, d_scales, d_rots, d_opac, a->scaling_grad,
+                                    a->rotation_grad, a->opacity_grad, sv)))
+        return fail_step(rc, "activation backward");
+
+    // densification statistics, exposure Adam, skybox lock, sparse Adam, shrink (train_single.py:193-241)
+    if ((rc = gsr_densify_stats(P, radii, d_means2D, a->max_radii2D, a->xyz_gradient_accum, a->denom, sv)))
+        return fail_step(rc, "densification statistics");
+    if ((rc = gsr_sparse_adam_step(1, a->exposure_group, a->n_images, nullptr, a->exposure_beta1, a->exposure_beta2,
+                                   a->exposure_eps, flag, sv)))
+        return fail_step(rc, "exposure Adam");
+    if (a->skybox_rows > 0 &&
+        hipMemsetAsync(a->opacity_grad, 0, sizeof(float) * (size_t)a->skybox_rows, s) != hipSuccess)
+        return fail_step(GSR_ERR_DEVICE, "skybox lock");
+    if ((rc = gsr_sparse_adam_step(a->n_groups, a->groups, P, a->opacity_grad, a->beta1, a->beta2, a->eps, flag, sv)))
+        return fail_step(rc, "sparse Adam");
+    if ((rc = gsr_shrink_scales(P, a->scaffold_rows, a->scaling, a->max_scale, sv))) return fail_step(rc, "shrink");
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_last_error(std::string("gsr_train_step: ") + hipGetErrorString(e));
+        return GSR_ERR_DEVICE;
+    }
+    if (num_rendered) *num_rendered = K;
+    return GSR_OK;
+}
+
+}  // extern "C"

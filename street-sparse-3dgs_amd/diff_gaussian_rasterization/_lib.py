@@ -30,6 +30,23 @@ class RowGroup(ctypes.Structure):
     _fields_ = [("param", _vp), ("exp_avg", _vp), ("exp_avg_sq", _vp), ("width", _i64)]
 
 
+class TrainStepArgs(ctypes.Structure):
+    """gsr_train_step_args (include/gsr_train.h)."""
+    _fields_ = [("P", _i64), ("D", _i), ("M", _i), ("width", _i), ("height", _i),
+                ("xyz", _vp), ("features", _vp), ("opacity", _vp), ("scaling", _vp), ("rotation", _vp),
+                ("xyz_grad", _vp), ("features_grad", _vp), ("opacity_grad", _vp), ("scaling_grad", _vp),
+                ("rotation_grad", _vp), ("exposure", _vp), ("exposure_grad", _vp), ("n_images", _i),
+                ("image_index", _i), ("viewmatrix", _vp), ("projmatrix", _vp), ("campos", _vp), ("tan_fovx", _f),
+                ("tan_fovy", _f), ("background", _vp), ("gt", _vp), ("alpha_mask", _vp), ("mono_invdepth", _vp),
+                ("depth_mask", _vp), ("depth_weight", _f), ("lambda_dssim", ctypes.c_double),
+                ("max_radii2D", _vp), ("xyz_gradient_accum", _vp), ("denom", _vp), ("n_groups", _i),
+                ("groups", ctypes.POINTER(AdamGroup)), ("beta1", ctypes.c_double), ("beta2", ctypes.c_double),
+                ("eps", ctypes.c_double), ("exposure_group", ctypes.POINTER(AdamGroup)),
+                ("exposure_beta1", ctypes.c_double), ("exposure_beta2", ctypes.c_double),
+                ("exposure_eps", ctypes.c_double), ("skybox_rows", _i64), ("scaffold_rows", _i64),
+                ("max_scale", _f), ("losses", _vp), ("stream", _vp)]
+
+
 # exported symbol -> (restype, argtypes); must match include/gsr.h, gsr_train.h, gsr_hier.h, gsr_knn.h, gsr_densify.h
 SIGNATURES = {
     "gsr_rasterize_forward": (_i, [RESIZE_FN, RESIZE_FN, RESIZE_FN, _vp, _i, _i, _i, _vp, _i, _i,
@@ -76,6 +93,9 @@ SIGNATURES = {
     "gsr_exposure_forward": (_i, [_vp, _vp, _i64, _vp, _vp]),
     "gsr_exposure_scratch_bytes": (ctypes.c_size_t, [_i64]),
     "gsr_exposure_backward": (_i, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
+    "gsr_train_ctx_create": (_vp, []),
+    "gsr_train_ctx_destroy": (None, [_vp]),
+    "gsr_train_step": (_i, [_vp, ctypes.POINTER(TrainStepArgs), ctypes.POINTER(_i64)]),
     # include/gsr_hier.h
     "gsr_interpolate_cut_forward": (_i, [_i64, _i, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                          _vp, _vp, _vp]),

@@ -8,6 +8,7 @@
   activations.activate             exp / normalize / sigmoid getters fwd+bwd in one launch each
   activations.shrink_scales        the per-step shrink of over-large Gaussians (train_single.py:235-241)
   harness.TrainStep                one train_single.py inner-loop iteration (the "train-step ms")
+  native_step.NativeTrainStep      the same iteration as one native call (gsr_train_step)
   synthetic                        seeded synthetic scenes / cameras
 """
 from .loss import l1_ssim, photo_loss  # noqa: F401

@@ -230,6 +230,65 @@ def test_train_step_fused_matches_reference_structured_step(depth, alpha, skybox
                 assert torch.equal(x[:skybox], x0[:skybox]), name
 
 
+@pytest.mark.parametrize("depth,alpha,skybox,scaffold", [(True, False, 0, 0), (False, True, 300, 0),
+                                                          (True, True, 300, 2000)])
+def test_native_step_equals_python_step(depth, alpha, skybox, scaffold):
+    """gsr_train_step (gs_train.native_step.NativeTrainStep) against the Python-driven fused step
+    (harness.TrainStep): the same entry points in the same order, so with the deterministic
+    backward every parameter, Adam moment, exposure, densification statistic and loss value is
+    bit-identical after several steps over cycled views."""
+    from helpers import deterministic
+    from gs_train.harness import make_problem
+    from gs_train.native_step import NativeTrainStep
+    names = ("_xyz", "_features", "_opacity", "_scaling", "_rotation", "_exposure")
+    out = {}
+    with deterministic():
+        for native in (False, True):
+            torch.manual_seed(0)
+            ts = make_problem(20_000, 256, 192, n_views=3, seed=1, step_cls=NativeTrainStep if native else None,
+                              depth=depth, alpha=alpha, skybox_points=skybox, scaffold_points=scaffold)
+            if scaffold:
+                with torch.no_grad():
+                    ts.g._scaling[scaffold - 50:scaffold + 50] += 3.0
+            torch.manual_seed(3)  # the random backgrounds
+            losses = [ts.step().clone() for _ in range(4)]
+            params = [getattr(ts.g, n).detach().clone() for n in names]
+            moments = [torch.cat([ts.optimizer.state[getattr(ts.g, n)][k].reshape(-1)
+                                  for n in names[:-1]]) for k in ("exp_avg", "exp_avg_sq")]
+            moments += [ts.exposure_optimizer.state[ts.g._exposure][k].clone() for k in ("exp_avg", "exp_avg_sq")]
+            steps = [float(ts.optimizer.state[getattr(ts.g, n)]["step"]) for n in names[:-1]]
+            stats = [ts.g.max_radii2D.clone(), ts.g.xyz_gradient_accum.clone(), ts.g.denom.clone()]
+            out[native] = (torch.stack(losses), params, moments, steps, stats)
+    (la, pa, ma, sa, ta), (lb, pb, mb, sb, tb) = out[False], out[True]
+    assert torch.equal(la, lb), (la, lb)
+    for n, x, y in zip(names, pa, pb):
+        assert torch.equal(x, y), n
+    for x, y in zip(ma, mb):
+        assert torch.equal(x, y)
+    assert sa == sb == [4.0] * 5
+    for x, y in zip(ta, tb):
+        assert torch.equal(x, y)
+
+
+def test_native_step_follows_densification():
+    """The executor re-reads the parameter tensors when densification replaces them."""
+    from gs_train.harness import make_problem
+    from gs_train.native_step import NativeTrainStep
+    from gs_train.densify import densify_and_prune
+    torch.manual_seed(0)
+    ts = make_problem(20_000, 256, 192, n_views=2, seed=2, perturb=0.05, step_cls=NativeTrainStep)
+    for _ in range(3):
+        ts.step()
+    # the executor's gradients stand in for the .grad fields densification statistics came from
+    P0 = ts.g.P
+    densify_and_prune(ts.g, ts.optimizer, 1e-6, 0.005, 10.0, 0.01)
+    assert ts.g.P != P0
+    first = ts.step().item()
+    for _ in range(10):
+        ts.step()
+    assert np.isfinite(first) and ts.last_K > 0 and ts._args.P == ts.g.P
+
+
 def test_depth_l1_node_matches_torch_expression():
     """gs_train.loss.depth_l1_loss vs train_single.py:138-140 through torch autograd: value to fp32
     rounding (fp64 accumulation here), dL/dinvdepth bit-identical (including sgn(0) = 0 where the

@@ -24,10 +24,13 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--baseline", action="store_true")
+    ap.add_argument("--python", action="store_true", help="the Python-driven step (default: gsr_train_step)")
     a = ap.parse_args()
     import torch
     from gs_train.harness import make_problem
     step_cls = None
+    if not a.python:
+        from gs_train.native_step import NativeTrainStep as step_cls
     if a.baseline:
         sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "oracle"))
         from train_torch_ref import ReferenceTrainStep as step_cls
@@ -43,7 +46,7 @@ def main():
         host += time.perf_counter() - h0
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / a.steps * 1e3
-    print(f"train step ({'baseline' if a.baseline else 'fused'}): wall {wall:.3f} ms/step, "
+    print(f"train step ({'baseline' if a.baseline else ('python' if a.python else 'native')}): wall {wall:.3f} ms/step, "
           f"host issue {host / a.steps * 1e3:.3f} ms/step")
 
 
