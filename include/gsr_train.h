@@ -140,10 +140,10 @@ int gsr_depth_l1_backward(const float *invdepth, const float *mono_invdepth, con
 /* ---- Native train-step executor ------------------------------------------------------------
  * gsr_train_step runs one whole Street-sparse iteration (train_single.py:65-247: render with
  * the exposure of the view, photometric loss + masked inverse-depth L1, backward, densification
- * statistics, exposure Adam, skybox lock, sparse Adam, scale shrink) as ONE host call, through
- * the entry points above and gsr_rasterize_forward_ex / _backward in the order
- * gs_train/harness.py TrainStep.step issues them, so its results are those of the Python step
- * (bit for bit in the deterministic backward mode).  The context owns every per-step
+ * statistics, exposure Adam, skybox lock, sparse Adam, scale shrink) as ONE host call, with the
+ * arithmetic of the entry points above and gsr_rasterize_forward_ex / _backward in the order
+ * gs_train/harness.py TrainStep.step issues them (several fused into one launch), so its results
+ * are those of the Python step (bit for bit in the deterministic backward mode).  The context owns every per-step
  * intermediate (rasterizer buffers, images, activated values and their gradients) in grow-only
  * device allocations reused across steps; the caller owns the parameters, their gradients
  * (overwritten each step), the Adam moments and the densification statistics.
@@ -183,8 +183,8 @@ typedef struct {
     int64_t skybox_rows;   /* the first rows: their opacity gradient is zeroed before the sparse step */
     int64_t scaffold_rows; /* the first rows: left alone by the scale shrink */
     float max_scale;       /* shrink rows whose largest scale exceeds this (extent * 0.02) */
-    /* out (device, 5 floats): L1, SSIM, photometric loss, then (depth term only) the unweighted
-     * and weighted depth L1; the step's loss is [2] + [4] */
+    /* out (device, 6 floats): L1, SSIM, photometric loss, (depth term only) the unweighted and
+     * weighted depth L1, then the step's loss ([2] + [4], or [2]) */
     float *losses;
     void *stream;
 } gsr_train_step_args;

@@ -4,6 +4,7 @@
 #include <stdint.h>
 #include <string>
 #include "gsr_device.h"
+#include "../../include/gsr_train.h"
 
 namespace gsr {
 
@@ -92,5 +93,28 @@ struct GaussianGrads {
 };
 void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const GeomState &gs, const ImageState &is,
                            const int *radii, const BwdScratch &sc, const GaussianGrads &out, hipStream_t s);
+
+// train.hip: the native train step's fused launches (train_step.hip).  sparse_adam is
+// gsr_sparse_adam_step (flag_ready: the relevance flag is already computed).
+int sparse_adam(int n_groups, const gsr_adam_group *groups, int64_t P, const float *relevance, double beta1,
+                double beta2, double eps, int *flag_scratch, bool flag_ready, hipStream_t s);
+// SSIM map forward (+ masked inverse-depth L1 forward with its gradient for an upstream of 1 when
+// mono != NULL) and the loss epilogue: losses[0..2] photometric, [3..4] depth, [5] total; *flag = 0
+int step_loss_forward(const float *img, const float *gt, int H, int W, double lambda_dssim, void *loss_scratch,
+                      float *gmap, const float *invd, const float *mono, const float *mask, float depth_w,
+                      void *depth_scratch, float *d_invd, float *losses, int *flag, hipStream_t s);
+int launch_exposure_forward(const float *color, const float *E, int64_t npix, float *out, const float *alpha,
+                            hipStream_t s);
+// photometric gradient (x alpha) through the exposure into d_color, the exposure gradient and the
+// exposure optimizer's dense Adam step
+int step_loss_backward(const float *img, const float *gt, const float *gmap, const float *one, double lambda_dssim,
+                       const float *alpha, const float *color, const float *E_view, int64_t npix, float *d_color,
+                       void *exp_scratch, int n_images, int view, const gsr_adam_group &eg, float *exposure_grad,
+                       double b1, double b2, double eps, hipStream_t s);
+// activation backward + skybox lock + relevance flag + densification statistics
+int step_activate_backward(int64_t P, const float *rotation_raw, const float *scales, const float *opac,
+                           const float *d_scales, const float *d_rots, const float *d_opac, float *scaling_grad,
+                           float *rotation_grad, float *opacity_grad, int64_t skybox, int *flag, const int *radii,
+                           const float *d_means2D, float *max_radii2D, float *accum, float *denom, hipStream_t s);
 
 }  // namespace gsr

@@ -223,9 +223,9 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_fwd_kernel(const float *
     }
 }
 
-__global__ __launch_bounds__(1024) void loss_finalize_kernel(const float2 *__restrict__ partials, int n, double inv_n,
-                                                             float *__restrict__ out, float w_l1,
-                                                             float w_ssim) {
+// fixed-order fp64 reduction of the per-block (L1, SSIM) sums (1024 threads)
+__device__ __forceinline__ void loss_finalize_body(const float2 *__restrict__ partials, int n, double inv_n,
+                                                   float *__restrict__ out, float w_l1, float w_ssim) {
     __shared__ double s1[1024], s2[1024];
     double a = 0.0, b = 0.0;
     for (int i = threadIdx.x; i < n; i += 1024) {
@@ -249,6 +249,12 @@ __global__ __launch_bounds__(1024) void loss_finalize_kernel(const float2 *__res
         if (w_l1 >= 0.f)
             out[2] = __fadd_rn(__fmul_rn(w_l1, out[0]), __fmul_rn(w_ssim, __fsub_rn(1.f, out[1])));
     }
+}
+
+__global__ __launch_bounds__(1024) void loss_finalize_kernel(const float2 *__restrict__ partials, int n, double inv_n,
+                                                             float *__restrict__ out, float w_l1,
+                                                             float w_ssim) {
+    loss_finalize_body(partials, n, inv_n, out, w_l1, w_ssim);
 }
 
 constexpr int kBwdIH = kTH + 4 * kR, kBwdIW = kTW + 4 * kR;  // 36 x 84 inputs
@@ -739,15 +745,19 @@ __global__ __launch_bounds__(kAdamThreads) void sparse_adam_kernel(AdamArgs a, c
 // relevant row, lanes across its columns (one contiguous 180-B segment per row).  The per-element
 // arithmetic is adam_element's, so the result is bit-identical to sparse_adam_kernel's; the
 // element-per-thread form launched P x 59 threads that mostly only read rel[row].
-__device__ __forceinline__ void adam_at(const gsr_adam_group &G, int64_t e, float b1, float b2, float omb1,
-                                        float omb2, float eps) {
-    const float g = G.grad[e];
+__device__ __forceinline__ void adam_at_g(const gsr_adam_group &G, int64_t e, float g, float b1, float b2, float omb1,
+                                          float omb2, float eps) {
     const float m = G.exp_avg[e] * b1 + omb1 * g;
     const float v = G.exp_avg_sq[e] * b2 + omb2 * (g * g);
     const float denom = sqrtf(v) / G.bias_correction2_sqrt + eps;
     G.exp_avg[e] = m;
     G.exp_avg_sq[e] = v;
     G.param[e] = G.param[e] + (-G.step_size) * (m / denom);
+}
+
+__device__ __forceinline__ void adam_at(const gsr_adam_group &G, int64_t e, float b1, float b2, float omb1,
+                                        float omb2, float eps) {
+    adam_at_g(G, e, G.grad[e], b1, b2, omb1, omb2, eps);
 }
 
 constexpr int kAdamNarrow = 8;
@@ -841,6 +851,42 @@ __global__ __launch_bounds__(256) void activate_bwd_kernel(int64_t P, const floa
     d_o[i] = g_o[i] * (1.f - y) * y;
 }
 
+// The native step's form: also the skybox lock (rows below `skybox` get a zero opacity gradient,
+// train_single.py:217-223), the sparse Adam's "any relevant row" flag (zeroed earlier in the step)
+// and the densification statistics of the same row (densify_stats_kernel's arithmetic).
+__global__ __launch_bounds__(256) void activate_bwd_step_kernel(
+    int64_t P, const float4 *__restrict__ q_raw, const float *__restrict__ scales, const float *__restrict__ opac,
+    const float *__restrict__ g_s, const float4 *__restrict__ g_q, const float *__restrict__ g_o,
+    float *__restrict__ d_s, float4 *__restrict__ d_q, float *__restrict__ d_o, int64_t skybox, int *__restrict__ flag,
+    const int *__restrict__ radii, const float *__restrict__ g2d, float *__restrict__ maxr, float *__restrict__ accum,
+    float *__restrict__ denom) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    float go = 0.f;
+    if (i < P) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) d_s[3 * i + k] = g_s[3 * i + k] * scales[3 * i + k];
+        const float4 x = q_raw[i], g = g_q[i];
+        const float n = sqrtf(x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w);
+        const float d = fmaxf(n, 1e-12f);
+        const float gd =
+            -(g.x * ((x.x / d) / d) + g.y * ((x.y / d) / d) + g.z * ((x.z / d) / d) + g.w * ((x.w / d) / d));
+        const float gn = n >= 1e-12f && n != 0.f ? gd / n : 0.f;
+        d_q[i] = make_float4(g.x / d + x.x * gn, g.y / d + x.y * gn, g.z / d + x.z * gn, g.w / d + x.w * gn);
+        const float y = opac[i];
+        go = i < skybox ? 0.f : g_o[i] * (1.f - y) * y;
+        d_o[i] = go;
+        const int r = radii[i];
+        if (r > 0) {
+            const float gx = g2d[3 * i], gy = g2d[3 * i + 1];
+            const float nn = sqrtf(gx * gx + gy * gy);
+            maxr[i] = fmaxf(maxr[i], (float)r);
+            accum[i] = fmaxf(nn, accum[i]);
+            denom[i] = denom[i] + 1.f;
+        }
+    }
+    if (__ballot(go != 0.f) != 0 && (threadIdx.x & 63) == 0) *flag = 1;
+}
+
 __global__ __launch_bounds__(256) void shrink_scales_kernel(int64_t P, int64_t first, float *__restrict__ s_raw,
                                                             float limit) {
     const int64_t i = first + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -867,34 +913,78 @@ __device__ __forceinline__ void exposure_pre(const float *__restrict__ E, float 
     o2 = c0 * E[2] + c1 * E[6] + c2 * E[10] + E[11];
 }
 
+// alpha (the native step): the image times the view's alpha mask (train_single.py:117-119) in the
+// same pass -- one rounding, as torch's separate multiply
 __global__ __launch_bounds__(kExpThreads) void exposure_fwd_kernel(const float *__restrict__ color,
                                                                    const float *__restrict__ E, int64_t n,
-                                                                   float *__restrict__ out) {
+                                                                   float *__restrict__ out,
+                                                                   const float *__restrict__ alpha) {
     for (int64_t p = (int64_t)blockIdx.x * kExpThreads + threadIdx.x; p < n; p += (int64_t)gridDim.x * kExpThreads) {
         float o0, o1, o2;
         exposure_pre(E, color[p], color[n + p], color[2 * n + p], o0, o1, o2);
-        out[p] = fminf(fmaxf(o0, 0.f), 1.f);
-        out[n + p] = fminf(fmaxf(o1, 0.f), 1.f);
-        out[2 * n + p] = fminf(fmaxf(o2, 0.f), 1.f);
+        o0 = fminf(fmaxf(o0, 0.f), 1.f);
+        o1 = fminf(fmaxf(o1, 0.f), 1.f);
+        o2 = fminf(fmaxf(o2, 0.f), 1.f);
+        if (alpha) {
+            const float a = alpha[p];
+            o0 = o0 * a;
+            o1 = o1 * a;
+            o2 = o2 * a;
+        }
+        out[p] = o0;
+        out[n + p] = o1;
+        out[2 * n + p] = o2;
     }
 }
 
+// The photometric loss gradient for kPhoto (the native step): gout is formed here from the
+// SSIM gradient field as l1_ssim_bwd_map_kernel forms it (then times the alpha mask, torch's
+// multiply backward) instead of being read, which saves writing and re-reading the (3, H, W)
+// image gradient.  Same loop and reduction order either way, so dcolor and the dE partials are
+// bit-identical.
+struct PhotoGrad {
+    const float *x, *y, *G;  // the (masked) exposed image, the target, the SSIM gradient field
+    const float *dout;       // dL/dloss (device)
+    const float *alpha;      // (H, W) or NULL
+    float inv_n, w_l1, w_ssim;
+};
+
+template <bool kPhoto>
 __global__ __launch_bounds__(kExpThreads) void exposure_bwd_kernel(const float *__restrict__ color,
                                                                    const float *__restrict__ E, int64_t n,
                                                                    const float *__restrict__ gout,
                                                                    float *__restrict__ gcolor,
-                                                                   float *__restrict__ partials) {
+                                                                   float *__restrict__ partials, PhotoGrad pg) {
     __shared__ float red[12][kExpThreads / 64];
     float acc[12];
 #pragma unroll
     for (int k = 0; k < 12; k++) acc[k] = 0.f;
+    float2 up = make_float2(0.f, 0.f);
+    if (kPhoto) up = loss_upstream(pg.dout, pg.inv_n, pg.w_l1, pg.w_ssim);
+    const auto photo = [&](int64_t i, float a) {
+        const float d = pg.x[i] - pg.y[i];
+        const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+        const float g = up.x * sgn + up.y * pg.G[i];
+        return pg.alpha ? g * a : g;
+    };
     for (int64_t p = (int64_t)blockIdx.x * kExpThreads + threadIdx.x; p < n; p += (int64_t)gridDim.x * kExpThreads) {
         const float c0 = color[p], c1 = color[n + p], c2 = color[2 * n + p];
         float o0, o1, o2;
         exposure_pre(E, c0, c1, c2, o0, o1, o2);
-        const float g0 = (o0 >= 0.f && o0 <= 1.f) ? gout[p] : 0.f;
-        const float g1 = (o1 >= 0.f && o1 <= 1.f) ? gout[n + p] : 0.f;
-        const float g2 = (o2 >= 0.f && o2 <= 1.f) ? gout[2 * n + p] : 0.f;
+        float u0, u1, u2;
+        if (kPhoto) {
+            const float a = pg.alpha ? pg.alpha[p] : 1.f;
+            u0 = photo(p, a);
+            u1 = photo(n + p, a);
+            u2 = photo(2 * n + p, a);
+        } else {
+            u0 = gout[p];
+            u1 = gout[n + p];
+            u2 = gout[2 * n + p];
+        }
+        const float g0 = (o0 >= 0.f && o0 <= 1.f) ? u0 : 0.f;
+        const float g1 = (o1 >= 0.f && o1 <= 1.f) ? u1 : 0.f;
+        const float g2 = (o2 >= 0.f && o2 <= 1.f) ? u2 : 0.f;
         gcolor[p] = E[0] * g0 + E[1] * g1 + E[2] * g2;
         gcolor[n + p] = E[4] * g0 + E[5] * g1 + E[6] * g2;
         gcolor[2 * n + p] = E[8] * g0 + E[9] * g1 + E[10] * g2;
@@ -928,6 +1018,29 @@ __global__ __launch_bounds__(768) void exposure_finalize_kernel(const float *__r
     if (lane == 0) dE[k] = s;
 }
 
+// The native step: the exposure gradient's reduction, then the exposure optimizer's dense Adam
+// step over all n_images x 12 values in the same launch (the gradient is dE in the view's row and
+// zero elsewhere, as autograd's index backward leaves it); adam_at's arithmetic, so the bits of
+// gsr_sparse_adam_step's dense step.
+__global__ __launch_bounds__(768) void exposure_finalize_adam_kernel(const float *__restrict__ partials, int nblocks,
+                                                                     int n_images, int view, gsr_adam_group G,
+                                                                     float *__restrict__ grad_out, float b1, float b2,
+                                                                     float omb1, float omb2, float eps) {
+    __shared__ float dE[12];
+    const int k = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float s = 0.f;
+    for (int b = lane; b < nblocks; b += 64) s += partials[(size_t)b * 12 + k];
+    s = wave_sum(s);
+    if (lane == 0) dE[k] = s;
+    __syncthreads();
+    for (int e = threadIdx.x; e < 12 * n_images; e += 768) {
+        const int row = e / 12;
+        const float g = row == view ? dE[e - 12 * view] : 0.f;
+        grad_out[e] = g;
+        adam_at_g(G, e, g, b1, b2, omb1, omb2, eps);
+    }
+}
+
 int exposure_blocks(int64_t n) {
     const int64_t b = (n + kExpThreads - 1) / kExpThreads;
     return (int)(b < kExpBlocks ? (b > 0 ? b : 1) : kExpBlocks);
@@ -954,12 +1067,21 @@ constexpr int kDepthPerBlock = 4 * kDepthThreads * 4;  // float4 per thread, 4 s
 
 __device__ __forceinline__ float depth_term(float x, float y, float m) { return (x - y) * m; }
 
+// kGrad: also dL/dinvdepth for an upstream of 1 (the native step, where the loss is the root):
+// the backward kernel's chain with gout = 1, element for element
+template <bool kGrad>
 __global__ __launch_bounds__(kDepthThreads) void depth_l1_fwd_kernel(const float *__restrict__ invd,
                                                                     const float *__restrict__ mono,
                                                                     const float *__restrict__ mask, int64_t n,
-                                                                    double *__restrict__ partials) {
+                                                                    double *__restrict__ partials, float w,
+                                                                    float inv_count, float *__restrict__ dinvd) {
     __shared__ double red[kDepthThreads / 64];
     const int64_t b0 = (int64_t)blockIdx.x * kDepthPerBlock;
+    const float g = kGrad ? __fmul_rn(__fmul_rn(1.f, w), inv_count) : 0.f;
+    const auto grad = [&](float d, float m) {
+        const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+        return __fmul_rn(__fmul_rn(g, sg), m);
+    };
     float acc = 0.f;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -968,10 +1090,19 @@ __global__ __launch_bounds__(kDepthThreads) void depth_l1_fwd_kernel(const float
             const float4 x = *reinterpret_cast<const float4 *>(invd + i);
             const float4 y = *reinterpret_cast<const float4 *>(mono + i);
             const float4 m = mask ? *reinterpret_cast<const float4 *>(mask + i) : make_float4(1.f, 1.f, 1.f, 1.f);
-            acc += fabsf(depth_term(x.x, y.x, m.x)) + fabsf(depth_term(x.y, y.y, m.y)) +
-                   fabsf(depth_term(x.z, y.z, m.z)) + fabsf(depth_term(x.w, y.w, m.w));
+            const float d0 = depth_term(x.x, y.x, m.x), d1 = depth_term(x.y, y.y, m.y);
+            const float d2 = depth_term(x.z, y.z, m.z), d3 = depth_term(x.w, y.w, m.w);
+            acc += fabsf(d0) + fabsf(d1) + fabsf(d2) + fabsf(d3);
+            if (kGrad)
+                *reinterpret_cast<float4 *>(dinvd + i) =
+                    make_float4(grad(d0, m.x), grad(d1, m.y), grad(d2, m.z), grad(d3, m.w));
         } else {
-            for (int64_t j = i; j < n && j < i + 4; j++) acc += fabsf(depth_term(invd[j], mono[j], mask ? mask[j] : 1.f));
+            for (int64_t j = i; j < n && j < i + 4; j++) {
+                const float mj = mask ? mask[j] : 1.f;
+                const float d = depth_term(invd[j], mono[j], mj);
+                acc += fabsf(d);
+                if (kGrad) dinvd[j] = grad(d, mj);
+            }
         }
     }
     double v = acc;
@@ -986,8 +1117,8 @@ __global__ __launch_bounds__(kDepthThreads) void depth_l1_fwd_kernel(const float
     }
 }
 
-__global__ __launch_bounds__(1024) void depth_l1_finalize_kernel(const double *__restrict__ partials, int nb,
-                                                                 double inv_n, float w, float *__restrict__ out) {
+__device__ __forceinline__ void depth_finalize_body(const double *__restrict__ partials, int nb, double inv_n,
+                                                    float w, float *__restrict__ out) {
     __shared__ double red[1024];
     double a = 0.0;
     for (int i = threadIdx.x; i < nb; i += 1024) a += partials[i];
@@ -1000,6 +1131,29 @@ __global__ __launch_bounds__(1024) void depth_l1_finalize_kernel(const double *_
     if (threadIdx.x == 0) {
         out[0] = (float)(red[0] * inv_n);       // Ll1depth_pure
         out[1] = __fmul_rn(w, out[0]);          // depth_l1_weight(iteration) * Ll1depth_pure
+    }
+}
+
+__global__ __launch_bounds__(1024) void depth_l1_finalize_kernel(const double *__restrict__ partials, int nb,
+                                                                 double inv_n, float w, float *__restrict__ out) {
+    depth_finalize_body(partials, nb, inv_n, w, out);
+}
+
+// The native step's loss epilogue: the photometric and (dp != NULL) depth reductions of
+// loss_finalize_kernel / depth_l1_finalize_kernel, the step's total loss (torch's fp32 add of the
+// two terms) in out[5], and the sparse Adam's relevance flag cleared for activate_bwd_step_kernel.
+__global__ __launch_bounds__(1024) void step_finalize_kernel(const float2 *__restrict__ pp, int np, double inv_np,
+                                                             float w_l1, float w_ssim, const double *__restrict__ dp,
+                                                             int nd, double inv_nd, float w, float *__restrict__ out,
+                                                             int *__restrict__ flag) {
+    loss_finalize_body(pp, np, inv_np, out, w_l1, w_ssim);
+    if (dp) {
+        __syncthreads();
+        depth_finalize_body(dp, nd, inv_nd, w, out + 3);
+    }
+    if (threadIdx.x == 0) {
+        out[5] = dp ? __fadd_rn(out[2], out[4]) : out[2];
+        *flag = 0;
     }
 }
 
@@ -1030,6 +1184,144 @@ void set_lds_attr() {
 }
 
 }  // namespace
+
+// flag_ready: *flag_scratch already holds "some row is relevant" (the native step's
+// activate_bwd_step_kernel computed it), so the any_nonzero pass is skipped.
+int sparse_adam(int n_groups, const gsr_adam_group *groups, int64_t P, const float *relevance, double beta1,
+                double beta2, double eps, int *flag_scratch, bool flag_ready, hipStream_t s) {
+    if (n_groups < 0 || n_groups > kMaxGroups || P < 0 || (P > 0 && (!groups || (relevance && !flag_scratch)))) {
+        set_last_error("gsr_sparse_adam_step: bad group count or NULL pointer");
+        return GSR_ERR_INVALID_ARGUMENT;
+    }
+    if (P == 0 || n_groups == 0) return GSR_OK;
+    AdamArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.n = n_groups;
+    int64_t blocks = 0;
+    for (int i = 0; i < n_groups; i++) {
+        const gsr_adam_group &g = groups[i];
+        if (!g.param || !g.grad || !g.exp_avg || !g.exp_avg_sq || g.width <= 0 ||
+            (g.row_stride != 0 && g.row_stride < g.width)) {
+            set_last_error("gsr_sparse_adam_step: group has a NULL array, non-positive width or row_stride < width");
+            return GSR_ERR_INVALID_ARGUMENT;
+        }
+        a.g[i] = g;
+        if (a.g[i].row_stride == 0) a.g[i].row_stride = g.width;
+        a.block_start[i] = blocks;
+        blocks += (P * g.width + kAdamThreads - 1) / kAdamThreads;
+    }
+    a.block_start[n_groups] = blocks;
+    if (blocks > 0x7fffffff) {
+        set_last_error("gsr_sparse_adam_step: parameter set too large for one launch");
+        return GSR_ERR_UNSUPPORTED;
+    }
+    // relevance NULL: a dense step (torch.optim.Adam over every row), one launch
+    int *flag = relevance ? flag_scratch : nullptr;
+    if (relevance && !flag_ready) {
+        (void)hipMemsetAsync(flag_scratch, 0, sizeof(int), s);
+        hipLaunchKernelGGL(any_nonzero_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, relevance, P,
+                           flag_scratch);
+    }
+    // torch applies python-float hyper-parameters as fp32 scalars: b, (1 - b) rounded from double
+    if (!adam_elementwise())
+        hipLaunchKernelGGL(sparse_adam_rows_kernel, dim3((unsigned)((P + kAdamThreads - 1) / kAdamThreads)),
+                           dim3(kAdamThreads), 0, s, a, relevance, P, (float)beta1, (float)beta2,
+                           (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps, flag);
+    else
+        hipLaunchKernelGGL(sparse_adam_kernel, dim3((unsigned)blocks), dim3(kAdamThreads), 0, s, a, relevance, P,
+                           (float)beta1, (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps,
+                           flag);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_last_error(std::string("gsr_sparse_adam_step: ") + hipGetErrorString(e));
+        return GSR_ERR_DEVICE;
+    }
+    return GSR_OK;
+}
+
+// ---- the native step's fused launches (csrc/train_step.hip) -------------------------------------
+
+int step_loss_forward(const float *img, const float *gt, int H, int W, double lambda_dssim, void *loss_scratch,
+                      float *gmap, const float *invd, const float *mono, const float *mask, float depth_w,
+                      void *depth_scratch, float *d_invd, float *losses, int *flag, hipStream_t s) {
+    set_lds_attr();
+    const int C = 3;
+    const bool tiled = ssim_tiled();
+    const dim3 g = tiled ? loss_grid(C, H, W) : stream_grid(C, H, W);
+    const int np = (int)(g.x * g.y * g.z);
+    float2 *pp = static_cast<float2 *>(loss_scratch);
+    if (tiled)
+        hipLaunchKernelGGL(l1_ssim_grad_kernel<true>, g, dim3(kLossThreads), kBwdLds, s, img, gt, H, W, ssim_window(),
+                           nullptr, 0.f, gmap, pp);
+    else
+        hipLaunchKernelGGL(l1_ssim_stream_kernel<true>, g, dim3(kLossThreads), 0, s, img, gt, H, W, ssim_window(),
+                           nullptr, 0.f, gmap, pp);
+    const int64_t n = (int64_t)H * W;
+    const int nd = (int)std::max<int64_t>(1, (n + kDepthPerBlock - 1) / kDepthPerBlock);
+    double *dp = static_cast<double *>(depth_scratch);
+    if (mono)
+        hipLaunchKernelGGL(depth_l1_fwd_kernel<true>, dim3(nd), dim3(kDepthThreads), 0, s, invd, mono, mask, n, dp,
+                           depth_w, 1.0f / (float)n, d_invd);
+    hipLaunchKernelGGL(step_finalize_kernel, dim3(1), dim3(1024), 0, s, pp, np, 1.0 / ((double)C * H * W),
+                       (float)(1.0 - lambda_dssim), (float)lambda_dssim, mono ? dp : nullptr, nd, 1.0 / (double)n,
+                       depth_w, losses, flag);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_last_error(std::string("step loss forward: ") + hipGetErrorString(e));
+        return GSR_ERR_DEVICE;
+    }
+    return GSR_OK;
+}
+
+int launch_exposure_forward(const float *color, const float *E, int64_t npix, float *out, const float *alpha,
+                            hipStream_t s) {
+    hipLaunchKernelGGL(exposure_fwd_kernel, dim3(exposure_blocks(npix)), dim3(kExpThreads), 0, s, color, E, npix, out,
+                       alpha);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_last_error(std::string("exposure forward: ") + hipGetErrorString(e));
+        return GSR_ERR_DEVICE;
+    }
+    return GSR_OK;
+}
+
+int step_loss_backward(const float *img, const float *gt, const float *gmap, const float *one, double lambda_dssim,
+                       const float *alpha, const float *color, const float *E_view, int64_t npix, float *d_color,
+                       void *exp_scratch, int n_images, int view, const gsr_adam_group &eg, float *exposure_grad,
+                       double b1, double b2, double eps, hipStream_t s) {
+    const int nb = exposure_blocks(npix);
+    float *part = static_cast<float *>(exp_scratch);
+    const PhotoGrad pg{img, gt, gmap, one, alpha, (float)(1.0 / (double)(3 * npix)), (float)(1.0 - lambda_dssim),
+                       (float)lambda_dssim};
+    hipLaunchKernelGGL(exposure_bwd_kernel<true>, dim3(nb), dim3(kExpThreads), 0, s, color, E_view, npix, nullptr,
+                       d_color, part, pg);
+    hipLaunchKernelGGL(exposure_finalize_adam_kernel, dim3(1), dim3(768), 0, s, part, nb, n_images, view, eg,
+                       exposure_grad, (float)b1, (float)b2, (float)(1.0 - b1), (float)(1.0 - b2), (float)eps);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_last_error(std::string("step loss backward: ") + hipGetErrorString(e));
+        return GSR_ERR_DEVICE;
+    }
+    return GSR_OK;
+}
+
+int step_activate_backward(int64_t P, const float *rotation_raw, const float *scales, const float *opac,
+                           const float *d_scales, const float *d_rots, const float *d_opac, float *scaling_grad,
+                           float *rotation_grad, float *opacity_grad, int64_t skybox, int *flag, const int *radii,
+                           const float *d_means2D, float *max_radii2D, float *accum, float *denom, hipStream_t s) {
+    hipLaunchKernelGGL(activate_bwd_step_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, P,
+                       reinterpret_cast<const float4 *>(rotation_raw), scales, opac, d_scales,
+                       reinterpret_cast<const float4 *>(d_rots), d_opac, scaling_grad,
+                       reinterpret_cast<float4 *>(rotation_grad), opacity_grad, skybox, flag, radii, d_means2D,
+                       max_radii2D, accum, denom);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_last_error(std::string("step activation backward: ") + hipGetErrorString(e));
+        return GSR_ERR_DEVICE;
+    }
+    return GSR_OK;
+}
+
 }  // namespace gsr
 
 using namespace gsr;
@@ -1193,55 +1485,8 @@ int gsr_photo_loss_backward(const float *img, const float *gt, const float *ssim
 
 int gsr_sparse_adam_step(int n_groups, const gsr_adam_group *groups, int64_t P, const float *relevance,
                          double beta1, double beta2, double eps, int *flag_scratch, void *stream) {
-    if (n_groups < 0 || n_groups > kMaxGroups || P < 0 || (P > 0 && (!groups || (relevance && !flag_scratch)))) {
-        set_last_error("gsr_sparse_adam_step: bad group count or NULL pointer");
-        return GSR_ERR_INVALID_ARGUMENT;
-    }
-    if (P == 0 || n_groups == 0) return GSR_OK;
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    AdamArgs a;
-    std::memset(&a, 0, sizeof(a));
-    a.n = n_groups;
-    int64_t blocks = 0;
-    for (int i = 0; i < n_groups; i++) {
-        const gsr_adam_group &g = groups[i];
-        if (!g.param || !g.grad || !g.exp_avg || !g.exp_avg_sq || g.width <= 0 ||
-            (g.row_stride != 0 && g.row_stride < g.width)) {
-            set_last_error("gsr_sparse_adam_step: group has a NULL array, non-positive width or row_stride < width");
-            return GSR_ERR_INVALID_ARGUMENT;
-        }
-        a.g[i] = g;
-        if (a.g[i].row_stride == 0) a.g[i].row_stride = g.width;
-        a.block_start[i] = blocks;
-        blocks += (P * g.width + kAdamThreads - 1) / kAdamThreads;
-    }
-    a.block_start[n_groups] = blocks;
-    if (blocks > 0x7fffffff) {
-        set_last_error("gsr_sparse_adam_step: parameter set too large for one launch");
-        return GSR_ERR_UNSUPPORTED;
-    }
-    // relevance NULL: a dense step (torch.optim.Adam over every row), one launch
-    int *flag = relevance ? flag_scratch : nullptr;
-    if (relevance) {
-        (void)hipMemsetAsync(flag_scratch, 0, sizeof(int), s);
-        hipLaunchKernelGGL(any_nonzero_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, relevance, P,
-                           flag_scratch);
-    }
-    // torch applies python-float hyper-parameters as fp32 scalars: b, (1 - b) rounded from double
-    if (!adam_elementwise())
-        hipLaunchKernelGGL(sparse_adam_rows_kernel, dim3((unsigned)((P + kAdamThreads - 1) / kAdamThreads)),
-                           dim3(kAdamThreads), 0, s, a, relevance, P, (float)beta1, (float)beta2,
-                           (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps, flag);
-    else
-        hipLaunchKernelGGL(sparse_adam_kernel, dim3((unsigned)blocks), dim3(kAdamThreads), 0, s, a, relevance, P,
-                           (float)beta1, (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps,
-                           flag);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) {
-        set_last_error(std::string("gsr_sparse_adam_step: ") + hipGetErrorString(e));
-        return GSR_ERR_DEVICE;
-    }
-    return GSR_OK;
+    return gsr::sparse_adam(n_groups, groups, P, relevance, beta1, beta2, eps, flag_scratch, false,
+                            static_cast<hipStream_t>(stream));
 }
 
 int gsr_exposure_forward(const float *color, const float *exposure, int64_t npix, float *out, void *stream) {
@@ -1251,7 +1496,7 @@ int gsr_exposure_forward(const float *color, const float *exposure, int64_t npix
     }
     if (npix == 0) return GSR_OK;
     hipLaunchKernelGGL(exposure_fwd_kernel, dim3(exposure_blocks(npix)), dim3(kExpThreads), 0,
-                       static_cast<hipStream_t>(stream), color, exposure, npix, out);
+                       static_cast<hipStream_t>(stream), color, exposure, npix, out, nullptr);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_last_error(std::string("gsr_exposure_forward: ") + hipGetErrorString(e));
@@ -1272,8 +1517,8 @@ int gsr_exposure_backward(const float *color, const float *exposure, int64_t npi
     const int nb = exposure_blocks(npix);
     float *part = static_cast<float *>(scratch);
     if (npix > 0)
-        hipLaunchKernelGGL(exposure_bwd_kernel, dim3(nb), dim3(kExpThreads), 0, s, color, exposure, npix, dL_dout,
-                           dL_dcolor, part);
+        hipLaunchKernelGGL(exposure_bwd_kernel<false>, dim3(nb), dim3(kExpThreads), 0, s, color, exposure, npix,
+                           dL_dout, dL_dcolor, part, PhotoGrad{});
     else
         (void)hipMemsetAsync(part, 0, sizeof(float) * 12, s);
     hipLaunchKernelGGL(exposure_finalize_kernel, dim3(1), dim3(768), 0, s, part, npix > 0 ? nb : 1, dL_dexposure);
@@ -1382,8 +1627,8 @@ int gsr_depth_l1_forward(const float *invdepth, const float *mono_invdepth, cons
     const int nb = (int)std::max<int64_t>(1, (n + kDepthPerBlock - 1) / kDepthPerBlock);
     double *part = static_cast<double *>(scratch);
     if (n > 0)
-        hipLaunchKernelGGL(depth_l1_fwd_kernel, dim3(nb), dim3(kDepthThreads), 0, s, invdepth, mono_invdepth, mask, n,
-                           part);
+        hipLaunchKernelGGL(depth_l1_fwd_kernel<false>, dim3(nb), dim3(kDepthThreads), 0, s, invdepth, mono_invdepth,
+                           mask, n, part, 0.f, 0.f, nullptr);
     else if (hipMemsetAsync(part, 0, sizeof(double), s) != hipSuccess)
         return GSR_ERR_DEVICE;
     hipLaunchKernelGGL(depth_l1_finalize_kernel, dim3(1), dim3(1024), 0, s, part, nb,

@@ -5,8 +5,8 @@ The Python step issues ~45 launches through autograd nodes, tensor allocations a
 marshalling, and the host takes about as long to do so as the GPU takes to run them.  Here the
 host keeps only the schedule arithmetic of train_single.py (learning rates, Adam step counters and
 bias corrections, the depth-loss weight, the random background) and hands the rest to the
-executor, which issues the same entry points in the same order -- same results as TrainStep (bit
-for bit with the deterministic backward; tests/test_gpu_train.py).
+executor, which runs the same arithmetic in the same order with several launches fused -- same
+results as TrainStep (bit for bit with the deterministic backward; tests/test_gpu_train.py).
 
 The parameters, the Adam moments (the optimizer's own state tensors, so densification and
 checkpoint code keep working on them) and the densification statistics stay the Python
@@ -170,7 +170,7 @@ class NativeTrainStep(TrainStep):
         dm = self.dmask[k]
         a.depth_mask = dm.data_ptr() if (depth and dm is not None) else None
         a.depth_weight = w if depth else 0.0
-        losses = torch.empty(5, dtype=torch.float32, device=dev)  # a fresh tensor per step, as TrainStep's
+        losses = torch.empty(6, dtype=torch.float32, device=dev)  # a fresh tensor per step, as TrainStep's
         a.losses = losses.data_ptr()
         a.stream = stream(dev).value
         K = ctypes.c_int64(0)
@@ -178,4 +178,4 @@ class NativeTrainStep(TrainStep):
         self.last_K = K.value
         self._bg = bg  # keep the background alive until the stream has used it
         self.iteration += 1
-        return losses[2] + losses[4] if depth else losses[2]
+        return losses[5]
