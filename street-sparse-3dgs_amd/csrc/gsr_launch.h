@@ -95,9 +95,11 @@ void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const Ge
                            const int *radii, const BwdScratch &sc, const GaussianGrads &out, hipStream_t s);
 
 // train.hip: the native train step's fused launches (train_step.hip).  sparse_adam is
-// gsr_sparse_adam_step (flag_ready: the relevance flag is already computed).
+// gsr_sparse_adam_step (flag_ready: the relevance flag is already computed; shrink_raw != NULL:
+// train_single.py:235-241's scale shrink of rows >= shrink_first in the same launch).
 int sparse_adam(int n_groups, const gsr_adam_group *groups, int64_t P, const float *relevance, double beta1,
-                double beta2, double eps, int *flag_scratch, bool flag_ready, hipStream_t s);
+                double beta2, double eps, int *flag_scratch, bool flag_ready, hipStream_t s, float *shrink_raw,
+                int64_t shrink_first, float shrink_limit);
 // SSIM map forward (+ masked inverse-depth L1 forward with its gradient for an upstream of 1 when
 // mono != NULL) and the loss epilogue: losses[0..2] photometric, [3..4] depth, [5] total; *flag = 0
 int step_loss_forward(const float *img, const float *gt, int H, int W, double lambda_dssim, void *loss_scratch,

@@ -390,7 +390,7 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_grad_kernel(const float 
     }
 }
 
-// Streaming form of l1_ssim_grad_kernel: a block owns a 64-column x kSegH-row strip of one plane
+// Streaming form of l1_ssim_grad_kernel: a block owns a 64-column x seg-row strip of one plane
 // and walks it top to bottom kStep rows at a time.  Each step stages kStep input rows, and each
 // stage of the separable pipeline (horizontal moments -> vertical moments and dS/d(moment) ->
 // horizontal pass of a/b/c -> vertical pass to G) advances by kStep rows, the vertical passes
@@ -400,9 +400,8 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_grad_kernel(const float 
 // order as l1_ssim_grad_kernel, so G and dx are bit-identical to it.
 constexpr int kStW = 64;
 #ifndef GSR_SSIM_SEG_H
-#define GSR_SSIM_SEG_H 64
+#define GSR_SSIM_SEG_H 0  // rows per strip; 0: chosen per image (stream_seg)
 #endif
-constexpr int kSegH = GSR_SSIM_SEG_H;
 constexpr int kStep = 4;
 constexpr int kRing = 16;
 constexpr int kStIC = kStW + 4 * kR, kStMC = kStW + 2 * kR;  // 84 input, 74 SSIM-map columns
@@ -426,7 +425,7 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_stream_kernel(const floa
                                                                        const float *__restrict__ y, int H, int W,
                                                                        Window win, const float *__restrict__ dout,
                                                                        float inv_n, float *__restrict__ dx,
-                                                                       float2 *__restrict__ partials) {
+                                                                       float2 *__restrict__ partials, int seg) {
     // The staged input rows (read by (2)) and the a/b/c rows ((3) -> (4)) share one buffer: (3)
     // writes after the barrier that ends (2), and the next step's (1) writes after the barrier
     // that ends (4).  40.1 KiB in all, so four workgroups fit a CU.
@@ -444,7 +443,7 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_stream_kernel(const floa
     y += plane_off;
     dx += plane_off;
     const int tid = threadIdx.x;
-    const int cx = blockIdx.x * kStW, r0 = blockIdx.y * kSegH, r1 = min(r0 + kSegH, H);
+    const int cx = blockIdx.x * kStW, r0 = blockIdx.y * seg, r1 = min(r0 + seg, H);
     const float g_l1 = kMap ? 0.f : dout[0] * inv_n, g_ssim = kMap ? 0.f : dout[1] * inv_n;
     const int nsteps = (r1 - r0 + 4 * kR + kStep - 1) / kStep;
     float l1 = 0.f, ss = 0.f;
@@ -761,10 +760,18 @@ __device__ __forceinline__ void adam_at(const gsr_adam_group &G, int64_t e, floa
 }
 
 constexpr int kAdamNarrow = 8;
+// The native step's scale shrink (shrink_scales_kernel's arithmetic), applied by the lane that
+// owns the row after its Adam update: s_raw NULL = none.
+struct ShrinkArgs {
+    float *s_raw;
+    int64_t first;
+    float limit;
+};
+
 __global__ __launch_bounds__(kAdamThreads) void sparse_adam_rows_kernel(AdamArgs a, const float *__restrict__ rel,
                                                                         int64_t P, float b1, float b2, float omb1,
                                                                         float omb2, float eps,
-                                                                        const int *__restrict__ flag) {
+                                                                        const int *__restrict__ flag, ShrinkArgs sh) {
     const int lane = threadIdx.x & 63;
     const int64_t r0 = (((int64_t)blockIdx.x * kAdamThreads + threadIdx.x) >> 6) * 64;
     if (r0 >= P) return;  // wave-uniform
@@ -772,7 +779,20 @@ __global__ __launch_bounds__(kAdamThreads) void sparse_adam_rows_kernel(AdamArgs
     const bool dense = flag == nullptr || *flag == 0;  // no relevance given, or no relevant row
     const bool relv = row < P && (dense || rel[row] != 0.f);
     const uint64_t mask = __ballot(relv);
-    if (mask == 0) return;
+    const auto shrink = [&]() {
+        if (!sh.s_raw || row < sh.first || row >= P) return;
+        float *s = sh.s_raw + 3 * row;
+        const float x = expf(s[0]), y = expf(s[1]), z = expf(s[2]);
+        if (fmaxf(fmaxf(x, y), z) > sh.limit) {
+            s[0] = logf(x * 0.8f);
+            s[1] = logf(y * 0.8f);
+            s[2] = logf(z * 0.8f);
+        }
+    };
+    if (mask == 0) {
+        shrink();
+        return;
+    }
     for (int gi = 0; gi < a.n; gi++) {
         const gsr_adam_group &G = a.g[gi];
         const int w = G.width;
@@ -787,6 +807,7 @@ __global__ __launch_bounds__(kAdamThreads) void sparse_adam_rows_kernel(AdamArgs
             }
         }
     }
+    shrink();
 }
 
 // GSR_ADAM_ELEMENTWISE=1 selects the element-per-thread kernel (same bits; A/B test and
@@ -1047,7 +1068,34 @@ int exposure_blocks(int64_t n) {
 }
 
 dim3 loss_grid(int C, int H, int W) { return dim3((W + kTW - 1) / kTW, (H + kTH - 1) / kTH, C); }
-dim3 stream_grid(int C, int H, int W) { return dim3((W + kStW - 1) / kStW, (H + kSegH - 1) / kSegH, C); }
+// Rows per strip of the streaming kernel: enough strips to fill the resident workgroup slots once
+// (four per CU at 40 KiB of LDS), so every workgroup starts in the first round and the 4R rows of
+// halo each strip recomputes are spread over as many rows as that allows; at least 64 rows.
+int stream_seg(int C, int H, int W) {
+    if (GSR_SSIM_SEG_H > 0) return GSR_SSIM_SEG_H;
+    static int cus[16] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = -1;
+    int n = 256;
+    if (dev >= 0) {
+        if (!cus[dev]) {
+            int c = 0;
+            cus[dev] = hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && c > 0
+                           ? c : 256;
+        }
+        n = cus[dev];
+    }
+    const int cols = (W + kStW - 1) / kStW;
+    const int strips = std::max(1, 4 * n / std::max(1, C * cols));
+    int seg = (H + strips - 1) / strips;
+    seg = (seg + kStep - 1) / kStep * kStep;
+    return std::max(seg, 64);
+}
+
+dim3 stream_grid(int C, int H, int W) {
+    const int seg = stream_seg(C, H, W);
+    return dim3((W + kStW - 1) / kStW, (H + seg - 1) / seg, C);
+}
 
 // GSR_SSIM_TILED=1 selects the 64 x 16 tile gradient kernel instead of the streaming one (same
 // bits; kept for the A/B test and measurements).  Read per call so a test can switch it.
@@ -1188,7 +1236,12 @@ void set_lds_attr() {
 // flag_ready: *flag_scratch already holds "some row is relevant" (the native step's
 // activate_bwd_step_kernel computed it), so the any_nonzero pass is skipped.
 int sparse_adam(int n_groups, const gsr_adam_group *groups, int64_t P, const float *relevance, double beta1,
-                double beta2, double eps, int *flag_scratch, bool flag_ready, hipStream_t s) {
+                double beta2, double eps, int *flag_scratch, bool flag_ready, hipStream_t s, float *shrink_raw,
+                int64_t shrink_first, float shrink_limit) {
+    if (shrink_raw && adam_elementwise()) {
+        set_last_error("sparse Adam: the fused scale shrink needs the row-block kernel");
+        return GSR_ERR_UNSUPPORTED;
+    }
     if (n_groups < 0 || n_groups > kMaxGroups || P < 0 || (P > 0 && (!groups || (relevance && !flag_scratch)))) {
         set_last_error("gsr_sparse_adam_step: bad group count or NULL pointer");
         return GSR_ERR_INVALID_ARGUMENT;
@@ -1226,7 +1279,8 @@ int sparse_adam(int n_groups, const gsr_adam_group *groups, int64_t P, const flo
     if (!adam_elementwise())
         hipLaunchKernelGGL(sparse_adam_rows_kernel, dim3((unsigned)((P + kAdamThreads - 1) / kAdamThreads)),
                            dim3(kAdamThreads), 0, s, a, relevance, P, (float)beta1, (float)beta2,
-                           (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps, flag);
+                           (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps, flag,
+                           ShrinkArgs{shrink_raw, shrink_first, shrink_limit});
     else
         hipLaunchKernelGGL(sparse_adam_kernel, dim3((unsigned)blocks), dim3(kAdamThreads), 0, s, a, relevance, P,
                            (float)beta1, (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps,
@@ -1255,7 +1309,7 @@ int step_loss_forward(const float *img, const float *gt, int H, int W, double la
                            nullptr, 0.f, gmap, pp);
     else
         hipLaunchKernelGGL(l1_ssim_stream_kernel<true>, g, dim3(kLossThreads), 0, s, img, gt, H, W, ssim_window(),
-                           nullptr, 0.f, gmap, pp);
+                           nullptr, 0.f, gmap, pp, stream_seg(C, H, W));
     const int64_t n = (int64_t)H * W;
     const int nd = (int)std::max<int64_t>(1, (n + kDepthPerBlock - 1) / kDepthPerBlock);
     double *dp = static_cast<double *>(depth_scratch);
@@ -1370,7 +1424,7 @@ int gsr_l1_ssim_backward(const float *img, const float *gt, int C, int H, int W,
                            W, ssim_window(), dL_dout, inv_n, dL_dimg, nullptr);
     else
         hipLaunchKernelGGL(l1_ssim_stream_kernel<false>, stream_grid(C, H, W), dim3(kLossThreads), 0, s, img, gt, H,
-                           W, ssim_window(), dL_dout, inv_n, dL_dimg, nullptr);
+                           W, ssim_window(), dL_dout, inv_n, dL_dimg, nullptr, stream_seg(C, H, W));
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_last_error(std::string("gsr_l1_ssim_backward: ") + hipGetErrorString(e));
@@ -1401,7 +1455,7 @@ int forward_with_map(const char *who, const float *img, const float *gt, int C, 
                            nullptr, 0.f, ssim_grad_map, part);
     else
         hipLaunchKernelGGL(l1_ssim_stream_kernel<true>, g, dim3(kLossThreads), 0, s, img, gt, H, W, ssim_window(),
-                           nullptr, 0.f, ssim_grad_map, part);
+                           nullptr, 0.f, ssim_grad_map, part, stream_seg(C, H, W));
     hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(1024), 0, s, part, nb, 1.0 / ((double)C * H * W), out,
                        w_l1, w_ssim);
     const hipError_t e = hipGetLastError();
@@ -1486,7 +1540,7 @@ int gsr_photo_loss_backward(const float *img, const float *gt, const float *ssim
 int gsr_sparse_adam_step(int n_groups, const gsr_adam_group *groups, int64_t P, const float *relevance,
                          double beta1, double beta2, double eps, int *flag_scratch, void *stream) {
     return gsr::sparse_adam(n_groups, groups, P, relevance, beta1, beta2, eps, flag_scratch, false,
-                            static_cast<hipStream_t>(stream));
+                            static_cast<hipStream_t>(stream), nullptr, 0, 0.f);
 }
 
 int gsr_exposure_forward(const float *color, const float *exposure, int64_t npix, float *out, void *stream) {

@@ -162,9 +162,9 @@ int gsr_train_step(gsr_train_ctx *ctx, const gsr_train_step_args *a, int64_t *nu
     int *flag = static_cast<int *>(words);
     float *one = static_cast<float *>(words) + 1;
     if (!ctx->one_written) {  // once per context (the words slot is never re-allocated: 64 B)
-        const float one_h = 1.f;
-        if (hipMemcpy(one, &one_h, sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
-            return fail_step(GSR_ERR_DEVICE, "upstream gradient");
+        const uint32_t w[4] = {0u, 0x3f800000u /* 1.0f */, 0u, 0u};
+        if (hipMemcpy(words, w, sizeof(w), hipMemcpyHostToDevice) != hipSuccess)
+            return fail_step(GSR_ERR_DEVICE, "step words");
         ctx->one_written = true;
     }
     int rc;
@@ -209,9 +209,9 @@ int gsr_train_step(gsr_train_ctx *ctx, const gsr_train_step_args *a, int64_t *nu
                                      a->rotation_grad, a->opacity_grad, a->skybox_rows, flag, radii, d_means2D,
                                      a->max_radii2D, a->xyz_gradient_accum, a->denom, s)))
         return fail_step(rc, "activation backward");
-    if ((rc = sparse_adam(a->n_groups, a->groups, P, a->opacity_grad, a->beta1, a->beta2, a->eps, flag, true, s)))
-        return fail_step(rc, "sparse Adam");
-    if ((rc = gsr_shrink_scales(P, a->scaffold_rows, a->scaling, a->max_scale, sv))) return fail_step(rc, "shrink");
+    if ((rc = sparse_adam(a->n_groups, a->groups, P, a->opacity_grad, a->beta1, a->beta2, a->eps, flag, true, s,
+                          a->scaling, a->scaffold_rows, a->max_scale)))
+        return fail_step(rc, "sparse Adam + shrink");
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_last_error(std::string("gsr_train_step: ") + hipGetErrorString(e));
