@@ -318,7 +318,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
         if (valid) {
             st_out(&out.dmeans2D[3 * i + 0], g[0]);
             st_out(&out.dmeans2D[3 * i + 1], g[1]);
-            st_out(&out.dmeans2D[3 * i + 2], 0.f);
+            if (!out.sparse_rows) st_out(&out.dmeans2D[3 * i + 2], 0.f);  // sparse rows: the liveness, below
             st_out(&out.dopacity[i], g[5]);
         }
     } else {
@@ -354,6 +354,10 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
             live = vis && nz;
         }
     }
+    // sparse rows (the native train step): the liveness column; a dead row's other gradient rows
+    // are not written
+    const bool wr = live || !out.sparse_rows;
+    if (valid && out.sparse_rows) st_out(&out.dmeans2D[3 * i + 2], live ? 1.f : 0.f);
 
     float dm[3] = {0.f, 0.f, 0.f};
     float dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -502,7 +506,8 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
 #pragma unroll
         for (int k = 0; k < 12; k++) {
             const int f = k * kWave + lane, row = f / 12;
-            if (row0 + row < P) st_out(&dst4[f], S[row * kShPitch + (f - row * 12)]);
+            if (row0 + row < P && (!out.sparse_rows || ((need >> row) & 1ull)))
+                st_out(&dst4[f], S[row * kShPitch + (f - row * 12)]);
         }
         if (valid && out.dcolors) {
             out.dcolors[3 * i + 0] = 0.f;
@@ -516,7 +521,9 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
     } else if (has_shs) {
         float *dsh = out.dsh + (size_t)i * M * 3;
         if (!live) {
-            if (vec_sh) {
+            if (out.sparse_rows) {
+                // not written
+            } else if (vec_sh) {
                 float4 *d4 = reinterpret_cast<float4 *>(dsh);
 #pragma unroll
                 for (int c = 0; c < 12; c++) d4[c] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -555,9 +562,11 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
         out.dcolors[3 * i + 1] = g[7];
         out.dcolors[3 * i + 2] = g[8];
     }
-    st_out(&out.dmeans3D[3 * i + 0], dm[0]);
-    st_out(&out.dmeans3D[3 * i + 1], dm[1]);
-    st_out(&out.dmeans3D[3 * i + 2], dm[2]);
+    if (wr) {
+        st_out(&out.dmeans3D[3 * i + 0], dm[0]);
+        st_out(&out.dmeans3D[3 * i + 1], dm[1]);
+        st_out(&out.dmeans3D[3 * i + 2], dm[2]);
+    }
 
     // ---- cov3D -> scale / rotation ----
     if (has_scales) {
@@ -595,10 +604,12 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
             dq[3] = 2.f * (-2.f * z * Gr[0][0] - r * Gr[0][1] + x * Gr[0][2] + r * Gr[1][0] - 2.f * z * Gr[1][1] +
                            y * Gr[1][2] + x * Gr[2][0] + y * Gr[2][1]);
         }
-        st_out(&out.dscales[3 * i + 0], ds[0]);
-        st_out(&out.dscales[3 * i + 1], ds[1]);
-        st_out(&out.dscales[3 * i + 2], ds[2]);
-        st_out(&reinterpret_cast<float4 *>(out.drots)[i], make_float4(dq[0], dq[1], dq[2], dq[3]));
+        if (wr) {
+            st_out(&out.dscales[3 * i + 0], ds[0]);
+            st_out(&out.dscales[3 * i + 1], ds[1]);
+            st_out(&out.dscales[3 * i + 2], ds[2]);
+            st_out(&reinterpret_cast<float4 *>(out.drots)[i], make_float4(dq[0], dq[1], dq[2], dq[3]));
+        }
         if (out.dcov3D)  // optional with scales/rotations (no cov3D_precomp input)
 #pragma unroll
             for (int k = 0; k < 6; k++) out.dcov3D[6 * i + k] = 0.f;

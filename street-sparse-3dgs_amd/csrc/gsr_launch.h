@@ -88,18 +88,29 @@ void launch_render_bwd(const Camera &cam, const GeomState &gs, const BinningStat
                        const BwdScratch &sc, hipStream_t s);
 
 // backward.hip
+// sparse_rows (the native train step only, set_sparse_grad_rows): the rows of Gaussians with ten
+// zero accumulated sums (every gradient zero) are not written in dmeans3D / dsh / dscales / drots,
+// and dmeans2D's third column carries the row's liveness (1 written, 0 not) instead of its zero.
+// Only rows whose opacity gradient is nonzero are read by the sparse Adam (OurAdam's `relevant`,
+// train_single.py:226), and its dense fallback reads the liveness column.
 struct GaussianGrads {
     float *dmeans2D, *dcolors, *dopacity, *dmeans3D, *dcov3D, *dsh, *dscales, *drots;
+    int sparse_rows;
 };
+// rasterizer.hip: gsr_rasterize_backward on this thread writes sparse rows (see above)
+void set_sparse_grad_rows(bool on);
 void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const GeomState &gs, const ImageState &is,
                            const int *radii, const BwdScratch &sc, const GaussianGrads &out, hipStream_t s);
 
 // train.hip: the native train step's fused launches (train_step.hip).  sparse_adam is
 // gsr_sparse_adam_step (flag_ready: the relevance flag is already computed; shrink_raw != NULL:
 // train_single.py:235-241's scale shrink of rows >= shrink_first in the same launch).
+// live3 != NULL (sparse gradient rows): when no row is relevant, the dense fallback takes a zero
+// gradient for rows whose live3[3 row + 2] is 0 (never written) and for the locked skybox rows
+// below `skybox` (train_single.py:217-223 zeroes all six of their gradients).
 int sparse_adam(int n_groups, const gsr_adam_group *groups, int64_t P, const float *relevance, double beta1,
                 double beta2, double eps, int *flag_scratch, bool flag_ready, hipStream_t s, float *shrink_raw,
-                int64_t shrink_first, float shrink_limit);
+                int64_t shrink_first, float shrink_limit, const float *live3 = nullptr, int64_t skybox = 0);
 // SSIM map forward (+ masked inverse-depth L1 forward with its gradient for an upstream of 1 when
 // mono != NULL) and the loss epilogue: losses[0..2] photometric, [3..4] depth, [5] total; *flag = 0
 int step_loss_forward(const float *img, const float *gt, int H, int W, double lambda_dssim, void *loss_scratch,
@@ -113,10 +124,13 @@ int step_loss_backward(const float *img, const float *gt, const float *gmap, con
                        const float *alpha, const float *color, const float *E_view, int64_t npix, float *d_color,
                        void *exp_scratch, int n_images, int view, const gsr_adam_group &eg, float *exposure_grad,
                        double b1, double b2, double eps, hipStream_t s);
-// activation backward + skybox lock + relevance flag + densification statistics
+// activation backward + skybox lock + relevance flag + densification statistics.  sparse_rows:
+// the rasterizer backward wrote sparse rows (GaussianGrads): the scale / rotation gradients of
+// rows it did not write are neither read nor written.
 int step_activate_backward(int64_t P, const float *rotation_raw, const float *scales, const float *opac,
                            const float *d_scales, const float *d_rots, const float *d_opac, float *scaling_grad,
                            float *rotation_grad, float *opacity_grad, int64_t skybox, int *flag, const int *radii,
-                           const float *d_means2D, float *max_radii2D, float *accum, float *denom, hipStream_t s);
+                           const float *d_means2D, float *max_radii2D, float *accum, float *denom, hipStream_t s,
+                           bool sparse_rows = false);
 
 }  // namespace gsr

@@ -40,6 +40,8 @@ std::atomic<int64_t> g_frames{0}, g_reruns{0}, g_local_frames{0}, g_fallbacks{0}
 #define GSR_BINNING_DEFAULT 1
 #endif
 std::atomic<int> g_binning_mode{GSR_BINNING_DEFAULT};
+// the native train step's sparse gradient rows (gsr_launch.h GaussianGrads), per calling thread
+thread_local bool g_sparse_grad_rows = false;
 constexpr int kMaxDevicesK = 64;
 thread_local hipEvent_t g_k_ready[kMaxDevicesK] = {};
 // per device: capacity for the next frame's point list, 0 = none yet.  It is the largest K of the
@@ -353,6 +355,7 @@ std::atomic<int> g_true_scale_grad{0};
 std::atomic<int> g_deterministic{GSR_DETERMINISTIC_DEFAULT};
 }
 bool gsr::true_scale_gradient() { return g_true_scale_grad.load(std::memory_order_relaxed) != 0; }
+void gsr::set_sparse_grad_rows(bool on) { g_sparse_grad_rows = on; }
 
 namespace {
 // Geometry buffers whose accumulator rows the forward did not clear: forwards made with
@@ -816,8 +819,9 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
     BwdScratch sc = carve_bwd(sbase, R_inst, P, atomic, nullptr);
     sc.acc = gs.acc;
 
+    // sparse rows only for plain frames (the cut's rows are scattered to the input rows below)
     GaussianGrads out{dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
-                      dL_drotations};
+                      dL_drotations, g_sparse_grad_rows && R == 0 ? 1 : 0};
     CutRows rows{}, grows{};
     if (R > 0) {
         rows = cut_rows_of(geom_buffer, P, cam.gx, cam.gy, M);

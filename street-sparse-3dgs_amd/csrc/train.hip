@@ -767,11 +767,20 @@ struct ShrinkArgs {
     int64_t first;
     float limit;
 };
+// Sparse gradient rows (the native step): in the dense fallback (no relevant row) a row takes a
+// zero gradient when the rasterizer backward did not write it (live3[3 row + 2] == 0) or when it is
+// a locked skybox row (train_single.py:217-223 zeroes its six gradients).  live3 NULL: every row
+// is read.
+struct DenseRows {
+    const float *live3;
+    int64_t skybox;
+};
 
 __global__ __launch_bounds__(kAdamThreads) void sparse_adam_rows_kernel(AdamArgs a, const float *__restrict__ rel,
                                                                         int64_t P, float b1, float b2, float omb1,
                                                                         float omb2, float eps,
-                                                                        const int *__restrict__ flag, ShrinkArgs sh) {
+                                                                        const int *__restrict__ flag, ShrinkArgs sh,
+                                                                        DenseRows dr) {
     const int lane = threadIdx.x & 63;
     const int64_t r0 = (((int64_t)blockIdx.x * kAdamThreads + threadIdx.x) >> 6) * 64;
     if (r0 >= P) return;  // wave-uniform
@@ -779,6 +788,9 @@ __global__ __launch_bounds__(kAdamThreads) void sparse_adam_rows_kernel(AdamArgs
     const bool dense = flag == nullptr || *flag == 0;  // no relevance given, or no relevant row
     const bool relv = row < P && (dense || rel[row] != 0.f);
     const uint64_t mask = __ballot(relv);
+    // dense fallback over sparse rows: rows whose gradient reads as zero
+    const bool zrow = dense && dr.live3 && row < P && (row < dr.skybox || dr.live3[3 * row + 2] == 0.f);
+    const uint64_t zmask = __ballot(zrow);
     const auto shrink = [&]() {
         if (!sh.s_raw || row < sh.first || row >= P) return;
         float *s = sh.s_raw + 3 * row;
@@ -799,11 +811,16 @@ __global__ __launch_bounds__(kAdamThreads) void sparse_adam_rows_kernel(AdamArgs
         const int64_t rs = G.row_stride;
         if (w <= kAdamNarrow) {
             if (relv)
-                for (int c = 0; c < w; c++) adam_at(G, row * rs + c, b1, b2, omb1, omb2, eps);
+                for (int c = 0; c < w; c++) {
+                    const int64_t e = row * rs + c;
+                    adam_at_g(G, e, zrow ? 0.f : G.grad[e], b1, b2, omb1, omb2, eps);
+                }
         } else {
             for (uint64_t m = mask; m; m &= m - 1) {
-                const int64_t base = (r0 + __builtin_ctzll(m)) * rs;
-                for (int c = lane; c < w; c += 64) adam_at(G, base + c, b1, b2, omb1, omb2, eps);
+                const int rl = __builtin_ctzll(m);
+                const int64_t base = (r0 + rl) * rs;
+                const bool z = (zmask >> rl) & 1ull;
+                for (int c = lane; c < w; c += 64) adam_at_g(G, base + c, z ? 0.f : G.grad[base + c], b1, b2, omb1, omb2, eps);
             }
         }
     }
@@ -880,30 +897,36 @@ __global__ __launch_bounds__(256) void activate_bwd_step_kernel(
     const float *__restrict__ g_s, const float4 *__restrict__ g_q, const float *__restrict__ g_o,
     float *__restrict__ d_s, float4 *__restrict__ d_q, float *__restrict__ d_o, int64_t skybox, int *__restrict__ flag,
     const int *__restrict__ radii, const float *__restrict__ g2d, float *__restrict__ maxr, float *__restrict__ accum,
-    float *__restrict__ denom) {
+    float *__restrict__ denom, int sparse_rows) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     float go = 0.f;
     if (i < P) {
-#pragma unroll
-        for (int k = 0; k < 3; k++) d_s[3 * i + k] = g_s[3 * i + k] * scales[3 * i + k];
-        const float4 x = q_raw[i], g = g_q[i];
-        const float n = sqrtf(x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w);
-        const float d = fmaxf(n, 1e-12f);
-        const float gd =
-            -(g.x * ((x.x / d) / d) + g.y * ((x.y / d) / d) + g.z * ((x.z / d) / d) + g.w * ((x.w / d) / d));
-        const float gn = n >= 1e-12f && n != 0.f ? gd / n : 0.f;
-        d_q[i] = make_float4(g.x / d + x.x * gn, g.y / d + x.y * gn, g.z / d + x.z * gn, g.w / d + x.w * gn);
-        const float y = opac[i];
-        go = i < skybox ? 0.f : g_o[i] * (1.f - y) * y;
-        d_o[i] = go;
         const int r = radii[i];
+        // sparse rows: only the rows the rasterizer backward wrote (liveness in g2d's third column;
+        // invisible rows never are) have scale / rotation gradients -- the others are never relevant
+        bool live = !sparse_rows;
         if (r > 0) {
             const float gx = g2d[3 * i], gy = g2d[3 * i + 1];
+            if (sparse_rows) live = g2d[3 * i + 2] != 0.f;
             const float nn = sqrtf(gx * gx + gy * gy);
             maxr[i] = fmaxf(maxr[i], (float)r);
             accum[i] = fmaxf(nn, accum[i]);
             denom[i] = denom[i] + 1.f;
         }
+        if (live) {
+#pragma unroll
+            for (int k = 0; k < 3; k++) d_s[3 * i + k] = g_s[3 * i + k] * scales[3 * i + k];
+            const float4 x = q_raw[i], g = g_q[i];
+            const float n = sqrtf(x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w);
+            const float d = fmaxf(n, 1e-12f);
+            const float gd =
+                -(g.x * ((x.x / d) / d) + g.y * ((x.y / d) / d) + g.z * ((x.z / d) / d) + g.w * ((x.w / d) / d));
+            const float gn = n >= 1e-12f && n != 0.f ? gd / n : 0.f;
+            d_q[i] = make_float4(g.x / d + x.x * gn, g.y / d + x.y * gn, g.z / d + x.z * gn, g.w / d + x.w * gn);
+        }
+        const float y = opac[i];
+        go = i < skybox ? 0.f : g_o[i] * (1.f - y) * y;
+        d_o[i] = go;
     }
     if (__ballot(go != 0.f) != 0 && (threadIdx.x & 63) == 0) *flag = 1;
 }
@@ -1237,9 +1260,9 @@ void set_lds_attr() {
 // activate_bwd_step_kernel computed it), so the any_nonzero pass is skipped.
 int sparse_adam(int n_groups, const gsr_adam_group *groups, int64_t P, const float *relevance, double beta1,
                 double beta2, double eps, int *flag_scratch, bool flag_ready, hipStream_t s, float *shrink_raw,
-                int64_t shrink_first, float shrink_limit) {
-    if (shrink_raw && adam_elementwise()) {
-        set_last_error("sparse Adam: the fused scale shrink needs the row-block kernel");
+                int64_t shrink_first, float shrink_limit, const float *live3, int64_t skybox) {
+    if ((shrink_raw || live3) && adam_elementwise()) {
+        set_last_error("sparse Adam: the fused scale shrink / sparse rows need the row-block kernel");
         return GSR_ERR_UNSUPPORTED;
     }
     if (n_groups < 0 || n_groups > kMaxGroups || P < 0 || (P > 0 && (!groups || (relevance && !flag_scratch)))) {
@@ -1280,7 +1303,7 @@ int sparse_adam(int n_groups, const gsr_adam_group *groups, int64_t P, const flo
         hipLaunchKernelGGL(sparse_adam_rows_kernel, dim3((unsigned)((P + kAdamThreads - 1) / kAdamThreads)),
                            dim3(kAdamThreads), 0, s, a, relevance, P, (float)beta1, (float)beta2,
                            (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps, flag,
-                           ShrinkArgs{shrink_raw, shrink_first, shrink_limit});
+                           ShrinkArgs{shrink_raw, shrink_first, shrink_limit}, DenseRows{live3, skybox});
     else
         hipLaunchKernelGGL(sparse_adam_kernel, dim3((unsigned)blocks), dim3(kAdamThreads), 0, s, a, relevance, P,
                            (float)beta1, (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps,
@@ -1362,12 +1385,13 @@ int step_loss_backward(const float *img, const float *gt, const float *gmap, con
 int step_activate_backward(int64_t P, const float *rotation_raw, const float *scales, const float *opac,
                            const float *d_scales, const float *d_rots, const float *d_opac, float *scaling_grad,
                            float *rotation_grad, float *opacity_grad, int64_t skybox, int *flag, const int *radii,
-                           const float *d_means2D, float *max_radii2D, float *accum, float *denom, hipStream_t s) {
+                           const float *d_means2D, float *max_radii2D, float *accum, float *denom, hipStream_t s,
+                           bool sparse_rows) {
     hipLaunchKernelGGL(activate_bwd_step_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, P,
                        reinterpret_cast<const float4 *>(rotation_raw), scales, opac, d_scales,
                        reinterpret_cast<const float4 *>(d_rots), d_opac, scaling_grad,
                        reinterpret_cast<float4 *>(rotation_grad), opacity_grad, skybox, flag, radii, d_means2D,
-                       max_radii2D, accum, denom);
+                       max_radii2D, accum, denom, sparse_rows ? 1 : 0);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_last_error(std::string("step activation backward: ") + hipGetErrorString(e));

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -94,6 +95,11 @@ int fail_step(int rc, const char *what) {
     if (rc == GSR_OK) return rc;
     set_last_error(std::string("gsr_train_step: ") + what + ": " + gsr_last_error());
     return rc;
+}
+
+bool step_sparse_rows() {
+    const char *e = std::getenv("GSR_STEP_DENSE_ROWS");  // read per call: A/B runs switch it
+    return !(e != nullptr && e[0] == '1');
 }
 
 int invalid(const char *msg) {
@@ -196,21 +202,29 @@ int gsr_train_step(gsr_train_ctx *ctx, const gsr_train_step_args *a, int64_t *nu
                                  exp_scratch, a->n_images, a->image_index, eg, a->exposure_grad, a->exposure_beta1,
                                  a->exposure_beta2, a->exposure_eps, s)))
         return fail_step(rc, "loss backward");
-    if ((rc = gsr_rasterize_backward(resize_scratch, ctx, (int)P, a->D, a->M, K, a->background, W, H, a->xyz,
+    // sparse gradient rows (gsr_launch.h GaussianGrads): the Gaussians no pixel's backward reached
+    // (88% of the bench scene) have zero gradients and are never relevant to the sparse Adam, so
+    // their 232 B of gradient rows are not written (GSR_STEP_DENSE_ROWS=1: every row, as the
+    // Python-driven step)
+    const bool sparse_rows = step_sparse_rows();
+    set_sparse_grad_rows(sparse_rows);
+    rc = gsr_rasterize_backward(resize_scratch, ctx, (int)P, a->D, a->M, K, a->background, W, H, a->xyz,
                                      a->features, nullptr, scales, 1.0f, rots, nullptr, a->viewmatrix, a->projmatrix,
                                      a->campos, a->tan_fovx, a->tan_fovy, radii, buf_ptr(ctx, kGeom),
                                      buf_ptr(ctx, kBinning), buf_ptr(ctx, kImage), d_color, depth ? d_invd : nullptr,
                                      d_means2D, nullptr, d_opac, a->xyz_grad, nullptr, a->features_grad, d_scales,
-                                     d_rots, nullptr, nullptr, nullptr, nullptr, 0, 0, sv)))
-        return fail_step(rc, "rasterizer backward");
+                                     d_rots, nullptr, nullptr, nullptr, nullptr, 0, 0, sv);
+    set_sparse_grad_rows(false);
+    if (rc) return fail_step(rc, "rasterizer backward");
     // activation backward with the skybox lock, the relevance flag and the densification
     // statistics (train_single.py:193-194, 217-223); then the sparse Adam and the shrink (:225-241)
     if ((rc = step_activate_backward(P, a->rotation, scales, opac, d_scales, d_rots, d_opac, a->scaling_grad,
                                      a->rotation_grad, a->opacity_grad, a->skybox_rows, flag, radii, d_means2D,
-                                     a->max_radii2D, a->xyz_gradient_accum, a->denom, s)))
+                                     a->max_radii2D, a->xyz_gradient_accum, a->denom, s, sparse_rows)))
         return fail_step(rc, "activation backward");
     if ((rc = sparse_adam(a->n_groups, a->groups, P, a->opacity_grad, a->beta1, a->beta2, a->eps, flag, true, s,
-                          a->scaling, a->scaffold_rows, a->max_scale)))
+                          a->scaling, a->scaffold_rows, a->max_scale, sparse_rows ? d_means2D : nullptr,
+                          a->skybox_rows)))
         return fail_step(rc, "sparse Adam + shrink");
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {

@@ -227,10 +227,13 @@ class TrainStep:
         add_densification_stats(radii, grad2d, g.max_radii2D, g.xyz_gradient_accum, g.denom)
 
     def _lock_skybox(self):
-        # train_single.py:217-223 zeroes all six gradients of the skybox rows; the rows then have a
-        # zero opacity gradient, so the sparse step skips them -- zeroing that one gradient is the
-        # whole effect (the others are discarded by zero_grad)
-        self.g._opacity.grad[:self.skybox] = 0
+        # train_single.py:217-223 zeroes all six gradients of the skybox rows.  The rows then have a
+        # zero opacity gradient, so the sparse step skips them; the other gradients matter only in
+        # the dense fallback (no relevant row at all), which reads every row
+        for p in self.optimizer.param_groups:
+            for t in p["params"]:
+                if t.grad is not None and t.shape[0] == self.g.P:
+                    t.grad[:self.skybox] = 0
 
     def _sparse_step(self):
         self.optimizer.step(relevance=self.g._opacity.grad)

@@ -270,6 +270,46 @@ def test_native_step_equals_python_step(depth, alpha, skybox, scaffold):
         assert torch.equal(x, y)
 
 
+@pytest.mark.parametrize("dense_rows", ["0", "1"])
+def test_native_step_sparse_rows_and_dense_fallback(dense_rows, monkeypatch):
+    """The native step's sparse gradient rows (gradient rows of Gaussians no pixel's backward
+    reached are not written: GSR_STEP_DENSE_ROWS unset) and its dense rows give the Python-driven
+    step's bits, including the sparse Adam's dense fallback: after two ordinary steps every opacity
+    is pushed to ~0, no pixel blends, no row is relevant and OurAdam updates every row with zero
+    gradients (train_single.py:226-231, OurAdam.py:214) -- the skybox rows' six gradients zeroed
+    by the lock (:217-223), the never-written rows read as zero."""
+    from helpers import deterministic
+    from gs_train.harness import make_problem
+    from gs_train.native_step import NativeTrainStep
+    monkeypatch.setenv("GSR_STEP_DENSE_ROWS", dense_rows)
+    names = ("_xyz", "_features", "_opacity", "_scaling", "_rotation")
+    out = {}
+    with deterministic():
+        for native in (False, True):
+            torch.manual_seed(0)
+            ts = make_problem(20_000, 256, 192, n_views=2, seed=4, step_cls=NativeTrainStep if native else None,
+                              depth=True, skybox_points=300)
+            torch.manual_seed(3)
+            ts.step()
+            ts.step()
+            with torch.no_grad():
+                ts.g._opacity.fill_(-30.0)
+            before = [getattr(ts.g, n).detach().clone() for n in names]
+            ts.step()
+            params = [getattr(ts.g, n).detach().clone() for n in names]
+            moments = [ts.optimizer.state[getattr(ts.g, n)][k].clone() for n in names for k in ("exp_avg", "exp_avg_sq")]
+            out[native] = (before, params, moments)
+    (b0, pa, ma), (b1, pb, mb) = out[False], out[True]
+    for n, x, y in zip(names, b0, b1):
+        assert torch.equal(x, y), n
+    for n, x, y, x0 in zip(names, pa, pb, b0):
+        assert torch.equal(x, y), n
+        if n != "_opacity":
+            assert not torch.equal(x[300:], x0[300:]), n  # the fallback moved the rows (momentum)
+    for x, y in zip(ma, mb):
+        assert torch.equal(x, y)
+
+
 def test_native_step_follows_densification():
     """The executor re-reads the parameter tensors when densification replaces them."""
     from gs_train.harness import make_problem
