@@ -283,6 +283,140 @@ __device__ __forceinline__ void st_out(float4 *p, float4 v) {
 #define GSR_BWD_SKIP_DEAD 1
 #endif
 
+// The chain rule of one live Gaussian's geometry (its ten accumulated sums g): conic -> 2D
+// covariance -> (3D covariance, mean) through the EWA Jacobian, screen-space mean -> mean3D
+// through projmatrix, inverse depth -> mean3D.  Leaves the 3D-covariance gradient in dcov, the mean
+// gradient in dm, and the covariance, rotation and scale it read in c3 / q / s_in.
+__device__ __forceinline__ void geom_chain(int i, float3 p, const Mat4 &V, const float *__restrict__ projmatrix, float fx,
+                                           float fy, float tanx, float tany, bool has_scales,
+                                           const float *__restrict__ scales, const float *__restrict__ rotations,
+                                           float mod, const float *__restrict__ cov3D_precomp, const float g[10],
+                                           float c3[6], float4 &q, float3 &s_in, float dm[3], float dcov[6]) {
+    // ---- conic -> cov2D -> cov3D and mean ----
+    if (has_scales) {
+        s_in = make_float3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
+        q = reinterpret_cast<const float4 *>(rotations)[i];
+        cov3d_from_scale_rot(s_in, mod, q, c3);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 6; k++) c3[k] = cov3D_precomp[6 * i + k];
+    }
+    const Ewa e = ewa_rows(p, V, fx, fy, tanx, tany);
+    const float a = quad_form(e.m0, c3, e.m0) + 0.3f;
+    const float b = quad_form(e.m0, c3, e.m1);
+    const float c = quad_form(e.m1, c3, e.m1) + 0.3f;
+    const float gca = g[2], gcb = g[3], gcc = g[4];
+    const float denom = a * c - b * b;
+    const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+    float dL_da = 0.f, dL_db = 0.f, dL_dc = 0.f;
+    if (denom2inv != 0.f) {
+        dL_da = denom2inv * (-c * c * gca + 2.f * b * c * gcb + (denom - a * c) * gcc);
+        dL_dc = denom2inv * (-a * a * gcc + 2.f * a * b * gcb + (denom - a * c) * gca);
+        dL_db = denom2inv * 2.f * (b * c * gca - (denom + 2.f * b * b) * gcb + a * b * gcc);
+        const float *m0 = e.m0, *m1 = e.m1;
+        dcov[0] = m0[0] * m0[0] * dL_da + m0[0] * m1[0] * dL_db + m1[0] * m1[0] * dL_dc;
+        dcov[3] = m0[1] * m0[1] * dL_da + m0[1] * m1[1] * dL_db + m1[1] * m1[1] * dL_dc;
+        dcov[5] = m0[2] * m0[2] * dL_da + m0[2] * m1[2] * dL_db + m1[2] * m1[2] * dL_dc;
+        dcov[1] = 2.f * m0[0] * m0[1] * dL_da + (m0[0] * m1[1] + m0[1] * m1[0]) * dL_db +
+                  2.f * m1[0] * m1[1] * dL_dc;
+        dcov[2] = 2.f * m0[0] * m0[2] * dL_da + (m0[0] * m1[2] + m0[2] * m1[0]) * dL_db +
+                  2.f * m1[0] * m1[2] * dL_dc;
+        dcov[4] = 2.f * m0[2] * m0[1] * dL_da + (m0[1] * m1[2] + m0[2] * m1[1]) * dL_db +
+                  2.f * m1[1] * m1[2] * dL_dc;
+    }
+    float Sm0[3], Sm1[3];
+    const float *m0 = e.m0, *m1 = e.m1;
+    Sm0[0] = c3[0] * m0[0] + c3[1] * m0[1] + c3[2] * m0[2];
+    Sm0[1] = c3[1] * m0[0] + c3[3] * m0[1] + c3[4] * m0[2];
+    Sm0[2] = c3[2] * m0[0] + c3[4] * m0[1] + c3[5] * m0[2];
+    Sm1[0] = c3[0] * m1[0] + c3[1] * m1[1] + c3[2] * m1[2];
+    Sm1[1] = c3[1] * m1[0] + c3[3] * m1[1] + c3[4] * m1[2];
+    Sm1[2] = c3[2] * m1[0] + c3[4] * m1[1] + c3[5] * m1[2];
+    float dm0[3], dm1[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        dm0[k] = 2.f * Sm0[k] * dL_da + Sm1[k] * dL_db;
+        dm1[k] = 2.f * Sm1[k] * dL_dc + Sm0[k] * dL_db;
+    }
+    const float *v = V.m;
+    const float dj00 = v[0] * dm0[0] + v[4] * dm0[1] + v[8] * dm0[2];
+    const float dj02 = v[2] * dm0[0] + v[6] * dm0[1] + v[10] * dm0[2];
+    const float dj11 = v[1] * dm1[0] + v[5] * dm1[1] + v[9] * dm1[2];
+    const float dj12 = v[2] * dm1[0] + v[6] * dm1[1] + v[10] * dm1[2];
+    const float tz = 1.f / e.t.z, tz2 = tz * tz, tz3 = tz2 * tz;
+    const float dtx = e.xmul * -fx * tz2 * dj02;
+    const float dty = e.ymul * -fy * tz2 * dj12;
+    const float dtz = -fx * tz2 * dj00 - fy * tz2 * dj11 + (2.f * fx * e.t.x) * tz3 * dj02 +
+                      (2.f * fy * e.t.y) * tz3 * dj12;
+    dm[0] = v[0] * dtx + v[1] * dty + v[2] * dtz;
+    dm[1] = v[4] * dtx + v[5] * dty + v[6] * dtz;
+    dm[2] = v[8] * dtx + v[9] * dty + v[10] * dtz;
+
+    // ---- screen-space mean -> mean3D ----
+    const Mat4 Pm = load_mat4(projmatrix);
+    const float *pr = Pm.m;
+    const float4 mh = xf_point44(p, Pm);
+    const float mw = 1.0f / (mh.w + 0.0000001f);
+    const float mul1 = mh.x * mw * mw, mul2 = mh.y * mw * mw;
+    dm[0] += (pr[0] * mw - pr[3] * mul1) * g[0] + (pr[1] * mw - pr[3] * mul2) * g[1];
+    dm[1] += (pr[4] * mw - pr[7] * mul1) * g[0] + (pr[5] * mw - pr[7] * mul2) * g[1];
+    dm[2] += (pr[8] * mw - pr[11] * mul1) * g[0] + (pr[9] * mw - pr[11] * mul2) * g[1];
+
+    // ---- inverse depth -> mean3D ----
+    {
+        const float3 pv = xf_point43(p, V);
+        const float dz = -g[9] / (pv.z * pv.z);
+        dm[0] += dz * v[2];
+        dm[1] += dz * v[6];
+        dm[2] += dz * v[10];
+    }
+}
+
+// 3D covariance gradient -> scale and rotation gradients (dscale_mod: 1 for upstream's convention,
+// scale_modifier for the exact derivative).
+__device__ __forceinline__ void scale_rot_chain(float4 q, float3 s_in, float mod, float dscale_mod, const float dcov[6],
+                                                float ds[3], float dq[4]) {
+    const float r = q.x, x = q.y, y = q.z, z = q.w;
+    const float s[3] = {mod * s_in.x, mod * s_in.y, mod * s_in.z};
+    const Rot3 R = quat_to_rot(q);
+    const float G3[3][3] = {{dcov[0], 0.5f * dcov[1], 0.5f * dcov[2]},
+                            {0.5f * dcov[1], dcov[3], 0.5f * dcov[4]},
+                            {0.5f * dcov[2], 0.5f * dcov[4], dcov[5]}};
+    float dLL[3][3];
+#pragma unroll
+    for (int rr = 0; rr < 3; rr++)
+#pragma unroll
+        for (int cc = 0; cc < 3; cc++)
+            dLL[rr][cc] = 2.f * (G3[rr][0] * R.m[0][cc] * s[cc] + G3[rr][1] * R.m[1][cc] * s[cc] +
+                                 G3[rr][2] * R.m[2][cc] * s[cc]);
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+        // dscale_mod = 1 (upstream: dL/d(mod s) reported as dL/ds) or mod (the exact
+        // derivative, gsr_set_true_scale_gradient)
+        ds[k] = dscale_mod * (dLL[0][k] * R.m[0][k] + dLL[1][k] * R.m[1][k] + dLL[2][k] * R.m[2][k]);
+    float Gr[3][3];
+#pragma unroll
+    for (int rr = 0; rr < 3; rr++)
+#pragma unroll
+        for (int cc = 0; cc < 3; cc++) Gr[rr][cc] = dLL[rr][cc] * s[cc];
+    dq[0] = 2.f * (-z * Gr[0][1] + y * Gr[0][2] + z * Gr[1][0] - x * Gr[1][2] - y * Gr[2][0] + x * Gr[2][1]);
+    dq[1] = 2.f * (y * Gr[0][1] + z * Gr[0][2] + y * Gr[1][0] - 2.f * x * Gr[1][1] - r * Gr[1][2] +
+                   z * Gr[2][0] + r * Gr[2][1] - 2.f * x * Gr[2][2]);
+    dq[2] = 2.f * (-2.f * y * Gr[0][0] + x * Gr[0][1] + r * Gr[0][2] + x * Gr[1][0] + z * Gr[1][2] -
+                   r * Gr[2][0] + z * Gr[2][1] - 2.f * y * Gr[2][2]);
+    dq[3] = 2.f * (-2.f * z * Gr[0][0] - r * Gr[0][1] + x * Gr[0][2] + r * Gr[1][0] - 2.f * z * Gr[1][1] +
+                   y * Gr[1][2] + x * Gr[2][0] + y * Gr[2][1]);
+}
+
+// d normalize(v)/dv applied to the SH direction gradient gd, added into the mean gradient
+__device__ __forceinline__ void dir_chain(const float dor[3], const float gd[3], float dm[3]) {
+    const float s2 = dor[0] * dor[0] + dor[1] * dor[1] + dor[2] * dor[2];
+    const float inv32 = 1.0f / sqrtf(s2 * s2 * s2);
+    dm[0] += ((s2 - dor[0] * dor[0]) * gd[0] - dor[1] * dor[0] * gd[1] - dor[2] * dor[0] * gd[2]) * inv32;
+    dm[1] += (-dor[0] * dor[1] * gd[0] + (s2 - dor[1] * dor[1]) * gd[1] - dor[2] * dor[1] * gd[2]) * inv32;
+    dm[2] += (-dor[0] * dor[2] * gd[0] - dor[1] * dor[2] * gd[1] + (s2 - dor[2] * dor[2]) * gd[2]) * inv32;
+}
+
 __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
     int P, int D, int M, const float *__restrict__ means3D, const int *__restrict__ radii,
     const float *__restrict__ shs, const uint8_t *__restrict__ clamped, const float *__restrict__ scales,
@@ -368,84 +502,8 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
     float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
     float3 s_in = make_float3(0.f, 0.f, 0.f);
     if (live) {
-        // ---- conic -> cov2D -> cov3D and mean ----
-        if (has_scales) {
-            s_in = make_float3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
-            q = reinterpret_cast<const float4 *>(rotations)[i];
-            cov3d_from_scale_rot(s_in, mod, q, c3);
-        } else {
-#pragma unroll
-            for (int k = 0; k < 6; k++) c3[k] = cov3D_precomp[6 * i + k];
-        }
-        const Ewa e = ewa_rows(p, V, fx, fy, tanx, tany);
-        const float a = quad_form(e.m0, c3, e.m0) + 0.3f;
-        const float b = quad_form(e.m0, c3, e.m1);
-        const float c = quad_form(e.m1, c3, e.m1) + 0.3f;
-        const float gca = g[2], gcb = g[3], gcc = g[4];
-        const float denom = a * c - b * b;
-        const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
-        float dL_da = 0.f, dL_db = 0.f, dL_dc = 0.f;
-        if (denom2inv != 0.f) {
-            dL_da = denom2inv * (-c * c * gca + 2.f * b * c * gcb + (denom - a * c) * gcc);
-            dL_dc = denom2inv * (-a * a * gcc + 2.f * a * b * gcb + (denom - a * c) * gca);
-            dL_db = denom2inv * 2.f * (b * c * gca - (denom + 2.f * b * b) * gcb + a * b * gcc);
-            const float *m0 = e.m0, *m1 = e.m1;
-            dcov[0] = m0[0] * m0[0] * dL_da + m0[0] * m1[0] * dL_db + m1[0] * m1[0] * dL_dc;
-            dcov[3] = m0[1] * m0[1] * dL_da + m0[1] * m1[1] * dL_db + m1[1] * m1[1] * dL_dc;
-            dcov[5] = m0[2] * m0[2] * dL_da + m0[2] * m1[2] * dL_db + m1[2] * m1[2] * dL_dc;
-            dcov[1] = 2.f * m0[0] * m0[1] * dL_da + (m0[0] * m1[1] + m0[1] * m1[0]) * dL_db +
-                      2.f * m1[0] * m1[1] * dL_dc;
-            dcov[2] = 2.f * m0[0] * m0[2] * dL_da + (m0[0] * m1[2] + m0[2] * m1[0]) * dL_db +
-                      2.f * m1[0] * m1[2] * dL_dc;
-            dcov[4] = 2.f * m0[2] * m0[1] * dL_da + (m0[1] * m1[2] + m0[2] * m1[1]) * dL_db +
-                      2.f * m1[1] * m1[2] * dL_dc;
-        }
-        float Sm0[3], Sm1[3];
-        const float *m0 = e.m0, *m1 = e.m1;
-        Sm0[0] = c3[0] * m0[0] + c3[1] * m0[1] + c3[2] * m0[2];
-        Sm0[1] = c3[1] * m0[0] + c3[3] * m0[1] + c3[4] * m0[2];
-        Sm0[2] = c3[2] * m0[0] + c3[4] * m0[1] + c3[5] * m0[2];
-        Sm1[0] = c3[0] * m1[0] + c3[1] * m1[1] + c3[2] * m1[2];
-        Sm1[1] = c3[1] * m1[0] + c3[3] * m1[1] + c3[4] * m1[2];
-        Sm1[2] = c3[2] * m1[0] + c3[4] * m1[1] + c3[5] * m1[2];
-        float dm0[3], dm1[3];
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-            dm0[k] = 2.f * Sm0[k] * dL_da + Sm1[k] * dL_db;
-            dm1[k] = 2.f * Sm1[k] * dL_dc + Sm0[k] * dL_db;
-        }
-        const float *v = V.m;
-        const float dj00 = v[0] * dm0[0] + v[4] * dm0[1] + v[8] * dm0[2];
-        const float dj02 = v[2] * dm0[0] + v[6] * dm0[1] + v[10] * dm0[2];
-        const float dj11 = v[1] * dm1[0] + v[5] * dm1[1] + v[9] * dm1[2];
-        const float dj12 = v[2] * dm1[0] + v[6] * dm1[1] + v[10] * dm1[2];
-        const float tz = 1.f / e.t.z, tz2 = tz * tz, tz3 = tz2 * tz;
-        const float dtx = e.xmul * -fx * tz2 * dj02;
-        const float dty = e.ymul * -fy * tz2 * dj12;
-        const float dtz = -fx * tz2 * dj00 - fy * tz2 * dj11 + (2.f * fx * e.t.x) * tz3 * dj02 +
-                          (2.f * fy * e.t.y) * tz3 * dj12;
-        dm[0] = v[0] * dtx + v[1] * dty + v[2] * dtz;
-        dm[1] = v[4] * dtx + v[5] * dty + v[6] * dtz;
-        dm[2] = v[8] * dtx + v[9] * dty + v[10] * dtz;
-
-        // ---- screen-space mean -> mean3D ----
-        const Mat4 Pm = load_mat4(projmatrix);
-        const float *pr = Pm.m;
-        const float4 mh = xf_point44(p, Pm);
-        const float mw = 1.0f / (mh.w + 0.0000001f);
-        const float mul1 = mh.x * mw * mw, mul2 = mh.y * mw * mw;
-        dm[0] += (pr[0] * mw - pr[3] * mul1) * g[0] + (pr[1] * mw - pr[3] * mul2) * g[1];
-        dm[1] += (pr[4] * mw - pr[7] * mul1) * g[0] + (pr[5] * mw - pr[7] * mul2) * g[1];
-        dm[2] += (pr[8] * mw - pr[11] * mul1) * g[0] + (pr[9] * mw - pr[11] * mul2) * g[1];
-
-        // ---- inverse depth -> mean3D ----
-        {
-            const float3 pv = xf_point43(p, V);
-            const float dz = -g[9] / (pv.z * pv.z);
-            dm[0] += dz * v[2];
-            dm[1] += dz * v[6];
-            dm[2] += dz * v[10];
-        }
+        geom_chain(i, p, V, projmatrix, fx, fy, tanx, tany, has_scales, scales, rotations, mod, cov3D_precomp, g,
+                   c3, q, s_in, dm, dcov);
     }
 
     // ---- colour ----
@@ -491,11 +549,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
                 case 2: sh_backward<2, true>(row, M, true, dir, gc, drow, gd); break;
                 default: sh_backward<3, true>(row, M, true, dir, gc, drow, gd); break;
             }
-            const float s2 = dor[0] * dor[0] + dor[1] * dor[1] + dor[2] * dor[2];
-            const float inv32 = 1.0f / sqrtf(s2 * s2 * s2);
-            dm[0] += ((s2 - dor[0] * dor[0]) * gd[0] - dor[1] * dor[0] * gd[1] - dor[2] * dor[0] * gd[2]) * inv32;
-            dm[1] += (-dor[0] * dor[1] * gd[0] + (s2 - dor[1] * dor[1]) * gd[1] - dor[2] * dor[1] * gd[2]) * inv32;
-            dm[2] += (-dor[0] * dor[2] * gd[0] - dor[1] * dor[2] * gd[1] + (s2 - dor[2] * dor[2]) * gd[2]) * inv32;
+            dir_chain(dor, gd, dm);
         } else {
 #pragma unroll
             for (int c = 0; c < 12; c++) mine[c] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -546,11 +600,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
                 default: sh_backward<3>(sh, M, vec_sh, dir, gc, dsh, gd); break;
             }
             // d normalize(v)/dv applied to the direction gradient
-            const float s2 = dor[0] * dor[0] + dor[1] * dor[1] + dor[2] * dor[2];
-            const float inv32 = 1.0f / sqrtf(s2 * s2 * s2);
-            dm[0] += ((s2 - dor[0] * dor[0]) * gd[0] - dor[1] * dor[0] * gd[1] - dor[2] * dor[0] * gd[2]) * inv32;
-            dm[1] += (-dor[0] * dor[1] * gd[0] + (s2 - dor[1] * dor[1]) * gd[1] - dor[2] * dor[1] * gd[2]) * inv32;
-            dm[2] += (-dor[0] * dor[2] * gd[0] - dor[1] * dor[2] * gd[1] + (s2 - dor[2] * dor[2]) * gd[2]) * inv32;
+            dir_chain(dor, gd, dm);
         }
         if (out.dcolors) {  // optional with shs (no colors_precomp input to differentiate)
             out.dcolors[3 * i + 0] = 0.f;
@@ -573,36 +623,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
         float ds[3] = {0.f, 0.f, 0.f};
         float dq[4] = {0.f, 0.f, 0.f, 0.f};
         if (live) {
-            const float r = q.x, x = q.y, y = q.z, z = q.w;
-            const float s[3] = {mod * s_in.x, mod * s_in.y, mod * s_in.z};
-            const Rot3 R = quat_to_rot(q);
-            const float G3[3][3] = {{dcov[0], 0.5f * dcov[1], 0.5f * dcov[2]},
-                                    {0.5f * dcov[1], dcov[3], 0.5f * dcov[4]},
-                                    {0.5f * dcov[2], 0.5f * dcov[4], dcov[5]}};
-            float dLL[3][3];
-#pragma unroll
-            for (int rr = 0; rr < 3; rr++)
-#pragma unroll
-                for (int cc = 0; cc < 3; cc++)
-                    dLL[rr][cc] = 2.f * (G3[rr][0] * R.m[0][cc] * s[cc] + G3[rr][1] * R.m[1][cc] * s[cc] +
-                                         G3[rr][2] * R.m[2][cc] * s[cc]);
-#pragma unroll
-            for (int k = 0; k < 3; k++)
-                // dscale_mod = 1 (upstream: dL/d(mod s) reported as dL/ds) or mod (the exact
-                // derivative, gsr_set_true_scale_gradient)
-                ds[k] = dscale_mod * (dLL[0][k] * R.m[0][k] + dLL[1][k] * R.m[1][k] + dLL[2][k] * R.m[2][k]);
-            float Gr[3][3];
-#pragma unroll
-            for (int rr = 0; rr < 3; rr++)
-#pragma unroll
-                for (int cc = 0; cc < 3; cc++) Gr[rr][cc] = dLL[rr][cc] * s[cc];
-            dq[0] = 2.f * (-z * Gr[0][1] + y * Gr[0][2] + z * Gr[1][0] - x * Gr[1][2] - y * Gr[2][0] + x * Gr[2][1]);
-            dq[1] = 2.f * (y * Gr[0][1] + z * Gr[0][2] + y * Gr[1][0] - 2.f * x * Gr[1][1] - r * Gr[1][2] +
-                           z * Gr[2][0] + r * Gr[2][1] - 2.f * x * Gr[2][2]);
-            dq[2] = 2.f * (-2.f * y * Gr[0][0] + x * Gr[0][1] + r * Gr[0][2] + x * Gr[1][0] + z * Gr[1][2] -
-                           r * Gr[2][0] + z * Gr[2][1] - 2.f * y * Gr[2][2]);
-            dq[3] = 2.f * (-2.f * z * Gr[0][0] - r * Gr[0][1] + x * Gr[0][2] + r * Gr[1][0] - 2.f * z * Gr[1][1] +
-                           y * Gr[1][2] + x * Gr[2][0] + y * Gr[2][1]);
+            scale_rot_chain(q, s_in, mod, dscale_mod, dcov, ds, dq);
         }
         if (wr) {
             st_out(&out.dscales[3 * i + 0], ds[0]);
@@ -619,12 +640,192 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
     }
 }
 
+// ---- split form (atomic mode, M = 16 SH rows, scales / rotations): the dead rows and the live rows
+// in two launches.  In the single kernel every wave (64 rows, ~8 of them live on the bench scene)
+// carried its live rows' two extra dependent round trips (parameters, then SH rows) in front of
+// the dead rows' zero stores, and its 53-KiB SH staging tile held occupancy to 3 blocks per CU:
+// ~4.2 TB/s.  grad_rows_kernel streams every row's screen-space mean / opacity gradient and the
+// dead rows' zero rows (skipped in sparse-rows mode) and publishes the live rows as one 64-bit
+// mask per wave; grad_live_kernel compacts each 2048-row range's live rows in LDS, so its lanes are
+// all live, and runs the chain rule on them.  The arithmetic is the single kernel's (geom_chain,
+// sh_backward, dir_chain, scale_rot_chain): the bits do not change.
+// The ten per-Gaussian sums: the atomic accumulator row, or (record mode) record_sum's gsum row
+// with the screen-space mean and opacity gradients it wrote; zero for an invisible Gaussian.
+__device__ __forceinline__ void load_sums(const BwdScratch &sc, const GaussianGrads &out, int i, bool vis, float g[10]) {
+    if (sc.atomic) {
+        const float4 a0 = ld_acc(sc.acc + 4 * (size_t)i), a1 = ld_acc(sc.acc + 4 * (size_t)i + 1),
+                     a2 = ld_acc(sc.acc + 4 * (size_t)i + 2);
+        g[0] = a0.x; g[1] = a0.y; g[2] = a0.z; g[3] = a0.w;
+        g[4] = a1.x; g[5] = a1.y; g[6] = a1.z; g[7] = a1.w;
+        g[8] = a2.x; g[9] = a2.y;
+    } else {
+        const float4 s0 = sc.gsum[2 * (size_t)i], s1 = sc.gsum[2 * (size_t)i + 1];
+        g[2] = s0.x; g[3] = s0.y; g[4] = s0.z; g[9] = s0.w;
+        g[6] = s1.x; g[7] = s1.y; g[8] = s1.z;
+        g[0] = vis ? out.dmeans2D[3 * i + 0] : 0.f;
+        g[1] = vis ? out.dmeans2D[3 * i + 1] : 0.f;
+        g[5] = vis ? out.dopacity[i] : 0.f;
+    }
+    if (!vis)
+#pragma unroll
+        for (int k = 0; k < 10; k++) g[k] = 0.f;
+}
+
+__global__ __launch_bounds__(256) void grad_rows_kernel(int P, const int *__restrict__ radii, BwdScratch sc,
+                                                        GaussianGrads out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & (kWave - 1);
+    const bool valid = i < P;
+    const int iv = valid ? i : 0;
+    const bool vis = valid && radii[iv] > 0;
+    float g[10];
+    load_sums(sc, out, iv, vis, g);
+    bool nz = false;
+#pragma unroll
+    for (int t = 0; t < 10; t++) nz = nz || g[t] != 0.f;
+    const bool live = vis && nz;
+    const uint64_t lm = __ballot(live);
+    if (lane == 0 && (i >> 6) < (P + 63) / 64) sc.live[i >> 6] = lm;
+    if (valid) {
+        if (sc.atomic) {  // record mode: written by record_sum_kernel
+            st_out(&out.dmeans2D[3 * i + 0], g[0]);
+            st_out(&out.dmeans2D[3 * i + 1], g[1]);
+            st_out(&out.dopacity[i], g[5]);
+        }
+        if (sc.atomic || out.sparse_rows) st_out(&out.dmeans2D[3 * i + 2], out.sparse_rows && live ? 1.f : 0.f);
+        if (out.dcolors) {
+            out.dcolors[3 * i + 0] = 0.f;
+            out.dcolors[3 * i + 1] = 0.f;
+            out.dcolors[3 * i + 2] = 0.f;
+        }
+        if (out.dcov3D)
+#pragma unroll
+            for (int k = 0; k < 6; k++) out.dcov3D[6 * i + k] = 0.f;
+    }
+    if (out.sparse_rows) return;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (valid && !live) {
+        st_out(&out.dmeans3D[3 * i + 0], 0.f);
+        st_out(&out.dmeans3D[3 * i + 1], 0.f);
+        st_out(&out.dmeans3D[3 * i + 2], 0.f);
+        st_out(&out.dscales[3 * i + 0], 0.f);
+        st_out(&out.dscales[3 * i + 1], 0.f);
+        st_out(&out.dscales[3 * i + 2], 0.f);
+        st_out(&reinterpret_cast<float4 *>(out.drots)[i], z4);
+    }
+    // the wave's 64 zero SH rows as 1 KiB contiguous stores (float4 k*64 + l of the wave's rows)
+    const int64_t row0 = (int64_t)i - lane;
+    float4 *dst4 = reinterpret_cast<float4 *>(out.dsh) + row0 * 12;
+#pragma unroll
+    for (int k = 0; k < 12; k++) {
+        const int f = k * kWave + lane, row = f / 12;
+        if (row0 + row < P && !((lm >> row) & 1ull)) st_out(&dst4[f], z4);
+    }
+}
+
+constexpr int kLiveRange = 2048;  // rows per grad_live_kernel block (32 live masks)
+
+__global__ __launch_bounds__(256) void grad_live_kernel(
+    int P, int D, const float *__restrict__ means3D, const float *__restrict__ shs, const uint8_t *__restrict__ clamped,
+    const float *__restrict__ scales, const float *__restrict__ rotations, float mod, float dscale_mod,
+    const float *__restrict__ viewmatrix, const float *__restrict__ projmatrix, const float *__restrict__ campos_p,
+    float tanx, float tany, float fx, float fy, BwdScratch sc, GaussianGrads out) {
+    __shared__ uint16_t s_list[kLiveRange];
+    __shared__ uint32_t s_off[kLiveRange / 64 + 1];
+    const int t = threadIdx.x;
+    const int64_t base = (int64_t)blockIdx.x * kLiveRange;
+    const int nw = (P + 63) / 64;
+    // thread t owns rows [8t, 8t + 8) of the range: byte t % 8 of live mask t / 8
+    const int wi = (int)(base / 64) + t / 8;
+    const uint64_t m = wi < nw ? sc.live[wi] : 0ull;
+    const uint32_t byte = (uint32_t)(m >> (8 * (t & 7))) & 0xFFu;
+    if ((t & 7) == 0) s_off[t / 8] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (t == 0) {
+        uint32_t run = 0;
+        for (int k = 0; k < kLiveRange / 64; k++) {
+            const uint32_t c = s_off[k];
+            s_off[k] = run;
+            run += c;
+        }
+        s_off[kLiveRange / 64] = run;
+    }
+    __syncthreads();
+    {
+        uint32_t pos = s_off[t / 8] + (uint32_t)__popcll(m & ((1ull << (8 * (t & 7))) - 1ull));
+        for (uint32_t b = byte; b; b &= b - 1u) s_list[pos++] = (uint16_t)(8 * t + __builtin_ctz(b));
+    }
+    __syncthreads();
+    const uint32_t n = s_off[kLiveRange / 64];
+    const Mat4 V = load_mat4(viewmatrix);
+    for (uint32_t e = (uint32_t)t; e < n; e += blockDim.x) {
+        const int i = (int)(base + s_list[e]);
+        float g[10];
+        load_sums(sc, out, i, true, g);
+        const float3 p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
+        float dm[3] = {0.f, 0.f, 0.f};
+        float dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        float c3[6];
+        float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+        float3 s_in = make_float3(0.f, 0.f, 0.f);
+        geom_chain(i, p, V, projmatrix, fx, fy, tanx, tany, true, scales, rotations, mod, nullptr, g, c3, q, s_in, dm,
+                   dcov);
+        if (sc.atomic) {
+            // the row is consumed: cleared for a repeated backward (see preprocess_bwd_kernel)
+            float4 *a = sc.acc + 4 * (size_t)i;
+            const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int k = 0; k < 4; k++) a[k] = z4;
+        }
+        float dir[3], dor[3];
+        sh_dir(p, make_float3(campos_p[0], campos_p[1], campos_p[2]), dir, dor);
+        const uint8_t cl = clamped[i];
+        float gc[3];
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) gc[ch] = (cl >> ch) & 1 ? 0.f : g[6 + ch];
+        float gd[3];
+        const float *sh = shs + (size_t)i * 48;
+        float *dsh = out.dsh + (size_t)i * 48;
+        switch (D) {
+            case 0: sh_backward<0>(sh, 16, true, dir, gc, dsh, gd); break;
+            case 1: sh_backward<1>(sh, 16, true, dir, gc, dsh, gd); break;
+            case 2: sh_backward<2>(sh, 16, true, dir, gc, dsh, gd); break;
+            default: sh_backward<3>(sh, 16, true, dir, gc, dsh, gd); break;
+        }
+        dir_chain(dor, gd, dm);
+        st_out(&out.dmeans3D[3 * i + 0], dm[0]);
+        st_out(&out.dmeans3D[3 * i + 1], dm[1]);
+        st_out(&out.dmeans3D[3 * i + 2], dm[2]);
+        float ds[3], dq[4];
+        scale_rot_chain(q, s_in, mod, dscale_mod, dcov, ds, dq);
+        st_out(&out.dscales[3 * i + 0], ds[0]);
+        st_out(&out.dscales[3 * i + 1], ds[1]);
+        st_out(&out.dscales[3 * i + 2], ds[2]);
+        st_out(&reinterpret_cast<float4 *>(out.drots)[i], make_float4(dq[0], dq[1], dq[2], dq[3]));
+    }
+}
+
+#ifndef GSR_BWD_SPLIT
+#define GSR_BWD_SPLIT 1  // 0: the single preprocess_bwd_kernel for every frame
+#endif
+
 void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const GeomState &gs, const ImageState &is,
                            const int *radii, const BwdScratch &sc, const GaussianGrads &out, hipStream_t s) {
     if (in.P == 0) return;
     if (!sc.atomic)  // atomic mode: the sums are already in GeomState.acc
         hipLaunchKernelGGL(record_sum_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, cam.gx, in.means3D,
                        cam.view, gs.rect8, gs.rect4, gs.offsets, is.boundary, sc, out.dmeans2D, out.dopacity);
+    const bool split = GSR_BWD_SPLIT && GSR_BWD_SKIP_DEAD && sc.live && in.shs && in.M == 16 &&
+                       !in.cov3D_precomp && in.scales && in.rotations &&
+                       reinterpret_cast<uintptr_t>(in.shs) % 16 == 0 && reinterpret_cast<uintptr_t>(out.dsh) % 16 == 0;
+    if (split) {
+        hipLaunchKernelGGL(grad_rows_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, radii, sc, out);
+        hipLaunchKernelGGL(grad_live_kernel, dim3((in.P + kLiveRange - 1) / kLiveRange), dim3(256), 0, s, in.P, in.D,
+                           in.means3D, in.shs, gs.clamped, in.scales, in.rotations, in.scale_modifier,
+                           true_scale_gradient() ? in.scale_modifier : 1.0f, cam.view, cam.proj, cam.campos, cam.tanx,
+                           cam.tany, cam.fx, cam.fy, sc, out);
+        return;
+    }
     hipLaunchKernelGGL(preprocess_bwd_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, in.D, in.M, in.means3D,
                        radii, in.shs, gs.clamped, in.scales, in.rotations, in.scale_modifier,
                        true_scale_gradient() ? in.scale_modifier : 1.0f, in.cov3D_precomp,

@@ -249,6 +249,7 @@ BwdScratch carve_bwd(void *base, int64_t K, int P, bool atomic, size_t *bytes) {
         s.rec = c.take<float4>(4 * (size_t)K);
         s.gsum = c.take<float4>(2 * (size_t)P);
     }
+    s.live = c.take<uint64_t>(((size_t)P + 63) / 64);
     if (bytes) *bytes = align_up(c.off, 256);
     return s;
 }
@@ -814,7 +815,7 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
         cut_off = sbytes;
         sbytes = align_up(c.off, 256);
     }
-    void *sbase = scratch(resize_ctx, std::max<size_t>(sbytes, 256));  // atomic mode: nothing carved
+    void *sbase = scratch(resize_ctx, std::max<size_t>(sbytes, 256));  // atomic mode: the live masks only
     if (!sbase) return fail(GSR_ERR_ALLOCATION, "backward scratch allocation failed");
     BwdScratch sc = carve_bwd(sbase, R_inst, P, atomic, nullptr);
     sc.acc = gs.acc;

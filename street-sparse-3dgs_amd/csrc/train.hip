@@ -776,14 +776,45 @@ struct DenseRows {
     int64_t skybox;
 };
 
+// One wave per (64 consecutive rows, group): blockIdx.y is the group, so the groups' updates run
+// in parallel waves instead of one after the other in one wave (each group's loads were a
+// dependent round trip behind the previous group's stores).  Every element's loads are issued
+// before its stores in program order (the arrays may alias as far as the compiler knows), so a
+// lane's loads are in flight together.  The scale shrink runs in the wave that updates the
+// scaling group (sh_group; -1: group 0's wave, no group writes the scales).
+template <int kW>
+__device__ __forceinline__ void adam_narrow(const gsr_adam_group &G, int64_t base, bool z, float b1, float b2,
+                                            float omb1, float omb2, float eps) {
+    float g[kW], m[kW], v[kW], p[kW];
+#pragma unroll
+    for (int c = 0; c < kW; c++) {
+        g[c] = z ? 0.f : G.grad[base + c];
+        m[c] = G.exp_avg[base + c];
+        v[c] = G.exp_avg_sq[base + c];
+        p[c] = G.param[base + c];
+    }
+#pragma unroll
+    for (int c = 0; c < kW; c++) {
+        const float mm = m[c] * b1 + omb1 * g[c];
+        const float vv = v[c] * b2 + omb2 * (g[c] * g[c]);
+        const float denom = sqrtf(vv) / G.bias_correction2_sqrt + eps;
+        G.exp_avg[base + c] = mm;
+        G.exp_avg_sq[base + c] = vv;
+        G.param[base + c] = p[c] + (-G.step_size) * (mm / denom);
+    }
+}
+
 __global__ __launch_bounds__(kAdamThreads) void sparse_adam_rows_kernel(AdamArgs a, const float *__restrict__ rel,
                                                                         int64_t P, float b1, float b2, float omb1,
                                                                         float omb2, float eps,
                                                                         const int *__restrict__ flag, ShrinkArgs sh,
-                                                                        DenseRows dr) {
-    const int lane = threadIdx.x & 63;
+                                                                        DenseRows dr, int sh_group) {
+    __shared__ uint8_t s_idx[kAdamThreads / 64][64];  // the wave's relevant rows, compacted
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t r0 = (((int64_t)blockIdx.x * kAdamThreads + threadIdx.x) >> 6) * 64;
     if (r0 >= P) return;  // wave-uniform
+    const int gi = (int)blockIdx.y;
+    const gsr_adam_group &G = a.g[gi];
     const int64_t row = r0 + lane;
     const bool dense = flag == nullptr || *flag == 0;  // no relevance given, or no relevant row
     const bool relv = row < P && (dense || rel[row] != 0.f);
@@ -791,40 +822,70 @@ __global__ __launch_bounds__(kAdamThreads) void sparse_adam_rows_kernel(AdamArgs
     // dense fallback over sparse rows: rows whose gradient reads as zero
     const bool zrow = dense && dr.live3 && row < P && (row < dr.skybox || dr.live3[3 * row + 2] == 0.f);
     const uint64_t zmask = __ballot(zrow);
-    const auto shrink = [&]() {
-        if (!sh.s_raw || row < sh.first || row >= P) return;
-        float *s = sh.s_raw + 3 * row;
-        const float x = expf(s[0]), y = expf(s[1]), z = expf(s[2]);
-        if (fmaxf(fmaxf(x, y), z) > sh.limit) {
-            s[0] = logf(x * 0.8f);
-            s[1] = logf(y * 0.8f);
-            s[2] = logf(z * 0.8f);
-        }
-    };
-    if (mask == 0) {
-        shrink();
-        return;
-    }
-    for (int gi = 0; gi < a.n; gi++) {
-        const gsr_adam_group &G = a.g[gi];
-        const int w = G.width;
-        const int64_t rs = G.row_stride;
+    const int w = G.width;
+    const int64_t rs = G.row_stride;
+    if (mask != 0) {
         if (w <= kAdamNarrow) {
-            if (relv)
-                for (int c = 0; c < w; c++) {
-                    const int64_t e = row * rs + c;
-                    adam_at_g(G, e, zrow ? 0.f : G.grad[e], b1, b2, omb1, omb2, eps);
+            if (relv) {
+                const int64_t base = row * rs;
+                switch (w) {
+                    case 1: adam_narrow<1>(G, base, zrow, b1, b2, omb1, omb2, eps); break;
+                    case 3: adam_narrow<3>(G, base, zrow, b1, b2, omb1, omb2, eps); break;
+                    case 4: adam_narrow<4>(G, base, zrow, b1, b2, omb1, omb2, eps); break;
+                    default:
+                        for (int c = 0; c < w; c++) adam_narrow<1>(G, base + c, zrow, b1, b2, omb1, omb2, eps);
+                        break;
                 }
+            }
         } else {
-            for (uint64_t m = mask; m; m &= m - 1) {
-                const int rl = __builtin_ctzll(m);
-                const int64_t base = (r0 + rl) * rs;
-                const bool z = (zmask >> rl) & 1ull;
-                for (int c = lane; c < w; c += 64) adam_at_g(G, base + c, z ? 0.f : G.grad[base + c], b1, b2, omb1, omb2, eps);
+            // wide group: the relevant rows' elements flattened over the lanes (element e of the
+            // wave's n rows: row slot e / w, column e % w), two per lane per trip with both loads
+            // issued first
+            if (relv) s_idx[wv][__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u))] = (uint8_t)lane;
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_wave_barrier();
+            const int tot = __popcll(mask) * w;
+            for (int e0 = 0; e0 < tot; e0 += 128) {
+                int64_t off[2];
+                bool ok[2];
+                float g[2], m[2], v[2], p[2];
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int e = e0 + 64 * h + lane;
+                    ok[h] = e < tot;
+                    const int slot = ok[h] ? e / w : 0;
+                    const int rl = s_idx[wv][slot];
+                    off[h] = (r0 + rl) * rs + (e - slot * w);
+                    const bool z = (zmask >> rl) & 1ull;
+                    if (ok[h]) {
+                        g[h] = z ? 0.f : G.grad[off[h]];
+                        m[h] = G.exp_avg[off[h]];
+                        v[h] = G.exp_avg_sq[off[h]];
+                        p[h] = G.param[off[h]];
+                    }
+                }
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    if (!ok[h]) continue;
+                    const float mm = m[h] * b1 + omb1 * g[h];
+                    const float vv = v[h] * b2 + omb2 * (g[h] * g[h]);
+                    const float denom = sqrtf(vv) / G.bias_correction2_sqrt + eps;
+                    G.exp_avg[off[h]] = mm;
+                    G.exp_avg_sq[off[h]] = vv;
+                    G.param[off[h]] = p[h] + (-G.step_size) * (mm / denom);
+                }
             }
         }
     }
-    shrink();
+    if (gi == (sh_group < 0 ? 0 : sh_group) && sh.s_raw && row >= sh.first && row < P) {
+        float *sr = sh.s_raw + 3 * row;
+        const float x = expf(sr[0]), y = expf(sr[1]), z = expf(sr[2]);
+        if (fmaxf(fmaxf(x, y), z) > sh.limit) {
+            sr[0] = logf(x * 0.8f);
+            sr[1] = logf(y * 0.8f);
+            sr[2] = logf(z * 0.8f);
+        }
+    }
 }
 
 // GSR_ADAM_ELEMENTWISE=1 selects the element-per-thread kernel (same bits; A/B test and
@@ -1300,10 +1361,17 @@ int sparse_adam(int n_groups, const gsr_adam_group *groups, int64_t P, const flo
     }
     // torch applies python-float hyper-parameters as fp32 scalars: b, (1 - b) rounded from double
     if (!adam_elementwise())
-        hipLaunchKernelGGL(sparse_adam_rows_kernel, dim3((unsigned)((P + kAdamThreads - 1) / kAdamThreads)),
+    {
+        // the shrink reads the scales after their Adam update: it runs in the scaling group's wave
+        int sh_group = -1;
+        for (int i = 0; i < n_groups; i++)
+            if (shrink_raw && groups[i].param == shrink_raw) sh_group = i;
+        hipLaunchKernelGGL(sparse_adam_rows_kernel,
+                           dim3((unsigned)((P + kAdamThreads - 1) / kAdamThreads), (unsigned)n_groups),
                            dim3(kAdamThreads), 0, s, a, relevance, P, (float)beta1, (float)beta2,
                            (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps, flag,
-                           ShrinkArgs{shrink_raw, shrink_first, shrink_limit}, DenseRows{live3, skybox});
+                           ShrinkArgs{shrink_raw, shrink_first, shrink_limit}, DenseRows{live3, skybox}, sh_group);
+    }
     else
         hipLaunchKernelGGL(sparse_adam_kernel, dim3((unsigned)blocks), dim3(kAdamThreads), 0, s, a, relevance, P,
                            (float)beta1, (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps,
