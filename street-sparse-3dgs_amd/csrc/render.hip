@@ -445,6 +445,9 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
 #ifndef GSR_TILE_REVERSE
 #define GSR_TILE_REVERSE 0
 #endif
+#ifndef GSR_BWD_HALVES
+#define GSR_BWD_HALVES 1  // 0: halves added per instance (5.5 KiB of LDS, 29 instead of 17 waves per CU): 0.2259 -> 0.2333 ms (r03f)
+#endif
 #ifndef GSR_REC_PAD
 #define GSR_REC_PAD 1  // write the unused 4th float4 of a 64-B record (full 64-B segments)
 #endif
@@ -485,8 +488,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
     __shared__ float4 s_a[kWave];  // x, y, a_s, b_s
     __shared__ float4 s_b[kWave];  // c_s, opacity, list position << 4 | sub-block mask, id / record index
     __shared__ float4 s_c[kWave];  // r, g, b, 1 / depth
-    __shared__ float4 s_d[kWave];  // conic a, b, c
-    __shared__ float2 s_red[kWave * 2 * 5];  // per instance, per half wave: 10 partial sums
+    // per compacted instance: the two half-wave partials of its 10 sums, added once per batch
+    // (GSR_BWD_HALVES = 0: the halves added per instance, half the LDS -- 29 instead of 17 waves per
+    // CU -- but two more VALU per instance: slower, the kernel is issue-bound, not latency-bound)
+    __shared__ float s_red[kWave * 10 * (GSR_BWD_HALVES ? 2 : 1)];
+    __shared__ float4 s_d[GSR_BWD_HALVES ? kWave : 1];  // GSR_BWD_HALVES: conic a, b, c for the epilogue
 
     // Tiles run heaviest first (longest-processing-time order from the forward's per-tile work):
     // with ~2.7 tiles per wave slot, index order leaves a tail of a few heavy tiles.
@@ -587,12 +593,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
             b_inst += cnt;
             b_batches += 1;
         }
+        const uint32_t slot = lane_prefix(keep);
         if (m) {
-            const uint32_t slot = lane_prefix(keep);
             s_a[slot] = make_float4(qa.x, qa.y, qa.z * kHalfLog2e, qa.w * kLog2e);  // scaled conic: gauss_p2
             s_b[slot] = make_float4(qb.x * kHalfLog2e, qb.y, __uint_as_float(pos << 4 | m), __uint_as_float(u));
             s_c[slot] = qc;
-            s_d[slot] = make_float4(qa.z, qa.w, qb.x, 0.f);
+            if (GSR_BWD_HALVES) s_d[slot] = make_float4(qa.z, qa.w, qb.x, 0.f);
         }
         __syncthreads();
         for (uint32_t j = 0; j < cnt; j++) {
@@ -713,25 +719,45 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
             q[3] = dx * q[1];
             // reduce-scatter: lane `rs_slot` of rows 1 and 3 parks its half-wave partial; the two
             // halves are added once per batch below instead of per instance
-            const float h = __any(any) ? wave_rs10(q, lane) : 0.f;
-            if ((lane & 16) && rs_slot >= 0)
-                reinterpret_cast<float *>(s_red)[(j * 2 + (lane >> 5)) * 10 + rs_slot] = h;
+            float h = __any(any) ? wave_rs10(q, lane) : 0.f;
+            if (GSR_BWD_HALVES) {
+                if ((lane & 16) && rs_slot >= 0) s_red[(j * 2 + (lane >> 5)) * 10 + rs_slot] = h;
+            } else {
+                // the two halves added here (lanes l and l ^ 32 hold them): one sum per instance
+                const auto hs = __builtin_amdgcn_permlane32_swap(__float_as_uint(h), __float_as_uint(h), false, false);
+                h = __uint_as_float(hs[0]) + __uint_as_float(hs[1]);
+                if (lane < 16 && rs_slot >= 0) s_red[j * 10 + rs_slot] = h;
+            }
         }
         __syncthreads();
         float r[10];
-        if ((uint32_t)lane < cnt) {
-            const float2 *d = s_red + lane * 10;
+        // GSR_BWD_HALVES: the epilogue in slot order (lane < cnt); otherwise in the batch's own lane
+        // order (its instance's conic, opacity and id are still in this lane's registers)
+        const bool ep = GSR_BWD_HALVES ? (uint32_t)lane < cnt : m != 0u;
+        const uint32_t es = GSR_BWD_HALVES ? (uint32_t)lane : slot;
+        if (ep) {
+            if (GSR_BWD_HALVES) {
+                const float2 *d = reinterpret_cast<const float2 *>(s_red) + es * 10;
 #pragma unroll
-            for (int t = 0; t < 5; t++) {
-                const float2 p0 = d[t], p1 = d[5 + t];
-                r[2 * t] = p0.x + p1.x;
-                r[2 * t + 1] = p0.y + p1.y;
+                for (int t = 0; t < 5; t++) {
+                    const float2 p0 = d[t], p1 = d[5 + t];
+                    r[2 * t] = p0.x + p1.x;
+                    r[2 * t + 1] = p0.y + p1.y;
+                }
+            } else {
+                const float2 *d = reinterpret_cast<const float2 *>(s_red) + es * 5;
+#pragma unroll
+                for (int t = 0; t < 5; t++) {
+                    const float2 p = d[t];
+                    r[2 * t] = p.x;
+                    r[2 * t + 1] = p.y;
+                }
             }
-            const size_t o = 4 * (size_t)__float_as_uint(s_b[lane].w);
+            const size_t o = 4 * (size_t)(GSR_BWD_HALVES ? __float_as_uint(s_b[es].w) : u);
             {
                 // moments -> (dmean2D, dconic): dL/dG = opacity dL/dalpha, dG/d(dx) = -G (a dx + b dy), ...
-                const float4 id = s_d[lane];
-                const float op = s_b[lane].y, ca = id.x, cb = id.y, cc = id.z;
+                const float4 id = GSR_BWD_HALVES ? s_d[es] : make_float4(qa.z, qa.w, qb.x, 0.f);
+                const float op = GSR_BWD_HALVES ? s_b[es].y : qb.y, ca = id.x, cb = id.y, cc = id.z;
                 const float m0 = r[0], m1 = r[1], mxx = r[2], mxy = r[3], myy = r[4];
                 r[0] = -op * fmaf(cb, m1, ca * m0);
                 r[1] = -op * fmaf(cb, m0, cc * m1);
@@ -756,11 +782,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
             // read its halves), then ten atomic instructions: lane l of round k adds value
             // (64k + l) % 10 of instance (64k + l) / 10 -- consecutive lanes, consecutive floats
             // of one Gaussian's row
-            __syncthreads();
-            float *st = reinterpret_cast<float *>(s_red);
-            if ((uint32_t)lane < cnt) {
+            if (GSR_BWD_HALVES) __syncthreads();  // otherwise each lane rewrites the slot it read
+            float *st = s_red;
+            if (ep) {
 #pragma unroll
-                for (int t = 0; t < 10; t++) st[lane * 10 + t] = r[t];
+                for (int t = 0; t < 10; t++) st[es * 10 + t] = r[t];
             }
             __syncthreads();
 #pragma unroll 1
