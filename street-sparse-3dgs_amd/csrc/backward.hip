@@ -291,11 +291,16 @@ __device__ __forceinline__ void geom_chain(int i, float3 p, const Mat4 &V, const
                                            float fy, float tanx, float tany, bool has_scales,
                                            const float *__restrict__ scales, const float *__restrict__ rotations,
                                            float mod, const float *__restrict__ cov3D_precomp, const float g[10],
-                                           float c3[6], float4 &q, float3 &s_in, float dm[3], float dcov[6]) {
+                                           float c3[6], float4 &q, float3 &s_in, float dm[3], float dcov[6],
+                                           int raw) {
     // ---- conic -> cov2D -> cov3D and mean ----
     if (has_scales) {
         s_in = make_float3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
         q = reinterpret_cast<const float4 *>(rotations)[i];
+        if (raw) {  // pre-activation parameters (GaussianInputs.raw)
+            s_in = make_float3(act_scale(s_in.x), act_scale(s_in.y), act_scale(s_in.z));
+            q = act_rot(q);
+        }
         cov3d_from_scale_rot(s_in, mod, q, c3);
     } else {
 #pragma unroll
@@ -423,7 +428,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
     const float *__restrict__ rotations, float mod, float dscale_mod, const float *__restrict__ cov3D_precomp,
     const float *__restrict__ viewmatrix, const float *__restrict__ projmatrix, const float *__restrict__ campos_p,
     float tanx, float tany, float fx, float fy, int gx, const uint32_t *__restrict__ tiles,
-    const GRec *__restrict__ rec, const uint64_t *__restrict__ boundary, BwdScratch sc, GaussianGrads out) {
+    const GRec *__restrict__ rec, const uint64_t *__restrict__ boundary, BwdScratch sc, GaussianGrads out, int raw) {
     __shared__ float4 s_sh[4 * kWave * kShPitch];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & (kWave - 1);
@@ -503,7 +508,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
     float3 s_in = make_float3(0.f, 0.f, 0.f);
     if (live) {
         geom_chain(i, p, V, projmatrix, fx, fy, tanx, tany, has_scales, scales, rotations, mod, cov3D_precomp, g,
-                   c3, q, s_in, dm, dcov);
+                   c3, q, s_in, dm, dcov, raw);
     }
 
     // ---- colour ----
@@ -729,7 +734,7 @@ __global__ __launch_bounds__(256) void grad_live_kernel(
     int P, int D, const float *__restrict__ means3D, const float *__restrict__ shs, const uint8_t *__restrict__ clamped,
     const float *__restrict__ scales, const float *__restrict__ rotations, float mod, float dscale_mod,
     const float *__restrict__ viewmatrix, const float *__restrict__ projmatrix, const float *__restrict__ campos_p,
-    float tanx, float tany, float fx, float fy, BwdScratch sc, GaussianGrads out) {
+    float tanx, float tany, float fx, float fy, BwdScratch sc, GaussianGrads out, int raw) {
     __shared__ uint16_t s_list[kLiveRange];
     __shared__ uint32_t s_off[kLiveRange / 64 + 1];
     const int t = threadIdx.x;
@@ -769,7 +774,7 @@ __global__ __launch_bounds__(256) void grad_live_kernel(
         float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
         float3 s_in = make_float3(0.f, 0.f, 0.f);
         geom_chain(i, p, V, projmatrix, fx, fy, tanx, tany, true, scales, rotations, mod, nullptr, g, c3, q, s_in, dm,
-                   dcov);
+                   dcov, raw);
         if (sc.atomic) {
             // the row is consumed: cleared for a repeated backward (see preprocess_bwd_kernel)
             float4 *a = sc.acc + 4 * (size_t)i;
@@ -823,14 +828,14 @@ void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const Ge
         hipLaunchKernelGGL(grad_live_kernel, dim3((in.P + kLiveRange - 1) / kLiveRange), dim3(256), 0, s, in.P, in.D,
                            in.means3D, in.shs, gs.clamped, in.scales, in.rotations, in.scale_modifier,
                            true_scale_gradient() ? in.scale_modifier : 1.0f, cam.view, cam.proj, cam.campos, cam.tanx,
-                           cam.tany, cam.fx, cam.fy, sc, out);
+                           cam.tany, cam.fx, cam.fy, sc, out, in.raw);
         return;
     }
     hipLaunchKernelGGL(preprocess_bwd_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, in.D, in.M, in.means3D,
                        radii, in.shs, gs.clamped, in.scales, in.rotations, in.scale_modifier,
                        true_scale_gradient() ? in.scale_modifier : 1.0f, in.cov3D_precomp,
                        cam.view, cam.proj, cam.campos, cam.tanx, cam.tany, cam.fx, cam.fy, cam.gx, gs.tiles, gs.rec,
-                       is.boundary, sc, out);
+                       is.boundary, sc, out, in.raw);
 }
 
 }  // namespace gsr

@@ -146,6 +146,16 @@ __device__ __forceinline__ float quad_form(const float a[3], const float c[6], c
     return a[0] * s0 + a[1] * s1 + a[2] * s2;
 }
 
+// Parameter activations (scene/gaussian_model.py:39-47, getters :125-156), in torch's op order:
+// exp, x / max(||x||, 1e-12), sigmoid.  train.hip's activate kernels and the raw-parameter mode of
+// the rasterizer (GaussianInputs.raw: the native train step) use these, so both form the same bits.
+__device__ __forceinline__ float act_scale(float s) { return expf(s); }
+__device__ __forceinline__ float4 act_rot(float4 q) {
+    const float d = fmaxf(sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w), 1e-12f);
+    return make_float4(q.x / d, q.y / d, q.z / d, q.w / d);
+}
+__device__ __forceinline__ float act_opacity(float o) { return 1.f / (1.f + expf(-o)); }
+
 __device__ __forceinline__ void sh_dir(float3 mean, float3 campos, float dir[3], float dor[3]) {
     dor[0] = mean.x - campos.x;
     dor[1] = mean.y - campos.y;

@@ -21,11 +21,18 @@ struct Camera {
     int W, H, gx, gy;
 };
 
+// raw (the native train step, set_raw_params): scales / rotations / opacities are the
+// pre-activation parameters (log-scales, unnormalised quaternions, logits), activated in the
+// kernels that read them (gsr_device.h act_*), so no activated copy is written and re-read.
 struct GaussianInputs {
     int P, D, M;
     const float *means3D, *shs, *colors_precomp, *opacities, *scales, *rotations, *cov3D_precomp;
     float scale_modifier;
+    int raw;
 };
+// rasterizer.hip: gsr_rasterize_forward_ex / gsr_rasterize_backward on this thread take raw
+// parameters (plain frames: no precomputed covariance, no hierarchy cut)
+void set_raw_params(bool on);
 
 // preprocess.hip
 void launch_preprocess(const GaussianInputs &in, const Camera &cam, const GeomState &gs, int *radii,
@@ -127,10 +134,12 @@ int step_loss_backward(const float *img, const float *gt, const float *gmap, con
 // activation backward + skybox lock + relevance flag + densification statistics.  sparse_rows:
 // the rasterizer backward wrote sparse rows (GaussianGrads): the scale / rotation gradients of
 // rows it did not write are neither read nor written.
+// scales / opac NULL: recomputed from the raw parameters (scaling_raw, opacity_raw) -- the raw mode
 int step_activate_backward(int64_t P, const float *rotation_raw, const float *scales, const float *opac,
                            const float *d_scales, const float *d_rots, const float *d_opac, float *scaling_grad,
                            float *rotation_grad, float *opacity_grad, int64_t skybox, int *flag, const int *radii,
                            const float *d_means2D, float *max_radii2D, float *accum, float *denom, hipStream_t s,
-                           bool sparse_rows = false);
+                           bool sparse_rows = false, const float *scaling_raw = nullptr,
+                           const float *opacity_raw = nullptr);
 
 }  // namespace gsr

@@ -25,7 +25,8 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
     const float *__restrict__ rotations, const float *__restrict__ opacities, const float *__restrict__ shs,
     const float *__restrict__ colors_precomp, const float *__restrict__ cov3D_precomp,
     const float *__restrict__ viewmatrix, const float *__restrict__ projmatrix, const float *__restrict__ campos,
-    int W, int H, float tanx, float tany, float fx, float fy, int gx, int gy, GeomState gs, int *__restrict__ radii) {
+    int W, int H, float tanx, float tany, float fx, float fy, int gx, int gy, GeomState gs, int *__restrict__ radii,
+    int raw) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     // the depth sort's control words (tickets, histograms, lookback status) start at zero
     for (uint32_t c = (uint32_t)i; c < gs.ctrl_zero; c += gridDim.x * blockDim.x) gs.ctrl[c] = 0u;
@@ -51,9 +52,13 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
 #pragma unroll
         for (int k = 0; k < 6; k++) c3[k] = cov3D_precomp[6 * i + k];
     } else {
-        const float3 s = make_float3(ldp(scales + 3 * i), ldp(scales + 3 * i + 1), ldp(scales + 3 * i + 2));
-        const float4 q = make_float4(ldp(rotations + 4 * i), ldp(rotations + 4 * i + 1), ldp(rotations + 4 * i + 2),
-                                     ldp(rotations + 4 * i + 3));
+        float3 s = make_float3(ldp(scales + 3 * i), ldp(scales + 3 * i + 1), ldp(scales + 3 * i + 2));
+        float4 q = make_float4(ldp(rotations + 4 * i), ldp(rotations + 4 * i + 1), ldp(rotations + 4 * i + 2),
+                               ldp(rotations + 4 * i + 3));
+        if (raw) {  // the native step's pre-activation parameters (GaussianInputs.raw)
+            s = make_float3(act_scale(s.x), act_scale(s.y), act_scale(s.z));
+            q = act_rot(q);
+        }
         cov3d_from_scale_rot(s, mod, q, c3);
     }
     const Ewa e = ewa_rows(p, V, fx, fy, tanx, tany);
@@ -108,7 +113,7 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
         col = make_float4(rgb[0], rgb[1], rgb[2], 0.f);
     }
     if (!kSplitColor) col.w = 1.f / pv.z;
-    const float op = ldp(opacities + i);
+    const float op = raw ? act_opacity(ldp(opacities + i)) : ldp(opacities + i);
     const float ca_ = cc * det_inv, cb_ = -cb * det_inv, cc_ = ca * det_inv;
     // Half-extents of the region where alpha = op * exp(power) can reach 1/255:
     // power >= -t, t = ln(255 op)  <=>  d^T Q d <= 2t  ->  |dx| <= sqrt(2t (Q^-1)_xx).  Evaluated
@@ -258,7 +263,7 @@ void launch_preprocess(const GaussianInputs &in, const Camera &cam, const GeomSt
 #define GSR_PRE_ARGS                                                                                                 \
     in.P, in.D, in.M, in.means3D, in.scales, in.scale_modifier, in.rotations, in.opacities, in.shs, in.colors_precomp, \
         in.cov3D_precomp, cam.view, cam.proj, cam.campos, cam.W, cam.H, cam.tanx, cam.tany, cam.fx, cam.fy, cam.gx,   \
-        cam.gy, gs, radii
+        cam.gy, gs, radii, in.raw
     if (split_color)
         hipLaunchKernelGGL((preprocess_kernel<true, true>), dim3(blocks), dim3(256), 0, s, GSR_PRE_ARGS);
     else if (vec)

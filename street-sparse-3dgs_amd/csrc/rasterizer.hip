@@ -42,6 +42,7 @@ std::atomic<int64_t> g_frames{0}, g_reruns{0}, g_local_frames{0}, g_fallbacks{0}
 std::atomic<int> g_binning_mode{GSR_BINNING_DEFAULT};
 // the native train step's sparse gradient rows (gsr_launch.h GaussianGrads), per calling thread
 thread_local bool g_sparse_grad_rows = false;
+thread_local bool g_raw_params = false;  // GaussianInputs.raw, per calling thread
 constexpr int kMaxDevicesK = 64;
 thread_local hipEvent_t g_k_ready[kMaxDevicesK] = {};
 // per device: capacity for the next frame's point list, 0 = none yet.  It is the largest K of the
@@ -357,6 +358,7 @@ std::atomic<int> g_deterministic{GSR_DETERMINISTIC_DEFAULT};
 }
 bool gsr::true_scale_gradient() { return g_true_scale_grad.load(std::memory_order_relaxed) != 0; }
 void gsr::set_sparse_grad_rows(bool on) { g_sparse_grad_rows = on; }
+void gsr::set_raw_params(bool on) { g_raw_params = on; }
 
 namespace {
 // Geometry buffers whose accumulator rows the forward did not clear: forwards made with
@@ -507,8 +509,10 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
         if ((rc = check("hierarchy cut blend", debug, s))) return rc;
     }
 
+    if (g_raw_params && (R > 0 || cov3D_precomp))
+        return fail(GSR_ERR_UNSUPPORTED, "raw parameters with a hierarchy cut or precomputed covariances");
     GaussianInputs in{P, D, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp,
-                      scale_modifier};
+                      scale_modifier, g_raw_params ? 1 : 0};
     hipStream_t side = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
     // GSR_COLOR_SERIAL=1 runs the SH colour pass on the main stream right after the preprocess:
@@ -844,8 +848,10 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
                            hipSuccess)
             return fail(GSR_ERR_DEVICE, "means2D gradient clear failed");
     }
+    if (g_raw_params && (R > 0 || cov3D_precomp))
+        return fail(GSR_ERR_UNSUPPORTED, "raw parameters with a hierarchy cut or precomputed covariances");
     GaussianInputs in{P, D, M, means3D, shs, colors_precomp, nullptr, scales, rotations, cov3D_precomp,
-                      scale_modifier};
+                      scale_modifier, g_raw_params ? 1 : 0};
     {
         StageTimer st(6, s);
         if (R_inst > 0) launch_render_bwd(cam, gs, bs, is, radii, background, dL_dpix, dL_dinvdepth, sc, s);

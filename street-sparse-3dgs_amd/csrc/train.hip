@@ -922,11 +922,9 @@ __global__ __launch_bounds__(256) void activate_fwd_kernel(int64_t P, const floa
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P) return;
 #pragma unroll
-    for (int k = 0; k < 3; k++) scales[3 * i + k] = expf(s_raw[3 * i + k]);
-    const float4 q = q_raw[i];
-    const float d = fmaxf(sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w), 1e-12f);
-    rots[i] = make_float4(q.x / d, q.y / d, q.z / d, q.w / d);
-    opac[i] = 1.f / (1.f + expf(-o_raw[i]));
+    for (int k = 0; k < 3; k++) scales[3 * i + k] = act_scale(s_raw[3 * i + k]);
+    rots[i] = act_rot(q_raw[i]);
+    opac[i] = act_opacity(o_raw[i]);
 }
 
 __global__ __launch_bounds__(256) void activate_bwd_kernel(int64_t P, const float4 *__restrict__ q_raw,
@@ -958,7 +956,9 @@ __global__ __launch_bounds__(256) void activate_bwd_step_kernel(
     const float *__restrict__ g_s, const float4 *__restrict__ g_q, const float *__restrict__ g_o,
     float *__restrict__ d_s, float4 *__restrict__ d_q, float *__restrict__ d_o, int64_t skybox, int *__restrict__ flag,
     const int *__restrict__ radii, const float *__restrict__ g2d, float *__restrict__ maxr, float *__restrict__ accum,
-    float *__restrict__ denom, int sparse_rows) {
+    float *__restrict__ denom, int sparse_rows, const float *__restrict__ s_raw, const float *__restrict__ o_raw) {
+    // scales / opac NULL: the raw mode (the rasterizer read the pre-activation parameters): the
+    // activations are recomputed here from s_raw / o_raw, with the forward's expressions
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     float go = 0.f;
     if (i < P) {
@@ -976,7 +976,8 @@ __global__ __launch_bounds__(256) void activate_bwd_step_kernel(
         }
         if (live) {
 #pragma unroll
-            for (int k = 0; k < 3; k++) d_s[3 * i + k] = g_s[3 * i + k] * scales[3 * i + k];
+            for (int k = 0; k < 3; k++)
+                d_s[3 * i + k] = g_s[3 * i + k] * (scales ? scales[3 * i + k] : act_scale(s_raw[3 * i + k]));
             const float4 x = q_raw[i], g = g_q[i];
             const float n = sqrtf(x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w);
             const float d = fmaxf(n, 1e-12f);
@@ -985,7 +986,7 @@ __global__ __launch_bounds__(256) void activate_bwd_step_kernel(
             const float gn = n >= 1e-12f && n != 0.f ? gd / n : 0.f;
             d_q[i] = make_float4(g.x / d + x.x * gn, g.y / d + x.y * gn, g.z / d + x.z * gn, g.w / d + x.w * gn);
         }
-        const float y = opac[i];
+        const float y = opac ? opac[i] : act_opacity(o_raw[i]);
         go = i < skybox ? 0.f : g_o[i] * (1.f - y) * y;
         d_o[i] = go;
     }
@@ -1454,12 +1455,12 @@ int step_activate_backward(int64_t P, const float *rotation_raw, const float *sc
                            const float *d_scales, const float *d_rots, const float *d_opac, float *scaling_grad,
                            float *rotation_grad, float *opacity_grad, int64_t skybox, int *flag, const int *radii,
                            const float *d_means2D, float *max_radii2D, float *accum, float *denom, hipStream_t s,
-                           bool sparse_rows) {
+                           bool sparse_rows, const float *scaling_raw, const float *opacity_raw) {
     hipLaunchKernelGGL(activate_bwd_step_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, P,
                        reinterpret_cast<const float4 *>(rotation_raw), scales, opac, d_scales,
                        reinterpret_cast<const float4 *>(d_rots), d_opac, scaling_grad,
                        reinterpret_cast<float4 *>(rotation_grad), opacity_grad, skybox, flag, radii, d_means2D,
-                       max_radii2D, accum, denom, sparse_rows ? 1 : 0);
+                       max_radii2D, accum, denom, sparse_rows ? 1 : 0, scaling_raw, opacity_raw);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_last_error(std::string("step activation backward: ") + hipGetErrorString(e));

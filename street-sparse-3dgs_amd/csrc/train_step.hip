@@ -97,6 +97,14 @@ int fail_step(int rc, const char *what) {
     return rc;
 }
 
+// GSR_STEP_ACTIVATIONS=1: activations written by their own launch and read by the rasterizer (the
+// Python-driven step's form); default: the rasterizer and the activation backward read the raw
+// parameters and activate them where they are used (GaussianInputs.raw)
+bool step_raw_params() {
+    const char *e = std::getenv("GSR_STEP_ACTIVATIONS");
+    return !(e != nullptr && e[0] == '1');
+}
+
 bool step_sparse_rows() {
     const char *e = std::getenv("GSR_STEP_DENSE_ROWS");  // read per call: A/B runs switch it
     return !(e != nullptr && e[0] == '1');
@@ -175,15 +183,21 @@ int gsr_train_step(gsr_train_ctx *ctx, const gsr_train_step_args *a, int64_t *nu
     }
     int rc;
 
-    // render(): activations, rasterizer, exposure of this view (harness.py TrainStep.render)
-    if ((rc = gsr_activate_forward(P, a->scaling, a->rotation, a->opacity, scales, rots, opac, sv)))
+    // render(): activations, rasterizer, exposure of this view (harness.py TrainStep.render).  Raw
+    // mode: the preprocess activates the parameters it reads (no activated copy written and re-read)
+    const bool raw = step_raw_params();
+    if (!raw && (rc = gsr_activate_forward(P, a->scaling, a->rotation, a->opacity, scales, rots, opac, sv)))
         return fail_step(rc, "activations");
+    const float *r_scales = raw ? a->scaling : scales, *r_rots = raw ? a->rotation : rots,
+                *r_opac = raw ? a->opacity : opac;
     int64_t K = 0;
-    if ((rc = gsr_rasterize_forward_ex(resize_geom, resize_binning, resize_image, ctx, (int)P, a->D, a->M,
-                                       a->background, W, H, a->xyz, a->features, nullptr, opac, scales, 1.0f, rots,
-                                       nullptr, a->viewmatrix, a->projmatrix, a->campos, a->tan_fovx, a->tan_fovy, 0,
-                                       color, invd, radii, nullptr, nullptr, nullptr, nullptr, 0, 0, sv, &K, 0)))
-        return fail_step(rc, "rasterizer forward");
+    set_raw_params(raw);
+    rc = gsr_rasterize_forward_ex(resize_geom, resize_binning, resize_image, ctx, (int)P, a->D, a->M, a->background,
+                                  W, H, a->xyz, a->features, nullptr, r_opac, r_scales, 1.0f, r_rots, nullptr,
+                                  a->viewmatrix, a->projmatrix, a->campos, a->tan_fovx, a->tan_fovy, 0, color, invd,
+                                  radii, nullptr, nullptr, nullptr, nullptr, 0, 0, sv, &K, 0);
+    set_raw_params(false);
+    if (rc) return fail_step(rc, "rasterizer forward");
     const float *E = a->exposure + 12 * (int64_t)a->image_index;
     // exposure (x the alpha mask, train_single.py:117-119, in the same pass)
     if ((rc = launch_exposure_forward(color, E, npix, image, a->alpha_mask, s))) return fail_step(rc, "exposure");
@@ -208,19 +222,22 @@ int gsr_train_step(gsr_train_ctx *ctx, const gsr_train_step_args *a, int64_t *nu
     // Python-driven step)
     const bool sparse_rows = step_sparse_rows();
     set_sparse_grad_rows(sparse_rows);
+    set_raw_params(raw);
     rc = gsr_rasterize_backward(resize_scratch, ctx, (int)P, a->D, a->M, K, a->background, W, H, a->xyz,
-                                     a->features, nullptr, scales, 1.0f, rots, nullptr, a->viewmatrix, a->projmatrix,
+                                     a->features, nullptr, r_scales, 1.0f, r_rots, nullptr, a->viewmatrix, a->projmatrix,
                                      a->campos, a->tan_fovx, a->tan_fovy, radii, buf_ptr(ctx, kGeom),
                                      buf_ptr(ctx, kBinning), buf_ptr(ctx, kImage), d_color, depth ? d_invd : nullptr,
                                      d_means2D, nullptr, d_opac, a->xyz_grad, nullptr, a->features_grad, d_scales,
                                      d_rots, nullptr, nullptr, nullptr, nullptr, 0, 0, sv);
     set_sparse_grad_rows(false);
+    set_raw_params(false);
     if (rc) return fail_step(rc, "rasterizer backward");
     // activation backward with the skybox lock, the relevance flag and the densification
     // statistics (train_single.py:193-194, 217-223); then the sparse Adam and the shrink (:225-241)
-    if ((rc = step_activate_backward(P, a->rotation, scales, opac, d_scales, d_rots, d_opac, a->scaling_grad,
-                                     a->rotation_grad, a->opacity_grad, a->skybox_rows, flag, radii, d_means2D,
-                                     a->max_radii2D, a->xyz_gradient_accum, a->denom, s, sparse_rows)))
+    if ((rc = step_activate_backward(P, a->rotation, raw ? nullptr : scales, raw ? nullptr : opac, d_scales, d_rots,
+                                     d_opac, a->scaling_grad, a->rotation_grad, a->opacity_grad, a->skybox_rows, flag,
+                                     radii, d_means2D, a->max_radii2D, a->xyz_gradient_accum, a->denom, s, sparse_rows,
+                                     a->scaling, a->opacity)))
         return fail_step(rc, "activation backward");
     if ((rc = sparse_adam(a->n_groups, a->groups, P, a->opacity_grad, a->beta1, a->beta2, a->eps, flag, true, s,
                           a->scaling, a->scaffold_rows, a->max_scale, sparse_rows ? d_means2D : nullptr,
