@@ -676,6 +676,11 @@ __device__ __forceinline__ void load_sums(const BwdScratch &sc, const GaussianGr
         for (int k = 0; k < 10; k++) g[k] = 0.f;
 }
 
+#ifndef GSR_GRAD_WIDE
+#define GSR_GRAD_WIDE 0  // 1: float4 stores of whole waves' 3-float rows; measured slower (r03k: 0.0943 vs 0.0901 ms)
+#endif
+__device__ __forceinline__ bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
 __global__ __launch_bounds__(256) void grad_rows_kernel(int P, const int *__restrict__ radii, BwdScratch sc,
                                                         GaussianGrads out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -691,13 +696,28 @@ __global__ __launch_bounds__(256) void grad_rows_kernel(int P, const int *__rest
     const bool live = vis && nz;
     const uint64_t lm = __ballot(live);
     if (lane == 0 && (i >> 6) < (P + 63) / 64) sc.live[i >> 6] = lm;
+    const int64_t row0 = (int64_t)i - lane;
+    // GSR_GRAD_WIDE: a full wave's 3-float rows (768 B per array) go out as 48 float4 stores instead
+    // of three strided dword stores per lane -- the mean2D values staged through a wave-private LDS
+    // row, the zero rows of means3D / scales written as float4s wherever no live row shares them
+    const bool wide = GSR_GRAD_WIDE && row0 + kWave <= P && aligned16(out.dmeans2D) && aligned16(out.dmeans3D) &&
+                      aligned16(out.dscales);
+    __shared__ __attribute__((aligned(16))) float s_m2[256 / kWave][3 * kWave];
+    float *m2 = s_m2[threadIdx.x >> 6];
     if (valid) {
-        if (sc.atomic) {  // record mode: written by record_sum_kernel
-            st_out(&out.dmeans2D[3 * i + 0], g[0]);
-            st_out(&out.dmeans2D[3 * i + 1], g[1]);
-            st_out(&out.dopacity[i], g[5]);
+        const float c2 = out.sparse_rows && live ? 1.f : 0.f;
+        if (wide && sc.atomic) {
+            m2[3 * lane + 0] = g[0];
+            m2[3 * lane + 1] = g[1];
+            m2[3 * lane + 2] = c2;
+        } else {
+            if (sc.atomic) {  // record mode: written by record_sum_kernel
+                st_out(&out.dmeans2D[3 * i + 0], g[0]);
+                st_out(&out.dmeans2D[3 * i + 1], g[1]);
+            }
+            if (sc.atomic || out.sparse_rows) st_out(&out.dmeans2D[3 * i + 2], c2);
         }
-        if (sc.atomic || out.sparse_rows) st_out(&out.dmeans2D[3 * i + 2], out.sparse_rows && live ? 1.f : 0.f);
+        if (sc.atomic) st_out(&out.dopacity[i], g[5]);
         if (out.dcolors) {
             out.dcolors[3 * i + 0] = 0.f;
             out.dcolors[3 * i + 1] = 0.f;
@@ -707,19 +727,44 @@ __global__ __launch_bounds__(256) void grad_rows_kernel(int P, const int *__rest
 #pragma unroll
             for (int k = 0; k < 6; k++) out.dcov3D[6 * i + k] = 0.f;
     }
+    if (wide && sc.atomic) {
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS row is complete
+        __builtin_amdgcn_wave_barrier();
+        if (lane < 48) {
+            const float4 v = *reinterpret_cast<const float4 *>(m2 + 4 * lane);
+            st_out(reinterpret_cast<float4 *>(out.dmeans2D + 3 * row0) + lane, v);
+        }
+    }
     if (out.sparse_rows) return;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (valid && !live) {
+    if (wide) {
+        if (lane < 48) {
+            // floats 4 lane .. 4 lane + 3 of the wave's rows: rows 4 lane / 3 and (4 lane + 3) / 3
+            const int ra = (4 * lane) / 3, rb = (4 * lane + 3) / 3;
+            float4 *m3 = reinterpret_cast<float4 *>(out.dmeans3D + 3 * row0) + lane;
+            float4 *sc3 = reinterpret_cast<float4 *>(out.dscales + 3 * row0) + lane;
+            if (!(((lm >> ra) | (lm >> rb)) & 1ull)) {
+                st_out(m3, z4);
+                st_out(sc3, z4);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; e++)
+                    if (!((lm >> ((4 * lane + e) / 3)) & 1ull)) {
+                        st_out(reinterpret_cast<float *>(m3) + e, 0.f);
+                        st_out(reinterpret_cast<float *>(sc3) + e, 0.f);
+                    }
+            }
+        }
+    } else if (valid && !live) {
         st_out(&out.dmeans3D[3 * i + 0], 0.f);
         st_out(&out.dmeans3D[3 * i + 1], 0.f);
         st_out(&out.dmeans3D[3 * i + 2], 0.f);
         st_out(&out.dscales[3 * i + 0], 0.f);
         st_out(&out.dscales[3 * i + 1], 0.f);
         st_out(&out.dscales[3 * i + 2], 0.f);
-        st_out(&reinterpret_cast<float4 *>(out.drots)[i], z4);
     }
+    if (valid && !live) st_out(&reinterpret_cast<float4 *>(out.drots)[i], z4);
     // the wave's 64 zero SH rows as 1 KiB contiguous stores (float4 k*64 + l of the wave's rows)
-    const int64_t row0 = (int64_t)i - lane;
     float4 *dst4 = reinterpret_cast<float4 *>(out.dsh) + row0 * 12;
 #pragma unroll
     for (int k = 0; k < 12; k++) {

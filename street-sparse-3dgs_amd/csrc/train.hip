@@ -404,6 +404,10 @@ constexpr int kStW = 64;
 #endif
 constexpr int kStep = 4;
 constexpr int kRing = 16;
+#ifndef GSR_SSIM_PF
+#define GSR_SSIM_PF 1  // steps of input rows in flight; 2 measured no faster (r03j: train step 0.951-0.958 vs 0.949-0.958 ms)
+#endif
+static_assert(GSR_SSIM_PF == 1 || GSR_SSIM_PF == 2, "GSR_SSIM_PF: 1 or 2");
 constexpr int kStIC = kStW + 4 * kR, kStMC = kStW + 2 * kR;  // 84 input, 74 SSIM-map columns
 // Even pitches: the row-pair passes (2) and (4) move two adjacent columns per LDS instruction
 // (8-B aligned float2), lanes on consecutive pairs, so they are conflict-free without padding.
@@ -450,32 +454,41 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_stream_kernel(const floa
 
     // Loads are unconditional (clamped coordinates) and the zero padding is applied when the
     // values are staged: no branch around a load, so the compiler does not drain the loads early.
-    float px[kStInPer], py[kStInPer];
-    bool pin[kStInPer];
-    const auto fetch = [&](int p0) {
+    // GSR_SSIM_PF = 2: the input rows of the next two steps in flight (two register sets, the step
+    // loop unrolled by two so each set stays in fixed registers).  Measured no faster than one step
+    // ahead (profiles/r03j_ab_ssim_prefetch_negative.txt): a step's time is its four dependent LDS
+    // stages and barriers, not the row loads.
+    struct InRows {
+        float px[kStInPer], py[kStInPer];
+        bool pin[kStInPer];
+    };
+    const auto fetch = [&](InRows &f, int p0) {
 #pragma unroll
         for (int k = 0; k < kStInPer; k++) {
             const int e = min(tid + k * kLossThreads, kStInElems - 1);
             const int r = e / kStIC, c = e - r * kStIC;
             const int gy = p0 + r, gx = cx - 2 * kR + c;
-            pin[k] = gy >= 0 && gy < H && gx >= 0 && gx < W;
+            f.pin[k] = gy >= 0 && gy < H && gx >= 0 && gx < W;
             const size_t o = (size_t)min(max(gy, 0), H - 1) * W + min(max(gx, 0), W - 1);
-            px[k] = x[o];
-            py[k] = y[o];
+            f.px[k] = x[o];
+            f.py[k] = y[o];
         }
     };
-    fetch(r0 - 2 * kR);
+    constexpr int kPf = GSR_SSIM_PF;
+    InRows fa, fb;
+    fetch(fa, r0 - 2 * kR);
+    if (kPf == 2) fetch(fb, r0 - 2 * kR + kStep);
 
-    for (int st = 0; st < nsteps; st++) {
+    const auto step = [&](int st, InRows &cur) {
         const int p0 = r0 - 2 * kR + kStep * st;  // first input row of this step
-        // (1) stage input rows p0 .. p0 + kStep - 1 and start loading the next step's
+        // (1) stage input rows p0 .. p0 + kStep - 1 and start loading those kPf steps ahead
 #pragma unroll
         for (int k = 0; k < kStInPer; k++) {
             const int e = tid + k * kLossThreads;
             if (e < kStInElems) {
                 const int r = e / kStIC, c = e - r * kStIC;
-                s_in[0][r][c] = pin[k] ? px[k] : 0.f;
-                s_in[1][r][c] = pin[k] ? py[k] : 0.f;
+                s_in[0][r][c] = cur.pin[k] ? cur.px[k] : 0.f;
+                s_in[1][r][c] = cur.pin[k] ? cur.py[k] : 0.f;
             }
         }
         // (5)'s output pixels: rows orow, orow + 1 of column ocol (tasks tid < 128)
@@ -487,7 +500,7 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_stream_kernel(const floa
             xv[k] = x[oo];
             yv[k] = y[oo];
         }
-        fetch(p0 + kStep);  // unconditional (clamped): a branch here would make every wait a full drain
+        fetch(cur, p0 + kPf * kStep);  // unconditional (clamped): a branch here would make every wait a full drain
         lds_barrier();
 
         // (2) horizontal moments of the staged rows at the 74 map columns, two per task
@@ -624,6 +637,14 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_stream_kernel(const floa
                 }
             }
         }
+    };
+    if (kPf == 2) {
+        for (int st = 0; st < nsteps; st += 2) {
+            step(st, fa);
+            if (st + 1 < nsteps) step(st + 1, fb);
+        }
+    } else {
+        for (int st = 0; st < nsteps; st++) step(st, fa);
     }
     if (kMap) {
         l1 = block_sum(l1, s_red);
