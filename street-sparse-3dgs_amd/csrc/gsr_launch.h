@@ -119,10 +119,13 @@ int sparse_adam(int n_groups, const gsr_adam_group *groups, int64_t P, const flo
                 double beta2, double eps, int *flag_scratch, bool flag_ready, hipStream_t s, float *shrink_raw,
                 int64_t shrink_first, float shrink_limit, const float *live3 = nullptr, int64_t skybox = 0);
 // SSIM map forward (+ masked inverse-depth L1 forward with its gradient for an upstream of 1 when
-// mono != NULL) and the loss epilogue: losses[0..2] photometric, [3..4] depth, [5] total; *flag = 0
+// mono != NULL) and the loss epilogue: losses[0..2] photometric, [3..4] depth, [5] total; *flag = 0.
+// one != NULL: gmap receives the photometric gradient itself (dL/dloss = *one, times alpha when
+// given), and *gmap_is_photo says so (the streaming SSIM kernel; the tile kernel writes G)
 int step_loss_forward(const float *img, const float *gt, int H, int W, double lambda_dssim, void *loss_scratch,
                       float *gmap, const float *invd, const float *mono, const float *mask, float depth_w,
-                      void *depth_scratch, float *d_invd, float *losses, int *flag, hipStream_t s);
+                      void *depth_scratch, float *d_invd, float *losses, int *flag, hipStream_t s,
+                      const float *one = nullptr, const float *alpha = nullptr, bool *gmap_is_photo = nullptr);
 int launch_exposure_forward(const float *color, const float *E, int64_t npix, float *out, const float *alpha,
                             hipStream_t s);
 // photometric gradient (x alpha) through the exposure into d_color, the exposure gradient and the
@@ -130,7 +133,7 @@ int launch_exposure_forward(const float *color, const float *E, int64_t npix, fl
 int step_loss_backward(const float *img, const float *gt, const float *gmap, const float *one, double lambda_dssim,
                        const float *alpha, const float *color, const float *E_view, int64_t npix, float *d_color,
                        void *exp_scratch, int n_images, int view, const gsr_adam_group &eg, float *exposure_grad,
-                       double b1, double b2, double eps, hipStream_t s);
+                       double b1, double b2, double eps, hipStream_t s, bool gmap_is_photo = false);
 // activation backward + skybox lock + relevance flag + densification statistics.  sparse_rows:
 // the rasterizer backward wrote sparse rows (GaussianGrads): the scale / rotation gradients of
 // rows it did not write are neither read nor written.

@@ -266,6 +266,33 @@ static_assert(3 * kBwdVS - 1 + 2 * kR <= kBwdIH, "vertical stats pass reads at m
 static_assert(3 * kBwdSH * kBwdSP <= 2 * kBwdIH * kBwdIP, "a/b/c maps alias the input halo");
 static_assert(3 * kBwdSH * kBwdTP <= 5 * kBwdIH * kBwdSP, "second horizontal pass aliases the moments");
 
+// dx = (dout[0] sign(x - y) + dout[1] G) / n from the field l1_ssim_grad_kernel<true> stored.
+// Upstream (dL/dL1, dL/dSSIM) scaled by 1/n: from the 2-vector dout, or (photo loss, w_l1 >= 0)
+// from the scalar dL/dloss as torch's backward of (1-l) * L1 + l * (1 - SSIM) forms them.
+__device__ __forceinline__ float2 loss_upstream(const float *dout, float inv_n, float w_l1, float w_ssim) {
+    if (w_l1 >= 0.f) return make_float2((w_l1 * dout[0]) * inv_n, (-(w_ssim * dout[0])) * inv_n);
+    return make_float2(dout[0] * inv_n, dout[1] * inv_n);
+}
+
+// The photometric loss gradient at one pixel from its SSIM gradient field value G: upstream
+// (L1, SSIM) weights up times (sign(x - y), G) -- the one expression every kernel that forms it uses
+// (exposure_bwd_kernel, the native step's SSIM pass), so they agree bit for bit.
+__device__ __forceinline__ float photo_value(float2 up, float x, float y, float G) {
+    const float d = x - y;
+    const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+    return up.x * sgn + up.y * G;
+}
+
+// The native step's SSIM pass writes the photometric gradient itself instead of G (one != NULL):
+// dL/dloss = *one (1), the loss weights and 1/n, times the alpha mask (NULL: none) as torch's
+// multiply backward -- so the exposure backward reads one (3, H, W) field instead of the image,
+// the target and G.
+struct PhotoOut {
+    const float *one;
+    const float *alpha;
+    float inv_n, w_l1, w_ssim;
+};
+
 // kMap = false: dx = dL/d(img) for the upstream 2-vector dout (the backward proper).
 // kMap = true: the forward with the gradient field: per block the L1 and SSIM sums (as
 // l1_ssim_fwd_kernel) and per pixel G = dSSIM_sum/dx (unscaled), from which the backward is the
@@ -429,7 +456,8 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_stream_kernel(const floa
                                                                        const float *__restrict__ y, int H, int W,
                                                                        Window win, const float *__restrict__ dout,
                                                                        float inv_n, float *__restrict__ dx,
-                                                                       float2 *__restrict__ partials, int seg) {
+                                                                       float2 *__restrict__ partials, int seg,
+                                                                       PhotoOut po) {
     // The staged input rows (read by (2)) and the a/b/c rows ((3) -> (4)) share one buffer: (3)
     // writes after the barrier that ends (2), and the next step's (1) writes after the barrier
     // that ends (4).  40.1 KiB in all, so four workgroups fit a CU.
@@ -449,6 +477,7 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_stream_kernel(const floa
     const int tid = threadIdx.x;
     const int cx = blockIdx.x * kStW, r0 = blockIdx.y * seg, r1 = min(r0 + seg, H);
     const float g_l1 = kMap ? 0.f : dout[0] * inv_n, g_ssim = kMap ? 0.f : dout[1] * inv_n;
+    const float2 up = kMap && po.one ? loss_upstream(po.one, po.inv_n, po.w_l1, po.w_ssim) : make_float2(0.f, 0.f);
     const int nsteps = (r1 - r0 + 4 * kR + kStep - 1) / kStep;
     float l1 = 0.f, ss = 0.f;
 
@@ -629,7 +658,12 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_stream_kernel(const floa
                 const float d = xv[k] - yv[k];
                 const float G = acc[0][k] + 2.f * xv[k] * acc[1][k] + yv[k] * acc[2][k];
                 if (kMap) {
-                    dx[o] = G;
+                    if (po.one) {
+                        const float g = photo_value(up, xv[k], yv[k], G);
+                        dx[o] = po.alpha ? g * po.alpha[o] : g;
+                    } else {
+                        dx[o] = G;
+                    }
                     l1 += fabsf(d);
                 } else {
                     const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
@@ -656,13 +690,6 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_stream_kernel(const floa
     }
 }
 
-// dx = (dout[0] sign(x - y) + dout[1] G) / n from the field l1_ssim_grad_kernel<true> stored.
-// Upstream (dL/dL1, dL/dSSIM) scaled by 1/n: from the 2-vector dout, or (photo loss, w_l1 >= 0)
-// from the scalar dL/dloss as torch's backward of (1-l) * L1 + l * (1 - SSIM) forms them.
-__device__ __forceinline__ float2 loss_upstream(const float *dout, float inv_n, float w_l1, float w_ssim) {
-    if (w_l1 >= 0.f) return make_float2((w_l1 * dout[0]) * inv_n, (-(w_ssim * dout[0])) * inv_n);
-    return make_float2(dout[0] * inv_n, dout[1] * inv_n);
-}
 
 __global__ __launch_bounds__(256) void l1_ssim_bwd_map_kernel(const float4 *__restrict__ x, const float4 *__restrict__ y,
                                                               const float4 *__restrict__ G, int64_t n4,
@@ -1089,9 +1116,7 @@ __global__ __launch_bounds__(kExpThreads) void exposure_bwd_kernel(const float *
     float2 up = make_float2(0.f, 0.f);
     if (kPhoto) up = loss_upstream(pg.dout, pg.inv_n, pg.w_l1, pg.w_ssim);
     const auto photo = [&](int64_t i, float a) {
-        const float d = pg.x[i] - pg.y[i];
-        const float sgn = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
-        const float g = up.x * sgn + up.y * pg.G[i];
+        const float g = photo_value(up, pg.x[i], pg.y[i], pg.G[i]);
         return pg.alpha ? g * a : g;
     };
     for (int64_t p = (int64_t)blockIdx.x * kExpThreads + threadIdx.x; p < n; p += (int64_t)gridDim.x * kExpThreads) {
@@ -1410,7 +1435,8 @@ int sparse_adam(int n_groups, const gsr_adam_group *groups, int64_t P, const flo
 
 int step_loss_forward(const float *img, const float *gt, int H, int W, double lambda_dssim, void *loss_scratch,
                       float *gmap, const float *invd, const float *mono, const float *mask, float depth_w,
-                      void *depth_scratch, float *d_invd, float *losses, int *flag, hipStream_t s) {
+                      void *depth_scratch, float *d_invd, float *losses, int *flag, hipStream_t s, const float *one,
+                      const float *alpha, bool *gmap_is_photo) {
     set_lds_attr();
     const int C = 3;
     const bool tiled = ssim_tiled();
@@ -1422,7 +1448,10 @@ int step_loss_forward(const float *img, const float *gt, int H, int W, double la
                            nullptr, 0.f, gmap, pp);
     else
         hipLaunchKernelGGL(l1_ssim_stream_kernel<true>, g, dim3(kLossThreads), 0, s, img, gt, H, W, ssim_window(),
-                           nullptr, 0.f, gmap, pp, stream_seg(C, H, W));
+                           nullptr, 0.f, gmap, pp, stream_seg(C, H, W),
+                           PhotoOut{one, alpha, (float)(1.0 / (double)(3 * (int64_t)H * W)), (float)(1.0 - lambda_dssim),
+                                    (float)lambda_dssim});
+    if (gmap_is_photo) *gmap_is_photo = !tiled && one != nullptr;
     const int64_t n = (int64_t)H * W;
     const int nd = (int)std::max<int64_t>(1, (n + kDepthPerBlock - 1) / kDepthPerBlock);
     double *dp = static_cast<double *>(depth_scratch);
@@ -1455,13 +1484,17 @@ int launch_exposure_forward(const float *color, const float *E, int64_t npix, fl
 int step_loss_backward(const float *img, const float *gt, const float *gmap, const float *one, double lambda_dssim,
                        const float *alpha, const float *color, const float *E_view, int64_t npix, float *d_color,
                        void *exp_scratch, int n_images, int view, const gsr_adam_group &eg, float *exposure_grad,
-                       double b1, double b2, double eps, hipStream_t s) {
+                       double b1, double b2, double eps, hipStream_t s, bool gmap_is_photo) {
     const int nb = exposure_blocks(npix);
     float *part = static_cast<float *>(exp_scratch);
     const PhotoGrad pg{img, gt, gmap, one, alpha, (float)(1.0 / (double)(3 * npix)), (float)(1.0 - lambda_dssim),
                        (float)lambda_dssim};
-    hipLaunchKernelGGL(exposure_bwd_kernel<true>, dim3(nb), dim3(kExpThreads), 0, s, color, E_view, npix, nullptr,
-                       d_color, part, pg);
+    if (gmap_is_photo)  // the SSIM pass already formed the photometric gradient (PhotoOut)
+        hipLaunchKernelGGL(exposure_bwd_kernel<false>, dim3(nb), dim3(kExpThreads), 0, s, color, E_view, npix, gmap,
+                           d_color, part, pg);
+    else
+        hipLaunchKernelGGL(exposure_bwd_kernel<true>, dim3(nb), dim3(kExpThreads), 0, s, color, E_view, npix, nullptr,
+                           d_color, part, pg);
     hipLaunchKernelGGL(exposure_finalize_adam_kernel, dim3(1), dim3(768), 0, s, part, nb, n_images, view, eg,
                        exposure_grad, (float)b1, (float)b2, (float)(1.0 - b1), (float)(1.0 - b2), (float)eps);
     const hipError_t e = hipGetLastError();
@@ -1538,7 +1571,7 @@ int gsr_l1_ssim_backward(const float *img, const float *gt, int C, int H, int W,
                            W, ssim_window(), dL_dout, inv_n, dL_dimg, nullptr);
     else
         hipLaunchKernelGGL(l1_ssim_stream_kernel<false>, stream_grid(C, H, W), dim3(kLossThreads), 0, s, img, gt, H,
-                           W, ssim_window(), dL_dout, inv_n, dL_dimg, nullptr, stream_seg(C, H, W));
+                           W, ssim_window(), dL_dout, inv_n, dL_dimg, nullptr, stream_seg(C, H, W), PhotoOut{});
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_last_error(std::string("gsr_l1_ssim_backward: ") + hipGetErrorString(e));
@@ -1569,7 +1602,7 @@ int forward_with_map(const char *who, const float *img, const float *gt, int C, 
                            nullptr, 0.f, ssim_grad_map, part);
     else
         hipLaunchKernelGGL(l1_ssim_stream_kernel<true>, g, dim3(kLossThreads), 0, s, img, gt, H, W, ssim_window(),
-                           nullptr, 0.f, ssim_grad_map, part, stream_seg(C, H, W));
+                           nullptr, 0.f, ssim_grad_map, part, stream_seg(C, H, W), PhotoOut{});
     hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(1024), 0, s, part, nb, 1.0 / ((double)C * H * W), out,
                        w_l1, w_ssim);
     const hipError_t e = hipGetLastError();

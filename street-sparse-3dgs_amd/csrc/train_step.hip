@@ -100,6 +100,10 @@ int fail_step(int rc, const char *what) {
 // GSR_STEP_ACTIVATIONS=1: activations written by their own launch and read by the rasterizer (the
 // Python-driven step's form); default: the rasterizer and the activation backward read the raw
 // parameters and activate them where they are used (GaussianInputs.raw)
+#ifndef GSR_STEP_PHOTO_IN_SSIM
+#define GSR_STEP_PHOTO_IN_SSIM 1  // 0: the SSIM pass writes G and the exposure backward forms the gradient
+#endif
+
 bool step_raw_params() {
     const char *e = std::getenv("GSR_STEP_ACTIVATIONS");
     return !(e != nullptr && e[0] == '1');
@@ -204,9 +208,11 @@ int gsr_train_step(gsr_train_ctx *ctx, const gsr_train_step_args *a, int64_t *nu
 
     // losses (train_single.py:121-141): the SSIM map pass with its gradient field, the depth L1 with
     // its gradient (the loss is the root: dL/dloss = 1), one epilogue for both values and the total
+    bool photo = false;  // the SSIM pass wrote the photometric gradient itself (gsr_launch.h)
     if ((rc = step_loss_forward(image, a->gt, H, W, a->lambda_dssim, loss_scratch, gmap, invd,
                                 depth ? a->mono_invdepth : nullptr, a->depth_mask, a->depth_weight, depth_scratch,
-                                d_invd, a->losses, flag, s)))
+                                d_invd, a->losses, flag, s, GSR_STEP_PHOTO_IN_SSIM ? one : nullptr, a->alpha_mask,
+                                &photo)))
         return fail_step(rc, "losses");
 
     // loss.backward(): photometric gradient -> alpha mask -> exposure (colour gradient, exposure
@@ -214,7 +220,7 @@ int gsr_train_step(gsr_train_ctx *ctx, const gsr_train_step_args *a, int64_t *nu
     gsr_adam_group eg = *a->exposure_group;
     if ((rc = step_loss_backward(image, a->gt, gmap, one, a->lambda_dssim, a->alpha_mask, color, E, npix, d_color,
                                  exp_scratch, a->n_images, a->image_index, eg, a->exposure_grad, a->exposure_beta1,
-                                 a->exposure_beta2, a->exposure_eps, s)))
+                                 a->exposure_beta2, a->exposure_eps, s, photo)))
         return fail_step(rc, "loss backward");
     // sparse gradient rows (gsr_launch.h GaussianGrads): the Gaussians no pixel's backward reached
     // (88% of the bench scene) have zero gradients and are never relevant to the sparse Adam, so
