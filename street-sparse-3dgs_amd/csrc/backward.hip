@@ -682,7 +682,7 @@ __device__ __forceinline__ void load_sums(const BwdScratch &sc, const GaussianGr
 __device__ __forceinline__ bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 __global__ __launch_bounds__(256) void grad_rows_kernel(int P, const int *__restrict__ radii, BwdScratch sc,
-                                                        GaussianGrads out) {
+                                                        GaussianGrads out, int zero_dead) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & (kWave - 1);
     const bool valid = i < P;
@@ -735,7 +735,7 @@ __global__ __launch_bounds__(256) void grad_rows_kernel(int P, const int *__rest
             st_out(reinterpret_cast<float4 *>(out.dmeans2D + 3 * row0) + lane, v);
         }
     }
-    if (out.sparse_rows) return;
+    if (out.sparse_rows || !zero_dead) return;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     if (wide) {
         if (lane < 48) {
@@ -855,6 +855,9 @@ __global__ __launch_bounds__(256) void grad_live_kernel(
     }
 }
 
+#ifndef GSR_BWD_MEMSET
+#define GSR_BWD_MEMSET 0  // 1: hipMemsetAsync fills; preprocess_bwd 0.0891 -> 0.0866 ms but the fills leave dirty lines that slow the next frame (preprocess 0.035 -> 0.040, sort 0.106 -> 0.111 ms; r03n)
+#endif
 #ifndef GSR_BWD_SPLIT
 #define GSR_BWD_SPLIT 1  // 0: the single preprocess_bwd_kernel for every frame
 #endif
@@ -869,7 +872,19 @@ void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const Ge
                        !in.cov3D_precomp && in.scales && in.rotations &&
                        reinterpret_cast<uintptr_t>(in.shs) % 16 == 0 && reinterpret_cast<uintptr_t>(out.dsh) % 16 == 0;
     if (split) {
-        hipLaunchKernelGGL(grad_rows_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, radii, sc, out);
+        // dense rows: the dead rows' zeros as one fill per gradient array (streaming stores of whole
+        // arrays) instead of grad_rows_kernel's per-row stores; grad_live_kernel then overwrites the
+        // live rows (GSR_BWD_MEMSET=0: grad_rows_kernel writes the zeros)
+        const bool fill = GSR_BWD_MEMSET && !out.sparse_rows;
+        if (fill) {
+            const size_t P = (size_t)in.P;
+            (void)hipMemsetAsync(out.dsh, 0, sizeof(float) * P * 48, s);
+            (void)hipMemsetAsync(out.dmeans3D, 0, sizeof(float) * P * 3, s);
+            (void)hipMemsetAsync(out.dscales, 0, sizeof(float) * P * 3, s);
+            (void)hipMemsetAsync(out.drots, 0, sizeof(float) * P * 4, s);
+        }
+        hipLaunchKernelGGL(grad_rows_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, radii, sc, out,
+                           fill ? 0 : 1);
         hipLaunchKernelGGL(grad_live_kernel, dim3((in.P + kLiveRange - 1) / kLiveRange), dim3(256), 0, s, in.P, in.D,
                            in.means3D, in.shs, gs.clamped, in.scales, in.rotations, in.scale_modifier,
                            true_scale_gradient() ? in.scale_modifier : 1.0f, cam.view, cam.proj, cam.campos, cam.tanx,
