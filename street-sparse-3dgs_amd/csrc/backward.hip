@@ -855,6 +855,9 @@ __global__ __launch_bounds__(256) void grad_live_kernel(
     }
 }
 
+#ifndef GSR_BWD_ZERO_IN_RENDER
+#define GSR_BWD_ZERO_IN_RENDER 1  // the dense zero rows stored by render_bwd's waves after their replay
+#endif
 #ifndef GSR_BWD_MEMSET
 #define GSR_BWD_MEMSET 0  // 1: hipMemsetAsync fills; preprocess_bwd 0.0891 -> 0.0866 ms but the fills leave dirty lines that slow the next frame (preprocess 0.035 -> 0.040, sort 0.106 -> 0.111 ms; r03n)
 #endif
@@ -862,20 +865,45 @@ __global__ __launch_bounds__(256) void grad_live_kernel(
 #define GSR_BWD_SPLIT 1  // 0: the single preprocess_bwd_kernel for every frame
 #endif
 
+namespace {
+bool split_ok(const GaussianInputs &in, const GaussianGrads &out, const BwdScratch &sc) {
+    return GSR_BWD_SPLIT && GSR_BWD_SKIP_DEAD && sc.live && in.shs && in.M == 16 && !in.cov3D_precomp && in.scales &&
+           in.rotations && reinterpret_cast<uintptr_t>(in.shs) % 16 == 0 &&
+           reinterpret_cast<uintptr_t>(out.dsh) % 16 == 0;
+}
+}  // namespace
+
+bool bwd_zero_rows(const GaussianInputs &in, const GaussianGrads &out, const BwdScratch &sc, int nblocks,
+                   ZeroRows *z) {
+    if (!GSR_BWD_ZERO_IN_RENDER || in.P == 0 || nblocks <= 0 || out.sparse_rows || !split_ok(in, out, sc))
+        return false;
+    float *p[4] = {out.dsh, out.dmeans3D, out.dscales, out.drots};
+    const uint64_t P = (uint64_t)in.P, n[4] = {48 * P, 3 * P, 3 * P, 4 * P};
+    for (int k = 0; k < 4; k++)
+        if (!p[k] || (reinterpret_cast<uintptr_t>(p[k]) & 15u)) return false;
+    z->c4[0] = 0;
+    for (int k = 0; k < 4; k++) {
+        z->p[k] = p[k];
+        z->n[k] = n[k];
+        z->c4[k + 1] = z->c4[k] + n[k] / 4;
+    }
+    z->per4 = (z->c4[4] + (uint64_t)nblocks - 1) / (uint64_t)nblocks;
+    return true;
+}
+
 void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const GeomState &gs, const ImageState &is,
-                           const int *radii, const BwdScratch &sc, const GaussianGrads &out, hipStream_t s) {
+                           const int *radii, const BwdScratch &sc, const GaussianGrads &out, hipStream_t s,
+                           bool rows_zeroed) {
     if (in.P == 0) return;
     if (!sc.atomic)  // atomic mode: the sums are already in GeomState.acc
         hipLaunchKernelGGL(record_sum_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, cam.gx, in.means3D,
                        cam.view, gs.rect8, gs.rect4, gs.offsets, is.boundary, sc, out.dmeans2D, out.dopacity);
-    const bool split = GSR_BWD_SPLIT && GSR_BWD_SKIP_DEAD && sc.live && in.shs && in.M == 16 &&
-                       !in.cov3D_precomp && in.scales && in.rotations &&
-                       reinterpret_cast<uintptr_t>(in.shs) % 16 == 0 && reinterpret_cast<uintptr_t>(out.dsh) % 16 == 0;
+    const bool split = split_ok(in, out, sc);
     if (split) {
         // dense rows: the dead rows' zeros as one fill per gradient array (streaming stores of whole
         // arrays) instead of grad_rows_kernel's per-row stores; grad_live_kernel then overwrites the
         // live rows (GSR_BWD_MEMSET=0: grad_rows_kernel writes the zeros)
-        const bool fill = GSR_BWD_MEMSET && !out.sparse_rows;
+        const bool fill = GSR_BWD_MEMSET && !out.sparse_rows && !rows_zeroed;
         if (fill) {
             const size_t P = (size_t)in.P;
             (void)hipMemsetAsync(out.dsh, 0, sizeof(float) * P * 48, s);
@@ -884,7 +912,7 @@ void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const Ge
             (void)hipMemsetAsync(out.drots, 0, sizeof(float) * P * 4, s);
         }
         hipLaunchKernelGGL(grad_rows_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, radii, sc, out,
-                           fill ? 0 : 1);
+                           fill || rows_zeroed ? 0 : 1);
         hipLaunchKernelGGL(grad_live_kernel, dim3((in.P + kLiveRange - 1) / kLiveRange), dim3(256), 0, s, in.P, in.D,
                            in.means3D, in.shs, gs.clamped, in.scales, in.rotations, in.scale_modifier,
                            true_scale_gradient() ? in.scale_modifier : 1.0f, cam.view, cam.proj, cam.campos, cam.tanx,

@@ -87,12 +87,23 @@ void launch_binning_scatter(int P, const Camera &cam, const GeomState &gs, const
 void launch_binning_tiles(int P, const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                           bool local_sort, const uint32_t *maxsb, hipStream_t s);
 
+// The dense gradient arrays render_bwd zeroes beside its replay (ZeroRows): the four arrays
+// (float counts n[k], 16-B aligned) as one concatenated float4 range split evenly over the
+// backward's workgroups (per4 float4 each; c4 the cumulative float4 counts).  preprocess_bwd then
+// writes only the live rows (and every row's screen-space mean / opacity gradient).
+struct ZeroRows {
+    float *p[4];
+    uint64_t n[4];
+    uint64_t c4[5];
+    uint64_t per4;
+};
+
 // render.hip
 void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                        const float *bg, float *out_color, float *out_invdepth, hipStream_t s);
 void launch_render_bwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                        const int *radii, const float *bg, const float *dL_dpix, const float *dL_dinvdepth,
-                       const BwdScratch &sc, hipStream_t s);
+                       const BwdScratch &sc, hipStream_t s, const ZeroRows *zr = nullptr);
 
 // backward.hip
 // sparse_rows (the native train step only, set_sparse_grad_rows): the rows of Gaussians with ten
@@ -107,7 +118,12 @@ struct GaussianGrads {
 // rasterizer.hip: gsr_rasterize_backward on this thread writes sparse rows (see above)
 void set_sparse_grad_rows(bool on);
 void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const GeomState &gs, const ImageState &is,
-                           const int *radii, const BwdScratch &sc, const GaussianGrads &out, hipStream_t s);
+                           const int *radii, const BwdScratch &sc, const GaussianGrads &out, hipStream_t s,
+                           bool rows_zeroed = false);
+// the frame's dense gradient arrays for render_bwd to zero (false: preprocess_bwd writes the zeros
+// itself -- sparse rows, the single-kernel path, unaligned arrays or GSR_BWD_ZERO_IN_RENDER=0)
+bool bwd_zero_rows(const GaussianInputs &in, const GaussianGrads &out, const BwdScratch &sc, int nblocks,
+                   ZeroRows *z);
 
 // train.hip: the native train step's fused launches (train_step.hip).  sparse_adam is
 // gsr_sparse_adam_step (flag_ready: the relevance flag is already computed; shrink_raw != NULL:

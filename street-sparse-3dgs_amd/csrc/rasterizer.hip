@@ -852,14 +852,19 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
         return fail(GSR_ERR_UNSUPPORTED, "raw parameters with a hierarchy cut or precomputed covariances");
     GaussianInputs in{P, D, M, means3D, shs, colors_precomp, nullptr, scales, rotations, cov3D_precomp,
                       scale_modifier, g_raw_params ? 1 : 0};
+    bool zeroed = false;
+    ZeroRows zr{};
     {
         StageTimer st(6, s);
-        if (R_inst > 0) launch_render_bwd(cam, gs, bs, is, radii, background, dL_dpix, dL_dinvdepth, sc, s);
+        // the dense zero gradient rows go out beside render_bwd's replay (bwd_zero_rows)
+        zeroed = R_inst > 0 && bwd_zero_rows(in, out, sc, T, &zr);
+        if (R_inst > 0)
+            launch_render_bwd(cam, gs, bs, is, radii, background, dL_dpix, dL_dinvdepth, sc, s, zeroed ? &zr : nullptr);
     }
     if ((rc = check("render backward", debug, s))) return rc;
     {
         StageTimer st(7, s);
-        launch_preprocess_bwd(in, cam, gs, is, radii, sc, out, s);
+        launch_preprocess_bwd(in, cam, gs, is, radii, sc, out, s, zeroed);
     }
     if ((rc = check("preprocess backward", debug, s))) return rc;
     if (R > 0) {

@@ -480,7 +480,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
     const GRec *__restrict__ rec, const float *__restrict__ bg, const float *__restrict__ final_Ts,
     const uint32_t *__restrict__ n_contrib, const float *__restrict__ dL_dpix, const float *__restrict__ dL_dinvd,
     const uint32_t *__restrict__ tile_order, const uint32_t *__restrict__ goff, uint64_t *__restrict__ boundary,
-    float4 *__restrict__ out) {
+    float4 *__restrict__ out, ZeroRows zr) {
     // 9 KiB of LDS per wave: each compacted instance's mean and conic (scaled for gauss_p2 by the
     // lane that stages it, once per instance instead of by the whole wave), opacity, list position
     // << 4 | sub-block mask, Gaussian id (atomic mode) or record index, colour, and the unscaled
@@ -799,6 +799,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
         }
         __syncthreads();
     }
+    if (zr.per4) {
+        // this workgroup's share of the frame's dense zero gradient rows (ZeroRows): issued after
+        // the replay, so no wait of the replay covers them -- the VALU-bound replay leaves HBM
+        // nearly idle, and preprocess_bwd no longer streams these bytes on its own
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        const uint64_t q0 = (uint64_t)blockIdx.x * zr.per4, q1 = min(zr.c4[4], q0 + zr.per4);
+        for (uint64_t q = q0 + (uint64_t)lane; q < q1; q += kWave) {
+            const int k = (q >= zr.c4[1]) + (q >= zr.c4[2]) + (q >= zr.c4[3]);
+            __builtin_nontemporal_store(f4{0.f, 0.f, 0.f, 0.f}, reinterpret_cast<f4 *>(zr.p[k]) + (q - zr.c4[k]));
+        }
+        if (blockIdx.x == 0 && lane < 16) {  // the floats past each array's last whole float4
+            const int k = lane >> 2, t = lane & 3;
+            const uint64_t e = 4 * (zr.c4[k + 1] - zr.c4[k]) + (uint64_t)t;
+            if (e < zr.n[k]) __builtin_nontemporal_store(0.f, zr.p[k] + e);
+        }
+    }
     if (GSR_BLEND_STATS) {
         bst.flush(kBwdPairs);
         if (lane == 0) {
@@ -811,14 +827,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
 
 void launch_render_bwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                        const int *radii, const float *bg, const float *dL_dpix, const float *dL_dinvdepth,
-                       const BwdScratch &sc, hipStream_t s) {
+                       const BwdScratch &sc, hipStream_t s, const ZeroRows *zr) {
     (void)radii;
     const int T = cam.gx * cam.gy;
     if (T == 0) return;
+    const ZeroRows z = zr ? *zr : ZeroRows{};
 #define GSR_BWD_LAUNCH(D, A)                                                                                       \
     hipLaunchKernelGGL((render_bwd_kernel<D, A>), dim3(T), dim3(kWave), 0, s, is.ranges, bs.point_list, cam.W, cam.H, \
                        cam.gx, gs.rec, bg, is.final_T, is.n_contrib, dL_dpix, dL_dinvdepth, is.tile_order, gs.offsets, \
-                       is.boundary, A ? sc.acc : sc.rec)
+                       is.boundary, A ? sc.acc : sc.rec, z)
     if (dL_dinvdepth) {
         if (sc.atomic) GSR_BWD_LAUNCH(true, true);
         else GSR_BWD_LAUNCH(true, false);
