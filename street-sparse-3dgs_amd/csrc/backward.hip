@@ -5,6 +5,8 @@
 // SH -> (coefficients, view direction -> mean3D) and 3D covariance -> (scale, rotation).
 // Every output row is written (zeros for culled Gaussians and unused SH coefficients), so
 // the caller's gradient tensors need no memset pass.
+#include <algorithm>
+
 #include "gsr_launch.h"
 
 namespace gsr {
@@ -858,6 +860,9 @@ __global__ __launch_bounds__(256) void grad_live_kernel(
 #ifndef GSR_BWD_ZERO_IN_RENDER
 #define GSR_BWD_ZERO_IN_RENDER 1  // the dense zero rows stored by render_bwd's waves after their replay
 #endif
+#ifndef GSR_BWD_ZERO_PCT
+#define GSR_BWD_ZERO_PCT 100
+#endif
 #ifndef GSR_BWD_MEMSET
 #define GSR_BWD_MEMSET 0  // 1: hipMemsetAsync fills; preprocess_bwd 0.0891 -> 0.0866 ms but the fills leave dirty lines that slow the next frame (preprocess 0.035 -> 0.040, sort 0.106 -> 0.111 ms; r03n)
 #endif
@@ -887,7 +892,10 @@ bool bwd_zero_rows(const GaussianInputs &in, const GaussianGrads &out, const Bwd
         z->n[k] = n[k];
         z->c4[k + 1] = z->c4[k] + n[k] / 4;
     }
-    z->per4 = (z->c4[4] + (uint64_t)nblocks - 1) / (uint64_t)nblocks;
+    // only the first GSR_BWD_ZERO_PCT % of the backward's workgroups in launch order (the heaviest
+    // tiles first) carry zero rows: the light tiles at the end of the launch finish without them
+    const uint64_t nz = std::max<uint64_t>(1, (uint64_t)nblocks * GSR_BWD_ZERO_PCT / 100);
+    z->per4 = (z->c4[4] + nz - 1) / nz;
     return true;
 }
 
