@@ -6,6 +6,7 @@
 // Every output row is written (zeros for culled Gaussians and unused SH coefficients), so
 // the caller's gradient tensors need no memset pass.
 #include <algorithm>
+#include <atomic>
 
 #include "gsr_launch.h"
 
@@ -781,16 +782,34 @@ __global__ __launch_bounds__(256) void grad_live_kernel(
     int P, int D, const float *__restrict__ means3D, const float *__restrict__ shs, const uint8_t *__restrict__ clamped,
     const float *__restrict__ scales, const float *__restrict__ rotations, float mod, float dscale_mod,
     const float *__restrict__ viewmatrix, const float *__restrict__ projmatrix, const float *__restrict__ campos_p,
-    float tanx, float tany, float fx, float fy, BwdScratch sc, GaussianGrads out, int raw) {
+    float tanx, float tany, float fx, float fy, BwdScratch sc, GaussianGrads out, int raw,
+    const uint32_t *__restrict__ stamps, uint32_t stamp) {
     __shared__ uint16_t s_list[kLiveRange];
     __shared__ uint32_t s_off[kLiveRange / 64 + 1];
+    __shared__ uint8_t s_byte[256];
     const int t = threadIdx.x;
     const int64_t base = (int64_t)blockIdx.x * kLiveRange;
     const int nw = (P + 63) / 64;
-    // thread t owns rows [8t, 8t + 8) of the range: byte t % 8 of live mask t / 8
+    // thread t owns rows [8t, 8t + 8) of the range: byte t % 8 of live mask t / 8 -- from
+    // grad_rows_kernel's masks, or (stamps != NULL) from the rows render_bwd stamped this backward
     const int wi = (int)(base / 64) + t / 8;
-    const uint64_t m = wi < nw ? sc.live[wi] : 0ull;
-    const uint32_t byte = (uint32_t)(m >> (8 * (t & 7))) & 0xFFu;
+    uint64_t m;
+    uint32_t byte;
+    if (stamps) {
+        byte = 0u;
+        const int64_t r0 = base + 8 * t;
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (r0 + k < P && stamps[r0 + k] == stamp) byte |= 1u << k;
+        s_byte[t] = (uint8_t)byte;
+        __syncthreads();
+        m = 0ull;
+#pragma unroll
+        for (int k = 0; k < 8; k++) m |= (uint64_t)s_byte[(t & ~7) + k] << (8 * k);
+    } else {
+        m = wi < nw ? sc.live[wi] : 0ull;
+        byte = (uint32_t)(m >> (8 * (t & 7))) & 0xFFu;
+    }
     if ((t & 7) == 0) s_off[t / 8] = (uint32_t)__popcll(m);
     __syncthreads();
     if (t == 0) {
@@ -822,6 +841,12 @@ __global__ __launch_bounds__(256) void grad_live_kernel(
         float3 s_in = make_float3(0.f, 0.f, 0.f);
         geom_chain(i, p, V, projmatrix, fx, fy, tanx, tany, true, scales, rotations, mod, nullptr, g, c3, q, s_in, dm,
                    dcov, raw);
+        if (stamps) {  // the live rows' screen-space mean / opacity gradients (render_bwd zeroed the rest)
+            st_out(&out.dmeans2D[3 * i + 0], g[0]);
+            st_out(&out.dmeans2D[3 * i + 1], g[1]);
+            st_out(&out.dmeans2D[3 * i + 2], out.sparse_rows ? 1.f : 0.f);
+            st_out(&out.dopacity[i], g[5]);
+        }
         if (sc.atomic) {
             // the row is consumed: cleared for a repeated backward (see preprocess_bwd_kernel)
             float4 *a = sc.acc + 4 * (size_t)i;
@@ -878,30 +903,37 @@ bool split_ok(const GaussianInputs &in, const GaussianGrads &out, const BwdScrat
 }
 }  // namespace
 
-bool bwd_zero_rows(const GaussianInputs &in, const GaussianGrads &out, const BwdScratch &sc, int nblocks,
-                   ZeroRows *z) {
-    if (!GSR_BWD_ZERO_IN_RENDER || in.P == 0 || nblocks <= 0 || out.sparse_rows || !split_ok(in, out, sc))
+bool bwd_zero_rows(const GaussianInputs &in, const GaussianGrads &out, const BwdScratch &sc, uint32_t *gs_stamps,
+                   int nblocks, ZeroRows *z) {
+    if (!GSR_BWD_ZERO_IN_RENDER || in.P == 0 || nblocks <= 0 || !sc.atomic || !gs_stamps || !split_ok(in, out, sc))
         return false;
-    float *p[4] = {out.dsh, out.dmeans3D, out.dscales, out.drots};
-    const uint64_t P = (uint64_t)in.P, n[4] = {48 * P, 3 * P, 3 * P, 4 * P};
-    for (int k = 0; k < 4; k++)
+    // sparse rows: only the screen-space mean and opacity gradients are dense
+    const uint64_t P = (uint64_t)in.P;
+    float *p[kZeroArrays] = {out.dmeans2D, out.dopacity, out.dsh, out.dmeans3D, out.dscales, out.drots};
+    const uint64_t n[kZeroArrays] = {3 * P, P, 48 * P, 3 * P, 3 * P, 4 * P};
+    const int na = out.sparse_rows ? 2 : kZeroArrays;
+    for (int k = 0; k < na; k++)
         if (!p[k] || (reinterpret_cast<uintptr_t>(p[k]) & 15u)) return false;
     z->c4[0] = 0;
-    for (int k = 0; k < 4; k++) {
-        z->p[k] = p[k];
-        z->n[k] = n[k];
-        z->c4[k + 1] = z->c4[k] + n[k] / 4;
+    for (int k = 0; k < kZeroArrays; k++) {
+        z->p[k] = k < na ? p[k] : nullptr;
+        z->n[k] = k < na ? n[k] : 0;
+        z->c4[k + 1] = z->c4[k] + z->n[k] / 4;
     }
+    static std::atomic<uint32_t> g_stamp{0};
+    z->stamps = gs_stamps;
+    z->stamp = g_stamp.fetch_add(1, std::memory_order_relaxed) + 1u;
     // only the first GSR_BWD_ZERO_PCT % of the backward's workgroups in launch order (the heaviest
     // tiles first) carry zero rows: the light tiles at the end of the launch finish without them
     const uint64_t nz = std::max<uint64_t>(1, (uint64_t)nblocks * GSR_BWD_ZERO_PCT / 100);
-    z->per4 = (z->c4[4] + nz - 1) / nz;
+    z->per4 = (z->c4[kZeroArrays] + nz - 1) / nz;
     return true;
 }
 
 void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const GeomState &gs, const ImageState &is,
                            const int *radii, const BwdScratch &sc, const GaussianGrads &out, hipStream_t s,
-                           bool rows_zeroed) {
+                           const ZeroRows *zr) {
+    const bool rows_zeroed = zr != nullptr;
     if (in.P == 0) return;
     if (!sc.atomic)  // atomic mode: the sums are already in GeomState.acc
         hipLaunchKernelGGL(record_sum_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, cam.gx, in.means3D,
@@ -919,12 +951,15 @@ void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const Ge
             (void)hipMemsetAsync(out.dscales, 0, sizeof(float) * P * 3, s);
             (void)hipMemsetAsync(out.drots, 0, sizeof(float) * P * 4, s);
         }
-        hipLaunchKernelGGL(grad_rows_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, radii, sc, out,
-                           fill || rows_zeroed ? 0 : 1);
+        // rows zeroed by render_bwd: its stamps name the live rows (no grad_rows pass)
+        if (!rows_zeroed)
+            hipLaunchKernelGGL(grad_rows_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, radii, sc, out,
+                               fill ? 0 : 1);
         hipLaunchKernelGGL(grad_live_kernel, dim3((in.P + kLiveRange - 1) / kLiveRange), dim3(256), 0, s, in.P, in.D,
                            in.means3D, in.shs, gs.clamped, in.scales, in.rotations, in.scale_modifier,
                            true_scale_gradient() ? in.scale_modifier : 1.0f, cam.view, cam.proj, cam.campos, cam.tanx,
-                           cam.tany, cam.fx, cam.fy, sc, out, in.raw);
+                           cam.tany, cam.fx, cam.fy, sc, out, in.raw, rows_zeroed ? zr->stamps : nullptr,
+                           rows_zeroed ? zr->stamp : 0u);
         return;
     }
     hipLaunchKernelGGL(preprocess_bwd_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, in.D, in.M, in.means3D,

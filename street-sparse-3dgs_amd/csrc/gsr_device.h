@@ -487,6 +487,7 @@ struct GeomState {          // per Gaussian, written by preprocess
     uint32_t *sb_base_i;
     float4 *acc;            // backward accumulators, 4 float4 (64 B) per Gaussian, zeroed by render_fwd
     int nacc;               // rows of acc (P)
+    uint32_t *live_stamp;   // per Gaussian: the stamp of the last backward whose render_bwd staged it
 };
 // a 4-B packed rect (x0 | y0 << 8 | x1 << 16 | y1 << 24) in the 8-B form (x0 | y0 << 16, x1 | y1 << 16)
 __host__ __device__ __forceinline__ uint2 unpack_rect4(uint32_t q) {

@@ -87,15 +87,19 @@ void launch_binning_scatter(int P, const Camera &cam, const GeomState &gs, const
 void launch_binning_tiles(int P, const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                           bool local_sort, const uint32_t *maxsb, hipStream_t s);
 
-// The dense gradient arrays render_bwd zeroes beside its replay (ZeroRows): the four arrays
-// (float counts n[k], 16-B aligned) as one concatenated float4 range split evenly over the
-// backward's workgroups (per4 float4 each; c4 the cumulative float4 counts).  preprocess_bwd then
-// writes only the live rows (and every row's screen-space mean / opacity gradient).
+// The gradient arrays render_bwd zeroes beside its replay (ZeroRows): up to six arrays (float
+// counts n[k], 16-B aligned; unused entries n = 0) as one concatenated float4 range split evenly
+// over the backward's workgroups (per4 float4 each; c4 the cumulative float4 counts).  render_bwd
+// also stamps the Gaussians it stages (GeomState.live_stamp = this backward's stamp), and
+// preprocess_bwd then runs the chain rule over the stamped rows only and writes nothing else.
+constexpr int kZeroArrays = 6;
 struct ZeroRows {
-    float *p[4];
-    uint64_t n[4];
-    uint64_t c4[5];
+    float *p[kZeroArrays];
+    uint64_t n[kZeroArrays];
+    uint64_t c4[kZeroArrays + 1];
     uint64_t per4;
+    uint32_t *stamps;  // != NULL: render_bwd stamps every staged Gaussian (live_stamp) with `stamp`
+    uint32_t stamp;
 };
 
 // render.hip
@@ -119,11 +123,12 @@ struct GaussianGrads {
 void set_sparse_grad_rows(bool on);
 void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const GeomState &gs, const ImageState &is,
                            const int *radii, const BwdScratch &sc, const GaussianGrads &out, hipStream_t s,
-                           bool rows_zeroed = false);
-// the frame's dense gradient arrays for render_bwd to zero (false: preprocess_bwd writes the zeros
-// itself -- sparse rows, the single-kernel path, unaligned arrays or GSR_BWD_ZERO_IN_RENDER=0)
-bool bwd_zero_rows(const GaussianInputs &in, const GaussianGrads &out, const BwdScratch &sc, int nblocks,
-                   ZeroRows *z);
+                           const ZeroRows *zr = nullptr);
+// the frame's gradient arrays for render_bwd to zero and its live stamps (false: preprocess_bwd
+// writes the zeros itself -- record mode, the single-kernel path, unaligned arrays or
+// GSR_BWD_ZERO_IN_RENDER=0)
+bool bwd_zero_rows(const GaussianInputs &in, const GaussianGrads &out, const BwdScratch &sc, uint32_t *gs_stamps,
+                   int nblocks, ZeroRows *z);
 
 // train.hip: the native train step's fused launches (train_step.hip).  sparse_adam is
 // gsr_sparse_adam_step (flag_ready: the relevance flag is already computed; shrink_raw != NULL:

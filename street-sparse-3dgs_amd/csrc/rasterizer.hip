@@ -207,6 +207,7 @@ GeomState carve_geom(void *base, int P, int gx, int gy, size_t *bytes) {
     g.sb_base_i = c.take<uint32_t>((size_t)g.sb.nsb + 1);
     g.acc = c.take<float4>(4 * (size_t)P);
     g.nacc = P;
+    g.live_stamp = c.take<uint32_t>(P);
     if (bytes) *bytes = align_up(c.off, 256);
     return g;
 }
@@ -857,14 +858,14 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
     {
         StageTimer st(6, s);
         // the dense zero gradient rows go out beside render_bwd's replay (bwd_zero_rows)
-        zeroed = R_inst > 0 && bwd_zero_rows(in, out, sc, T, &zr);
+        zeroed = R_inst > 0 && bwd_zero_rows(in, out, sc, gs.live_stamp, T, &zr);
         if (R_inst > 0)
             launch_render_bwd(cam, gs, bs, is, radii, background, dL_dpix, dL_dinvdepth, sc, s, zeroed ? &zr : nullptr);
     }
     if ((rc = check("render backward", debug, s))) return rc;
     {
         StageTimer st(7, s);
-        launch_preprocess_bwd(in, cam, gs, is, radii, sc, out, s, zeroed);
+        launch_preprocess_bwd(in, cam, gs, is, radii, sc, out, s, zeroed ? &zr : nullptr);
     }
     if ((rc = check("preprocess backward", debug, s))) return rc;
     if (R > 0) {

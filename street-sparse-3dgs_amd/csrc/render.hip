@@ -770,6 +770,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
             r[2] *= -0.5f;
             r[3] *= -0.5f;
             r[4] *= -0.5f;
+            // the Gaussian is live for preprocess_bwd (its sums may still be zero: harmless)
+            if (kAtomic && zr.stamps) zr.stamps[o / 4] = zr.stamp;
             if (!kAtomic) {
                 out[o + 0] = make_float4(r[0], r[1], r[2], r[3]);
                 out[o + 1] = make_float4(r[4], r[5], r[6], r[7]);
@@ -804,12 +806,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
         // the replay, so no wait of the replay covers them -- the VALU-bound replay leaves HBM
         // nearly idle, and preprocess_bwd no longer streams these bytes on its own
         typedef float f4 __attribute__((ext_vector_type(4)));
-        const uint64_t q0 = (uint64_t)blockIdx.x * zr.per4, q1 = min(zr.c4[4], q0 + zr.per4);
+        const uint64_t q0 = (uint64_t)blockIdx.x * zr.per4, q1 = min(zr.c4[kZeroArrays], q0 + zr.per4);
         for (uint64_t q = q0 + (uint64_t)lane; q < q1; q += kWave) {
-            const int k = (q >= zr.c4[1]) + (q >= zr.c4[2]) + (q >= zr.c4[3]);
+            int k = 0;
+#pragma unroll
+            for (int a = 1; a < kZeroArrays; a++) k += q >= zr.c4[a];
             __builtin_nontemporal_store(f4{0.f, 0.f, 0.f, 0.f}, reinterpret_cast<f4 *>(zr.p[k]) + (q - zr.c4[k]));
         }
-        if (blockIdx.x == 0 && lane < 16) {  // the floats past each array's last whole float4
+        if (blockIdx.x == 0 && lane < 4 * kZeroArrays) {  // the floats past each array's last whole float4
             const int k = lane >> 2, t = lane & 3;
             const uint64_t e = 4 * (zr.c4[k + 1] - zr.c4[k]) + (uint64_t)t;
             if (e < zr.n[k]) __builtin_nontemporal_store(0.f, zr.p[k] + e);
