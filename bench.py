@@ -68,15 +68,20 @@ def parse():
 OVERLAPPED_STAGES = ("sh_color",)
 
 
-def algorithmic_bytes(P, Pv, K, T, npix, P1, M=16):
+def algorithmic_bytes(P, Pv, K, T, npix, P1, M=16, Pl=None):
     """Per-launch algorithmic bytes per stage.  SURVEY.md 8(d) figures (M=16 constants; the SH
     term scales with M) for the stages it defines; the binning stages follow this build's
     algorithm: a 32-bit depth sort of P ids (4 LSD passes, 16 B/elem/pass) + the
     gathered scan; level-1 binning reads (order, tiles, rect) twice per Gaussian and writes the
     superblock lists (P1 entries of 8 B, measured per frame: gsr_frame_stats); level 2 re-reads
     them with the rects twice and writes the K-entry point list + ranges.  Upstream's 64-bit
-    6-pass key sort alone would be 24*K*6."""
+    6-pass key sort alone would be 24*K*6.  The dense gradient outputs (56 + 12 M B per Gaussian:
+    means2D 12, opacity 4, means3D 12, SH, scales 12, rotations 16) are zeroed by render_bwd's
+    waves after their replay; preprocess_bwd reads every row's live stamp (4 B), and for the Pl live rows the accumulator (48 B), parameters (40 B) and SH row
+    in and the full gradient row out."""
     sh = 12 * M
+    grad_row = 56 + sh
+    Pl = Pv if Pl is None else Pl
     return {
         # geometry: 44 B of inputs, the GRec minus its colour (48 B) and 4 x 4 B of per-Gaussian
         # outputs; the SH colour pass (side stream, overlapped): SH rows + means + radii in,
@@ -93,8 +98,8 @@ def algorithmic_bytes(P, Pv, K, T, npix, P1, M=16):
         "tile_order": 16 * T,
         "tile_order_bwd": 12 * T,
         "render_fwd": 44 * K + 24 * npix,
-        "render_bwd": 44 * K + 24 * npix + 40 * Pv,
-        "preprocess_bwd": (356 + sh - 192) * P + (260 + sh - 192) * P,
+        "render_bwd": 44 * K + 24 * npix + 40 * Pv + grad_row * P,
+        "preprocess_bwd": 4 * P + (48 + 40 + sh + 12 + grad_row) * Pl,
     }
 
 
@@ -612,9 +617,13 @@ def main():
     # workload statistics for the algorithmic-bytes model (P1 measured: gsr_frame_stats)
     wl = frame_workload(rs, inp, W, H, deg, dev)
     K, Pv, P1 = wl["K"], wl["Pv"], wl["P1"]
+    # live rows (nonzero accumulated sums) of the frame: the rows whose means3D gradient is nonzero
+    # after the last step
+    g3 = inp["means3D"].grad
+    Pl = int((g3 != 0).any(dim=1).sum().item()) if g3 is not None else None
     T = ((W + 15) // 16) * ((H + 15) // 16)
     npix = W * H
-    abytes = algorithmic_bytes(P, Pv, K, T, npix, P1, M=inp["shs"].shape[1])
+    abytes = algorithmic_bytes(P, Pv, K, T, npix, P1, M=inp["shs"].shape[1], Pl=Pl)
     serial_ms = sum(v for k, v in stages.items() if k not in OVERLAPPED_STAGES)
     dom = max(stages, key=lambda k: stages[k]) if stages else "render_bwd"
     dom_ms = stages.get(dom, 0.0)
@@ -639,7 +648,7 @@ def main():
         "data": "synthetic (seeded Gaussians in the frustum, SURVEY.md 8(d); one chunk per rank, seed = rank)",
         "config": {"workload": f"rasterizer fwd+bwd, {P} Gaussians, SH degree {deg}, {W}x{H}, do_depth",
                    "gaussians": P, "width": W, "height": H, "sh_degree": deg, "visible": Pv, "tile_instances": K,
-                   "level1_entries": P1, "tiles": T, "parallelism": f"chunk-per-gpu x{world}"},
+                   "level1_entries": P1, "live_rows": Pl, "tiles": T, "parallelism": f"chunk-per-gpu x{world}"},
         # frac: algorithmic bytes / the kernel's HIP-event time measured here; frac_rocprof: the same
         # bytes / the average duration in the committed rocprofv3 summary of these kernel sources
         # (profiles/, null when no summary of the current sources is committed)
