@@ -783,7 +783,7 @@ __global__ __launch_bounds__(256) void grad_live_kernel(
     const float *__restrict__ scales, const float *__restrict__ rotations, float mod, float dscale_mod,
     const float *__restrict__ viewmatrix, const float *__restrict__ projmatrix, const float *__restrict__ campos_p,
     float tanx, float tany, float fx, float fy, BwdScratch sc, GaussianGrads out, int raw,
-    const uint32_t *__restrict__ stamps, uint32_t stamp) {
+    const uint32_t *__restrict__ stamps, uint32_t stamp, StepAct act) {
     __shared__ uint16_t s_list[kLiveRange];
     __shared__ uint32_t s_off[kLiveRange / 64 + 1];
     __shared__ uint8_t s_byte[256];
@@ -828,6 +828,23 @@ __global__ __launch_bounds__(256) void grad_live_kernel(
     }
     __syncthreads();
     const uint32_t n = s_off[kLiveRange / 64];
+    if (act.on) {
+        // the native step: densification statistics of this thread's visible rows that are not
+        // live (their screen-space gradient is zero: densify_stats_kernel's arithmetic with n = 0)
+        const int64_t r0 = base + 8 * t;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int64_t i = r0 + k;
+            if (i >= P || ((byte >> k) & 1u)) continue;
+            const int r = act.radii[i];
+            if (r > 0) {
+                const float nn = sqrtf(0.f * 0.f + 0.f * 0.f);
+                act.maxr[i] = fmaxf(act.maxr[i], (float)r);
+                act.accum[i] = fmaxf(nn, act.accum[i]);
+                act.denom[i] = act.denom[i] + 1.f;
+            }
+        }
+    }
     const Mat4 V = load_mat4(viewmatrix);
     for (uint32_t e = (uint32_t)t; e < n; e += blockDim.x) {
         const int i = (int)(base + s_list[e]);
@@ -875,6 +892,36 @@ __global__ __launch_bounds__(256) void grad_live_kernel(
         st_out(&out.dmeans3D[3 * i + 2], dm[2]);
         float ds[3], dq[4];
         scale_rot_chain(q, s_in, mod, dscale_mod, dcov, ds, dq);
+        if (act.on) {
+            // the activation backward (train.hip activate_bwd_step_kernel's expressions): exp,
+            // normalise and sigmoid with the skybox lock, the densification statistics and the
+            // relevance flag of this live row
+#pragma unroll
+            for (int k = 0; k < 3; k++) ds[k] = ds[k] * act_scale(act.s_raw[3 * i + k]);
+            const float4 x = act.q_raw[i];
+            const float4 gq = make_float4(dq[0], dq[1], dq[2], dq[3]);
+            const float nq = sqrtf(x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w);
+            const float d = fmaxf(nq, 1e-12f);
+            const float gd =
+                -(gq.x * ((x.x / d) / d) + gq.y * ((x.y / d) / d) + gq.z * ((x.z / d) / d) + gq.w * ((x.w / d) / d));
+            const float gn = nq >= 1e-12f && nq != 0.f ? gd / nq : 0.f;
+            dq[0] = gq.x / d + x.x * gn;
+            dq[1] = gq.y / d + x.y * gn;
+            dq[2] = gq.z / d + x.z * gn;
+            dq[3] = gq.w / d + x.w * gn;
+            const float y = act_opacity(act.o_raw[i]);
+            const float go = (int64_t)i < act.skybox ? 0.f : g[5] * (1.f - y) * y;
+            st_out(&out.dopacity[i], go);
+            if (go != 0.f) *act.flag = 1;
+            const int r = act.radii[i];
+            if (r > 0) {
+                const float gx = g[0], gy = g[1];
+                const float nn = sqrtf(gx * gx + gy * gy);
+                act.maxr[i] = fmaxf(act.maxr[i], (float)r);
+                act.accum[i] = fmaxf(nn, act.accum[i]);
+                act.denom[i] = act.denom[i] + 1.f;
+            }
+        }
         st_out(&out.dscales[3 * i + 0], ds[0]);
         st_out(&out.dscales[3 * i + 1], ds[1]);
         st_out(&out.dscales[3 * i + 2], ds[2]);
@@ -939,6 +986,10 @@ void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const Ge
         hipLaunchKernelGGL(record_sum_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, cam.gx, in.means3D,
                        cam.view, gs.rect8, gs.rect4, gs.offsets, is.boundary, sc, out.dmeans2D, out.dopacity);
     const bool split = split_ok(in, out, sc);
+    note_step_act_done(false);
+    // the native step's fused activation backward needs the raw parameters (GaussianInputs.raw)
+    StepAct act = step_act();
+    if (!in.raw || !out.sparse_rows) act.on = 0;
     if (split) {
         // dense rows: the dead rows' zeros as one fill per gradient array (streaming stores of whole
         // arrays) instead of grad_rows_kernel's per-row stores; grad_live_kernel then overwrites the
@@ -959,7 +1010,8 @@ void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const Ge
                            in.means3D, in.shs, gs.clamped, in.scales, in.rotations, in.scale_modifier,
                            true_scale_gradient() ? in.scale_modifier : 1.0f, cam.view, cam.proj, cam.campos, cam.tanx,
                            cam.tany, cam.fx, cam.fy, sc, out, in.raw, rows_zeroed ? zr->stamps : nullptr,
-                           rows_zeroed ? zr->stamp : 0u);
+                           rows_zeroed ? zr->stamp : 0u, act);
+        note_step_act_done(act.on != 0);
         return;
     }
     hipLaunchKernelGGL(preprocess_bwd_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, in.D, in.M, in.means3D,

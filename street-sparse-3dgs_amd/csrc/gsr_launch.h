@@ -121,6 +121,27 @@ struct GaussianGrads {
 };
 // rasterizer.hip: gsr_rasterize_backward on this thread writes sparse rows (see above)
 void set_sparse_grad_rows(bool on);
+
+// The native step's activation backward fused into the live-row pass of preprocess_bwd
+// (set_step_act around gsr_rasterize_backward): the gradient outputs are then the raw parameters'
+// gradients (dscales / drots / dopacity: of the log-scales, the unnormalised quaternions and the
+// logits, skybox rows' opacity gradient locked at zero, train_single.py:217-223), the
+// densification statistics of every visible row are updated (train_single.py:193-194) and *flag
+// is set when a row's opacity gradient is nonzero (OurAdam's `relevant`).  step_act_done() says
+// whether the last backward on this thread did it (else the caller runs the activation backward).
+struct StepAct {
+    const float *s_raw, *o_raw;
+    const float4 *q_raw;
+    int64_t skybox;
+    const int *radii;
+    float *maxr, *accum, *denom;
+    int *flag;
+    int on;
+};
+void set_step_act(const StepAct *a);
+StepAct step_act();
+void note_step_act_done(bool done);
+bool step_act_done();
 void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const GeomState &gs, const ImageState &is,
                            const int *radii, const BwdScratch &sc, const GaussianGrads &out, hipStream_t s,
                            const ZeroRows *zr = nullptr);

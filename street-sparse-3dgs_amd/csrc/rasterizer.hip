@@ -43,6 +43,8 @@ std::atomic<int> g_binning_mode{GSR_BINNING_DEFAULT};
 // the native train step's sparse gradient rows (gsr_launch.h GaussianGrads), per calling thread
 thread_local bool g_sparse_grad_rows = false;
 thread_local bool g_raw_params = false;  // GaussianInputs.raw, per calling thread
+thread_local gsr::StepAct g_step_act{};    // set_step_act
+thread_local bool g_step_act_done = false;
 constexpr int kMaxDevicesK = 64;
 thread_local hipEvent_t g_k_ready[kMaxDevicesK] = {};
 // per device: capacity for the next frame's point list, 0 = none yet.  It is the largest K of the
@@ -360,6 +362,10 @@ std::atomic<int> g_deterministic{GSR_DETERMINISTIC_DEFAULT};
 bool gsr::true_scale_gradient() { return g_true_scale_grad.load(std::memory_order_relaxed) != 0; }
 void gsr::set_sparse_grad_rows(bool on) { g_sparse_grad_rows = on; }
 void gsr::set_raw_params(bool on) { g_raw_params = on; }
+void gsr::set_step_act(const StepAct *a) { g_step_act = a ? *a : StepAct{}; }
+gsr::StepAct gsr::step_act() { return g_step_act; }
+void gsr::note_step_act_done(bool done) { g_step_act_done = done; }
+bool gsr::step_act_done() { return g_step_act_done; }
 
 namespace {
 // Geometry buffers whose accumulator rows the forward did not clear: forwards made with

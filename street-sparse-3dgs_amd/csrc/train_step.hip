@@ -100,6 +100,9 @@ int fail_step(int rc, const char *what) {
 // GSR_STEP_ACTIVATIONS=1: activations written by their own launch and read by the rasterizer (the
 // Python-driven step's form); default: the rasterizer and the activation backward read the raw
 // parameters and activate them where they are used (GaussianInputs.raw)
+#ifndef GSR_STEP_FUSE_ACT
+#define GSR_STEP_FUSE_ACT 1
+#endif
 #ifndef GSR_STEP_PHOTO_IN_SSIM
 #define GSR_STEP_PHOTO_IN_SSIM 1  // 0: the SSIM pass writes G and the exposure backward forms the gradient
 #endif
@@ -227,20 +230,34 @@ int gsr_train_step(gsr_train_ctx *ctx, const gsr_train_step_args *a, int64_t *nu
     // their 232 B of gradient rows are not written (GSR_STEP_DENSE_ROWS=1: every row, as the
     // Python-driven step)
     const bool sparse_rows = step_sparse_rows();
+    // the activation backward (skybox lock, relevance flag, densification statistics:
+    // train_single.py:193-194, 217-223) fused into the rasterizer backward's live-row pass, which
+    // then writes the raw parameters' gradients itself (gsr_launch.h StepAct); the conditions
+    // mirror backward.hip's split path (GSR_STEP_FUSE_ACT=0: the separate activation backward)
+    const bool fuse_act = GSR_STEP_FUSE_ACT && raw && sparse_rows && a->M == 16 &&
+                          (reinterpret_cast<uintptr_t>(a->features) & 15u) == 0 &&
+                          (reinterpret_cast<uintptr_t>(a->features_grad) & 15u) == 0;
+    const StepAct act{a->scaling, a->opacity, reinterpret_cast<const float4 *>(a->rotation), a->skybox_rows, radii,
+                      a->max_radii2D, a->xyz_gradient_accum, a->denom, flag, 1};
     set_sparse_grad_rows(sparse_rows);
     set_raw_params(raw);
+    set_step_act(fuse_act ? &act : nullptr);
     rc = gsr_rasterize_backward(resize_scratch, ctx, (int)P, a->D, a->M, K, a->background, W, H, a->xyz,
                                      a->features, nullptr, r_scales, 1.0f, r_rots, nullptr, a->viewmatrix, a->projmatrix,
                                      a->campos, a->tan_fovx, a->tan_fovy, radii, buf_ptr(ctx, kGeom),
                                      buf_ptr(ctx, kBinning), buf_ptr(ctx, kImage), d_color, depth ? d_invd : nullptr,
-                                     d_means2D, nullptr, d_opac, a->xyz_grad, nullptr, a->features_grad, d_scales,
-                                     d_rots, nullptr, nullptr, nullptr, nullptr, 0, 0, sv);
+                                     d_means2D, nullptr, fuse_act ? a->opacity_grad : d_opac, a->xyz_grad, nullptr,
+                                     a->features_grad, fuse_act ? a->scaling_grad : d_scales,
+                                     fuse_act ? a->rotation_grad : d_rots, nullptr, nullptr, nullptr, nullptr, 0, 0, sv);
     set_sparse_grad_rows(false);
     set_raw_params(false);
+    set_step_act(nullptr);
     if (rc) return fail_step(rc, "rasterizer backward");
-    // activation backward with the skybox lock, the relevance flag and the densification
-    // statistics (train_single.py:193-194, 217-223); then the sparse Adam and the shrink (:225-241)
-    if ((rc = step_activate_backward(P, a->rotation, raw ? nullptr : scales, raw ? nullptr : opac, d_scales, d_rots,
+    if (fuse_act != step_act_done())
+        return invalid("the rasterizer backward did not take the fused activation backward it was given");
+    // otherwise the activation backward on its own; then the sparse Adam and the shrink (:225-241)
+    if (!fuse_act &&
+        (rc = step_activate_backward(P, a->rotation, raw ? nullptr : scales, raw ? nullptr : opac, d_scales, d_rots,
                                      d_opac, a->scaling_grad, a->rotation_grad, a->opacity_grad, a->skybox_rows, flag,
                                      radii, d_means2D, a->max_radii2D, a->xyz_gradient_accum, a->denom, s, sparse_rows,
                                      a->scaling, a->opacity)))
