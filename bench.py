@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--config5", action="store_true", help=argparse.SUPPRESS)  # round-2 spelling: now the default
     ap.add_argument("--no-street", action="store_true",
                     help="skip the street-frame point (1536x1536 cube face, 90 deg fov: fwd+bwd and train step)")
+    ap.add_argument("--no-coarse-debug", action="store_true", help="skip the render_coarse debug-mode timing")
     ap.add_argument("--no-config4", action="store_true",
                     help="skip config 4 (500k-Gaussian chunk per rank, seed = chunk id: fwd+bwd and train step)")
     ap.add_argument("--metric-only", action="store_true",
@@ -429,14 +430,14 @@ class Ranks:
         return max(self.gather(x))
 
 
-def rasterizer_for(s, W, H, deg, dev):
+def rasterizer_for(s, W, H, deg, dev, debug=False):
     import torch
     from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
     t = lambda x: torch.tensor(x, dtype=torch.float32, device=dev)
     rs = GaussianRasterizationSettings(
         image_height=H, image_width=W, tanfovx=float(s["tanfovx"]), tanfovy=float(s["tanfovy"]), bg=t(s["bg"]),
         scale_modifier=1.0, viewmatrix=t(s["view"]).reshape(4, 4), projmatrix=t(s["proj"]).reshape(4, 4),
-        sh_degree=deg, campos=t(s["campos"]), prefiltered=False, debug=False, do_depth=True,
+        sh_degree=deg, campos=t(s["campos"]), prefiltered=False, debug=debug, do_depth=True,
         render_indices=torch.empty(0, dtype=torch.int32), parent_indices=torch.empty(0, dtype=torch.int32),
         interpolation_weights=torch.empty(0, device=dev), num_node_kids=torch.empty(0, dtype=torch.int32, device=dev))
     return rs, GaussianRasterizer(rs)
@@ -549,12 +550,40 @@ def street_frame(a, dev):
     return out
 
 
+def coarse_debug(a, dev):
+    """render_coarse's frames: debug forced on (gaussian_renderer/__init__.py:341), SH degree 1
+    (shs (P, 4, 3), train_coarse.py:31), 500k Gaussians at 1080p.  fwd+bwd ms with debug off, with
+    debug on (device-side input snapshots and a synchronize + error check after every stage), and
+    with upstream's host snapshots (GSR_DEBUG_HOST_SNAPSHOT=1: every input deep-copied to the host
+    before each forward and backward, diff_gaussian_rasterization/__init__.py:26-28,53-54,90-91)."""
+    import torch
+    P, W, H, deg = 500_000, a.width, a.height, 1
+    s, inp, gcol, ginv = make_inputs(P, W, H, deg, seed=0, device=dev)
+    one = Ranks(1, 0, False, dev)
+    out = {"workload": f"render_coarse frame: {P} Gaussians, SH degree 1 (M = 4), {W}x{H}, fwd+bwd, do_depth"}
+    steps = max(5, a.steps // 2)
+    for name, debug, host in (("debug_off_ms", False, False), ("debug_ms", True, False),
+                              ("debug_host_snapshot_ms", True, True)):
+        if host:
+            os.environ["GSR_DEBUG_HOST_SNAPSHOT"] = "1"
+        try:
+            _, raster = rasterizer_for(s, W, H, deg, dev, debug=debug)
+            el = timed(fwd_bwd_step(raster, inp, gcol, ginv), steps, 3, one)
+        finally:
+            os.environ.pop("GSR_DEBUG_HOST_SNAPSHOT", None)
+        out[name] = round(el / steps * 1e3, 4)
+    del inp
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     a = parse()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(a))
     if a.metric_only:
         a.train_steps, a.no_config5, a.no_street, a.no_config4, a.no_cpu_baseline = 0, True, True, True, True
+        a.no_coarse_debug = True
     import torch
     import torch.distributed as dist
 
@@ -693,6 +722,9 @@ def main():
     if world == 1 and not a.no_street:
         log("street frame")
         out["street_frame"] = street_frame(a, dev)
+    if world == 1 and not a.no_coarse_debug:
+        log("render_coarse debug mode")
+        out["coarse_debug"] = coarse_debug(a, dev)
     if world == 1 and not a.no_config5:
         log("config 5")
         out["config5"] = config5(a, dev)

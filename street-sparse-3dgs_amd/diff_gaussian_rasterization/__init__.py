@@ -13,6 +13,7 @@ hand-written HIP kernels of libgsr_hip.so (street-sparse-3dgs_amd/csrc); there i
 """
 from __future__ import annotations
 
+import os
 from typing import NamedTuple
 
 import torch
@@ -23,9 +24,22 @@ from . import _C
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "_C"]
 
 
-def _host_copy(args):
-    """Host copies of the call's tensors, kept so a failing debug-mode call can be replayed."""
-    return tuple(a.cpu().clone() if isinstance(a, torch.Tensor) else a for a in args)
+def _snapshot(args):
+    """Debug mode: copies of the call's tensors, kept so a failing call can be replayed.
+
+    Upstream deep-copies every tensor to the host before each debug-mode call
+    (diff_gaussian_rasterization/__init__.py:26-28,53-54,90-91), which render_coarse pays on every
+    frame (gaussian_renderer/__init__.py:341 forces debug).  Here the copies stay on the device (one
+    device-to-device clone per tensor, at HBM rate) and move to the host only when the call fails --
+    the dump the caller sees is the same host tuple.  A failure that leaves the device unusable
+    aborts the process on ROCm before any Python handler runs, so a host copy would not survive it
+    either.  GSR_DEBUG_HOST_SNAPSHOT=1 takes upstream's host copies instead (read per call)."""
+    host = os.environ.get("GSR_DEBUG_HOST_SNAPSHOT") == "1"
+    return tuple((a.cpu().clone() if host else a.clone()) if isinstance(a, torch.Tensor) else a for a in args)
+
+
+def _dump(saved, path):
+    torch.save(tuple(a.cpu() if isinstance(a, torch.Tensor) else a for a in saved), path)
 
 
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
@@ -56,12 +70,12 @@ class _RasterizeGaussians(torch.autograd.Function):
                 _hier(rs, "parent_indices"), _hier(rs, "interpolation_weights"), _hier(rs, "num_node_kids"),
                 do_depth)
         if rs.debug:
-            saved = _host_copy(args)
+            saved = _snapshot(args)
             try:
                 num_rendered, color, invdepth, radii, geomBuffer, binningBuffer, imgBuffer = \
                     _C.rasterize_gaussians(*args, need_backward=need_backward)
             except Exception:
-                torch.save(saved, "snapshot_fw.dump")
+                _dump(saved, "snapshot_fw.dump")
                 print("\n[diff_gaussian_rasterization] forward failed in debug mode; its inputs are in "
                       "snapshot_fw.dump (torch.load it and call _C.rasterize_gaussians(*args) to replay)")
                 raise
@@ -94,11 +108,11 @@ class _RasterizeGaussians(torch.autograd.Function):
                 ctx.num_rendered, binningBuffer, imgBuffer, _hier(rs, "render_indices"), _hier(rs, "parent_indices"),
                 _hier(rs, "interpolation_weights"), _hier(rs, "num_node_kids"), rs.debug)
         if rs.debug:
-            saved = _host_copy(args)
+            saved = _snapshot(args)
             try:
                 grads = _C.rasterize_gaussians_backward(*args)
             except Exception:
-                torch.save(saved, "snapshot_bw.dump")
+                _dump(saved, "snapshot_bw.dump")
                 print("\n[diff_gaussian_rasterization] backward failed in debug mode; its inputs are in "
                       "snapshot_bw.dump (replay with _C.rasterize_gaussians_backward(*args))")
                 raise

@@ -136,3 +136,25 @@ def test_product_never_imports_oracle():
                 bad = re.findall(r"(?:import|from)\s+(?:gs_oracle|dense_torch)|#include\s*[<\"][^>\"]*oracle|"
                                  r"CDLL\([^)]*oracle", text)
                 assert not bad, (f, bad)
+
+
+@pytest.mark.parametrize("host_snapshot", [False, True])
+def test_debug_mode_dumps_inputs_of_a_failing_call(tmp_path, monkeypatch, host_snapshot):
+    """Debug mode (upstream diff_gaussian_rasterization/__init__.py:26-28,53-67): a failing forward
+    writes its inputs to snapshot_fw.dump as host tensors and re-raises.  The copies are taken on
+    the tensors' device before the call (GSR_DEBUG_HOST_SNAPSHOT=1: upstream's host copies)."""
+    from diff_gaussian_rasterization import GaussianRasterizer
+    monkeypatch.chdir(tmp_path)
+    if host_snapshot:
+        monkeypatch.setenv("GSR_DEBUG_HOST_SNAPSHOT", "1")
+    r = GaussianRasterizer(_settings(debug=True, sh_degree=1))
+    g = torch.Generator().manual_seed(0)
+    m = torch.randn(4, 3, generator=g)
+    shs = torch.randn(4, 4, 3, generator=g)
+    with pytest.raises(RuntimeError, match="ROCm GPU"):  # CPU tensors: the library refuses them
+        r(means3D=m, means2D=torch.zeros(4, 3), opacities=torch.rand(4, 1, generator=g), shs=shs, scales=m.abs(),
+          rotations=torch.randn(4, 4, generator=g))
+    saved = torch.load(tmp_path / "snapshot_fw.dump", weights_only=True)
+    # upstream's argument order (_RasterizeGaussians.forward): bg, means3D, colors, opacities, ...
+    assert torch.equal(saved[1], m) and torch.equal(saved[14], shs) and saved[15] == 1 and saved[18] is True
+    assert all(a.device.type == "cpu" for a in saved if isinstance(a, torch.Tensor))
