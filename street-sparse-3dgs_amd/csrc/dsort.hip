@@ -91,6 +91,13 @@ __device__ uint64_t *g_ds_trace;
 #define DS_STAMP_AFTER(kern, slot, x) DS_STAMP(kern, slot)
 #endif
 
+// GSR_DSORT_CARRY: with 4-B rects, the tile rect travels with the Gaussian id through the four
+// passes (read coalesced by pass 0 in index order, ping-ponged through the idle rect8 array), so
+// pass 3 stores it instead of gathering rect4[id] -- one random 64-B line per Gaussian.
+#ifndef GSR_DSORT_CARRY
+#define GSR_DSORT_CARRY 1
+#endif
+
 constexpr uint32_t kFlagAgg = 1u << 30, kFlagInc = 2u << 30, kCountMask = (1u << 30) - 1u;
 
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t *p) {
@@ -221,11 +228,17 @@ __global__ __launch_bounds__(kDsThreads) void dsort_pass_kernel(int P, int nb, c
                                                                  const uint2 *__restrict__ rect8,
                                                                  const uint32_t *__restrict__ rect4,
                                                                  uint2 *__restrict__ drect,
+                                                                 const uint32_t *__restrict__ rin,
+                                                                 uint32_t *__restrict__ rout,
                                                                  uint32_t *__restrict__ host_err) {
     constexpr bool kFirst = kPass == 0, kLast = kPass == kPasses - 1;
+    // rect carry (GSR_DSORT_CARRY): pass 0 reads rect4 itself, the others rin; pass 3 stores into
+    // drect's 4-B form, the others into rout
+    const bool carry = GSR_DSORT_CARRY && rect4 != nullptr;
     constexpr int kShift = 8 * kPass;
     __shared__ uint32_t s_key[kDsTile];
     __shared__ uint32_t s_val[kDsTile];
+    __shared__ uint32_t s_rc[GSR_DSORT_CARRY ? kDsTile : 1];  // carried rects
     __shared__ uint32_t s_wh[kDsWaves][kRadix];  // per-wave digit counts -> exclusive prefix over waves
     __shared__ uint32_t s_gb[4][kRadix];         // global digit base (4 partial sums, then [0] scanned)
     __shared__ uint32_t s_bex[kRadix];           // tile-local digit base
@@ -265,7 +278,8 @@ __global__ __launch_bounds__(kDsThreads) void dsort_pass_kernel(int P, int nb, c
     const int wbase = w * kDsItems * kWave;
     const size_t tile0 = (size_t)v * kDsTile;
     const int n = (int)min((size_t)kDsTile, (size_t)P - tile0);
-    uint32_t key[kDsItems], val[kDsItems], tl[kDsItems];
+    uint32_t key[kDsItems], val[kDsItems], tl[kDsItems], rc[kDsItems];
+    const uint32_t *rsrc = kFirst ? rect4 : rin;
 #pragma unroll
     for (int k = 0; k < kDsItems; k++) {
         const int i = wbase + k * kWave + lane;
@@ -273,6 +287,8 @@ __global__ __launch_bounds__(kDsThreads) void dsort_pass_kernel(int P, int nb, c
         key[k] = valid ? kin[tile0 + i] : 0xFFFFFFFFu;
         val[k] = kFirst ? (uint32_t)(tile0 + i) : (valid ? vin[tile0 + i] : 0u);
         tl[k] = (kFirst && valid) ? tiles[tile0 + i] : 0u;
+        // pass 0 loads its rects after the histogram rows are summed (register pressure)
+        rc[k] = (!kFirst && carry && valid) ? rsrc[tile0 + i] : 0u;
     }
     DS_STAMP_AFTER(1 + kPass, 6, key[kDsItems - 1] + val[kDsItems - 1]);
     uint32_t toff[kDsItems];
@@ -316,6 +332,13 @@ __global__ __launch_bounds__(kDsThreads) void dsort_pass_kernel(int P, int nb, c
         for (int q = 0; q < kUpMax / 4; q++) c += h[q];
         s_gb[t >> 8][t & (kRadix - 1)] = c;
     }
+    if (kFirst && carry) {
+#pragma unroll
+        for (int k = 0; k < kDsItems; k++) {
+            const int i = wbase + k * kWave + lane;
+            rc[k] = i < n ? rsrc[tile0 + i] : 0u;
+        }
+    }
     __syncthreads();
     DS_STAMP(1 + kPass, 1);
     if (kFirst) {
@@ -354,6 +377,7 @@ __global__ __launch_bounds__(kDsThreads) void dsort_pass_kernel(int P, int nb, c
             const uint32_t lp = s_bex[d] + s_wh[w][d] + rk[k];
             s_key[lp] = key[k];
             s_val[lp] = val[k];
+            if (GSR_DSORT_CARRY && carry) s_rc[lp] = rc[k];
         }
     }
     DS_STAMP(1 + kPass, 7);
@@ -404,7 +428,9 @@ __global__ __launch_bounds__(kDsThreads) void dsort_pass_kernel(int P, int nb, c
         const uint32_t g = s_val[i];
         if (kLast) {
             vout[j] = g;
-            if (rect4) {
+            if (GSR_DSORT_CARRY && carry) {
+                reinterpret_cast<uint32_t *>(drect)[j] = s_rc[i];  // drect4_of(gs), carried
+            } else if (rect4) {
                 reinterpret_cast<uint32_t *>(drect)[j] = rect4[g];  // drect4_of(gs)
             } else {
                 drect[j] = rect8[g];
@@ -412,6 +438,7 @@ __global__ __launch_bounds__(kDsThreads) void dsort_pass_kernel(int P, int nb, c
         } else {
             kout[j] = k;
             vout[j] = g;
+            if (GSR_DSORT_CARRY && carry) rout[j] = s_rc[i];
         }
     }
     DS_STAMP(1 + kPass, 4);
@@ -431,15 +458,19 @@ void launch_depth_sort(int P, const GeomState &gs, uint32_t *host_K, uint32_t *h
     hipLaunchKernelGGL(dsort_upsweep_kernel, dim3(up_blocks(nb)), dim3(kDsThreads), 0, s, P, nb, gs.dkey, gs.tiles,
                        gs.ctrl, host_K);
     if (k_ready) (void)hipEventRecord(k_ready, s);
-    // keys: dkey -> dkey_sorted -> dkey -> dkey_sorted -> (none); values: (index) -> ids -> order -> ids -> order
+    // keys: dkey -> dkey_sorted -> dkey -> dkey_sorted -> (none); values: (index) -> ids -> order -> ids -> order;
+    // carried 4-B rects (rect4 set: rect8 is idle, two P-word halves): rect4 -> A -> B -> A -> drect
+    uint32_t *ra = reinterpret_cast<uint32_t *>(gs.rect8), *rb = ra + P;
     hipLaunchKernelGGL(dsort_pass_kernel<0>, dim3(nb), dim3(kDsThreads), 0, s, P, nb, gs.dkey, gs.dkey_sorted,
-                       (const uint32_t *)nullptr, gs.ids, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.rect4, gs.drect, host_err);
+                       (const uint32_t *)nullptr, gs.ids, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.rect4, gs.drect,
+                       (const uint32_t *)nullptr, ra, host_err);
     hipLaunchKernelGGL(dsort_pass_kernel<1>, dim3(nb), dim3(kDsThreads), 0, s, P, nb, gs.dkey_sorted, gs.dkey, gs.ids,
-                       gs.order, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.rect4, gs.drect, host_err);
+                       gs.order, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.rect4, gs.drect, ra, rb, host_err);
     hipLaunchKernelGGL(dsort_pass_kernel<2>, dim3(nb), dim3(kDsThreads), 0, s, P, nb, gs.dkey, gs.dkey_sorted, gs.order,
-                       gs.ids, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.rect4, gs.drect, host_err);
+                       gs.ids, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.rect4, gs.drect, rb, ra, host_err);
     hipLaunchKernelGGL(dsort_pass_kernel<3>, dim3(nb), dim3(kDsThreads), 0, s, P, nb, gs.dkey_sorted,
-                       (uint32_t *)nullptr, gs.ids, gs.order, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.rect4, gs.drect, host_err);
+                       (uint32_t *)nullptr, gs.ids, gs.order, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.rect4, gs.drect,
+                       ra, (uint32_t *)nullptr, host_err);
 }
 
 uint32_t *dsort_K_word(const GeomState &gs) { return gs.ctrl + kCtlK; }
