@@ -170,38 +170,58 @@ constexpr int kColorWaves = GSR_COLOR_WAVES;  // waves per block (13 KiB of LDS 
 #endif
 constexpr int kColorThreads = kColorWaves * kWave;
 
-__device__ __forceinline__ void color_block(int vb, float4 *s_sh, int P, int D, const float *__restrict__ means3D,
-                                            const float *__restrict__ shs, const float *__restrict__ campos,
-                                            const float *__restrict__ viewmatrix, const int *__restrict__ radii,
-                                            const GeomState &gs) {
+// GSR_COLOR_PF: each wave issues the next row block's SH loads before it evaluates the current
+// one (the persistent grid walks row blocks; with one 8-wave block per CU the VGPR budget, not
+// occupancy, pays for the second 48-VGPR buffer), so a CU keeps twice the bytes in flight
+#ifndef GSR_COLOR_PF
+#define GSR_COLOR_PF 0  // measured: no step-time change (r03x), the pass is off the critical path
+#endif
+
+struct ShRows {
+    float4 v[kShRow];
+    bool vis;
+};
+
+// The wave's 64 SH rows of row block vb into registers, 1 KiB contiguous per load instruction.
+__device__ __forceinline__ void color_fetch(int vb, ShRows &r, int P, int D, const float *__restrict__ shs,
+                                            const int *__restrict__ radii) {
     const int i = vb * blockDim.x + threadIdx.x;
-    const bool vis = i < P && radii[i] > 0;
+    r.vis = i < P && radii[i] > 0;
     const int nc = (D + 1) * (D + 1);
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    float4 *S = s_sh + wv * kWave * kShPitch;
-    const uint64_t need = __ballot(vis);
+    const uint64_t need = __ballot(r.vis);
     const int64_t row0 = (int64_t)vb * blockDim.x + wv * kWave;
     const int cols = (nc * 3 + 3) / 4;  // float4 per row that hold active coefficients
     const float4 *src4 = reinterpret_cast<const float4 *>(shs) + row0 * kShRow;
-    float4 v[kShRow];
 #pragma unroll
     for (int k = 0; k < kShRow; k++) {
         const int f = k * kWave + lane, row = f / kShRow, col = f - row * kShRow;
-        v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        r.v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (((need >> row) & 1ull) && col < cols) {
             if (GSR_SH_NT) {
                 typedef float f4 __attribute__((ext_vector_type(4)));
                 const f4 t = __builtin_nontemporal_load(reinterpret_cast<const f4 *>(src4 + f));
-                v[k] = make_float4(t.x, t.y, t.z, t.w);
+                r.v[k] = make_float4(t.x, t.y, t.z, t.w);
             } else {
-                v[k] = src4[f];
+                r.v[k] = src4[f];
             }
         }
     }
+}
+
+// Rows through the wave's LDS tile to one row per lane, then the colour of that lane's Gaussian.
+__device__ __forceinline__ void color_finish(int vb, const ShRows &r, float4 *s_sh, int P, int D,
+                                             const float *__restrict__ means3D, const float *__restrict__ campos,
+                                             const float *__restrict__ viewmatrix, const GeomState &gs) {
+    const int i = vb * blockDim.x + threadIdx.x;
+    const int nc = (D + 1) * (D + 1);
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float4 *S = s_sh + wv * kWave * kShPitch;
+    __builtin_amdgcn_wave_barrier();  // the wave's previous reads of its tile are done
 #pragma unroll
     for (int k = 0; k < kShRow; k++) {
         const int f = k * kWave + lane, row = f / kShRow, col = f - row * kShRow;
-        S[row * kShPitch + col] = v[k];
+        S[row * kShPitch + col] = r.v[k];
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS writes landed
     __builtin_amdgcn_wave_barrier();
@@ -212,7 +232,7 @@ __device__ __forceinline__ void color_block(int vb, float4 *s_sh, int P, int D, 
         sh[4 * c] = w.x; sh[4 * c + 1] = w.y; sh[4 * c + 2] = w.z; sh[4 * c + 3] = w.w;
     }
     if (i >= P) return;
-    if (!vis) {
+    if (!r.vis) {
         gs.clamped[i] = 0;
         return;
     }
@@ -237,7 +257,8 @@ __device__ __forceinline__ void color_block(int vb, float4 *s_sh, int P, int D, 
 }
 
 // GSR_COLOR_BLOCKS > 0: a persistent grid of that many blocks walks the row blocks (so the pass
-// can be held to part of the chip while latency-bound work runs beside it)
+// can be held to part of the chip while latency-bound work runs beside it).  Each wave owns its
+// LDS tile (no block-wide barrier between row blocks).
 __global__ __launch_bounds__(kColorThreads) void preprocess_color_kernel(int P, int D, const float *__restrict__ means3D,
                                                                          const float *__restrict__ shs,
                                                                          const float *__restrict__ campos,
@@ -245,9 +266,22 @@ __global__ __launch_bounds__(kColorThreads) void preprocess_color_kernel(int P, 
                                                                          const int *__restrict__ radii, GeomState gs,
                                                                          int nvb) {
     __shared__ float4 s_sh[kColorWaves * kWave * kShPitch];
-    for (int vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
-        color_block(vb, s_sh, P, D, means3D, shs, campos, viewmatrix, radii, gs);
-        __syncthreads();  // the next row block's staging reuses s_sh
+    if (GSR_COLOR_PF) {
+        ShRows cur, nxt;
+        int vb = blockIdx.x;
+        if (vb < nvb) color_fetch(vb, cur, P, D, shs, radii);
+        for (; vb < nvb; vb += gridDim.x) {
+            const int vn = vb + (int)gridDim.x;
+            if (vn < nvb) color_fetch(vn, nxt, P, D, shs, radii);
+            color_finish(vb, cur, s_sh, P, D, means3D, campos, viewmatrix, gs);
+            cur = nxt;
+        }
+    } else {
+        for (int vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
+            ShRows cur;
+            color_fetch(vb, cur, P, D, shs, radii);
+            color_finish(vb, cur, s_sh, P, D, means3D, campos, viewmatrix, gs);
+        }
     }
 }
 
