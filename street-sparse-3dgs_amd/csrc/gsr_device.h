@@ -449,6 +449,15 @@ struct SBGrid {
     int shift, nsbx, nsby, nsb, nchunks, chunk;  // chunk: depth-ordered Gaussians per level-1 chunk
     int cper, ccols;                             // counter columns per XCD, row stride of the counters
 };
+// GSR_BWD_CLS: render_fwd's workgroups place their tile in one of kBwdClasses backward work
+// classes (a counter atomic) and render_bwd's workgroups find their tile from the class counts --
+// the backward launch order without a tile_order launch between the forward and the backward
+#ifndef GSR_BWD_CLS
+#define GSR_BWD_CLS 1
+#endif
+constexpr int kBwdClasses = 256;
+constexpr int kBwdClassShift = 2;  // class = 255 - min(work >> 2, 255): heaviest first
+
 #ifndef GSR_RECT4
 #define GSR_RECT4 1
 #endif
@@ -523,7 +532,9 @@ struct ImageState {
     uint32_t *n_contrib;    // per pixel: 1-based list position of the last contributor
     uint32_t *tile_work;    // per tile: backward work (last contributor position, max over pixels)
     uint32_t *tile_ids;     // forward launch order (tiles by descending list length)
-    uint32_t *tile_order;   // backward launch order (tiles by descending tile_work)
+    uint32_t *tile_order;   // backward launch order (tiles by descending tile_work; GSR_BWD_CLS = 0)
+    uint32_t *bwd_cnt;      // GSR_BWD_CLS: per backward work class, the tiles render_fwd placed in it
+    uint32_t *bwd_cls;      // ... and those tiles, class c at [c * T, c * T + bwd_cnt[c])
 };
 
 // Backward per-instance gradient records, one 64-B line each, indexed by the instance's unsorted

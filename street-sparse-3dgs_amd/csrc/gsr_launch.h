@@ -44,7 +44,7 @@ void launch_preprocess_color(const GaussianInputs &in, const Camera &cam, const 
                              hipStream_t s, int blocks = 0);
 // render.hip: tiles ordered heaviest first by work[t] (or, with work == NULL, by list length).
 void launch_tile_order(const uint32_t *work, const uint2 *ranges, int T, int shift, uint32_t *order, hipStream_t s,
-                       const uint32_t *kdev = nullptr, uint32_t cap = 0);
+                       const uint32_t *kdev = nullptr, uint32_t cap = 0, uint32_t *zero_classes = nullptr);
 void launch_mark_visible(int P, const float *means3D, const float *view, uint8_t *present, hipStream_t s);
 
 // sort.hip (rocPRIM)
@@ -104,7 +104,7 @@ struct ZeroRows {
 
 // render.hip
 void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
-                       const float *bg, float *out_color, float *out_invdepth, hipStream_t s);
+                       const float *bg, float *out_color, float *out_invdepth, hipStream_t s, bool need_bwd = true);
 void launch_render_bwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                        const int *radii, const float *bg, const float *dL_dpix, const float *dL_dinvdepth,
                        const BwdScratch &sc, hipStream_t s, const ZeroRows *zr = nullptr);

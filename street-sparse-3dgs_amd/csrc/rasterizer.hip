@@ -240,6 +240,8 @@ ImageState carve_image(void *base, int T, int npix, size_t *bytes) {
     s.tile_work = c.take<uint32_t>(T);
     s.tile_ids = c.take<uint32_t>(T);
     s.tile_order = c.take<uint32_t>(T);
+    s.bwd_cnt = c.take<uint32_t>(kBwdClasses);
+    s.bwd_cls = c.take<uint32_t>((size_t)kBwdClasses * T);
     if (bytes) *bytes = align_up(c.off, 256);
     return s;
 }
@@ -710,7 +712,9 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
         if ((r = check("binning (tiles)", debug, s))) return r;
         {
             StageTimer st(4, s);
-            launch_tile_order(nullptr, is.ranges, T, 4, is.tile_ids, s, bs.kdev, bs.cap);  // forward order: by list length
+            // forward order: by list length (and the backward's class counters zeroed)
+            launch_tile_order(nullptr, is.ranges, T, 4, is.tile_ids, s, bs.kdev, bs.cap,
+                              GSR_BWD_CLS && need_bwd ? is.bwd_cnt : nullptr);
         }
         if ((r = check("tile order", debug, s))) return r;
         if (split && !GSR_COLOR_SERIAL && !joined) {
@@ -720,9 +724,9 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
         }
         {
             StageTimer st(5, s);
-            launch_render_fwd(cam, gs, bs, is, background, out_color, out_invdepth, s);
+            launch_render_fwd(cam, gs, bs, is, background, out_color, out_invdepth, s, need_bwd);
         }
-        if (need_bwd) {
+        if (need_bwd && !GSR_BWD_CLS) {
             StageTimer st(9, s);  // backward launch order, from the forward's per-tile work
             launch_tile_order(is.tile_work, is.ranges, T, 2, is.tile_order, s, bs.kdev, bs.cap);
         }

@@ -170,7 +170,8 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kerne
     const GRec *__restrict__ rec, const float *__restrict__ bg, float *__restrict__ out_color,
     float *__restrict__ out_invd, float *__restrict__ final_T, uint32_t *__restrict__ n_contrib,
     uint32_t *__restrict__ tile_work, const uint32_t *__restrict__ fwd_order, const uint32_t *__restrict__ kdev,
-    uint32_t cap, const uint32_t *__restrict__ sort_err, float4 *__restrict__ acc, uint32_t acc_n4) {
+    uint32_t cap, const uint32_t *__restrict__ sort_err, float4 *__restrict__ acc, uint32_t acc_n4,
+    uint32_t *__restrict__ bwd_cnt, uint32_t *__restrict__ bwd_cls) {
     constexpr int kWaves = kPixPerLane / kSub;
     if (kdev && *kdev > cap) return;  // the point-list capacity is short: the host re-runs at K
     {
@@ -356,17 +357,55 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kerne
         }
     }
     wl = wave_max_u32(wl);
+    // the tile's backward work (last contributor position): tile_work, and with bwd_cnt its slot in
+    // the backward's heaviest-first class lists
+    const auto publish = [&](uint32_t mx) {
+        tile_work[tile] = mx;
+        if (bwd_cnt) {
+            const uint32_t k = mx >> kBwdClassShift;
+            const uint32_t c = (uint32_t)(kBwdClasses - 1) - (k < (uint32_t)(kBwdClasses - 1) ? k : (uint32_t)(kBwdClasses - 1));
+            const uint32_t r = atomicAdd(&bwd_cnt[c], 1u);
+            bwd_cls[(size_t)c * gridDim.x + r] = (uint32_t)tile;
+        }
+    };
     if (kWaves == 1) {
-        if (lane == 0) tile_work[tile] = wl;
+        if (lane == 0) publish(wl);
     } else {
         if (lane == 0) s_work[w] = wl;
         __syncthreads();
         if (threadIdx.x == 0) {
             uint32_t mx = s_work[0];
             for (int k = 1; k < kWaves; k++) mx = s_work[k] > mx ? s_work[k] : mx;
-            tile_work[tile] = mx;
+            publish(mx);
         }
     }
+}
+
+// render_bwd's tile with GSR_BWD_CLS: workgroup b takes the (b - first)-th tile of the class whose
+// range of launch positions holds b (class c covers [sum of counts below c, + count c)), from the
+// 256 class counts render_fwd left (4 per lane, one wave scan).
+__device__ __forceinline__ int bwd_tile_of(uint32_t b, const uint32_t *__restrict__ cnt, const uint32_t *__restrict__ cls,
+                                           int T) {
+    const int lane = threadIdx.x & 63;
+    const uint4 c4 = reinterpret_cast<const uint4 *>(cnt)[lane];
+    const uint32_t s4 = c4.x + c4.y + c4.z + c4.w;
+    uint32_t incl = s4;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    const uint32_t excl = incl - s4;
+    const uint64_t hit = __ballot(b >= excl && b < incl);
+    const int L = hit ? __ffsll((unsigned long long)hit) - 1 : 0;
+    uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)excl, L);
+    const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)c4.x, L), y = (uint32_t)__builtin_amdgcn_readlane((int)c4.y, L),
+                   z = (uint32_t)__builtin_amdgcn_readlane((int)c4.z, L);
+    int c = 4 * L;
+    if (b >= off + x) { off += x; c++;
+        if (b >= off + y) { off += y; c++;
+            if (b >= off + z) { off += z; c++; } } }
+    return (int)cls[(size_t)c * T + (b - off)];
 }
 
 // Launch order for a tile pass, heaviest first (longest-processing-time-first list scheduling):
@@ -374,7 +413,10 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kerne
 // 2^shift instances (LDS histogram, scan, scatter).  Order within a class is arbitrary; every
 // tile writes only its own outputs, so results do not depend on it.
 __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t *__restrict__ work, const uint2 *__restrict__ ranges,
-                                                          int T, int shift, uint32_t *__restrict__ order, const uint32_t *__restrict__ kdev, uint32_t cap) {
+                                                          int T, int shift, uint32_t *__restrict__ order, const uint32_t *__restrict__ kdev, uint32_t cap,
+                                                          uint32_t *__restrict__ zero_classes) {
+    // the forward order's launch also zeroes the backward class counters render_fwd fills
+    if (zero_classes && threadIdx.x < kBwdClasses) zero_classes[threadIdx.x] = 0u;
     if (kdev && *kdev > cap) return;  // ranges / work were not written this pass (capacity re-run)
     __shared__ uint32_t hist[256];
     if (threadIdx.x < 256) hist[threadIdx.x] = 0u;
@@ -406,20 +448,21 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t *__rest
 }
 
 void launch_tile_order(const uint32_t *work, const uint2 *ranges, int T, int shift, uint32_t *order, hipStream_t s,
-                       const uint32_t *kdev, uint32_t cap) {
+                       const uint32_t *kdev, uint32_t cap, uint32_t *zero_classes) {
     if (T == 0) return;
-    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, s, work, ranges, T, shift, order, kdev, cap);
+    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, s, work, ranges, T, shift, order, kdev, cap, zero_classes);
 }
 
 void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
-                       const float *bg, float *out_color, float *out_invdepth, hipStream_t s) {
+                       const float *bg, float *out_color, float *out_invdepth, hipStream_t s, bool need_bwd) {
     const int T = cam.gx * cam.gy;
     if (T == 0) return;
     // launch order: is.tile_ids (rasterizer.hip, by list length)
 #define GSR_FWD_LAUNCH(K, NT)                                                                                       \
     hipLaunchKernelGGL(K, dim3(T), dim3(NT), 0, s, is.ranges, bs.point_list, cam.W, cam.H, cam.gx, gs.rec, bg,      \
                        out_color, out_invdepth, is.final_T, is.n_contrib, is.tile_work, is.tile_ids, bs.kdev, bs.cap, \
-                       bs.kdev ? dsort_err_word(gs) : nullptr, gs.acc, (uint32_t)(4 * (size_t)gs.nacc))
+                       bs.kdev ? dsort_err_word(gs) : nullptr, gs.acc, (uint32_t)(4 * (size_t)gs.nacc),              \
+                       GSR_BWD_CLS && need_bwd ? is.bwd_cnt : nullptr, is.bwd_cls)
     static_assert(GSR_FWD_SUB == 1 || GSR_FWD_SUB == 2 || GSR_FWD_SUB == 4, "GSR_FWD_SUB: 1, 2 or 4");
     GSR_FWD_LAUNCH(render_fwd_kernel<GSR_FWD_SUB>, kWave * (kPixPerLane / GSR_FWD_SUB));
 #undef GSR_FWD_LAUNCH
@@ -480,7 +523,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
     const GRec *__restrict__ rec, const float *__restrict__ bg, const float *__restrict__ final_Ts,
     const uint32_t *__restrict__ n_contrib, const float *__restrict__ dL_dpix, const float *__restrict__ dL_dinvd,
     const uint32_t *__restrict__ tile_order, const uint32_t *__restrict__ goff, uint64_t *__restrict__ boundary,
-    float4 *__restrict__ out, ZeroRows zr) {
+    float4 *__restrict__ out, ZeroRows zr, const uint32_t *__restrict__ bwd_cnt, const uint32_t *__restrict__ bwd_cls) {
     // 9 KiB of LDS per wave: each compacted instance's mean and conic (scaled for gauss_p2 by the
     // lane that stages it, once per instance instead of by the whole wave), opacity, list position
     // << 4 | sub-block mask, Gaussian id (atomic mode) or record index, colour, and the unscaled
@@ -496,7 +539,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
 
     // Tiles run heaviest first (longest-processing-time order from the forward's per-tile work):
     // with ~2.7 tiles per wave slot, index order leaves a tail of a few heavy tiles.
-    const int tile = GSR_TILE_REVERSE ? (int)blockIdx.x : (int)tile_order[blockIdx.x];
+    const int tile = GSR_TILE_REVERSE ? (int)blockIdx.x
+                     : GSR_BWD_CLS    ? bwd_tile_of(blockIdx.x, bwd_cnt, bwd_cls, (int)gridDim.x)
+                                      : (int)tile_order[blockIdx.x];
     const int tx = tile % gx, ty = tile / gx;
     const int lane = threadIdx.x;
     const int px = tx * kTile + (lane & 15);
@@ -839,7 +884,7 @@ void launch_render_bwd(const Camera &cam, const GeomState &gs, const BinningStat
 #define GSR_BWD_LAUNCH(D, A)                                                                                       \
     hipLaunchKernelGGL((render_bwd_kernel<D, A>), dim3(T), dim3(kWave), 0, s, is.ranges, bs.point_list, cam.W, cam.H, \
                        cam.gx, gs.rec, bg, is.final_T, is.n_contrib, dL_dpix, dL_dinvdepth, is.tile_order, gs.offsets, \
-                       is.boundary, A ? sc.acc : sc.rec, z)
+                       is.boundary, A ? sc.acc : sc.rec, z, is.bwd_cnt, is.bwd_cls)
     if (dL_dinvdepth) {
         if (sc.atomic) GSR_BWD_LAUNCH(true, true);
         else GSR_BWD_LAUNCH(true, false);
