@@ -188,9 +188,13 @@ __global__ __launch_bounds__(kColThreads) void sb_colscan_kernel(SBGrid sg, uint
                                                                  const uint32_t *__restrict__ cnt_i,
                                                                  uint32_t *__restrict__ base_g,
                                                                  uint32_t *__restrict__ base_i,
-                                                                 uint32_t *__restrict__ done, FrameWords fw) {
+                                                                 uint32_t *__restrict__ done, FrameWords fw,
+                                                                 uint32_t *__restrict__ sb_order,
+                                                                 uint32_t *__restrict__ zero_classes) {
     __shared__ uint32_t wsum[kColThreads / 64];
     __shared__ uint32_t s_last;
+    __shared__ uint32_t s_ci[GSR_FWD_SB_ORDER ? kMaxSB : 1];  // last workgroup: SB instance totals
+    __shared__ uint32_t s_hist[GSR_FWD_SB_ORDER ? 256 : 1];
     const int s = blockIdx.x;
     uint32_t *row = cnt_g + (size_t)s * sg.ccols;
     const uint32_t *rowi = cnt_i + (size_t)s * sg.ccols;
@@ -224,6 +228,7 @@ __global__ __launch_bounds__(kColThreads) void sb_colscan_kernel(SBGrid sg, uint
         const uint32_t vg = k < nsb ? __hip_atomic_load(&base_g[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
         const uint32_t vi = k < nsb ? __hip_atomic_load(&base_i[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
         mg = max(mg, vg);
+        if (GSR_FWD_SB_ORDER && k < nsb) s_ci[k] = vi;
         uint32_t tg, ti;
         const uint32_t eg = block_exclusive_scan<kColThreads>(vg, wsum, tg);
         const uint32_t ei = block_exclusive_scan<kColThreads>(vi, wsum, ti);
@@ -237,6 +242,38 @@ __global__ __launch_bounds__(kColThreads) void sb_colscan_kernel(SBGrid sg, uint
     if (threadIdx.x == 0) {
         base_g[nsb] = cg;
         base_i[nsb] = ci;
+    }
+    if (zero_classes && threadIdx.x < kBwdClasses) zero_classes[threadIdx.x] = 0u;
+    if (GSR_FWD_SB_ORDER && sb_order) {
+        // the forward's launch order, heaviest first: SBs bucketed into 256 descending classes of
+        // their mean tile list length (16 instances per class), in order of the bucket scan
+        const int tshift = 2 * sg.shift;
+        const auto cls = [&](int k) {
+            const uint32_t c = (s_ci[k] >> tshift) >> 4;
+            return 255u - (c < 255u ? c : 255u);
+        };
+        s_hist[threadIdx.x] = 0u;  // kColThreads == 256
+        __syncthreads();
+        for (int k = threadIdx.x; k < nsb; k += kColThreads) atomicAdd(&s_hist[cls(k)], 1u);
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            const int l = threadIdx.x;
+            const uint32_t a = s_hist[4 * l], b = s_hist[4 * l + 1], c = s_hist[4 * l + 2], d = s_hist[4 * l + 3];
+            const uint32_t sum = a + b + c + d;
+            uint32_t incl = sum;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t v = (uint32_t)__shfl_up((int)incl, o, 64);
+                if (l >= o) incl += v;
+            }
+            const uint32_t ex = incl - sum;
+            s_hist[4 * l] = ex;
+            s_hist[4 * l + 1] = ex + a;
+            s_hist[4 * l + 2] = ex + a + b;
+            s_hist[4 * l + 3] = ex + a + b + c;
+        }
+        __syncthreads();
+        for (int k = threadIdx.x; k < nsb; k += kColThreads) sb_order[atomicAdd(&s_hist[cls(k)], 1u)] = (uint32_t)k;
     }
     if (fw.dev_K) {
         // local-sort frames: K (= the instance total) and the longest SB list for the kernels and
@@ -882,7 +919,7 @@ SBGrid sb_grid(int gx, int gy, int P) {
 bool sb_grid_supported(const SBGrid &g) { return g.nsb <= kMaxSB; }
 
 void launch_binning_count(int P, const Camera &cam, const GeomState &gs, bool index_order, const FrameWords &fw,
-                          hipStream_t s) {
+                          uint32_t *sb_order, uint32_t *zero_classes, hipStream_t s) {
     const SBGrid &sg = gs.sb;
     if (P == 0 || cam.gx * cam.gy == 0) return;
     const size_t l1 = sizeof(uint32_t) * 2 * (size_t)sg.nsb;
@@ -891,7 +928,7 @@ void launch_binning_count(int P, const Camera &cam, const GeomState &gs, bool in
     hipLaunchKernelGGL(sb_count_kernel, dim3(sg.nchunks), dim3(1024), l1, s, P, sg, rects, rects4, gs.sb_cnt_g,
                        gs.sb_cnt_i);
     hipLaunchKernelGGL(sb_colscan_kernel, dim3(sg.nsb), dim3(kColThreads), 0, s, sg, gs.sb_cnt_g, gs.sb_cnt_i,
-                       gs.sb_base_g, gs.sb_base_i, dsort_aux_word(gs), fw);
+                       gs.sb_base_g, gs.sb_base_i, dsort_aux_word(gs), fw, sb_order, zero_classes);
 }
 
 void launch_binning_scatter(int P, const Camera &cam, const GeomState &gs, const BinningState &bs, bool index_order,

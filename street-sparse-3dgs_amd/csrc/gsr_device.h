@@ -456,6 +456,12 @@ struct SBGrid {
 #define GSR_BWD_CLS 1
 #endif
 constexpr int kBwdClasses = 256;
+// GSR_FWD_SB_ORDER: the forward's launch order is by superblock (heaviest SB first, by its mean
+// tile-instance count; an SB's tiles consecutive), bucketed by the level-1 column scan's last
+// workgroup -- no tile_order launch between the tile binning and render_fwd
+#ifndef GSR_FWD_SB_ORDER
+#define GSR_FWD_SB_ORDER 0  // measured slower: render_fwd +11.5 us for the 10-us launch it saves (r03z)
+#endif
 constexpr int kBwdClassShift = 2;  // class = 255 - min(work >> 2, 255): heaviest first
 
 #ifndef GSR_RECT4

@@ -79,7 +79,10 @@ int sort_cap();  // the longest SB list the local sort holds
 int debug_trace(int64_t *out, int n, int reset);  // GSR_SB_TRACE builds: sb_sort_bin phase stamps
 // level-1 counts and SB bases; with fw.dev_K set (local sort) the column scan also stores K, the
 // longest SB list and the level-1 total (FrameWords)
+// sb_order != NULL: the SBs in forward launch order (GSR_FWD_SB_ORDER); zero_classes != NULL: the
+// backward class counters render_fwd fills are zeroed (GSR_BWD_CLS)
 void launch_binning_count(int P, const Camera &cam, const GeomState &gs, bool index_order, const FrameWords &fw,
+                          uint32_t *sb_order, uint32_t *zero_classes,
                           hipStream_t s);
 void launch_binning_scatter(int P, const Camera &cam, const GeomState &gs, const BinningState &bs, bool index_order,
                             hipStream_t s);
@@ -104,7 +107,8 @@ struct ZeroRows {
 
 // render.hip
 void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
-                       const float *bg, float *out_color, float *out_invdepth, hipStream_t s, bool need_bwd = true);
+                       const float *bg, float *out_color, float *out_invdepth, hipStream_t s, bool need_bwd = true,
+                       bool sb_order = false);
 void launch_render_bwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                        const int *radii, const float *bg, const float *dL_dpix, const float *dL_dinvdepth,
                        const BwdScratch &sc, hipStream_t s, const ZeroRows *zr = nullptr);

@@ -619,10 +619,15 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
     }
     const FrameWords fw_local{dsort_K_word(gs), dsort_maxsb_word(gs), g_pinned_dev};
     const FrameWords fw_none{nullptr, nullptr, nullptr};
+    // the forward's launch order by superblock and the backward class counters zeroed, both by the
+    // level-1 column scan (no tile_order launch); P == 0 frames run no binning: tile_order does both
+    const bool sb_order = GSR_FWD_SB_ORDER && P > 0;
+    uint32_t *const order_sb = sb_order ? is.tile_ids : nullptr;
+    uint32_t *const zero_cls = GSR_BWD_CLS && need_bwd && sb_order ? is.bwd_cnt : nullptr;
     if (local) {
         {
             StageTimer st(1, s);  // level-1 counts, SB bases, K
-            launch_binning_count(P, cam, gs, true, fw_local, s);
+            launch_binning_count(P, cam, gs, true, fw_local, order_sb, zero_cls, s);
             if (k_ready) (void)hipEventRecord(k_ready, s);
         }
         if ((rc = check("binning (counts)", debug, s))) return rc;
@@ -701,7 +706,7 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
         int r;
         {
             StageTimer st(2, s);
-            if (!local && !counted) launch_binning_count(P, cam, gs, false, fw_none, s);
+            if (!local && !counted) launch_binning_count(P, cam, gs, false, fw_none, order_sb, zero_cls, s);
             launch_binning_scatter(P, cam, gs, bs, local, s);
         }
         if ((r = check("binning (superblocks)", debug, s))) return r;
@@ -710,7 +715,7 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
             launch_binning_tiles(P, cam, gs, bs, is, local, dsort_maxsb_word(gs), s);
         }
         if ((r = check("binning (tiles)", debug, s))) return r;
-        {
+        if (!sb_order) {
             StageTimer st(4, s);
             // forward order: by list length (and the backward's class counters zeroed)
             launch_tile_order(nullptr, is.ranges, T, 4, is.tile_ids, s, bs.kdev, bs.cap,
@@ -724,7 +729,7 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
         }
         {
             StageTimer st(5, s);
-            launch_render_fwd(cam, gs, bs, is, background, out_color, out_invdepth, s, need_bwd);
+            launch_render_fwd(cam, gs, bs, is, background, out_color, out_invdepth, s, need_bwd, sb_order);
         }
         if (need_bwd && !GSR_BWD_CLS) {
             StageTimer st(9, s);  // backward launch order, from the forward's per-tile work

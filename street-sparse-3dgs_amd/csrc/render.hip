@@ -171,7 +171,7 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kerne
     float *__restrict__ out_invd, float *__restrict__ final_T, uint32_t *__restrict__ n_contrib,
     uint32_t *__restrict__ tile_work, const uint32_t *__restrict__ fwd_order, const uint32_t *__restrict__ kdev,
     uint32_t cap, const uint32_t *__restrict__ sort_err, float4 *__restrict__ acc, uint32_t acc_n4,
-    uint32_t *__restrict__ bwd_cnt, uint32_t *__restrict__ bwd_cls) {
+    uint32_t *__restrict__ bwd_cnt, uint32_t *__restrict__ bwd_cls, int ntiles, int gy, int sb_nsbx, int sb_shift) {
     constexpr int kWaves = kPixPerLane / kSub;
     if (kdev && *kdev > cap) return;  // the point-list capacity is short: the host re-runs at K
     {
@@ -192,8 +192,21 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kerne
     __shared__ float4 s_c[kWaves][kWave];  // r, g, b, 1 / depth
     __shared__ uint32_t s_work[kWaves];
 
-    const int tile = (int)fwd_order[blockIdx.x];
-    const int tx = tile % gx, ty = tile / gx;
+    int tile, tx, ty;
+    if (sb_shift >= 0) {
+        // superblock launch order (GSR_FWD_SB_ORDER): fwd_order lists the SBs, a workgroup per SB
+        // tile slot; slots past the grid's edge have no tile
+        const uint32_t per = 1u << (2 * sb_shift), b = blockIdx.x;
+        const uint32_t k = fwd_order[b >> (2 * sb_shift)], t = b & (per - 1u);
+        tx = (int)(k % (uint32_t)sb_nsbx) * (1 << sb_shift) + (int)(t & ((1u << sb_shift) - 1u));
+        ty = (int)(k / (uint32_t)sb_nsbx) * (1 << sb_shift) + (int)(t >> sb_shift);
+        if (tx >= gx || ty >= gy) return;
+        tile = ty * gx + tx;
+    } else {
+        tile = (int)fwd_order[blockIdx.x];
+        tx = tile % gx;
+        ty = tile / gx;
+    }
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int px = tx * kTile + (lane & 15);
     const int sy = ty * kTile + 4 * kSub * w;  // the wave's first pixel row
@@ -365,7 +378,7 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kerne
             const uint32_t k = mx >> kBwdClassShift;
             const uint32_t c = (uint32_t)(kBwdClasses - 1) - (k < (uint32_t)(kBwdClasses - 1) ? k : (uint32_t)(kBwdClasses - 1));
             const uint32_t r = atomicAdd(&bwd_cnt[c], 1u);
-            bwd_cls[(size_t)c * gridDim.x + r] = (uint32_t)tile;
+            bwd_cls[(size_t)c * ntiles + r] = (uint32_t)tile;
         }
     };
     if (kWaves == 1) {
@@ -454,15 +467,19 @@ void launch_tile_order(const uint32_t *work, const uint2 *ranges, int T, int shi
 }
 
 void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
-                       const float *bg, float *out_color, float *out_invdepth, hipStream_t s, bool need_bwd) {
+                       const float *bg, float *out_color, float *out_invdepth, hipStream_t s, bool need_bwd,
+                       bool sb_order) {
     const int T = cam.gx * cam.gy;
     if (T == 0) return;
+    const SBGrid &sg = gs.sb;
+    const int grid = sb_order ? sg.nsb << (2 * sg.shift) : T;
     // launch order: is.tile_ids (rasterizer.hip, by list length)
 #define GSR_FWD_LAUNCH(K, NT)                                                                                       \
-    hipLaunchKernelGGL(K, dim3(T), dim3(NT), 0, s, is.ranges, bs.point_list, cam.W, cam.H, cam.gx, gs.rec, bg,      \
+    hipLaunchKernelGGL(K, dim3(grid), dim3(NT), 0, s, is.ranges, bs.point_list, cam.W, cam.H, cam.gx, gs.rec, bg,   \
                        out_color, out_invdepth, is.final_T, is.n_contrib, is.tile_work, is.tile_ids, bs.kdev, bs.cap, \
                        bs.kdev ? dsort_err_word(gs) : nullptr, gs.acc, (uint32_t)(4 * (size_t)gs.nacc),              \
-                       GSR_BWD_CLS && need_bwd ? is.bwd_cnt : nullptr, is.bwd_cls)
+                       GSR_BWD_CLS && need_bwd ? is.bwd_cnt : nullptr, is.bwd_cls, T, cam.gy, sg.nsbx,        \
+                       sb_order ? sg.shift : -1)
     static_assert(GSR_FWD_SUB == 1 || GSR_FWD_SUB == 2 || GSR_FWD_SUB == 4, "GSR_FWD_SUB: 1, 2 or 4");
     GSR_FWD_LAUNCH(render_fwd_kernel<GSR_FWD_SUB>, kWave * (kPixPerLane / GSR_FWD_SUB));
 #undef GSR_FWD_LAUNCH
