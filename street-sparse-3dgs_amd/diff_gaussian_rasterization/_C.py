@@ -25,6 +25,7 @@ torch caching allocator and are freed with the autograd graph, as upstream's are
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import threading
 
@@ -37,23 +38,48 @@ _FWD_NO_BACKWARD = 1  # GSR_FWD_NO_BACKWARD (include/gsr.h)
 
 
 def _ptr(t):
+    """A tensor's device address as a plain int (the argtypes are c_void_p: ctypes converts it
+    without a c_void_p object per argument), or None (NULL) for an absent or empty tensor."""
     if t is None or t.numel() == 0:
         return None
-    return ctypes.c_void_p(t.data_ptr())
+    return t.data_ptr()
 
 
 def _dev_f32(t, name, device):
     if t is None or t.numel() == 0:
         return None
-    if t.device != device:
+    if t.get_device() != device.index:
         raise RuntimeError(f"{name} must be on {device} (got {t.device})")
     if t.dtype != torch.float32:
         raise RuntimeError(f"{name} must be float32 (got {t.dtype})")
-    return t.contiguous()
+    return t if t.is_contiguous() else t.contiguous()
+
+
+def _saved(t):
+    """A tensor the forward already validated (the autograd Function saved it): contiguous, or
+    None when absent / empty."""
+    if t is None or t.numel() == 0:
+        return None
+    return t if t.is_contiguous() else t.contiguous()
+
+
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 
 
 def _stream(device):
-    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    """The current HIP stream of `device` (the raw handle, without building a torch Stream object
+    per call when torch exposes it)."""
+    if _RAW_STREAM is not None:
+        return _RAW_STREAM(device.index if device.index is not None else torch.cuda.current_device())
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _on(device):
+    """torch.cuda.device(device), or nothing when it is already the current device (the library
+    works on the current HIP device; the usual single-device caller pays no device switch)."""
+    if device.index is None or device.index == torch.cuda.current_device():
+        return contextlib.nullcontext()
+    return torch.cuda.device(device)
 
 
 class _Resizer:
@@ -143,7 +169,7 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     radii = torch.empty(n_render if n_render > 0 else P, dtype=torch.int32, device=dev)
     res = _Resizer(dev)
     K = ctypes.c_int64(0)
-    with torch.cuda.device(dev):
+    with _on(dev):
         rc = _L.gsr_rasterize_forward_ex(
             res.fn("geom"), res.fn("binning"), res.fn("image"), None, P, int(degree), M, _ptr(bg_c), W, H,
             _ptr(means3D_c), _ptr(sh_c), _ptr(colors_c), _ptr(opac_c), _ptr(scales_c), float(scale_modifier),
@@ -172,14 +198,22 @@ def _cut_args(render_indices, parent_indices, interpolation_weights, num_node_ki
         interpolation_weights.to(device=dev, dtype=torch.float32).contiguous(), kids
 
 
+_GSR_DIST = []
+
+
 def _leaf_grad(t, shape, dev):
     """Output for the gradient of input `t`: a view of the capturing gsr_dist.GradBucket when
     one owns t (data-parallel training: the all-reduce then needs no cat / copy), else new."""
-    try:
-        import gsr_dist
-    except ImportError:  # the package used without the repo's multi-GPU helpers
+    if not _GSR_DIST:
+        try:
+            import gsr_dist
+            _GSR_DIST.append(gsr_dist)
+        except ImportError:  # the package used without the repo's multi-GPU helpers
+            _GSR_DIST.append(None)
+    gd = _GSR_DIST[0]
+    if gd is None:
         return torch.empty(shape, dtype=torch.float32, device=dev)
-    return gsr_dist.grad_out(t.data_ptr() if t is not None else None, shape, dev)
+    return gd.grad_out(t.data_ptr() if t is not None else None, shape, dev)
 
 
 _ZEROS = {}
@@ -197,17 +231,24 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
                                  cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color,
                                  dL_dout_invdepth, sh, degree, campos, geomBuffer, R, binningBuffer, imageBuffer,
                                  render_indices=None, parent_indices=None, interpolation_weights=None,
-                                 num_node_kids=None, debug=False):
+                                 num_node_kids=None, debug=False, validated=False):
+    """validated=True (an extension; the autograd Function passes it): the forward's inputs were
+    checked by rasterize_gaussians, so only the incoming gradients are checked again."""
     _require_gpu(means3D)
     dev = means3D.device
     P = means3D.size(0)
     H, W = dL_dout_color.size(1), dL_dout_color.size(2)
     M = sh.size(1) if (sh is not None and sh.numel() != 0) else 0
     f = lambda t, n: _dev_f32(t, n, dev)
-    means3D_c, sh_c, colors_c = f(means3D, "means3D"), f(sh, "sh"), f(colors, "colors_precomp")
-    scales_c, rots_c, cov_c = f(scales, "scales"), f(rotations, "rotations"), f(cov3D_precomp, "cov3D_precomp")
-    view_c, proj_c, campos_c, bg_c = f(viewmatrix, "viewmatrix"), f(projmatrix, "projmatrix"), f(campos, "campos"), \
-        f(background, "bg")
+    if validated:  # the autograd Function's own forward checked these tensors
+        means3D_c, sh_c, colors_c = _saved(means3D), _saved(sh), _saved(colors)
+        scales_c, rots_c, cov_c = _saved(scales), _saved(rotations), _saved(cov3D_precomp)
+        view_c, proj_c, campos_c, bg_c = _saved(viewmatrix), _saved(projmatrix), _saved(campos), _saved(background)
+    else:
+        means3D_c, sh_c, colors_c = f(means3D, "means3D"), f(sh, "sh"), f(colors, "colors_precomp")
+        scales_c, rots_c, cov_c = f(scales, "scales"), f(rotations, "rotations"), f(cov3D_precomp, "cov3D_precomp")
+        view_c, proj_c, campos_c, bg_c = f(viewmatrix, "viewmatrix"), f(projmatrix, "projmatrix"), f(campos, "campos"), \
+            f(background, "bg")
     dpix = f(dL_dout_color, "dL_dout_color")
     dinv = f(dL_dout_invdepth, "dL_dout_invdepth") if dL_dout_invdepth is not None else None
     radii_c = radii.contiguous()
@@ -228,7 +269,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     else:
         dL_dscales, dL_drotations = z(P, 3), z(P, 4)
     res = _Resizer(dev)
-    with torch.cuda.device(dev):
+    with _on(dev):
         rc = _L.gsr_rasterize_backward(
             res.fn("scratch"), None, P, int(degree), M, int(R), _ptr(bg_c), W, H, _ptr(means3D_c), _ptr(sh_c),
             _ptr(colors_c), _ptr(scales_c), float(scale_modifier), _ptr(rots_c), _ptr(cov_c), _ptr(view_c),

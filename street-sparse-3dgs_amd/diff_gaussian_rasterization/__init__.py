@@ -110,14 +110,14 @@ class _RasterizeGaussians(torch.autograd.Function):
         if rs.debug:
             saved = _snapshot(args)
             try:
-                grads = _C.rasterize_gaussians_backward(*args)
+                grads = _C.rasterize_gaussians_backward(*args, validated=True)
             except Exception:
                 _dump(saved, "snapshot_bw.dump")
                 print("\n[diff_gaussian_rasterization] backward failed in debug mode; its inputs are in "
                       "snapshot_bw.dump (replay with _C.rasterize_gaussians_backward(*args))")
                 raise
         else:
-            grads = _C.rasterize_gaussians_backward(*args)
+            grads = _C.rasterize_gaussians_backward(*args, validated=True)
         (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_sh, grad_scales,
          grad_rotations) = grads
 
@@ -149,6 +149,9 @@ class GaussianRasterizationSettings(NamedTuple):
     num_node_kids: torch.Tensor = None
 
 
+_EMPTY = torch.empty(0)  # the stand-in for an absent input (upstream builds torch.Tensor([]) per call)
+
+
 class GaussianRasterizer(nn.Module):
     def __init__(self, raster_settings):
         super().__init__()
@@ -169,7 +172,7 @@ class GaussianRasterizer(nn.Module):
         if ((scales is None or rotations is None) and cov3D_precomp is None) or \
                 ((scales is not None or rotations is not None) and cov3D_precomp is not None):
             raise Exception('Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!')
-        empty = torch.Tensor([])
+        empty = _EMPTY
         if shs is None:
             shs = empty
         if colors_precomp is None:
