@@ -16,6 +16,7 @@ splat of SURVEY.md 8(d) on config 1).
 from __future__ import annotations
 
 import argparse
+import contextlib
 import glob
 import json
 import os
@@ -197,11 +198,12 @@ def train_step_ms(P, W, H, steps, warmup, dev, street=True, reference=False, see
     for _ in range(warmup):
         ts.step()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        ts.step()
-    torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) / steps * 1e3
+    with quiet_gc():
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            ts.step()
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / steps * 1e3
     del ts
     torch.cuda.empty_cache()
     return ms
@@ -456,6 +458,22 @@ def fwd_bwd_step(raster, inp, gcol, ginv):
     return step
 
 
+@contextlib.contextmanager
+def quiet_gc():
+    """Python's cyclic collector settled before a timed region: one full collection, then every
+    surviving object frozen (gc.freeze), so a generation-2 pass over the interpreter's ~10^5
+    long-lived objects (torch's modules, the synthetic scene's builders) cannot land inside the
+    timed steps -- a few-ms host stall that showed up as a 10% low sample now and then.  Collection
+    stays enabled; the objects the steps themselves create are collected as usual."""
+    import gc
+    gc.collect()
+    gc.freeze()
+    try:
+        yield
+    finally:
+        gc.unfreeze()
+
+
 def timed(step, steps, warmup, ranks):
     """W untimed steps, then exactly `steps` steps bracketed by barrier + synchronize on both sides;
     the MAX over ranks of the elapsed seconds."""
@@ -465,13 +483,15 @@ def timed(step, steps, warmup, ranks):
     torch.cuda.synchronize()
     ranks.barrier()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
-    torch.cuda.synchronize()
-    ranks.barrier()
-    torch.cuda.synchronize()
-    return ranks.max(time.perf_counter() - t0)
+    with quiet_gc():
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        ranks.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+    return ranks.max(el)
 
 
 def stage_profile(step, n):
