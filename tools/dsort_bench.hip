@@ -4,7 +4,7 @@
 //         -I street-sparse-3dgs_amd/csrc -I include tools/dsort_bench.hip -o tools/dsort_bench
 //   tools/dsort_bench [P] [iters]
 // Synthetic keys: view depths z ~ U[2, 20] as float bits, 2% culled (0xFFFFFFFF); tile counts
-// 1..32.  Checks the order against std::stable_sort, the record offsets and K, then prints the
+// 1..32; 8-B tile rects (rect4 unset: pass 3 gathers them, no rect carry).  Checks the order against std::stable_sort, the record offsets and K, then prints the
 // per-kernel HIP-event times and the per-workgroup phase stamps (median / max over workgroups,
 // relative to the kernel's first workgroup start).
 #include <algorithm>
@@ -83,16 +83,20 @@ int main(int argc, char **argv) {
                            (uint32_t *)nullptr);
         CK(hipEventRecord(ev[1], s));
         hipLaunchKernelGGL(dsort_pass_kernel<0>, dim3(nb), dim3(kDsThreads), 0, s, P, nb, gs.dkey, gs.dkey_sorted,
-                           (const uint32_t *)nullptr, gs.ids, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect, (uint32_t *)nullptr);
+                           (const uint32_t *)nullptr, gs.ids, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, (const uint32_t *)nullptr, gs.drect,
+                           (const uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr);
         CK(hipEventRecord(ev[2], s));
         hipLaunchKernelGGL(dsort_pass_kernel<1>, dim3(nb), dim3(kDsThreads), 0, s, P, nb, gs.dkey_sorted, gs.dkey,
-                           gs.ids, gs.order, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect, (uint32_t *)nullptr);
+                           gs.ids, gs.order, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, (const uint32_t *)nullptr, gs.drect,
+                           (const uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr);
         CK(hipEventRecord(ev[3], s));
         hipLaunchKernelGGL(dsort_pass_kernel<2>, dim3(nb), dim3(kDsThreads), 0, s, P, nb, gs.dkey, gs.dkey_sorted,
-                           gs.order, gs.ids, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect, (uint32_t *)nullptr);
+                           gs.order, gs.ids, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, (const uint32_t *)nullptr, gs.drect,
+                           (const uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr);
         CK(hipEventRecord(ev[4], s));
         hipLaunchKernelGGL(dsort_pass_kernel<3>, dim3(nb), dim3(kDsThreads), 0, s, P, nb, gs.dkey_sorted,
-                           (uint32_t *)nullptr, gs.ids, gs.order, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, gs.drect, (uint32_t *)nullptr);
+                           (uint32_t *)nullptr, gs.ids, gs.order, gs.ctrl, gs.offsets, gs.tiles, gs.rect8, (const uint32_t *)nullptr, gs.drect,
+                           (const uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr);
         CK(hipEventRecord(ev[5], s));
         CK(hipStreamSynchronize(s));
         if (it >= 2)
