@@ -137,6 +137,22 @@ int gsr_depth_l1_forward(const float *invdepth, const float *mono_invdepth, cons
 int gsr_depth_l1_backward(const float *invdepth, const float *mono_invdepth, const float *mask, int64_t n,
                           float weight, const float *dL_dloss, float *dL_dinvdepth, void *stream);
 
+/* The loss of a depth-only view (Street-sparse's additional depth maps, train_single.py:145-156):
+ *   pure = mean(|(invdepth - mono_invdepth) * mask|)           (Ll1depth_pure; mask NULL = ones)
+ *   dens = mean(clamp(mono_invdepth - invdepth, min=0))         (Ll1depth_dens, unmasked)
+ *   loss = weight * (dens_weight * dens + (1 - dens_weight) * pure)
+ * weight = depth_l1_weight(iteration), dens_weight = additional_depth_maps_weight (0.9 by
+ * default, arguments/__init__.py:71).  _forward writes out3 = (pure, dens, loss) (the means in
+ * fp64, the combination in torch's fp32 op order); _backward writes dL/dinvdepth for the scalar
+ * dL/dloss (device pointer), torch's autograd chain through the reference's expression bit for
+ * bit.  Scratch of gsr_depth_only_scratch_bytes(n); 16-byte aligned arrays. */
+size_t gsr_depth_only_scratch_bytes(int64_t n);
+int gsr_depth_only_loss_forward(const float *invdepth, const float *mono_invdepth, const float *mask, int64_t n,
+                                float weight, double dens_weight, void *scratch, float *out3, void *stream);
+int gsr_depth_only_loss_backward(const float *invdepth, const float *mono_invdepth, const float *mask, int64_t n,
+                                 float weight, double dens_weight, const float *dL_dloss, float *dL_dinvdepth,
+                                 void *stream);
+
 /* ---- Native train-step executor ------------------------------------------------------------
  * gsr_train_step runs one whole Street-sparse iteration (train_single.py:65-247: render with
  * the exposure of the view, photometric loss + masked inverse-depth L1, backward, densification
@@ -184,9 +200,22 @@ typedef struct {
     int64_t scaffold_rows; /* the first rows: left alone by the scale shrink */
     float max_scale;       /* shrink rows whose largest scale exceeds this (extent * 0.02) */
     /* out (device, 6 floats): L1, SSIM, photometric loss, (depth term only) the unweighted and
-     * weighted depth L1, then the step's loss ([2] + [4], or [2]) */
+     * weighted depth L1, then the step's loss ([2] + [4], or [2]); depth-only view: Ll1depth_dens,
+     * 0, 0, Ll1depth_pure, Ll1depth, loss */
     float *losses;
     void *stream;
+    /* A depth-only view (train_single.py:69-72,145-161,203-214; ABI 3): no target image; the loss
+     * is gsr_depth_only_loss's (depth_weight > 0 and mono_invdepth required), the colour gradient
+     * is zero, the exposure gradient is zeroed and no exposure Adam step runs (the caller does not
+     * advance the exposure optimizer's step count).  gt may be NULL. */
+    int depth_only;
+    double depth_dens_weight; /* additional_depth_maps_weight */
+    /* Nonzero: everything up to the optimizers only (forward, losses, backward, densification
+     * statistics, exposure step) -- no Gaussian Adam step and no scale shrink.  An iteration of
+     * train_single.py that densifies / resets the opacities replaces the parameters between the
+     * statistics and the optimizers and then takes no Gaussian Adam step (:190-201, :217, :225);
+     * the caller runs those and the shrink itself (gsr_shrink_scales).  ABI 3. */
+    int skip_gaussian_step;
 } gsr_train_step_args;
 
 /* *num_rendered receives the frame's K. */

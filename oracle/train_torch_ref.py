@@ -199,6 +199,24 @@ def densify_and_prune(g, opt, max_grad, min_opacity, extent, percent_dense, firs
     g.max_radii2D = torch.zeros((g._xyz.shape[0]), device=dev)
 
 
+def reset_opacity(g, opt, skybox):
+    """scene/gaussian_model.py:528-532 + replace_tensor_to_optimizer (:546-559) on a split-layout set."""
+    op = g.get_opacity
+    x = torch.min(op[skybox:], torch.ones_like(op[skybox:]) * 0.01)
+    new = torch.cat((g._opacity[:skybox], torch.log(x / (1 - x))), 0)  # inverse_sigmoid
+    for group in opt.param_groups:
+        if group["name"] == "opacity":
+            st = opt.state.get(group["params"][0], None)
+            if st is not None:
+                st["exp_avg"] = torch.zeros_like(new)
+                st["exp_avg_sq"] = torch.zeros_like(new)
+                del opt.state[group["params"][0]]
+            group["params"][0] = torch.nn.Parameter(new.detach().requires_grad_(True))
+            if st is not None:
+                opt.state[group["params"][0]] = st
+            g._opacity = group["params"][0]
+
+
 # ---- one train_single.py iteration in the reference's formulation ------------------------------
 def _reference_step_cls():
     from gs_train.harness import LR, TrainStep
@@ -235,6 +253,20 @@ def _reference_step_cls():
             m = mask if mask is not None else torch.ones_like(invd)
             return w * torch.abs((invd - mono) * m).mean()
 
+        def _depth_only_loss(self, invd, mono, mask, w):
+            # train_single.py:152-156
+            m = mask if mask is not None else torch.ones_like(invd)
+            pure = torch.abs((invd - mono) * m).mean()
+            dens = (mono - invd).clamp(min=0).mean()
+            return (w * (self.dens_weight * dens + (1 - self.dens_weight) * pure)).clone()
+
+        def _zero_feature_grads(self):
+            # train_single.py:203-209
+            g = self.g
+            for p in (g._features_dc, g._features_rest, g._exposure):
+                if p.grad is not None:
+                    p.grad.zero_()
+
         def _backward(self, loss):
             loss.backward()
 
@@ -257,6 +289,17 @@ def _reference_step_cls():
             bad = sc.max(dim=1).values > self.extent * 0.02
             bad[:self.scaffold] = False  # train_single.py:239-240
             g._scaling[bad] = torch.log(sc[bad] * 0.8)
+
+        def densify_and_prune(self, max_grad, min_opacity, percent_dense, normals=None):
+            if normals is not None:
+                raise NotImplementedError("the reference formulation draws its split samples itself")
+            P0 = self.g._xyz.shape[0]
+            densify_and_prune(self.g, self.optimizer, max_grad, min_opacity, self.extent, percent_dense,
+                              first_row=self.scaffold)
+            return dict(total=self.g._xyz.shape[0], P0=P0)
+
+        def reset_opacity(self):
+            reset_opacity(self.g, self.optimizer, self.skybox)
 
     return ReferenceTrainStep
 

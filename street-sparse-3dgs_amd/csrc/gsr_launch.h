@@ -172,6 +172,10 @@ int step_loss_forward(const float *img, const float *gt, int H, int W, double la
                       float *gmap, const float *invd, const float *mono, const float *mask, float depth_w,
                       void *depth_scratch, float *d_invd, float *losses, int *flag, hipStream_t s,
                       const float *one = nullptr, const float *alpha = nullptr, bool *gmap_is_photo = nullptr);
+// the depth-only view's loss (gsr_depth_only_loss) with its gradient for an upstream of 1 in d_invd;
+// losses = (dens, 0, 0, pure, loss, loss); *flag = 0
+int step_depth_only_forward(const float *invd, const float *mono, const float *mask, int64_t n, float w, double a,
+                            void *depth_scratch, float *d_invd, float *losses, int *flag, hipStream_t s);
 int launch_exposure_forward(const float *color, const float *E, int64_t npix, float *out, const float *alpha,
                             hipStream_t s);
 // photometric gradient (x alpha) through the exposure into d_color, the exposure gradient and the

@@ -868,7 +868,7 @@ __global__ __launch_bounds__(kAdamThreads) void sparse_adam_rows_kernel(AdamArgs
     const bool relv = row < P && (dense || rel[row] != 0.f);
     const uint64_t mask = __ballot(relv);
     // dense fallback over sparse rows: rows whose gradient reads as zero
-    const bool zrow = dense && dr.live3 && row < P && (row < dr.skybox || dr.live3[3 * row + 2] == 0.f);
+    const bool zrow = dense && row < P && (row < dr.skybox || (dr.live3 && dr.live3[3 * row + 2] == 0.f));
     const uint64_t zmask = __ballot(zrow);
     const int w = G.width;
     const int64_t rs = G.row_stride;
@@ -1351,6 +1351,137 @@ __global__ __launch_bounds__(256) void depth_l1_bwd_kernel(const float *__restri
     dinvd[i] = __fmul_rn(__fmul_rn(g, sg), m);
 }
 
+// ---- the depth-only view's loss (train_single.py:145-156, Street-sparse's additional depth maps) --
+//   pure = mean |(invd - mono) * mask|,  dens = mean clamp(mono - invd, min=0)
+//   loss = w * (a * dens + (1 - a) * pure)          (a = additional_depth_maps_weight)
+// Both sums in one pass (fp32 per thread, fp64 across threads and blocks).  The gradient follows
+// torch's autograd through that expression term by term: g = gout * w; the clamp branch
+// -(g * a) * (1/N) where mono - invd >= 0 (clamp passes the gradient at the bound); the L1 branch
+// ((g * (1 - a)) * (1/N)) * sgn(d) * mask; their sum (the two uses of invDepth).
+struct DepthOnlyW {
+    float g_dens, g_pure;  // gout * w * a * (1/N), gout * w * (1 - a) * (1/N), in torch's order
+};
+
+__device__ __forceinline__ float depth_only_grad(float x, float y, float m, const DepthOnlyW &q) {
+    const float d = depth_term(x, y, m);
+    const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+    const float t2 = __fmul_rn(__fmul_rn(q.g_pure, sg), m);
+    const float t1 = (y - x) >= 0.f ? -q.g_dens : 0.f;
+    return __fadd_rn(t1, t2);
+}
+
+// host and device (the native step forms it on the host for an upstream of 1); products only, so
+// -ffp-contract=off leaves each one a rounded fp32 multiply
+__host__ __device__ __forceinline__ DepthOnlyW depth_only_w(float gout, float w, float a, float oma,
+                                                            float inv_count) {
+    const float g = gout * w;
+    return DepthOnlyW{(g * a) * inv_count, (g * oma) * inv_count};
+}
+
+// kGrad: dL/dinvdepth for an upstream of 1 in the same pass (the native step)
+template <bool kGrad>
+__global__ __launch_bounds__(kDepthThreads) void depth_only_fwd_kernel(const float *__restrict__ invd,
+                                                                      const float *__restrict__ mono,
+                                                                      const float *__restrict__ mask, int64_t n,
+                                                                      double2 *__restrict__ partials, DepthOnlyW q,
+                                                                      float *__restrict__ dinvd) {
+    __shared__ double2 red[kDepthThreads / 64];
+    const int64_t b0 = (int64_t)blockIdx.x * kDepthPerBlock;
+    float acc_p = 0.f, acc_d = 0.f;
+    const auto one = [&](float x, float y, float m, float &g) {
+        acc_p += fabsf(depth_term(x, y, m));
+        acc_d += fmaxf(y - x, 0.f);
+        if (kGrad) g = depth_only_grad(x, y, m, q);
+    };
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int64_t i = b0 + 4 * ((int64_t)k * kDepthThreads + threadIdx.x);
+        if (i + 3 < n) {
+            const float4 x = *reinterpret_cast<const float4 *>(invd + i);
+            const float4 y = *reinterpret_cast<const float4 *>(mono + i);
+            const float4 m = mask ? *reinterpret_cast<const float4 *>(mask + i) : make_float4(1.f, 1.f, 1.f, 1.f);
+            float4 g;
+            one(x.x, y.x, m.x, g.x);
+            one(x.y, y.y, m.y, g.y);
+            one(x.z, y.z, m.z, g.z);
+            one(x.w, y.w, m.w, g.w);
+            if (kGrad) *reinterpret_cast<float4 *>(dinvd + i) = g;
+        } else {
+            for (int64_t j = i; j < n && j < i + 4; j++) {
+                float g;
+                one(invd[j], mono[j], mask ? mask[j] : 1.f, g);
+                if (kGrad) dinvd[j] = g;
+            }
+        }
+    }
+    double vp = acc_p, vd = acc_d;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        vp += __shfl_xor(vp, o, 64);
+        vd += __shfl_xor(vd, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = make_double2(vp, vd);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double2 t = make_double2(0.0, 0.0);
+        for (int k = 0; k < kDepthThreads / 64; k++) {
+            t.x += red[k].x;
+            t.y += red[k].y;
+        }
+        partials[blockIdx.x] = t;
+    }
+}
+
+// out3 = (pure, dens, loss); step != 0 (the native step's epilogue): out6 = (dens, 0, 0, pure, loss,
+// loss) and the sparse Adam's relevance flag cleared
+__global__ __launch_bounds__(1024) void depth_only_finalize_kernel(const double2 *__restrict__ partials, int nb,
+                                                                   double inv_n, float w, float a, float oma,
+                                                                   float *__restrict__ out, int *__restrict__ flag) {
+    __shared__ double2 red[1024];
+    double2 v = make_double2(0.0, 0.0);
+    for (int i = threadIdx.x; i < nb; i += 1024) {
+        v.x += partials[i].x;
+        v.y += partials[i].y;
+    }
+    red[threadIdx.x] = v;
+    __syncthreads();
+    for (int k = 512; k > 0; k >>= 1) {
+        if ((int)threadIdx.x < k) {
+            red[threadIdx.x].x += red[threadIdx.x + k].x;
+            red[threadIdx.x].y += red[threadIdx.x + k].y;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const float pure = (float)(red[0].x * inv_n), dens = (float)(red[0].y * inv_n);
+        // w * (a * dens + (1 - a) * pure) in torch's fp32 op order
+        const float loss = __fmul_rn(__fadd_rn(__fmul_rn(dens, a), __fmul_rn(pure, oma)), w);
+        if (flag) {
+            out[0] = dens;
+            out[1] = 0.f;
+            out[2] = 0.f;
+            out[3] = pure;
+            out[4] = loss;
+            out[5] = loss;
+            *flag = 0;
+        } else {
+            out[0] = pure;
+            out[1] = dens;
+            out[2] = loss;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void depth_only_bwd_kernel(const float *__restrict__ invd,
+                                                             const float *__restrict__ mono,
+                                                             const float *__restrict__ mask, int64_t n,
+                                                             const float *__restrict__ gout, float w, float a,
+                                                             float oma, float inv_count, float *__restrict__ dinvd) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    dinvd[i] = depth_only_grad(invd[i], mono[i], mask ? mask[i] : 1.f, depth_only_w(gout[0], w, a, oma, inv_count));
+}
+
 bool g_lds_attr = false;
 
 void set_lds_attr() {
@@ -1464,6 +1595,26 @@ int step_loss_forward(const float *img, const float *gt, int H, int W, double la
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_last_error(std::string("step loss forward: ") + hipGetErrorString(e));
+        return GSR_ERR_DEVICE;
+    }
+    return GSR_OK;
+}
+
+int step_depth_only_forward(const float *invd, const float *mono, const float *mask, int64_t n, float w, double a,
+                            void *depth_scratch, float *d_invd, float *losses, int *flag, hipStream_t s) {
+    const int nb = (int)std::max<int64_t>(1, (n + kDepthPerBlock - 1) / kDepthPerBlock);
+    double2 *part = static_cast<double2 *>(depth_scratch);
+    const float af = (float)a, omaf = (float)(1.0 - a);
+    if (n > 0)
+        hipLaunchKernelGGL(depth_only_fwd_kernel<true>, dim3(nb), dim3(kDepthThreads), 0, s, invd, mono, mask, n, part,
+                           depth_only_w(1.f, w, af, omaf, 1.0f / (float)n), d_invd);
+    else if (hipMemsetAsync(part, 0, sizeof(double2), s) != hipSuccess)
+        return GSR_ERR_DEVICE;
+    hipLaunchKernelGGL(depth_only_finalize_kernel, dim3(1), dim3(1024), 0, s, part, nb, n > 0 ? 1.0 / (double)n : 0.0,
+                       w, af, omaf, losses, flag);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_last_error(std::string("step depth-only loss: ") + hipGetErrorString(e));
         return GSR_ERR_DEVICE;
     }
     return GSR_OK;
@@ -1855,6 +2006,61 @@ int gsr_depth_l1_backward(const float *invdepth, const float *mono_invdepth, con
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_last_error(std::string("gsr_depth_l1_backward: ") + hipGetErrorString(e));
+        return GSR_ERR_DEVICE;
+    }
+    return GSR_OK;
+}
+
+size_t gsr_depth_only_scratch_bytes(int64_t n) {
+    return sizeof(double2) * (size_t)std::max<int64_t>(1, (n + kDepthPerBlock - 1) / kDepthPerBlock);
+}
+
+int gsr_depth_only_loss_forward(const float *invdepth, const float *mono_invdepth, const float *mask, int64_t n,
+                                float weight, double dens_weight, void *scratch, float *out3, void *stream) {
+    if (n < 0 || (n > 0 && (!invdepth || !mono_invdepth)) || !scratch || !out3 ||
+        !(dens_weight >= 0.0 && dens_weight <= 1.0)) {
+        set_last_error("gsr_depth_only_loss_forward: bad size, weight or NULL pointer");
+        return GSR_ERR_INVALID_ARGUMENT;
+    }
+    if ((reinterpret_cast<uintptr_t>(invdepth) | reinterpret_cast<uintptr_t>(mono_invdepth) |
+         reinterpret_cast<uintptr_t>(mask)) % 16 != 0) {
+        set_last_error("gsr_depth_only_loss_forward: arrays must be 16-byte aligned");
+        return GSR_ERR_INVALID_ARGUMENT;
+    }
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int nb = (int)std::max<int64_t>(1, (n + kDepthPerBlock - 1) / kDepthPerBlock);
+    double2 *part = static_cast<double2 *>(scratch);
+    const float af = (float)dens_weight, omaf = (float)(1.0 - dens_weight);
+    if (n > 0)
+        hipLaunchKernelGGL(depth_only_fwd_kernel<false>, dim3(nb), dim3(kDepthThreads), 0, s, invdepth, mono_invdepth,
+                           mask, n, part, DepthOnlyW{0.f, 0.f}, nullptr);
+    else if (hipMemsetAsync(part, 0, sizeof(double2), s) != hipSuccess)
+        return GSR_ERR_DEVICE;
+    hipLaunchKernelGGL(depth_only_finalize_kernel, dim3(1), dim3(1024), 0, s, part, nb,
+                       n > 0 ? 1.0 / (double)n : 0.0, weight, af, omaf, out3, nullptr);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_last_error(std::string("gsr_depth_only_loss_forward: ") + hipGetErrorString(e));
+        return GSR_ERR_DEVICE;
+    }
+    return GSR_OK;
+}
+
+int gsr_depth_only_loss_backward(const float *invdepth, const float *mono_invdepth, const float *mask, int64_t n,
+                                 float weight, double dens_weight, const float *dL_dloss, float *dL_dinvdepth,
+                                 void *stream) {
+    if (n < 0 || (n > 0 && (!invdepth || !mono_invdepth || !dL_dloss || !dL_dinvdepth)) ||
+        !(dens_weight >= 0.0 && dens_weight <= 1.0)) {
+        set_last_error("gsr_depth_only_loss_backward: bad size, weight or NULL pointer");
+        return GSR_ERR_INVALID_ARGUMENT;
+    }
+    if (n == 0) return GSR_OK;
+    hipLaunchKernelGGL(depth_only_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), invdepth, mono_invdepth, mask, n, dL_dloss, weight,
+                       (float)dens_weight, (float)(1.0 - dens_weight), 1.0f / (float)n, dL_dinvdepth);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_last_error(std::string("gsr_depth_only_loss_backward: ") + hipGetErrorString(e));
         return GSR_ERR_DEVICE;
     }
     return GSR_OK;

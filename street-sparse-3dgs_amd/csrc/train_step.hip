@@ -146,8 +146,14 @@ int gsr_train_step(gsr_train_ctx *ctx, const gsr_train_step_args *a, int64_t *nu
         return invalid("NULL parameter or gradient");
     if (!a->exposure || !a->exposure_grad || a->n_images <= 0 || a->image_index < 0 || a->image_index >= a->n_images)
         return invalid("bad exposure arguments");
-    if (!a->viewmatrix || !a->projmatrix || !a->campos || !a->background || !a->gt || !a->losses)
+    const bool depth_only = a->depth_only != 0;
+    if (!a->viewmatrix || !a->projmatrix || !a->campos || !a->background || (!a->gt && !depth_only) || !a->losses)
         return invalid("NULL camera, background, target or loss output");
+    if (depth_only && (!a->mono_invdepth || !(a->depth_weight > 0.f)))
+        return invalid("a depth-only view needs its inverse-depth map and a positive depth weight "
+                       "(train_single.py:158-161 has no loss otherwise)");
+    if (depth_only && !(a->depth_dens_weight >= 0.0 && a->depth_dens_weight <= 1.0))
+        return invalid("depth_dens_weight outside [0, 1]");
     if (!a->max_radii2D || !a->xyz_gradient_accum || !a->denom) return invalid("NULL densification statistics");
     if (a->n_groups <= 0 || !a->groups || !a->exposure_group) return invalid("no optimizer groups");
     if (a->skybox_rows < 0 || a->skybox_rows > P || a->scaffold_rows < 0)
@@ -155,7 +161,13 @@ int gsr_train_step(gsr_train_ctx *ctx, const gsr_train_step_args *a, int64_t *nu
     if (!(a->lambda_dssim >= 0.0 && a->lambda_dssim <= 1.0)) return invalid("lambda_dssim outside [0, 1]");
 
     hipStream_t s = static_cast<hipStream_t>(a->stream);
-    ctx->stream = s;
+    // the grow-only buffers are freed after a wait on ctx->stream only: a caller that switches
+    // streams first drains the previous one, whose queued kernels may still use them
+    if (ctx->stream != s) {
+        if (ctx->stream && hipStreamSynchronize(ctx->stream) != hipSuccess)
+            return fail_step(GSR_ERR_DEVICE, "previous stream");
+        ctx->stream = s;
+    }
     void *sv = a->stream;
     const int64_t npix = (int64_t)W * H;
     const bool depth = a->mono_invdepth != nullptr && a->depth_weight > 0.f;
@@ -170,7 +182,8 @@ int gsr_train_step(gsr_train_ctx *ctx, const gsr_train_step_args *a, int64_t *nu
     float *d_invd = ctx->f32(kDInvDepth, npix);
     void *loss_scratch = ctx->get(kLossScratch, gsr_l1_ssim_scratch_bytes(3, H, W));
     void *exp_scratch = ctx->get(kExpScratch, gsr_exposure_scratch_bytes(npix));
-    void *depth_scratch = ctx->get(kDepthScratch, gsr_depth_l1_scratch_bytes(npix));
+    void *depth_scratch =
+        ctx->get(kDepthScratch, std::max(gsr_depth_l1_scratch_bytes(npix), gsr_depth_only_scratch_bytes(npix)));
     // words: [0] the Adam relevance flag, [1] dL/dloss = 1 (the upstream of loss.backward())
     void *words = ctx->get(kWords, 64);
     if (ctx->failed_alloc || !scales || !rots || !opac || !d_scales || !d_rots || !d_opac || !d_means2D || !radii ||
@@ -206,25 +219,39 @@ int gsr_train_step(gsr_train_ctx *ctx, const gsr_train_step_args *a, int64_t *nu
     set_raw_params(false);
     if (rc) return fail_step(rc, "rasterizer forward");
     const float *E = a->exposure + 12 * (int64_t)a->image_index;
-    // exposure (x the alpha mask, train_single.py:117-119, in the same pass)
-    if ((rc = launch_exposure_forward(color, E, npix, image, a->alpha_mask, s))) return fail_step(rc, "exposure");
+    if (depth_only) {
+        // a depth-only view (train_single.py:145-161): the rendered image is in no loss, so the
+        // exposure pass, the SSIM pass and the exposure step (:213-214) do not run; the colour
+        // gradient is zero and the exposure gradient is zeroed (:203-209)
+        if ((rc = step_depth_only_forward(invd, a->mono_invdepth, a->depth_mask, npix, a->depth_weight,
+                                          a->depth_dens_weight, depth_scratch, d_invd, a->losses, flag, s)))
+            return fail_step(rc, "depth-only loss");
+        if (hipMemsetAsync(d_color, 0, sizeof(float) * 3 * npix, s) != hipSuccess ||
+            hipMemsetAsync(a->exposure_grad, 0, sizeof(float) * 12 * (size_t)a->n_images, s) != hipSuccess)
+            return fail_step(GSR_ERR_DEVICE, "depth-only zero gradients");
+    } else {
+        // exposure (x the alpha mask, train_single.py:117-119, in the same pass)
+        if ((rc = launch_exposure_forward(color, E, npix, image, a->alpha_mask, s)))
+            return fail_step(rc, "exposure");
 
-    // losses (train_single.py:121-141): the SSIM map pass with its gradient field, the depth L1 with
-    // its gradient (the loss is the root: dL/dloss = 1), one epilogue for both values and the total
-    bool photo = false;  // the SSIM pass wrote the photometric gradient itself (gsr_launch.h)
-    if ((rc = step_loss_forward(image, a->gt, H, W, a->lambda_dssim, loss_scratch, gmap, invd,
-                                depth ? a->mono_invdepth : nullptr, a->depth_mask, a->depth_weight, depth_scratch,
-                                d_invd, a->losses, flag, s, GSR_STEP_PHOTO_IN_SSIM ? one : nullptr, a->alpha_mask,
-                                &photo)))
-        return fail_step(rc, "losses");
+        // losses (train_single.py:121-141): the SSIM map pass with its gradient field, the depth L1
+        // with its gradient (the loss is the root: dL/dloss = 1), one epilogue for both values and
+        // the total
+        bool photo = false;  // the SSIM pass wrote the photometric gradient itself (gsr_launch.h)
+        if ((rc = step_loss_forward(image, a->gt, H, W, a->lambda_dssim, loss_scratch, gmap, invd,
+                                    depth ? a->mono_invdepth : nullptr, a->depth_mask, a->depth_weight,
+                                    depth_scratch, d_invd, a->losses, flag, s, GSR_STEP_PHOTO_IN_SSIM ? one : nullptr,
+                                    a->alpha_mask, &photo)))
+            return fail_step(rc, "losses");
 
-    // loss.backward(): photometric gradient -> alpha mask -> exposure (colour gradient, exposure
-    // gradient and the exposure optimizer's step in the same two launches)
-    gsr_adam_group eg = *a->exposure_group;
-    if ((rc = step_loss_backward(image, a->gt, gmap, one, a->lambda_dssim, a->alpha_mask, color, E, npix, d_color,
-                                 exp_scratch, a->n_images, a->image_index, eg, a->exposure_grad, a->exposure_beta1,
-                                 a->exposure_beta2, a->exposure_eps, s, photo)))
-        return fail_step(rc, "loss backward");
+        // loss.backward(): photometric gradient -> alpha mask -> exposure (colour gradient, exposure
+        // gradient and the exposure optimizer's step in the same two launches)
+        gsr_adam_group eg = *a->exposure_group;
+        if ((rc = step_loss_backward(image, a->gt, gmap, one, a->lambda_dssim, a->alpha_mask, color, E, npix, d_color,
+                                     exp_scratch, a->n_images, a->image_index, eg, a->exposure_grad,
+                                     a->exposure_beta1, a->exposure_beta2, a->exposure_eps, s, photo)))
+            return fail_step(rc, "loss backward");
+    }
     // sparse gradient rows (gsr_launch.h GaussianGrads): the Gaussians no pixel's backward reached
     // (88% of the bench scene) have zero gradients and are never relevant to the sparse Adam, so
     // their 232 B of gradient rows are not written (GSR_STEP_DENSE_ROWS=1: every row, as the
@@ -262,7 +289,8 @@ int gsr_train_step(gsr_train_ctx *ctx, const gsr_train_step_args *a, int64_t *nu
                                      radii, d_means2D, a->max_radii2D, a->xyz_gradient_accum, a->denom, s, sparse_rows,
                                      a->scaling, a->opacity)))
         return fail_step(rc, "activation backward");
-    if ((rc = sparse_adam(a->n_groups, a->groups, P, a->opacity_grad, a->beta1, a->beta2, a->eps, flag, true, s,
+    if (!a->skip_gaussian_step &&
+        (rc = sparse_adam(a->n_groups, a->groups, P, a->opacity_grad, a->beta1, a->beta2, a->eps, flag, true, s,
                           a->scaling, a->scaffold_rows, a->max_scale, sparse_rows ? d_means2D : nullptr,
                           a->skybox_rows)))
         return fail_step(rc, "sparse Adam + shrink");

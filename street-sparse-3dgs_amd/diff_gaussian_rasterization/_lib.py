@@ -44,7 +44,8 @@ class TrainStepArgs(ctypes.Structure):
                 ("eps", ctypes.c_double), ("exposure_group", ctypes.POINTER(AdamGroup)),
                 ("exposure_beta1", ctypes.c_double), ("exposure_beta2", ctypes.c_double),
                 ("exposure_eps", ctypes.c_double), ("skybox_rows", _i64), ("scaffold_rows", _i64),
-                ("max_scale", _f), ("losses", _vp), ("stream", _vp)]
+                ("max_scale", _f), ("losses", _vp), ("stream", _vp), ("depth_only", _i),
+                ("depth_dens_weight", ctypes.c_double), ("skip_gaussian_step", _i)]
 
 
 # exported symbol -> (restype, argtypes); must match include/gsr.h, gsr_train.h, gsr_hier.h, gsr_knn.h, gsr_densify.h
@@ -90,6 +91,9 @@ SIGNATURES = {
     "gsr_depth_l1_scratch_bytes": (ctypes.c_size_t, [_i64]),
     "gsr_depth_l1_forward": (_i, [_vp, _vp, _vp, _i64, _f, _vp, _vp, _vp]),
     "gsr_depth_l1_backward": (_i, [_vp, _vp, _vp, _i64, _f, _vp, _vp, _vp]),
+    "gsr_depth_only_scratch_bytes": (ctypes.c_size_t, [_i64]),
+    "gsr_depth_only_loss_forward": (_i, [_vp, _vp, _vp, _i64, _f, ctypes.c_double, _vp, _vp, _vp]),
+    "gsr_depth_only_loss_backward": (_i, [_vp, _vp, _vp, _i64, _f, ctypes.c_double, _vp, _vp, _vp]),
     "gsr_exposure_forward": (_i, [_vp, _vp, _i64, _vp, _vp]),
     "gsr_exposure_scratch_bytes": (ctypes.c_size_t, [_i64]),
     "gsr_exposure_backward": (_i, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
@@ -113,7 +117,7 @@ SIGNATURES = {
                                           _vp, _vp, _vp, _vp, _vp]),
 }
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 _lib = None
 
 

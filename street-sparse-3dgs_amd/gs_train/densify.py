@@ -38,8 +38,8 @@ def densify_and_prune(g, optimizer, max_grad: float, min_opacity: float, extent:
     the parameters (and their optimizer state) with the densified / pruned rows and resets the
     densification statistics, as the reference does.  first_row: scaffold_points (rows never
     densified or pruned).  normals: the (2 n_split, 3) standard-normal draws behind the split
-    samples, if given (parity tests inject the reference's own); drawn here otherwise.  Returns the
-    plan's counts."""
+    samples, if given (parity tests inject the reference's own; a callable gets n_split and returns
+    them); drawn here otherwise.  Returns the plan's counts."""
     from diff_gaussian_rasterization._lib import RowGroup
     if not getattr(g, "joined", False):
         raise ValueError("densify_and_prune works on the joined (P,16,3) SH layout")
@@ -59,6 +59,8 @@ def densify_and_prune(g, optimizer, max_grad: float, min_opacity: float, extent:
     n_old, n_clone, n_split, total = (int(v) for v in counts.cpu())
     # the reference's torch.normal(mean=zeros, std=stds) draws normal_(0, 1) on a (2 n_split, 3)
     # tensor and scales it: the same generator stream
+    if callable(normals):
+        normals = normals(n_split)
     if normals is None:
         normals = torch.empty((2 * n_split, 3), device=dev).normal_() if n_split else None
     else:

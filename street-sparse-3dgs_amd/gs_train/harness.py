@@ -23,8 +23,13 @@ reference's .item() calls feed only its progress bar).  The reference-structured
 the same step (conv2d SSIM, OurAdam gather/scatter, ...) lives in oracle/train_torch_ref.py
 (ReferenceTrainStep, test infrastructure and the bench's baseline leg) and overrides the hook
 methods below.  Densify/prune, opacity reset, SH degree increments and checkpointing run every
-few hundred/thousand iterations and are out of scope (gs_train.densify
-has the densify/prune kernels).  Depth-only views (additional_depth_maps) are not modelled.
+few hundred/thousand iterations: gs_train.chunk.TrainChunk runs train_single.py's whole loop around
+this step (step(between=...) hands it the point between the statistics and the optimizers).
+
+Depth-only views (Street-sparse's additional depth maps, train_single.py:69-72,145-161,203-214):
+the loss is depth_l1_weight * (a * mean(clamp(mono - invD, 0)) + (1 - a) * |(invD - mono) *
+mask|.mean()) with a = additional_depth_maps_weight; the image is in no loss (no colour gradient),
+the SH gradients are zeroed and the exposure optimizer does not step.
 """
 from __future__ import annotations
 
@@ -38,7 +43,7 @@ from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianR
 from .activations import activate, shrink_scales
 from .densify import add_densification_stats
 from .exposure import apply_exposure
-from .loss import depth_l1_loss, photo_loss
+from .loss import depth_l1_loss, depth_only_loss, photo_loss
 from .optim import Adam
 
 # arguments/__init__.py:89-109 (OptimizationParams defaults)
@@ -47,6 +52,7 @@ LR = dict(position_lr_init=0.00002, position_lr_final=0.0000002, position_lr_del
           exposure_lr_init=0.001, exposure_lr_final=0.0001, exposure_lr_delay_steps=5000,
           exposure_lr_delay_mult=0.001, depth_l1_weight_init=1.0, depth_l1_weight_final=0.01, iterations=30_000,
           lambda_dssim=0.2)
+ADDITIONAL_DEPTH_MAPS_WEIGHT = 0.9  # arguments/__init__.py:71
 
 
 def expon_lr(step, lr_init, lr_final, lr_delay_steps=0, lr_delay_mult=1.0, max_steps=1_000_000):
@@ -149,11 +155,13 @@ class TrainStep:
     alpha_masks (1, H, W).  skybox_points: the first rows are the locked skybox
     (scene/gaussian_model.py:73-74,182-187).  scaffold_points: the first rows are the coarse
     scaffold (scene/gaussian_model.py:224-262, loaded with a scaffold_file), which the scale shrink
-    leaves alone (train_single.py:239-240: violators[:scaffold_points] = False)."""
+    leaves alone (train_single.py:239-240: violators[:scaffold_points] = False).  depth_only: per
+    view, True for a depth-only view (its gts entry may be None; it needs a mono inverse-depth map);
+    dens_weight: additional_depth_maps_weight."""
 
     def __init__(self, gaussians: GaussianSet, cameras, gts, W, H, cameras_extent=10.0, mono_invdepths=None,
                  depth_masks=None, alpha_masks=None, skybox_points=0, scaffold_points=0,
-                 iterations=LR["iterations"]):
+                 iterations=LR["iterations"], depth_only=None, dens_weight=ADDITIONAL_DEPTH_MAPS_WEIGHT):
         self.g = gaussians
         self.W, self.H = W, H
         self.extent = cameras_extent
@@ -162,6 +170,13 @@ class TrainStep:
         self.mono = mono_invdepths if mono_invdepths is not None else [None] * n
         self.dmask = depth_masks if depth_masks is not None else [None] * n
         self.amask = alpha_masks if alpha_masks is not None else [None] * n
+        self.depth_only = [bool(v) for v in depth_only] if depth_only is not None else [False] * n
+        if len(self.depth_only) != n:
+            raise ValueError("depth_only: one flag per view")
+        for k, d in enumerate(self.depth_only):
+            if d and self.mono[k] is None:
+                raise ValueError(f"view {k}: a depth-only view needs its inverse-depth map")
+        self.dens_weight = float(dens_weight)
         self.skybox = int(skybox_points)
         self.scaffold = int(scaffold_points)
         dev = gaussians._xyz.device
@@ -178,6 +193,7 @@ class TrainStep:
                                                lr_delay_mult=LR["exposure_lr_delay_mult"], max_steps=iterations)
         self.depth_weight = lambda it: expon_lr(it, LR["depth_l1_weight_init"], LR["depth_l1_weight_final"],
                                                 max_steps=iterations)
+        self.iterations = int(iterations)
         self.iteration = 1
         self._means2D = None
         self._one = None
@@ -217,6 +233,16 @@ class TrainStep:
     def _depth_loss(self, invd, mono, mask, w):
         return depth_l1_loss(invd, mono, mask, w)
 
+    def _depth_only_loss(self, invd, mono, mask, w):
+        return depth_only_loss(invd, mono, mask, w, self.dens_weight)[0]
+
+    def _zero_feature_grads(self):
+        # train_single.py:203-207 (the exposure gradient of :208-209 never exists here: the image is
+        # in no loss)
+        g = self.g._features.grad
+        if g is not None:
+            g.zero_()
+
     def _backward(self, loss):
         if self._one is None:
             self._one = torch.ones((), device=loss.device)
@@ -241,6 +267,18 @@ class TrainStep:
     def _shrink(self):
         shrink_scales(self.g._scaling, self.extent * 0.02, first_row=self.scaffold)
 
+    # ---- the loop's events (gs_train.chunk.TrainChunk; train_single.py:196-201) ----
+    def densify_and_prune(self, max_grad, min_opacity, percent_dense, normals=None):
+        """gaussians.densify_and_prune(max_grad, min_opacity, cameras_extent, False) on the device
+        (gs_train.densify).  normals: callable(n_split) -> the split draws, or None."""
+        from .densify import densify_and_prune
+        return densify_and_prune(self.g, self.optimizer, max_grad, min_opacity, self.extent, percent_dense,
+                                 first_row=self.scaffold, normals=normals)
+
+    def reset_opacity(self):
+        from .chunk import reset_opacity
+        reset_opacity(self.g, self.optimizer, self.skybox)
+
     def render(self, cam_idx, bg):
         c = self.cams[cam_idx]
         g = self.g
@@ -256,11 +294,20 @@ class TrainStep:
                                                     rotations=rotations, cov3D_precomp=None)
         return self._apply_exposure(color, g._exposure[cam_idx]), invd, means2D, radii
 
-    def step(self, cam_idx=None):
-        """One iteration; returns the loss tensor (no host synchronisation on the fused path)."""
+    def _view(self, cam_idx):
+        return (self.iteration - 1) % len(self.cams) if cam_idx is None else cam_idx
+
+    def step(self, cam_idx=None, between=None):
+        """One iteration; returns the loss tensor (no host synchronisation on the fused path).
+
+        between: called after the densification statistics, before the optimizers
+        (train_single.py:190-201: densify_and_prune / reset_opacity).  Those replace the Gaussian
+        nn.Parameters, whose .grad is then None, so the reference's sparse Adam does not run in such
+        an iteration (:217, :225); neither does it here.  The scale shrink still does."""
         g = self.g
         it = self.iteration
-        k = (it - 1) % len(self.cams) if cam_idx is None else cam_idx
+        k = self._view(cam_idx)
+        depth_only = self.depth_only[k]
         for pg in self.optimizer.param_groups:
             if pg["name"] == "xyz":
                 pg["lr"] = self.xyz_lr(it)
@@ -268,20 +315,31 @@ class TrainStep:
             pg["lr"] = self.exposure_lr(it)
         bg = torch.rand(3, device=g._xyz.device)
         image, invd, means2D, radii = self.render(k, bg)
-        if self.amask[k] is not None:
-            image = image * self.amask[k]
-        loss = self._photo_loss(image, self.gts[k])
         w = self.depth_weight(it)
-        if self.mono[k] is not None and w > 0:
-            loss = loss + self._depth_loss(invd, self.mono[k], self.dmask[k], w)
+        if depth_only:
+            if not w > 0:
+                raise ValueError("a depth-only iteration with no depth weight has no loss (train_single.py:158-161)")
+            loss = self._depth_only_loss(invd, self.mono[k], self.dmask[k], w)
+        else:
+            if self.amask[k] is not None:
+                image = image * self.amask[k]
+            loss = self._photo_loss(image, self.gts[k])
+            if self.mono[k] is not None and w > 0:
+                loss = loss + self._depth_loss(invd, self.mono[k], self.dmask[k], w)
         self._backward(loss)
         with torch.no_grad():
             self._densify_stats(radii, means2D.grad)
-            self.exposure_optimizer.step()
+            if between is not None:
+                between()
+            if depth_only:
+                self._zero_feature_grads()
+            else:
+                self.exposure_optimizer.step()
             self.exposure_optimizer.zero_grad(set_to_none=True)
-            if self.skybox > 0 and g._opacity.grad is not None:
-                self._lock_skybox()
-            self._sparse_step()
+            if between is None:
+                if self.skybox > 0 and g._opacity.grad is not None:
+                    self._lock_skybox()
+                self._sparse_step()
             self.optimizer.zero_grad(set_to_none=True)
             self._shrink()  # train_single.py:235-241: shrink Gaussians larger than 2% of the extent
         self.iteration += 1
@@ -289,13 +347,16 @@ class TrainStep:
 
 
 def make_problem(P, W, H, n_views=4, seed=0, sh_degree=3, device="cuda", step_cls=None, perturb=0.02,
-                 depth=True, depth_mask_frac=0.85, alpha=False, skybox_points=0, scaffold_points=0, fovx_deg=60.0):
+                 depth=True, depth_mask_frac=0.85, alpha=False, skybox_points=0, scaffold_points=0, fovx_deg=60.0,
+                 depth_only=0, iterations=LR["iterations"]):
     """A synthetic Street-sparse training problem: ground-truth views and inverse-depth maps
     rendered from a seeded scene over `n_views` orbit cameras, depth masks (a random ~85% of each
     map valid, as the reference's depth_mask), optional alpha masks, and a step (TrainStep, or
     `step_cls`, e.g. oracle/train_torch_ref.ReferenceTrainStep) that starts from a perturbed copy.
     The mono depth maps are the true inverse depth with 5% multiplicative noise.  fovx_deg: 90 for
-    Street-sparse's cube faces (ss_utils/generate_colmap_calibration.py:476-479: f = size / 2)."""
+    Street-sparse's cube faces (ss_utils/generate_colmap_calibration.py:476-479: f = size / 2).
+    depth_only: the last `depth_only` views are depth-only (no target image; a LiDAR-like map: the
+    true inverse depth on a random 30% of the pixels, zero elsewhere)."""
     from .synthetic import orbit_cameras, synthetic_scene
     step_cls = step_cls or TrainStep
     s = synthetic_scene(P, W, H, seed=seed, sh_degree=sh_degree, fovx_deg=fovx_deg)
@@ -313,6 +374,10 @@ def make_problem(P, W, H, n_views=4, seed=0, sh_degree=3, device="cuda", step_cl
             monos.append((invd * noise).contiguous())
             dmasks.append((torch.rand(invd.shape, generator=gen, device=device) < depth_mask_frac).float())
             amasks.append((torch.rand(invd.shape, generator=gen, device=device) < 0.97).float())
+            if k >= n_views - depth_only:
+                gts[-1] = None
+                monos[-1] = (invd * (torch.rand(invd.shape, generator=gen, device=device) < 0.3).float()).contiguous()
+                amasks[-1] = None
     rng = np.random.default_rng(seed + 99)
     noisy = dict(means3D=s["means3D"] + perturb * rng.normal(size=s["means3D"].shape).astype(np.float32),
                  shs=s["shs"] + perturb * rng.normal(size=s["shs"].shape).astype(np.float32),
@@ -321,6 +386,9 @@ def make_problem(P, W, H, n_views=4, seed=0, sh_degree=3, device="cuda", step_cl
     model = GaussianSet(noisy["means3D"], noisy["shs"], noisy["opacities"], noisy["scales"].astype(np.float32),
                         noisy["rotations"], n_images=n_views, sh_degree=sh_degree, device=device,
                         joined_features=getattr(step_cls, "JOINED_FEATURES", True))
+    if depth_only and not depth:
+        raise ValueError("depth-only views need depth supervision (depth=True)")
     return step_cls(model, cams, gts, W, H, mono_invdepths=monos if depth else None,
                     depth_masks=dmasks if depth else None, alpha_masks=amasks if alpha else None,
-                    skybox_points=skybox_points, scaffold_points=scaffold_points)
+                    skybox_points=skybox_points, scaffold_points=scaffold_points, iterations=iterations,
+                    depth_only=[k >= n_views - depth_only for k in range(n_views)])

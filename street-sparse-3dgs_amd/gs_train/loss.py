@@ -162,3 +162,50 @@ def depth_l1_loss(invd: torch.Tensor, mono: torch.Tensor, mask: torch.Tensor | N
     """depth_l1_weight * |(invDepth - mono_invdepth) * depth_mask|.mean()  (train_single.py:138-140),
     differentiable w.r.t. invd.  Returns the weighted loss (a 0-dim tensor)."""
     return _DepthL1.apply(invd, mono, mask, weight)[0]
+
+
+class _DepthOnlyLoss(torch.autograd.Function):
+    """A depth-only view's loss (include/gsr_train.h gsr_depth_only_loss_*), train_single.py:152-156:
+    w * (a * mean(clamp(mono - invD, min=0)) + (1 - a) * mean(|(invD - mono) * mask|)), a =
+    additional_depth_maps_weight.  Gradient bit-identical to torch's autograd through that
+    expression; the means are fp64-accumulated (fp32 rounding from torch's)."""
+
+    @staticmethod
+    def forward(ctx, invd, mono, mask, weight, dens_weight):
+        require_gpu(invd, mono, mask)
+        if invd.shape != mono.shape or (mask is not None and mask.shape != invd.shape):
+            raise ValueError("invdepth, mono_invdepth and depth_mask must have one shape")
+        x = invd.detach().float().contiguous()
+        y = mono.detach().float().contiguous()
+        m = mask.detach().float().contiguous() if mask is not None else None
+        n = x.numel()
+        L = lib()
+        out = torch.empty(3, dtype=torch.float32, device=x.device)
+        scratch = torch.empty(max(16, int(L.gsr_depth_only_scratch_bytes(n))), dtype=torch.uint8, device=x.device)
+        check(L.gsr_depth_only_loss_forward(ptr(x), ptr(y), ptr(m), n, float(weight), float(dens_weight),
+                                            ptr(scratch), ptr(out), stream(x.device)), "gsr_depth_only_loss_forward")
+        ctx.save_for_backward(x, y, m)
+        ctx.weight = float(weight)
+        ctx.dens_weight = float(dens_weight)
+        ctx.set_materialize_grads(False)
+        loss, pure, dens = out[2], out[0], out[1]
+        ctx.mark_non_differentiable(pure, dens)
+        return loss, pure, dens
+
+    @staticmethod
+    def backward(ctx, gloss, _gpure, _gdens):
+        if gloss is None:
+            return None, None, None, None, None
+        x, y, m = ctx.saved_tensors
+        d = torch.empty_like(x)
+        check(lib().gsr_depth_only_loss_backward(ptr(x), ptr(y), ptr(m), x.numel(), ctx.weight, ctx.dens_weight,
+                                                 ptr(gloss.float().contiguous()), ptr(d), stream(x.device)),
+              "gsr_depth_only_loss_backward")
+        return d, None, None, None, None
+
+
+def depth_only_loss(invd: torch.Tensor, mono: torch.Tensor, mask: torch.Tensor | None, weight: float,
+                    dens_weight: float = 0.9):
+    """depth_l1_weight * (a * Ll1depth_dens + (1 - a) * Ll1depth_pure) for a depth-only view
+    (train_single.py:152-156), differentiable w.r.t. invd.  Returns (loss, pure, dens)."""
+    return _DepthOnlyLoss.apply(invd, mono, mask, weight, dens_weight)

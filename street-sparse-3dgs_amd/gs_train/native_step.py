@@ -10,8 +10,11 @@ results as TrainStep (bit for bit with the deterministic backward; tests/test_gp
 
 The parameters, the Adam moments (the optimizer's own state tensors, so densification and
 checkpoint code keep working on them) and the densification statistics stay the Python
-objects'.  The gradients land in persistent buffers (`grads`, overwritten every step) instead of
-`.grad`, which stays None as after TrainStep's zero_grad(set_to_none=True).
+objects'.  The gradients land in persistent buffers (`grads`) instead of `.grad`, which stays None
+as after TrainStep's zero_grad(set_to_none=True).  `grads` is sparse by default: the opacity
+gradient is written for every row each step, the other rows only for the Gaussians the backward
+reached this step (every other row's gradient is zero by definition and its buffer row keeps an
+older value; the buffers start zeroed).  GSR_STEP_DENSE_ROWS=1 writes every row.
 """
 from __future__ import annotations
 
@@ -80,8 +83,8 @@ class NativeTrainStep(TrainStep):
             if t.dtype != torch.float32 or not t.is_contiguous():
                 raise ValueError(f"{n}: the native step needs contiguous float32 parameters")
         dev = g._xyz.device
-        self.grads = {n: torch.empty_like(getattr(g, n)) for n in _PARAMS}
-        self.grads["_exposure"] = torch.empty_like(g._exposure)
+        self.grads = {n: torch.zeros_like(getattr(g, n)) for n in _PARAMS}
+        self.grads["_exposure"] = torch.zeros_like(g._exposure)
         by_id = {id(getattr(g, n)): self.grads[n] for n in _PARAMS + ("_exposure",)}
         self._main = self._entries(self.optimizer, by_id)
         self._expo = self._entries(self.exposure_optimizer, by_id)
@@ -117,10 +120,17 @@ class NativeTrainStep(TrainStep):
         self._key = self._params_key()
 
     def _params_key(self):
+        """Everything the cached argument block points at: the parameters, the statistics and the
+        optimizers' moment tensors (load_state_dict or a cleared state swaps those in without
+        touching the parameters)."""
         g = self.g
+        moments = tuple(
+            (id(st), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr()) if "exp_avg" in st else (id(st),)
+            for opt in (self.optimizer, self.exposure_optimizer) for group in opt.param_groups
+            for p in group["params"] for st in (opt.state.get(p, {}),))
         return tuple((getattr(g, n).data_ptr(), tuple(getattr(g, n).shape)) for n in _PARAMS) + \
             (g._exposure.data_ptr(), g.max_radii2D.data_ptr(), g.xyz_gradient_accum.data_ptr(), g.denom.data_ptr(),
-             g.active_sh_degree)
+             g.active_sh_degree) + moments
 
     @staticmethod
     def _advance(entries, carr):
@@ -138,20 +148,26 @@ class NativeTrainStep(TrainStep):
             carr[i].step_size = lr / (1 - b1 ** s)
             carr[i].bias_correction2_sqrt = math.sqrt(1 - b2 ** s)
 
-    def step(self, cam_idx=None):
-        """One iteration through gsr_train_step; returns the loss tensor (no host synchronisation)."""
+    def step(self, cam_idx=None, between=None):
+        """One iteration through gsr_train_step; returns the loss tensor (no host synchronisation
+        unless `between` is given).  between: as TrainStep.step -- the native step stops after the
+        exposure step, `between` replaces the parameters, and the scale shrink runs on the new ones
+        (no Gaussian Adam step in such an iteration, as in train_single.py)."""
         if self._key is None or self._key != self._params_key():
             self._setup()
         g = self.g
         it = self.iteration
-        k = (it - 1) % len(self.cams) if cam_idx is None else cam_idx
+        k = self._view(cam_idx)
+        depth_only = self.depth_only[k]
         for pg in self.optimizer.param_groups:
             if pg["name"] == "xyz":
                 pg["lr"] = self.xyz_lr(it)
         for pg in self.exposure_optimizer.param_groups:
             pg["lr"] = self.exposure_lr(it)
-        self._advance(self._main, self._groups)
-        self._advance(self._expo, self._egroup)
+        if between is None:
+            self._advance(self._main, self._groups)
+        if not depth_only:
+            self._advance(self._expo, self._egroup)
         dev = g._xyz.device
         bg = torch.rand(3, device=dev)
         c = self.cams[k]
@@ -160,16 +176,21 @@ class NativeTrainStep(TrainStep):
         a.viewmatrix, a.projmatrix, a.campos = c["view"].data_ptr(), c["proj"].data_ptr(), c["campos"].data_ptr()
         a.tan_fovx, a.tan_fovy = c["tx"], c["ty"]
         a.background = bg.data_ptr()
-        a.gt = self.gts[k].data_ptr()
+        a.gt = self.gts[k].data_ptr() if not depth_only else None
         am = self.amask[k]
-        a.alpha_mask = am.data_ptr() if am is not None else None
+        a.alpha_mask = am.data_ptr() if (am is not None and not depth_only) else None
         w = self.depth_weight(it)
         mono = self.mono[k]
         depth = mono is not None and w > 0
+        if depth_only and not depth:
+            raise ValueError("a depth-only iteration with no depth weight has no loss (train_single.py:158-161)")
         a.mono_invdepth = mono.data_ptr() if depth else None
         dm = self.dmask[k]
         a.depth_mask = dm.data_ptr() if (depth and dm is not None) else None
         a.depth_weight = w if depth else 0.0
+        a.depth_only = int(depth_only)
+        a.depth_dens_weight = self.dens_weight
+        a.skip_gaussian_step = int(between is not None)
         losses = torch.empty(6, dtype=torch.float32, device=dev)  # a fresh tensor per step, as TrainStep's
         a.losses = losses.data_ptr()
         a.stream = stream(dev).value
@@ -177,5 +198,9 @@ class NativeTrainStep(TrainStep):
         check(lib().gsr_train_step(self._ctx, ctypes.byref(a), ctypes.byref(K)), "gsr_train_step")
         self.last_K = K.value
         self._bg = bg  # keep the background alive until the stream has used it
+        if between is not None:
+            with torch.no_grad():
+                between()
+                self._shrink()
         self.iteration += 1
         return losses[5]

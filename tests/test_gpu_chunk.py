@@ -1,0 +1,296 @@
+"""GPU tests of the Street-sparse per-chunk loop (gs_train.chunk.TrainChunk: train_single.py:65-247)
+and of its depth-only iterations (train_single.py:69-72,145-161,203-214).
+
+* the depth-only loss node vs torch's autograd through the reference's expression: gradient bit
+  for bit, value to fp32 rounding;
+* the native step (gsr_train_step) vs the Python-driven step over a view cycle mixing photometric
+  and depth-only views: bit-identical with the deterministic backward;
+* the whole chunk loop -- densify / prune events, opacity resets, SH-degree increments, lr and depth
+  weight schedules -- native vs Python-driven: bit-identical, P identical after every event; and
+  vs the reference's torch formulation (oracle/train_torch_ref.ReferenceTrainStep, its own
+  densify_and_prune / reset_opacity) on the same generator stream: P identical after every event,
+  parameters within an fp32 tolerance;
+* checkpoint / resume (capture + restore, which swaps every parameter and moment tensor) is
+  bit-identical to the uninterrupted run;
+* the native step's dense-rows fallback zeroes the locked skybox rows' six gradients.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+NAMES = ("_xyz", "_features", "_opacity", "_scaling", "_rotation", "_exposure")
+
+
+def _snapshot(ts):
+    g = ts.g
+    return ([getattr(g, n).detach().clone() for n in NAMES],
+            [ts.optimizer.state[getattr(g, n)][k].clone() for n in NAMES[:-1] for k in ("exp_avg", "exp_avg_sq")],
+            [float(ts.optimizer.state[getattr(g, n)]["step"]) for n in NAMES[:-1]],
+            [g.max_radii2D.clone(), g.xyz_gradient_accum.clone(), g.denom.clone()], g.active_sh_degree)
+
+
+def _assert_equal_snapshots(a, b):
+    (pa, ma, sa, ta, da), (pb, mb, sb, tb, db) = a, b
+    for n, x, y in zip(NAMES, pa, pb):
+        assert x.shape == y.shape and torch.equal(x, y), n
+    for x, y in zip(ma, mb):
+        assert torch.equal(x, y)
+    assert sa == sb and da == db
+    for x, y in zip(ta, tb):
+        assert torch.equal(x, y)
+
+
+def test_depth_only_loss_matches_torch_expression():
+    """gs_train.loss.depth_only_loss vs train_single.py:152-156 through torch autograd: dL/dinvdepth
+    bit-identical (the clamp passes the gradient at mono == invD, sgn(0) = 0), the value to fp32
+    rounding; with a mask and without."""
+    from gs_train.loss import depth_only_loss
+    g = torch.Generator(device=DEV).manual_seed(9)
+    for H, W in ((1536, 1536), (37, 53)):
+        invd = torch.rand(1, H, W, generator=g, device=DEV)
+        mono = invd * (1 + 0.1 * torch.randn(1, H, W, generator=g, device=DEV))
+        mono *= (torch.rand(1, H, W, generator=g, device=DEV) < 0.4).float()  # sparse LiDAR-like map
+        mono[:, :3] = invd[:, :3]  # exact ties of the clamp and of sgn
+        mask = (torch.rand(1, H, W, generator=g, device=DEV) < 0.9).float()
+        for m in (mask, None):
+            w, a = 0.61, 0.9
+            x = invd.clone().requires_grad_(True)
+            lx, pure, dens = depth_only_loss(x, mono, m, w, a)
+            lx.backward()
+            y = invd.clone().requires_grad_(True)
+            mm = m if m is not None else torch.ones_like(invd)
+            p_ref = torch.abs((y - mono) * mm).mean()
+            d_ref = (mono - y).clamp(min=0).mean()
+            ly = (w * (a * d_ref + (1 - a) * p_ref)).clone()
+            ly.backward()
+            assert torch.equal(x.grad, y.grad)
+            assert abs(lx.item() - ly.item()) <= 2e-6 * abs(ly.item())
+            assert abs(pure.item() - p_ref.item()) <= 2e-6 * abs(p_ref.item())
+            assert abs(dens.item() - d_ref.item()) <= 2e-6 * abs(d_ref.item())
+
+
+@pytest.mark.parametrize("skybox,alpha", [(0, False), (300, True)])
+def test_native_step_with_depth_only_views_equals_python_step(skybox, alpha):
+    """A view cycle of three photometric and two depth-only views: the native step (depth-only
+    branch: no SSIM / exposure pass, zero colour gradient, exposure gradient zeroed, no exposure
+    step) is bit-identical to the Python-driven step, which zeroes the SH gradients explicitly."""
+    from helpers import deterministic
+    from gs_train.harness import make_problem
+    from gs_train.native_step import NativeTrainStep
+    out = {}
+    with deterministic():
+        for native in (False, True):
+            torch.manual_seed(0)
+            ts = make_problem(20_000, 256, 192, n_views=5, seed=1, step_cls=NativeTrainStep if native else None,
+                              depth=True, alpha=alpha, skybox_points=skybox, depth_only=2)
+            torch.manual_seed(3)
+            losses = torch.stack([ts.step().clone() for _ in range(7)])
+            out[native] = (losses, _snapshot(ts),
+                           [ts.exposure_optimizer.state[ts.g._exposure][k].clone() for k in ("exp_avg", "exp_avg_sq")],
+                           float(ts.exposure_optimizer.state[ts.g._exposure]["step"]))
+    (la, sa, ea, esa), (lb, sb, eb, esb) = out[False], out[True]
+    assert torch.equal(la, lb), (la, lb)
+    _assert_equal_snapshots(sa, sb)
+    for x, y in zip(ea, eb):
+        assert torch.equal(x, y)
+    # 7 steps over [p, p, p, d, d, p, p]: the exposure optimizer stepped on the 5 photometric ones
+    assert esa == esb == 5.0
+    assert sa[2] == [7.0] * 5
+
+
+def test_depth_only_step_matches_reference_structured_step():
+    """The depth-only iteration against the reference's torch formulation (ReferenceTrainStep: the
+    torch expression of :152-156, SH and exposure gradients zeroed, no exposure step)."""
+    from gs_train.harness import make_problem
+    from train_torch_ref import ReferenceTrainStep
+    names = ("_xyz", "_features_dc", "_opacity", "_scaling", "_rotation")
+    res = {}
+    for fused in (True, False):
+        torch.manual_seed(0)
+        ts = make_problem(20_000, 256, 192, n_views=2, seed=2, depth=True, depth_only=2,
+                          step_cls=None if fused else ReferenceTrainStep)
+        init = [getattr(ts.g, n).detach().clone() for n in names]
+        losses = [ts.step().item() for _ in range(4)]
+        res[fused] = (losses, [getattr(ts.g, n).detach().clone() for n in names], init,
+                      ts.g._exposure.detach().clone())
+    (la, pa, ia, ea), (lb, pb, _, eb) = res[True], res[False]
+    np.testing.assert_allclose(la, lb, rtol=1e-5, atol=1e-7)
+    for n, x, y, x0 in zip(names, pa, pb, ia):
+        close = torch.isclose(x, y, rtol=0, atol=1e-5).float().mean().item()
+        assert close >= 0.999, (n, close)
+        if n != "_features_dc":
+            assert not torch.equal(x, x0), n  # the depth loss moved it
+    assert torch.equal(ea, eb) and torch.equal(ea, torch.eye(3, 4, device=DEV)[None].expand_as(ea))
+
+
+def _small_schedule(iterations):
+    from gs_train.chunk import ChunkSchedule
+    # train_single.py's loop on a scaled schedule: densify every 60 iterations in (60, 300), an opacity
+    # reset at 180 (with a densify, as every reset of the default schedule), SH increments every 100
+    return ChunkSchedule(iterations=iterations, densification_interval=60, opacity_reset_interval=180,
+                         densify_from_iter=60, densify_until_iter=300, sh_interval=100,
+                         densify_grad_threshold=0.0008, percent_dense=0.01)
+
+
+def _chunk_problem(step_cls, iterations, seed=3):
+    from gs_train.harness import make_problem
+    ts = make_problem(30_000, 192, 160, n_views=6, seed=seed, step_cls=step_cls, depth=True, alpha=True,
+                      skybox_points=200, scaffold_points=1000, depth_only=2, perturb=0.05, iterations=iterations)
+    with torch.no_grad():
+        ts.g.active_sh_degree = 0  # create_from_pcd's GaussianModel starts at degree 0
+    return ts
+
+
+def test_chunk_loop_native_equals_python():
+    """train_single.py's loop with 4 densify / prune events, an opacity reset, SH increments and
+    depth-only views: native executor vs Python-driven step, bit for bit (deterministic backward),
+    P after every event identical, the Adam step counts showing the skipped Gaussian updates."""
+    from helpers import deterministic
+    from gs_train.chunk import TrainChunk
+    from gs_train.native_step import NativeTrainStep
+    iters = 320
+    out = {}
+    with deterministic():
+        for native in (False, True):
+            torch.manual_seed(0)
+            ts = _chunk_problem(NativeTrainStep if native else None, iters)
+            torch.manual_seed(5)
+            tc = TrainChunk(ts, _small_schedule(iters))
+            tc.run()
+            out[native] = ([(e["iteration"], e["P_before"], e["P_after"]) for e in tc.events], _snapshot(ts))
+    (ea, sa), (eb, sb) = out[False], out[True]
+    assert ea == eb
+    assert [e[0] for e in ea] == [120, 180, 240]  # > densify_from_iter, < densify_until_iter
+    assert any(e[2] != e[1] for e in ea)
+    _assert_equal_snapshots(sa, sb)
+    assert sa[4] == 3  # degree 0 -> 3 at iterations 100, 200, 300
+    # Gaussian Adam steps: iterations 1..319 minus the 3 event iterations
+    assert sa[2] == [316.0] * 5
+
+
+def test_chunk_loop_matches_reference_structured_loop():
+    """~700 iterations of the loop against the reference's torch formulation: OurAdam-style gather /
+    scatter, conv2d SSIM, the torch depth expressions, the reference's own densify_and_prune and
+    reset_opacity, on the same generator stream (the random backgrounds and the split draws).  P is
+    identical after every densify / prune event; parameters agree within fp32 tolerance at every
+    event and at the end."""
+    from gs_train.chunk import ChunkSchedule, TrainChunk
+    from train_torch_ref import ReferenceTrainStep
+    iters = 700
+    sched = ChunkSchedule(iterations=iters, densification_interval=100, opacity_reset_interval=300,
+                          densify_from_iter=100, densify_until_iter=600, sh_interval=200,
+                          densify_grad_threshold=0.0008, percent_dense=0.01)
+    runs = {}
+    for fused in (True, False):
+        torch.manual_seed(0)
+        ts = _chunk_problem(None if fused else ReferenceTrainStep, iters)
+        snaps = []
+        tc = TrainChunk(ts, sched)
+        orig = tc._between
+
+        def between(it, dens, reset, tc=tc, orig=orig, snaps=snaps):
+            run = orig(it, dens, reset)
+
+            def wrapped():
+                run()
+                g = tc.ts.g
+                feats = g._features if fused else torch.cat((g._features_dc, g._features_rest), 1)
+                snaps.append([g._xyz.detach().clone(), feats.detach().clone(), g._opacity.detach().clone(),
+                              g._scaling.detach().clone(), g._rotation.detach().clone()])
+            return wrapped
+        tc._between = between
+        torch.manual_seed(5)
+        tc.run()
+        g = ts.g
+        feats = g._features if fused else torch.cat((g._features_dc, g._features_rest), 1)
+        snaps.append([g._xyz.detach().clone(), feats.detach().clone(), g._opacity.detach().clone(),
+                      g._scaling.detach().clone(), g._rotation.detach().clone()])
+        runs[fused] = ([(e["iteration"], e["P_before"], e["P_after"]) for e in tc.events], snaps)
+    (ea, sa), (eb, sb) = runs[True], runs[False]
+    assert [e[0] for e in ea] == [200, 300, 400, 500]
+    assert ea == eb, (ea, eb)
+    assert any(e[2] > e[1] for e in ea)
+    for k, (xa, xb) in enumerate(zip(sa, sb)):
+        for name, x, y in zip(("xyz", "features", "opacity", "scaling", "rotation"), xa, xb):
+            assert x.shape == y.shape, (k, name)
+            close = torch.isclose(x, y, rtol=1e-3, atol=2e-4).float().mean().item()
+            assert close >= 0.999, (k, name, close)
+
+
+def test_checkpoint_resume_is_bit_identical():
+    """capture() at an iteration and restore() into a fresh native step (new parameter and moment
+    tensors: the executor must re-read them) continues exactly as the uninterrupted run."""
+    from helpers import deterministic
+    from gs_train.chunk import TrainChunk, capture, restore
+    from gs_train.native_step import NativeTrainStep
+    iters = 260
+    with deterministic():
+        torch.manual_seed(0)
+        ts = _chunk_problem(NativeTrainStep, iters)
+        torch.manual_seed(5)
+        saved = {}
+        sched = _small_schedule(iters)
+        sched.checkpoint_iterations = (150,)
+        tc = TrainChunk(ts, sched, on_checkpoint=lambda it, st: saved.setdefault(it, st))
+        tc.run()
+        full = _snapshot(ts)
+        assert 150 in saved
+        torch.manual_seed(0)
+        ts2 = _chunk_problem(NativeTrainStep, iters)
+        ts2.step()  # the executor caches its argument block for the old tensors
+        restore(ts2, saved[150])
+        assert ts2.iteration == 151
+        TrainChunk(ts2, _small_schedule(iters)).run()
+        _assert_equal_snapshots(full, _snapshot(ts2))
+
+
+def test_native_step_after_optimizer_load_state_dict():
+    """optimizer.load_state_dict between native steps swaps in new moment tensors with the same
+    parameters (a checkpoint resume): the executor follows them, bit-identical to the Python step."""
+    from helpers import deterministic
+    from gs_train.harness import make_problem
+    from gs_train.native_step import NativeTrainStep
+    out = {}
+    with deterministic():
+        for native in (False, True):
+            torch.manual_seed(0)
+            ts = make_problem(20_000, 256, 192, n_views=3, seed=1, step_cls=NativeTrainStep if native else None)
+            torch.manual_seed(3)
+            ts.step()
+            ts.step()
+            sd = ts.optimizer.state_dict()
+            sd = {"state": {k: {kk: (vv.clone() if torch.is_tensor(vv) else vv) for kk, vv in v.items()}
+                            for k, v in sd["state"].items()}, "param_groups": sd["param_groups"]}
+            ts.step()
+            ts.optimizer.load_state_dict(sd)  # back to the moments after two steps, new tensors
+            ts.step()
+            out[native] = _snapshot(ts)
+    _assert_equal_snapshots(out[False], out[True])
+
+
+def test_native_dense_fallback_zeroes_skybox_rows(monkeypatch):
+    """GSR_STEP_DENSE_ROWS=1 and only the locked skybox rows blending: their opacity gradient is
+    locked at zero, no row is relevant and OurAdam's dense fallback updates every row -- with all six
+    of the skybox rows' gradients zero (train_single.py:217-223), as the Python step has them."""
+    from helpers import deterministic
+    from gs_train.harness import make_problem
+    from gs_train.native_step import NativeTrainStep
+    monkeypatch.setenv("GSR_STEP_DENSE_ROWS", "1")
+    S = 2000
+    out = {}
+    with deterministic():
+        for native in (False, True):
+            torch.manual_seed(0)
+            ts = make_problem(20_000, 256, 192, n_views=2, seed=4, step_cls=NativeTrainStep if native else None,
+                              depth=True, skybox_points=S)
+            torch.manual_seed(3)
+            ts.step()
+            with torch.no_grad():
+                ts.g._opacity[S:] = -30.0
+            ts.step()
+            out[native] = _snapshot(ts)
+    _assert_equal_snapshots(out[False], out[True])

@@ -168,3 +168,19 @@ def test_torch_ref_densify_matches_reference_run(case):
         np.testing.assert_array_equal(opt.state[p]["exp_avg_sq"].numpy(), d["out_v_" + k])
     np.testing.assert_array_equal(g.denom.numpy(), d["out_denom"])
     np.testing.assert_array_equal(g.max_radii2D.numpy(), d["out_max_radii2D"])
+
+
+def test_chunk_schedule_events_follow_train_single():
+    """gs_train.chunk.ChunkSchedule.events on the default OptimizationParams: densify every 300
+    iterations after 500 and before 15000, a reset every 3000 (each on a densify iteration), none from
+    densify_until_iter on (train_single.py:191-201, arguments/__init__.py:103-107)."""
+    from gs_train.chunk import ChunkSchedule
+    s = ChunkSchedule()
+    ev = {it: s.events(it) for it in range(1, s.iterations + 1)}
+    dens = [it for it, (d, _) in ev.items() if d]
+    resets = [it for it, (_, r) in ev.items() if r]
+    assert dens == list(range(600, 15000, 300))
+    assert resets == [3000, 6000, 9000, 12000]
+    assert set(resets) <= set(dens)
+    w = ChunkSchedule(white_background=True)
+    assert w.events(500) == (False, True)
