@@ -61,6 +61,15 @@ def parse():
                     help="render_hierarchy.py tau in pixels (its default list: 0, 3, 6, 15)")
     ap.add_argument("--c5-log-scale", type=float, default=-6.0,
                     help="mean log leaf scale of the config-5 tree (-6: ~7.4M-node cut of 50M at tau 15)")
+    ap.add_argument("--no-config3", action="store_true",
+                    help="skip the config-3 stand-in (train_single.py's whole loop on a synthetic street chunk)")
+    ap.add_argument("--chunk-iterations", type=int, default=30_000)
+    ap.add_argument("--chunk-size", type=int, default=1536, help="cube-face width = height of the chunk's views")
+    ap.add_argument("--chunk-positions", type=int, default=48, help="camera stations (4 cube faces each)")
+    ap.add_argument("--chunk-truth", type=int, default=1_000_000, help="Gaussians of the synthetic truth street")
+    ap.add_argument("--chunk-init", type=int, default=300_000, help="LiDAR-like initial points")
+    ap.add_argument("--post-leaves", type=int, default=3_000_000,
+                    help="leaves of the train_post step's synthetic hierarchy (0 = skip that step)")
     ap.add_argument("--train-baseline", action="store_true",
                     help="also time the reference-structured torch train step (oracle/train_torch_ref.py: conv2d "
                          "SSIM, OurAdam gather/scatter) -- a baseline leg, like cpu_baseline")
@@ -176,7 +185,8 @@ def psnr_vs_oracle(gpu_color, gpu_invd, st):
     return out
 
 
-def train_step_ms(P, W, H, steps, warmup, dev, street=True, reference=False, seed=0, fovx_deg=60.0, native=True):
+def train_step_ms(P, W, H, steps, warmup, dev, street=True, reference=False, seed=0, fovx_deg=60.0, native=True,
+                  depth_only=False):
     """one train_single.py iteration on the bench scene (1M Gaussians at
     1080p, perturbed), wall time per step between synchronisations (the fused step never syncs).
     street=True: the Street-sparse iteration -- 4 training views cycled, the masked inverse-depth
@@ -185,7 +195,9 @@ def train_step_ms(P, W, H, steps, warmup, dev, street=True, reference=False, see
     view (round 1's number, kept as a labelled variant).  reference=True: the same step in the
     reference's torch formulation (oracle/train_torch_ref.py, a baseline leg).  native=True: the
     step as one gsr_train_step call (gs_train.native_step); False: issued from Python through the
-    autograd API (gs_train.harness.TrainStep) -- the same kernels in the same order."""
+    autograd API (gs_train.harness.TrainStep) -- the same kernels in the same order.  depth_only:
+    every view a depth-only view (train_single.py:145-161: the depth-only loss, no photometric
+    term, no exposure step)."""
     import torch
     from gs_train.harness import make_problem
     step_cls = None
@@ -194,7 +206,7 @@ def train_step_ms(P, W, H, steps, warmup, dev, street=True, reference=False, see
     if reference:
         from train_torch_ref import ReferenceTrainStep as step_cls
     ts = make_problem(P, W, H, n_views=4 if street else 1, seed=seed, step_cls=step_cls, depth=street,
-                      skybox_points=10_000 if street else 0, fovx_deg=fovx_deg)
+                      skybox_points=10_000 if street else 0, fovx_deg=fovx_deg, depth_only=4 if depth_only else 0)
     for _ in range(warmup):
         ts.step()
     torch.cuda.synchronize()
@@ -207,6 +219,112 @@ def train_step_ms(P, W, H, steps, warmup, dev, street=True, reference=False, see
     del ts
     torch.cuda.empty_cache()
     return ms
+
+
+def config3(a, dev):
+    """The config-3 stand-in (BASELINE.json configs[2]: train_single.py's whole loop per chunk; the
+    example_dataset is absent): gs_train.chunk.TrainChunk over a synthetic Street-sparse chunk
+    (street_chunk: cube faces along a street, LiDAR-like initial points, skybox + scaffold rows,
+    depth-only views) with the native step, the default OptimizationParams schedule (densify /
+    prune, opacity resets, SH increments, lr / depth-weight schedules) scaled to --chunk-iterations.
+    Per-iteration device time from HIP events between iterations; the chunk's wall clock from
+    after set-up to the last iteration."""
+    import torch
+    from diff_gaussian_rasterization import _C
+    from gs_train.chunk import ChunkSchedule, TrainChunk, street_chunk
+    from gs_train.native_step import NativeTrainStep
+    n_it = a.chunk_iterations
+    f = n_it / 30_000
+    sched = ChunkSchedule(iterations=n_it)
+    if n_it != 30_000:  # the same schedule compressed in time
+        sched = ChunkSchedule(iterations=n_it, densification_interval=max(1, round(300 * f)),
+                              opacity_reset_interval=max(1, round(3000 * f)), densify_from_iter=round(500 * f),
+                              densify_until_iter=round(15_000 * f), sh_interval=max(1, round(1000 * f)))
+    t_set = time.perf_counter()
+    torch.manual_seed(0)
+    ts, info = street_chunk(NativeTrainStep, W=a.chunk_size, H=a.chunk_size, positions=a.chunk_positions,
+                            n_truth=a.chunk_truth, n_init=a.chunk_init, iterations=n_it, device=dev)
+    torch.cuda.synchronize()
+    setup_s = time.perf_counter() - t_set
+
+    from gs_train.chunk import view_psnr
+    psnr0 = view_psnr(ts)
+    tc = TrainChunk(ts, sched)
+    evs, losses = [], {}
+
+    def cb(it, loss):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        evs.append(e)
+        if it % 1000 == 0 or it == 1:
+            losses[it] = loss
+    r0 = _C.forward_stats()
+    torch.cuda.synchronize()
+    with quiet_gc():
+        start = torch.cuda.Event(enable_timing=True)
+        start.record()
+        t0 = time.perf_counter()
+        tc.run(callback=cb)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+    r1 = _C.forward_stats()
+    per = np.array([start.elapsed_time(evs[0])] + [evs[i].elapsed_time(evs[i + 1]) for i in range(len(evs) - 1)])
+    psnr1 = view_psnr(ts)
+    ev = tc.events
+    out = {"workload": f"train_single.py loop on a synthetic Street-sparse chunk: {info['views']} views "
+                       f"({info['depth_only_views']} depth-only) of {info['W']}x{info['H']} (90 deg cube faces), "
+                       f"{info['P_init']} initial Gaussians (10k skybox + 20k scaffold + LiDAR-like points), "
+                       f"{n_it} iterations with the default schedule" + ("" if n_it == 30_000 else " compressed"),
+           "iterations": n_it, "updates": len(per), "chunk_wall_s": round(wall, 3), "setup_s": round(setup_s, 2),
+           "iteration_ms": {"mean": round(float(per.mean()), 4), "median": round(float(np.median(per)), 4),
+                            "p90": round(float(np.percentile(per, 90)), 4), "max": round(float(per.max()), 3),
+                            "source": "HIP events between iterations"},
+           "P_init": info["P_init"], "P_final": ts.g.P, "P_max": max([e["P_after"] for e in ev] + [info["P_init"]]),
+           "densify_events": sum(1 for e in ev if "total" in e), "opacity_resets": sum(1 for e in ev if e.get("reset")),
+           "event_s": round(tc.event_s, 3), "capacity_reruns": int(r1["reruns"] - r0["reruns"]),
+           "final_sh_degree": ts.g.active_sh_degree,
+           "loss": {str(k): round(float(v), 5) for k, v in sorted(losses.items())},
+           "train_view_psnr_db": {"before": psnr0, "after": psnr1},
+           "P_trace": [[e["iteration"], e["P_after"]] for e in ev][::4],
+           "data": "synthetic street chunk generated on the device (gs_train.chunk.street_chunk); the example_dataset "
+                   "is not available offline"}
+    del ts, tc
+    torch.cuda.empty_cache()
+    return out
+
+
+def train_post_ms(a, dev):
+    """One train_post.py iteration (train_post.py:69-198, gs_train.post.PostTrainStep): a random LOD
+    limit, expand_to_size + get_interpolation_weights, the activation-fused render_post blend,
+    rasterizer fwd+bwd of the cut at the chunk's view size, pretrained exposure, L1 + SSIM on
+    image * alpha, skybox / anchor gradient zeroing, dense Adam -- on a synthetic hierarchy of
+    --post-leaves leaves (~4/3 as many nodes).  Wall time per iteration between synchronisations
+    (the cut length is read by the host every iteration, as in the reference)."""
+    import torch
+    from gs_train.post import synthetic_post_problem
+    W = H = a.chunk_size
+    torch.manual_seed(0)
+    post = synthetic_post_problem(a.post_leaves, W, H, n_views=4, skybox=10_000, n_anchors=10_000, seed=1, device=dev)
+    for _ in range(5):
+        post.step()
+    torch.cuda.synchronize()
+    cuts = []
+    steps = max(10, a.train_steps)
+    with quiet_gc():
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            post.step()
+            cuts.append(post.last_cut)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / steps * 1e3
+    out = {"ms": round(ms, 4), "steps": steps, "nodes": post.m.N, "cut_rows_mean": int(np.mean(cuts)),
+           "cut_rows_max": int(np.max(cuts)), "width": W, "height": H,
+           "workload": "train_post.py iteration on a synthetic hierarchy (Morton-grouped tree, 10k skybox rows last, "
+                       "10k anchors): random LOD limit in [0.005, 0.1], cut + weights, fused blend over raw "
+                       "parameters, rasterizer fwd+bwd, pretrained exposure, L1 + SSIM, locked-row zeroing, dense Adam"}
+    del post
+    torch.cuda.empty_cache()
+    return out
 
 
 def config5(a, dev):
@@ -474,24 +592,127 @@ def quiet_gc():
         gc.unfreeze()
 
 
-def timed(step, steps, warmup, ranks):
+def timed(step, steps, warmup, ranks, per_step=None):
     """W untimed steps, then exactly `steps` steps bracketed by barrier + synchronize on both sides;
-    the MAX over ranks of the elapsed seconds."""
+    the MAX over ranks of the elapsed seconds.  per_step (a list): receives each timed step's device
+    duration in ms -- HIP events recorded on the current stream between consecutive steps (no
+    synchronisation inside the timed region)."""
     import torch
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
     ranks.barrier()
     torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)] if per_step is not None else None
     with quiet_gc():
         t0 = time.perf_counter()
-        for _ in range(steps):
+        if ev is not None:
+            ev[0].record()
+        for i in range(steps):
             step()
+            if ev is not None:
+                ev[i + 1].record()
         torch.cuda.synchronize()
         ranks.barrier()
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
+    if ev is not None:
+        per_step.extend(ev[i].elapsed_time(ev[i + 1]) for i in range(steps))
     return ranks.max(el)
+
+
+def dispersion(ms):
+    """Median / p10 / p90 / min / max of per-step device times (ms): SURVEY.md 8(d) asks for the
+    median; the mean comes from the wall clock."""
+    if not ms:
+        return None
+    a = np.asarray(ms, np.float64)
+    return {"median_ms": round(float(np.median(a)), 5), "p10_ms": round(float(np.percentile(a, 10)), 5),
+            "p90_ms": round(float(np.percentile(a, 90)), 5), "min_ms": round(float(a.min()), 5),
+            "max_ms": round(float(a.max()), 5), "n": int(a.size), "source": "HIP events between consecutive steps"}
+
+
+class ClockProbe:
+    """Shader clock, power and temperature of the bench's GPU (amdsmi GPU metrics; None where the
+    library or the metric is unavailable): the blend kernels are VALU-issue bound, so their times
+    scale with the clock the box runs at, and a line without it cannot be compared with another
+    box's.  read() is one sample; sample_while(fn) samples every ~10 ms on a thread while fn runs
+    (used around untimed steps only)."""
+    KEYS = ("current_gfxclk", "average_gfxclk_frequency", "current_uclk", "current_socket_power",
+            "average_socket_power", "temperature_hotspot", "gfx_activity")
+
+    def __init__(self, dev):
+        self.h = None
+        self.err = None
+        try:
+            import amdsmi
+            import torch
+            amdsmi.amdsmi_init()
+            pr = torch.cuda.get_device_properties(dev)
+            want = (int(pr.pci_domain_id), int(pr.pci_bus_id), int(pr.pci_device_id))
+            for h in amdsmi.amdsmi_get_processor_handles():
+                bdf = amdsmi.amdsmi_get_gpu_device_bdf(h)  # "dddd:bb:dd.f"
+                dom, bus, rest = bdf.split(":")
+                if (int(dom, 16), int(bus, 16), int(rest.split(".")[0], 16)) == want:
+                    self.h = h
+                    break
+            if self.h is None:
+                self.err = "no amdsmi handle with the device's PCI address"
+            self.amdsmi = amdsmi
+        except Exception as e:  # pragma: no cover - depends on the box
+            self.err = f"{type(e).__name__}: {e}"[:160]
+
+    def read(self):
+        if self.h is None:
+            return None
+        try:
+            m = self.amdsmi.amdsmi_get_gpu_metrics_info(self.h)
+        except Exception as e:  # pragma: no cover
+            self.err = f"{type(e).__name__}: {e}"[:160]
+            return None
+        out = {}
+        for k in self.KEYS:
+            v = m.get(k)
+            if isinstance(v, (list, tuple)):  # per-XCD clocks on some parts
+                v = [x for x in v if isinstance(x, (int, float)) and x < 0xFFFF]
+                v = max(v) if v else None
+            if isinstance(v, (int, float)) and v < 0xFFFFFFFF:
+                out[k] = v
+        clks = m.get("current_gfxclks")
+        if isinstance(clks, (list, tuple)):
+            c = [x for x in clks if isinstance(x, (int, float)) and 0 < x < 0xFFFF]
+            if c:
+                out["current_gfxclks_min_max"] = [min(c), max(c)]
+        return out
+
+    def sample_while(self, fn):
+        import threading
+        samples, stop = [], threading.Event()
+
+        def loop():
+            while not stop.is_set():
+                r = self.read()
+                if r:
+                    samples.append(r)
+                stop.wait(0.01)
+        th = threading.Thread(target=loop, daemon=True)
+        if self.h is not None:
+            th.start()
+        try:
+            fn()
+        finally:
+            stop.set()
+            if self.h is not None:
+                th.join()
+        if not samples:
+            return None
+        summ = {"samples": len(samples)}
+        for k in ("current_gfxclk", "current_socket_power", "temperature_hotspot"):
+            v = [x[k] for x in samples if k in x]
+            if v:
+                summ[k + "_median"] = float(np.median(v))
+                summ[k + "_max"] = float(np.max(v))
+        return summ
 
 
 def stage_profile(step, n):
@@ -603,7 +824,7 @@ def main():
         sys.exit(spawn_ranks(a))
     if a.metric_only:
         a.train_steps, a.no_config5, a.no_street, a.no_config4, a.no_cpu_baseline = 0, True, True, True, True
-        a.no_coarse_debug = True
+        a.no_coarse_debug = a.no_config3 = True
     import torch
     import torch.distributed as dist
 
@@ -658,7 +879,18 @@ def main():
         pr.disable()
         pstats.Stats(pr, stream=sys.stderr).sort_stats("cumulative").print_stats(18)
     log("metric: timing")
-    elapsed = timed(step, a.steps, a.warmup, ranks)
+    probe = ClockProbe(dev)
+    per_step = []
+    clk_before = probe.read()
+    elapsed = timed(step, a.steps, a.warmup, ranks, per_step=per_step)
+    clk_after = probe.read()
+
+    # the clock under the bench's load: sampled over ~400 more (untimed) steps
+    def burst():
+        for _ in range(400):
+            step()
+        torch.cuda.synchronize()
+    clk_load = probe.sample_while(burst)
 
     # per-stage device time with HIP events on the rasterizer's stream (separate, untimed steps)
     stages = stage_profile(step, a.profile_steps)
@@ -708,6 +940,9 @@ def main():
                      "frac_rocprof": round(abytes[dom] / (rp_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if rp_ms else None,
                      "kernel_source_sha": kernel_source_sha()},
         "valu_roofline": [r for r in (valu_roofline(k, stages.get(k)) for k in ("render_bwd", "render_fwd")) if r],
+        "step_dispersion": dispersion(per_step),
+        "gpu_clock": {"before": clk_before, "after": clk_after, "under_load": clk_load,
+                      "unit": "MHz / W / C (amdsmi GPU metrics)", "error": probe.err},
         "stages_ms": {k: round(v, 5) for k, v in stages.items()},
         "stage_bytes": {k: int(v) for k, v in abytes.items()},
         # stages on the main stream (sh_color overlaps the sort / binning on a side stream)
@@ -731,6 +966,7 @@ def main():
         tr["binning_reruns"] = r1["reruns"] - r0["reruns"]
         tr["python_driven_ms"] = round(train_step_ms(P, W, H, a.train_steps, 5, dev, seed=rank, native=False), 4)
         tr["photo_only_fixed_view_ms"] = round(train_step_ms(P, W, H, a.train_steps, 5, dev, street=False), 4)
+        tr["depth_only_view_ms"] = round(train_step_ms(P, W, H, a.train_steps, 5, dev, seed=rank, depth_only=True), 4)
         if a.train_baseline:
             tr["reference_structured_ms"] = round(train_step_ms(P, W, H, a.train_steps, 5, dev, reference=True), 4)
         out["train_step"] = tr
@@ -745,6 +981,12 @@ def main():
     if world == 1 and not a.no_coarse_debug:
         log("render_coarse debug mode")
         out["coarse_debug"] = coarse_debug(a, dev)
+    if world == 1 and a.train_steps > 0 and a.post_leaves > 0:
+        log("train_post step")
+        out["train_post_step"] = train_post_ms(a, dev)
+    if world == 1 and not a.no_config3:
+        log("config 3 stand-in: train_single.py loop on a synthetic street chunk")
+        out["config3_proxy"] = config3(a, dev)
     if world == 1 and not a.no_config5:
         log("config 5")
         out["config5"] = config5(a, dev)

@@ -43,6 +43,36 @@ int gsr_interpolate_cut_backward(int64_t N, int M, int64_t R, int64_t S, const i
                                  const float *dL_dout_shs, float *dL_dmeans3D, float *dL_dscales,
                                  float *dL_drotations, float *dL_dopacities, float *dL_dshs, void *stream);
 
+/* The same blend over the PRE-activation parameters (ABI 3): scales are log-scales (exp applied),
+ * rotations unnormalised quaternions (F.normalize applied before the dot test and the lerp) and
+ * opacities the stored values with opacity_act applied -- the getters of
+ * scene/gaussian_model.py:39-47,125-156 evaluated only on the rows the cut reads (train_post.py's
+ * model: create_from_hier sets opacity_activation = torch.abs, :411-412).  The backward
+ * accumulates the gradients of the raw parameters (activation derivatives chained per gathered
+ * row); it reads the raw scales, rotations and opacities.  Means and SH have no activation. */
+#define GSR_OPACITY_IDENTITY 0
+#define GSR_OPACITY_SIGMOID 1
+#define GSR_OPACITY_ABS 2
+int gsr_interpolate_cut_forward_act(int64_t N, int M, int64_t R, int64_t S, const int *render_indices,
+                                    const int *parent_indices, const float *interpolation_weights,
+                                    const float *means3D, const float *scaling_raw, const float *rotation_raw,
+                                    const float *opacity_raw, const float *shs, int opacity_act, float *out_means3D,
+                                    float *out_scales, float *out_rotations, float *out_opacities, float *out_shs,
+                                    void *stream);
+int gsr_interpolate_cut_backward_act(int64_t N, int M, int64_t R, int64_t S, const int *render_indices,
+                                     const int *parent_indices, const float *interpolation_weights,
+                                     const float *scaling_raw, const float *rotation_raw, const float *opacity_raw,
+                                     int opacity_act, const float *dL_dout_means3D, const float *dL_dout_scales,
+                                     const float *dL_dout_rotations, const float *dL_dout_opacities,
+                                     const float *dL_dout_shs, float *dL_dmeans3D, float *dL_dscaling_raw,
+                                     float *dL_drotation_raw, float *dL_dopacity_raw, float *dL_dshs, void *stream);
+
+/* Zero the gradient rows train_post.py:167-181 locks: the last `tail` rows (the skybox) and the
+ * rows listed in `rows` (the anchors, int64, may repeat), in each of n arrays of widths[k] floats
+ * per row over N rows.  One launch. */
+int gsr_zero_grad_rows(int n, float *const *grads, const int64_t *widths, int64_t N, int64_t tail,
+                       const int64_t *rows, int64_t n_rows, void *stream);
+
 /* ---- LOD cut (csrc/lod.hip) ------------------------------------------------------------
  * Replace gaussian_hierarchy._C.expand_to_size / get_interpolation_weights (the gaussianhierarchy
  * extension, un-vendored; called at render_hierarchy.py:63-85, train_post.py:91-113,

@@ -308,3 +308,92 @@ def __getattr__(name):
     if name == "ReferenceTrainStep":
         return _reference_step_cls()
     raise AttributeError(name)
+
+
+# ---- one train_post.py iteration in the reference's formulation (the checker of gs_train.post) -----
+class ReferencePostStep:
+    """train_post.py:69-198 with the reference's torch pieces: the getters (exp, F.normalize,
+    torch.abs -- scene/gaussian_model.py:411-412), render_post's Python gather
+    (gaussian_renderer/__init__.py:200-243, interp_python=True), the matmul exposure + clamp
+    (:280-286), conv2d SSIM on image * alpha (:134-140), the skybox / anchor gradient zeroing by
+    indexing (:167-181) and torch.optim.Adam (training_setup(our_adam=False)) over split f_dc /
+    f_rest parameters.  Built from a gs_train.post.PostTrainStep (same views, model copy); the cut
+    (expand_to_size / get_interpolation_weights) is the product's, as both run it the same way."""
+
+    def __init__(self, post):
+        from gs_train.post import POST_LR
+        m = post.m
+        self.post = post
+        P = lambda t: torch.nn.Parameter(t.detach().clone().contiguous())
+        self._xyz, self._opacity, self._scaling, self._rotation = P(m._xyz), P(m._opacity), P(m._scaling), P(m._rotation)
+        self._features_dc = P(m._features[:, :1])
+        self._features_rest = P(m._features[:, 1:])
+        lr = POST_LR
+        s = m.spatial_lr_scale
+        self.optimizer = torch.optim.Adam(
+            [{"params": [self._xyz], "lr": lr["position_lr_init"] * s, "name": "xyz"},
+             {"params": [self._features_dc], "lr": lr["feature_lr"], "name": "f_dc"},
+             {"params": [self._features_rest], "lr": lr["feature_lr"] / 20.0, "name": "f_rest"},
+             {"params": [self._opacity], "lr": lr["opacity_lr"], "name": "opacity"},
+             {"params": [self._scaling], "lr": lr["scaling_lr"], "name": "scaling"},
+             {"params": [self._rotation], "lr": lr["rotation_lr"], "name": "rotation"}], lr=0.0, eps=1e-15)
+        self.iteration = 1
+
+    def features(self):
+        return torch.cat((self._features_dc, self._features_rest), 1)
+
+    def step(self, k, limit):
+        from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+        post, m = self.post, self.post.m
+        for pg in self.optimizer.param_groups:
+            if pg["name"] == "xyz":
+                pg["lr"] = post.xyz_lr(self.iteration)
+        n = post.cut(k, limit)
+        c = post.cams[k]
+        means3D, opacity = self._xyz, torch.abs(self._opacity)
+        scales, rotations = torch.exp(self._scaling), F.normalize(self._rotation)
+        shs = self.features()
+        render_inds = post.ri[:n].long()
+        t = post.w[:n].unsqueeze(1)
+        ti = (1 - post.w[:n]).unsqueeze(1)
+        pinds = post.pi[:n].long()
+        m3 = (t * means3D[render_inds] + ti * means3D[pinds]).contiguous()
+        sc = (t * scales[render_inds] + ti * scales[pinds]).contiguous()
+        sh = (t.unsqueeze(2) * shs[render_inds] + ti.unsqueeze(2) * shs[pinds]).contiguous()
+        parents = rotations[pinds]
+        rots = rotations[render_inds]
+        dots = torch.bmm(rots.unsqueeze(1), parents.unsqueeze(2)).flatten()
+        parents[dots < 0] *= -1
+        rot = ((t * rots) + ti * parents).contiguous()
+        op = (t * opacity[render_inds] + ti * opacity[pinds]).contiguous()
+        S = m.skybox_points
+        sk = torch.arange(means3D.shape[0] - S, means3D.shape[0], device=means3D.device)
+        m3, sh, op = torch.cat((m3, means3D[sk])), torch.cat((sh, shs[sk])), torch.cat((op, opacity[sk]))
+        rot, sc = torch.cat((rot, rotations[sk])), torch.cat((sc, scales[sk]))
+        rs = GaussianRasterizationSettings(
+            image_height=post.H, image_width=post.W, tanfovx=c["tx"], tanfovy=c["ty"], bg=post.bg, scale_modifier=1.0,
+            viewmatrix=c["view"], projmatrix=c["proj"], sh_degree=m.active_sh_degree, campos=c["campos"],
+            prefiltered=False, debug=False, do_depth=False, render_indices=post.empty_i, parent_indices=post.empty_i,
+            interpolation_weights=post.empty_f, num_node_kids=post.empty_id)
+        means2D = torch.zeros_like(m3, requires_grad=True) + 0
+        image, _, _ = GaussianRasterizer(rs)(means3D=m3, means2D=means2D, shs=sh, colors_precomp=None, opacities=op,
+                                             scales=sc, rotations=rot, cov3D_precomp=None)
+        E = post.expo[k]
+        if E is not None:
+            image = torch.matmul(image.permute(1, 2, 0), E[:3, :3]).permute(2, 0, 1) + E[:3, 3, None, None]
+        image = image.clamp(0, 1)
+        am = post.amask[k]
+        img = image * am if am is not None else image
+        loss = photo_loss(img, post.gts[k], post.lambda_dssim)
+        loss.backward()
+        with torch.no_grad():
+            params = (self._xyz, self._rotation, self._features_dc, self._features_rest, self._opacity, self._scaling)
+            if S:
+                for p in params:
+                    p.grad[-S:] = 0
+            for p in params:
+                p.grad[m.anchors] = 0
+            self.optimizer.step()
+            self.optimizer.zero_grad(set_to_none=True)
+        self.iteration += 1
+        return loss.detach()

@@ -40,6 +40,35 @@ __device__ __forceinline__ CutRow cut_row(int64_t r, int64_t N, int64_t R, int64
 
 __device__ __forceinline__ float lerp_w(float t, float a, float b) { return t * a + (1.f - t) * b; }
 
+// act (gsr_interpolate_cut_forward_act): the inputs are the pre-activation parameters and the
+// getters of scene/gaussian_model.py:39-47 are applied to the rows the cut reads -- exp of the
+// log-scales, normalize of the quaternions, the opacity activation (GSR_OPACITY_SIGMOID, or
+// GSR_OPACITY_ABS: the hierarchy model's torch.abs, :411-412) -- so no N-row activated copy is
+// written and re-read; the backward chains the activation derivatives into the scatter.
+__device__ __forceinline__ float act_opac(int act, float o) {
+    return act == GSR_OPACITY_ABS ? fabsf(o) : act == GSR_OPACITY_SIGMOID ? act_opacity(o) : o;
+}
+__device__ __forceinline__ float act_opac_grad(int act, float o, float g) {
+    if (act == GSR_OPACITY_ABS) return o > 0.f ? g : (o < 0.f ? -g : 0.f);  // torch: g * sgn(o)
+    if (act == GSR_OPACITY_SIGMOID) {
+        const float y = act_opacity(o);
+        return g * (1.f - y) * y;
+    }
+    return g;
+}
+// F.normalize's backward at the raw quaternion x for the upstream g (activate_bwd_kernel's form)
+__device__ __forceinline__ float4 normalize_grad(float4 x, float4 g) {
+    const float n = sqrtf(x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w);
+    const float d = fmaxf(n, 1e-12f);
+    const float gd = -(g.x * ((x.x / d) / d) + g.y * ((x.y / d) / d) + g.z * ((x.z / d) / d) + g.w * ((x.w / d) / d));
+    const float gn = n >= 1e-12f && n != 0.f ? gd / n : 0.f;
+    return make_float4(g.x / d + x.x * gn, g.y / d + x.y * gn, g.z / d + x.z * gn, g.w / d + x.w * gn);
+}
+__device__ __forceinline__ float4 ld_rot(const float *rots, int64_t i, int act) {
+    const float4 q = reinterpret_cast<const float4 *>(rots)[i];
+    return act ? act_rot(q) : q;
+}
+
 // Thread per output row for the 14 scalar fields.  The 192-B SH rows (M = 16, 16-B aligned) are
 // moved by the wave as a whole: 16 lanes per row (12 active, one float4 each), four rows per
 // instruction, so every load reads whole contiguous rows instead of one float4 from each of 64
@@ -50,30 +79,31 @@ __global__ __launch_bounds__(256) void cut_fwd_kernel(int64_t N, int M, int64_t 
                                                       const float *__restrict__ opac, const float *__restrict__ shs,
                                                       float *__restrict__ om, float *__restrict__ os,
                                                       float *__restrict__ orot, float *__restrict__ oop,
-                                                      float *__restrict__ osh, bool vec) {
+                                                      float *__restrict__ osh, bool vec, int act) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t rows = R + S;
     const bool valid = r < rows;
+    const auto sc = [&](int64_t i) { return act ? act_scale(scales[i]) : scales[i]; };
     CutRow q{0, 0, 1.f, true};
     if (valid) q = cut_row(r, N, R, S, ri, pi, w);
     const float t = q.t;
     if (valid) {
         if (q.copy) {
             for (int k = 0; k < 3; k++) om[3 * r + k] = means[3 * q.c + k];
-            for (int k = 0; k < 3; k++) os[3 * r + k] = scales[3 * q.c + k];
-            for (int k = 0; k < 4; k++) orot[4 * r + k] = rots[4 * q.c + k];
-            oop[r] = opac[q.c];
+            for (int k = 0; k < 3; k++) os[3 * r + k] = sc(3 * q.c + k);
+            reinterpret_cast<float4 *>(orot)[r] = ld_rot(rots, q.c, act);
+            oop[r] = act_opac(act, opac[q.c]);
         } else {
             for (int k = 0; k < 3; k++) om[3 * r + k] = lerp_w(t, means[3 * q.c + k], means[3 * q.p + k]);
-            for (int k = 0; k < 3; k++) os[3 * r + k] = lerp_w(t, scales[3 * q.c + k], scales[3 * q.p + k]);
-            const float4 qc = reinterpret_cast<const float4 *>(rots)[q.c];
-            float4 qp = reinterpret_cast<const float4 *>(rots)[q.p];
+            for (int k = 0; k < 3; k++) os[3 * r + k] = lerp_w(t, sc(3 * q.c + k), sc(3 * q.p + k));
+            const float4 qc = ld_rot(rots, q.c, act);
+            float4 qp = ld_rot(rots, q.p, act);
             // torch.bmm(rots (1x4), parents (4x1)): the dot in float, left to right
             const float dot = qc.x * qp.x + qc.y * qp.y + qc.z * qp.z + qc.w * qp.w;
             if (dot < 0.f) qp = make_float4(-qp.x, -qp.y, -qp.z, -qp.w);
             reinterpret_cast<float4 *>(orot)[r] = make_float4(lerp_w(t, qc.x, qp.x), lerp_w(t, qc.y, qp.y),
                                                               lerp_w(t, qc.z, qp.z), lerp_w(t, qc.w, qp.w));
-            oop[r] = lerp_w(t, opac[q.c], opac[q.p]);
+            oop[r] = lerp_w(t, act_opac(act, opac[q.c]), act_opac(act, opac[q.p]));
         }
     }
     if (vec) {
@@ -113,16 +143,28 @@ __global__ __launch_bounds__(256) void cut_bwd_kernel(int64_t N, int M, int64_t 
                                                       const float *__restrict__ gm, const float *__restrict__ gs,
                                                       const float *__restrict__ grot, const float *__restrict__ gop,
                                                       const float *__restrict__ gsh, float *dm, float *ds, float *drot,
-                                                      float *dop, float *dsh, bool vec) {
+                                                      float *dop, float *dsh, bool vec, int act,
+                                                      const float *__restrict__ s_raw,
+                                                      const float *__restrict__ o_raw) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= R + S) return;
     const CutRow q = cut_row(r, N, R, S, ri, pi, w);
     const float t = q.t, u = 1.f - q.t;
+    // d(act(x))/dx times the upstream, per input row (act == 0: the identity)
+    const auto dsc = [&](int64_t i, float g) { return act ? g * act_scale(s_raw[i]) : g; };
+    const auto add_rot = [&](int64_t row, float4 g) {
+        if (act) g = normalize_grad(reinterpret_cast<const float4 *>(rots)[row], g);
+        atomicAdd(&drot[4 * row + 0], g.x);
+        atomicAdd(&drot[4 * row + 1], g.y);
+        atomicAdd(&drot[4 * row + 2], g.z);
+        atomicAdd(&drot[4 * row + 3], g.w);
+    };
+    const float4 gr = make_float4(grot[4 * r + 0], grot[4 * r + 1], grot[4 * r + 2], grot[4 * r + 3]);
     if (q.copy) {
         for (int k = 0; k < 3; k++) atomicAdd(&dm[3 * q.c + k], gm[3 * r + k]);
-        for (int k = 0; k < 3; k++) atomicAdd(&ds[3 * q.c + k], gs[3 * r + k]);
-        for (int k = 0; k < 4; k++) atomicAdd(&drot[4 * q.c + k], grot[4 * r + k]);
-        atomicAdd(&dop[q.c], gop[r]);
+        for (int k = 0; k < 3; k++) atomicAdd(&ds[3 * q.c + k], dsc(3 * q.c + k, gs[3 * r + k]));
+        add_rot(q.c, gr);
+        atomicAdd(&dop[q.c], act_opac_grad(act, act ? o_raw[q.c] : 0.f, gop[r]));
         if (!vec)
             for (int k = 0; k < 3 * M; k++) atomicAdd(&dsh[(size_t)q.c * 3 * M + k], gsh[(size_t)r * 3 * M + k]);
         return;
@@ -130,19 +172,17 @@ __global__ __launch_bounds__(256) void cut_bwd_kernel(int64_t N, int M, int64_t 
     for (int k = 0; k < 3; k++) {
         atomicAdd(&dm[3 * q.c + k], t * gm[3 * r + k]);
         atomicAdd(&dm[3 * q.p + k], u * gm[3 * r + k]);
-        atomicAdd(&ds[3 * q.c + k], t * gs[3 * r + k]);
-        atomicAdd(&ds[3 * q.p + k], u * gs[3 * r + k]);
+        atomicAdd(&ds[3 * q.c + k], dsc(3 * q.c + k, t * gs[3 * r + k]));
+        atomicAdd(&ds[3 * q.p + k], dsc(3 * q.p + k, u * gs[3 * r + k]));
     }
-    const float4 qc = reinterpret_cast<const float4 *>(rots)[q.c];
-    const float4 qp = reinterpret_cast<const float4 *>(rots)[q.p];
+    const float4 qc = ld_rot(rots, q.c, act);
+    const float4 qp = ld_rot(rots, q.p, act);
     const float dot = qc.x * qp.x + qc.y * qp.y + qc.z * qp.z + qc.w * qp.w;
     const float sgn = dot < 0.f ? -1.f : 1.f;
-    for (int k = 0; k < 4; k++) {
-        atomicAdd(&drot[4 * q.c + k], t * grot[4 * r + k]);
-        atomicAdd(&drot[4 * q.p + k], sgn * u * grot[4 * r + k]);
-    }
-    atomicAdd(&dop[q.c], t * gop[r]);
-    atomicAdd(&dop[q.p], u * gop[r]);
+    add_rot(q.c, make_float4(t * gr.x, t * gr.y, t * gr.z, t * gr.w));
+    add_rot(q.p, make_float4(sgn * u * gr.x, sgn * u * gr.y, sgn * u * gr.z, sgn * u * gr.w));
+    atomicAdd(&dop[q.c], act_opac_grad(act, act ? o_raw[q.c] : 0.f, t * gop[r]));
+    atomicAdd(&dop[q.p], act_opac_grad(act, act ? o_raw[q.p] : 0.f, u * gop[r]));
     if (vec) return;
     for (int k = 0; k < 3 * M; k++) {
         const float g = gsh[(size_t)r * 3 * M + k];
@@ -186,21 +226,24 @@ __global__ __launch_bounds__(256) void cut_bwd_sh_kernel(int64_t N, int64_t R, i
 
 using namespace gsr;
 
-extern "C" {
+namespace {
 
-int gsr_interpolate_cut_forward(int64_t N, int M, int64_t R, int64_t S, const int *render_indices,
-                                const int *parent_indices, const float *interpolation_weights, const float *means3D,
-                                const float *scales, const float *rotations, const float *opacities, const float *shs,
-                                float *out_means3D, float *out_scales, float *out_rotations, float *out_opacities,
-                                float *out_shs, void *stream) {
-    if (N < 0 || R < 0 || S < 0 || S > N || M <= 0 || M > 16) {
-        set_last_error("gsr_interpolate_cut_forward: bad sizes (need 0 <= S <= N, 1 <= M <= 16)");
+int cut_forward(int64_t N, int M, int64_t R, int64_t S, const int *render_indices, const int *parent_indices,
+                const float *interpolation_weights, const float *means3D, const float *scales, const float *rotations,
+                const float *opacities, const float *shs, int act, float *out_means3D, float *out_scales,
+                float *out_rotations, float *out_opacities, float *out_shs, void *stream, const char *who) {
+    if (N < 0 || R < 0 || S < 0 || S > N || M <= 0 || M > 16 || act < 0 || act > GSR_OPACITY_ABS) {
+        set_last_error(std::string(who) + ": bad sizes or activation (need 0 <= S <= N, 1 <= M <= 16)");
         return GSR_ERR_INVALID_ARGUMENT;
     }
     if (R + S == 0) return GSR_OK;
     if (!means3D || !scales || !rotations || !opacities || !shs || !out_means3D || !out_scales || !out_rotations ||
         !out_opacities || !out_shs || (R > 0 && (!render_indices || !parent_indices || !interpolation_weights))) {
-        set_last_error("gsr_interpolate_cut_forward: NULL pointer");
+        set_last_error(std::string(who) + ": NULL pointer");
+        return GSR_ERR_INVALID_ARGUMENT;
+    }
+    if ((reinterpret_cast<uintptr_t>(rotations) | reinterpret_cast<uintptr_t>(out_rotations)) % 16 != 0) {
+        set_last_error(std::string(who) + ": rotations must be 16-byte aligned");
         return GSR_ERR_INVALID_ARGUMENT;
     }
     const bool vec = M == 16 && reinterpret_cast<uintptr_t>(shs) % 16 == 0 && reinterpret_cast<uintptr_t>(out_shs) % 16 == 0;
@@ -208,30 +251,33 @@ int gsr_interpolate_cut_forward(int64_t N, int M, int64_t R, int64_t S, const in
     hipLaunchKernelGGL(cut_fwd_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0,
                        static_cast<hipStream_t>(stream), N, M, R, S, render_indices, parent_indices,
                        interpolation_weights, means3D, scales, rotations, opacities, shs, out_means3D, out_scales,
-                       out_rotations, out_opacities, out_shs, vec);
+                       out_rotations, out_opacities, out_shs, vec, act);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
-        set_last_error(std::string("gsr_interpolate_cut_forward: ") + hipGetErrorString(e));
+        set_last_error(std::string(who) + ": " + hipGetErrorString(e));
         return GSR_ERR_DEVICE;
     }
     return GSR_OK;
 }
 
-int gsr_interpolate_cut_backward(int64_t N, int M, int64_t R, int64_t S, const int *render_indices,
-                                 const int *parent_indices, const float *interpolation_weights,
-                                 const float *rotations, const float *dL_dout_means3D, const float *dL_dout_scales,
-                                 const float *dL_dout_rotations, const float *dL_dout_opacities,
-                                 const float *dL_dout_shs, float *dL_dmeans3D, float *dL_dscales,
-                                 float *dL_drotations, float *dL_dopacities, float *dL_dshs, void *stream) {
-    if (N < 0 || R < 0 || S < 0 || S > N || M <= 0 || M > 16) {
-        set_last_error("gsr_interpolate_cut_backward: bad sizes (need 0 <= S <= N, 1 <= M <= 16)");
+int cut_backward(int64_t N, int M, int64_t R, int64_t S, const int *render_indices, const int *parent_indices,
+                 const float *interpolation_weights, const float *s_raw, const float *rotations, const float *o_raw,
+                 int act, const float *dL_dout_means3D, const float *dL_dout_scales, const float *dL_dout_rotations,
+                 const float *dL_dout_opacities, const float *dL_dout_shs, float *dL_dmeans3D, float *dL_dscales,
+                 float *dL_drotations, float *dL_dopacities, float *dL_dshs, void *stream, const char *who) {
+    if (N < 0 || R < 0 || S < 0 || S > N || M <= 0 || M > 16 || act < 0 || act > GSR_OPACITY_ABS) {
+        set_last_error(std::string(who) + ": bad sizes or activation (need 0 <= S <= N, 1 <= M <= 16)");
         return GSR_ERR_INVALID_ARGUMENT;
     }
     if (R + S == 0) return GSR_OK;
     if (!rotations || !dL_dout_means3D || !dL_dout_scales || !dL_dout_rotations || !dL_dout_opacities ||
         !dL_dout_shs || !dL_dmeans3D || !dL_dscales || !dL_drotations || !dL_dopacities || !dL_dshs ||
-        (R > 0 && (!render_indices || !parent_indices || !interpolation_weights))) {
-        set_last_error("gsr_interpolate_cut_backward: NULL pointer");
+        (act && (!s_raw || !o_raw)) || (R > 0 && (!render_indices || !parent_indices || !interpolation_weights))) {
+        set_last_error(std::string(who) + ": NULL pointer");
+        return GSR_ERR_INVALID_ARGUMENT;
+    }
+    if (reinterpret_cast<uintptr_t>(rotations) % 16 != 0) {
+        set_last_error(std::string(who) + ": rotations must be 16-byte aligned");
         return GSR_ERR_INVALID_ARGUMENT;
     }
     const int64_t rows = R + S;
@@ -240,14 +286,120 @@ int gsr_interpolate_cut_backward(int64_t N, int M, int64_t R, int64_t S, const i
                        static_cast<hipStream_t>(stream), N, M, R, S, render_indices, parent_indices,
                        interpolation_weights, rotations, dL_dout_means3D, dL_dout_scales, dL_dout_rotations,
                        dL_dout_opacities, dL_dout_shs, dL_dmeans3D, dL_dscales, dL_drotations, dL_dopacities,
-                       dL_dshs, vec);
+                       dL_dshs, vec, act, s_raw, o_raw);
     if (vec)
         hipLaunchKernelGGL(cut_bwd_sh_kernel, dim3((unsigned)((16 * rows + 255) / 256)), dim3(256), 0,
                            static_cast<hipStream_t>(stream), N, R, S, render_indices, parent_indices,
                            interpolation_weights, dL_dout_shs, dL_dshs);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
-        set_last_error(std::string("gsr_interpolate_cut_backward: ") + hipGetErrorString(e));
+        set_last_error(std::string(who) + ": " + hipGetErrorString(e));
+        return GSR_ERR_DEVICE;
+    }
+    return GSR_OK;
+}
+
+constexpr int kZeroMax = 8;
+struct ZeroArrays {
+    float *p[kZeroMax];
+    int64_t w[kZeroMax];
+};
+
+// one thread per (locked row, array): the last `tail` rows, then the listed rows
+__global__ __launch_bounds__(256) void zero_rows_kernel(ZeroArrays z, int n, int64_t N, int64_t tail,
+                                                        const int64_t *__restrict__ rows, int64_t n_rows) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int k = (int)blockIdx.y;
+    if (i >= tail + n_rows || k >= n) return;
+    const int64_t row = i < tail ? N - tail + i : rows[i - tail];
+    if (row < 0 || row >= N) return;
+    float *d = z.p[k] + row * z.w[k];
+    for (int64_t c = 0; c < z.w[k]; c++) d[c] = 0.f;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gsr_interpolate_cut_forward(int64_t N, int M, int64_t R, int64_t S, const int *render_indices,
+                                const int *parent_indices, const float *interpolation_weights, const float *means3D,
+                                const float *scales, const float *rotations, const float *opacities, const float *shs,
+                                float *out_means3D, float *out_scales, float *out_rotations, float *out_opacities,
+                                float *out_shs, void *stream) {
+    return cut_forward(N, M, R, S, render_indices, parent_indices, interpolation_weights, means3D, scales, rotations,
+                       opacities, shs, 0, out_means3D, out_scales, out_rotations, out_opacities, out_shs, stream,
+                       "gsr_interpolate_cut_forward");
+}
+
+int gsr_interpolate_cut_forward_act(int64_t N, int M, int64_t R, int64_t S, const int *render_indices,
+                                    const int *parent_indices, const float *interpolation_weights,
+                                    const float *means3D, const float *scaling_raw, const float *rotation_raw,
+                                    const float *opacity_raw, const float *shs, int opacity_act, float *out_means3D,
+                                    float *out_scales, float *out_rotations, float *out_opacities, float *out_shs,
+                                    void *stream) {
+    // act 0 is reserved for the activated inputs: the raw form always activates scales / rotations
+    const int act = opacity_act == GSR_OPACITY_IDENTITY ? -1 : opacity_act;
+    if (act < 0) {
+        set_last_error("gsr_interpolate_cut_forward_act: opacity_act must be GSR_OPACITY_SIGMOID or GSR_OPACITY_ABS");
+        return GSR_ERR_INVALID_ARGUMENT;
+    }
+    return cut_forward(N, M, R, S, render_indices, parent_indices, interpolation_weights, means3D, scaling_raw,
+                       rotation_raw, opacity_raw, shs, act, out_means3D, out_scales, out_rotations, out_opacities,
+                       out_shs, stream, "gsr_interpolate_cut_forward_act");
+}
+
+int gsr_interpolate_cut_backward(int64_t N, int M, int64_t R, int64_t S, const int *render_indices,
+                                 const int *parent_indices, const float *interpolation_weights,
+                                 const float *rotations, const float *dL_dout_means3D, const float *dL_dout_scales,
+                                 const float *dL_dout_rotations, const float *dL_dout_opacities,
+                                 const float *dL_dout_shs, float *dL_dmeans3D, float *dL_dscales,
+                                 float *dL_drotations, float *dL_dopacities, float *dL_dshs, void *stream) {
+    return cut_backward(N, M, R, S, render_indices, parent_indices, interpolation_weights, nullptr, rotations,
+                        nullptr, 0, dL_dout_means3D, dL_dout_scales, dL_dout_rotations, dL_dout_opacities, dL_dout_shs,
+                        dL_dmeans3D, dL_dscales, dL_drotations, dL_dopacities, dL_dshs, stream,
+                        "gsr_interpolate_cut_backward");
+}
+
+int gsr_interpolate_cut_backward_act(int64_t N, int M, int64_t R, int64_t S, const int *render_indices,
+                                     const int *parent_indices, const float *interpolation_weights,
+                                     const float *scaling_raw, const float *rotation_raw, const float *opacity_raw,
+                                     int opacity_act, const float *dL_dout_means3D, const float *dL_dout_scales,
+                                     const float *dL_dout_rotations, const float *dL_dout_opacities,
+                                     const float *dL_dout_shs, float *dL_dmeans3D, float *dL_dscaling_raw,
+                                     float *dL_drotation_raw, float *dL_dopacity_raw, float *dL_dshs, void *stream) {
+    if (opacity_act != GSR_OPACITY_SIGMOID && opacity_act != GSR_OPACITY_ABS) {
+        set_last_error("gsr_interpolate_cut_backward_act: opacity_act must be GSR_OPACITY_SIGMOID or GSR_OPACITY_ABS");
+        return GSR_ERR_INVALID_ARGUMENT;
+    }
+    return cut_backward(N, M, R, S, render_indices, parent_indices, interpolation_weights, scaling_raw, rotation_raw,
+                        opacity_raw, opacity_act, dL_dout_means3D, dL_dout_scales, dL_dout_rotations,
+                        dL_dout_opacities, dL_dout_shs, dL_dmeans3D, dL_dscaling_raw, dL_drotation_raw,
+                        dL_dopacity_raw, dL_dshs, stream, "gsr_interpolate_cut_backward_act");
+}
+
+int gsr_zero_grad_rows(int n, float *const *grads, const int64_t *widths, int64_t N, int64_t tail,
+                       const int64_t *rows, int64_t n_rows, void *stream) {
+    if (n < 0 || n > kZeroMax || N < 0 || tail < 0 || tail > N || n_rows < 0 || (n > 0 && (!grads || !widths)) ||
+        (n_rows > 0 && !rows)) {
+        set_last_error("gsr_zero_grad_rows: bad sizes or NULL pointer (at most 8 arrays)");
+        return GSR_ERR_INVALID_ARGUMENT;
+    }
+    ZeroArrays z{};
+    for (int k = 0; k < n; k++) {
+        if (!grads[k] || widths[k] <= 0) {
+            set_last_error("gsr_zero_grad_rows: NULL array or non-positive width");
+            return GSR_ERR_INVALID_ARGUMENT;
+        }
+        z.p[k] = grads[k];
+        z.w[k] = widths[k];
+    }
+    const int64_t m = tail + n_rows;
+    if (m == 0 || n == 0) return GSR_OK;
+    hipLaunchKernelGGL(zero_rows_kernel, dim3((unsigned)((m + 255) / 256), (unsigned)n), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), z, n, N, tail, rows, n_rows);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_last_error(std::string("gsr_zero_grad_rows: ") + hipGetErrorString(e));
         return GSR_ERR_DEVICE;
     }
     return GSR_OK;

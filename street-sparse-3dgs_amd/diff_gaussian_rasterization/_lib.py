@@ -115,6 +115,11 @@ SIGNATURES = {
     "gsr_knn_mean_dist2": (_i, [_i64, _vp, _vp, _vp, _vp]),
     "gsr_interpolate_cut_backward": (_i, [_i64, _i, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                           _vp, _vp, _vp, _vp, _vp]),
+    "gsr_interpolate_cut_forward_act": (_i, [_i64, _i, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp,
+                                             _vp, _vp, _vp, _vp, _vp]),
+    "gsr_interpolate_cut_backward_act": (_i, [_i64, _i, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp,
+                                              _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gsr_zero_grad_rows": (_i, [_i, ctypes.POINTER(_vp), ctypes.POINTER(_i64), _i64, _i64, _vp, _i64, _vp]),
 }
 
 ABI_VERSION = 3

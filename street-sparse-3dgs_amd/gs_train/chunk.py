@@ -368,3 +368,23 @@ def street_chunk(step_cls=None, W=1536, H=1536, positions=48, faces=4, depth_onl
     info = dict(views=n, depth_only_views=int(sum(donly)), P_init=model.P, extent=extent, W=W, H=H,
                 truth=int(truth["means3D"].shape[0]))
     return ts, info
+
+
+@torch.no_grad()
+def view_psnr(ts, n=8):
+    """Mean PSNR (dB, peak 1) of the step's current model against the targets of its first `n`
+    photometric views: render with the view's exposure and a black background (the targets were
+    rendered over black), alpha mask applied as in the loss."""
+    out = []
+    dev = ts.g._xyz.device
+    for k in range(len(ts.cams)):
+        if ts.depth_only[k]:
+            continue
+        img, _, _, _ = ts.render(k, torch.zeros(3, device=dev))
+        if ts.amask[k] is not None:
+            img = img * ts.amask[k]
+        mse = torch.mean((img - ts.gts[k]) ** 2).item()
+        out.append(10 * math.log10(1.0 / mse) if mse > 0 else float("inf"))
+        if len(out) == n:
+            break
+    return round(float(np.mean(out)), 3) if out else None
