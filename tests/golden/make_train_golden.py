@@ -8,6 +8,11 @@
                  rates of scene/gaussian_model.py:286-296: two sparse steps (relevant = rows with
                  nonzero opacity grad, train_single.py:224-230) then one step with no relevant
                  row (the _single_tensor_adam2 dense branch)
+  adam_coarse.npz  the same optimizer as train_coarse.py:131-134 drives it: relevant =
+                 (opacity.grad != 0).nonzero() of the (P, 1) gradient, an (R, 2) index whose second
+                 column is all 0, so OurAdam's gather / scatter (scene/OurAdam.py:267-270,334-337)
+                 also updates row 0; the coarse model's degree-1 SH (f_rest (P, 3, 3)); row 0 kept
+                 irrelevant so the quirk shows
   lr.npz         utils/general_utils.py:31-70 get_expon_lr_func with the xyz and exposure
                  schedules of scene/gaussian_model.py:301-305 (arguments/__init__.py:89-100)
   densify.npz    scene/gaussian_model.py:780-793 add_densification_stats + the max_radii2D update
@@ -97,6 +102,36 @@ def make_adam(ref):
             out[f"v{step}_{n}"] = st["exp_avg_sq"].numpy().copy()
     out["lrs"] = np.array([LRS[n] for n in SHAPES], np.float64)
     np.savez_compressed(os.path.join(OUT, "adam.npz"), **out)
+
+
+def make_adam_coarse(ref):
+    our_adam = load_by_path("ref_our_adam_coarse", os.path.join(ref, "scene", "OurAdam.py"))
+    g = torch.Generator().manual_seed(12)
+    P = 40
+    shapes = dict(SHAPES, f_rest=(3, 3))
+    params = {n: torch.nn.Parameter(torch.randn((P,) + s, generator=g)) for n, s in shapes.items()}
+    groups = [{"params": [params[n]], "lr": LRS[n], "name": n} for n in shapes]
+    opt = our_adam.Adam(groups, lr=0.0, eps=1e-15)
+    out = {f"init_{n}": p.detach().numpy().copy() for n, p in params.items()}
+    for step in range(2):
+        grads = {n: torch.randn((P,) + s, generator=g) for n, s in shapes.items()}
+        mask = torch.rand(P, generator=g) < 0.5
+        mask[0] = False
+        grads["opacity"][~mask] = 0.0
+        for n, p in params.items():
+            p.grad = grads[n].clone()
+            out[f"grad{step}_{n}"] = grads[n].numpy().copy()
+        relevant = (params["opacity"].grad != 0).nonzero()  # train_coarse.py:133, shape (R, 2)
+        assert relevant.dim() == 2 and relevant.shape[1] == 2
+        out[f"relevant{step}"] = relevant.numpy().copy()
+        opt.step(relevant)
+        for n, p in params.items():
+            out[f"after{step}_{n}"] = p.detach().numpy().copy()
+            st = opt.state[p]
+            out[f"m{step}_{n}"] = st["exp_avg"].numpy().copy()
+            out[f"v{step}_{n}"] = st["exp_avg_sq"].numpy().copy()
+    out["lrs"] = np.array([LRS[n] for n in shapes], np.float64)
+    np.savez_compressed(os.path.join(OUT, "adam_coarse.npz"), **out)
 
 
 def make_densify():
@@ -229,8 +264,9 @@ if __name__ == "__main__":
     sys.path.insert(0, ARGS.ref)
     make_loss(ARGS.ref)
     make_adam(ARGS.ref)
+    make_adam_coarse(ARGS.ref)
     make_densify()
     make_lr(ARGS.ref)
     sys.path.insert(0, OUT)
     make_densify_prune(ARGS.ref)
-    print("wrote loss.npz adam.npz densify.npz lr.npz densify_prune_*.npz")
+    print("wrote loss.npz adam.npz adam_coarse.npz densify.npz lr.npz densify_prune_*.npz")

@@ -140,3 +140,18 @@ def deterministic():
         yield
     finally:
         _C.set_deterministic(prev)
+
+
+def record_margins(name, **values):
+    """Observed parity margins of a GPU test (PSNR, n_contrib mismatch, gradient errors), appended as
+    one JSON line to $GSR_PARITY_RECORD when set: the bars in the tests are set from these
+    (profiles/r04_parity_margins.jsonl)."""
+    import json
+    import os
+    path = os.environ.get("GSR_PARITY_RECORD")
+    if not path:
+        return
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    with open(path, "a") as f:
+        f.write(json.dumps(dict(case=name, **{k: (float(v) if v is not None else None) for k, v in values.items()}))
+                + "\n")

@@ -18,7 +18,7 @@ import contextlib
 import numpy as np
 import pytest
 
-from helpers import decode_state, psnr, rel_l2, settings, torch_inputs
+from helpers import decode_state, psnr, record_margins, rel_l2, settings, torch_inputs
 
 GRAD_TOL = 2e-4
 
@@ -162,26 +162,35 @@ def compare(c, st, g, h, check_grads=True, global_sort=False):
     nzr = rs[rs[:, 1] > rs[:, 0]]
     assert len(nzr) == 0 or (nzr[0, 0] == 0 and nzr[-1, 1] == h["K"] and np.all(nzr[1:, 0] == nzr[:-1, 1]))
     nc_bad = float(np.mean(S["n_contrib"] != st["n_contrib"]))
-    assert nc_bad <= 1e-3, f"n_contrib mismatch fraction {nc_bad}"
-    assert psnr(h["color"], st["color"]) >= 80.0, psnr(h["color"], st["color"])
-    assert float(np.mean(np.abs(h["color"] - st["color"]) > 1e-4)) <= 1e-3
-    if c.get("do_depth", True):
-        assert rel_l2(h["invdepth"], st["invdepth"]) <= 1e-4
-    if not check_grads:
-        return
-    G = h["grads"]
-    pairs = [("means3D", "dL_dmeans3D"), ("means2D", "dL_dmeans2D"), ("opacities", "dL_dopacity")]
-    if G.get("shs") is not None:
-        pairs.append(("shs", "dL_dsh"))
-    if G.get("colors_precomp") is not None:
-        pairs.append(("colors_precomp", "dL_dcolors"))
-    if G.get("scales") is not None:
-        pairs += [("scales", "dL_dscales"), ("rotations", "dL_drotations")]
-    if G.get("cov3D_precomp") is not None:
-        pairs.append(("cov3D_precomp", "dL_dcov3D"))
-    for hk, ok in pairs:
-        err = rel_l2(G[hk].reshape(g[ok].shape), g[ok])
-        assert err <= GRAD_TOL, f"{c['name']}: grad {hk} rel L2 {err}"
+    p_img = psnr(h["color"], st["color"])
+    off = float(np.mean(np.abs(h["color"] - st["color"]) > 1e-4))
+    inv = rel_l2(h["invdepth"], st["invdepth"]) if c.get("do_depth", True) else None
+    margins = dict(psnr=p_img if np.isfinite(p_img) else 999.0, nc_bad=nc_bad, frac_off=off, invdepth_rel_l2=inv)
+    try:
+        assert nc_bad <= 1e-3, f"n_contrib mismatch fraction {nc_bad}"
+        assert p_img >= 80.0, p_img
+        assert off <= 1e-3
+        if inv is not None:
+            assert inv <= 1e-4
+        if not check_grads:
+            return
+        G = h["grads"]
+        pairs = [("means3D", "dL_dmeans3D"), ("means2D", "dL_dmeans2D"), ("opacities", "dL_dopacity")]
+        if G.get("shs") is not None:
+            pairs.append(("shs", "dL_dsh"))
+        if G.get("colors_precomp") is not None:
+            pairs.append(("colors_precomp", "dL_dcolors"))
+        if G.get("scales") is not None:
+            pairs += [("scales", "dL_dscales"), ("rotations", "dL_drotations")]
+        if G.get("cov3D_precomp") is not None:
+            pairs.append(("cov3D_precomp", "dL_dcov3D"))
+        for hk, ok in pairs:
+            err = rel_l2(G[hk].reshape(g[ok].shape), g[ok])
+            margins["grad_" + hk] = err
+            assert err <= GRAD_TOL, f"{c['name']}: grad {hk} rel L2 {err}"
+    finally:
+        record_margins(c["name"], **margins)
+    return
 
 
 def upstream_grads(c, seed=99):

@@ -156,6 +156,33 @@ def test_sparse_adam_matches_reference_ouradam():
         assert torch.equal(x, y)
 
 
+def test_sparse_adam_coarse_pair_index_quirk():
+    """train_coarse.py:133-134 hands OurAdam `(opacity.grad != 0).nonzero()` of the (P, 1) gradient:
+    an (R, 2) index whose second column is 0.  OurAdam's gather / scatter
+    (scene/OurAdam.py:267-270,334-337) then also updates row 0 once per step (its copies are all
+    updated alike).  gs_train.optim.Adam.step(relevant) flattens the index, which marks the same
+    rows: bit for bit (within fp32 ulps) the reference run in tests/golden/adam_coarse.npz, where
+    row 0 is never relevant by itself."""
+    from gs_train import Adam
+    d = np.load(os.path.join(GOLD, "adam_coarse.npz"))
+    params = [torch.nn.Parameter(torch.tensor(d[f"init_{n}"], device=DEV)) for n in NAMES]
+    opt = Adam([{"params": [p], "lr": float(lr), "name": n} for p, lr, n in zip(params, d["lrs"], NAMES)],
+               lr=0.0, eps=1e-15)
+    for it in range(2):
+        for j, n in enumerate(NAMES):
+            params[j].grad = torch.tensor(d[f"grad{it}_{n}"], device=DEV)
+        relevant = (params[3].grad != 0).nonzero()
+        assert tuple(relevant.shape) == tuple(d[f"relevant{it}"].shape)
+        opt.step(relevant)
+        for j, n in enumerate(NAMES):
+            got = params[j].detach().cpu().numpy()
+            np.testing.assert_allclose(got, d[f"after{it}_{n}"], rtol=0, atol=5e-7, err_msg=f"{n} step {it}")
+            # row 0 moved although its opacity gradient is zero (the quirk); a never-relevant row did not
+            assert not np.array_equal(got[0], d[f"init_{n}"][0]) or it > 0
+            np.testing.assert_allclose(opt.state[params[j]]["exp_avg"].cpu().numpy(), d[f"m{it}_{n}"], rtol=0,
+                                       atol=2e-7)
+
+
 def test_sparse_adam_large_matches_oracle():
     from gs_train import Adam
     P = 300_001
