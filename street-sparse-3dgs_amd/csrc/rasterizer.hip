@@ -48,9 +48,9 @@ thread_local bool g_step_act_done = false;
 constexpr int kMaxDevicesK = 64;
 thread_local hipEvent_t g_k_ready[kMaxDevicesK] = {};
 // per device: capacity for the next frame's point list, 0 = none yet.  It is the largest K of the
-// last kKHist frames + 1/8 + 4096, so a training loop cycling its cameras (whose K differs from
+// last kKHist (256) frames + 1/8 + 4096, so a training loop cycling its cameras (whose K differs from
 // view to view) rarely comes up short and re-runs the binning (gsr_forward_stats counts re-runs).
-constexpr int kKHist = 8;
+constexpr int kKHist = 256;
 thread_local int64_t g_khint[kMaxDevicesK] = {};
 thread_local int64_t g_khist[kMaxDevicesK][kKHist] = {};
 thread_local int g_khead[kMaxDevicesK] = {};

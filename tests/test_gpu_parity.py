@@ -6,10 +6,17 @@ Bars (stated here, SURVEY.md 8 / BASELINE.json north_star):
   * integer / index work bit-exact: radii, tiles_touched, K, sorted 64-bit keys, point list,
     tile ranges;
   * n_contrib: exact except where an exp() ulp flips the alpha < 1/255 or T < 1e-4 test:
-    mismatching pixel fraction <= 1e-3;
-  * colour / inverse depth: PSNR vs oracle >= 80 dB and at most 1e-3 of pixels off by
-    > 1e-4;
+    mismatching pixel fraction <= NC_TOL;
+  * colour / inverse depth: PSNR vs oracle >= PSNR_BAR, at most OFF_TOL of the pixels off by
+    > 1e-4, inverse depth relative L2 <= INV_TOL;
   * gradients: relative L2 error <= GRAD_TOL per tensor (fp32, summation order differs).
+
+The bars sit about 10x from what the kernels achieve (profiles/r04_parity_margins.jsonl, every
+case of this file, test_gpu_metric.py and test_gpu_lod.py recorded on MI355X with
+GSR_PARITY_RECORD): PSNR >= 157.8 dB, n_contrib mismatch <= 8.5e-7 (1-2 pixels of 2.4M), no pixel
+off by 1e-4, inverse depth <= 2.4e-8 and gradients <= 4.9e-6 relative L2.  Round 2's quadratic
+exponent (132 dB, 3.5e-4 gradient error) would fail them; only the drift test against upstream's
+own exponent formulation (test_gpu_metric.py) keeps loose bars.
 """
 from __future__ import annotations
 
@@ -20,7 +27,11 @@ import pytest
 
 from helpers import decode_state, psnr, record_margins, rel_l2, settings, torch_inputs
 
-GRAD_TOL = 2e-4
+GRAD_TOL = 5e-5
+PSNR_BAR = 145.0
+NC_TOL = 1e-5
+OFF_TOL = 1e-6
+INV_TOL = 3e-7
 
 CASES = [
     dict(name="tiny_deg3", P=300, W=64, H=48, deg=3, seed=1, log_scale=-2.5),
@@ -167,11 +178,11 @@ def compare(c, st, g, h, check_grads=True, global_sort=False):
     inv = rel_l2(h["invdepth"], st["invdepth"]) if c.get("do_depth", True) else None
     margins = dict(psnr=p_img if np.isfinite(p_img) else 999.0, nc_bad=nc_bad, frac_off=off, invdepth_rel_l2=inv)
     try:
-        assert nc_bad <= 1e-3, f"n_contrib mismatch fraction {nc_bad}"
-        assert p_img >= 80.0, p_img
-        assert off <= 1e-3
+        assert nc_bad <= NC_TOL, f"n_contrib mismatch fraction {nc_bad}"
+        assert p_img >= PSNR_BAR, p_img
+        assert off <= OFF_TOL, off
         if inv is not None:
-            assert inv <= 1e-4
+            assert inv <= INV_TOL, inv
         if not check_grads:
             return
         G = h["grads"]
