@@ -527,16 +527,17 @@ class Ranks:
     """Process-group helpers: barrier, MAX / gather of host floats (gloo on CPU tensors when the
     ranks share one GPU, RCCL otherwise)."""
 
-    def __init__(self, world, rank, share, dev):
+    def __init__(self, world, rank, share, dev, pg=None):
         self.world, self.rank, self.share, self.dev = world, rank, share, dev
+        self.pg = world > 1 if pg is None else pg  # a process group exists (GSR_BENCH_FORCE_PG: also at N = 1)
 
     def barrier(self):
-        if self.world > 1:
+        if self.pg:
             import torch.distributed as dist
             dist.barrier()
 
     def gather(self, x):
-        if self.world == 1:
+        if not self.pg:
             return [float(x)]
         import torch
         import torch.distributed as dist
@@ -835,14 +836,18 @@ def main():
     # device 0 and gloo for the barriers / timing reduction (RCCL refuses two ranks on one device).
     # The driver's runs use one GPU per rank and RCCL.
     share = os.environ.get("GSR_BENCH_SHARE_GPU") == "1"
-    if world > 1:
+    # GSR_BENCH_FORCE_PG=1 (launched by torch.distributed.run): the RCCL process group, barriers and
+    # timing all-reduce even for one rank -- the collective path the driver's multi-GPU runs take,
+    # exercised on a one-GPU box (RCCL refuses two ranks on one device)
+    use_pg = world > 1 or (os.environ.get("GSR_BENCH_FORCE_PG") == "1" and "RANK" in os.environ)
+    if use_pg:
         torch.cuda.set_device(0 if share else local)
         if share:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", 0 if share or world == 1 else local)
-    ranks = Ranks(world, rank, share, dev)
+    ranks = Ranks(world, rank, share, dev, pg=use_pg)
 
     P, W, H, deg = a.gaussians, a.width, a.height, a.sh_degree
     s, inp, gcol, ginv = make_inputs(P, W, H, deg, seed=rank, device=dev)
@@ -997,9 +1002,10 @@ def main():
         with torch.no_grad():
             color, _, invd = raster_again(s, inp, W, H, deg, dev)
         out["psnr_vs_oracle"] = psnr_vs_oracle(color, invd, st)
+    out["process_group"] = dist.get_backend() if use_pg else None
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_pg:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -33,3 +33,24 @@ def test_bench_gpus2_spawns_two_ranks():
     c4 = d["config4"]
     assert c4["n_gpus"] == 2 and c4["value"] > 0 and len(c4["train_step_ms_per_rank"]) == 2
     assert all(v > 0 for v in c4["train_step_ms_per_rank"])
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_bench_rccl_process_group_single_rank():
+    """The collective path of the driver's multi-GPU runs on the one-GPU box: bench.py under
+    torch.distributed.run with GSR_BENCH_FORCE_PG=1 initialises the RCCL ("nccl") process group
+    for its one rank and times through its barriers and all-reduce (RCCL refuses two ranks on one
+    device, so N > 1 cannot run here)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT", "LOCAL_WORLD_SIZE", "GSR_BENCH_SHARE_GPU")}
+    env["GSR_BENCH_FORCE_PG"] = "1"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr",
+           "127.0.0.1", "--master-port", "29517", os.path.join(REPO, "bench.py"), "--gpus", "1", "--steps", "3",
+           "--warmup", "1", "--gaussians", "200000", "--profile-steps", "1", "--metric-only"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=env, cwd=REPO)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert len(lines) == 1, r.stdout[-3000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["value"] > 0 and d["process_group"] == "nccl"
