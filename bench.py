@@ -270,6 +270,16 @@ def config3(a, dev):
     r1 = _C.forward_stats()
     per = np.array([start.elapsed_time(evs[0])] + [evs[i].elapsed_time(evs[i + 1]) for i in range(len(evs) - 1)])
     psnr1 = view_psnr(ts)
+    # where a late iteration's time goes: the rasterizer's stages (HIP events) over 32 more steps
+    # of the trained chunk (the view cycle continues; these steps are outside the timed run)
+    _C.set_profiling(True)
+    acc, nprof = {}, 32
+    for _ in range(nprof):
+        ts.step()
+        for k_, v_ in _C.stage_times_ms().items():
+            acc[k_] = acc.get(k_, 0.0) + v_ / nprof
+    _C.set_profiling(False)
+    late_K = int(ts.last_K)
     ev = tc.events
     out = {"workload": f"train_single.py loop on a synthetic Street-sparse chunk: {info['views']} views "
                        f"({info['depth_only_views']} depth-only) of {info['W']}x{info['H']} (90 deg cube faces), "
@@ -286,6 +296,7 @@ def config3(a, dev):
            "loss": {str(k): round(float(v), 5) for k, v in sorted(losses.items())},
            "train_view_psnr_db": {"before": psnr0, "after": psnr1},
            "P_trace": [[e["iteration"], e["P_after"]] for e in ev][::4],
+           "late_raster_stages_ms": {k_: round(v_, 4) for k_, v_ in acc.items()}, "late_tile_instances": late_K,
            "data": "synthetic street chunk generated on the device (gs_train.chunk.street_chunk); the example_dataset "
                    "is not available offline"}
     del ts, tc
