@@ -165,6 +165,11 @@ int gsr_set_binning(int mode);
  * (a superblock list too long for LDS).  Returns the number of values written (<= n). */
 int gsr_forward_stats(int64_t *out, int n);
 
+/* Forget the calling thread's point-list capacity hint (the largest K of its last 256 frames per
+ * device): the next frame reads K before binning, as the first one does.  For a caller that
+ * switches to a much smaller workload (the buffers follow the hint) and for tests.  ABI 3. */
+int gsr_reset_capacity_hint(void);
+
 /* Statistics of one forward frame, read from its geometry buffer (synchronises the device):
  * out[0] = level-1 binning entries (Gaussian x superblock pairs, "P1" of DESIGN.md), out[1] = tile
  * instances (K).  P = the frame's rendered rows (num_render when non-zero).  Returns the number of

@@ -920,6 +920,15 @@ int gsr_forward_stats(int64_t *out, int n) {
     return k;
 }
 
+int gsr_reset_capacity_hint(void) {
+    for (int d = 0; d < kMaxDevicesK; d++) {
+        g_khint[d] = 0;
+        g_khead[d] = 0;
+        for (int i = 0; i < kKHist; i++) g_khist[d][i] = 0;
+    }
+    return GSR_OK;
+}
+
 int gsr_frame_stats(const void *geom_buffer, int P, int width, int height, int64_t *out, int n) {
     if (!out || n < 0 || P < 0 || width <= 0 || height <= 0)
         return fail(GSR_ERR_INVALID_ARGUMENT, "gsr_frame_stats: bad arguments");

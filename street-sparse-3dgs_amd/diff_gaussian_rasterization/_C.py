@@ -319,6 +319,11 @@ def set_binning(mode: int) -> int:
     return r
 
 
+def reset_capacity_hint() -> None:
+    """Forget this thread's point-list capacity hint (gsr_reset_capacity_hint)."""
+    _L.gsr_reset_capacity_hint()
+
+
 def forward_stats() -> dict:
     """Frames rasterized since load, how many re-ran their binning at K, how many were binned by
     the local sort and how many of those fell back to the global sort (gsr_forward_stats)."""

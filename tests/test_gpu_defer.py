@@ -38,7 +38,8 @@ def _capacity_overflow_rerun_matches():
     big = O.synthetic_scene(20000, 480, 320, seed=32, sh_degree=3, log_scale_mean=-2.0)
     from diff_gaussian_rasterization import _C
     reruns = lambda: _C.forward_stats()["reruns"]
-    for _ in range(8):     # the hint is the largest K of the last 8 frames: leave a small one
+    _C.reset_capacity_hint()  # the hint is the largest K of the last 256 frames: start from a small one
+    for _ in range(3):
         _frame(small)
     r0 = reruns()
     a = _frame(big)        # K far above the hint: binned and rendered twice
