@@ -70,6 +70,8 @@ def parse():
     ap.add_argument("--chunk-init", type=int, default=300_000, help="LiDAR-like initial points")
     ap.add_argument("--post-leaves", type=int, default=3_000_000,
                     help="leaves of the train_post step's synthetic hierarchy (0 = skip that step)")
+    ap.add_argument("--bwd-seg", type=int, default=None,
+                    help="backward segment length (gsr_set_bwd_segment; default: the library's setting)")
     ap.add_argument("--train-baseline", action="store_true",
                     help="also time the reference-structured torch train step (oracle/train_torch_ref.py: conv2d "
                          "SSIM, OurAdam gather/scatter) -- a baseline leg, like cpu_baseline")
@@ -860,6 +862,11 @@ def main():
     dev = torch.device("cuda", 0 if share or world == 1 else local)
     ranks = Ranks(world, rank, share, dev, pg=use_pg)
 
+    from diff_gaussian_rasterization import _C as _gsr
+    if a.bwd_seg is not None:
+        _gsr.set_bwd_segment(a.bwd_seg)
+    bwd_seg = _gsr.set_bwd_segment(0)
+    _gsr.set_bwd_segment(bwd_seg)
     P, W, H, deg = a.gaussians, a.width, a.height, a.sh_degree
     s, inp, gcol, ginv = make_inputs(P, W, H, deg, seed=rank, device=dev)
     rs, raster = rasterizer_for(s, W, H, deg, dev)
@@ -945,7 +952,8 @@ def main():
         "data": "synthetic (seeded Gaussians in the frustum, SURVEY.md 8(d); one chunk per rank, seed = rank)",
         "config": {"workload": f"rasterizer fwd+bwd, {P} Gaussians, SH degree {deg}, {W}x{H}, do_depth",
                    "gaussians": P, "width": W, "height": H, "sh_degree": deg, "visible": Pv, "tile_instances": K,
-                   "level1_entries": P1, "live_rows": Pl, "tiles": T, "parallelism": f"chunk-per-gpu x{world}"},
+                   "level1_entries": P1, "live_rows": Pl, "tiles": T, "bwd_segment": bwd_seg,
+                   "parallelism": f"chunk-per-gpu x{world}"},
         # frac: algorithmic bytes / the kernel's HIP-event time measured here; frac_rocprof: the same
         # bytes / the average duration in the committed rocprofv3 summary of these kernel sources
         # (profiles/, null when no summary of the current sources is committed)

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 3
+#define GSR_ABI_VERSION 4
 
 typedef enum {
     GSR_OK = 0,
@@ -151,6 +151,15 @@ int gsr_set_true_scale_gradient(int enable);
  * forward + backward bitwise reproducible, slower.  A frame's backward uses the mode that was in
  * force at its forward.  Returns the previous mode. */
 int gsr_set_deterministic(int enable);
+
+/* Backward work split, process-wide.  L = 0 (default): render_bwd replays every tile in one
+ * workgroup.  L > 0 (a multiple of 64, >= 512): the forward checkpoints each pixel's transmittance
+ * and accumulated colour every L list positions of its tile, and the backward replays a tile whose
+ * last contributor lies past L as ceil(work / L) independent segments (the few very long tiles of a
+ * street view no longer form the kernel's tail).  Gradients agree with the unsegmented replay to
+ * fp32 rounding.  A frame's backward uses the length its forward was made with.  Returns the
+ * previous length, or GSR_ERR_INVALID_ARGUMENT / GSR_ERR_UNSUPPORTED. */
+int gsr_set_bwd_segment(int L);
 
 /* Depth-order strategy of the binning, process-wide.  0: the local sort -- level 1 in Gaussian
  * index order, each superblock list sorted by depth in LDS -- except for frames forwarded in

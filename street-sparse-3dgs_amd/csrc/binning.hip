@@ -244,6 +244,7 @@ __global__ __launch_bounds__(kColThreads) void sb_colscan_kernel(SBGrid sg, uint
         base_i[nsb] = ci;
     }
     if (zero_classes && threadIdx.x < kBwdClasses) zero_classes[threadIdx.x] = 0u;
+    if (zero_classes && threadIdx.x == 0) zero_classes[kBwdSegCount] = 0u;
     if (GSR_FWD_SB_ORDER && sb_order) {
         // the forward's launch order, heaviest first: SBs bucketed into 256 descending classes of
         // their mean tile list length (16 instances per class), in order of the bucket scan

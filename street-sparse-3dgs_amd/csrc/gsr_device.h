@@ -464,6 +464,23 @@ constexpr int kBwdClasses = 256;
 #endif
 constexpr int kBwdClassShift = 2;  // class = 255 - min(work >> 2, 255): heaviest first
 
+// Backward segments (gsr_set_bwd_segment): a tile whose backward work (last contributor position)
+// exceeds L list positions is replayed as ceil(work / L) independent work items of L positions, the
+// later ones starting from checkpoints render_fwd stores at every L-th position of the tile's list
+// (per pixel: the transmittance there and the colour / inverse depth accumulated behind it), so one
+// street view's vanishing-point tiles (tens of thousands of instances) no longer set the kernel's
+// tail.  The checkpoints and the segment list live in the binning buffer past the point list (the
+// level-1 lists are dead once the tiles are binned): slot floor(position / L) is unique per
+// checkpoint (any two are >= L positions apart in the point list).
+constexpr int kBwdSegCount = kBwdClasses;  // bwd_cnt[kBwdSegCount]: full segments listed by render_fwd
+constexpr int kCkFloats = 5;               // T, behind r, g, b, inverse depth (x 256 pixels per slot)
+__host__ __device__ __forceinline__ size_t ck_offset(int64_t K) { return (size_t)(((4 * K) + 255) / 256 * 256); }
+__host__ __device__ __forceinline__ size_t ck_slots(int64_t K, uint32_t L) { return L ? (size_t)(K / L) + 2 : 0; }
+constexpr uint32_t kMinBwdSeg = 512;     // the shortest segment: checkpoints + list fit in 16 B / instance + kSegReserve
+constexpr size_t kSegReserve = 16384;    // carved past the level-1 lists (a small K's checkpoint slots)
+// render_bwd's grid: every tile's last segment plus at most K / L full segments
+inline int64_t bwd_grid(int T, int64_t K, uint32_t L) { return (int64_t)T + (L ? K / L : 0); }
+
 #ifndef GSR_RECT4
 #define GSR_RECT4 1
 #endif

@@ -108,10 +108,13 @@ struct ZeroRows {
 // render.hip
 void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                        const float *bg, float *out_color, float *out_invdepth, hipStream_t s, bool need_bwd = true,
-                       bool sb_order = false);
+                       bool sb_order = false, uint32_t seg_len = 0);
+// seg_len != 0: the backward's heavy tiles are cut into segments of seg_len list positions
+// (gsr_set_bwd_segment; the backward must get the value its forward was made with)
 void launch_render_bwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                        const int *radii, const float *bg, const float *dL_dpix, const float *dL_dinvdepth,
-                       const BwdScratch &sc, hipStream_t s, const ZeroRows *zr = nullptr);
+                       const BwdScratch &sc, hipStream_t s, const ZeroRows *zr = nullptr, uint32_t seg_len = 0);
+bool bwd_segments_supported();
 
 // backward.hip
 // sparse_rows (the native train step only, set_sparse_grad_rows): the rows of Gaussians with ten

@@ -224,6 +224,7 @@ BinningState carve_binning(void *base, int64_t K, size_t *bytes) {
     // -) on the local-sort path -- carved for the larger
     b.sblist4 = c.take<uint4>(K);
     b.sblist = reinterpret_cast<uint2 *>(b.sblist4);
+    (void)c.take<uint8_t>(kSegReserve);  // backward segments: the checkpoints use the level-1 lists' room
     b.cap = (uint32_t)K;
     b.kdev = nullptr;
     if (bytes) *bytes = align_up(c.off, 256);
@@ -240,7 +241,7 @@ ImageState carve_image(void *base, int T, int npix, size_t *bytes) {
     s.tile_work = c.take<uint32_t>(T);
     s.tile_ids = c.take<uint32_t>(T);
     s.tile_order = c.take<uint32_t>(T);
-    s.bwd_cnt = c.take<uint32_t>(kBwdClasses);
+    s.bwd_cnt = c.take<uint32_t>(kBwdClasses + 64);  // + the segment count (kBwdSegCount)
     s.bwd_cls = c.take<uint32_t>((size_t)kBwdClasses * T);
     if (bytes) *bytes = align_up(c.off, 256);
     return s;
@@ -394,6 +395,32 @@ uint8_t forward_uncleared(const void *geom) {
     if (g_unclr.empty()) return 0;
     const auto it = g_unclr.find(geom);
     return it == g_unclr.end() ? 0 : it->second;
+}
+
+// Backward segments (gsr_set_bwd_segment): the segment length a forward published its backward
+// items with, per image buffer (the backward must cut tiles the same way).  Same bookkeeping as
+// g_unclr: a forward made without segments erases its buffer's entry; bounded by kUnclearedMax (a
+// backward whose entry was dropped takes the current setting).
+#ifndef GSR_BWD_SEG_DEFAULT
+#define GSR_BWD_SEG_DEFAULT 0
+#endif
+std::atomic<uint32_t> g_bwd_seg{GSR_BWD_SEG_DEFAULT};
+std::mutex g_seg_mu;
+std::unordered_map<const void *, uint32_t> g_seg_of;
+void note_forward_seg(const void *image, uint32_t L) {
+    std::lock_guard<std::mutex> lk(g_seg_mu);
+    if (!L) {
+        if (!g_seg_of.empty()) g_seg_of.erase(image);
+        return;
+    }
+    if (g_seg_of.size() >= kUnclearedMax) g_seg_of.clear();
+    g_seg_of[image] = L;
+}
+uint32_t forward_seg(const void *image) {
+    std::lock_guard<std::mutex> lk(g_seg_mu);
+    if (g_seg_of.empty()) return 0;
+    const auto it = g_seg_of.find(image);
+    return it == g_seg_of.end() ? g_bwd_seg.load(std::memory_order_relaxed) : it->second;
 }
 }  // namespace
 
@@ -695,7 +722,11 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
     }
     if (split && !GSR_COLOR_SERIAL && !color_early && (rc = fork_color())) return rc;
     bool joined = false;
+    const uint32_t seg_req = need_bwd && bwd_segments_supported() ? g_bwd_seg.load(std::memory_order_relaxed) : 0u;
+    uint32_t seg_used = 0;
     auto bin_and_render = [&](int64_t cap, bool counted) -> int {
+        // backward items are numbered tile + T * segment (32 bits)
+        seg_used = seg_req && (uint64_t)T * (uint64_t)(cap / seg_req + 1) < (1ull << 32) ? seg_req : 0u;
         size_t bbytes = 0;
         carve_binning(nullptr, cap, &bbytes);
         void *bbase = binning_buffer(resize_ctx, bbytes);
@@ -729,7 +760,7 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
         }
         {
             StageTimer st(5, s);
-            launch_render_fwd(cam, gs, bs, is, background, out_color, out_invdepth, s, need_bwd, sb_order);
+            launch_render_fwd(cam, gs, bs, is, background, out_color, out_invdepth, s, need_bwd, sb_order, seg_used);
         }
         if (need_bwd && !GSR_BWD_CLS) {
             StageTimer st(9, s);  // backward launch order, from the forward's per-tile work
@@ -761,6 +792,7 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
             return fail(GSR_ERR_DEVICE, "binning counter reset failed");
         if ((rc = bin_and_render(K, local))) return rc;
     }
+    note_forward_seg(ibase, seg_used);  // the re-run's segment length (its capacity may differ)
     if (P > 0 && local) g_local_frames.fetch_add(1, std::memory_order_relaxed);
     // the kernels compare K with a 32-bit capacity: keep the hint representable
     if (P > 0) {
@@ -873,9 +905,11 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
     {
         StageTimer st(6, s);
         // the dense zero gradient rows go out beside render_bwd's replay (bwd_zero_rows)
-        zeroed = R_inst > 0 && bwd_zero_rows(in, out, sc, gs.live_stamp, T, &zr);
+        const uint32_t seg = forward_seg(image_buffer);
+        zeroed = R_inst > 0 && bwd_zero_rows(in, out, sc, gs.live_stamp, (int)bwd_grid(T, R_inst, seg), &zr);
         if (R_inst > 0)
-            launch_render_bwd(cam, gs, bs, is, radii, background, dL_dpix, dL_dinvdepth, sc, s, zeroed ? &zr : nullptr);
+            launch_render_bwd(cam, gs, bs, is, radii, background, dL_dpix, dL_dinvdepth, sc, s, zeroed ? &zr : nullptr,
+                              seg);
     }
     if ((rc = check("render backward", debug, s))) return rc;
     {
@@ -906,6 +940,14 @@ int gsr_set_true_scale_gradient(int enable) {
 }
 
 int gsr_set_deterministic(int enable) { return g_deterministic.exchange(enable ? 1 : 0); }
+
+int gsr_set_bwd_segment(int L) {
+    if (L < 0 || (L > 0 && (L < (int)kMinBwdSeg || L % kWave != 0)))
+        return fail(GSR_ERR_INVALID_ARGUMENT, "backward segment length: 0 (off) or a multiple of 64 >= 512");
+    if (L > 0 && !bwd_segments_supported())
+        return fail(GSR_ERR_UNSUPPORTED, "backward segments need the class launch order and the 1-row sub-block forward");
+    return (int)g_bwd_seg.exchange((uint32_t)L);
+}
 
 int gsr_set_binning(int mode) {
     if (mode < 0 || mode > 1) return fail(GSR_ERR_INVALID_ARGUMENT, "gsr_set_binning: mode 0 or 1");

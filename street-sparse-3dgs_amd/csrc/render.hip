@@ -171,7 +171,8 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kerne
     float *__restrict__ out_invd, float *__restrict__ final_T, uint32_t *__restrict__ n_contrib,
     uint32_t *__restrict__ tile_work, const uint32_t *__restrict__ fwd_order, const uint32_t *__restrict__ kdev,
     uint32_t cap, const uint32_t *__restrict__ sort_err, float4 *__restrict__ acc, uint32_t acc_n4,
-    uint32_t *__restrict__ bwd_cnt, uint32_t *__restrict__ bwd_cls, int ntiles, int gy, int sb_nsbx, int sb_shift) {
+    uint32_t *__restrict__ bwd_cnt, uint32_t *__restrict__ bwd_cls, int ntiles, int gy, int sb_nsbx, int sb_shift,
+    uint32_t seg_len, uint32_t *__restrict__ bin_base) {
     constexpr int kWaves = kPixPerLane / kSub;
     if (kdev && *kdev > cap) return;  // the point-list capacity is short: the host re-runs at K
     {
@@ -243,6 +244,13 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kerne
         fwd_gather(rec, point_list[min(rg.x + (uint32_t)lane, lastpos)], cur);
         gnext = point_list[min(rg.x + kWave + (uint32_t)lane, lastpos)];
     }
+    // backward segments (seg_len != 0, kSub == 1): at every seg_len-th list position of the tile the
+    // wave checkpoints its pixels' transmittance and accumulated colour / inverse depth (the state
+    // in front of that position) into the binning buffer past the point list (bwd_segments)
+    const bool segs = kSub == 1 && seg_len != 0u && bwd_cnt != nullptr;
+    float *ck = nullptr;
+    uint32_t ncross = 0;
+    if (segs) ck = reinterpret_cast<float *>(reinterpret_cast<char *>(bin_base) + ck_offset(kdev ? *kdev : cap));
     for (uint32_t base = rg.x; base < rg.y; base += kWave) {
         uint32_t live = 0;  // sub-blocks with a pixel still accumulating (wave-uniform)
 #pragma unroll
@@ -251,6 +259,15 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kerne
                         ? 1u << k
                         : 0u;
         if (!live) break;
+        if (segs && base > rg.x && (base - rg.x) % seg_len == 0u) {
+            float *c = ck + (size_t)(base / seg_len) * (kCkFloats * 256) + w * kWave + lane;
+            c[0] = T[0];
+            c[256] = C0[0];
+            c[512] = C1[0];
+            c[768] = C2[0];
+            c[1024] = ID[0];
+            ncross++;
+        }
         const bool valid = base + (uint32_t)lane < rg.y;
         const float4 qa = cur.a, qb = cur.b, qc = cur.c;
         const uint32_t m = valid ? sub_block_mask_n<kSub>(qa, qb, cur.tm, tx0, sy0) & live : 0u;
@@ -352,6 +369,14 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kerne
         fst.flush(kFwdPairs);
         if (lane == 0) atomicAdd(&g_blend_stats[kFwdAcc], (unsigned long long)fwd_acc);
     }
+    // the checkpoints' colour as the part still to come: B = C_final - C(in front)
+    for (uint32_t i = 1; i <= ncross; i++) {
+        float *c = ck + (size_t)((rg.x + i * seg_len) / seg_len) * (kCkFloats * 256) + w * kWave + lane;
+        c[256] = C0[0] - c[256];
+        c[512] = C1[0] - c[512];
+        c[768] = C2[0] - c[768];
+        c[1024] = ID[0] - c[1024];
+    }
     const bool bad = sort_err && *sort_err;  // the depth sort gave up on a lookback: NaN frame
     uint32_t wl = 0;
 #pragma unroll
@@ -372,13 +397,26 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kerne
     wl = wave_max_u32(wl);
     // the tile's backward work (last contributor position): tile_work, and with bwd_cnt its slot in
     // the backward's heaviest-first class lists
+    // With segments a tile of more than seg_len positions of work is cut into ceil(work / seg_len)
+    // backward items (tile + ntiles * segment): all but the last go to the segment list (past the
+    // checkpoints), run first; the last one goes into its work class like a whole tile.
     const auto publish = [&](uint32_t mx) {
         tile_work[tile] = mx;
         if (bwd_cnt) {
-            const uint32_t k = mx >> kBwdClassShift;
+            uint32_t item = (uint32_t)tile, wk = mx;
+            if (segs && mx > seg_len) {
+                const uint32_t nseg = (mx + seg_len - 1u) / seg_len;
+                const uint32_t kf = kdev ? *kdev : cap;
+                uint32_t *items = reinterpret_cast<uint32_t *>(ck + ck_slots(kf, seg_len) * (kCkFloats * 256));
+                const uint32_t b = atomicAdd(&bwd_cnt[kBwdSegCount], nseg - 1u);
+                for (uint32_t sgi = 0; sgi + 1u < nseg; sgi++) items[b + sgi] = (uint32_t)tile + (uint32_t)ntiles * sgi;
+                item = (uint32_t)tile + (uint32_t)ntiles * (nseg - 1u);
+                wk = mx - (nseg - 1u) * seg_len;
+            }
+            const uint32_t k = wk >> kBwdClassShift;
             const uint32_t c = (uint32_t)(kBwdClasses - 1) - (k < (uint32_t)(kBwdClasses - 1) ? k : (uint32_t)(kBwdClasses - 1));
             const uint32_t r = atomicAdd(&bwd_cnt[c], 1u);
-            bwd_cls[(size_t)c * ntiles + r] = (uint32_t)tile;
+            bwd_cls[(size_t)c * ntiles + r] = item;
         }
     };
     if (kWaves == 1) {
@@ -410,7 +448,8 @@ __device__ __forceinline__ int bwd_tile_of(uint32_t b, const uint32_t *__restric
     }
     const uint32_t excl = incl - s4;
     const uint64_t hit = __ballot(b >= excl && b < incl);
-    const int L = hit ? __ffsll((unsigned long long)hit) - 1 : 0;
+    if (!hit) return -1;  // past the listed items (the grid's room for segments)
+    const int L = __ffsll((unsigned long long)hit) - 1;
     uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)excl, L);
     const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)c4.x, L), y = (uint32_t)__builtin_amdgcn_readlane((int)c4.y, L),
                    z = (uint32_t)__builtin_amdgcn_readlane((int)c4.z, L);
@@ -430,6 +469,7 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t *__rest
                                                           uint32_t *__restrict__ zero_classes) {
     // the forward order's launch also zeroes the backward class counters render_fwd fills
     if (zero_classes && threadIdx.x < kBwdClasses) zero_classes[threadIdx.x] = 0u;
+    if (zero_classes && threadIdx.x == 0) zero_classes[kBwdSegCount] = 0u;
     if (kdev && *kdev > cap) return;  // ranges / work were not written this pass (capacity re-run)
     __shared__ uint32_t hist[256];
     if (threadIdx.x < 256) hist[threadIdx.x] = 0u;
@@ -468,7 +508,7 @@ void launch_tile_order(const uint32_t *work, const uint2 *ranges, int T, int shi
 
 void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                        const float *bg, float *out_color, float *out_invdepth, hipStream_t s, bool need_bwd,
-                       bool sb_order) {
+                       bool sb_order, uint32_t seg_len) {
     const int T = cam.gx * cam.gy;
     if (T == 0) return;
     const SBGrid &sg = gs.sb;
@@ -479,7 +519,7 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
                        out_color, out_invdepth, is.final_T, is.n_contrib, is.tile_work, is.tile_ids, bs.kdev, bs.cap, \
                        bs.kdev ? dsort_err_word(gs) : nullptr, gs.acc, (uint32_t)(4 * (size_t)gs.nacc),              \
                        GSR_BWD_CLS && need_bwd ? is.bwd_cnt : nullptr, is.bwd_cls, T, cam.gy, sg.nsbx,        \
-                       sb_order ? sg.shift : -1)
+                       sb_order ? sg.shift : -1, GSR_BWD_CLS && need_bwd ? seg_len : 0u, bs.point_list)
     static_assert(GSR_FWD_SUB == 1 || GSR_FWD_SUB == 2 || GSR_FWD_SUB == 4, "GSR_FWD_SUB: 1, 2 or 4");
     GSR_FWD_LAUNCH(render_fwd_kernel<GSR_FWD_SUB>, kWave * (kPixPerLane / GSR_FWD_SUB));
 #undef GSR_FWD_LAUNCH
@@ -528,6 +568,29 @@ __device__ __forceinline__ void bwd_gather(const GRec *__restrict__ rec, const u
     o.goff = kAtomic ? g : goff[g];
 }
 
+// this workgroup's share of the frame's dense zero gradient rows (ZeroRows): issued after the
+// replay, so no wait of the replay covers them -- the VALU-bound replay leaves HBM nearly idle, and
+// preprocess_bwd no longer streams these bytes on its own
+__device__ __forceinline__ void bwd_zero_slice(const ZeroRows &zr) {
+    const int lane = threadIdx.x;
+    if (!zr.per4) return;
+    {
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        const uint64_t q0 = (uint64_t)blockIdx.x * zr.per4, q1 = min(zr.c4[kZeroArrays], q0 + zr.per4);
+        for (uint64_t q = q0 + (uint64_t)lane; q < q1; q += kWave) {
+            int k = 0;
+#pragma unroll
+            for (int a = 1; a < kZeroArrays; a++) k += q >= zr.c4[a];
+            __builtin_nontemporal_store(f4{0.f, 0.f, 0.f, 0.f}, reinterpret_cast<f4 *>(zr.p[k]) + (q - zr.c4[k]));
+        }
+        if (blockIdx.x == 0 && lane < 4 * kZeroArrays) {  // the floats past each array's last whole float4
+            const int k = lane >> 2, t = lane & 3;
+            const uint64_t e = 4 * (zr.c4[k + 1] - zr.c4[k]) + (uint64_t)t;
+            if (e < zr.n[k]) __builtin_nontemporal_store(0.f, zr.p[k] + e);
+        }
+    }
+}
+
 // kAtomic (default): every live instance's ten sums are added into its Gaussian's accumulator row
 // (GeomState.acc) with no-return float atomics once per batch -- ten wave-wide atomic instructions,
 // lanes = (instance, value) pairs, so each instance is ONE contiguous 40-B segment of a 64-B row
@@ -540,7 +603,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
     const GRec *__restrict__ rec, const float *__restrict__ bg, const float *__restrict__ final_Ts,
     const uint32_t *__restrict__ n_contrib, const float *__restrict__ dL_dpix, const float *__restrict__ dL_dinvd,
     const uint32_t *__restrict__ tile_order, const uint32_t *__restrict__ goff, uint64_t *__restrict__ boundary,
-    float4 *__restrict__ out, ZeroRows zr, const uint32_t *__restrict__ bwd_cnt, const uint32_t *__restrict__ bwd_cls) {
+    float4 *__restrict__ out, ZeroRows zr, const uint32_t *__restrict__ bwd_cnt, const uint32_t *__restrict__ bwd_cls,
+    uint32_t ntiles, uint32_t seg_len, const float *__restrict__ ck, const uint32_t *__restrict__ seg_items) {
     // 9 KiB of LDS per wave: each compacted instance's mean and conic (scaled for gauss_p2 by the
     // lane that stages it, once per instance instead of by the whole wave), opacity, list position
     // << 4 | sub-block mask, Gaussian id (atomic mode) or record index, colour, and the unscaled
@@ -556,9 +620,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
 
     // Tiles run heaviest first (longest-processing-time order from the forward's per-tile work):
     // with ~2.7 tiles per wave slot, index order leaves a tail of a few heavy tiles.
-    const int tile = GSR_TILE_REVERSE ? (int)blockIdx.x
-                     : GSR_BWD_CLS    ? bwd_tile_of(blockIdx.x, bwd_cnt, bwd_cls, (int)gridDim.x)
-                                      : (int)tile_order[blockIdx.x];
+    // With segments (seg_len != 0) the full segments render_fwd listed run first, then the class
+    // lists; workgroups past both only zero their share of the gradient rows.
+    int item;
+    if (GSR_TILE_REVERSE) item = (int)blockIdx.x;
+    else if (GSR_BWD_CLS) {
+        const uint32_t nsg = seg_len ? bwd_cnt[kBwdSegCount] : 0u;
+        item = blockIdx.x < nsg ? (int)seg_items[blockIdx.x] : bwd_tile_of(blockIdx.x - nsg, bwd_cnt, bwd_cls, (int)ntiles);
+    } else item = (int)tile_order[blockIdx.x];
+    if (item < 0) {
+        bwd_zero_slice(zr);
+        return;
+    }
+    const int tile = (int)((uint32_t)item % ntiles), seg = (int)((uint32_t)item / ntiles);
     const int tx = tile % gx, ty = tile / gx;
     const int lane = threadIdx.x;
     const int px = tx * kTile + (lane & 15);
@@ -605,6 +679,30 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
         maxlast = lastk[k] > maxlast ? lastk[k] : maxlast;
     }
     const uint2 rg = ranges[tile];
+    // the item's list positions [lo, hi): the whole tile's [0, maxlast), or segment `seg` of
+    // ceil(maxlast / seg_len).  A pixel still accumulating past hi starts from the forward's
+    // checkpoint at hi: T there, and S from the colour still to come B = C_final - C(hi),
+    // S = ((B + T_final bg) . dL/dpix + B_d dL/dinvdepth) / T.
+    uint32_t lo = 0, hi0 = maxlast;
+    if (seg_len && maxlast > seg_len) {
+        const uint32_t nseg = (maxlast + seg_len - 1u) / seg_len;
+        lo = (uint32_t)seg * seg_len;
+        hi0 = (uint32_t)seg + 1u == nseg ? maxlast : lo + seg_len;
+    }
+    if (hi0 < maxlast) {
+        const float *c = ck + (size_t)((rg.x + hi0) / seg_len) * (kCkFloats * 256) + lane;
+#pragma unroll
+        for (int k = 0; k < kPixPerLane; k++) {
+            if (last[k] > hi0) {
+                const float Tb = c[k * kWave];
+                float num = fmaf(c[256 + k * kWave] + T[k] * b0, dp0[k],
+                                 fmaf(c[512 + k * kWave] + T[k] * b1, dp1[k], (c[768 + k * kWave] + T[k] * b2) * dp2[k]));
+                if (kDepth) num = fmaf(c[1024 + k * kWave], did[k], num);
+                S[k] = num / Tb;
+                T[k] = Tb;
+            }
+        }
+    }
     const float sx = 0.5f * (float)W, sy = 0.5f * (float)H;
     const int rs_slot = wave_rs10_slot(lane);
     (void)rs_slot;
@@ -617,16 +715,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
     BwdBatch cur;
     uint32_t gnext = 0;
     if (maxlast > 0) {
-        const uint32_t g0 = point_list[rg.x + (uint32_t)max((int)maxlast - 1 - lane, 0)];
+        const uint32_t g0 = point_list[rg.x + (uint32_t)max((int)hi0 - 1 - lane, (int)lo)];
         bwd_gather<kAtomic>(rec, goff, g0, cur);
-        gnext = point_list[rg.x + (uint32_t)max((int)maxlast - 1 - kWave - lane, 0)];
-        // the tile's boundary key: lane 0 holds the last instance any pixel uses
-        if (!kAtomic && lane == 0) boundary[tile] = ((uint64_t)cur.q3.z << 32) | g0;
+        gnext = point_list[rg.x + (uint32_t)max((int)hi0 - 1 - kWave - lane, (int)lo)];
+        // the tile's boundary key (its last segment): lane 0 holds the last instance any pixel uses
+        if (!kAtomic && lane == 0 && hi0 == maxlast) boundary[tile] = ((uint64_t)cur.q3.z << 32) | g0;
     } else if (!kAtomic && lane == 0) {
         boundary[tile] = 0ull;
     }
-    for (int hi = (int)maxlast; hi > 0; hi -= kWave) {
-        const int n = hi < kWave ? hi : kWave;
+    for (int hi = (int)hi0; hi > (int)lo; hi -= kWave) {
+        const int n = hi - (int)lo < kWave ? hi - (int)lo : kWave;
         uint32_t m = 0, u = 0, pos = 0;
         const float4 qa = cur.a, qb = cur.b, qc = cur.c;
         if (lane < n) {
@@ -641,7 +739,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
         }
         // next batch in flight while this one replays
         bwd_gather<kAtomic>(rec, goff, gnext, cur);
-        gnext = point_list[rg.x + (uint32_t)max(hi - 1 - 2 * kWave - lane, 0)];
+        gnext = point_list[rg.x + (uint32_t)max(hi - 1 - 2 * kWave - lane, (int)lo)];
         if (!kAtomic && lane < n && m == 0u) {  // in the live range but touches no pixel that needs it: zero record
             const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
             out[4 * (size_t)u + 0] = z;
@@ -863,24 +961,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
         }
         __syncthreads();
     }
-    if (zr.per4) {
-        // this workgroup's share of the frame's dense zero gradient rows (ZeroRows): issued after
-        // the replay, so no wait of the replay covers them -- the VALU-bound replay leaves HBM
-        // nearly idle, and preprocess_bwd no longer streams these bytes on its own
-        typedef float f4 __attribute__((ext_vector_type(4)));
-        const uint64_t q0 = (uint64_t)blockIdx.x * zr.per4, q1 = min(zr.c4[kZeroArrays], q0 + zr.per4);
-        for (uint64_t q = q0 + (uint64_t)lane; q < q1; q += kWave) {
-            int k = 0;
-#pragma unroll
-            for (int a = 1; a < kZeroArrays; a++) k += q >= zr.c4[a];
-            __builtin_nontemporal_store(f4{0.f, 0.f, 0.f, 0.f}, reinterpret_cast<f4 *>(zr.p[k]) + (q - zr.c4[k]));
-        }
-        if (blockIdx.x == 0 && lane < 4 * kZeroArrays) {  // the floats past each array's last whole float4
-            const int k = lane >> 2, t = lane & 3;
-            const uint64_t e = 4 * (zr.c4[k + 1] - zr.c4[k]) + (uint64_t)t;
-            if (e < zr.n[k]) __builtin_nontemporal_store(0.f, zr.p[k] + e);
-        }
-    }
+    bwd_zero_slice(zr);
     if (GSR_BLEND_STATS) {
         bst.flush(kBwdPairs);
         if (lane == 0) {
@@ -891,17 +972,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
     }
 }
 
+bool bwd_segments_supported() { return GSR_BWD_CLS && GSR_FWD_SUB == 1 && GSR_BWD_BG_IN_S && !GSR_TILE_REVERSE; }
+
 void launch_render_bwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                        const int *radii, const float *bg, const float *dL_dpix, const float *dL_dinvdepth,
-                       const BwdScratch &sc, hipStream_t s, const ZeroRows *zr) {
+                       const BwdScratch &sc, hipStream_t s, const ZeroRows *zr, uint32_t seg_len) {
     (void)radii;
     const int T = cam.gx * cam.gy;
     if (T == 0) return;
     const ZeroRows z = zr ? *zr : ZeroRows{};
+    const float *ck = nullptr;
+    const uint32_t *items = nullptr;
+    if (seg_len) {
+        ck = reinterpret_cast<const float *>(reinterpret_cast<const char *>(bs.point_list) + ck_offset(bs.cap));
+        items = reinterpret_cast<const uint32_t *>(ck + ck_slots(bs.cap, seg_len) * (kCkFloats * 256));
+    }
+    const unsigned grid = (unsigned)bwd_grid(T, bs.cap, seg_len);
 #define GSR_BWD_LAUNCH(D, A)                                                                                       \
-    hipLaunchKernelGGL((render_bwd_kernel<D, A>), dim3(T), dim3(kWave), 0, s, is.ranges, bs.point_list, cam.W, cam.H, \
-                       cam.gx, gs.rec, bg, is.final_T, is.n_contrib, dL_dpix, dL_dinvdepth, is.tile_order, gs.offsets, \
-                       is.boundary, A ? sc.acc : sc.rec, z, is.bwd_cnt, is.bwd_cls)
+    hipLaunchKernelGGL((render_bwd_kernel<D, A>), dim3(grid), dim3(kWave), 0, s, is.ranges, bs.point_list, cam.W,   \
+                       cam.H, cam.gx, gs.rec, bg, is.final_T, is.n_contrib, dL_dpix, dL_dinvdepth, is.tile_order,    \
+                       gs.offsets, is.boundary, A ? sc.acc : sc.rec, z, is.bwd_cnt, is.bwd_cls, (uint32_t)T, seg_len, \
+                       ck, items)
     if (dL_dinvdepth) {
         if (sc.atomic) GSR_BWD_LAUNCH(true, true);
         else GSR_BWD_LAUNCH(true, false);

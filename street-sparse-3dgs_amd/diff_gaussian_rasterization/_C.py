@@ -319,6 +319,15 @@ def set_binning(mode: int) -> int:
     return r
 
 
+def set_bwd_segment(length: int) -> int:
+    """Backward work split (gsr_set_bwd_segment): 0 = one workgroup per tile (default), L = a
+    multiple of 64 >= 512 = heavy tiles replayed as segments of L list positions.  Process-wide;
+    returns the previous length."""
+    r = _L.gsr_set_bwd_segment(int(length))
+    _check(0 if r >= 0 else r, "set_bwd_segment")
+    return r
+
+
 def reset_capacity_hint() -> None:
     """Forget this thread's point-list capacity hint (gsr_reset_capacity_hint)."""
     _L.gsr_reset_capacity_hint()

@@ -66,6 +66,7 @@ SIGNATURES = {
     "gsr_stage_times_ms": (_i, [ctypes.POINTER(_f), _i]),
     "gsr_forward_stats": (_i, [ctypes.POINTER(_i64), _i]),
     "gsr_reset_capacity_hint": (_i, []),
+    "gsr_set_bwd_segment": (_i, [_i]),
     "gsr_frame_stats": (_i, [_vp, _i, _i, _i, ctypes.POINTER(_i64), _i]),
     "gsr_blend_stats": (_i, [ctypes.POINTER(_i64), _i, _i]),
     "gsr_debug_trace": (_i, [ctypes.POINTER(_i64), _i, _i]),
@@ -123,7 +124,7 @@ SIGNATURES = {
     "gsr_zero_grad_rows": (_i, [_i, ctypes.POINTER(_vp), ctypes.POINTER(_i64), _i64, _i64, _vp, _i64, _vp]),
 }
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 _lib = None
 
 

@@ -1,0 +1,144 @@
+"""GPU tests of the backward work split (gsr_set_bwd_segment, render.hip): with a segment length L
+the forward checkpoints every pixel's transmittance and accumulated colour / inverse depth every L
+list positions of its tile, and the backward replays a tile whose last contributor lies past L as
+independent segments.  The split changes only where the replay starts, so:
+
+* forward outputs are bitwise those of the unsplit run;
+* gradients meet the same oracle bars as test_gpu_parity.py (GRAD_TOL 5e-5 relative L2) and agree
+  with the unsplit run to fp32 rounding (SEG_TOL);
+* the record (deterministic) mode stays bitwise reproducible with segments;
+* a backward uses the length its forward was made with, whatever the setting is in between.
+
+The scenes are translucent (opacity 0.004 .. 0.012) so that tiles keep thousands of contributors:
+tile work well past L, several segments per tile.
+"""
+from __future__ import annotations
+
+import contextlib
+
+import numpy as np
+import pytest
+
+from helpers import deterministic, rel_l2
+from test_gpu_parity import compare, make_scene, run_hip, run_oracle, upstream_grads
+
+pytestmark = pytest.mark.gpu
+
+SEG_TOL = 1e-5  # segmented vs unsplit gradients, relative L2 (fp32 rounding of S at the checkpoints; measured <= 2.2e-6)
+
+CASES = [
+    dict(name="seg_translucent_deg3", P=40000, W=96, H=64, deg=3, seed=21, log_scale=-2.0, opac=(0.004, 0.012)),
+    dict(name="seg_translucent_odd_deg1", P=60000, W=150, H=70, deg=1, seed=22, log_scale=-2.1, opac=(0.004, 0.012)),
+    dict(name="seg_no_depth", P=40000, W=96, H=64, deg=2, seed=23, log_scale=-2.0, opac=(0.004, 0.012), do_depth=False),
+    # opaque splats mixed in: pixels saturate at different segments of the same tile
+    dict(name="seg_mixed_opacity", P=40000, W=96, H=64, deg=3, seed=24, log_scale=-2.0, opac=(0.004, 0.012),
+         opaque=0.002),
+]
+
+
+def seg_scene(c):
+    s = make_scene(c)
+    rng = np.random.default_rng(c["seed"] + 7)
+    lo, hi = c["opac"]
+    op = rng.uniform(lo, hi, (c["P"], 1)).astype(np.float32)
+    if c.get("opaque"):
+        idx = rng.random(c["P"]) < c["opaque"]
+        op[idx] = rng.uniform(0.5, 0.99, (int(idx.sum()), 1)).astype(np.float32)
+    s["opacities"] = op
+    return s
+
+
+@contextlib.contextmanager
+def bwd_segment(L):
+    from diff_gaussian_rasterization import _C
+    prev = _C.set_bwd_segment(L)
+    try:
+        yield
+    finally:
+        _C.set_bwd_segment(prev)
+
+
+def max_tile_work(h, c):
+    nc = h["state"]["n_contrib"].reshape(c["H"], c["W"])
+    gy, gx = (c["H"] + 15) // 16, (c["W"] + 15) // 16
+    pad = np.zeros((gy * 16, gx * 16), nc.dtype)
+    pad[:c["H"], :c["W"]] = nc
+    return int(pad.reshape(gy, 16, gx, 16).max(axis=(1, 3)).max())
+
+
+@pytest.mark.parametrize("L", [512, 1024])
+@pytest.mark.parametrize("c", CASES, ids=[c["name"] for c in CASES])
+def test_segments_vs_oracle_and_unsplit(c, L):
+    s = seg_scene(c)
+    dcol, dinv = upstream_grads(c)
+    st, g = run_oracle(s, c, dcol, dinv)
+    base = run_hip(s, c, dcol, dinv)
+    with bwd_segment(L):
+        h = run_hip(s, c, dcol, dinv)
+    work = max_tile_work(h, c)
+    print(f"{c['name']} L={L}: max tile work {work}")
+    assert work > 2 * 1024, f"scene too light for the split: max tile work {work}"
+    compare(c, st, g, h)
+    # forward untouched (checkpoints are extra writes only)
+    np.testing.assert_array_equal(h["color"], base["color"])
+    np.testing.assert_array_equal(h["invdepth"], base["invdepth"])
+    np.testing.assert_array_equal(h["state"]["n_contrib"], base["state"]["n_contrib"])
+    for k, v in h["grads"].items():
+        if v is None:
+            continue
+        err = rel_l2(v, base["grads"][k])
+        assert err <= SEG_TOL, (k, err)
+
+
+def test_segments_deterministic_mode():
+    c = CASES[0]
+    s = seg_scene(c)
+    dcol, dinv = upstream_grads(c)
+    st, g = run_oracle(s, c, dcol, dinv)
+    with deterministic(), bwd_segment(512):
+        h1 = run_hip(s, c, dcol, dinv)
+        h2 = run_hip(s, c, dcol, dinv)
+    compare(c, st, g, h1)
+    for k, v in h1["grads"].items():
+        if v is not None:
+            np.testing.assert_array_equal(v, h2["grads"][k], err_msg=k)
+
+
+def test_backward_uses_the_forwards_length():
+    """Forward with L = 512, setting switched to 0 (and to 1024) before the backward: the backward
+    still cuts tiles at 512 (its items and checkpoints were published that way)."""
+    import torch
+    from diff_gaussian_rasterization import GaussianRasterizer, _C
+    from helpers import settings, torch_inputs
+    c = CASES[1]
+    s = seg_scene(c)
+    dcol, dinv = upstream_grads(c)
+    st, g = run_oracle(s, c, dcol, dinv)
+    dev = torch.device("cuda:0")
+    for later in (0, 1024):
+        inp = torch_inputs(s, dev)
+        rs = settings(s, dev, c["deg"])
+        with bwd_segment(512):
+            color, radii, invd = GaussianRasterizer(rs)(**inp)
+        with bwd_segment(later):
+            loss = (color * torch.tensor(dcol, device=dev)).sum() + (invd * torch.tensor(dinv, device=dev)).sum()
+            loss.backward()
+        torch.cuda.synchronize()
+        for hk, ok in (("means3D", "dL_dmeans3D"), ("opacities", "dL_dopacity"), ("shs", "dL_dsh"),
+                       ("scales", "dL_dscales"), ("rotations", "dL_drotations")):
+            err = rel_l2(inp[hk].grad.detach().cpu().numpy().reshape(g[ok].shape), g[ok])
+            assert err <= 5e-5, (later, hk, err)
+    assert _C.set_bwd_segment(0) == 0
+
+
+def test_set_bwd_segment_validation():
+    from diff_gaussian_rasterization import _C
+    prev = _C.set_bwd_segment(0)
+    try:
+        for bad in (-64, 64, 448, 520):
+            with pytest.raises(RuntimeError):
+                _C.set_bwd_segment(bad)
+        assert _C.set_bwd_segment(2048) == 0
+        assert _C.set_bwd_segment(512) == 2048
+    finally:
+        _C.set_bwd_segment(prev)

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--iters", type=int, default=12000)
     ap.add_argument("--views", type=int, default=8)
     ap.add_argument("--size", type=int, default=1536)
+    ap.add_argument("--segs", default="0,512,1024,2048,4096", help="backward segment lengths to time (A/B)")
+    ap.add_argument("--reps", type=int, default=10)
     a = ap.parse_args()
     import torch
     from diff_gaussian_rasterization import _C
@@ -76,9 +78,80 @@ def main():
             "bwd_work": {"mean": float(work.mean()), "p50": float(np.median(work)), "p99": float(np.percentile(work, 99)),
                          "max": int(ws[0]), "top8": ws[:8].tolist(), "sum": int(work.sum()),
                          "top1pct_share": float(ws[:T // 100].sum() / max(1, ws.sum()))}})
+        out["views"][-1]["bwd_ms_by_seg"] = time_segments(g, c, H, W, [int(x) for x in a.segs.split(",")], a.reps)
         done += 1
         k += 1
     print(json.dumps(out))
+
+
+def time_segments(g, c, H, W, segs, reps):
+    """fwd+bwd of one view through the public rasterizer per backward segment length: the stage
+    times (render_bwd, render_fwd) and the fwd+bwd wall time, medians over reps."""
+    import torch
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer, _C
+    dev = g._xyz.device
+    rs = GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=float(c["tx"]), tanfovy=float(c["ty"]),
+        bg=torch.zeros(3, device=dev), scale_modifier=1.0, viewmatrix=c["view"], projmatrix=c["proj"],
+        sh_degree=g.active_sh_degree, campos=c["campos"], prefiltered=False, debug=False, do_depth=True,
+        render_indices=torch.empty(0, dtype=torch.int32), parent_indices=torch.empty(0, dtype=torch.int32),
+        interpolation_weights=torch.empty(0, dtype=torch.float32, device=dev),
+        num_node_kids=torch.empty(0, dtype=torch.int32, device=dev))
+    gen = torch.Generator(device=dev).manual_seed(5)
+    up_c = torch.randn(3, H, W, generator=gen, device=dev) * 1e-3
+    up_d = torch.randn(1, H, W, generator=gen, device=dev) * 1e-3
+    res = {}
+    ref = ref_det = None
+
+    def det_grads():
+        prev_det = _C.set_deterministic(True)
+        xs = [t.detach().clone().requires_grad_(True) for t in
+              (g._xyz, g._features, torch.sigmoid(g._opacity), torch.exp(g._scaling),
+               torch.nn.functional.normalize(g._rotation))]
+        col, _, invd = GaussianRasterizer(rs)(means3D=xs[0], means2D=torch.zeros_like(g._xyz, requires_grad=True),
+                                              shs=xs[1], opacities=xs[2], scales=xs[3], rotations=xs[4])
+        ((col * up_c).sum() + (invd * up_d).sum()).backward()
+        _C.set_deterministic(prev_det)
+        return [x.grad for x in xs]
+
+    rel = lambda ga, gb: max(float((a - b).norm() / b.norm().clamp_min(1e-30)) for a, b in zip(ga, gb))
+    for L in segs:
+        prev = _C.set_bwd_segment(L)
+        st_all, wall, last2 = [], [], []
+        for r in range(reps + 2):
+            xs = [t.detach().clone().requires_grad_(True) for t in
+                  (g._xyz, g._features, torch.sigmoid(g._opacity), torch.exp(g._scaling),
+                   torch.nn.functional.normalize(g._rotation))]
+            m2 = torch.zeros_like(g._xyz, requires_grad=True)
+            _C.set_profiling(True)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            col, _, invd = GaussianRasterizer(rs)(means3D=xs[0], means2D=m2, shs=xs[1], opacities=xs[2],
+                                                  scales=xs[3], rotations=xs[4])
+            ((col * up_c).sum() + (invd * up_d).sum()).backward()
+            e1.record()
+            torch.cuda.synchronize()
+            st = _C.stage_times_ms()
+            _C.set_profiling(False)
+            if r >= 2:
+                st_all.append(st)
+                wall.append(e0.elapsed_time(e1))
+            last2 = (last2 + [[x.grad for x in xs]])[-2:]
+        grads = last2[-1]
+        if ref is None:
+            ref = grads
+        gd = det_grads()
+        if ref_det is None:
+            ref_det = gd
+        _C.set_bwd_segment(prev)
+        med = lambda k: float(np.median([s_[k] for s_ in st_all]))
+        # grad errors (max over tensors of relative L2): atomic vs the first length's atomic run, the
+        # run-to-run atomic noise at this length, and record mode (bitwise ordered sums) vs the first
+        # length's record mode -- the split's own rounding
+        res[str(L)] = {"render_bwd": round(med("render_bwd"), 4), "render_fwd": round(med("render_fwd"), 4),
+                       "fwd_bwd_wall": round(float(np.median(wall)), 4), "grad_rel_l2_vs_first": rel(grads, ref),
+                       "atomic_noise": rel(last2[0], last2[1]), "det_grad_rel_l2_vs_first": rel(gd, ref_det)}
+    return res
 
 
 if __name__ == "__main__":
