@@ -72,6 +72,8 @@ def parse():
                     help="leaves of the train_post step's synthetic hierarchy (0 = skip that step)")
     ap.add_argument("--bwd-seg", type=int, default=None,
                     help="backward segment length (gsr_set_bwd_segment; default: the library's setting)")
+    ap.add_argument("--fwd-seg", type=int, default=None,
+                    help="forward segment length (gsr_set_fwd_segment; default: the library's setting)")
     ap.add_argument("--train-baseline", action="store_true",
                     help="also time the reference-structured torch train step (oracle/train_torch_ref.py: conv2d "
                          "SSIM, OurAdam gather/scatter) -- a baseline leg, like cpu_baseline")
@@ -865,8 +867,12 @@ def main():
     from diff_gaussian_rasterization import _C as _gsr
     if a.bwd_seg is not None:
         _gsr.set_bwd_segment(a.bwd_seg)
+    if a.fwd_seg is not None:
+        _gsr.set_fwd_segment(a.fwd_seg)
     bwd_seg = _gsr.set_bwd_segment(0)
     _gsr.set_bwd_segment(bwd_seg)
+    fwd_seg = _gsr.set_fwd_segment(0)
+    _gsr.set_fwd_segment(fwd_seg)
     P, W, H, deg = a.gaussians, a.width, a.height, a.sh_degree
     s, inp, gcol, ginv = make_inputs(P, W, H, deg, seed=rank, device=dev)
     rs, raster = rasterizer_for(s, W, H, deg, dev)
@@ -952,7 +958,7 @@ def main():
         "data": "synthetic (seeded Gaussians in the frustum, SURVEY.md 8(d); one chunk per rank, seed = rank)",
         "config": {"workload": f"rasterizer fwd+bwd, {P} Gaussians, SH degree {deg}, {W}x{H}, do_depth",
                    "gaussians": P, "width": W, "height": H, "sh_degree": deg, "visible": Pv, "tile_instances": K,
-                   "level1_entries": P1, "live_rows": Pl, "tiles": T, "bwd_segment": bwd_seg,
+                   "level1_entries": P1, "live_rows": Pl, "tiles": T, "bwd_segment": bwd_seg, "fwd_segment": fwd_seg,
                    "parallelism": f"chunk-per-gpu x{world}"},
         # frac: algorithmic bytes / the kernel's HIP-event time measured here; frac_rocprof: the same
         # bytes / the average duration in the committed rocprofv3 summary of these kernel sources

@@ -161,6 +161,16 @@ int gsr_set_deterministic(int enable);
  * previous length, or GSR_ERR_INVALID_ARGUMENT / GSR_ERR_UNSUPPORTED. */
 int gsr_set_bwd_segment(int L);
 
+/* Forward work split, process-wide.  L = 0 (default): render_fwd blends every tile in one
+ * workgroup.  L > 0 (a multiple of 64, >= 4096): a tile whose list is longer than L is blended as
+ * ceil(len / L) work items by a pool of worker workgroups -- each item multiplies out the
+ * transmittance through its positions, takes its predecessors' product (a decoupled lookback) and
+ * blends its positions from there; the tile's last item adds the items' colours in order.  Colours
+ * agree with the one-workgroup blend to fp32 summation order; the stop rule is the same up to an
+ * ulp of the transmittance product.  Returns the previous length, or GSR_ERR_INVALID_ARGUMENT /
+ * GSR_ERR_UNSUPPORTED. */
+int gsr_set_fwd_segment(int L);
+
 /* Depth-order strategy of the binning, process-wide.  0: the local sort -- level 1 in Gaussian
  * index order, each superblock list sorted by depth in LDS -- except for frames forwarded in
  * deterministic mode and frames with a superblock list longer than the LDS sort holds, which take

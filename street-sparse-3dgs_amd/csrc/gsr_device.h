@@ -476,10 +476,56 @@ constexpr int kBwdSegCount = kBwdClasses;  // bwd_cnt[kBwdSegCount]: full segmen
 constexpr int kCkFloats = 5;               // T, behind r, g, b, inverse depth (x 256 pixels per slot)
 __host__ __device__ __forceinline__ size_t ck_offset(int64_t K) { return (size_t)(((4 * K) + 255) / 256 * 256); }
 __host__ __device__ __forceinline__ size_t ck_slots(int64_t K, uint32_t L) { return L ? (size_t)(K / L) + 2 : 0; }
-constexpr uint32_t kMinBwdSeg = 512;     // the shortest segment: checkpoints + list fit in 16 B / instance + kSegReserve
-constexpr size_t kSegReserve = 16384;    // carved past the level-1 lists (a small K's checkpoint slots)
+constexpr uint32_t kMinBwdSeg = 512;     // the shortest segment (with kMinFwdSeg: all fits in 16 B / instance + kSegReserve)
+constexpr size_t kSegReserve = 32768;    // carved past the level-1 lists (a small K's slots)
 // render_bwd's grid: every tile's last segment plus at most K / L full segments
 inline int64_t bwd_grid(int T, int64_t K, uint32_t L) { return (int64_t)T + (L ? K / L : 0); }
+__host__ __device__ __forceinline__ size_t align256(size_t b) { return (b + 255) / 256 * 256; }
+
+// Forward segments (gsr_set_fwd_segment): a tile whose list is longer than 2 Lf positions is
+// blended as ceil(len / Lf) work items by render_fwd_seg_kernel's kFwdWorkers workgroups (an item
+// queue tile_order fills), launched before render_fwd.  Item s first multiplies out (1 - alpha) over its positions (the pixels'
+// transmittance through the segment), publishes it and takes the product of its predecessors'
+// (a decoupled lookback per pixel), then blends its positions from that transmittance with the
+// usual stop rule; the tile's last item to finish sums the items' colours in order and writes the
+// pixels.  Per item, past the backward's region: its queue entry, a ticket (the tile's first
+// item's counts the finished items), a lookback flag (0 none, 1 the segment's own transmittance
+// published, 2 the product through it; zeroed with the queue), 4 checkpoint counts, the two
+// per-pixel transmittance rows and 256 x 6 partials.
+constexpr uint32_t kMinFwdSeg = 4096;
+// a tile is split when its list holds more than two segments (3+ items: with two, the second
+// item's wait for the first one's transmittance pass leaves little to gain)
+__host__ __device__ __forceinline__ bool fseg_splits(uint32_t len, uint32_t Lf) { return Lf && len > 2u * Lf; }
+constexpr int kFwdWorkers = 256;
+constexpr int kFwdPartials = 6;  // r, g, b, inverse depth, T at the end, last contributor | stop << 31
+// bwd_cnt's words past the backward's: the item count tile_order wrote, the queue's next item
+constexpr int kFwdItemsWord = kBwdSegCount + 1, kFwdNextWord = kBwdSegCount + 2;
+struct FwdSegLayout {
+    uint32_t *items, *tickets, *flags, *nc;
+    float *agg, *incl;  // per item x 256 pixels: the segment's own transmittance, the product through it
+    float *part;
+};
+__host__ __device__ __forceinline__ size_t fseg_max_items(int64_t K, uint32_t Lf) { return Lf ? (size_t)(2 * K / Lf) + 2 : 0; }
+__host__ __device__ __forceinline__ FwdSegLayout fseg_layout(void *bin_base, int64_t K, uint32_t L, uint32_t Lf) {
+    const size_t n = fseg_max_items(K, Lf);
+    size_t off = ck_offset(K) + (L ? align256(ck_slots(K, L) * (kCkFloats * 256) * 4 + ck_slots(K, L) * 4) : 0);
+    char *b = static_cast<char *>(bin_base);
+    FwdSegLayout f;
+    f.items = reinterpret_cast<uint32_t *>(b + off);
+    off = align256(off + 4 * n);
+    f.tickets = reinterpret_cast<uint32_t *>(b + off);
+    off = align256(off + 4 * n);
+    f.flags = reinterpret_cast<uint32_t *>(b + off);
+    off = align256(off + 4 * n);
+    f.nc = reinterpret_cast<uint32_t *>(b + off);
+    off = align256(off + 16 * n);
+    f.agg = reinterpret_cast<float *>(b + off);
+    off = align256(off + 4 * 256 * n);
+    f.incl = reinterpret_cast<float *>(b + off);
+    off = align256(off + 4 * 256 * n);
+    f.part = reinterpret_cast<float *>(b + off);
+    return f;
+}
 
 #ifndef GSR_RECT4
 #define GSR_RECT4 1

@@ -43,8 +43,11 @@ bool color_split_supported(const GaussianInputs &in);
 void launch_preprocess_color(const GaussianInputs &in, const Camera &cam, const GeomState &gs, const int *radii,
                              hipStream_t s, int blocks = 0);
 // render.hip: tiles ordered heaviest first by work[t] (or, with work == NULL, by list length).
+// fctl != NULL and fseg_len != 0: also the forward segments' item queue (FwdSegLayout in the
+// binning buffer at bin_base; fctl = bwd_cnt + kFwdItemsWord).
 void launch_tile_order(const uint32_t *work, const uint2 *ranges, int T, int shift, uint32_t *order, hipStream_t s,
-                       const uint32_t *kdev = nullptr, uint32_t cap = 0, uint32_t *zero_classes = nullptr);
+                       const uint32_t *kdev = nullptr, uint32_t cap = 0, uint32_t *zero_classes = nullptr,
+                       uint32_t *fctl = nullptr, void *bin_base = nullptr, uint32_t seg_len = 0, uint32_t fseg_len = 0);
 void launch_mark_visible(int P, const float *means3D, const float *view, uint8_t *present, hipStream_t s);
 
 // sort.hip (rocPRIM)
@@ -108,13 +111,14 @@ struct ZeroRows {
 // render.hip
 void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                        const float *bg, float *out_color, float *out_invdepth, hipStream_t s, bool need_bwd = true,
-                       bool sb_order = false, uint32_t seg_len = 0);
+                       bool sb_order = false, uint32_t seg_len = 0, uint32_t fseg_len = 0);
 // seg_len != 0: the backward's heavy tiles are cut into segments of seg_len list positions
 // (gsr_set_bwd_segment; the backward must get the value its forward was made with)
 void launch_render_bwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                        const int *radii, const float *bg, const float *dL_dpix, const float *dL_dinvdepth,
                        const BwdScratch &sc, hipStream_t s, const ZeroRows *zr = nullptr, uint32_t seg_len = 0);
 bool bwd_segments_supported();
+bool fwd_segments_supported();
 
 // backward.hip
 // sparse_rows (the native train step only, set_sparse_grad_rows): the rows of Gaussians with ten

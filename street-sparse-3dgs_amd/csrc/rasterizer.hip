@@ -405,6 +405,10 @@ uint8_t forward_uncleared(const void *geom) {
 #define GSR_BWD_SEG_DEFAULT 0
 #endif
 std::atomic<uint32_t> g_bwd_seg{GSR_BWD_SEG_DEFAULT};
+#ifndef GSR_FWD_SEG_DEFAULT
+#define GSR_FWD_SEG_DEFAULT 0
+#endif
+std::atomic<uint32_t> g_fwd_seg{GSR_FWD_SEG_DEFAULT};
 std::mutex g_seg_mu;
 std::unordered_map<const void *, uint32_t> g_seg_of;
 void note_forward_seg(const void *image, uint32_t L) {
@@ -723,10 +727,13 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
     if (split && !GSR_COLOR_SERIAL && !color_early && (rc = fork_color())) return rc;
     bool joined = false;
     const uint32_t seg_req = need_bwd && bwd_segments_supported() ? g_bwd_seg.load(std::memory_order_relaxed) : 0u;
+    const uint32_t fseg_req = fwd_segments_supported() && !sb_order ? g_fwd_seg.load(std::memory_order_relaxed) : 0u;
     uint32_t seg_used = 0;
     auto bin_and_render = [&](int64_t cap, bool counted) -> int {
-        // backward items are numbered tile + T * segment (32 bits)
+        // backward / forward items are numbered tile + T * segment (32 bits)
         seg_used = seg_req && (uint64_t)T * (uint64_t)(cap / seg_req + 1) < (1ull << 32) ? seg_req : 0u;
+        const uint32_t fseg_used =
+            fseg_req && cap > 0 && (uint64_t)T * (uint64_t)(cap / fseg_req + 1) < (1ull << 32) ? fseg_req : 0u;
         size_t bbytes = 0;
         carve_binning(nullptr, cap, &bbytes);
         void *bbase = binning_buffer(resize_ctx, bbytes);
@@ -750,7 +757,8 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
             StageTimer st(4, s);
             // forward order: by list length (and the backward's class counters zeroed)
             launch_tile_order(nullptr, is.ranges, T, 4, is.tile_ids, s, bs.kdev, bs.cap,
-                              GSR_BWD_CLS && need_bwd ? is.bwd_cnt : nullptr);
+                              GSR_BWD_CLS && need_bwd ? is.bwd_cnt : nullptr, is.bwd_cnt + kFwdItemsWord, bs.point_list,
+                              seg_used, fseg_used);
         }
         if ((r = check("tile order", debug, s))) return r;
         if (split && !GSR_COLOR_SERIAL && !joined) {
@@ -760,7 +768,8 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
         }
         {
             StageTimer st(5, s);
-            launch_render_fwd(cam, gs, bs, is, background, out_color, out_invdepth, s, need_bwd, sb_order, seg_used);
+            launch_render_fwd(cam, gs, bs, is, background, out_color, out_invdepth, s, need_bwd, sb_order, seg_used,
+                              fseg_used);
         }
         if (need_bwd && !GSR_BWD_CLS) {
             StageTimer st(9, s);  // backward launch order, from the forward's per-tile work
@@ -940,6 +949,14 @@ int gsr_set_true_scale_gradient(int enable) {
 }
 
 int gsr_set_deterministic(int enable) { return g_deterministic.exchange(enable ? 1 : 0); }
+
+int gsr_set_fwd_segment(int L) {
+    if (L < 0 || (L > 0 && (L < (int)kMinFwdSeg || L % kWave != 0)))
+        return fail(GSR_ERR_INVALID_ARGUMENT, "forward segment length: 0 (off) or a multiple of 64 >= 4096");
+    if (L > 0 && !fwd_segments_supported())
+        return fail(GSR_ERR_UNSUPPORTED, "forward segments need the list-length launch order and the 1-row sub-block forward");
+    return (int)g_fwd_seg.exchange((uint32_t)L);
+}
 
 int gsr_set_bwd_segment(int L) {
     if (L < 0 || (L > 0 && (L < (int)kMinBwdSeg || L % kWave != 0)))

@@ -21,6 +21,7 @@
 // deterministic mode, as one 64-B record per instance at its Gaussian-major index, summed by
 // backward.hip in a fixed order (bitwise reproducible).  Only instances in front of the tile's
 // last contributor are visited (13% of them on the 1M-Gaussian bench scene).
+#include <atomic>
 #include <type_traits>
 
 #include "gsr_launch.h"
@@ -164,6 +165,306 @@ __device__ __forceinline__ uint32_t sub_block_mask_n(const float4 &qa, const flo
     return m;
 }
 
+// The tile's backward work (last contributor position): tile_work, and with bwd_cnt its slot in
+// the backward's heaviest-first class lists.  With backward segments (seg_len != 0) a tile of more
+// than seg_len positions of work is cut into ceil(work / seg_len) backward items (tile + ntiles *
+// segment): all but the last go to the segment list (past the checkpoints), run first; the last one
+// goes into its work class like a whole tile.
+__device__ __forceinline__ void fwd_publish(uint32_t mx, int tile, uint32_t *__restrict__ tile_work,
+                                            uint32_t *__restrict__ bwd_cnt, uint32_t *__restrict__ bwd_cls, int ntiles,
+                                            uint32_t seg_len, float *ck, uint32_t kf) {
+    tile_work[tile] = mx;
+    if (!bwd_cnt) return;
+    uint32_t item = (uint32_t)tile, wk = mx;
+    if (seg_len && mx > seg_len) {
+        const uint32_t nseg = (mx + seg_len - 1u) / seg_len;
+        uint32_t *items = reinterpret_cast<uint32_t *>(ck + ck_slots(kf, seg_len) * (kCkFloats * 256));
+        const uint32_t b = atomicAdd(&bwd_cnt[kBwdSegCount], nseg - 1u);
+        for (uint32_t sgi = 0; sgi + 1u < nseg; sgi++) items[b + sgi] = (uint32_t)tile + (uint32_t)ntiles * sgi;
+        item = (uint32_t)tile + (uint32_t)ntiles * (nseg - 1u);
+        wk = mx - (nseg - 1u) * seg_len;
+    }
+    const uint32_t k = wk >> kBwdClassShift;
+    const uint32_t c = (uint32_t)(kBwdClasses - 1) - (k < (uint32_t)(kBwdClasses - 1) ? k : (uint32_t)(kBwdClasses - 1));
+    const uint32_t r = atomicAdd(&bwd_cnt[c], 1u);
+    bwd_cls[(size_t)c * ntiles + r] = item;
+}
+
+
+// One wave's pass over list positions [p0, p1) of its 16x4 sub-block (forward segments), with the
+// arithmetic of render_fwd's blend (kSub 1, wave masks).
+// kBlend = false: the transmittance through the positions -- T *= 1 - alpha for every alpha the
+//   blend would take (inside the ellipse, alpha >= 1/255) -- without the stop rule; a lane whose
+//   product fell below 1e-4 leaves (any later position stops at its first contributor anyway).
+// kBlend = true: the blend from the lane's T with the stop rule (stopm: lanes that stopped here)
+//   and the backward checkpoints (colour accumulated in front of them since p0).
+template <bool kBlend>
+__device__ __forceinline__ void fwd_seg_pass(const uint32_t *__restrict__ point_list, const GRec *__restrict__ rec,
+                                             uint32_t rgx, uint32_t p0, uint32_t p1, float4 *sa, float4 *sb, float4 *sc,
+                                             float pfx, float pfy, float tx0, float sy0, uint64_t &livem, uint64_t &stopm,
+                                             float &T, float &C0, float &C1, float &C2, float &ID, uint32_t &last,
+                                             float *ck, uint32_t seg_len, uint32_t &ncross) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t lastpos = p1 - 1u;
+    FwdBatch cur;
+    fwd_gather(rec, point_list[min(p0 + (uint32_t)lane, lastpos)], cur);
+    uint32_t gnext = point_list[min(p0 + kWave + (uint32_t)lane, lastpos)];
+    for (uint32_t base = p0; base < p1; base += kWave) {
+        if (!livem) break;
+        if (kBlend && ck && base > rgx && (base - rgx) % seg_len == 0u) {
+            float *c = ck + (size_t)(base / seg_len) * (kCkFloats * 256) + w * kWave + lane;
+            c[0] = T;
+            c[256] = C0;
+            c[512] = C1;
+            c[768] = C2;
+            c[1024] = ID;
+            ncross++;
+        }
+        const bool valid = base + (uint32_t)lane < p1;
+        const float4 qa = cur.a, qb = cur.b, qc = cur.c;
+        const uint32_t m = valid ? sub_block_mask_n<1>(qa, qb, cur.tm, tx0, sy0) : 0u;
+        fwd_gather(rec, gnext, cur);
+        gnext = point_list[min(base + 2 * kWave + (uint32_t)lane, lastpos)];
+        const uint64_t keep = __ballot(m != 0u);
+        const uint32_t cnt = (uint32_t)__popcll(keep);
+        if (m) {
+            const uint32_t slot = lane_prefix(keep);
+            sa[slot] = make_float4(qa.x, qa.y, qa.z * kHalfLog2e, qa.w * kLog2e);
+            sb[slot] = make_float4(qb.x * kHalfLog2e, qb.y, 0.f, __uint_as_float(base - rgx + (uint32_t)lane + 1u));
+            if (kBlend) sc[slot] = qc;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t j = 0; j < cnt; j++) {
+            const float4 a = sa[j];
+            const float4 b = sb[j];
+            const float dx = a.x - pfx;
+            const float adxdx_s = a.z * dx * dx;
+            const float bdx_s = a.w * dx;
+            const float dy = a.y - pfy;
+            const float p2 = gauss_p2(adxdx_s, bdx_s, b.x, dy);
+            const float alpha = fminf(0.99f, b.y * gexp2(p2));
+            const uint64_t okm = livem & __builtin_amdgcn_fcmpf(p2, 0.0f, kFcmpULE) &
+                                 __builtin_amdgcn_fcmpf(alpha, 1.0f / 255.0f, kFcmpUGE);
+            const float test_T = T * (1.f - alpha);
+            if (kBlend) {
+                const float4 c = sc[j];
+                const uint64_t contm = __builtin_amdgcn_fcmpf(test_T, 0.0001f, kFcmpUGE);
+                const uint64_t accm = okm & contm;
+                stopm |= okm & ~contm;
+                livem &= ~okm | contm;
+                const float wgt = lane_select(accm, alpha * T, 0.f);
+                C0 = fmaf(c.x, wgt, C0);
+                C1 = fmaf(c.y, wgt, C1);
+                C2 = fmaf(c.z, wgt, C2);
+                ID = fmaf(c.w, wgt, ID);
+                T = lane_select(accm, test_T, T);
+                last = __float_as_uint(lane_select(accm, b.w, __uint_as_float(last)));
+            } else {
+                T = lane_select(okm, test_T, T);
+                livem &= __builtin_amdgcn_fcmpf(T, 0.0001f, kFcmpUGE);
+            }
+            if (!livem) break;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// a forward item's lookback row is complete: every thread's stores made visible device-wide (all
+// XCDs' L2s), then the flag
+__device__ __forceinline__ void seg_publish(uint32_t *flag, uint32_t v) {
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// render_fwd_seg_kernel's workgroups (forward segments): items from the queue tile_order
+// filled until it is empty (FwdSegLayout).  Item i = segment s of its tile: (1) the transmittance
+// through the segment (skipped for the tile's last segment) published per pixel; (2) the product of
+// the predecessors' -- a decoupled lookback over per-item flags (1: the segment's own row is
+// published, 2: the product through it), each row made visible with a release fence before its flag
+// (items of a tile are taken in order, so every predecessor's workgroup is resident); (3) the blend from that transmittance into the item's partials; (4) the
+// tile's last item to finish (a ticket) adds the partials in segment order (up to the pixel's stop),
+// turns the backward checkpoints into colour-behind and writes the tile's pixels.
+__device__ void fwd_seg_worker(const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list, int W, int H,
+                               int gx, const GRec *__restrict__ rec, const float *__restrict__ bg, float *__restrict__ out_color,
+                               float *__restrict__ out_invd, float *__restrict__ final_T, uint32_t *__restrict__ n_contrib,
+                               uint32_t *__restrict__ tile_work, uint32_t kf, const uint32_t *__restrict__ sort_err,
+                               uint32_t *__restrict__ bwd_cnt, uint32_t *__restrict__ bwd_cls, int ntiles, uint32_t seg_len,
+                               uint32_t fseg_len, uint32_t *bin_base, uint32_t *fctl, float4 *sa, float4 *sb,
+                               float4 *sc, uint32_t *s_work, uint32_t *s_scalar) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const FwdSegLayout f = fseg_layout(bin_base, kf, seg_len, fseg_len);
+    float *ck = seg_len && bwd_cnt ? reinterpret_cast<float *>(reinterpret_cast<char *>(bin_base) + ck_offset(kf)) : nullptr;
+    const uint32_t nitems = fctl[0];
+    for (;;) {
+        if (threadIdx.x == 0) s_scalar[0] = __hip_atomic_fetch_add(&fctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const uint32_t i = s_scalar[0];
+        __syncthreads();
+        if (i >= nitems) return;
+        const uint32_t item = f.items[i];
+        const int tile = (int)(item % (uint32_t)ntiles);
+        const uint32_t sgi = item / (uint32_t)ntiles;
+        const uint2 rg = ranges[tile];
+        const uint32_t nseg = (rg.y - rg.x + fseg_len - 1u) / fseg_len;
+        const uint32_t p0 = rg.x + sgi * fseg_len, p1 = min(p0 + fseg_len, rg.y);
+        const uint32_t i0 = i - sgi;  // the tile's first item
+        const int tx = tile % gx, ty = tile / gx;
+        const int px = tx * kTile + (lane & 15), py = ty * kTile + 4 * w + (lane >> 4);
+        const bool inside = px < W && py < H;
+        const float pfx = (float)px, pfy = (float)py, tx0 = (float)(tx * kTile), sy0 = (float)(ty * kTile + 4 * w);
+        const uint64_t insm = __ballot(inside);
+        float Ta = 1.f, d0 = 0.f, d1 = 0.f, d2 = 0.f, d3 = 0.f;
+        uint32_t du = 0, dn = 0;
+        if (sgi + 1u < nseg) {  // (1)
+            uint64_t lm = insm, sm = 0;
+            fwd_seg_pass<false>(point_list, rec, rg.x, p0, p1, sa, sb, sc, pfx, pfy, tx0, sy0, lm, sm, Ta, d0, d1, d2, d3,
+                                du, nullptr, 0u, dn);
+            Ta = Ta < 0.0001f ? 0.f : Ta;
+            (sgi == 0 ? f.incl : f.agg)[(size_t)i * 256 + threadIdx.x] = Ta;
+            seg_publish(f.flags + i, sgi == 0 ? 2u : 1u);
+        }
+        float Tin = 1.f;
+        bool hung = false;
+        if (sgi > 0) {  // (2) the predecessors' rows back to the nearest product-through
+            float prod = 1.f;
+            for (uint32_t j = sgi - 1u;; j--) {
+                if (threadIdx.x == 0) {
+                    uint32_t fl = 0;
+                    for (uint32_t spins = 0; spins < (1u << 22); spins++) {
+                        fl = __hip_atomic_load(f.flags + i0 + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                        if (fl) break;
+                        __builtin_amdgcn_s_sleep(2);
+                    }
+                    s_scalar[2] = fl;
+                }
+                __syncthreads();
+                const uint32_t fl = s_scalar[2];
+                __syncthreads();
+                if (fl == 0u || (fl == 1u && j == 0u)) {  // never expected: the tile's pixels become NaN (loud)
+                    hung = true;
+                    break;
+                }
+                __threadfence();
+                if (fl == 2u) {
+                    prod *= f.incl[(size_t)(i0 + j) * 256 + threadIdx.x];
+                    break;
+                }
+                prod *= f.agg[(size_t)(i0 + j) * 256 + threadIdx.x];
+            }
+            Tin = prod;
+            if (sgi + 1u < nseg) {
+                f.incl[(size_t)i * 256 + threadIdx.x] = Tin * Ta;
+                seg_publish(f.flags + i, 2u);
+            }
+        }
+        // (3)
+        float T = Tin, C0 = 0.f, C1 = 0.f, C2 = 0.f, ID = 0.f;
+        uint32_t last = 0, ncross = 0;
+        {
+            uint64_t lm = insm, sm = 0;
+            fwd_seg_pass<true>(point_list, rec, rg.x, p0, p1, sa, sb, sc, pfx, pfy, tx0, sy0, lm, sm, T, C0, C1, C2, ID,
+                               last, ck, seg_len, ncross);
+            float *q = f.part + (size_t)i * (kFwdPartials * 256) + threadIdx.x;
+            q[0] = C0;
+            q[256] = C1;
+            q[512] = C2;
+            q[768] = ID;
+            q[1024] = T;
+            q[1280] = __uint_as_float(last | (((sm >> lane) & 1ull) ? 0x80000000u : 0u) | (hung ? 0x40000000u : 0u));
+            if (lane == 0) f.nc[(size_t)i * 4 + w] = ncross;
+        }
+        __threadfence();
+        __syncthreads();
+        if (threadIdx.x == 0)
+            s_scalar[1] = __hip_atomic_fetch_add(&f.tickets[i0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        if (s_scalar[1] + 1u != nseg) continue;
+        __threadfence();
+        // (4) the tile's pixels: partials added in segment order up to the segment the pixel stopped in
+        float A0 = 0.f, A1 = 0.f, A2 = 0.f, A3 = 0.f, Tf = 1.f;
+        uint32_t lp = 0;
+        bool bad = sort_err && *sort_err;
+        for (uint32_t k = 0; k < nseg; k++) {
+            const float *q = f.part + (size_t)(i0 + k) * (kFwdPartials * 256) + threadIdx.x;
+            const uint32_t lw = __float_as_uint(q[1280]);
+            A0 += q[0];
+            A1 += q[256];
+            A2 += q[512];
+            A3 += q[768];
+            Tf = q[1024];
+            if (lw & 0x3FFFFFFFu) lp = lw & 0x3FFFFFFFu;
+            bad = bad || (lw & 0x40000000u);
+            if (lw & 0x80000000u) break;
+        }
+        if (ck) {
+            // backward checkpoints: colour in front (the segments before + the segment's own part in
+            // front of the checkpoint) -> colour still to come, B = C_final - C(in front)
+            float P0 = 0.f, P1 = 0.f, P2 = 0.f, P3 = 0.f;
+            bool stopped = false;
+            for (uint32_t k = 0; k < nseg; k++) {
+                const uint32_t nc = f.nc[(size_t)(i0 + k) * 4 + w];
+                const uint32_t m0 = max(1u, (k * fseg_len + seg_len - 1u) / seg_len);
+                for (uint32_t m = 0; m < nc; m++) {
+                    float *c = ck + (size_t)((rg.x + (m0 + m) * seg_len) / seg_len) * (kCkFloats * 256) + w * kWave + lane;
+                    c[256] = A0 - (P0 + c[256]);
+                    c[512] = A1 - (P1 + c[512]);
+                    c[768] = A2 - (P2 + c[768]);
+                    c[1024] = A3 - (P3 + c[1024]);
+                }
+                if (!stopped) {
+                    const float *q = f.part + (size_t)(i0 + k) * (kFwdPartials * 256) + threadIdx.x;
+                    P0 += q[0];
+                    P1 += q[256];
+                    P2 += q[512];
+                    P3 += q[768];
+                    stopped = (__float_as_uint(q[1280]) & 0x80000000u) != 0u;
+                }
+            }
+        }
+        if (inside) {
+            const int pix = py * W + px;
+            const float nan = __builtin_nanf("");
+            final_T[pix] = Tf;
+            n_contrib[pix] = lp;
+            out_color[pix] = bad ? nan : A0 + Tf * bg[0];
+            out_color[H * W + pix] = bad ? nan : A1 + Tf * bg[1];
+            out_color[2 * H * W + pix] = bad ? nan : A2 + Tf * bg[2];
+            if (out_invd) out_invd[pix] = bad ? nan : A3;
+        }
+        const uint32_t wl = wave_max_u32(lp);
+        if (lane == 0) s_work[w] = wl;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t mx = s_work[0];
+            for (int k = 1; k < kPixPerLane; k++) mx = s_work[k] > mx ? s_work[k] : mx;
+            fwd_publish(mx, tile, tile_work, bwd_cnt, bwd_cls, ntiles, ck ? seg_len : 0u, ck, kf);
+        }
+        __syncthreads();
+    }
+}
+
+// Forward segments' worker pool: kFwdWorkers workgroups, launched before render_fwd (which skips
+// the split tiles), until the item queue is empty.
+__global__ __launch_bounds__(kWave * kPixPerLane) void render_fwd_seg_kernel(
+    const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list, int W, int H, int gx,
+    const GRec *__restrict__ rec, const float *__restrict__ bg, float *__restrict__ out_color,
+    float *__restrict__ out_invd, float *__restrict__ final_T, uint32_t *__restrict__ n_contrib,
+    uint32_t *__restrict__ tile_work, const uint32_t *__restrict__ kdev, uint32_t cap,
+    const uint32_t *__restrict__ sort_err, uint32_t *__restrict__ bwd_cnt, uint32_t *__restrict__ bwd_cls, int ntiles,
+    uint32_t seg_len, uint32_t *bin_base, uint32_t fseg_len, uint32_t *fctl) {
+    if (kdev && *kdev > cap) return;  // the point-list capacity is short: the host re-runs at K
+    __shared__ float4 s_a[kPixPerLane][kWave];
+    __shared__ float4 s_b[kPixPerLane][kWave];
+    __shared__ float4 s_c[kPixPerLane][kWave];
+    __shared__ uint32_t s_work[kPixPerLane], s_scalar[3];
+    const int w = threadIdx.x >> 6;
+    fwd_seg_worker(ranges, point_list, W, H, gx, rec, bg, out_color, out_invd, final_T, n_contrib, tile_work,
+                   kdev ? *kdev : cap, sort_err, bwd_cnt, bwd_cls, ntiles, seg_len, fseg_len, bin_base, fctl, s_a[w],
+                   s_b[w], s_c[w], s_work, s_scalar);
+}
+
 template <int kSub>
 __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kernel(
     const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list, int W, int H, int gx,
@@ -172,7 +473,7 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kerne
     uint32_t *__restrict__ tile_work, const uint32_t *__restrict__ fwd_order, const uint32_t *__restrict__ kdev,
     uint32_t cap, const uint32_t *__restrict__ sort_err, float4 *__restrict__ acc, uint32_t acc_n4,
     uint32_t *__restrict__ bwd_cnt, uint32_t *__restrict__ bwd_cls, int ntiles, int gy, int sb_nsbx, int sb_shift,
-    uint32_t seg_len, uint32_t *__restrict__ bin_base) {
+    uint32_t seg_len, uint32_t *__restrict__ bin_base, uint32_t fseg_len, uint32_t *__restrict__ fctl) {
     constexpr int kWaves = kPixPerLane / kSub;
     if (kdev && *kdev > cap) return;  // the point-list capacity is short: the host re-runs at K
     {
@@ -193,21 +494,24 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kerne
     __shared__ float4 s_c[kWaves][kWave];  // r, g, b, 1 / depth
     __shared__ uint32_t s_work[kWaves];
 
+    const uint32_t bidx = blockIdx.x;
+
     int tile, tx, ty;
     if (sb_shift >= 0) {
         // superblock launch order (GSR_FWD_SB_ORDER): fwd_order lists the SBs, a workgroup per SB
         // tile slot; slots past the grid's edge have no tile
-        const uint32_t per = 1u << (2 * sb_shift), b = blockIdx.x;
+        const uint32_t per = 1u << (2 * sb_shift), b = bidx;
         const uint32_t k = fwd_order[b >> (2 * sb_shift)], t = b & (per - 1u);
         tx = (int)(k % (uint32_t)sb_nsbx) * (1 << sb_shift) + (int)(t & ((1u << sb_shift) - 1u));
         ty = (int)(k / (uint32_t)sb_nsbx) * (1 << sb_shift) + (int)(t >> sb_shift);
         if (tx >= gx || ty >= gy) return;
         tile = ty * gx + tx;
     } else {
-        tile = (int)fwd_order[blockIdx.x];
+        tile = (int)fwd_order[bidx];
         tx = tile % gx;
         ty = tile / gx;
     }
+    if (fseg_splits(ranges[tile].y - ranges[tile].x, fseg_len)) return;  // render_fwd_seg_kernel's tile
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int px = tx * kTile + (lane & 15);
     const int sy = ty * kTile + 4 * kSub * w;  // the wave's first pixel row
@@ -397,27 +701,8 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kerne
     wl = wave_max_u32(wl);
     // the tile's backward work (last contributor position): tile_work, and with bwd_cnt its slot in
     // the backward's heaviest-first class lists
-    // With segments a tile of more than seg_len positions of work is cut into ceil(work / seg_len)
-    // backward items (tile + ntiles * segment): all but the last go to the segment list (past the
-    // checkpoints), run first; the last one goes into its work class like a whole tile.
     const auto publish = [&](uint32_t mx) {
-        tile_work[tile] = mx;
-        if (bwd_cnt) {
-            uint32_t item = (uint32_t)tile, wk = mx;
-            if (segs && mx > seg_len) {
-                const uint32_t nseg = (mx + seg_len - 1u) / seg_len;
-                const uint32_t kf = kdev ? *kdev : cap;
-                uint32_t *items = reinterpret_cast<uint32_t *>(ck + ck_slots(kf, seg_len) * (kCkFloats * 256));
-                const uint32_t b = atomicAdd(&bwd_cnt[kBwdSegCount], nseg - 1u);
-                for (uint32_t sgi = 0; sgi + 1u < nseg; sgi++) items[b + sgi] = (uint32_t)tile + (uint32_t)ntiles * sgi;
-                item = (uint32_t)tile + (uint32_t)ntiles * (nseg - 1u);
-                wk = mx - (nseg - 1u) * seg_len;
-            }
-            const uint32_t k = wk >> kBwdClassShift;
-            const uint32_t c = (uint32_t)(kBwdClasses - 1) - (k < (uint32_t)(kBwdClasses - 1) ? k : (uint32_t)(kBwdClasses - 1));
-            const uint32_t r = atomicAdd(&bwd_cnt[c], 1u);
-            bwd_cls[(size_t)c * ntiles + r] = item;
-        }
+        fwd_publish(mx, tile, tile_work, bwd_cnt, bwd_cls, ntiles, segs ? seg_len : 0u, ck, kdev ? *kdev : cap);
     };
     if (kWaves == 1) {
         if (lane == 0) publish(wl);
@@ -466,14 +751,38 @@ __device__ __forceinline__ int bwd_tile_of(uint32_t b, const uint32_t *__restric
 // tile writes only its own outputs, so results do not depend on it.
 __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t *__restrict__ work, const uint2 *__restrict__ ranges,
                                                           int T, int shift, uint32_t *__restrict__ order, const uint32_t *__restrict__ kdev, uint32_t cap,
-                                                          uint32_t *__restrict__ zero_classes) {
+                                                          uint32_t *__restrict__ zero_classes, uint32_t *__restrict__ fctl,
+                                                          void *bin_base, uint32_t seg_len, uint32_t fseg_len) {
     // the forward order's launch also zeroes the backward class counters render_fwd fills
     if (zero_classes && threadIdx.x < kBwdClasses) zero_classes[threadIdx.x] = 0u;
     if (zero_classes && threadIdx.x == 0) zero_classes[kBwdSegCount] = 0u;
     if (kdev && *kdev > cap) return;  // ranges / work were not written this pass (capacity re-run)
     __shared__ uint32_t hist[256];
+    __shared__ uint32_t s_items;
     if (threadIdx.x < 256) hist[threadIdx.x] = 0u;
+    if (threadIdx.x == 0) s_items = 0u;
     __syncthreads();
+    if (fseg_len) {
+        // forward segments: the work-item queue of the tiles longer than fseg_len (a tile's items
+        // consecutive, segment order), their tickets zeroed
+        const FwdSegLayout f = fseg_layout(bin_base, kdev ? *kdev : cap, seg_len, fseg_len);
+        for (int t = threadIdx.x; t < T; t += 1024) {
+            const uint32_t len = ranges[t].y - ranges[t].x;
+            if (!fseg_splits(len, fseg_len)) continue;
+            const uint32_t n = (len + fseg_len - 1u) / fseg_len;
+            const uint32_t b = atomicAdd(&s_items, n);
+            for (uint32_t k = 0; k < n; k++) {
+                f.items[b + k] = (uint32_t)t + (uint32_t)T * k;
+                f.tickets[b + k] = 0u;
+                f.flags[b + k] = 0u;
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            fctl[0] = s_items;  // kFwdItemsWord
+            fctl[1] = 0u;       // kFwdNextWord
+        }
+    }
     auto bucket = [&](int t) {
         const uint32_t wk = work ? work[t] : ranges[t].y - ranges[t].x;
         const uint32_t k = wk >> shift;
@@ -501,25 +810,34 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t *__rest
 }
 
 void launch_tile_order(const uint32_t *work, const uint2 *ranges, int T, int shift, uint32_t *order, hipStream_t s,
-                       const uint32_t *kdev, uint32_t cap, uint32_t *zero_classes) {
+                       const uint32_t *kdev, uint32_t cap, uint32_t *zero_classes, uint32_t *fctl, void *bin_base,
+                       uint32_t seg_len, uint32_t fseg_len) {
     if (T == 0) return;
-    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, s, work, ranges, T, shift, order, kdev, cap, zero_classes);
+    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, s, work, ranges, T, shift, order, kdev, cap, zero_classes,
+                       fctl, bin_base, seg_len, fctl ? fseg_len : 0u);
 }
 
 void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                        const float *bg, float *out_color, float *out_invdepth, hipStream_t s, bool need_bwd,
-                       bool sb_order, uint32_t seg_len) {
+                       bool sb_order, uint32_t seg_len, uint32_t fseg_len) {
     const int T = cam.gx * cam.gy;
     if (T == 0) return;
     const SBGrid &sg = gs.sb;
+    if (sb_order || GSR_FWD_SUB != 1) fseg_len = 0;
     const int grid = sb_order ? sg.nsb << (2 * sg.shift) : T;
+    uint32_t *const bcnt = GSR_BWD_CLS && need_bwd ? is.bwd_cnt : nullptr;
+    if (fseg_len)
+        hipLaunchKernelGGL(render_fwd_seg_kernel, dim3(kFwdWorkers), dim3(kWave * kPixPerLane), 0, s, is.ranges,
+                           bs.point_list, cam.W, cam.H, cam.gx, gs.rec, bg, out_color, out_invdepth, is.final_T,
+                           is.n_contrib, is.tile_work, bs.kdev, bs.cap, bs.kdev ? dsort_err_word(gs) : nullptr, bcnt,
+                           is.bwd_cls, T, seg_len, bs.point_list, fseg_len, is.bwd_cnt + kFwdItemsWord);
     // launch order: is.tile_ids (rasterizer.hip, by list length)
 #define GSR_FWD_LAUNCH(K, NT)                                                                                       \
     hipLaunchKernelGGL(K, dim3(grid), dim3(NT), 0, s, is.ranges, bs.point_list, cam.W, cam.H, cam.gx, gs.rec, bg,   \
                        out_color, out_invdepth, is.final_T, is.n_contrib, is.tile_work, is.tile_ids, bs.kdev, bs.cap, \
                        bs.kdev ? dsort_err_word(gs) : nullptr, gs.acc, (uint32_t)(4 * (size_t)gs.nacc),              \
                        GSR_BWD_CLS && need_bwd ? is.bwd_cnt : nullptr, is.bwd_cls, T, cam.gy, sg.nsbx,        \
-                       sb_order ? sg.shift : -1, GSR_BWD_CLS && need_bwd ? seg_len : 0u, bs.point_list)
+                       sb_order ? sg.shift : -1, seg_len, bs.point_list, fseg_len, is.bwd_cnt + kFwdItemsWord)
     static_assert(GSR_FWD_SUB == 1 || GSR_FWD_SUB == 2 || GSR_FWD_SUB == 4, "GSR_FWD_SUB: 1, 2 or 4");
     GSR_FWD_LAUNCH(render_fwd_kernel<GSR_FWD_SUB>, kWave * (kPixPerLane / GSR_FWD_SUB));
 #undef GSR_FWD_LAUNCH
@@ -971,6 +1289,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
         }
     }
 }
+
+bool fwd_segments_supported() { return GSR_FWD_SUB == 1 && !GSR_FWD_SB_ORDER; }
 
 bool bwd_segments_supported() { return GSR_BWD_CLS && GSR_FWD_SUB == 1 && GSR_BWD_BG_IN_S && !GSR_TILE_REVERSE; }
 

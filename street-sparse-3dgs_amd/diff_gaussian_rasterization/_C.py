@@ -328,6 +328,15 @@ def set_bwd_segment(length: int) -> int:
     return r
 
 
+def set_fwd_segment(length: int) -> int:
+    """Forward work split (gsr_set_fwd_segment): 0 = one workgroup per tile (default), L = a
+    multiple of 64 >= 4096 = tiles with longer lists blended as segments of L positions by a
+    worker pool.  Process-wide; returns the previous length."""
+    r = _L.gsr_set_fwd_segment(int(length))
+    _check(0 if r >= 0 else r, "set_fwd_segment")
+    return r
+
+
 def reset_capacity_hint() -> None:
     """Forget this thread's point-list capacity hint (gsr_reset_capacity_hint)."""
     _L.gsr_reset_capacity_hint()

@@ -142,3 +142,125 @@ def test_set_bwd_segment_validation():
         assert _C.set_bwd_segment(512) == 2048
     finally:
         _C.set_bwd_segment(prev)
+
+
+# ---------------------------------------------------------------------------------------------
+# Forward segments (gsr_set_fwd_segment): tiles with lists longer than Lf blended as Lf-position
+# items by a worker pool (transmittance products, per-pixel lookback, blend, ordered sum).  The
+# colours are the same sums in a different association, and each item's starting transmittance is
+# the product of its predecessors' instead of the running product, so the bars are stated for fp32
+# reassociation: FWD_PSNR_BAR / FWD_MAXABS on colour and inverse depth, FWD_NC_TOL for n_contrib
+# (an ulp of T at the 1e-4 stop test), gradients on the oracle's GRAD_TOL.
+FWD_PSNR_BAR = 125.0
+FWD_MAXABS = 2e-5
+FWD_NC_TOL = 1e-3
+GRAD_TOL = 5e-5
+
+FWD_CASES = [
+    dict(name="fseg_translucent_deg3", P=80000, W=96, H=64, deg=3, seed=31, log_scale=-2.0, opac=(0.004, 0.012)),
+    dict(name="fseg_odd_deg1", P=120000, W=150, H=70, deg=1, seed=32, log_scale=-2.1, opac=(0.004, 0.012)),
+    # opaque splats mixed in: pixels stop in different items of one tile
+    dict(name="fseg_mixed_opacity", P=80000, W=96, H=64, deg=3, seed=34, log_scale=-2.0, opac=(0.004, 0.012),
+         opaque=0.004),
+    dict(name="fseg_no_depth", P=80000, W=96, H=64, deg=2, seed=33, log_scale=-2.0, opac=(0.004, 0.012),
+         do_depth=False),
+]
+
+
+@contextlib.contextmanager
+def fwd_segment(L):
+    from diff_gaussian_rasterization import _C
+    prev = _C.set_fwd_segment(L)
+    try:
+        yield
+    finally:
+        _C.set_fwd_segment(prev)
+
+
+def fwd_compare(c, st, g, h, base=None):
+    from helpers import psnr
+    assert h["K"] == st["K"]
+    np.testing.assert_array_equal(h["radii"], st["radii"])
+    S = h["state"]
+    np.testing.assert_array_equal(S["point_list"], st["point_list"])
+    np.testing.assert_array_equal(S["ranges"], st["ranges"])
+    nc_bad = float(np.mean(S["n_contrib"] != st["n_contrib"]))
+    p_img = psnr(h["color"], st["color"])
+    mx = float(np.abs(h["color"] - st["color"]).max())
+    m = dict(nc_bad=nc_bad, psnr=p_img, maxabs=mx)
+    if c.get("do_depth", True):
+        m["inv_maxabs"] = float(np.abs(h["invdepth"] - st["invdepth"]).max() / max(1e-30, np.abs(st["invdepth"]).max()))
+    G = h["grads"]
+    for hk, ok in (("means3D", "dL_dmeans3D"), ("means2D", "dL_dmeans2D"), ("opacities", "dL_dopacity"),
+                   ("shs", "dL_dsh"), ("scales", "dL_dscales"), ("rotations", "dL_drotations")):
+        m["grad_" + hk] = rel_l2(G[hk].reshape(g[ok].shape), g[ok])
+    print(c["name"], m)
+    assert nc_bad <= FWD_NC_TOL, m
+    assert p_img >= FWD_PSNR_BAR, m
+    assert mx <= FWD_MAXABS, m
+    if "inv_maxabs" in m:
+        assert m["inv_maxabs"] <= FWD_MAXABS, m
+    for k, v in m.items():
+        if k.startswith("grad_"):
+            assert v <= GRAD_TOL, (k, m)
+
+
+@pytest.mark.parametrize("bwd_L", [0, 512])
+@pytest.mark.parametrize("c", FWD_CASES, ids=[c["name"] for c in FWD_CASES])
+def test_fwd_segments_vs_oracle(c, bwd_L):
+    s = seg_scene(c)
+    dcol, dinv = upstream_grads(c)
+    st, g = run_oracle(s, c, dcol, dinv)
+    lens = np.diff(st["ranges"].astype(np.int64), axis=1)
+    assert lens.max() > 2 * 4096, f"lists too short for three items: {lens.max()}"
+    with fwd_segment(4096), bwd_segment(bwd_L):
+        h = run_hip(s, c, dcol, dinv)
+    fwd_compare(c, st, g, h)
+
+
+def test_fwd_segments_deterministic_and_repeatable():
+    """Record mode with both splits: two runs bitwise equal (the item order of the worker pool
+    varies run to run; every sum is in segment order regardless)."""
+    c = FWD_CASES[0]
+    s = seg_scene(c)
+    dcol, dinv = upstream_grads(c)
+    st, g = run_oracle(s, c, dcol, dinv)
+    with deterministic(), fwd_segment(4096), bwd_segment(512):
+        h1 = run_hip(s, c, dcol, dinv)
+        h2 = run_hip(s, c, dcol, dinv)
+    fwd_compare(c, st, g, h1)
+    np.testing.assert_array_equal(h1["color"], h2["color"])
+    np.testing.assert_array_equal(h1["state"]["n_contrib"], h2["state"]["n_contrib"])
+    for k, v in h1["grads"].items():
+        if v is not None:
+            np.testing.assert_array_equal(v, h2["grads"][k], err_msg=k)
+
+
+def test_fwd_segments_no_backward_forward():
+    """A no-grad forward (no backward state) with the forward split: same image."""
+    import torch
+    from diff_gaussian_rasterization import GaussianRasterizer
+    from helpers import settings, torch_inputs
+    c = FWD_CASES[1]
+    s = seg_scene(c)
+    dcol, dinv = upstream_grads(c)
+    st, _ = run_oracle(s, c, dcol, dinv)
+    dev = torch.device("cuda:0")
+    inp = torch_inputs(s, dev, requires_grad=False)
+    with torch.no_grad(), fwd_segment(4096):
+        color, _, invd = GaussianRasterizer(settings(s, dev, c["deg"]))(**inp)
+    err = float(np.abs(color.cpu().numpy() - st["color"]).max())
+    assert err <= FWD_MAXABS, err
+
+
+def test_set_fwd_segment_validation():
+    from diff_gaussian_rasterization import _C
+    prev = _C.set_fwd_segment(0)
+    try:
+        for bad in (-64, 512, 4000, 4097):
+            with pytest.raises(RuntimeError):
+                _C.set_fwd_segment(bad)
+        assert _C.set_fwd_segment(8192) == 0
+        assert _C.set_fwd_segment(4096) == 8192
+    finally:
+        _C.set_fwd_segment(prev)

@@ -26,7 +26,8 @@ def main():
     ap.add_argument("--iters", type=int, default=12000)
     ap.add_argument("--views", type=int, default=8)
     ap.add_argument("--size", type=int, default=1536)
-    ap.add_argument("--segs", default="0,512,1024,2048,4096", help="backward segment lengths to time (A/B)")
+    ap.add_argument("--segs", default="0:0,0:512,4096:512,8192:512",
+                    help="forward:backward segment lengths to time (A/B), comma separated")
     ap.add_argument("--reps", type=int, default=10)
     a = ap.parse_args()
     import torch
@@ -78,7 +79,7 @@ def main():
             "bwd_work": {"mean": float(work.mean()), "p50": float(np.median(work)), "p99": float(np.percentile(work, 99)),
                          "max": int(ws[0]), "top8": ws[:8].tolist(), "sum": int(work.sum()),
                          "top1pct_share": float(ws[:T // 100].sum() / max(1, ws.sum()))}})
-        out["views"][-1]["bwd_ms_by_seg"] = time_segments(g, c, H, W, [int(x) for x in a.segs.split(",")], a.reps)
+        out["views"][-1]["bwd_ms_by_seg"] = time_segments(g, c, H, W, a.segs.split(","), a.reps)
         done += 1
         k += 1
     print(json.dumps(out))
@@ -101,7 +102,7 @@ def time_segments(g, c, H, W, segs, reps):
     up_c = torch.randn(3, H, W, generator=gen, device=dev) * 1e-3
     up_d = torch.randn(1, H, W, generator=gen, device=dev) * 1e-3
     res = {}
-    ref = ref_det = None
+    ref = ref_det = ref_col = None
 
     def det_grads():
         prev_det = _C.set_deterministic(True)
@@ -115,8 +116,9 @@ def time_segments(g, c, H, W, segs, reps):
         return [x.grad for x in xs]
 
     rel = lambda ga, gb: max(float((a - b).norm() / b.norm().clamp_min(1e-30)) for a, b in zip(ga, gb))
-    for L in segs:
-        prev = _C.set_bwd_segment(L)
+    for cfg in segs:
+        fL, L = (int(x) for x in cfg.split(":"))
+        prev, fprev = _C.set_bwd_segment(L), _C.set_fwd_segment(fL)
         st_all, wall, last2 = [], [], []
         for r in range(reps + 2):
             xs = [t.detach().clone().requires_grad_(True) for t in
@@ -137,20 +139,23 @@ def time_segments(g, c, H, W, segs, reps):
                 st_all.append(st)
                 wall.append(e0.elapsed_time(e1))
             last2 = (last2 + [[x.grad for x in xs]])[-2:]
+            col_last = col.detach()
         grads = last2[-1]
         if ref is None:
-            ref = grads
+            ref, ref_col = grads, col_last
         gd = det_grads()
         if ref_det is None:
             ref_det = gd
         _C.set_bwd_segment(prev)
+        _C.set_fwd_segment(fprev)
         med = lambda k: float(np.median([s_[k] for s_ in st_all]))
         # grad errors (max over tensors of relative L2): atomic vs the first length's atomic run, the
         # run-to-run atomic noise at this length, and record mode (bitwise ordered sums) vs the first
         # length's record mode -- the split's own rounding
-        res[str(L)] = {"render_bwd": round(med("render_bwd"), 4), "render_fwd": round(med("render_fwd"), 4),
+        res[cfg] = {"render_bwd": round(med("render_bwd"), 4), "render_fwd": round(med("render_fwd"), 4),
                        "fwd_bwd_wall": round(float(np.median(wall)), 4), "grad_rel_l2_vs_first": rel(grads, ref),
-                       "atomic_noise": rel(last2[0], last2[1]), "det_grad_rel_l2_vs_first": rel(gd, ref_det)}
+                       "atomic_noise": rel(last2[0], last2[1]), "det_grad_rel_l2_vs_first": rel(gd, ref_det),
+                       "color_maxabs_vs_first": float((col_last - ref_col).abs().max())}
     return res
 
 
