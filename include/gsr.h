@@ -171,6 +171,11 @@ int gsr_set_bwd_segment(int L);
  * GSR_ERR_UNSUPPORTED. */
 int gsr_set_fwd_segment(int L);
 
+/* Diagnostic (host arithmetic only): the bytes the backward checkpoints and the forward items need
+ * past the start of a binning buffer carved for K instances with segment lengths L / Lf (*need),
+ * and the buffer's size (*have).  GSR_OK when they fit. */
+int gsr_segment_layout_check(int64_t K, int L, int Lf, int64_t *need, int64_t *have);
+
 /* Depth-order strategy of the binning, process-wide.  0: the local sort -- level 1 in Gaussian
  * index order, each superblock list sorted by depth in LDS -- except for frames forwarded in
  * deterministic mode and frames with a superblock list longer than the LDS sort holds, which take

@@ -979,6 +979,22 @@ int gsr_forward_stats(int64_t *out, int n) {
     return k;
 }
 
+int gsr_segment_layout_check(int64_t K, int L, int Lf, int64_t *need, int64_t *have) {
+    if (K < 0 || L < 0 || Lf < 0) return fail(GSR_ERR_INVALID_ARGUMENT, "negative size");
+    size_t bytes = 0;
+    carve_binning(nullptr, K, &bytes);
+    size_t end = ck_offset(K);
+    if (L) end += align256(ck_slots(K, (uint32_t)L) * (kCkFloats * 256) * 4 + ck_slots(K, (uint32_t)L) * 4);
+    if (Lf) {
+        // the forward items' arrays end past the partials
+        const FwdSegLayout f = fseg_layout(nullptr, K, (uint32_t)L, (uint32_t)Lf);
+        end = (size_t)reinterpret_cast<uintptr_t>(f.part) + fseg_max_items(K, (uint32_t)Lf) * kFwdPartials * 256 * 4;
+    }
+    if (need) *need = (int64_t)end;
+    if (have) *have = (int64_t)bytes;
+    return end <= bytes ? GSR_OK : GSR_ERR_INVALID_ARGUMENT;
+}
+
 int gsr_reset_capacity_hint(void) {
     for (int d = 0; d < kMaxDevicesK; d++) {
         g_khint[d] = 0;

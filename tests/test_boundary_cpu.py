@@ -44,6 +44,20 @@ def test_library_metadata_calls_without_gpu():
     assert L.gsr_stage_times_ms(buf, 8) >= 0
 
 
+@pytest.mark.parametrize("L,Lf", [(512, 0), (0, 4096), (512, 4096), (1024, 8192), (64 * 9, 64 * 65)])
+def test_segment_regions_fit_the_binning_buffer(L, Lf):
+    """The backward checkpoints / segment list and the forward items' arrays fit
+    in the binning buffer past the point list for every K (host arithmetic, no GPU)."""
+    from diff_gaussian_rasterization import _lib
+    lib = _lib.load()
+    need, have = ctypes.c_int64(), ctypes.c_int64()
+    for K in [0, 1, 63, 64, 511, 512, 513, 4095, 4096, 8193, 10_000, 123_457, 1 << 20, 13_900_000,
+              (1 << 31) - 1, 3_000_000_000]:
+        rc = lib.gsr_segment_layout_check(K, L, Lf, ctypes.byref(need), ctypes.byref(have))
+        assert rc == 0 and need.value <= have.value, (K, need.value, have.value)
+    assert lib.gsr_segment_layout_check(-1, L, Lf, None, None) != 0
+
+
 def test_library_is_gfx950_code_object():
     from diff_gaussian_rasterization import _lib
     data = open(_lib.LIB_PATH, "rb").read()
