@@ -22,6 +22,7 @@
 // backward.hip in a fixed order (bitwise reproducible).  Only instances in front of the tile's
 // last contributor are visited (13% of them on the 1M-Gaussian bench scene).
 #include <atomic>
+#include <cstdlib>
 #include <type_traits>
 
 #include "gsr_launch.h"
@@ -817,6 +818,16 @@ void launch_tile_order(const uint32_t *work, const uint2 *ranges, int T, int shi
                        fctl, bin_base, seg_len, fctl ? fseg_len : 0u);
 }
 
+// the worker pool's size: kFwdWorkers, or GSR_FWD_WORKERS from the environment (measurement A/B)
+static int fwd_workers() {
+    static const int n = [] {
+        const char *e = getenv("GSR_FWD_WORKERS");
+        const int v = e ? atoi(e) : 0;
+        return v > 0 ? v : kFwdWorkers;
+    }();
+    return n;
+}
+
 void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                        const float *bg, float *out_color, float *out_invdepth, hipStream_t s, bool need_bwd,
                        bool sb_order, uint32_t seg_len, uint32_t fseg_len) {
@@ -827,7 +838,7 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
     const int grid = sb_order ? sg.nsb << (2 * sg.shift) : T;
     uint32_t *const bcnt = GSR_BWD_CLS && need_bwd ? is.bwd_cnt : nullptr;
     if (fseg_len)
-        hipLaunchKernelGGL(render_fwd_seg_kernel, dim3(kFwdWorkers), dim3(kWave * kPixPerLane), 0, s, is.ranges,
+        hipLaunchKernelGGL(render_fwd_seg_kernel, dim3(fwd_workers()), dim3(kWave * kPixPerLane), 0, s, is.ranges,
                            bs.point_list, cam.W, cam.H, cam.gx, gs.rec, bg, out_color, out_invdepth, is.final_T,
                            is.n_contrib, is.tile_work, bs.kdev, bs.cap, bs.kdev ? dsort_err_word(gs) : nullptr, bcnt,
                            is.bwd_cls, T, seg_len, bs.point_list, fseg_len, is.bwd_cnt + kFwdItemsWord);

@@ -58,6 +58,16 @@ def bwd_segment(L):
         _C.set_bwd_segment(prev)
 
 
+@contextlib.contextmanager
+def fwd_segment(L):
+    from diff_gaussian_rasterization import _C
+    prev = _C.set_fwd_segment(L)
+    try:
+        yield
+    finally:
+        _C.set_fwd_segment(prev)
+
+
 def max_tile_work(h, c):
     nc = h["state"]["n_contrib"].reshape(c["H"], c["W"])
     gy, gx = (c["H"] + 15) // 16, (c["W"] + 15) // 16
@@ -72,8 +82,9 @@ def test_segments_vs_oracle_and_unsplit(c, L):
     s = seg_scene(c)
     dcol, dinv = upstream_grads(c)
     st, g = run_oracle(s, c, dcol, dinv)
-    base = run_hip(s, c, dcol, dinv)
-    with bwd_segment(L):
+    with bwd_segment(0), fwd_segment(0):
+        base = run_hip(s, c, dcol, dinv)
+    with bwd_segment(L), fwd_segment(0):
         h = run_hip(s, c, dcol, dinv)
     work = max_tile_work(h, c)
     print(f"{c['name']} L={L}: max tile work {work}")
@@ -95,7 +106,7 @@ def test_segments_deterministic_mode():
     s = seg_scene(c)
     dcol, dinv = upstream_grads(c)
     st, g = run_oracle(s, c, dcol, dinv)
-    with deterministic(), bwd_segment(512):
+    with deterministic(), bwd_segment(512), fwd_segment(0):
         h1 = run_hip(s, c, dcol, dinv)
         h2 = run_hip(s, c, dcol, dinv)
     compare(c, st, g, h1)
@@ -115,6 +126,8 @@ def test_backward_uses_the_forwards_length():
     dcol, dinv = upstream_grads(c)
     st, g = run_oracle(s, c, dcol, dinv)
     dev = torch.device("cuda:0")
+    setting = _C.set_bwd_segment(0)
+    _C.set_bwd_segment(setting)
     for later in (0, 1024):
         inp = torch_inputs(s, dev)
         rs = settings(s, dev, c["deg"])
@@ -128,7 +141,7 @@ def test_backward_uses_the_forwards_length():
                        ("scales", "dL_dscales"), ("rotations", "dL_drotations")):
             err = rel_l2(inp[hk].grad.detach().cpu().numpy().reshape(g[ok].shape), g[ok])
             assert err <= 5e-5, (later, hk, err)
-    assert _C.set_bwd_segment(0) == 0
+    assert _C.set_bwd_segment(setting) == setting
 
 
 def test_set_bwd_segment_validation():
@@ -166,15 +179,6 @@ FWD_CASES = [
          do_depth=False),
 ]
 
-
-@contextlib.contextmanager
-def fwd_segment(L):
-    from diff_gaussian_rasterization import _C
-    prev = _C.set_fwd_segment(L)
-    try:
-        yield
-    finally:
-        _C.set_fwd_segment(prev)
 
 
 def fwd_compare(c, st, g, h, base=None):

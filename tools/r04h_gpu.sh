@@ -6,14 +6,16 @@ timeout -k 10 300 python3 -u -m pytest tests/test_gpu_segments.py -v -s --timeou
 rc=$?
 echo "segtest rc=$rc"
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-for cfg in "0 0" "0 512" "4096 512" "0 0" "0 512" "4096 512"; do
+for cfg in "0 0 256" "0 512 256" "4096 512 256" "4096 512 1536" "0 512 256" "4096 512 1536"; do
   set -- $cfg
-  timeout -k 10 200 python3 -u bench.py --metric-only --steps 50 --warmup 10 --fwd-seg $1 --bwd-seg $2 > $O/bench_$1_$2.json 2>>$O/bench.err || exit 3
-  cat $O/bench_$1_$2.json >> $O/bench_all.jsonl
+  GSR_FWD_WORKERS=$3 timeout -k 10 200 python3 -u bench.py --metric-only --steps 50 --warmup 10 --fwd-seg $1 --bwd-seg $2 > $O/bench_$1_$2_$3.json 2>>$O/bench.err || exit 3
+  cat $O/bench_$1_$2_$3.json >> $O/bench_all.jsonl
+done
+for w in 256 1024; do
+  GSR_FWD_WORKERS=$w timeout -k 10 300 python3 -u tools/street_tiles.py --iters 12000 --views 6 --segs 0:512,4096:512,8192:512 > $O/street_tiles_w$w.json 2> $O/street_tiles_w$w.err || exit 5
 done
 C3="--steps 5 --warmup 2 --train-steps 0 --no-config5 --no-street --no-config4 --no-coarse-debug --no-cpu-baseline --post-leaves 0"
 for cfg in "0 0" "4096 512"; do
   set -- $cfg
-  timeout -k 10 400 python3 -u bench.py $C3 --fwd-seg $1 --bwd-seg $2 > $O/c3_$1_$2.json 2>>$O/c3.err || exit 4
+  GSR_FWD_WORKERS=1024 timeout -k 10 300 python3 -u bench.py $C3 --fwd-seg $1 --bwd-seg $2 > $O/c3_$1_$2.json 2>>$O/c3.err || exit 4
 done
-timeout -k 10 500 python3 -u tools/street_tiles.py --iters 12000 --views 6 --segs 0:0,0:512,4096:512,8192:512 > $O/street_tiles.json 2> $O/street_tiles.err
