@@ -162,9 +162,9 @@ int gsr_set_deterministic(int enable);
 int gsr_set_bwd_segment(int L);
 
 /* Forward work split, process-wide.  L = 0 (default): render_fwd blends every tile in one
- * workgroup.  L > 0 (a multiple of 64, >= 4096): a tile whose list is longer than L is blended as
+ * workgroup.  L > 0 (a multiple of 64, >= 4096): a tile whose list is longer than 2 L is blended as
  * ceil(len / L) work items by a pool of worker workgroups -- each item multiplies out the
- * transmittance through its positions, takes its predecessors' product (a decoupled lookback) and
+ * transmittance through its positions, takes its predecessors' product (in segment order) and
  * blends its positions from there; the tile's last item adds the items' colours in order.  Colours
  * agree with the one-workgroup blend to fp32 summation order; the stop rule is the same up to an
  * ulp of the transmittance product.  Returns the previous length, or GSR_ERR_INVALID_ARGUMENT /

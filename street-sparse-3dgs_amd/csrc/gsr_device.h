@@ -484,14 +484,13 @@ __host__ __device__ __forceinline__ size_t align256(size_t b) { return (b + 255)
 
 // Forward segments (gsr_set_fwd_segment): a tile whose list is longer than 2 Lf positions is
 // blended as ceil(len / Lf) work items by render_fwd_seg_kernel's kFwdWorkers workgroups (an item
-// queue tile_order fills), launched before render_fwd.  Item s first multiplies out (1 - alpha) over its positions (the pixels'
-// transmittance through the segment), publishes it and takes the product of its predecessors'
-// (a decoupled lookback per pixel), then blends its positions from that transmittance with the
-// usual stop rule; the tile's last item to finish sums the items' colours in order and writes the
+// queue tile_order fills), launched beside render_fwd on a side stream.  Item s first multiplies
+// out (1 - alpha) over its positions (the pixels' transmittance through the segment), publishes it,
+// waits for its predecessors' and takes their product in segment order, then blends its positions
+// from that transmittance with the usual stop rule; the tile's last item to finish sums the items' colours in order and writes the
 // pixels.  Per item, past the backward's region: its queue entry, a ticket (the tile's first
-// item's counts the finished items), a lookback flag (0 none, 1 the segment's own transmittance
-// published, 2 the product through it; zeroed with the queue), 4 checkpoint counts, the two
-// per-pixel transmittance rows and 256 x 6 partials.
+// item's counts the finished items), a flag (1: its transmittance row is published; zeroed with
+// the queue), 4 checkpoint counts, the per-pixel transmittance row and 256 x 6 partials.
 constexpr uint32_t kMinFwdSeg = 4096;
 // a tile is split when its list holds more than two segments (3+ items: with two, the second
 // item's wait for the first one's transmittance pass leaves little to gain)
@@ -502,7 +501,7 @@ constexpr int kFwdPartials = 6;  // r, g, b, inverse depth, T at the end, last c
 constexpr int kFwdItemsWord = kBwdSegCount + 1, kFwdNextWord = kBwdSegCount + 2;
 struct FwdSegLayout {
     uint32_t *items, *tickets, *flags, *nc;
-    float *agg, *incl;  // per item x 256 pixels: the segment's own transmittance, the product through it
+    float *agg;  // per item x 256 pixels: the transmittance through the segment
     float *part;
 };
 __host__ __device__ __forceinline__ size_t fseg_max_items(int64_t K, uint32_t Lf) { return Lf ? (size_t)(2 * K / Lf) + 2 : 0; }
@@ -520,8 +519,6 @@ __host__ __device__ __forceinline__ FwdSegLayout fseg_layout(void *bin_base, int
     f.nc = reinterpret_cast<uint32_t *>(b + off);
     off = align256(off + 16 * n);
     f.agg = reinterpret_cast<float *>(b + off);
-    off = align256(off + 4 * 256 * n);
-    f.incl = reinterpret_cast<float *>(b + off);
     off = align256(off + 4 * 256 * n);
     f.part = reinterpret_cast<float *>(b + off);
     return f;

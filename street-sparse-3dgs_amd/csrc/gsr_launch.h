@@ -111,7 +111,8 @@ struct ZeroRows {
 // render.hip
 void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                        const float *bg, float *out_color, float *out_invdepth, hipStream_t s, bool need_bwd = true,
-                       bool sb_order = false, uint32_t seg_len = 0, uint32_t fseg_len = 0);
+                       bool sb_order = false, uint32_t seg_len = 0, uint32_t fseg_len = 0,
+                       hipStream_t worker_stream = nullptr);
 // seg_len != 0: the backward's heavy tiles are cut into segments of seg_len list positions
 // (gsr_set_bwd_segment; the backward must get the value its forward was made with)
 void launch_render_bwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,

@@ -768,8 +768,18 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
         }
         {
             StageTimer st(5, s);
+            // forward segments: the worker pool on the side stream, beside render_fwd (which skips the
+            // split tiles); joined before anything reads the frame
+            hipStream_t wside = s;
+            hipEvent_t wfork = nullptr, wjoin = nullptr;
+            if (fseg_used && !side_stream(s, &wside, &wfork, &wjoin)) wside = s;
+            const bool forked = fseg_used && wside != s;
+            if (forked && (hipEventRecord(wfork, s) != hipSuccess || hipStreamWaitEvent(wside, wfork, 0) != hipSuccess))
+                return fail(GSR_ERR_DEVICE, "side stream fork failed");
             launch_render_fwd(cam, gs, bs, is, background, out_color, out_invdepth, s, need_bwd, sb_order, seg_used,
-                              fseg_used);
+                              fseg_used, wside);
+            if (forked && (hipEventRecord(wjoin, wside) != hipSuccess || hipStreamWaitEvent(s, wjoin, 0) != hipSuccess))
+                return fail(GSR_ERR_DEVICE, "side stream join failed");
         }
         if (need_bwd && !GSR_BWD_CLS) {
             StageTimer st(9, s);  // backward launch order, from the forward's per-tile work

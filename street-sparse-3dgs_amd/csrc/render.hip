@@ -273,18 +273,18 @@ __device__ __forceinline__ void fwd_seg_pass(const uint32_t *__restrict__ point_
 
 // a forward item's lookback row is complete: every thread's stores made visible device-wide (all
 // XCDs' L2s), then the flag
-__device__ __forceinline__ void seg_publish(uint32_t *flag, uint32_t v) {
+__device__ __forceinline__ void seg_publish(uint32_t *flag) {
     __threadfence();
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // render_fwd_seg_kernel's workgroups (forward segments): items from the queue tile_order
 // filled until it is empty (FwdSegLayout).  Item i = segment s of its tile: (1) the transmittance
 // through the segment (skipped for the tile's last segment) published per pixel; (2) the product of
-// the predecessors' -- a decoupled lookback over per-item flags (1: the segment's own row is
-// published, 2: the product through it), each row made visible with a release fence before its flag
-// (items of a tile are taken in order, so every predecessor's workgroup is resident); (3) the blend from that transmittance into the item's partials; (4) the
+// the predecessors', in segment order once every predecessor's flag is set (each row made visible
+// with a release fence before its flag; items of a tile are taken in order, so every predecessor's
+// workgroup is resident), so the product does not depend on which item finished first; (3) the blend from that transmittance into the item's partials; (4) the
 // tile's last item to finish (a ticket) adds the partials in segment order (up to the pixel's stop),
 // turns the backward checkpoints into colour-behind and writes the tile's pixels.
 __device__ void fwd_seg_worker(const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list, int W, int H,
@@ -322,43 +322,32 @@ __device__ void fwd_seg_worker(const uint2 *__restrict__ ranges, const uint32_t 
             uint64_t lm = insm, sm = 0;
             fwd_seg_pass<false>(point_list, rec, rg.x, p0, p1, sa, sb, sc, pfx, pfy, tx0, sy0, lm, sm, Ta, d0, d1, d2, d3,
                                 du, nullptr, 0u, dn);
-            Ta = Ta < 0.0001f ? 0.f : Ta;
-            (sgi == 0 ? f.incl : f.agg)[(size_t)i * 256 + threadIdx.x] = Ta;
-            seg_publish(f.flags + i, sgi == 0 ? 2u : 1u);
+            f.agg[(size_t)i * 256 + threadIdx.x] = Ta < 0.0001f ? 0.f : Ta;
+            seg_publish(f.flags + i);
         }
+        // (2) the predecessors' rows, multiplied in segment order (the same product whichever
+        // finished first: the frame is bitwise repeatable)
         float Tin = 1.f;
         bool hung = false;
-        if (sgi > 0) {  // (2) the predecessors' rows back to the nearest product-through
-            float prod = 1.f;
-            for (uint32_t j = sgi - 1u;; j--) {
-                if (threadIdx.x == 0) {
-                    uint32_t fl = 0;
-                    for (uint32_t spins = 0; spins < (1u << 22); spins++) {
-                        fl = __hip_atomic_load(f.flags + i0 + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                        if (fl) break;
+        if (sgi > 0) {
+            if (threadIdx.x == 0) {
+                uint32_t ok = 1u;
+                for (uint32_t j = 0; j < sgi && ok; j++) {
+                    uint32_t spins = 0;
+                    while (!__hip_atomic_load(f.flags + i0 + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) {
+                        if (++spins > (1u << 22)) {  // never expected: the tile's pixels become NaN (loud)
+                            ok = 0u;
+                            break;
+                        }
                         __builtin_amdgcn_s_sleep(2);
                     }
-                    s_scalar[2] = fl;
                 }
-                __syncthreads();
-                const uint32_t fl = s_scalar[2];
-                __syncthreads();
-                if (fl == 0u || (fl == 1u && j == 0u)) {  // never expected: the tile's pixels become NaN (loud)
-                    hung = true;
-                    break;
-                }
-                __threadfence();
-                if (fl == 2u) {
-                    prod *= f.incl[(size_t)(i0 + j) * 256 + threadIdx.x];
-                    break;
-                }
-                prod *= f.agg[(size_t)(i0 + j) * 256 + threadIdx.x];
+                s_scalar[2] = ok;
             }
-            Tin = prod;
-            if (sgi + 1u < nseg) {
-                f.incl[(size_t)i * 256 + threadIdx.x] = Tin * Ta;
-                seg_publish(f.flags + i, 2u);
-            }
+            __syncthreads();
+            hung = s_scalar[2] == 0u;
+            __threadfence();
+            for (uint32_t j = 0; j < sgi; j++) Tin *= f.agg[(size_t)(i0 + j) * 256 + threadIdx.x];
         }
         // (3)
         float T = Tin, C0 = 0.f, C1 = 0.f, C2 = 0.f, ID = 0.f;
@@ -446,8 +435,8 @@ __device__ void fwd_seg_worker(const uint2 *__restrict__ ranges, const uint32_t 
     }
 }
 
-// Forward segments' worker pool: kFwdWorkers workgroups, launched before render_fwd (which skips
-// the split tiles), until the item queue is empty.
+// Forward segments' worker pool: kFwdWorkers workgroups, launched beside render_fwd (which skips
+// the split tiles) on a side stream, until the item queue is empty.
 __global__ __launch_bounds__(kWave * kPixPerLane) void render_fwd_seg_kernel(
     const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list, int W, int H, int gx,
     const GRec *__restrict__ rec, const float *__restrict__ bg, float *__restrict__ out_color,
@@ -830,7 +819,7 @@ static int fwd_workers() {
 
 void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                        const float *bg, float *out_color, float *out_invdepth, hipStream_t s, bool need_bwd,
-                       bool sb_order, uint32_t seg_len, uint32_t fseg_len) {
+                       bool sb_order, uint32_t seg_len, uint32_t fseg_len, hipStream_t worker_stream) {
     const int T = cam.gx * cam.gy;
     if (T == 0) return;
     const SBGrid &sg = gs.sb;
@@ -838,7 +827,8 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
     const int grid = sb_order ? sg.nsb << (2 * sg.shift) : T;
     uint32_t *const bcnt = GSR_BWD_CLS && need_bwd ? is.bwd_cnt : nullptr;
     if (fseg_len)
-        hipLaunchKernelGGL(render_fwd_seg_kernel, dim3(fwd_workers()), dim3(kWave * kPixPerLane), 0, s, is.ranges,
+        hipLaunchKernelGGL(render_fwd_seg_kernel, dim3(fwd_workers()), dim3(kWave * kPixPerLane), 0,
+                           worker_stream ? worker_stream : s, is.ranges,
                            bs.point_list, cam.W, cam.H, cam.gx, gs.rec, bg, out_color, out_invdepth, is.final_T,
                            is.n_contrib, is.tile_work, bs.kdev, bs.cap, bs.kdev ? dsort_err_word(gs) : nullptr, bcnt,
                            is.bwd_cls, T, seg_len, bs.point_list, fseg_len, is.bwd_cnt + kFwdItemsWord);
