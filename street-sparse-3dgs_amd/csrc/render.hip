@@ -271,12 +271,24 @@ __device__ __forceinline__ void fwd_seg_pass(const uint32_t *__restrict__ point_
     }
 }
 
-// a forward item's lookback row is complete: every thread's stores made visible device-wide (all
-// XCDs' L2s), then the flag
-__device__ __forceinline__ void seg_publish(uint32_t *flag) {
-    __threadfence();
+// Cross-workgroup hand-offs of the forward segments (MI355X_MICROARCH.md, the hand-off rules):
+// producer -- every wave drains its stores, the workgroup meets, lane 0 writes the XCD's L2 back
+// (agent release) and drains that before the flag / counter; consumer -- after lane 0 saw the flag,
+// one agent acquire, drained, then the barrier, then plain loads.
+__device__ __forceinline__ void wg_release() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
+__device__ __forceinline__ void wg_acquire() {
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
 }
 
 // render_fwd_seg_kernel's workgroups (forward segments): items from the queue tile_order
@@ -323,7 +335,8 @@ __device__ void fwd_seg_worker(const uint2 *__restrict__ ranges, const uint32_t 
             fwd_seg_pass<false>(point_list, rec, rg.x, p0, p1, sa, sb, sc, pfx, pfy, tx0, sy0, lm, sm, Ta, d0, d1, d2, d3,
                                 du, nullptr, 0u, dn);
             f.agg[(size_t)i * 256 + threadIdx.x] = Ta < 0.0001f ? 0.f : Ta;
-            seg_publish(f.flags + i);
+            wg_release();
+            if (threadIdx.x == 0) __hip_atomic_store(f.flags + i, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         // (2) the predecessors' rows, multiplied in segment order (the same product whichever
         // finished first: the frame is bitwise repeatable)
@@ -334,7 +347,7 @@ __device__ void fwd_seg_worker(const uint2 *__restrict__ ranges, const uint32_t 
                 uint32_t ok = 1u;
                 for (uint32_t j = 0; j < sgi && ok; j++) {
                     uint32_t spins = 0;
-                    while (!__hip_atomic_load(f.flags + i0 + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) {
+                    while (!__hip_atomic_load(f.flags + i0 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
                         if (++spins > (1u << 22)) {  // never expected: the tile's pixels become NaN (loud)
                             ok = 0u;
                             break;
@@ -344,9 +357,8 @@ __device__ void fwd_seg_worker(const uint2 *__restrict__ ranges, const uint32_t 
                 }
                 s_scalar[2] = ok;
             }
-            __syncthreads();
+            wg_acquire();
             hung = s_scalar[2] == 0u;
-            __threadfence();
             for (uint32_t j = 0; j < sgi; j++) Tin *= f.agg[(size_t)(i0 + j) * 256 + threadIdx.x];
         }
         // (3)
@@ -365,13 +377,12 @@ __device__ void fwd_seg_worker(const uint2 *__restrict__ ranges, const uint32_t 
             q[1280] = __uint_as_float(last | (((sm >> lane) & 1ull) ? 0x80000000u : 0u) | (hung ? 0x40000000u : 0u));
             if (lane == 0) f.nc[(size_t)i * 4 + w] = ncross;
         }
-        __threadfence();
-        __syncthreads();
+        wg_release();
         if (threadIdx.x == 0)
-            s_scalar[1] = __hip_atomic_fetch_add(&f.tickets[i0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            s_scalar[1] = __hip_atomic_fetch_add(&f.tickets[i0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
         if (s_scalar[1] + 1u != nseg) continue;
-        __threadfence();
+        wg_acquire();
         // (4) the tile's pixels: partials added in segment order up to the segment the pixel stopped in
         float A0 = 0.f, A1 = 0.f, A2 = 0.f, A3 = 0.f, Tf = 1.f;
         uint32_t lp = 0;
