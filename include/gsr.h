@@ -152,8 +152,8 @@ int gsr_set_true_scale_gradient(int enable);
  * force at its forward.  Returns the previous mode. */
 int gsr_set_deterministic(int enable);
 
-/* Backward work split, process-wide.  L = 0 (default): render_bwd replays every tile in one
- * workgroup.  L > 0 (a multiple of 64, >= 512): the forward checkpoints each pixel's transmittance
+/* Backward work split, process-wide.  L = 0: render_bwd replays every tile in one workgroup.
+ * L > 0 (a multiple of 64, >= 512; default 512): the forward checkpoints each pixel's transmittance
  * and accumulated colour every L list positions of its tile, and the backward replays a tile whose
  * last contributor lies past L as ceil(work / L) independent segments (the few very long tiles of a
  * street view no longer form the kernel's tail).  Gradients agree with the unsegmented replay to

@@ -320,8 +320,8 @@ def set_binning(mode: int) -> int:
 
 
 def set_bwd_segment(length: int) -> int:
-    """Backward work split (gsr_set_bwd_segment): 0 = one workgroup per tile (default), L = a
-    multiple of 64 >= 512 = heavy tiles replayed as segments of L list positions.  Process-wide;
+    """Backward work split (gsr_set_bwd_segment): 0 = one workgroup per tile, L = a multiple of
+    64 >= 512 (default 512) = heavy tiles replayed as segments of L list positions.  Process-wide;
     returns the previous length."""
     r = _L.gsr_set_bwd_segment(int(length))
     _check(0 if r >= 0 else r, "set_bwd_segment")
