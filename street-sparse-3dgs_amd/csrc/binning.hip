@@ -190,9 +190,11 @@ __global__ __launch_bounds__(kColThreads) void sb_colscan_kernel(SBGrid sg, uint
                                                                  uint32_t *__restrict__ base_i,
                                                                  uint32_t *__restrict__ done, FrameWords fw,
                                                                  uint32_t *__restrict__ sb_order,
-                                                                 uint32_t *__restrict__ zero_classes) {
+                                                                 uint32_t *__restrict__ zero_classes,
+                                                                 uint32_t *__restrict__ tb_flag,
+                                                                 uint32_t *__restrict__ tb_items) {
     __shared__ uint32_t wsum[kColThreads / 64];
-    __shared__ uint32_t s_last;
+    __shared__ uint32_t s_last, s_tb;
     __shared__ uint32_t s_ci[GSR_FWD_SB_ORDER ? kMaxSB : 1];  // last workgroup: SB instance totals
     __shared__ uint32_t s_hist[GSR_FWD_SB_ORDER ? 256 : 1];
     const int s = blockIdx.x;
@@ -222,12 +224,23 @@ __global__ __launch_bounds__(kColThreads) void sb_colscan_kernel(SBGrid sg, uint
     __syncthreads();
     if (!s_last) return;
     const int nsb = sg.nsb;
+    if (threadIdx.x == 0) s_tb = 0u;
+    __syncthreads();
     uint32_t cg = 0, ci = 0, mg = 0;
     for (int b = 0; b < nsb; b += kColThreads) {
         const int k = b + (int)threadIdx.x;
         const uint32_t vg = k < nsb ? __hip_atomic_load(&base_g[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
         const uint32_t vi = k < nsb ? __hip_atomic_load(&base_i[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
         mg = max(mg, vg);
+        if (tb_flag && k < nsb) {
+            // tile_bin split: a long list's slices (consecutive items); a full queue leaves it whole
+            uint32_t nsl = vg > (uint32_t)GSR_TB_SPLIT ? min((vg + GSR_TB_SPLIT - 1u) / GSR_TB_SPLIT, kTBMaxSlices) : 0u;
+            const uint32_t at = nsl ? atomicAdd(&s_tb, nsl) : 0u;
+            const bool fits = nsl && at + nsl <= (uint32_t)kTBMaxItems;
+            for (uint32_t j = 0; j < nsl && at + j < (uint32_t)kTBMaxItems; j++)
+                tb_items[at + j] = fits ? ((uint32_t)k | j << 12 | nsl << 18) : kTBVoid;
+            tb_flag[k] = fits ? 1u : 0u;
+        }
         if (GSR_FWD_SB_ORDER && k < nsb) s_ci[k] = vi;
         uint32_t tg, ti;
         const uint32_t eg = block_exclusive_scan<kColThreads>(vg, wsum, tg);
@@ -242,6 +255,10 @@ __global__ __launch_bounds__(kColThreads) void sb_colscan_kernel(SBGrid sg, uint
     if (threadIdx.x == 0) {
         base_g[nsb] = cg;
         base_i[nsb] = ci;
+    }
+    if (tb_flag) {
+        __syncthreads();
+        if (threadIdx.x == 0) tb_flag[nsb] = min(s_tb, (uint32_t)kTBMaxItems);
     }
     if (zero_classes && threadIdx.x < kBwdClasses) zero_classes[threadIdx.x] = 0u;
     if (zero_classes && threadIdx.x == 0) zero_classes[kBwdSegCount] = 0u;
@@ -478,6 +495,7 @@ __global__ __launch_bounds__(64 * kScatterWaves) void sb_scatter_kernel(int P, S
 #define GSR_TB_LONG 4096
 #endif
 constexpr int kTileGroup = 16;
+constexpr int kTBSplitBlocks = 256;  // tb_split_kernel's grid (items dealt round-robin)
 
 #ifndef GSR_TB_DEPTH
 #define GSR_TB_DEPTH 2  // list batches in flight per wave (loads issued one group ahead)
@@ -502,22 +520,17 @@ __device__ __forceinline__ uint32_t group_mask(uint32_t r, int tg, int shift) {
     return m;
 }
 
-template <int kTBWaves>
-__global__ __launch_bounds__(64 * kTBWaves) void tile_bin_kernel(SBGrid sg, int gx, int gy,
-                                                                 const uint32_t *__restrict__ base_g,
-                                                                 const uint32_t *__restrict__ base_i,
-                                                                 const uint2 *__restrict__ sblist,
-                                                                 uint32_t *__restrict__ point_list,
-                                                                 uint2 *__restrict__ ranges,
-                                                                 const uint32_t *__restrict__ kdev, uint32_t cap) {
-    if (*kdev > cap) return;  // the point-list capacity is short: the host re-runs at K
-    __shared__ uint32_t tc[kTBWaves][kMaxTilesPerSB];
-    const int s = blockIdx.x;
+// tile_bin's two list walks over entries [a, b) of an SB list at L0, split over the workgroup's
+// kTBWaves waves (wave w: a contiguous 1/kTBWaves): count = per-wave tile counts into tc[w][t];
+// place = stable placement from per-wave tile starts tc[w][t].
+template <int kTBWaves, bool kPlace>
+__device__ __forceinline__ void tb_walk(const SBGrid &sg, uint32_t L0, uint32_t a, uint32_t b,
+                                        const uint2 *__restrict__ sblist, uint32_t *__restrict__ point_list,
+                                        uint32_t (*tc)[kMaxTilesPerSB]) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int side = 1 << sg.shift, tps = side * side;
-    const int ox = (s % sg.nsbx) * side, oy = (s / sg.nsbx) * side;
-    const uint32_t L0 = base_g[s], L = base_g[s + 1] - L0;
-    const uint32_t seg0 = (uint32_t)(((uint64_t)L * w) / kTBWaves), seg1 = (uint32_t)(((uint64_t)L * (w + 1)) / kTBWaves);
+    const int tps = 1 << (2 * sg.shift);
+    const uint32_t n = b - a;
+    const uint32_t seg0 = a + (uint32_t)(((uint64_t)n * w) / kTBWaves), seg1 = a + (uint32_t)(((uint64_t)n * (w + 1)) / kTBWaves);
     const uint64_t lt = (1ull << lane) - 1ull;
     // the wave's list segment in groups of kTBDepth batches: group n + 1's entries are loaded
     // while group n is ranked (one dependent load latency per group instead of one per batch)
@@ -529,64 +542,10 @@ __global__ __launch_bounds__(64 * kTBWaves) void tile_bin_kernel(SBGrid sg, int 
         }
     };
     constexpr uint32_t kGroup = 64 * kTBDepth;
-
-    // pass A: per-wave tile counts
     for (int tg = 0; tg < tps; tg += kTileGroup) {
-        uint32_t cnt[kTileGroup];
+        uint32_t acc[kTileGroup];
 #pragma unroll
-        for (int k = 0; k < kTileGroup; k++) cnt[k] = 0u;
-        uint2 cur[kTBDepth], nxt[kTBDepth];
-        load(seg0, cur);
-        for (uint32_t gb = seg0; gb < seg1; gb += kGroup) {
-            load(gb + kGroup, nxt);
-#pragma unroll
-            for (int d = 0; d < kTBDepth; d++) {
-                const uint32_t m = group_mask(cur[d].y, tg, sg.shift);
-#pragma unroll
-                for (int k = 0; k < kTileGroup; k++) cnt[k] += (uint32_t)__popcll(__ballot((m >> k) & 1u));
-            }
-#pragma unroll
-            for (int d = 0; d < kTBDepth; d++) cur[d] = nxt[d];
-        }
-        if (lane == 0)
-#pragma unroll
-            for (int k = 0; k < kTileGroup; k++)
-                if (tg + k < tps) tc[w][tg + k] = cnt[k];
-    }
-    __syncthreads();
-    // tile bases (SB-local row-major tile order, waves in list order) and the tile ranges
-    if (w == 0) {
-        uint32_t carry = 0;
-        for (int t0 = 0; t0 < tps; t0 += 64) {
-            const int t = t0 + lane;
-            uint32_t c = 0;
-            if (t < tps)
-                for (int k = 0; k < kTBWaves; k++) c += tc[k][t];
-            uint32_t incl = c;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t v = (uint32_t)__shfl_up((int)incl, o, 64);
-                if (lane >= o) incl += v;
-            }
-            if (t < tps) {
-                uint32_t b = base_i[s] + carry + incl - c;
-                const int x = ox + (t & (side - 1)), y = oy + (t >> sg.shift);
-                if (x < gx && y < gy) ranges[y * gx + x] = make_uint2(b, b + c);
-                for (int k = 0; k < kTBWaves; k++) {
-                    const uint32_t ck = tc[k][t];
-                    tc[k][t] = b;
-                    b += ck;
-                }
-            }
-            carry += (uint32_t)__shfl((int)incl, 63, 64);
-        }
-    }
-    __syncthreads();
-    // pass B: stable placement
-    for (int tg = 0; tg < tps; tg += kTileGroup) {
-        uint32_t pos[kTileGroup];
-#pragma unroll
-        for (int k = 0; k < kTileGroup; k++) pos[k] = tg + k < tps ? tc[w][tg + k] : 0u;
+        for (int k = 0; k < kTileGroup; k++) acc[k] = kPlace ? (tg + k < tps ? tc[w][tg + k] : 0u) : 0u;
         uint2 cur[kTBDepth], nxt[kTBDepth];
         load(seg0, cur);
         for (uint32_t gb = seg0; gb < seg1; gb += kGroup) {
@@ -598,13 +557,140 @@ __global__ __launch_bounds__(64 * kTBWaves) void tile_bin_kernel(SBGrid sg, int 
                 for (int k = 0; k < kTileGroup; k++) {
                     const bool hit = (m >> k) & 1u;
                     const uint64_t bm = __ballot(hit);
-                    if (hit) point_list[pos[k] + (uint32_t)__popcll(bm & lt)] = cur[d].x;
-                    pos[k] += (uint32_t)__popcll(bm);
+                    if (kPlace && hit) point_list[acc[k] + (uint32_t)__popcll(bm & lt)] = cur[d].x;
+                    acc[k] += (uint32_t)__popcll(bm);
                 }
             }
 #pragma unroll
             for (int d = 0; d < kTBDepth; d++) cur[d] = nxt[d];
         }
+        if (!kPlace && lane == 0)
+#pragma unroll
+            for (int k = 0; k < kTileGroup; k++)
+                if (tg + k < tps) tc[w][tg + k] = acc[k];
+    }
+}
+
+// Per-wave tile counts tc[w][t] -> per-wave starts, tiles in SB-local row-major order from `base`
+// plus extra[t] (the instances of tile t placed before this workgroup's entries, tb_place), waves
+// in list order; wave 0 writes the ranges (tile totals tot[t] when given, else this workgroup's
+// counts) when `ranges` is set.
+template <int kTBWaves>
+__device__ __forceinline__ void tb_bases(const SBGrid &sg, int gx, int gy, int s, uint32_t base,
+                                         uint32_t (*tc)[kMaxTilesPerSB], const uint32_t *tot, const uint32_t *extra,
+                                         uint2 *__restrict__ ranges) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int side = 1 << sg.shift, tps = side * side;
+    const int ox = (s % sg.nsbx) * side, oy = (s / sg.nsbx) * side;
+    if (w != 0) return;
+    uint32_t carry = 0;
+    for (int t0 = 0; t0 < tps; t0 += 64) {
+        const int t = t0 + lane;
+        uint32_t c = 0;
+        if (t < tps) {
+            if (tot) c = tot[t];
+            else
+                for (int k = 0; k < kTBWaves; k++) c += tc[k][t];
+        }
+        uint32_t incl = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = (uint32_t)__shfl_up((int)incl, o, 64);
+            if (lane >= o) incl += v;
+        }
+        if (t < tps) {
+            const uint32_t t_base = base + carry + incl - c;
+            const int x = ox + (t & (side - 1)), y = oy + (t >> sg.shift);
+            if (ranges && x < gx && y < gy) ranges[y * gx + x] = make_uint2(t_base, t_base + c);
+            uint32_t b = t_base + (extra ? extra[t] : 0u);
+            for (int k = 0; k < kTBWaves; k++) {
+                const uint32_t ck = tc[k][t];
+                tc[k][t] = b;
+                b += ck;
+            }
+        }
+        carry += (uint32_t)__shfl((int)incl, 63, 64);
+    }
+}
+
+template <int kTBWaves>
+__global__ __launch_bounds__(64 * kTBWaves) void tile_bin_kernel(SBGrid sg, int gx, int gy,
+                                                                 const uint32_t *__restrict__ base_g,
+                                                                 const uint32_t *__restrict__ base_i,
+                                                                 const uint2 *__restrict__ sblist,
+                                                                 uint32_t *__restrict__ point_list,
+                                                                 uint2 *__restrict__ ranges,
+                                                                 const uint32_t *__restrict__ kdev, uint32_t cap,
+                                                                 const uint32_t *__restrict__ tb_flag) {
+    if (*kdev > cap) return;  // the point-list capacity is short: the host re-runs at K
+    const int s = blockIdx.x;
+    if (tb_flag && tb_flag[s]) return;  // a long list: binned in slices (tb_split_kernel)
+    __shared__ uint32_t tc[kTBWaves][kMaxTilesPerSB];
+    const uint32_t L0 = base_g[s], L = base_g[s + 1] - L0;
+    tb_walk<kTBWaves, false>(sg, L0, 0u, L, sblist, point_list, tc);  // pass A: per-wave tile counts
+    __syncthreads();
+    // tile bases (SB-local row-major tile order, waves in list order) and the tile ranges
+    tb_bases<kTBWaves>(sg, gx, gy, s, base_i[s], tc, nullptr, nullptr, ranges);
+    __syncthreads();
+    tb_walk<kTBWaves, true>(sg, L0, 0u, L, sblist, point_list, tc);  // pass B: stable placement
+}
+
+// Long SB lists (tile_bin split): the SB's list in nsl slices of ~L / nsl entries, one work item
+// each, on the side stream beside tile_bin.  kPlace = false (first launch): the slice's tile counts
+// into tb_cnt[item][t].  kPlace = true (second launch): the tile totals and the counts of the
+// slices before this one from every slice's tb_cnt, then tile_bin's bases and placement for the
+// slice -- the same stable order (slices in list order), so the point list is the one tile_bin
+// would write.  Items are dealt round-robin (no waits between items).
+template <int kTBWaves, bool kPlace>
+__global__ __launch_bounds__(64 * kTBWaves) void tb_split_kernel(SBGrid sg, int gx, int gy,
+                                                                 const uint32_t *__restrict__ base_g,
+                                                                 const uint32_t *__restrict__ base_i,
+                                                                 const uint2 *__restrict__ sblist,
+                                                                 uint32_t *__restrict__ point_list,
+                                                                 uint2 *__restrict__ ranges,
+                                                                 const uint32_t *__restrict__ kdev, uint32_t cap,
+                                                                 const uint32_t *__restrict__ tb_flag,
+                                                                 const uint32_t *__restrict__ tb_items,
+                                                                 uint32_t *__restrict__ tb_cnt) {
+    if (*kdev > cap) return;
+    __shared__ uint32_t tc[kTBWaves][kMaxTilesPerSB];
+    __shared__ uint32_t s_tot[kMaxTilesPerSB], s_pre[kMaxTilesPerSB];
+    const int tps = 1 << (2 * sg.shift);
+    const uint32_t n = tb_flag[sg.nsb];
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const uint32_t it = tb_items[i];
+        if (it == kTBVoid) continue;
+        const int s = (int)(it & 0xFFFu);
+        const uint32_t j = (it >> 12) & 0x3Fu, nsl = it >> 18;
+        const uint32_t L0 = base_g[s], L = base_g[s + 1] - L0;
+        const uint32_t Ls = (L + nsl - 1u) / nsl;
+        const uint32_t a = min(L, j * Ls), b = min(L, a + Ls);
+        tb_walk<kTBWaves, false>(sg, L0, a, b, sblist, point_list, tc);
+        __syncthreads();
+        if (!kPlace) {
+            for (int t = threadIdx.x; t < tps; t += 64 * kTBWaves) {
+                uint32_t c = 0;
+                for (int k = 0; k < kTBWaves; k++) c += tc[k][t];
+                tb_cnt[(size_t)i * tps + t] = c;
+            }
+        } else {
+            const uint32_t i0 = i - j;
+            for (int t = threadIdx.x; t < tps; t += 64 * kTBWaves) {
+                uint32_t tot = 0, pre = 0;
+                for (uint32_t jj = 0; jj < nsl; jj++) {
+                    const uint32_t c = tb_cnt[(size_t)(i0 + jj) * tps + t];
+                    tot += c;
+                    pre += jj < j ? c : 0u;
+                }
+                s_tot[t] = tot;
+                s_pre[t] = pre;
+            }
+            __syncthreads();
+            tb_bases<kTBWaves>(sg, gx, gy, s, base_i[s], tc, s_tot, s_pre, j == 0 ? ranges : nullptr);
+            __syncthreads();
+            tb_walk<kTBWaves, true>(sg, L0, a, b, sblist, point_list, tc);
+        }
+        __syncthreads();  // tc / s_tot reused by the next item
     }
 }
 
@@ -920,7 +1006,7 @@ SBGrid sb_grid(int gx, int gy, int P) {
 bool sb_grid_supported(const SBGrid &g) { return g.nsb <= kMaxSB; }
 
 void launch_binning_count(int P, const Camera &cam, const GeomState &gs, bool index_order, const FrameWords &fw,
-                          uint32_t *sb_order, uint32_t *zero_classes, hipStream_t s) {
+                          uint32_t *sb_order, uint32_t *zero_classes, hipStream_t s, bool tb_split) {
     const SBGrid &sg = gs.sb;
     if (P == 0 || cam.gx * cam.gy == 0) return;
     const size_t l1 = sizeof(uint32_t) * 2 * (size_t)sg.nsb;
@@ -929,7 +1015,8 @@ void launch_binning_count(int P, const Camera &cam, const GeomState &gs, bool in
     hipLaunchKernelGGL(sb_count_kernel, dim3(sg.nchunks), dim3(1024), l1, s, P, sg, rects, rects4, gs.sb_cnt_g,
                        gs.sb_cnt_i);
     hipLaunchKernelGGL(sb_colscan_kernel, dim3(sg.nsb), dim3(kColThreads), 0, s, sg, gs.sb_cnt_g, gs.sb_cnt_i,
-                       gs.sb_base_g, gs.sb_base_i, dsort_aux_word(gs), fw, sb_order, zero_classes);
+                       gs.sb_base_g, gs.sb_base_i, dsort_aux_word(gs), fw, sb_order, zero_classes,
+                       tb_split && !index_order ? gs.tb_flag : nullptr, gs.tb_items);
 }
 
 void launch_binning_scatter(int P, const Camera &cam, const GeomState &gs, const BinningState &bs, bool index_order,
@@ -945,7 +1032,7 @@ void launch_binning_scatter(int P, const Camera &cam, const GeomState &gs, const
 }
 
 void launch_binning_tiles(int P, const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
-                          bool local_sort, const uint32_t *maxsb, hipStream_t s) {
+                          bool local_sort, const uint32_t *maxsb, hipStream_t s, bool tb_split, hipStream_t split_stream) {
     const SBGrid &sg = gs.sb;
     const int T = cam.gx * cam.gy;
     if (T == 0) return;
@@ -958,14 +1045,25 @@ void launch_binning_tiles(int P, const Camera &cam, const GeomState &gs, const B
                            gs.sb_base_i, bs.sblist4, bs.point_list, is.ranges, bs.kdev, bs.cap, maxsb);
         return;
     }
+    const uint32_t *flag = tb_split ? gs.tb_flag : nullptr;
+    if (tb_split) {
+        // the long lists' slices beside tile_bin (the caller forked split_stream and joins it)
+        const hipStream_t ss = split_stream ? split_stream : s;
+        hipLaunchKernelGGL((tb_split_kernel<GSR_TB_WAVES_LONG, false>), dim3(kTBSplitBlocks), dim3(64 * GSR_TB_WAVES_LONG), 0,
+                           ss, sg, cam.gx, cam.gy, gs.sb_base_g, gs.sb_base_i, bs.sblist, bs.point_list, is.ranges,
+                           bs.kdev, bs.cap, gs.tb_flag, gs.tb_items, gs.tb_cnt);
+        hipLaunchKernelGGL((tb_split_kernel<GSR_TB_WAVES_LONG, true>), dim3(kTBSplitBlocks), dim3(64 * GSR_TB_WAVES_LONG), 0,
+                           ss, sg, cam.gx, cam.gy, gs.sb_base_g, gs.sb_base_i, bs.sblist, bs.point_list, is.ranges,
+                           bs.kdev, bs.cap, gs.tb_flag, gs.tb_items, gs.tb_cnt);
+    }
     // long superblock lists (large P): more waves per superblock, the 510-ish workgroups of a
     // 1080p frame are too few to hide the list walk's latency otherwise
     if ((int64_t)P > (int64_t)GSR_TB_LONG * sg.nsb)
         hipLaunchKernelGGL(tile_bin_kernel<GSR_TB_WAVES_LONG>, dim3(sg.nsb), dim3(64 * GSR_TB_WAVES_LONG), 0, s, sg, cam.gx, cam.gy, gs.sb_base_g,
-                       gs.sb_base_i, bs.sblist, bs.point_list, is.ranges, bs.kdev, bs.cap);
+                       gs.sb_base_i, bs.sblist, bs.point_list, is.ranges, bs.kdev, bs.cap, flag);
     else
         hipLaunchKernelGGL(tile_bin_kernel<GSR_TB_WAVES>, dim3(sg.nsb), dim3(64 * GSR_TB_WAVES), 0, s, sg, cam.gx, cam.gy, gs.sb_base_g,
-                       gs.sb_base_i, bs.sblist, bs.point_list, is.ranges, bs.kdev, bs.cap);
+                       gs.sb_base_i, bs.sblist, bs.point_list, is.ranges, bs.kdev, bs.cap, flag);
 }
 
 }  // namespace gsr

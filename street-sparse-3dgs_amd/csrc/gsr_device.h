@@ -445,6 +445,16 @@ constexpr int kSBChunk = GSR_SB_CHUNK;  // smallest level-1 chunk (SBGrid.chunk 
 constexpr int kMaxChunks = GSR_MAX_CHUNKS;  // chunks before SBGrid.chunk doubles
 constexpr int kMaxSB = 1536;          // superblocks (3 x 8 waves x 4 B of LDS each in sb_scatter)
 constexpr int kMaxTilesPerSB = 256;   // up to 16 x 16 tiles per superblock
+// Level 2 of long superblock lists (tile_bin split, binning.hip): an SB list longer than
+// GSR_TB_SPLIT entries is binned in up to kTBMaxSlices slices by tb_split_kernel's work items
+// (queued by sb_colscan's last workgroup, at most kTBMaxItems per frame; a full queue leaves the
+// rest to tile_bin).
+#ifndef GSR_TB_SPLIT
+#define GSR_TB_SPLIT 16384
+#endif
+constexpr int kTBMaxItems = 4096;
+constexpr uint32_t kTBMaxSlices = 63;
+constexpr uint32_t kTBVoid = 0xFFFFFFFFu;
 struct SBGrid {
     int shift, nsbx, nsby, nsb, nchunks, chunk;  // chunk: depth-ordered Gaussians per level-1 chunk
     int cper, ccols;                             // counter columns per XCD, row stride of the counters
@@ -563,6 +573,9 @@ struct GeomState {          // per Gaussian, written by preprocess
     float4 *acc;            // backward accumulators, 4 float4 (64 B) per Gaussian, zeroed by render_fwd
     int nacc;               // rows of acc (P)
     uint32_t *live_stamp;   // per Gaussian: the stamp of the last backward whose render_bwd staged it
+    uint32_t *tb_flag;      // tile_bin split: per SB 1 = binned in slices; [nsb] = queued items
+    uint32_t *tb_items;     // ... the slice items (kTBMaxItems: SB | slice << 12 | slices << 18)
+    uint32_t *tb_cnt;       // ... per item and SB tile: the slice's instance count
 };
 // a 4-B packed rect (x0 | y0 << 8 | x1 << 16 | y1 << 24) in the 8-B form (x0 | y0 << 16, x1 | y1 << 16)
 __host__ __device__ __forceinline__ uint2 unpack_rect4(uint32_t q) {

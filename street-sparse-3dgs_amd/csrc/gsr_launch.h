@@ -86,12 +86,13 @@ int debug_trace(int64_t *out, int n, int reset);  // GSR_SB_TRACE builds: sb_sor
 // backward class counters render_fwd fills are zeroed (GSR_BWD_CLS)
 void launch_binning_count(int P, const Camera &cam, const GeomState &gs, bool index_order, const FrameWords &fw,
                           uint32_t *sb_order, uint32_t *zero_classes,
-                          hipStream_t s);
+                          hipStream_t s, bool tb_split = false);
 void launch_binning_scatter(int P, const Camera &cam, const GeomState &gs, const BinningState &bs, bool index_order,
                             hipStream_t s);
 // local_sort: sb_sort_bin (exits when *maxsb > sort_cap()); else tile_bin over depth-ordered lists
 void launch_binning_tiles(int P, const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
-                          bool local_sort, const uint32_t *maxsb, hipStream_t s);
+                          bool local_sort, const uint32_t *maxsb, hipStream_t s, bool tb_split = false,
+                          hipStream_t split_stream = nullptr);
 
 // The gradient arrays render_bwd zeroes beside its replay (ZeroRows): up to six arrays (float
 // counts n[k], 16-B aligned; unused entries n = 0) as one concatenated float4 range split evenly

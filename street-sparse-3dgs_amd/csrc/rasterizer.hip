@@ -72,8 +72,9 @@ bool g_ev_recorded[kStages];
 // inside a captured HIP graph.  One per device, created on first use.
 constexpr int kMaxDevices = 64;
 std::mutex g_side_mu;
-hipStream_t g_side[kMaxDevices] = {};
-hipEvent_t g_fork[kMaxDevices] = {}, g_join[kMaxDevices] = {};
+constexpr int kSides = 2;  // 0: the colour pass and the forward segments' workers; 1: the tile_bin split
+hipStream_t g_side[kSides][kMaxDevices] = {};
+hipEvent_t g_fork[kSides][kMaxDevices] = {}, g_join[kSides][kMaxDevices] = {};
 
 #ifndef GSR_SIDE_STREAM
 #define GSR_SIDE_STREAM 1
@@ -84,20 +85,29 @@ hipEvent_t g_fork[kMaxDevices] = {}, g_join[kMaxDevices] = {};
 #ifndef GSR_K_POLL
 #define GSR_K_POLL 1  // deferred K read by polling the pinned word (0: an event after the upsweep)
 #endif
-bool side_stream(hipStream_t main, hipStream_t *side, hipEvent_t *fork, hipEvent_t *join) {
+bool side_stream(hipStream_t main, hipStream_t *side, hipEvent_t *fork, hipEvent_t *join, int which = 0) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return false;
     std::lock_guard<std::mutex> lk(g_side_mu);
-    if (!g_side[dev]) {
-        if (hipStreamCreateWithFlags(&g_side[dev], hipStreamNonBlocking) != hipSuccess) return false;
-        if (hipEventCreateWithFlags(&g_fork[dev], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&g_join[dev], hipEventDisableTiming) != hipSuccess)
+    if (!g_side[which][dev]) {
+        if (hipStreamCreateWithFlags(&g_side[which][dev], hipStreamNonBlocking) != hipSuccess) return false;
+        if (hipEventCreateWithFlags(&g_fork[which][dev], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&g_join[which][dev], hipEventDisableTiming) != hipSuccess)
             return false;
     }
-    *side = GSR_SIDE_STREAM ? g_side[dev] : main;  // 0: the colour pass serialises (timing experiments)
-    *fork = g_fork[dev];
-    *join = g_join[dev];
+    *side = GSR_SIDE_STREAM ? g_side[which][dev] : main;  // 0: the colour pass serialises (timing experiments)
+    *fork = g_fork[which][dev];
+    *join = g_join[which][dev];
     return true;
+}
+
+// tile_bin split of long superblock lists (GSR_TB_SPLIT): on unless GSR_TB_SPLIT_OFF=1 (A/B)
+bool tb_split_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("GSR_TB_SPLIT_OFF");
+        return !(e && atoi(e) == 1);
+    }();
+    return on;
 }
 
 // Joins the side stream into the main one when the forward leaves early (errors), so the
@@ -210,6 +220,9 @@ GeomState carve_geom(void *base, int P, int gx, int gy, size_t *bytes) {
     g.acc = c.take<float4>(4 * (size_t)P);
     g.nacc = P;
     g.live_stamp = c.take<uint32_t>(P);
+    g.tb_flag = c.take<uint32_t>((size_t)g.sb.nsb + 1);
+    g.tb_items = c.take<uint32_t>(kTBMaxItems);
+    g.tb_cnt = c.take<uint32_t>((size_t)kTBMaxItems << (2 * g.sb.shift));
     if (bytes) *bytes = align_up(c.off, 256);
     return g;
 }
@@ -658,7 +671,7 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
     if (local) {
         {
             StageTimer st(1, s);  // level-1 counts, SB bases, K
-            launch_binning_count(P, cam, gs, true, fw_local, order_sb, zero_cls, s);
+            launch_binning_count(P, cam, gs, true, fw_local, order_sb, zero_cls, s, false);
             if (k_ready) (void)hipEventRecord(k_ready, s);
         }
         if ((rc = check("binning (counts)", debug, s))) return rc;
@@ -730,6 +743,7 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
     const uint32_t fseg_req = fwd_segments_supported() && !sb_order ? g_fwd_seg.load(std::memory_order_relaxed) : 0u;
     uint32_t seg_used = 0;
     auto bin_and_render = [&](int64_t cap, bool counted) -> int {
+        const bool tbs = tb_split_enabled() && !local && P > 0;
         // backward / forward items are numbered tile + T * segment (32 bits)
         seg_used = seg_req && (uint64_t)T * (uint64_t)(cap / seg_req + 1) < (1ull << 32) ? seg_req : 0u;
         const uint32_t fseg_used =
@@ -744,13 +758,22 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
         int r;
         {
             StageTimer st(2, s);
-            if (!local && !counted) launch_binning_count(P, cam, gs, false, fw_none, order_sb, zero_cls, s);
+            if (!local && !counted) launch_binning_count(P, cam, gs, false, fw_none, order_sb, zero_cls, s, tbs);
             launch_binning_scatter(P, cam, gs, bs, local, s);
         }
         if ((r = check("binning (superblocks)", debug, s))) return r;
         {
             StageTimer st(3, s);
-            launch_binning_tiles(P, cam, gs, bs, is, local, dsort_maxsb_word(gs), s);
+            // long superblock lists in slices beside tile_bin (a second side stream: the first may
+            // still carry the colour pass)
+            hipStream_t ts = s;
+            hipEvent_t tf = nullptr, tj = nullptr;
+            const bool tfork = tbs && side_stream(s, &ts, &tf, &tj, 1) && ts != s;
+            if (tfork && (hipEventRecord(tf, s) != hipSuccess || hipStreamWaitEvent(ts, tf, 0) != hipSuccess))
+                return fail(GSR_ERR_DEVICE, "side stream fork failed");
+            launch_binning_tiles(P, cam, gs, bs, is, local, dsort_maxsb_word(gs), s, tbs, tfork ? ts : nullptr);
+            if (tfork && (hipEventRecord(tj, ts) != hipSuccess || hipStreamWaitEvent(s, tj, 0) != hipSuccess))
+                return fail(GSR_ERR_DEVICE, "side stream join failed");
         }
         if ((r = check("binning (tiles)", debug, s))) return r;
         if (!sb_order) {
