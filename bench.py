@@ -755,7 +755,8 @@ def frame_workload(rs, inp, W, H, deg, dev):
                                      False, rs.render_indices, rs.parent_indices, rs.interpolation_weights,
                                      rs.num_node_kids, True)
         fs = _C.frame_stats(raw[4], inp["means3D"].shape[0], H, W)
-    return dict(K=int(raw[0]), Pv=int((raw[3] > 0).sum().item()), P1=fs["level1_entries"])
+    return dict(K=int(raw[0]), Pv=int((raw[3] > 0).sum().item()), P1=fs["level1_entries"],
+                tb_split_items=fs["tb_split_items"], max_sb_list=fs["max_sb_list"])
 
 
 def config4(a, ranks, dev):
@@ -958,7 +959,8 @@ def main():
         "data": "synthetic (seeded Gaussians in the frustum, SURVEY.md 8(d); one chunk per rank, seed = rank)",
         "config": {"workload": f"rasterizer fwd+bwd, {P} Gaussians, SH degree {deg}, {W}x{H}, do_depth",
                    "gaussians": P, "width": W, "height": H, "sh_degree": deg, "visible": Pv, "tile_instances": K,
-                   "level1_entries": P1, "live_rows": Pl, "tiles": T, "bwd_segment": bwd_seg, "fwd_segment": fwd_seg,
+                   "level1_entries": P1, "max_sb_list": wl["max_sb_list"],
+                   "tb_split_items": wl["tb_split_items"], "live_rows": Pl, "tiles": T, "bwd_segment": bwd_seg, "fwd_segment": fwd_seg,
                    "parallelism": f"chunk-per-gpu x{world}"},
         # frac: algorithmic bytes / the kernel's HIP-event time measured here; frac_rocprof: the same
         # bytes / the average duration in the committed rocprofv3 summary of these kernel sources

@@ -196,8 +196,9 @@ int gsr_reset_capacity_hint(void);
 
 /* Statistics of one forward frame, read from its geometry buffer (synchronises the device):
  * out[0] = level-1 binning entries (Gaussian x superblock pairs, "P1" of DESIGN.md), out[1] = tile
- * instances (K).  P = the frame's rendered rows (num_render when non-zero).  Returns the number of
- * values written (<= n).  For bench.py's algorithmic-bytes model. */
+ * instances (K), out[2] = tile_bin split items queued (global-sort frames), out[3] = the longest
+ * superblock list.  P = the frame's rendered rows (num_render when non-zero).  Returns the number
+ * of values written (<= n).  For bench.py's algorithmic-bytes model. */
 int gsr_frame_stats(const void *geom_buffer, int P, int width, int height, int64_t *out, int n);
 
 /* Measurement builds only (a variant library compiled with -DGSR_BLEND_STATS=1; zeros otherwise):

@@ -192,7 +192,7 @@ __global__ __launch_bounds__(kColThreads) void sb_colscan_kernel(SBGrid sg, uint
                                                                  uint32_t *__restrict__ sb_order,
                                                                  uint32_t *__restrict__ zero_classes,
                                                                  uint32_t *__restrict__ tb_flag,
-                                                                 uint32_t *__restrict__ tb_items) {
+                                                                 uint32_t *__restrict__ tb_items, uint32_t tb_len) {
     __shared__ uint32_t wsum[kColThreads / 64];
     __shared__ uint32_t s_last, s_tb;
     __shared__ uint32_t s_ci[GSR_FWD_SB_ORDER ? kMaxSB : 1];  // last workgroup: SB instance totals
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(kColThreads) void sb_colscan_kernel(SBGrid sg, uint
         mg = max(mg, vg);
         if (tb_flag && k < nsb) {
             // tile_bin split: a long list's slices (consecutive items); a full queue leaves it whole
-            uint32_t nsl = vg > (uint32_t)GSR_TB_SPLIT ? min((vg + GSR_TB_SPLIT - 1u) / GSR_TB_SPLIT, kTBMaxSlices) : 0u;
+            uint32_t nsl = vg > tb_len ? min((vg + tb_len - 1u) / tb_len, kTBMaxSlices) : 0u;
             const uint32_t at = nsl ? atomicAdd(&s_tb, nsl) : 0u;
             const bool fits = nsl && at + nsl <= (uint32_t)kTBMaxItems;
             for (uint32_t j = 0; j < nsl && at + j < (uint32_t)kTBMaxItems; j++)
@@ -1006,7 +1006,7 @@ SBGrid sb_grid(int gx, int gy, int P) {
 bool sb_grid_supported(const SBGrid &g) { return g.nsb <= kMaxSB; }
 
 void launch_binning_count(int P, const Camera &cam, const GeomState &gs, bool index_order, const FrameWords &fw,
-                          uint32_t *sb_order, uint32_t *zero_classes, hipStream_t s, bool tb_split) {
+                          uint32_t *sb_order, uint32_t *zero_classes, hipStream_t s, uint32_t tb_split) {
     const SBGrid &sg = gs.sb;
     if (P == 0 || cam.gx * cam.gy == 0) return;
     const size_t l1 = sizeof(uint32_t) * 2 * (size_t)sg.nsb;
@@ -1016,7 +1016,7 @@ void launch_binning_count(int P, const Camera &cam, const GeomState &gs, bool in
                        gs.sb_cnt_i);
     hipLaunchKernelGGL(sb_colscan_kernel, dim3(sg.nsb), dim3(kColThreads), 0, s, sg, gs.sb_cnt_g, gs.sb_cnt_i,
                        gs.sb_base_g, gs.sb_base_i, dsort_aux_word(gs), fw, sb_order, zero_classes,
-                       tb_split && !index_order ? gs.tb_flag : nullptr, gs.tb_items);
+                       tb_split && !index_order ? gs.tb_flag : nullptr, gs.tb_items, tb_split);
 }
 
 void launch_binning_scatter(int P, const Camera &cam, const GeomState &gs, const BinningState &bs, bool index_order,

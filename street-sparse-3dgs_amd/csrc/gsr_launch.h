@@ -86,7 +86,7 @@ int debug_trace(int64_t *out, int n, int reset);  // GSR_SB_TRACE builds: sb_sor
 // backward class counters render_fwd fills are zeroed (GSR_BWD_CLS)
 void launch_binning_count(int P, const Camera &cam, const GeomState &gs, bool index_order, const FrameWords &fw,
                           uint32_t *sb_order, uint32_t *zero_classes,
-                          hipStream_t s, bool tb_split = false);
+                          hipStream_t s, uint32_t tb_split = 0);
 void launch_binning_scatter(int P, const Camera &cam, const GeomState &gs, const BinningState &bs, bool index_order,
                             hipStream_t s);
 // local_sort: sb_sort_bin (exits when *maxsb > sort_cap()); else tile_bin over depth-ordered lists

@@ -101,13 +101,14 @@ bool side_stream(hipStream_t main, hipStream_t *side, hipEvent_t *fork, hipEvent
     return true;
 }
 
-// tile_bin split of long superblock lists (GSR_TB_SPLIT): on unless GSR_TB_SPLIT_OFF=1 (A/B)
-bool tb_split_enabled() {
-    static const bool on = [] {
-        const char *e = getenv("GSR_TB_SPLIT_OFF");
-        return !(e && atoi(e) == 1);
+// tile_bin split of long superblock lists: the list length past which an SB is sliced, GSR_TB_SPLIT
+// or the environment's GSR_TB_SPLIT (measurement A/B; 0 = off)
+uint32_t tb_split_len() {
+    static const uint32_t len = [] {
+        const char *e = getenv("GSR_TB_SPLIT");
+        return e ? (uint32_t)std::max(0, atoi(e)) : (uint32_t)GSR_TB_SPLIT;
     }();
-    return on;
+    return len;
 }
 
 // Joins the side stream into the main one when the forward leaves early (errors), so the
@@ -743,7 +744,7 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
     const uint32_t fseg_req = fwd_segments_supported() && !sb_order ? g_fwd_seg.load(std::memory_order_relaxed) : 0u;
     uint32_t seg_used = 0;
     auto bin_and_render = [&](int64_t cap, bool counted) -> int {
-        const bool tbs = tb_split_enabled() && !local && P > 0;
+        const uint32_t tbs = !local && P > 0 ? tb_split_len() : 0u;
         // backward / forward items are numbered tile + T * segment (32 bits)
         seg_used = seg_req && (uint64_t)T * (uint64_t)(cap / seg_req + 1) < (1ull << 32) ? seg_req : 0u;
         const uint32_t fseg_used =
@@ -768,10 +769,10 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
             // still carry the colour pass)
             hipStream_t ts = s;
             hipEvent_t tf = nullptr, tj = nullptr;
-            const bool tfork = tbs && side_stream(s, &ts, &tf, &tj, 1) && ts != s;
+            const bool tfork = tbs != 0u && side_stream(s, &ts, &tf, &tj, 1) && ts != s;
             if (tfork && (hipEventRecord(tf, s) != hipSuccess || hipStreamWaitEvent(ts, tf, 0) != hipSuccess))
                 return fail(GSR_ERR_DEVICE, "side stream fork failed");
-            launch_binning_tiles(P, cam, gs, bs, is, local, dsort_maxsb_word(gs), s, tbs, tfork ? ts : nullptr);
+            launch_binning_tiles(P, cam, gs, bs, is, local, dsort_maxsb_word(gs), s, tbs != 0u, tfork ? ts : nullptr);
             if (tfork && (hipEventRecord(tj, ts) != hipSuccess || hipStreamWaitEvent(s, tj, 0) != hipSuccess))
                 return fail(GSR_ERR_DEVICE, "side stream join failed");
         }
@@ -1041,18 +1042,22 @@ int gsr_frame_stats(const void *geom_buffer, int P, int width, int height, int64
     if (!out || n < 0 || P < 0 || width <= 0 || height <= 0)
         return fail(GSR_ERR_INVALID_ARGUMENT, "gsr_frame_stats: bad arguments");
     if (P == 0 || n == 0) {
-        for (int k = 0; k < n && k < 2; k++) out[k] = 0;
-        return n < 2 ? n : 2;
+        for (int k = 0; k < n && k < 4; k++) out[k] = 0;
+        return n < 4 ? n : 4;
     }
     if (!geom_buffer) return fail(GSR_ERR_INVALID_ARGUMENT, "gsr_frame_stats: NULL geometry buffer");
     const int gx = (width + kTile - 1) / kTile, gy = (height + kTile - 1) / kTile;
     const GeomState gs = carve_geom(const_cast<void *>(geom_buffer), P, gx, gy, nullptr);
-    uint32_t v[2] = {0u, 0u};
-    if (hipMemcpy(&v[0], gs.sb_base_g + gs.sb.nsb, sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemcpy(&v[1], gs.sb_base_i + gs.sb.nsb, sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
+    std::vector<uint32_t> bg((size_t)gs.sb.nsb + 1);
+    uint32_t v[4] = {0u, 0u, 0u, 0u};
+    if (hipMemcpy(bg.data(), gs.sb_base_g, sizeof(uint32_t) * bg.size(), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(&v[1], gs.sb_base_i + gs.sb.nsb, sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(&v[2], gs.tb_flag + gs.sb.nsb, sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
         return fail(GSR_ERR_DEVICE, "gsr_frame_stats: copy failed");
+    v[0] = bg[gs.sb.nsb];
+    for (int k = 0; k < gs.sb.nsb; k++) v[3] = std::max(v[3], bg[k + 1] - bg[k]);
     int k = 0;
-    for (; k < n && k < 2; k++) out[k] = (int64_t)v[k];
+    for (; k < n && k < 4; k++) out[k] = (int64_t)v[k];
     return k;
 }
 

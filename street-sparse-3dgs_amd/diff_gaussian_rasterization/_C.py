@@ -352,14 +352,15 @@ def forward_stats() -> dict:
 
 
 def frame_stats(geomBuffer, P, image_height, image_width) -> dict:
-    """Level-1 binning entries and tile instances of the frame whose geometry buffer this is
-    (gsr_frame_stats; one device sync)."""
-    buf = (ctypes.c_int64 * 2)()
+    """Level-1 binning entries, tile instances, tile_bin split items and the longest superblock
+    list of the frame whose geometry buffer this is (gsr_frame_stats; one device sync)."""
+    buf = (ctypes.c_int64 * 4)()
     with torch.cuda.device(geomBuffer.device):
-        n = _L.gsr_frame_stats(_ptr(geomBuffer), int(P), int(image_width), int(image_height), buf, 2)
+        n = _L.gsr_frame_stats(_ptr(geomBuffer), int(P), int(image_width), int(image_height), buf, 4)
     if n < 0:
         _check(n, "frame_stats")
-    return {"level1_entries": int(buf[0]), "tile_instances": int(buf[1])}
+    return {"level1_entries": int(buf[0]), "tile_instances": int(buf[1]), "tb_split_items": int(buf[2]),
+            "max_sb_list": int(buf[3])}
 
 
 def set_profiling(enable: bool) -> None:
