@@ -161,8 +161,9 @@ int gsr_set_deterministic(int enable);
  * previous length, or GSR_ERR_INVALID_ARGUMENT / GSR_ERR_UNSUPPORTED. */
 int gsr_set_bwd_segment(int L);
 
-/* Forward work split, process-wide.  L = 0 (default): render_fwd blends every tile in one
- * workgroup.  L > 0 (a multiple of 64, >= 4096): a tile whose list is longer than 2 L is blended as
+/* Forward work split, process-wide.  L = 0: render_fwd blends every tile in one workgroup.  L > 0
+ * (a multiple of 64, >= 4096; default 4096, behind the split gate): a tile whose list is longer than
+ * 2 L is blended as
  * ceil(len / L) work items by a pool of worker workgroups -- each item multiplies out the
  * transmittance through its positions, takes its predecessors' product (in segment order) and
  * blends its positions from there; the tile's last item adds the items' colours in order.  Colours
@@ -170,6 +171,14 @@ int gsr_set_bwd_segment(int L);
  * ulp of the transmittance product.  Returns the previous length, or GSR_ERR_INVALID_ARGUMENT /
  * GSR_ERR_UNSUPPORTED. */
 int gsr_set_fwd_segment(int L);
+
+/* The split gate, process-wide.  1 (default): the forward split (gsr_set_fwd_segment) and the
+ * tile binning's split of long superblock lists are armed only for the 256 frames (per device and
+ * calling thread) after one whose longest tile / superblock list called for them -- they cost a few
+ * microseconds of launches and stream hand-offs per frame and pay only on such frames.  0: armed on
+ * every frame (the outputs are the same either way, to fp32 summation order).  Returns the previous
+ * setting. */
+int gsr_set_split_gate(int enable);
 
 /* Diagnostic (host arithmetic only): the bytes the backward checkpoints and the forward items need
  * past the start of a binning buffer carved for K instances with segment lengths L / Lf (*need),
@@ -190,8 +199,9 @@ int gsr_set_binning(int mode);
 int gsr_forward_stats(int64_t *out, int n);
 
 /* Forget the calling thread's point-list capacity hint (the largest K of its last 256 frames per
- * device): the next frame reads K before binning, as the first one does.  For a caller that
- * switches to a much smaller workload (the buffers follow the hint) and for tests.  ABI 3. */
+ * device) and its split-gate history: the next frame reads K before binning, as the first one does,
+ * and the gated splits wait for a long-list frame again.  For a caller that switches to a much
+ * smaller workload (the buffers follow the hint) and for tests.  ABI 3. */
 int gsr_reset_capacity_hint(void);
 
 /* Statistics of one forward frame, read from its geometry buffer (synchronises the device):

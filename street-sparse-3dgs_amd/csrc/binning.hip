@@ -192,7 +192,8 @@ __global__ __launch_bounds__(kColThreads) void sb_colscan_kernel(SBGrid sg, uint
                                                                  uint32_t *__restrict__ sb_order,
                                                                  uint32_t *__restrict__ zero_classes,
                                                                  uint32_t *__restrict__ tb_flag,
-                                                                 uint32_t *__restrict__ tb_items, uint32_t tb_len) {
+                                                                 uint32_t *__restrict__ tb_items, uint32_t tb_len,
+                                                                 uint32_t *__restrict__ host_sblist) {
     __shared__ uint32_t wsum[kColThreads / 64];
     __shared__ uint32_t s_last, s_tb;
     __shared__ uint32_t s_ci[GSR_FWD_SB_ORDER ? kMaxSB : 1];  // last workgroup: SB instance totals
@@ -234,7 +235,7 @@ __global__ __launch_bounds__(kColThreads) void sb_colscan_kernel(SBGrid sg, uint
         mg = max(mg, vg);
         if (tb_flag && k < nsb) {
             // tile_bin split: a long list's slices (consecutive items); a full queue leaves it whole
-            uint32_t nsl = vg > tb_len ? min((vg + tb_len - 1u) / tb_len, kTBMaxSlices) : 0u;
+            uint32_t nsl = tb_len && vg > tb_len ? min((vg + tb_len - 1u) / tb_len, kTBMaxSlices) : 0u;
             const uint32_t at = nsl ? atomicAdd(&s_tb, nsl) : 0u;
             const bool fits = nsl && at + nsl <= (uint32_t)kTBMaxItems;
             for (uint32_t j = 0; j < nsl && at + j < (uint32_t)kTBMaxItems; j++)
@@ -293,9 +294,10 @@ __global__ __launch_bounds__(kColThreads) void sb_colscan_kernel(SBGrid sg, uint
         __syncthreads();
         for (int k = threadIdx.x; k < nsb; k += kColThreads) sb_order[atomicAdd(&s_hist[cls(k)], 1u)] = (uint32_t)k;
     }
-    if (fw.dev_K) {
-        // local-sort frames: K (= the instance total) and the longest SB list for the kernels and
-        // the host.  The host's K word is stored last (the host reads the others once it is set).
+    if (fw.dev_K || host_sblist) {
+        // the longest SB list: for the split gate's hint (host_sblist), and on local-sort frames K
+        // (= the instance total) and that maximum for the kernels and the host.  The host's K word
+        // is stored last (the host reads the others once it is set).
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) mg = max(mg, (uint32_t)__shfl_xor((int)mg, o, 64));
         __syncthreads();
@@ -303,6 +305,11 @@ __global__ __launch_bounds__(kColThreads) void sb_colscan_kernel(SBGrid sg, uint
         __syncthreads();
         if (threadIdx.x == 0) {
             for (int k = 1; k < kColThreads / 64; k++) mg = max(mg, wsum[k]);
+            if (host_sblist) __hip_atomic_store(host_sblist, mg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    if (fw.dev_K) {
+        if (threadIdx.x == 0) {
             // an SB list too long for the local sort: the device K word reads "capacity short" to
             // every later kernel of the frame (they exit at once; the host re-runs the frame
             // through the global sort, which stores the real K there again)
@@ -1006,7 +1013,8 @@ SBGrid sb_grid(int gx, int gy, int P) {
 bool sb_grid_supported(const SBGrid &g) { return g.nsb <= kMaxSB; }
 
 void launch_binning_count(int P, const Camera &cam, const GeomState &gs, bool index_order, const FrameWords &fw,
-                          uint32_t *sb_order, uint32_t *zero_classes, hipStream_t s, uint32_t tb_split) {
+                          uint32_t *sb_order, uint32_t *zero_classes, hipStream_t s, uint32_t tb_split,
+                          uint32_t *host_sblist) {
     const SBGrid &sg = gs.sb;
     if (P == 0 || cam.gx * cam.gy == 0) return;
     const size_t l1 = sizeof(uint32_t) * 2 * (size_t)sg.nsb;
@@ -1016,7 +1024,7 @@ void launch_binning_count(int P, const Camera &cam, const GeomState &gs, bool in
                        gs.sb_cnt_i);
     hipLaunchKernelGGL(sb_colscan_kernel, dim3(sg.nsb), dim3(kColThreads), 0, s, sg, gs.sb_cnt_g, gs.sb_cnt_i,
                        gs.sb_base_g, gs.sb_base_i, dsort_aux_word(gs), fw, sb_order, zero_classes,
-                       tb_split && !index_order ? gs.tb_flag : nullptr, gs.tb_items, tb_split);
+                       index_order ? nullptr : gs.tb_flag, gs.tb_items, tb_split, host_sblist);
 }
 
 void launch_binning_scatter(int P, const Camera &cam, const GeomState &gs, const BinningState &bs, bool index_order,

@@ -589,7 +589,9 @@ __host__ __device__ __forceinline__ const uint32_t *drect4_of(const GeomState &g
 // Frame words a local-sort frame's column scan publishes (binning.hip): device copies for the
 // kernels (dev_K = the depth sort's K word, which every capacity test reads) and, when host is set,
 // the pinned host words the host waits on.  host[kHostK] is stored last.
-enum HostWord { kHostK = 0, kHostErr = 1, kHostMaxSB = 2, kHostP1 = 3, kHostWords = 4 };
+// kHostSBList / kHostTileList: every frame's longest superblock list (sb_colscan) and longest tile
+// list (the forward's tile_order), read by the host as the split gate's hint (rasterizer.hip)
+enum HostWord { kHostK = 0, kHostErr = 1, kHostMaxSB = 2, kHostP1 = 3, kHostSBList = 4, kHostTileList = 5, kHostWords = 6 };
 struct FrameWords {
     uint32_t *dev_K;      // nullptr: global-sort frame (dsort publishes K)
     uint32_t *dev_maxsb;  // longest SB list

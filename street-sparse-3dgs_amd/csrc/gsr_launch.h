@@ -47,7 +47,8 @@ void launch_preprocess_color(const GaussianInputs &in, const Camera &cam, const 
 // binning buffer at bin_base; fctl = bwd_cnt + kFwdItemsWord).
 void launch_tile_order(const uint32_t *work, const uint2 *ranges, int T, int shift, uint32_t *order, hipStream_t s,
                        const uint32_t *kdev = nullptr, uint32_t cap = 0, uint32_t *zero_classes = nullptr,
-                       uint32_t *fctl = nullptr, void *bin_base = nullptr, uint32_t seg_len = 0, uint32_t fseg_len = 0);
+                       uint32_t *fctl = nullptr, void *bin_base = nullptr, uint32_t seg_len = 0, uint32_t fseg_len = 0,
+                       uint32_t *host_tilelist = nullptr);
 void launch_mark_visible(int P, const float *means3D, const float *view, uint8_t *present, hipStream_t s);
 
 // sort.hip (rocPRIM)
@@ -86,7 +87,7 @@ int debug_trace(int64_t *out, int n, int reset);  // GSR_SB_TRACE builds: sb_sor
 // backward class counters render_fwd fills are zeroed (GSR_BWD_CLS)
 void launch_binning_count(int P, const Camera &cam, const GeomState &gs, bool index_order, const FrameWords &fw,
                           uint32_t *sb_order, uint32_t *zero_classes,
-                          hipStream_t s, uint32_t tb_split = 0);
+                          hipStream_t s, uint32_t tb_split = 0, uint32_t *host_sblist = nullptr);
 void launch_binning_scatter(int P, const Camera &cam, const GeomState &gs, const BinningState &bs, bool index_order,
                             hipStream_t s);
 // local_sort: sb_sort_bin (exits when *maxsb > sort_cap()); else tile_bin over depth-ordered lists

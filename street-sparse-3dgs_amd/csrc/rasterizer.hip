@@ -58,6 +58,16 @@ thread_local int g_khead[kMaxDevicesK] = {};
 #define GSR_DEFER_K 1
 #endif
 constexpr uint32_t kKPending = 0xFFFFFFFFu;
+// The split gate (gsr_set_split_gate): the forward split and the tile_bin split cost launches and
+// stream hand-offs on every frame they are armed for, and pay only on frames with very long lists
+// (a street view after an opacity reset), so they are armed for kSplitMemory frames after a frame
+// (per device and thread) whose longest tile / superblock list called for them -- the kernels report
+// those lengths in pinned memory, read at the next forward.
+constexpr int64_t kSplitMemory = 256;
+thread_local int64_t g_frame_no[kMaxDevicesK] = {};
+thread_local int64_t g_long_tile_at[kMaxDevicesK] = {};
+thread_local int64_t g_long_sb_at[kMaxDevicesK] = {};
+std::atomic<int> g_split_gate{1};
 
 // Stage profiling is process-wide: torch runs the backward on its autograd device thread.
 constexpr int kStages = 10;
@@ -420,7 +430,7 @@ uint8_t forward_uncleared(const void *geom) {
 #endif
 std::atomic<uint32_t> g_bwd_seg{GSR_BWD_SEG_DEFAULT};
 #ifndef GSR_FWD_SEG_DEFAULT
-#define GSR_FWD_SEG_DEFAULT 0
+#define GSR_FWD_SEG_DEFAULT 4096  // behind the split gate (gsr_set_split_gate)
 #endif
 std::atomic<uint32_t> g_fwd_seg{GSR_FWD_SEG_DEFAULT};
 std::mutex g_seg_mu;
@@ -654,6 +664,7 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
                 hipHostGetDevicePointer(reinterpret_cast<void **>(&g_pinned_dev), g_pinned, 0) != hipSuccess)
                 return fail(GSR_ERR_ALLOCATION, "pinned host allocation failed");
             for (int k = 0; k < kHostWords; k++) g_pinned[k] = 0u;
+            for (int d = 0; d < kMaxDevicesK; d++) g_long_tile_at[d] = g_long_sb_at[d] = -2 * kSplitMemory;
         }
         if (!g_k_ready[dev] && hipEventCreateWithFlags(&g_k_ready[dev], hipEventDisableTiming) != hipSuccess)
             return fail(GSR_ERR_DEVICE, "event creation failed");
@@ -741,10 +752,23 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
     if (split && !GSR_COLOR_SERIAL && !color_early && (rc = fork_color())) return rc;
     bool joined = false;
     const uint32_t seg_req = need_bwd && bwd_segments_supported() ? g_bwd_seg.load(std::memory_order_relaxed) : 0u;
-    const uint32_t fseg_req = fwd_segments_supported() && !sb_order ? g_fwd_seg.load(std::memory_order_relaxed) : 0u;
+    uint32_t fseg_req = fwd_segments_supported() && !sb_order ? g_fwd_seg.load(std::memory_order_relaxed) : 0u;
+    uint32_t tb_req = tb_split_len();
+    if (P > 0) {
+        // the split gate: the longest lists of the frames before (whatever the pinned words hold now)
+        const int64_t f = ++g_frame_no[dev];
+        const uint32_t tl = __atomic_load_n(&g_pinned[kHostTileList], __ATOMIC_RELAXED);
+        const uint32_t sl = __atomic_load_n(&g_pinned[kHostSBList], __ATOMIC_RELAXED);
+        if (fseg_req && tl > 2u * fseg_req) g_long_tile_at[dev] = f;
+        if (tb_req && sl > tb_req) g_long_sb_at[dev] = f;
+        if (g_split_gate.load(std::memory_order_relaxed)) {
+            if (f - g_long_tile_at[dev] > kSplitMemory) fseg_req = 0;
+            if (f - g_long_sb_at[dev] > kSplitMemory) tb_req = 0;
+        }
+    }
     uint32_t seg_used = 0;
     auto bin_and_render = [&](int64_t cap, bool counted) -> int {
-        const uint32_t tbs = !local && P > 0 ? tb_split_len() : 0u;
+        const uint32_t tbs = !local && P > 0 ? tb_req : 0u;
         // backward / forward items are numbered tile + T * segment (32 bits)
         seg_used = seg_req && (uint64_t)T * (uint64_t)(cap / seg_req + 1) < (1ull << 32) ? seg_req : 0u;
         const uint32_t fseg_used =
@@ -759,7 +783,8 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
         int r;
         {
             StageTimer st(2, s);
-            if (!local && !counted) launch_binning_count(P, cam, gs, false, fw_none, order_sb, zero_cls, s, tbs);
+            if (!local && !counted)
+                launch_binning_count(P, cam, gs, false, fw_none, order_sb, zero_cls, s, tbs, g_pinned_dev + kHostSBList);
             launch_binning_scatter(P, cam, gs, bs, local, s);
         }
         if ((r = check("binning (superblocks)", debug, s))) return r;
@@ -782,7 +807,7 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
             // forward order: by list length (and the backward's class counters zeroed)
             launch_tile_order(nullptr, is.ranges, T, 4, is.tile_ids, s, bs.kdev, bs.cap,
                               GSR_BWD_CLS && need_bwd ? is.bwd_cnt : nullptr, is.bwd_cnt + kFwdItemsWord, bs.point_list,
-                              seg_used, fseg_used);
+                              seg_used, fseg_used, P > 0 ? g_pinned_dev + kHostTileList : nullptr);
         }
         if ((r = check("tile order", debug, s))) return r;
         if (split && !GSR_COLOR_SERIAL && !joined) {
@@ -984,6 +1009,8 @@ int gsr_set_true_scale_gradient(int enable) {
 
 int gsr_set_deterministic(int enable) { return g_deterministic.exchange(enable ? 1 : 0); }
 
+int gsr_set_split_gate(int enable) { return g_split_gate.exchange(enable ? 1 : 0); }
+
 int gsr_set_fwd_segment(int L) {
     if (L < 0 || (L > 0 && (L < (int)kMinFwdSeg || L % kWave != 0)))
         return fail(GSR_ERR_INVALID_ARGUMENT, "forward segment length: 0 (off) or a multiple of 64 >= 4096");
@@ -1030,7 +1057,9 @@ int gsr_segment_layout_check(int64_t K, int L, int Lf, int64_t *need, int64_t *h
 }
 
 int gsr_reset_capacity_hint(void) {
+    if (g_pinned) g_pinned[kHostTileList] = g_pinned[kHostSBList] = 0u;
     for (int d = 0; d < kMaxDevicesK; d++) {
+        g_long_tile_at[d] = g_long_sb_at[d] = g_frame_no[d] - 2 * kSplitMemory;
         g_khint[d] = 0;
         g_khead[d] = 0;
         for (int i = 0; i < kKHist; i++) g_khist[d][i] = 0;

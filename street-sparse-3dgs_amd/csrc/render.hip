@@ -753,16 +753,25 @@ __device__ __forceinline__ int bwd_tile_of(uint32_t b, const uint32_t *__restric
 __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t *__restrict__ work, const uint2 *__restrict__ ranges,
                                                           int T, int shift, uint32_t *__restrict__ order, const uint32_t *__restrict__ kdev, uint32_t cap,
                                                           uint32_t *__restrict__ zero_classes, uint32_t *__restrict__ fctl,
-                                                          void *bin_base, uint32_t seg_len, uint32_t fseg_len) {
+                                                          void *bin_base, uint32_t seg_len, uint32_t fseg_len,
+                                                          uint32_t *__restrict__ host_tilelist) {
     // the forward order's launch also zeroes the backward class counters render_fwd fills
     if (zero_classes && threadIdx.x < kBwdClasses) zero_classes[threadIdx.x] = 0u;
     if (zero_classes && threadIdx.x == 0) zero_classes[kBwdSegCount] = 0u;
     if (kdev && *kdev > cap) return;  // ranges / work were not written this pass (capacity re-run)
     __shared__ uint32_t hist[256];
-    __shared__ uint32_t s_items;
+    __shared__ uint32_t s_items, s_max;
     if (threadIdx.x < 256) hist[threadIdx.x] = 0u;
-    if (threadIdx.x == 0) s_items = 0u;
+    if (threadIdx.x == 0) s_items = s_max = 0u;
     __syncthreads();
+    if (host_tilelist) {
+        // the longest tile list, for the split gate's hint
+        uint32_t mx = 0;
+        for (int t = threadIdx.x; t < T; t += 1024) mx = max(mx, ranges[t].y - ranges[t].x);
+        atomicMax(&s_max, mx);
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_store(host_tilelist, s_max, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     if (fseg_len) {
         // forward segments: the work-item queue of the tiles longer than fseg_len (a tile's items
         // consecutive, segment order), their tickets zeroed
@@ -812,10 +821,10 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t *__rest
 
 void launch_tile_order(const uint32_t *work, const uint2 *ranges, int T, int shift, uint32_t *order, hipStream_t s,
                        const uint32_t *kdev, uint32_t cap, uint32_t *zero_classes, uint32_t *fctl, void *bin_base,
-                       uint32_t seg_len, uint32_t fseg_len) {
+                       uint32_t seg_len, uint32_t fseg_len, uint32_t *host_tilelist) {
     if (T == 0) return;
     hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, s, work, ranges, T, shift, order, kdev, cap, zero_classes,
-                       fctl, bin_base, seg_len, fctl ? fseg_len : 0u);
+                       fctl, bin_base, seg_len, fctl ? fseg_len : 0u, host_tilelist);
 }
 
 // the worker pool's size: kFwdWorkers, or GSR_FWD_WORKERS from the environment (measurement A/B)

@@ -329,12 +329,19 @@ def set_bwd_segment(length: int) -> int:
 
 
 def set_fwd_segment(length: int) -> int:
-    """Forward work split (gsr_set_fwd_segment): 0 = one workgroup per tile (default), L = a
-    multiple of 64 >= 4096 = tiles with longer lists blended as segments of L positions by a
-    worker pool.  Process-wide; returns the previous length."""
+    """Forward work split (gsr_set_fwd_segment): 0 = one workgroup per tile, L = a multiple of 64
+    >= 4096 (default 4096, behind the split gate) = tiles with lists longer than 2 L blended as
+    segments of L positions by a worker pool.  Process-wide; returns the previous length."""
     r = _L.gsr_set_fwd_segment(int(length))
     _check(0 if r >= 0 else r, "set_fwd_segment")
     return r
+
+
+def set_split_gate(enable: bool) -> bool:
+    """gsr_set_split_gate: True (default) arms the forward split and the tile binning's superblock
+    split only for the 256 frames after one whose lists called for them; False arms them on every
+    frame.  Process-wide; returns the previous setting."""
+    return bool(_L.gsr_set_split_gate(int(bool(enable))))
 
 
 def reset_capacity_hint() -> None:

@@ -24,6 +24,15 @@ from test_gpu_parity import compare, make_scene, run_hip, run_oracle, upstream_g
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True)
+def _splits_every_frame():
+    """The split gate off: every frame of these tests takes the splits it is set up for."""
+    from diff_gaussian_rasterization import _C
+    prev = _C.set_split_gate(False)
+    yield
+    _C.set_split_gate(prev)
+
 SEG_TOL = 1e-5  # segmented vs unsplit gradients, relative L2 (fp32 rounding of S at the checkpoints; measured <= 2.2e-6)
 
 CASES = [
@@ -268,3 +277,41 @@ def test_set_fwd_segment_validation():
         assert _C.set_fwd_segment(4096) == 8192
     finally:
         _C.set_fwd_segment(prev)
+
+
+def test_split_gate_arms_after_a_long_list_frame():
+    """Gate on: the first frame of long lists runs unsplit and reports its lengths; the frames after
+    it take the tile binning split (frame_stats counts its items) and the forward split; a scene
+    with short lists never arms them."""
+    import torch
+    from diff_gaussian_rasterization import _C
+    from helpers import settings, torch_inputs
+    dev = torch.device("cuda:0")
+
+    def frame(c):
+        s = seg_scene(c)
+        inp = torch_inputs(s, dev, requires_grad=False)
+        rs = settings(s, dev, c["deg"])
+        e = torch.empty(0, device=dev)
+        raw = _C.rasterize_gaussians(rs.bg, inp["means3D"], e, inp["opacities"], inp["scales"], inp["rotations"],
+                                     1.0, e, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, c["H"], c["W"],
+                                     inp["shs"], c["deg"], rs.campos, False, False, rs.render_indices,
+                                     rs.parent_indices, rs.interpolation_weights, rs.num_node_kids, True)
+        torch.cuda.synchronize()
+        return _C.frame_stats(raw[4], c["P"], c["H"], c["W"]), raw[1].cpu().numpy()
+
+    _C.set_split_gate(True)
+    _C.reset_capacity_hint()
+    short = dict(name="short", P=2000, W=96, H=64, deg=1, seed=5, log_scale=-3.0, opac=(0.3, 0.9))
+    for _ in range(2):
+        st, _ = frame(short)
+        assert st["tb_split_items"] == 0
+    long_ = FWD_CASES[0]
+    st1, img1 = frame(long_)
+    assert st1["max_sb_list"] > 16384 and st1["tb_split_items"] == 0  # the first long frame: gate closed
+    st2, img2 = frame(long_)
+    assert st2["tb_split_items"] > 0  # armed by the frame before
+    np.testing.assert_allclose(img2, img1, rtol=0, atol=FWD_MAXABS)  # forward split: same image
+    _C.reset_capacity_hint()
+    st3, _ = frame(long_)
+    assert st3["tb_split_items"] == 0
