@@ -492,7 +492,7 @@ constexpr size_t kSegReserve = 32768;    // carved past the level-1 lists (a sma
 inline int64_t bwd_grid(int T, int64_t K, uint32_t L) { return (int64_t)T + (L ? K / L : 0); }
 __host__ __device__ __forceinline__ size_t align256(size_t b) { return (b + 255) / 256 * 256; }
 
-// Forward segments (gsr_set_fwd_segment): a tile whose list is longer than 2 Lf positions is
+// Forward segments (gsr_set_fwd_segment): a tile whose list is longer than fseg_min_len(Lf) is
 // blended as ceil(len / Lf) work items by render_fwd_seg_kernel's kFwdWorkers workgroups (an item
 // queue tile_order fills), launched beside render_fwd on a side stream.  Item s first multiplies
 // out (1 - alpha) over its positions (the pixels' transmittance through the segment), publishes it,
@@ -502,9 +502,12 @@ __host__ __device__ __forceinline__ size_t align256(size_t b) { return (b + 255)
 // item's counts the finished items), a flag (1: its transmittance row is published; zeroed with
 // the queue), 4 checkpoint counts, the per-pixel transmittance row and 256 x 6 partials.
 constexpr uint32_t kMinFwdSeg = 4096;
-// a tile is split when its list holds more than two segments (3+ items: with two, the second
-// item's wait for the first one's transmittance pass leaves little to gain)
-__host__ __device__ __forceinline__ bool fseg_splits(uint32_t len, uint32_t Lf) { return Lf && len > 2u * Lf; }
+// a tile is split when its list is longer than fseg_min (kFsegFactor segments by default: a tile
+// of a few segments whose pixels saturate early gains little)
+#ifndef GSR_FSEG_FACTOR
+#define GSR_FSEG_FACTOR 4
+#endif
+__host__ __device__ __forceinline__ bool fseg_splits(uint32_t len, uint32_t fseg_min) { return fseg_min && len > fseg_min; }
 constexpr int kFwdWorkers = 256;
 constexpr int kFwdPartials = 6;  // r, g, b, inverse depth, T at the end, last contributor | stop << 31
 // bwd_cnt's words past the backward's: the item count tile_order wrote, the queue's next item

@@ -759,7 +759,7 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
         const int64_t f = ++g_frame_no[dev];
         const uint32_t tl = __atomic_load_n(&g_pinned[kHostTileList], __ATOMIC_RELAXED);
         const uint32_t sl = __atomic_load_n(&g_pinned[kHostSBList], __ATOMIC_RELAXED);
-        if (fseg_req && tl > 2u * fseg_req) g_long_tile_at[dev] = f;
+        if (fseg_req && tl > fseg_min_len(fseg_req)) g_long_tile_at[dev] = f;
         if (tb_req && sl > tb_req) g_long_sb_at[dev] = f;
         if (g_split_gate.load(std::memory_order_relaxed)) {
             if (f - g_long_tile_at[dev] > kSplitMemory) fseg_req = 0;

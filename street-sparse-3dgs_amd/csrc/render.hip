@@ -293,7 +293,9 @@ __device__ __forceinline__ void wg_acquire() {
 
 // render_fwd_seg_kernel's workgroups (forward segments): items from the queue tile_order
 // filled until it is empty (FwdSegLayout).  Item i = segment s of its tile: (1) the transmittance
-// through the segment (skipped for the tile's last segment) published per pixel; (2) the product of
+// through the segment published per pixel (skipped for the tile's last segment; segment 0 publishes
+// the transmittance its blend ends with instead, so a tile whose pixels saturate early costs about
+// what it costs unsplit); (2) the product of
 // the predecessors', in segment order once every predecessor's flag is set (each row made visible
 // with a release fence before its flag; items of a tile are taken in order, so every predecessor's
 // workgroup is resident), so the product does not depend on which item finished first; (3) the blend from that transmittance into the item's partials; (4) the
@@ -330,7 +332,7 @@ __device__ void fwd_seg_worker(const uint2 *__restrict__ ranges, const uint32_t 
         const uint64_t insm = __ballot(inside);
         float Ta = 1.f, d0 = 0.f, d1 = 0.f, d2 = 0.f, d3 = 0.f;
         uint32_t du = 0, dn = 0;
-        if (sgi + 1u < nseg) {  // (1)
+        if (sgi > 0 && sgi + 1u < nseg) {  // (1) (item 0 publishes its blend's end transmittance instead)
             uint64_t lm = insm, sm = 0;
             fwd_seg_pass<false>(point_list, rec, rg.x, p0, p1, sa, sb, sc, pfx, pfy, tx0, sy0, lm, sm, Ta, d0, d1, d2, d3,
                                 du, nullptr, 0u, dn);
@@ -368,6 +370,13 @@ __device__ void fwd_seg_worker(const uint2 *__restrict__ ranges, const uint32_t 
             uint64_t lm = insm, sm = 0;
             fwd_seg_pass<true>(point_list, rec, rg.x, p0, p1, sa, sb, sc, pfx, pfy, tx0, sy0, lm, sm, T, C0, C1, C2, ID,
                                last, ck, seg_len, ncross);
+            if (sgi == 0) {
+                // item 0's row: the transmittance its blend ended with (exactly the sequential one;
+                // 0 for pixels that stopped), published as soon as the blend is done
+                f.agg[(size_t)i * 256 + threadIdx.x] = ((sm >> lane) & 1ull) ? 0.f : T;
+                wg_release();
+                if (threadIdx.x == 0) __hip_atomic_store(f.flags + i, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             float *q = f.part + (size_t)i * (kFwdPartials * 256) + threadIdx.x;
             q[0] = C0;
             q[256] = C1;
@@ -474,7 +483,7 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kerne
     uint32_t *__restrict__ tile_work, const uint32_t *__restrict__ fwd_order, const uint32_t *__restrict__ kdev,
     uint32_t cap, const uint32_t *__restrict__ sort_err, float4 *__restrict__ acc, uint32_t acc_n4,
     uint32_t *__restrict__ bwd_cnt, uint32_t *__restrict__ bwd_cls, int ntiles, int gy, int sb_nsbx, int sb_shift,
-    uint32_t seg_len, uint32_t *__restrict__ bin_base, uint32_t fseg_len, uint32_t *__restrict__ fctl) {
+    uint32_t seg_len, uint32_t *__restrict__ bin_base, uint32_t fseg_len, uint32_t *__restrict__ fctl, uint32_t fseg_min) {
     constexpr int kWaves = kPixPerLane / kSub;
     if (kdev && *kdev > cap) return;  // the point-list capacity is short: the host re-runs at K
     {
@@ -512,7 +521,7 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kerne
         tx = tile % gx;
         ty = tile / gx;
     }
-    if (fseg_splits(ranges[tile].y - ranges[tile].x, fseg_len)) return;  // render_fwd_seg_kernel's tile
+    if (fseg_splits(ranges[tile].y - ranges[tile].x, fseg_min)) return;  // render_fwd_seg_kernel's tile
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int px = tx * kTile + (lane & 15);
     const int sy = ty * kTile + 4 * kSub * w;  // the wave's first pixel row
@@ -746,6 +755,17 @@ __device__ __forceinline__ int bwd_tile_of(uint32_t b, const uint32_t *__restric
     return (int)cls[(size_t)c * T + (b - off)];
 }
 
+// the shortest list the forward split takes: GSR_FSEG_FACTOR segments, or the environment's
+// GSR_FSEG_FACTOR (measurement A/B)
+uint32_t fseg_min_len(uint32_t Lf) {
+    static const uint32_t f = [] {
+        const char *e = getenv("GSR_FSEG_FACTOR");
+        const int v = e ? atoi(e) : 0;
+        return (uint32_t)(v > 0 ? v : GSR_FSEG_FACTOR);
+    }();
+    return f * Lf;
+}
+
 // Launch order for a tile pass, heaviest first (longest-processing-time-first list scheduling):
 // one 1024-thread workgroup buckets the T work estimates into 256 descending classes of
 // 2^shift instances (LDS histogram, scan, scatter).  Order within a class is arbitrary; every
@@ -754,7 +774,7 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t *__rest
                                                           int T, int shift, uint32_t *__restrict__ order, const uint32_t *__restrict__ kdev, uint32_t cap,
                                                           uint32_t *__restrict__ zero_classes, uint32_t *__restrict__ fctl,
                                                           void *bin_base, uint32_t seg_len, uint32_t fseg_len,
-                                                          uint32_t *__restrict__ host_tilelist) {
+                                                          uint32_t fseg_min, uint32_t *__restrict__ host_tilelist) {
     // the forward order's launch also zeroes the backward class counters render_fwd fills
     if (zero_classes && threadIdx.x < kBwdClasses) zero_classes[threadIdx.x] = 0u;
     if (zero_classes && threadIdx.x == 0) zero_classes[kBwdSegCount] = 0u;
@@ -778,7 +798,7 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t *__rest
         const FwdSegLayout f = fseg_layout(bin_base, kdev ? *kdev : cap, seg_len, fseg_len);
         for (int t = threadIdx.x; t < T; t += 1024) {
             const uint32_t len = ranges[t].y - ranges[t].x;
-            if (!fseg_splits(len, fseg_len)) continue;
+            if (!fseg_splits(len, fseg_min)) continue;
             const uint32_t n = (len + fseg_len - 1u) / fseg_len;
             const uint32_t b = atomicAdd(&s_items, n);
             for (uint32_t k = 0; k < n; k++) {
@@ -824,7 +844,8 @@ void launch_tile_order(const uint32_t *work, const uint2 *ranges, int T, int shi
                        uint32_t seg_len, uint32_t fseg_len, uint32_t *host_tilelist) {
     if (T == 0) return;
     hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, s, work, ranges, T, shift, order, kdev, cap, zero_classes,
-                       fctl, bin_base, seg_len, fctl ? fseg_len : 0u, host_tilelist);
+                       fctl, bin_base, seg_len, fctl ? fseg_len : 0u, fctl && fseg_len ? fseg_min_len(fseg_len) : 0u,
+                       host_tilelist);
 }
 
 // the worker pool's size: kFwdWorkers, or GSR_FWD_WORKERS from the environment (measurement A/B)
@@ -858,7 +879,8 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
                        out_color, out_invdepth, is.final_T, is.n_contrib, is.tile_work, is.tile_ids, bs.kdev, bs.cap, \
                        bs.kdev ? dsort_err_word(gs) : nullptr, gs.acc, (uint32_t)(4 * (size_t)gs.nacc),              \
                        GSR_BWD_CLS && need_bwd ? is.bwd_cnt : nullptr, is.bwd_cls, T, cam.gy, sg.nsbx,        \
-                       sb_order ? sg.shift : -1, seg_len, bs.point_list, fseg_len, is.bwd_cnt + kFwdItemsWord)
+                       sb_order ? sg.shift : -1, seg_len, bs.point_list, fseg_len, is.bwd_cnt + kFwdItemsWord,       \
+                       fseg_len ? fseg_min_len(fseg_len) : 0u)
     static_assert(GSR_FWD_SUB == 1 || GSR_FWD_SUB == 2 || GSR_FWD_SUB == 4, "GSR_FWD_SUB: 1, 2 or 4");
     GSR_FWD_LAUNCH(render_fwd_kernel<GSR_FWD_SUB>, kWave * (kPixPerLane / GSR_FWD_SUB));
 #undef GSR_FWD_LAUNCH
