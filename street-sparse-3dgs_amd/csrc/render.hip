@@ -312,6 +312,7 @@ __device__ void fwd_seg_worker(const uint2 *__restrict__ ranges, const uint32_t 
     const FwdSegLayout f = fseg_layout(bin_base, kf, seg_len, fseg_len);
     float *ck = seg_len && bwd_cnt ? reinterpret_cast<float *>(reinterpret_cast<char *>(bin_base) + ck_offset(kf)) : nullptr;
     const uint32_t nitems = fctl[0];
+    if (blockIdx.x >= nitems) return;  // more workers than items: the rest leave without a dequeue
     for (;;) {
         if (threadIdx.x == 0) s_scalar[0] = __hip_atomic_fetch_add(&fctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
@@ -784,41 +785,41 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t *__rest
     if (threadIdx.x < 256) hist[threadIdx.x] = 0u;
     if (threadIdx.x == 0) s_items = s_max = 0u;
     __syncthreads();
-    if (host_tilelist) {
-        // the longest tile list, for the split gate's hint
-        uint32_t mx = 0;
-        for (int t = threadIdx.x; t < T; t += 1024) mx = max(mx, ranges[t].y - ranges[t].x);
-        atomicMax(&s_max, mx);
-        __syncthreads();
-        if (threadIdx.x == 0) __hip_atomic_store(host_tilelist, s_max, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    if (fseg_len) {
-        // forward segments: the work-item queue of the tiles longer than fseg_len (a tile's items
-        // consecutive, segment order), their tickets zeroed
-        const FwdSegLayout f = fseg_layout(bin_base, kdev ? *kdev : cap, seg_len, fseg_len);
-        for (int t = threadIdx.x; t < T; t += 1024) {
-            const uint32_t len = ranges[t].y - ranges[t].x;
-            if (!fseg_splits(len, fseg_min)) continue;
-            const uint32_t n = (len + fseg_len - 1u) / fseg_len;
-            const uint32_t b = atomicAdd(&s_items, n);
-            for (uint32_t k = 0; k < n; k++) {
-                f.items[b + k] = (uint32_t)t + (uint32_t)T * k;
-                f.tickets[b + k] = 0u;
-                f.flags[b + k] = 0u;
-            }
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            fctl[0] = s_items;  // kFwdItemsWord
-            fctl[1] = 0u;       // kFwdNextWord
-        }
-    }
     auto bucket = [&](int t) {
         const uint32_t wk = work ? work[t] : ranges[t].y - ranges[t].x;
         const uint32_t k = wk >> shift;
         return 255u - (k < 255u ? k : 255u);
     };
-    for (int t = threadIdx.x; t < T; t += 1024) atomicAdd(&hist[bucket(t)], 1u);
+    // one pass over the tiles: the work histogram, the longest list (the split gate's hint) and,
+    // with forward segments, the work-item queue of the tiles longer than fseg_min (a tile's items
+    // consecutive, segment order; their tickets and flags zeroed)
+    FwdSegLayout f{};
+    if (fseg_len) f = fseg_layout(bin_base, kdev ? *kdev : cap, seg_len, fseg_len);
+    uint32_t mx = 0;
+    for (int t = threadIdx.x; t < T; t += 1024) {
+        const uint32_t len = ranges[t].y - ranges[t].x;
+        const uint32_t k = (work ? work[t] : len) >> shift;
+        atomicAdd(&hist[255u - (k < 255u ? k : 255u)], 1u);
+        mx = max(mx, len);
+        if (fseg_splits(len, fseg_min)) {
+            const uint32_t n = (len + fseg_len - 1u) / fseg_len;
+            const uint32_t b = atomicAdd(&s_items, n);
+            for (uint32_t q = 0; q < n; q++) {
+                f.items[b + q] = (uint32_t)t + (uint32_t)T * q;
+                f.tickets[b + q] = 0u;
+                f.flags[b + q] = 0u;
+            }
+        }
+    }
+    if (host_tilelist) atomicMax(&s_max, mx);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (host_tilelist) __hip_atomic_store(host_tilelist, s_max, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (fseg_len) {
+            fctl[0] = s_items;  // kFwdItemsWord
+            fctl[1] = 0u;       // kFwdNextWord
+        }
+    }
     __syncthreads();
     if (threadIdx.x < 64) {  // exclusive scan of 256 counts, 4 per lane
         const int l = threadIdx.x;
