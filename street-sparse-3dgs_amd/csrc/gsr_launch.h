@@ -122,6 +122,7 @@ void launch_render_bwd(const Camera &cam, const GeomState &gs, const BinningStat
                        const BwdScratch &sc, hipStream_t s, const ZeroRows *zr = nullptr, uint32_t seg_len = 0);
 bool bwd_segments_supported();
 bool fwd_segments_supported();
+bool fwd_segments_in_kernel();  // the worker pool inside render_fwd's launch (no side stream)
 uint32_t fseg_min_len(uint32_t Lf);  // the shortest list the forward split takes
 
 // backward.hip

@@ -821,7 +821,7 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
             // split tiles); joined before anything reads the frame
             hipStream_t wside = s;
             hipEvent_t wfork = nullptr, wjoin = nullptr;
-            if (fseg_used && !side_stream(s, &wside, &wfork, &wjoin)) wside = s;
+            if (fseg_used && !fwd_segments_in_kernel() && !side_stream(s, &wside, &wfork, &wjoin)) wside = s;
             const bool forked = fseg_used && wside != s;
             if (forked && (hipEventRecord(wfork, s) != hipSuccess || hipStreamWaitEvent(wside, wfork, 0) != hipSuccess))
                 return fail(GSR_ERR_DEVICE, "side stream fork failed");

@@ -476,8 +476,16 @@ __global__ __launch_bounds__(kWave * kPixPerLane) void render_fwd_seg_kernel(
                    s_b[w], s_c[w], s_work, s_scalar);
 }
 
+#ifndef GSR_FWD_SEG_INKERNEL
+#define GSR_FWD_SEG_INKERNEL 0  // 1: the worker pool as render_fwd's first workgroups (no side stream)
+#endif
+#if GSR_FWD_SEG_INKERNEL
+#define GSR_FWD_ATTR __attribute__((amdgpu_waves_per_eu(8)))
+#else
+#define GSR_FWD_ATTR
+#endif
 template <int kSub>
-__global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kernel(
+__global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) GSR_FWD_ATTR void render_fwd_kernel(
     const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list, int W, int H, int gx,
     const GRec *__restrict__ rec, const float *__restrict__ bg, float *__restrict__ out_color,
     float *__restrict__ out_invd, float *__restrict__ final_T, uint32_t *__restrict__ n_contrib,
@@ -505,7 +513,25 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) void render_fwd_kerne
     __shared__ float4 s_c[kWaves][kWave];  // r, g, b, 1 / depth
     __shared__ uint32_t s_work[kWaves];
 
+#if GSR_FWD_SEG_INKERNEL
+    // forward segments: the first kFwdWorkers workgroups are the worker pool (fwd_seg_worker)
+    uint32_t bidx = blockIdx.x;
+    if constexpr (kSub == 1) {
+        if (fseg_len) {
+            if (bidx < (uint32_t)kFwdWorkers) {
+                __shared__ uint32_t s_scalar[3];
+                fwd_seg_worker(ranges, point_list, W, H, gx, rec, bg, out_color, out_invd, final_T, n_contrib,
+                               tile_work, kdev ? *kdev : cap, sort_err, bwd_cnt, bwd_cls, ntiles, seg_len, fseg_len,
+                               bin_base, fctl, s_a[threadIdx.x >> 6], s_b[threadIdx.x >> 6], s_c[threadIdx.x >> 6],
+                               s_work, s_scalar);
+                return;
+            }
+            bidx -= (uint32_t)kFwdWorkers;
+        }
+    }
+#else
     const uint32_t bidx = blockIdx.x;
+#endif
 
     int tile, tx, ty;
     if (sb_shift >= 0) {
@@ -866,9 +892,9 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
     if (T == 0) return;
     const SBGrid &sg = gs.sb;
     if (sb_order || GSR_FWD_SUB != 1) fseg_len = 0;
-    const int grid = sb_order ? sg.nsb << (2 * sg.shift) : T;
+    const int grid = (sb_order ? sg.nsb << (2 * sg.shift) : T) + (GSR_FWD_SEG_INKERNEL && fseg_len ? kFwdWorkers : 0);
     uint32_t *const bcnt = GSR_BWD_CLS && need_bwd ? is.bwd_cnt : nullptr;
-    if (fseg_len)
+    if (fseg_len && !GSR_FWD_SEG_INKERNEL)
         hipLaunchKernelGGL(render_fwd_seg_kernel, dim3(fwd_workers()), dim3(kWave * kPixPerLane), 0,
                            worker_stream ? worker_stream : s, is.ranges,
                            bs.point_list, cam.W, cam.H, cam.gx, gs.rec, bg, out_color, out_invdepth, is.final_T,
@@ -1335,6 +1361,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
 }
 
 bool fwd_segments_supported() { return GSR_FWD_SUB == 1 && !GSR_FWD_SB_ORDER; }
+bool fwd_segments_in_kernel() { return GSR_FWD_SEG_INKERNEL != 0; }
 
 bool bwd_segments_supported() { return GSR_BWD_CLS && GSR_FWD_SUB == 1 && GSR_BWD_BG_IN_S && !GSR_TILE_REVERSE; }
 
