@@ -199,9 +199,8 @@ int gsr_set_binning(int mode);
 int gsr_forward_stats(int64_t *out, int n);
 
 /* Forget the calling thread's point-list capacity hint (the largest K of its last 256 frames per
- * device), its split-gate history and its backward segment-slot history: the next frame reads K
- * before binning, as the first one does, the gated splits wait for a long-list frame again, and the
- * next backward launches a slot per possible segment.  For a caller that switches to a much
+ * device) and its split-gate history: the next frame reads K before binning, as the first one does,
+ * and the gated splits wait for a long-list frame again.  For a caller that switches to a much
  * smaller workload (the buffers follow the hint) and for tests.  ABI 3. */
 int gsr_reset_capacity_hint(void);
 

@@ -119,8 +119,7 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
 // (gsr_set_bwd_segment; the backward must get the value its forward was made with)
 void launch_render_bwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                        const int *radii, const float *bg, const float *dL_dpix, const float *dL_dinvdepth,
-                       const BwdScratch &sc, hipStream_t s, const ZeroRows *zr = nullptr, uint32_t seg_len = 0,
-                       uint32_t seg_slots = 0, uint32_t *host_nsg = nullptr);
+                       const BwdScratch &sc, hipStream_t s, const ZeroRows *zr = nullptr, uint32_t seg_len = 0);
 bool bwd_segments_supported();
 bool fwd_segments_supported();
 bool fwd_segments_in_kernel();  // the worker pool inside render_fwd's launch (no side stream)

@@ -444,39 +444,6 @@ void note_forward_seg(const void *image, uint32_t L) {
     if (g_seg_of.size() >= kUnclearedMax) g_seg_of.clear();
     g_seg_of[image] = L;
 }
-// render_bwd's segment slots (workgroups that take the full segments): the most segments one of the
-// calling thread's last kSlotHist backwards on this device had (render_bwd reports its count in
-// pinned memory, read at the next backward) + 25% + 256, capped by K / L -- any count is correct (a
-// slot takes every seg_slots-th segment); the bound K / L alone launched 27k idle workgroups on the
-// bench frame.  No history yet: K / L.
-constexpr int kSlotHist = 256;
-thread_local uint32_t *g_bpinned = nullptr, *g_bpinned_dev = nullptr;
-thread_local uint32_t g_slot_hist[64][kSlotHist] = {};
-thread_local int g_slot_head[64] = {}, g_slot_n[64] = {};
-uint32_t bwd_seg_slots(int64_t K, uint32_t L) {
-    const uint32_t bound = (uint32_t)std::min<int64_t>(K / L, INT32_MAX);
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return bound;
-    if (!g_bpinned) {
-        if (hipHostMalloc(reinterpret_cast<void **>(&g_bpinned), 64, hipHostMallocCoherent) != hipSuccess ||
-            hipHostGetDevicePointer(reinterpret_cast<void **>(&g_bpinned_dev), g_bpinned, 0) != hipSuccess) {
-            g_bpinned = g_bpinned_dev = nullptr;
-            return bound;
-        }
-        *g_bpinned = kKPending;
-    }
-    const uint32_t last = __atomic_load_n(g_bpinned, __ATOMIC_RELAXED);
-    if (last != kKPending) {
-        g_slot_hist[dev][g_slot_head[dev]] = last;
-        g_slot_head[dev] = (g_slot_head[dev] + 1) % kSlotHist;
-        g_slot_n[dev] = std::min(g_slot_n[dev] + 1, kSlotHist);
-    }
-    if (g_slot_n[dev] == 0) return bound;
-    uint32_t mx = 0;
-    for (int i = 0; i < g_slot_n[dev]; i++) mx = std::max(mx, g_slot_hist[dev][i]);
-    return std::min<uint32_t>(bound, mx + mx / 4 + 256);
-}
-
 uint32_t forward_seg(const void *image) {
     std::lock_guard<std::mutex> lk(g_seg_mu);
     if (g_seg_of.empty()) return 0;
@@ -1007,11 +974,10 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
         StageTimer st(6, s);
         // the dense zero gradient rows go out beside render_bwd's replay (bwd_zero_rows)
         const uint32_t seg = forward_seg(image_buffer);
-        const uint32_t slots = seg ? bwd_seg_slots(R_inst, seg) : 0u;
-        zeroed = R_inst > 0 && bwd_zero_rows(in, out, sc, gs.live_stamp, T + (int)slots, &zr);
+        zeroed = R_inst > 0 && bwd_zero_rows(in, out, sc, gs.live_stamp, (int)bwd_grid(T, R_inst, seg), &zr);
         if (R_inst > 0)
             launch_render_bwd(cam, gs, bs, is, radii, background, dL_dpix, dL_dinvdepth, sc, s, zeroed ? &zr : nullptr,
-                              seg, slots, g_bpinned_dev);
+                              seg);
     }
     if ((rc = check("render backward", debug, s))) return rc;
     {
@@ -1092,8 +1058,6 @@ int gsr_segment_layout_check(int64_t K, int L, int Lf, int64_t *need, int64_t *h
 
 int gsr_reset_capacity_hint(void) {
     if (g_pinned) g_pinned[kHostTileList] = g_pinned[kHostSBList] = 0u;
-    if (g_bpinned) *g_bpinned = kKPending;
-    for (int d = 0; d < 64; d++) g_slot_n[d] = g_slot_head[d] = 0;
     for (int d = 0; d < kMaxDevicesK; d++) {
         g_long_tile_at[d] = g_long_sb_at[d] = g_frame_no[d] - 2 * kSplitMemory;
         g_khint[d] = 0;

@@ -992,8 +992,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
     const uint32_t *__restrict__ n_contrib, const float *__restrict__ dL_dpix, const float *__restrict__ dL_dinvd,
     const uint32_t *__restrict__ tile_order, const uint32_t *__restrict__ goff, uint64_t *__restrict__ boundary,
     float4 *__restrict__ out, ZeroRows zr, const uint32_t *__restrict__ bwd_cnt, const uint32_t *__restrict__ bwd_cls,
-    uint32_t ntiles, uint32_t seg_len, const float *__restrict__ ck, const uint32_t *__restrict__ seg_items,
-    uint32_t seg_slots, uint32_t *__restrict__ host_nsg) {
+    uint32_t ntiles, uint32_t seg_len, const float *__restrict__ ck, const uint32_t *__restrict__ seg_items) {
     // 9 KiB of LDS per wave: each compacted instance's mean and conic (scaled for gauss_p2 by the
     // lane that stages it, once per instance instead of by the whole wave), opacity, list position
     // << 4 | sub-block mask, Gaussian id (atomic mode) or record index, colour, and the unscaled
@@ -1011,10 +1010,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
     // with ~2.7 tiles per wave slot, index order leaves a tail of a few heavy tiles.
     // With segments (seg_len != 0) the full segments render_fwd listed run first, then the class
     // lists; workgroups past both only zero their share of the gradient rows.
-    // The first seg_slots workgroups take the full segments (slot b: segments b, b + seg_slots, ...;
-    // the host sizes seg_slots from the counts earlier backwards reported, any size is correct), the
-    // rest the class lists; every workgroup then clears its share of the zero gradient rows.
-    const auto replay = [&](const int item) {
+    int item;
+    if (GSR_TILE_REVERSE) item = (int)blockIdx.x;
+    else if (GSR_BWD_CLS) {
+        const uint32_t nsg = seg_len ? bwd_cnt[kBwdSegCount] : 0u;
+        item = blockIdx.x < nsg ? (int)seg_items[blockIdx.x] : bwd_tile_of(blockIdx.x - nsg, bwd_cnt, bwd_cls, (int)ntiles);
+    } else item = (int)tile_order[blockIdx.x];
+    if (item < 0) {
+        bwd_zero_slice(zr);
+        return;
+    }
     const int tile = (int)((uint32_t)item % ntiles), seg = (int)((uint32_t)item / ntiles);
     const int tx = tile % gx, ty = tile / gx;
     const int lane = threadIdx.x;
@@ -1344,6 +1349,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
         }
         __syncthreads();
     }
+    bwd_zero_slice(zr);
     if (GSR_BLEND_STATS) {
         bst.flush(kBwdPairs);
         if (lane == 0) {
@@ -1352,20 +1358,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
             atomicAdd(&g_blend_stats[kBwdTiles], 1ull);
         }
     }
-    };
-    if (GSR_TILE_REVERSE) replay((int)blockIdx.x);
-    else if (GSR_BWD_CLS) {
-        const uint32_t nsg = seg_len ? bwd_cnt[kBwdSegCount] : 0u;
-        if (host_nsg && blockIdx.x == 0 && threadIdx.x == 0)  // the host's hint for the next backward's seg_slots
-            __hip_atomic_store(host_nsg, nsg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (blockIdx.x < seg_slots) {
-            for (uint32_t j = blockIdx.x; j < nsg; j += seg_slots) replay((int)seg_items[j]);
-        } else {
-            const int it = bwd_tile_of(blockIdx.x - seg_slots, bwd_cnt, bwd_cls, (int)ntiles);
-            if (it >= 0) replay(it);
-        }
-    } else replay((int)tile_order[blockIdx.x]);
-    bwd_zero_slice(zr);
 }
 
 bool fwd_segments_supported() { return GSR_FWD_SUB == 1 && !GSR_FWD_SB_ORDER; }
@@ -1375,8 +1367,7 @@ bool bwd_segments_supported() { return GSR_BWD_CLS && GSR_FWD_SUB == 1 && GSR_BW
 
 void launch_render_bwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                        const int *radii, const float *bg, const float *dL_dpix, const float *dL_dinvdepth,
-                       const BwdScratch &sc, hipStream_t s, const ZeroRows *zr, uint32_t seg_len, uint32_t seg_slots,
-                       uint32_t *host_nsg) {
+                       const BwdScratch &sc, hipStream_t s, const ZeroRows *zr, uint32_t seg_len) {
     (void)radii;
     const int T = cam.gx * cam.gy;
     if (T == 0) return;
@@ -1387,13 +1378,12 @@ void launch_render_bwd(const Camera &cam, const GeomState &gs, const BinningStat
         ck = reinterpret_cast<const float *>(reinterpret_cast<const char *>(bs.point_list) + ck_offset(bs.cap));
         items = reinterpret_cast<const uint32_t *>(ck + ck_slots(bs.cap, seg_len) * (kCkFloats * 256));
     }
-    if (!seg_len) seg_slots = 0;
-    const unsigned grid = (unsigned)T + seg_slots;
+    const unsigned grid = (unsigned)bwd_grid(T, bs.cap, seg_len);
 #define GSR_BWD_LAUNCH(D, A)                                                                                       \
     hipLaunchKernelGGL((render_bwd_kernel<D, A>), dim3(grid), dim3(kWave), 0, s, is.ranges, bs.point_list, cam.W,   \
                        cam.H, cam.gx, gs.rec, bg, is.final_T, is.n_contrib, dL_dpix, dL_dinvdepth, is.tile_order,    \
                        gs.offsets, is.boundary, A ? sc.acc : sc.rec, z, is.bwd_cnt, is.bwd_cls, (uint32_t)T, seg_len, \
-                       ck, items, seg_slots, host_nsg)
+                       ck, items)
     if (dL_dinvdepth) {
         if (sc.atomic) GSR_BWD_LAUNCH(true, true);
         else GSR_BWD_LAUNCH(true, false);

@@ -315,25 +315,3 @@ def test_split_gate_arms_after_a_long_list_frame():
     _C.reset_capacity_hint()
     st3, _ = frame(long_)
     assert st3["tb_split_items"] == 0
-
-
-def test_segment_slots_fewer_than_segments():
-    """render_bwd's segment slots come from the segment counts of earlier backwards (+25%): after a
-    frame with none, a frame with thousands of segments runs them through 256 slots, each taking
-    every 256th segment -- the gradients still meet the oracle's bars."""
-    from diff_gaussian_rasterization import _C
-    _C.reset_capacity_hint()
-    light = dict(name="light", P=2000, W=96, H=64, deg=1, seed=5, log_scale=-3.0, opac=(0.3, 0.9))
-    s = seg_scene(light)
-    dcol, dinv = upstream_grads(light)
-    with bwd_segment(512):
-        run_hip(s, light, dcol, dinv)
-        c = FWD_CASES[1]
-        s = seg_scene(c)
-        dcol, dinv = upstream_grads(c)
-        st, g = run_oracle(s, c, dcol, dinv)
-        h = run_hip(s, c, dcol, dinv)
-    work = max_tile_work(h, c)
-    T = ((c["W"] + 15) // 16) * ((c["H"] + 15) // 16)
-    assert T * (work // 512) > 1000, work  # far more segments than the 256 slots
-    fwd_compare(c, st, g, h)
