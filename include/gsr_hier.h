@@ -53,6 +53,11 @@ int gsr_interpolate_cut_backward(int64_t N, int M, int64_t R, int64_t S, const i
 #define GSR_OPACITY_IDENTITY 0
 #define GSR_OPACITY_SIGMOID 1
 #define GSR_OPACITY_ABS 2
+/* OR'ed into opacity_act of gsr_interpolate_cut_backward_act: render_indices name every row at most
+ * once and none of them is also a parent row (a cut: expand_to_size's output), so the children's
+ * gradient rows are written, not accumulated with atomics (the gradients must be zero on entry, as
+ * for the accumulating form). */
+#define GSR_CUT_UNIQUE_CHILDREN 0x100
 int gsr_interpolate_cut_forward_act(int64_t N, int M, int64_t R, int64_t S, const int *render_indices,
                                     const int *parent_indices, const float *interpolation_weights,
                                     const float *means3D, const float *scaling_raw, const float *rotation_raw,

@@ -145,48 +145,60 @@ __global__ __launch_bounds__(256) void cut_bwd_kernel(int64_t N, int M, int64_t 
                                                       const float *__restrict__ gsh, float *dm, float *ds, float *drot,
                                                       float *dop, float *dsh, bool vec, int act,
                                                       const float *__restrict__ s_raw,
-                                                      const float *__restrict__ o_raw) {
+                                                      const float *__restrict__ o_raw, bool uniq) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= R + S) return;
     const CutRow q = cut_row(r, N, R, S, ri, pi, w);
     const float t = q.t, u = 1.f - q.t;
     // d(act(x))/dx times the upstream, per input row (act == 0: the identity)
     const auto dsc = [&](int64_t i, float g) { return act ? g * act_scale(s_raw[i]) : g; };
-    const auto add_rot = [&](int64_t row, float4 g) {
+    const auto add_rot = [&](int64_t row, float4 g, bool store) {
         if (act) g = normalize_grad(reinterpret_cast<const float4 *>(rots)[row], g);
+        if (store) {
+            drot[4 * row + 0] = g.x;
+            drot[4 * row + 1] = g.y;
+            drot[4 * row + 2] = g.z;
+            drot[4 * row + 3] = g.w;
+            return;
+        }
         atomicAdd(&drot[4 * row + 0], g.x);
         atomicAdd(&drot[4 * row + 1], g.y);
         atomicAdd(&drot[4 * row + 2], g.z);
         atomicAdd(&drot[4 * row + 3], g.w);
     };
+    // a cut's child rows are unique (uniq): written; parent rows are shared by siblings: accumulated
+    const auto put = [&](float *a, float v) {
+        if (uniq) *a = v;
+        else atomicAdd(a, v);
+    };
     const float4 gr = make_float4(grot[4 * r + 0], grot[4 * r + 1], grot[4 * r + 2], grot[4 * r + 3]);
     if (q.copy) {
-        for (int k = 0; k < 3; k++) atomicAdd(&dm[3 * q.c + k], gm[3 * r + k]);
-        for (int k = 0; k < 3; k++) atomicAdd(&ds[3 * q.c + k], dsc(3 * q.c + k, gs[3 * r + k]));
-        add_rot(q.c, gr);
-        atomicAdd(&dop[q.c], act_opac_grad(act, act ? o_raw[q.c] : 0.f, gop[r]));
+        for (int k = 0; k < 3; k++) put(&dm[3 * q.c + k], gm[3 * r + k]);
+        for (int k = 0; k < 3; k++) put(&ds[3 * q.c + k], dsc(3 * q.c + k, gs[3 * r + k]));
+        add_rot(q.c, gr, uniq);
+        put(&dop[q.c], act_opac_grad(act, act ? o_raw[q.c] : 0.f, gop[r]));
         if (!vec)
-            for (int k = 0; k < 3 * M; k++) atomicAdd(&dsh[(size_t)q.c * 3 * M + k], gsh[(size_t)r * 3 * M + k]);
+            for (int k = 0; k < 3 * M; k++) put(&dsh[(size_t)q.c * 3 * M + k], gsh[(size_t)r * 3 * M + k]);
         return;
     }
     for (int k = 0; k < 3; k++) {
-        atomicAdd(&dm[3 * q.c + k], t * gm[3 * r + k]);
+        put(&dm[3 * q.c + k], t * gm[3 * r + k]);
         atomicAdd(&dm[3 * q.p + k], u * gm[3 * r + k]);
-        atomicAdd(&ds[3 * q.c + k], dsc(3 * q.c + k, t * gs[3 * r + k]));
+        put(&ds[3 * q.c + k], dsc(3 * q.c + k, t * gs[3 * r + k]));
         atomicAdd(&ds[3 * q.p + k], dsc(3 * q.p + k, u * gs[3 * r + k]));
     }
     const float4 qc = ld_rot(rots, q.c, act);
     const float4 qp = ld_rot(rots, q.p, act);
     const float dot = qc.x * qp.x + qc.y * qp.y + qc.z * qp.z + qc.w * qp.w;
     const float sgn = dot < 0.f ? -1.f : 1.f;
-    add_rot(q.c, make_float4(t * gr.x, t * gr.y, t * gr.z, t * gr.w));
-    add_rot(q.p, make_float4(sgn * u * gr.x, sgn * u * gr.y, sgn * u * gr.z, sgn * u * gr.w));
-    atomicAdd(&dop[q.c], act_opac_grad(act, act ? o_raw[q.c] : 0.f, t * gop[r]));
+    add_rot(q.c, make_float4(t * gr.x, t * gr.y, t * gr.z, t * gr.w), uniq);
+    add_rot(q.p, make_float4(sgn * u * gr.x, sgn * u * gr.y, sgn * u * gr.z, sgn * u * gr.w), false);
+    put(&dop[q.c], act_opac_grad(act, act ? o_raw[q.c] : 0.f, t * gop[r]));
     atomicAdd(&dop[q.p], act_opac_grad(act, act ? o_raw[q.p] : 0.f, u * gop[r]));
     if (vec) return;
     for (int k = 0; k < 3 * M; k++) {
         const float g = gsh[(size_t)r * 3 * M + k];
-        atomicAdd(&dsh[(size_t)q.c * 3 * M + k], t * g);
+        put(&dsh[(size_t)q.c * 3 * M + k], t * g);
         atomicAdd(&dsh[(size_t)q.p * 3 * M + k], u * g);
     }
 }
@@ -195,26 +207,25 @@ __global__ __launch_bounds__(256) void cut_bwd_kernel(int64_t N, int M, int64_t 
 // wave instruction, so the atomics of one row hit one or two cache lines together.
 __global__ __launch_bounds__(256) void cut_bwd_sh_kernel(int64_t N, int64_t R, int64_t S, const int *ri, const int *pi,
                                                          const float *w, const float *__restrict__ gsh,
-                                                         float *dsh) {
+                                                         float *dsh, bool uniq) {
     const int64_t rr = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
     const int col = threadIdx.x & 15;
     if (rr >= R + S || col >= 12) return;
     const CutRow q = cut_row(rr, N, R, S, ri, pi, w);
     const float4 g = reinterpret_cast<const float4 *>(gsh)[12 * rr + col];
     float *dc = dsh + 48 * q.c + 4 * col;
-    if (q.copy) {
-        atomicAdd(dc + 0, g.x);
-        atomicAdd(dc + 1, g.y);
-        atomicAdd(dc + 2, g.z);
-        atomicAdd(dc + 3, g.w);
-        return;
+    const float t = q.copy ? 1.f : q.t, u = 1.f - q.t;
+    const float4 gc = make_float4(t * g.x, t * g.y, t * g.z, t * g.w);
+    if (uniq) {
+        reinterpret_cast<float4 *>(dc)[0] = gc;  // a cut's child row: one 16-B store
+    } else {
+        atomicAdd(dc + 0, gc.x);
+        atomicAdd(dc + 1, gc.y);
+        atomicAdd(dc + 2, gc.z);
+        atomicAdd(dc + 3, gc.w);
     }
-    const float t = q.t, u = 1.f - q.t;
+    if (q.copy) return;
     float *dp = dsh + 48 * q.p + 4 * col;
-    atomicAdd(dc + 0, t * g.x);
-    atomicAdd(dc + 1, t * g.y);
-    atomicAdd(dc + 2, t * g.z);
-    atomicAdd(dc + 3, t * g.w);
     atomicAdd(dp + 0, u * g.x);
     atomicAdd(dp + 1, u * g.y);
     atomicAdd(dp + 2, u * g.z);
@@ -265,6 +276,8 @@ int cut_backward(int64_t N, int M, int64_t R, int64_t S, const int *render_indic
                  int act, const float *dL_dout_means3D, const float *dL_dout_scales, const float *dL_dout_rotations,
                  const float *dL_dout_opacities, const float *dL_dout_shs, float *dL_dmeans3D, float *dL_dscales,
                  float *dL_drotations, float *dL_dopacities, float *dL_dshs, void *stream, const char *who) {
+    const bool uniq = (act & GSR_CUT_UNIQUE_CHILDREN) != 0;
+    act &= ~GSR_CUT_UNIQUE_CHILDREN;
     if (N < 0 || R < 0 || S < 0 || S > N || M <= 0 || M > 16 || act < 0 || act > GSR_OPACITY_ABS) {
         set_last_error(std::string(who) + ": bad sizes or activation (need 0 <= S <= N, 1 <= M <= 16)");
         return GSR_ERR_INVALID_ARGUMENT;
@@ -281,16 +294,17 @@ int cut_backward(int64_t N, int M, int64_t R, int64_t S, const int *render_indic
         return GSR_ERR_INVALID_ARGUMENT;
     }
     const int64_t rows = R + S;
-    const bool vec = M == 16 && reinterpret_cast<uintptr_t>(dL_dout_shs) % 16 == 0;
+    const bool vec = M == 16 && reinterpret_cast<uintptr_t>(dL_dout_shs) % 16 == 0 &&
+                     reinterpret_cast<uintptr_t>(dL_dshs) % 16 == 0;
     hipLaunchKernelGGL(cut_bwd_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0,
                        static_cast<hipStream_t>(stream), N, M, R, S, render_indices, parent_indices,
                        interpolation_weights, rotations, dL_dout_means3D, dL_dout_scales, dL_dout_rotations,
                        dL_dout_opacities, dL_dout_shs, dL_dmeans3D, dL_dscales, dL_drotations, dL_dopacities,
-                       dL_dshs, vec, act, s_raw, o_raw);
+                       dL_dshs, vec, act, s_raw, o_raw, uniq);
     if (vec)
         hipLaunchKernelGGL(cut_bwd_sh_kernel, dim3((unsigned)((16 * rows + 255) / 256)), dim3(256), 0,
                            static_cast<hipStream_t>(stream), N, R, S, render_indices, parent_indices,
-                           interpolation_weights, dL_dout_shs, dL_dshs);
+                           interpolation_weights, dL_dout_shs, dL_dshs, uniq);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_last_error(std::string(who) + ": " + hipGetErrorString(e));

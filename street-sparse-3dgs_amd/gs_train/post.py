@@ -33,6 +33,7 @@ from .optim import Adam
 
 GSR_OPACITY_SIGMOID = 1
 GSR_OPACITY_ABS = 2
+GSR_CUT_UNIQUE_CHILDREN = 0x100  # include/gsr_hier.h
 
 # scripts/full_train.py:155-158 (the post-optimisation's command line) over OptimizationParams
 POST_LR = dict(LR, iterations=15_000, feature_lr=0.0005, opacity_lr=0.01, scaling_lr=0.001)
@@ -41,7 +42,7 @@ LIMMAX, LIMMIN = 0.1, 0.005  # train_post.py:66-67
 
 class _CutAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, xyz, s_raw, q_raw, o_raw, shs, ri, pi, w, S, opacity_act):
+    def forward(ctx, xyz, s_raw, q_raw, o_raw, shs, ri, pi, w, S, opacity_act, unique_children=False):
         require_gpu(xyz, s_raw, q_raw, o_raw, shs, ri, pi, w)
         N, M, R = xyz.shape[0], shs.shape[1], ri.shape[0]
         ins = [t.detach().float().contiguous() for t in (xyz, s_raw, q_raw, o_raw, shs)]
@@ -54,7 +55,8 @@ class _CutAct(torch.autograd.Function):
                                                     int(opacity_act), *[ptr(t) for t in outs], stream(xyz.device)),
               "gsr_interpolate_cut_forward_act")
         ctx.save_for_backward(ri, pi, w, ins[1], ins[2], ins[3])
-        ctx.meta = (N, M, R, int(S), int(opacity_act), [tuple(t.shape) for t in ins])
+        ctx.meta = (N, M, R, int(S), int(opacity_act) | (GSR_CUT_UNIQUE_CHILDREN if unique_children else 0),
+                    [tuple(t.shape) for t in ins])
         return tuple(outs)
 
     @staticmethod
@@ -69,16 +71,19 @@ class _CutAct(torch.autograd.Function):
         check(lib().gsr_interpolate_cut_backward_act(N, M, R, S, ptr(ri), ptr(pi), ptr(w), ptr(s_raw), ptr(q_raw),
                                                      ptr(o_raw), act, *[ptr(t) for t in g], *[ptr(t) for t in grads],
                                                      stream(dev)), "gsr_interpolate_cut_backward_act")
-        return (*grads, None, None, None, None, None)
+        return (*grads, None, None, None, None, None, None)
 
 
 def interpolate_cut_act(xyz, scaling_raw, rotation_raw, opacity_raw, features, render_indices, parent_indices,
-                        interpolation_weights, skybox_points=0, opacity_act=GSR_OPACITY_ABS):
+                        interpolation_weights, skybox_points=0, opacity_act=GSR_OPACITY_ABS, unique_children=False):
     """render_post's blend (gaussian_renderer/__init__.py:200-243) of the pre-activation parameters
     (include/gsr_hier.h gsr_interpolate_cut_forward_act): returns the R + S rows (means, scales,
-    rotations, opacities, SH) the rasterizer renders, differentiable w.r.t. the five raw inputs."""
+    rotations, opacities, SH) the rasterizer renders, differentiable w.r.t. the five raw inputs.
+    unique_children: render_indices is a cut (no row twice, none a parent row, as expand_to_size
+    returns it), so the backward writes the children's gradient rows instead of accumulating them
+    (GSR_CUT_UNIQUE_CHILDREN)."""
     return _CutAct.apply(xyz, scaling_raw, rotation_raw, opacity_raw, features, render_indices, parent_indices,
-                         interpolation_weights, int(skybox_points), int(opacity_act))
+                         interpolation_weights, int(skybox_points), int(opacity_act), bool(unique_children))
 
 
 def zero_grad_rows(tensors, tail, rows=None):
@@ -196,7 +201,8 @@ class PostTrainStep:
         from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
         c, m = self.cams[k], self.m
         means, scales, rots, opac, shs = interpolate_cut_act(m._xyz, m._scaling, m._rotation, m._opacity, m._features,
-                                                            self.ri[:n], self.pi, self.w, m.skybox_points)
+                                                            self.ri[:n], self.pi, self.w, m.skybox_points,
+                                                            unique_children=True)
         rs = GaussianRasterizationSettings(
             image_height=self.H, image_width=self.W, tanfovx=c["tx"], tanfovy=c["ty"], bg=self.bg, scale_modifier=1.0,
             viewmatrix=c["view"], projmatrix=c["proj"], sh_degree=m.active_sh_degree, campos=c["campos"],

@@ -117,3 +117,39 @@ def test_post_step_matches_reference_formulation(steps):
     for x, x0 in zip(got, init):
         assert torch.equal(x.detach()[-S:], x0[-S:])
         assert torch.equal(x.detach()[m.anchors], x0[m.anchors])
+
+
+@pytest.mark.parametrize("limit", [0.004, 0.02, 0.08])
+def test_cut_unique_children_writes_match_accumulation(limit):
+    """A real cut (expand_to_size over a synthetic hierarchy): the backward that writes the child
+    rows (GSR_CUT_UNIQUE_CHILDREN) equals the accumulating one -- child rows exactly (an atomic add
+    into a zero row is the value), parent rows to fp32 summation order -- and the reference
+    formulation (float64 autograd of the getters + render_post's gather)."""
+    from gs_train.post import interpolate_cut_act, synthetic_post_problem
+    post = synthetic_post_problem(60_000, 320, 240, n_views=2, skybox=2000, n_anchors=100, seed=5)
+    m = post.m
+    n = post.cut(0, limit)
+    ri, pi, w = post.ri[:n], post.pi, post.w
+    assert n > 1000 and torch.unique(ri).numel() == n
+    S = m.skybox_points
+    raw = [m._xyz, m._scaling, m._rotation, m._opacity, m._features]
+    g = torch.Generator(device=DEV).manual_seed(3)
+    grads = {}
+    for uniq in (False, True):
+        xs = [t.detach().clone().requires_grad_(True) for t in raw]
+        out = interpolate_cut_act(*xs, ri, pi, w, S, unique_children=uniq)
+        if not grads:
+            ups = [torch.randn(o.shape, generator=g, device=DEV) for o in out]
+        sum((o * u).sum() for o, u in zip(out, ups)).backward()
+        grads[uniq] = [x.grad.detach() for x in xs]
+    child = ri.long()
+    for a, b in zip(grads[True], grads[False]):
+        assert torch.equal(a[child], b[child])
+        err = (a - b).abs().max().item()
+        assert err <= 1e-5 * max(1.0, b.abs().max().item()), err
+    xd = [t.detach().double().clone().requires_grad_(True) for t in raw]
+    ref = _reference_blend(xd, ri, pi, w, S, 2)
+    sum((o * u.double()).sum() for o, u in zip(ref, ups)).backward()
+    for a, b in zip(grads[True], xd):
+        err = (a.double() - b.grad).abs().max().item()
+        assert err <= 2e-5 * max(1.0, b.grad.abs().max().item()), err
