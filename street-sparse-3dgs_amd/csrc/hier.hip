@@ -381,8 +381,10 @@ int gsr_interpolate_cut_backward_act(int64_t N, int M, int64_t R, int64_t S, con
                                      const float *dL_dout_rotations, const float *dL_dout_opacities,
                                      const float *dL_dout_shs, float *dL_dmeans3D, float *dL_dscaling_raw,
                                      float *dL_drotation_raw, float *dL_dopacity_raw, float *dL_dshs, void *stream) {
-    if (opacity_act != GSR_OPACITY_SIGMOID && opacity_act != GSR_OPACITY_ABS) {
-        set_last_error("gsr_interpolate_cut_backward_act: opacity_act must be GSR_OPACITY_SIGMOID or GSR_OPACITY_ABS");
+    const int oa = opacity_act & ~GSR_CUT_UNIQUE_CHILDREN;
+    if (oa != GSR_OPACITY_SIGMOID && oa != GSR_OPACITY_ABS) {
+        set_last_error("gsr_interpolate_cut_backward_act: opacity_act must be GSR_OPACITY_SIGMOID or GSR_OPACITY_ABS "
+                       "(optionally | GSR_CUT_UNIQUE_CHILDREN)");
         return GSR_ERR_INVALID_ARGUMENT;
     }
     return cut_backward(N, M, R, S, render_indices, parent_indices, interpolation_weights, scaling_raw, rotation_raw,
