@@ -138,6 +138,7 @@ __global__ __launch_bounds__(256) void cut_fwd_kernel(int64_t N, int M, int64_t 
     }
 }
 
+constexpr int kScRun = 8;  // cut_bwd_kernel (uniq): consecutive rows per thread
 __global__ __launch_bounds__(256) void cut_bwd_kernel(int64_t N, int M, int64_t R, int64_t S, const int *ri,
                                                       const int *pi, const float *w, const float *__restrict__ rots,
                                                       const float *__restrict__ gm, const float *__restrict__ gs,
@@ -146,12 +147,76 @@ __global__ __launch_bounds__(256) void cut_bwd_kernel(int64_t N, int M, int64_t 
                                                       float *dop, float *dsh, bool vec, int act,
                                                       const float *__restrict__ s_raw,
                                                       const float *__restrict__ o_raw, bool uniq) {
+    // d(act(x))/dx times the upstream, per input row (act == 0: the identity)
+    const auto dsc = [&](int64_t i, float g) { return act ? g * act_scale(s_raw[i]) : g; };
+    if (uniq) {
+        // a cut: thread per kScRun consecutive rows; child rows written, parent contributions of
+        // consecutive rows with the same parent (siblings) summed before one set of atomics (the
+        // activation derivatives are linear in the upstream: applied once per run)
+        const int64_t r0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * kScRun, r1 = min(R + S, r0 + kScRun);
+        int64_t cur = -1;
+        float am[3] = {0.f, 0.f, 0.f}, as[3] = {0.f, 0.f, 0.f}, ao = 0.f;
+        float4 ar = make_float4(0.f, 0.f, 0.f, 0.f);
+        const auto flush = [&]() {
+            if (cur < 0) return;
+            for (int k = 0; k < 3; k++) {
+                atomicAdd(&dm[3 * cur + k], am[k]);
+                atomicAdd(&ds[3 * cur + k], dsc(3 * cur + k, as[k]));
+            }
+            float4 g = ar;
+            if (act) g = normalize_grad(reinterpret_cast<const float4 *>(rots)[cur], g);
+            atomicAdd(&drot[4 * cur + 0], g.x);
+            atomicAdd(&drot[4 * cur + 1], g.y);
+            atomicAdd(&drot[4 * cur + 2], g.z);
+            atomicAdd(&drot[4 * cur + 3], g.w);
+            atomicAdd(&dop[cur], act_opac_grad(act, act ? o_raw[cur] : 0.f, ao));
+        };
+        for (int64_t r = r0; r < r1; r++) {
+            const CutRow q = cut_row(r, N, R, S, ri, pi, w);
+            const float t = q.t, u = 1.f - q.t;
+            const float4 gr = make_float4(grot[4 * r + 0], grot[4 * r + 1], grot[4 * r + 2], grot[4 * r + 3]);
+            const float4 qc = ld_rot(rots, q.c, act);
+            for (int k = 0; k < 3; k++) {
+                dm[3 * q.c + k] = t * gm[3 * r + k];
+                ds[3 * q.c + k] = dsc(3 * q.c + k, t * gs[3 * r + k]);
+            }
+            {
+                float4 g = make_float4(t * gr.x, t * gr.y, t * gr.z, t * gr.w);
+                if (act) g = normalize_grad(reinterpret_cast<const float4 *>(rots)[q.c], g);
+                drot[4 * q.c + 0] = g.x;
+                drot[4 * q.c + 1] = g.y;
+                drot[4 * q.c + 2] = g.z;
+                drot[4 * q.c + 3] = g.w;
+            }
+            dop[q.c] = act_opac_grad(act, act ? o_raw[q.c] : 0.f, t * gop[r]);
+            if (!vec)
+                for (int k = 0; k < 3 * M; k++) dsh[(size_t)q.c * 3 * M + k] = t * gsh[(size_t)r * 3 * M + k];
+            if (q.copy) continue;
+            if (q.p != cur) {
+                flush();
+                cur = q.p;
+                am[0] = am[1] = am[2] = as[0] = as[1] = as[2] = ao = 0.f;
+                ar = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+            const float4 qp = ld_rot(rots, q.p, act);
+            const float dot = qc.x * qp.x + qc.y * qp.y + qc.z * qp.z + qc.w * qp.w;
+            const float su = (dot < 0.f ? -1.f : 1.f) * u;
+            for (int k = 0; k < 3; k++) {
+                am[k] = fmaf(u, gm[3 * r + k], am[k]);
+                as[k] = fmaf(u, gs[3 * r + k], as[k]);
+            }
+            ar = make_float4(fmaf(su, gr.x, ar.x), fmaf(su, gr.y, ar.y), fmaf(su, gr.z, ar.z), fmaf(su, gr.w, ar.w));
+            ao = fmaf(u, gop[r], ao);
+            if (!vec)
+                for (int k = 0; k < 3 * M; k++) atomicAdd(&dsh[(size_t)q.p * 3 * M + k], u * gsh[(size_t)r * 3 * M + k]);
+        }
+        flush();
+        return;
+    }
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= R + S) return;
     const CutRow q = cut_row(r, N, R, S, ri, pi, w);
     const float t = q.t, u = 1.f - q.t;
-    // d(act(x))/dx times the upstream, per input row (act == 0: the identity)
-    const auto dsc = [&](int64_t i, float g) { return act ? g * act_scale(s_raw[i]) : g; };
     const auto add_rot = [&](int64_t row, float4 g, bool store) {
         if (act) g = normalize_grad(reinterpret_cast<const float4 *>(rots)[row], g);
         if (store) {
@@ -203,33 +268,54 @@ __global__ __launch_bounds__(256) void cut_bwd_kernel(int64_t N, int M, int64_t 
     }
 }
 
-// SH part of the backward for M = 16: 16 lanes per row (12 active, 4 floats each), four rows per
-// wave instruction, so the atomics of one row hit one or two cache lines together.
+// SH part of the backward for M = 16: 16 lanes per row (12 active, 4 floats each).  uniq (a cut):
+// lane group g walks the kShRun consecutive rows [g kShRun, (g + 1) kShRun), writes each child row
+// with one 16-B store and adds the parent contributions of consecutive rows with the same parent
+// (siblings: expand_to_size emits a node's rendered children consecutively) before one atomic per
+// parent run.  Otherwise every row's child and parent contributions are atomics.
+constexpr int kShRun = 16;
 __global__ __launch_bounds__(256) void cut_bwd_sh_kernel(int64_t N, int64_t R, int64_t S, const int *ri, const int *pi,
                                                          const float *w, const float *__restrict__ gsh,
                                                          float *dsh, bool uniq) {
-    const int64_t rr = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+    const int64_t grp = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
     const int col = threadIdx.x & 15;
-    if (rr >= R + S || col >= 12) return;
-    const CutRow q = cut_row(rr, N, R, S, ri, pi, w);
-    const float4 g = reinterpret_cast<const float4 *>(gsh)[12 * rr + col];
-    float *dc = dsh + 48 * q.c + 4 * col;
-    const float t = q.copy ? 1.f : q.t, u = 1.f - q.t;
-    const float4 gc = make_float4(t * g.x, t * g.y, t * g.z, t * g.w);
-    if (uniq) {
-        reinterpret_cast<float4 *>(dc)[0] = gc;  // a cut's child row: one 16-B store
-    } else {
-        atomicAdd(dc + 0, gc.x);
-        atomicAdd(dc + 1, gc.y);
-        atomicAdd(dc + 2, gc.z);
-        atomicAdd(dc + 3, gc.w);
+    if (col >= 12) return;
+    const auto add4 = [&](float *a, float4 v) {
+        atomicAdd(a + 0, v.x);
+        atomicAdd(a + 1, v.y);
+        atomicAdd(a + 2, v.z);
+        atomicAdd(a + 3, v.w);
+    };
+    if (!uniq) {
+        const int64_t rr = grp;
+        if (rr >= R + S) return;
+        const CutRow q = cut_row(rr, N, R, S, ri, pi, w);
+        const float4 g = reinterpret_cast<const float4 *>(gsh)[12 * rr + col];
+        const float t = q.copy ? 1.f : q.t, u = 1.f - q.t;
+        add4(dsh + 48 * q.c + 4 * col, make_float4(t * g.x, t * g.y, t * g.z, t * g.w));
+        if (!q.copy) add4(dsh + 48 * q.p + 4 * col, make_float4(u * g.x, u * g.y, u * g.z, u * g.w));
+        return;
     }
-    if (q.copy) return;
-    float *dp = dsh + 48 * q.p + 4 * col;
-    atomicAdd(dp + 0, u * g.x);
-    atomicAdd(dp + 1, u * g.y);
-    atomicAdd(dp + 2, u * g.z);
-    atomicAdd(dp + 3, u * g.w);
+    const int64_t r0 = grp * kShRun, r1 = min(R + S, r0 + kShRun);
+    int64_t cur = -1;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t rr = r0; rr < r1; rr++) {
+        const CutRow q = cut_row(rr, N, R, S, ri, pi, w);
+        const float4 g = reinterpret_cast<const float4 *>(gsh)[12 * rr + col];
+        const float t = q.copy ? 1.f : q.t, u = 1.f - q.t;
+        reinterpret_cast<float4 *>(dsh + 48 * q.c + 4 * col)[0] = make_float4(t * g.x, t * g.y, t * g.z, t * g.w);
+        if (q.copy) continue;
+        if (q.p != cur) {
+            if (cur >= 0) add4(dsh + 48 * cur + 4 * col, acc);
+            cur = q.p;
+            acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        acc.x = fmaf(u, g.x, acc.x);
+        acc.y = fmaf(u, g.y, acc.y);
+        acc.z = fmaf(u, g.z, acc.z);
+        acc.w = fmaf(u, g.w, acc.w);
+    }
+    if (cur >= 0) add4(dsh + 48 * cur + 4 * col, acc);
 }
 
 }  // namespace
@@ -296,13 +382,14 @@ int cut_backward(int64_t N, int M, int64_t R, int64_t S, const int *render_indic
     const int64_t rows = R + S;
     const bool vec = M == 16 && reinterpret_cast<uintptr_t>(dL_dout_shs) % 16 == 0 &&
                      reinterpret_cast<uintptr_t>(dL_dshs) % 16 == 0;
-    hipLaunchKernelGGL(cut_bwd_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0,
+    hipLaunchKernelGGL(cut_bwd_kernel, dim3((unsigned)(((uniq ? (rows + kScRun - 1) / kScRun : rows) + 255) / 256)), dim3(256), 0,
                        static_cast<hipStream_t>(stream), N, M, R, S, render_indices, parent_indices,
                        interpolation_weights, rotations, dL_dout_means3D, dL_dout_scales, dL_dout_rotations,
                        dL_dout_opacities, dL_dout_shs, dL_dmeans3D, dL_dscales, dL_drotations, dL_dopacities,
                        dL_dshs, vec, act, s_raw, o_raw, uniq);
     if (vec)
-        hipLaunchKernelGGL(cut_bwd_sh_kernel, dim3((unsigned)((16 * rows + 255) / 256)), dim3(256), 0,
+        hipLaunchKernelGGL(cut_bwd_sh_kernel, dim3((unsigned)((16 * (uniq ? (rows + kShRun - 1) / kShRun : rows) + 255) / 256)),
+                           dim3(256), 0,
                            static_cast<hipStream_t>(stream), N, R, S, render_indices, parent_indices,
                            interpolation_weights, dL_dout_shs, dL_dshs, uniq);
     const hipError_t e = hipGetLastError();
