@@ -138,7 +138,6 @@ __global__ __launch_bounds__(256) void cut_fwd_kernel(int64_t N, int M, int64_t 
     }
 }
 
-constexpr int kScRun = 8;  // cut_bwd_kernel (uniq): consecutive rows per thread
 __global__ __launch_bounds__(256) void cut_bwd_kernel(int64_t N, int M, int64_t R, int64_t S, const int *ri,
                                                       const int *pi, const float *w, const float *__restrict__ rots,
                                                       const float *__restrict__ gm, const float *__restrict__ gs,
@@ -150,67 +149,77 @@ __global__ __launch_bounds__(256) void cut_bwd_kernel(int64_t N, int M, int64_t 
     // d(act(x))/dx times the upstream, per input row (act == 0: the identity)
     const auto dsc = [&](int64_t i, float g) { return act ? g * act_scale(s_raw[i]) : g; };
     if (uniq) {
-        // a cut: thread per kScRun consecutive rows; child rows written, parent contributions of
-        // consecutive rows with the same parent (siblings) summed before one set of atomics (the
-        // activation derivatives are linear in the upstream: applied once per run)
-        const int64_t r0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * kScRun, r1 = min(R + S, r0 + kScRun);
-        int64_t cur = -1;
-        float am[3] = {0.f, 0.f, 0.f}, as[3] = {0.f, 0.f, 0.f}, ao = 0.f;
-        float4 ar = make_float4(0.f, 0.f, 0.f, 0.f);
-        const auto flush = [&]() {
-            if (cur < 0) return;
-            for (int k = 0; k < 3; k++) {
-                atomicAdd(&dm[3 * cur + k], am[k]);
-                atomicAdd(&ds[3 * cur + k], dsc(3 * cur + k, as[k]));
-            }
-            float4 g = ar;
-            if (act) g = normalize_grad(reinterpret_cast<const float4 *>(rots)[cur], g);
-            atomicAdd(&drot[4 * cur + 0], g.x);
-            atomicAdd(&drot[4 * cur + 1], g.y);
-            atomicAdd(&drot[4 * cur + 2], g.z);
-            atomicAdd(&drot[4 * cur + 3], g.w);
-            atomicAdd(&dop[cur], act_opac_grad(act, act ? o_raw[cur] : 0.f, ao));
-        };
-        for (int64_t r = r0; r < r1; r++) {
-            const CutRow q = cut_row(r, N, R, S, ri, pi, w);
-            const float t = q.t, u = 1.f - q.t;
+        // a cut: thread per row (coalesced), child rows written; the parent contributions of
+        // consecutive rows with the same parent (siblings: expand_to_size emits a node's rendered
+        // children consecutively) summed across the wave by a segmented scan, then one set of atomics
+        // per sibling run (the activation derivatives are linear in the upstream: applied to the sum)
+        const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        const int lane = threadIdx.x & 63;
+        const bool valid = r < R + S;
+        CutRow q{0, 0, 1.f, true};
+        if (valid) q = cut_row(r, N, R, S, ri, pi, w);
+        const float t = q.t, u = 1.f - q.t;
+        float v[11];
+        for (int k = 0; k < 11; k++) v[k] = 0.f;
+        if (valid) {
             const float4 gr = make_float4(grot[4 * r + 0], grot[4 * r + 1], grot[4 * r + 2], grot[4 * r + 3]);
             const float4 qc = ld_rot(rots, q.c, act);
             for (int k = 0; k < 3; k++) {
                 dm[3 * q.c + k] = t * gm[3 * r + k];
                 ds[3 * q.c + k] = dsc(3 * q.c + k, t * gs[3 * r + k]);
             }
-            {
-                float4 g = make_float4(t * gr.x, t * gr.y, t * gr.z, t * gr.w);
-                if (act) g = normalize_grad(reinterpret_cast<const float4 *>(rots)[q.c], g);
-                drot[4 * q.c + 0] = g.x;
-                drot[4 * q.c + 1] = g.y;
-                drot[4 * q.c + 2] = g.z;
-                drot[4 * q.c + 3] = g.w;
-            }
+            float4 g = make_float4(t * gr.x, t * gr.y, t * gr.z, t * gr.w);
+            if (act) g = normalize_grad(reinterpret_cast<const float4 *>(rots)[q.c], g);
+            drot[4 * q.c + 0] = g.x;
+            drot[4 * q.c + 1] = g.y;
+            drot[4 * q.c + 2] = g.z;
+            drot[4 * q.c + 3] = g.w;
             dop[q.c] = act_opac_grad(act, act ? o_raw[q.c] : 0.f, t * gop[r]);
             if (!vec)
                 for (int k = 0; k < 3 * M; k++) dsh[(size_t)q.c * 3 * M + k] = t * gsh[(size_t)r * 3 * M + k];
-            if (q.copy) continue;
-            if (q.p != cur) {
-                flush();
-                cur = q.p;
-                am[0] = am[1] = am[2] = as[0] = as[1] = as[2] = ao = 0.f;
-                ar = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (!q.copy) {
+                const float4 qp = ld_rot(rots, q.p, act);
+                const float dot = qc.x * qp.x + qc.y * qp.y + qc.z * qp.z + qc.w * qp.w;
+                const float su = (dot < 0.f ? -1.f : 1.f) * u;
+                for (int k = 0; k < 3; k++) {
+                    v[k] = u * gm[3 * r + k];
+                    v[3 + k] = u * gs[3 * r + k];
+                }
+                v[6] = su * gr.x;
+                v[7] = su * gr.y;
+                v[8] = su * gr.z;
+                v[9] = su * gr.w;
+                v[10] = u * gop[r];
+                if (!vec)
+                    for (int k = 0; k < 3 * M; k++) atomicAdd(&dsh[(size_t)q.p * 3 * M + k], u * gsh[(size_t)r * 3 * M + k]);
             }
-            const float4 qp = ld_rot(rots, q.p, act);
-            const float dot = qc.x * qp.x + qc.y * qp.y + qc.z * qp.z + qc.w * qp.w;
-            const float su = (dot < 0.f ? -1.f : 1.f) * u;
-            for (int k = 0; k < 3; k++) {
-                am[k] = fmaf(u, gm[3 * r + k], am[k]);
-                as[k] = fmaf(u, gs[3 * r + k], as[k]);
-            }
-            ar = make_float4(fmaf(su, gr.x, ar.x), fmaf(su, gr.y, ar.y), fmaf(su, gr.z, ar.z), fmaf(su, gr.w, ar.w));
-            ao = fmaf(u, gop[r], ao);
-            if (!vec)
-                for (int k = 0; k < 3 * M; k++) atomicAdd(&dsh[(size_t)q.p * 3 * M + k], u * gsh[(size_t)r * 3 * M + k]);
         }
-        flush();
+        const int par = valid && !q.copy ? (int)q.p : -1;
+        const int prev = __shfl_up(par, 1, 64), next = __shfl_down(par, 1, 64);
+        const uint64_t heads = __ballot(lane == 0 || par != prev);
+        const int start = 63 - __clzll((long long)(heads & ((2ull << lane) - 1ull)));
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+#pragma unroll
+            for (int k = 0; k < 11; k++) {
+                const float up = __shfl_up(v[k], o, 64);
+                if (lane - o >= start) v[k] += up;
+            }
+        }
+        if (par >= 0 && (lane == 63 || next != par)) {  // the run's last lane holds its sums
+            const int64_t cur = par;
+            for (int k = 0; k < 3; k++) {
+                atomicAdd(&dm[3 * cur + k], v[k]);
+                atomicAdd(&ds[3 * cur + k], dsc(3 * cur + k, v[3 + k]));
+            }
+            float4 g = make_float4(v[6], v[7], v[8], v[9]);
+            if (act) g = normalize_grad(reinterpret_cast<const float4 *>(rots)[cur], g);
+            atomicAdd(&drot[4 * cur + 0], g.x);
+            atomicAdd(&drot[4 * cur + 1], g.y);
+            atomicAdd(&drot[4 * cur + 2], g.z);
+            atomicAdd(&drot[4 * cur + 3], g.w);
+            atomicAdd(&dop[cur], act_opac_grad(act, act ? o_raw[cur] : 0.f, v[10]));
+        }
         return;
     }
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -382,7 +391,7 @@ int cut_backward(int64_t N, int M, int64_t R, int64_t S, const int *render_indic
     const int64_t rows = R + S;
     const bool vec = M == 16 && reinterpret_cast<uintptr_t>(dL_dout_shs) % 16 == 0 &&
                      reinterpret_cast<uintptr_t>(dL_dshs) % 16 == 0;
-    hipLaunchKernelGGL(cut_bwd_kernel, dim3((unsigned)(((uniq ? (rows + kScRun - 1) / kScRun : rows) + 255) / 256)), dim3(256), 0,
+    hipLaunchKernelGGL(cut_bwd_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0,
                        static_cast<hipStream_t>(stream), N, M, R, S, render_indices, parent_indices,
                        interpolation_weights, rotations, dL_dout_means3D, dL_dout_scales, dL_dout_rotations,
                        dL_dout_opacities, dL_dout_shs, dL_dmeans3D, dL_dscales, dL_drotations, dL_dopacities,
