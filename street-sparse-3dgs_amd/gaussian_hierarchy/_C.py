@@ -93,10 +93,67 @@ def get_interpolation_weights(node_indices, size, nodes, boxes, viewpoint, viewd
     _check(rc, "get_interpolation_weights")
 
 
+# The .hier file (gaussian_hierarchy's writer / loader; the submodule is not vendored in the
+# reference, so this layout is restated from the upstream project's uncompressed format and is
+# parity-unpinned: no file written by the reference's tools is available here):
+#   int32 P; float32 positions[P][3]; float32 rotations[P][4]; float32 log_scales[P][3];
+#   float32 opacities[P]; float32 shs[P][48] (16 coefficients x RGB, coefficient-major);
+#   int32 N; int32 nodes[N][7] (depth, parent, start, count_leafs, count_merged, start_children,
+#   count_children); float32 boxes[N][2][4] (min xyz w, max xyz w).
+# A negative P marks the half-precision "compressed" variant, which is not supported (loud).
+_HIER_FIELDS = (("positions", 3), ("rotations", 4), ("log_scales", 3), ("opacities", 1), ("shs", 48))
+
+
 def load_hierarchy(path):
-    raise NotImplementedError("gaussian_hierarchy.load_hierarchy: the .hier file format (gaussianhierarchy, not "
-                              "vendored in the reference) is outside the rasterizer hot path this package rebuilds")
+    """(xyz (P,3), shs (P,16,3), alpha (P,1), log-scales (P,3), rotations (P,4), nodes (N,7) int32,
+    boxes (N,2,4)) as CPU tensors -- what scene/gaussian_model.py:347 unpacks."""
+    import numpy as np
+    import torch
+    with open(path, "rb") as f:
+        data = f.read()
+    off = 0
+
+    def take(dtype, count):
+        nonlocal off
+        a = np.frombuffer(data, dtype=dtype, count=count, offset=off)
+        off += a.nbytes
+        return a
+
+    P = int(take(np.int32, 1)[0])
+    if P < 0:
+        raise NotImplementedError("gaussian_hierarchy.load_hierarchy: compressed (half precision) .hier files are "
+                                  "not supported")
+    arrs = {name: take(np.float32, P * w).reshape(P, w) for name, w in _HIER_FIELDS}
+    N = int(take(np.int32, 1)[0])
+    nodes = take(np.int32, N * 7).reshape(N, 7)
+    boxes = take(np.float32, N * 8).reshape(N, 2, 4)
+    if off != len(data):
+        raise ValueError(f"gaussian_hierarchy.load_hierarchy: {len(data) - off} trailing bytes in {path}")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a))
+    return (t(arrs["positions"]), t(arrs["shs"]).reshape(P, 16, 3), t(arrs["opacities"]), t(arrs["log_scales"]),
+            t(arrs["rotations"]), t(nodes), t(boxes))
 
 
-def write_hierarchy(*args, **kwargs):
-    raise NotImplementedError("gaussian_hierarchy.write_hierarchy: the .hier file format is not rebuilt here")
+def write_hierarchy(path, xyz, shs, opacities, scales, rotations, nodes, boxes):
+    """The inverse of load_hierarchy (scene/gaussian_model.py:437-445 save_hier): log-scales and
+    activated opacities as the caller passes them, any device."""
+    import numpy as np
+    f32 = lambda x, w: np.ascontiguousarray(x.detach().float().cpu().numpy().reshape(-1, w), dtype=np.float32)
+    pos = f32(xyz, 3)
+    P = pos.shape[0]
+    fields = {"positions": pos, "rotations": f32(rotations, 4), "log_scales": f32(scales, 3),
+              "opacities": f32(opacities, 1), "shs": f32(shs, 48)}
+    for name, w in _HIER_FIELDS:
+        if fields[name].shape != (P, w):
+            raise ValueError(f"gaussian_hierarchy.write_hierarchy: {name} has {fields[name].shape[0]} rows, not {P}")
+    nd = np.ascontiguousarray(nodes.detach().cpu().numpy().reshape(-1, 7), dtype=np.int32)
+    bx = np.ascontiguousarray(boxes.detach().float().cpu().numpy().reshape(-1, 2, 4), dtype=np.float32)
+    if bx.shape[0] != nd.shape[0]:
+        raise ValueError("gaussian_hierarchy.write_hierarchy: nodes and boxes differ in length")
+    with open(path, "wb") as f:
+        f.write(np.int32(P).tobytes())
+        for name, _ in _HIER_FIELDS:
+            f.write(fields[name].tobytes())
+        f.write(np.int32(nd.shape[0]).tobytes())
+        f.write(nd.tobytes())
+        f.write(bx.tobytes())

@@ -10,6 +10,7 @@ node."""
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import pytest
@@ -122,3 +123,37 @@ def test_viewpoint_inside_root_box_expands_to_leaves(tree):
     ri, pi, ni = O.expand_to_size(nodes, boxes, np.float32(1.0), v)
     # every node whose box contains v is expanded; everything else is cut at its first small node
     assert 0 not in set(ni.tolist())
+
+
+def test_hier_file_round_trip(tmp_path):
+    """gaussian_hierarchy.load_hierarchy / write_hierarchy (scene/gaussian_model.py:347, 437-445):
+    the uncompressed .hier layout restated in _C.py (parity-unpinned: the gaussianhierarchy writer
+    is not vendored and no reference-written file is available) -- round trip, exact byte size, and
+    loud failures for the compressed variant and for trailing bytes."""
+    import numpy as np
+    import torch
+    from gaussian_hierarchy._C import load_hierarchy, write_hierarchy
+    rng = np.random.default_rng(3)
+    P, N = 1000, 400
+    xyz = torch.tensor(rng.normal(size=(P, 3)), dtype=torch.float32)
+    shs = torch.tensor(rng.normal(size=(P, 16, 3)), dtype=torch.float32)
+    opac = torch.tensor(rng.random((P, 1)), dtype=torch.float32)
+    scales = torch.tensor(rng.normal(-4, 1, size=(P, 3)), dtype=torch.float32)
+    rots = torch.tensor(rng.normal(size=(P, 4)), dtype=torch.float32)
+    nodes = torch.tensor(rng.integers(-1, P, size=(N, 7)), dtype=torch.int32)
+    boxes = torch.tensor(rng.normal(size=(N, 2, 4)), dtype=torch.float32)
+    path = str(tmp_path / "h.hier")
+    write_hierarchy(path, xyz, shs, opac, scales, rots, nodes, boxes)
+    assert os.path.getsize(path) == 4 + P * (3 + 4 + 3 + 1 + 48) * 4 + 4 + N * 7 * 4 + N * 8 * 4
+    got = load_hierarchy(path)
+    for a, b in zip(got, (xyz, shs, opac, scales, rots, nodes, boxes)):
+        assert a.shape == b.shape and a.dtype == b.dtype and torch.equal(a, b)
+    raw = open(path, "rb").read()
+    with open(path, "wb") as f:
+        f.write(np.int32(-P).tobytes() + raw[4:])
+    with pytest.raises(NotImplementedError):
+        load_hierarchy(path)
+    with open(path, "wb") as f:
+        f.write(raw + b"\0\0\0\0")
+    with pytest.raises(ValueError):
+        load_hierarchy(path)
