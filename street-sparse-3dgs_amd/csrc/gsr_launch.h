@@ -124,6 +124,7 @@ bool bwd_segments_supported();
 bool fwd_segments_supported();
 bool fwd_segments_in_kernel();  // the worker pool inside render_fwd's launch (no side stream)
 uint32_t fseg_min_len(uint32_t Lf);  // the shortest list the forward split takes
+uint32_t set_fwd_split_min(uint32_t len);  // gsr_set_fwd_split_min
 
 // backward.hip
 // sparse_rows (the native train step only, set_sparse_grad_rows): the rows of Gaussians with ten

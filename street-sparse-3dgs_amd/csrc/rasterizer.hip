@@ -1011,6 +1011,11 @@ int gsr_set_deterministic(int enable) { return g_deterministic.exchange(enable ?
 
 int gsr_set_split_gate(int enable) { return g_split_gate.exchange(enable ? 1 : 0); }
 
+int gsr_set_fwd_split_min(int len) {
+    if (len < 0) return fail(GSR_ERR_INVALID_ARGUMENT, "forward split minimum list length must be >= 0");
+    return (int)set_fwd_split_min((uint32_t)len);
+}
+
 int gsr_set_fwd_segment(int L) {
     if (L < 0 || (L > 0 && (L < (int)kMinFwdSeg || L % kWave != 0)))
         return fail(GSR_ERR_INVALID_ARGUMENT, "forward segment length: 0 (off) or a multiple of 64 >= 4096");

@@ -69,6 +69,7 @@ SIGNATURES = {
     "gsr_set_bwd_segment": (_i, [_i]),
     "gsr_set_fwd_segment": (_i, [_i]),
     "gsr_set_split_gate": (_i, [_i]),
+    "gsr_set_fwd_split_min": (_i, [_i]),
     "gsr_segment_layout_check": (_i, [ctypes.c_int64, _i, _i, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     "gsr_frame_stats": (_i, [_vp, _i, _i, _i, ctypes.POINTER(_i64), _i]),
     "gsr_blend_stats": (_i, [ctypes.POINTER(_i64), _i, _i]),

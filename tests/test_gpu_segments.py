@@ -30,8 +30,10 @@ def _splits_every_frame():
     """The split gate off: every frame of these tests takes the splits it is set up for."""
     from diff_gaussian_rasterization import _C
     prev = _C.set_split_gate(False)
+    prev_min = _C.set_fwd_split_min(4 * 4096)  # these scenes' 22k-28k lists take the forward split
     yield
     _C.set_split_gate(prev)
+    _C.set_fwd_split_min(prev_min)
 
 SEG_TOL = 1e-5  # segmented vs unsplit gradients, relative L2 (fp32 rounding of S at the checkpoints; measured <= 2.2e-6)
 
