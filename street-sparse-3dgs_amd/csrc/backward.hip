@@ -972,7 +972,15 @@ bool bwd_zero_rows(const GaussianInputs &in, const GaussianGrads &out, const Bwd
     z->stamp = g_stamp.fetch_add(1, std::memory_order_relaxed) + 1u;
     // only the first GSR_BWD_ZERO_PCT % of the backward's workgroups in launch order (the heaviest
     // tiles first) carry zero rows: the light tiles at the end of the launch finish without them
-    const uint64_t nz = std::max<uint64_t>(1, (uint64_t)nblocks * GSR_BWD_ZERO_PCT / 100);
+    // GSR_BWD_ZERO_FROM (environment, measurement A/B): the zero rows go to the workgroups from that
+    // percentage of the grid on (launch order: the light tiles and the idle segment slots last)
+    static const int zfrom_pct = [] {
+        const char *e = getenv("GSR_BWD_ZERO_FROM");
+        const int v = e ? atoi(e) : 0;
+        return v > 0 && v < 100 ? v : 0;
+    }();
+    z->zfrom = (uint32_t)((uint64_t)nblocks * zfrom_pct / 100);
+    const uint64_t nz = std::max<uint64_t>(1, ((uint64_t)nblocks - z->zfrom) * GSR_BWD_ZERO_PCT / 100);
     z->per4 = (z->c4[kZeroArrays] + nz - 1) / nz;
     return true;
 }

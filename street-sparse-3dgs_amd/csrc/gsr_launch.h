@@ -106,6 +106,7 @@ struct ZeroRows {
     uint64_t n[kZeroArrays];
     uint64_t c4[kZeroArrays + 1];
     uint64_t per4;
+    uint32_t zfrom;    // workgroups below zfrom carry no zero rows (workgroup b >= zfrom: slice b - zfrom)
     uint32_t *stamps;  // != NULL: render_bwd stamps every staged Gaussian (live_stamp) with `stamp`
     uint32_t stamp;
 };

@@ -964,17 +964,17 @@ __device__ __forceinline__ void bwd_gather(const GRec *__restrict__ rec, const u
 // preprocess_bwd no longer streams these bytes on its own
 __device__ __forceinline__ void bwd_zero_slice(const ZeroRows &zr) {
     const int lane = threadIdx.x;
-    if (!zr.per4) return;
+    if (!zr.per4 || blockIdx.x < zr.zfrom) return;
     {
         typedef float f4 __attribute__((ext_vector_type(4)));
-        const uint64_t q0 = (uint64_t)blockIdx.x * zr.per4, q1 = min(zr.c4[kZeroArrays], q0 + zr.per4);
+        const uint64_t q0 = (uint64_t)(blockIdx.x - zr.zfrom) * zr.per4, q1 = min(zr.c4[kZeroArrays], q0 + zr.per4);
         for (uint64_t q = q0 + (uint64_t)lane; q < q1; q += kWave) {
             int k = 0;
 #pragma unroll
             for (int a = 1; a < kZeroArrays; a++) k += q >= zr.c4[a];
             __builtin_nontemporal_store(f4{0.f, 0.f, 0.f, 0.f}, reinterpret_cast<f4 *>(zr.p[k]) + (q - zr.c4[k]));
         }
-        if (blockIdx.x == 0 && lane < 4 * kZeroArrays) {  // the floats past each array's last whole float4
+        if (blockIdx.x == zr.zfrom && lane < 4 * kZeroArrays) {  // the floats past each array's last whole float4
             const int k = lane >> 2, t = lane & 3;
             const uint64_t e = 4 * (zr.c4[k + 1] - zr.c4[k]) + (uint64_t)t;
             if (e < zr.n[k]) __builtin_nontemporal_store(0.f, zr.p[k] + e);
