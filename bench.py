@@ -935,6 +935,7 @@ def main():
     T = ((W + 15) // 16) * ((H + 15) // 16)
     npix = W * H
     abytes = algorithmic_bytes(P, Pv, K, T, npix, P1, M=inp["shs"].shape[1], Pl=Pl)
+    strict_8d = 44 * K + 24 * npix + 40 * Pv
     serial_ms = sum(v for k, v in stages.items() if k not in OVERLAPPED_STAGES)
     dom = max(stages, key=lambda k: stages[k]) if stages else "render_bwd"
     dom_ms = stages.get(dom, 0.0)
@@ -970,7 +971,11 @@ def main():
                      "algorithmic_bytes": abytes[dom], "avg_ms": round(dom_ms, 5),
                      "traffic_source": traffic_src, "profile_is_current": traffic_cur, "rocprof_avg_ms": rp_ms,
                      "frac_rocprof": round(abytes[dom] / (rp_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if rp_ms else None,
-                     "kernel_source_sha": kernel_source_sha()},
+                     "kernel_source_sha": kernel_source_sha(),
+                     # SURVEY.md 8(d)'s own render-bwd term (44 K + 24 Npix + 40 Pv), without the dense
+                     # zero gradient rows render_bwd also writes (they belong to preprocess-bwd's 260 P there)
+                     "algorithmic_bytes_strict_8d": strict_8d,
+                     "frac_strict_8d": round(strict_8d / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if dom == "render_bwd" else None},
         "valu_roofline": [r for r in (valu_roofline(k, stages.get(k)) for k in ("render_bwd", "render_fwd")) if r],
         "step_dispersion": dispersion(per_step),
         "gpu_clock": {"before": clk_before, "after": clk_after, "under_load": clk_load,
