@@ -936,6 +936,151 @@ __global__ __launch_bounds__(kAdamThreads) void sparse_adam_rows_kernel(AdamArgs
     }
 }
 
+// The dense step over whole rows (no relevance, no zero rows, no fused shrink: torch.optim.Adam's
+// update of every element, train_post's optimizer): each group is one flat run of P * row_stride
+// floats, streamed as float4.  A column-split pair (the DC and rest SH blocks of one buffer, each
+// with its own learning rate) is merged on the host into one run whose step size switches at
+// split_col, so the buffer is read once in full rows instead of twice in strided blocks.  Same
+// arithmetic as adam_narrow, element for element.
+struct FlatAdamRun {
+    float *param;
+    const float *grad;
+    float *exp_avg;
+    float *exp_avg_sq;
+    int64_t n;         // floats
+    int row;           // floats per row (the column of element e is e % row)
+    int split_col;     // columns < split_col take step0, the rest step1 (row: one step size)
+    float step0, step1;
+    float bc2s;
+    int vec;           // all four arrays 16-B aligned and row % 4 == 0: float4 access
+};
+struct FlatAdamArgs {
+    FlatAdamRun r[kMaxGroups];
+    int64_t block_start[kMaxGroups + 1];
+    int n;
+};
+constexpr int kFlatPerThread = 8;  // two float4 per lane
+constexpr int64_t kFlatPerBlock = (int64_t)kAdamThreads * kFlatPerThread;
+
+__device__ __forceinline__ void flat_adam_one(const FlatAdamRun &R, float &p, float &m, float &v, float g, float ss,
+                                              float b1, float b2, float omb1, float omb2, float eps) {
+    const float mm = m * b1 + omb1 * g;
+    const float vv = v * b2 + omb2 * (g * g);
+    const float denom = sqrtf(vv) / R.bc2s + eps;
+    m = mm;
+    v = vv;
+    p = p + (-ss) * (mm / denom);
+}
+
+__global__ __launch_bounds__(kAdamThreads) void dense_adam_flat_kernel(FlatAdamArgs a, float b1, float b2, float omb1,
+                                                                       float omb2, float eps) {
+    int k = 0;
+    while (k + 1 < a.n && (int64_t)blockIdx.x >= a.block_start[k + 1]) k++;
+    const FlatAdamRun &R = a.r[k];
+    const int64_t b0 = ((int64_t)blockIdx.x - a.block_start[k]) * kFlatPerBlock;
+    if (R.vec) {
+        float4 g[2], m[2], v[2], p[2];
+        bool ok[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int64_t e = b0 + (int64_t)h * (kAdamThreads * 4) + 4 * threadIdx.x;
+            ok[h] = e < R.n;  // n is a multiple of 4 (row % 4 == 0)
+            if (ok[h]) {
+                g[h] = *reinterpret_cast<const float4 *>(R.grad + e);
+                m[h] = *reinterpret_cast<const float4 *>(R.exp_avg + e);
+                v[h] = *reinterpret_cast<const float4 *>(R.exp_avg_sq + e);
+                p[h] = *reinterpret_cast<const float4 *>(R.param + e);
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            if (!ok[h]) continue;
+            const int64_t e = b0 + (int64_t)h * (kAdamThreads * 4) + 4 * threadIdx.x;
+            // the four share a row (row % 4 == 0); one step size: no column needed
+            const int c = R.split_col < R.row ? (int)(e % R.row) : 0;
+            float ss[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) ss[j] = c + j < R.split_col ? R.step0 : R.step1;
+            flat_adam_one(R, p[h].x, m[h].x, v[h].x, g[h].x, ss[0], b1, b2, omb1, omb2, eps);
+            flat_adam_one(R, p[h].y, m[h].y, v[h].y, g[h].y, ss[1], b1, b2, omb1, omb2, eps);
+            flat_adam_one(R, p[h].z, m[h].z, v[h].z, g[h].z, ss[2], b1, b2, omb1, omb2, eps);
+            flat_adam_one(R, p[h].w, m[h].w, v[h].w, g[h].w, ss[3], b1, b2, omb1, omb2, eps);
+            *reinterpret_cast<float4 *>(R.exp_avg + e) = m[h];
+            *reinterpret_cast<float4 *>(R.exp_avg_sq + e) = v[h];
+            *reinterpret_cast<float4 *>(R.param + e) = p[h];
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kFlatPerThread; j++) {
+            const int64_t e = b0 + (int64_t)j * kAdamThreads + threadIdx.x;
+            if (e >= R.n) break;
+            float p = R.param[e], m = R.exp_avg[e], v = R.exp_avg_sq[e];
+            const float ss = (int)(e % R.row) < R.split_col ? R.step0 : R.step1;
+            flat_adam_one(R, p, m, v, R.grad[e], ss, b1, b2, omb1, omb2, eps);
+            R.exp_avg[e] = m;
+            R.exp_avg_sq[e] = v;
+            R.param[e] = p;
+        }
+    }
+}
+
+// Builds the flat runs of a dense step.  A group that is a column block not pairing with its
+// neighbour into whole rows is left for the row-block kernel: its index goes to rest[].  Returns
+// the number of flat runs.
+int flat_adam_runs(int n_groups, const gsr_adam_group *groups, int64_t P, FlatAdamArgs &fa, int *rest,
+                   int &n_rest) {
+    std::memset(&fa, 0, sizeof(fa));
+    n_rest = 0;
+    int64_t blocks = 0;
+    for (int i = 0; i < n_groups; i++) {
+        const gsr_adam_group &g = groups[i];
+        const int64_t rs = g.row_stride == 0 ? g.width : g.row_stride;
+        FlatAdamRun r;
+        std::memset(&r, 0, sizeof(r));
+        r.param = g.param;
+        r.grad = g.grad;
+        r.exp_avg = g.exp_avg;
+        r.exp_avg_sq = g.exp_avg_sq;
+        r.step0 = r.step1 = g.step_size;
+        r.bc2s = g.bias_correction2_sqrt;
+        r.split_col = (int)rs;
+        if (rs > 0x7fffffff) {
+            rest[n_rest++] = i;
+            continue;
+        }
+        if (rs != g.width) {
+            const gsr_adam_group *h = i + 1 < n_groups ? &groups[i + 1] : nullptr;
+            const int64_t hs = h ? (h->row_stride == 0 ? h->width : h->row_stride) : 0;
+            if (!h || hs != rs || g.width + h->width != rs || h->param != g.param + g.width ||
+                h->grad != g.grad + g.width || h->exp_avg != g.exp_avg + g.width ||
+                h->exp_avg_sq != g.exp_avg_sq + g.width || h->bias_correction2_sqrt != g.bias_correction2_sqrt) {
+                rest[n_rest++] = i;
+                continue;
+            }
+            r.split_col = (int)g.width;
+            r.step1 = h->step_size;
+            i++;
+        }
+        r.row = (int)rs;
+        r.n = P * rs;
+        const uintptr_t al = reinterpret_cast<uintptr_t>(r.param) | reinterpret_cast<uintptr_t>(r.grad) |
+                             reinterpret_cast<uintptr_t>(r.exp_avg) | reinterpret_cast<uintptr_t>(r.exp_avg_sq);
+        r.vec = (al & 15) == 0 && rs % 4 == 0;
+        fa.r[fa.n] = r;
+        fa.block_start[fa.n] = blocks;
+        blocks += (r.n + kFlatPerBlock - 1) / kFlatPerBlock;
+        fa.n++;
+    }
+    fa.block_start[fa.n] = blocks;
+    return fa.n;
+}
+
+// GSR_ADAM_DENSE_ROWS=1 sends a dense step through the row-block kernel instead (A/B).
+bool adam_dense_rows() {
+    const char *e = std::getenv("GSR_ADAM_DENSE_ROWS");
+    return e != nullptr && e[0] == '1';
+}
+
 // GSR_ADAM_ELEMENTWISE=1 selects the element-per-thread kernel (same bits; A/B test and
 // measurements).  Read per call so a test can switch it.
 bool adam_elementwise() {
@@ -1538,7 +1683,27 @@ int sparse_adam(int n_groups, const gsr_adam_group *groups, int64_t P, const flo
                            flag_scratch);
     }
     // torch applies python-float hyper-parameters as fp32 scalars: b, (1 - b) rounded from double
-    if (!adam_elementwise())
+    if (!relevance && !live3 && skybox == 0 && !shrink_raw && !adam_elementwise() && !adam_dense_rows()) {
+        // the dense step: flat runs, and the row-block kernel for any group that is not one
+        FlatAdamArgs fa;
+        int rest[kMaxGroups], n_rest = 0;
+        if (flat_adam_runs(n_groups, groups, P, fa, rest, n_rest) > 0)
+            hipLaunchKernelGGL(dense_adam_flat_kernel, dim3((unsigned)fa.block_start[fa.n]), dim3(kAdamThreads), 0, s,
+                               fa, (float)beta1, (float)beta2, (float)(1.0 - beta1), (float)(1.0 - beta2),
+                               (float)eps);
+        if (n_rest > 0) {
+            AdamArgs ar;
+            std::memset(&ar, 0, sizeof(ar));
+            ar.n = n_rest;
+            for (int j = 0; j < n_rest; j++) ar.g[j] = a.g[rest[j]];
+            hipLaunchKernelGGL(sparse_adam_rows_kernel,
+                               dim3((unsigned)((P + kAdamThreads - 1) / kAdamThreads), (unsigned)n_rest),
+                               dim3(kAdamThreads), 0, s, ar, relevance, P, (float)beta1, (float)beta2,
+                               (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps, (const int *)nullptr,
+                               ShrinkArgs{nullptr, 0, 0.f}, DenseRows{nullptr, 0}, -1);
+        }
+    }
+    else if (!adam_elementwise())
     {
         // the shrink reads the scales after their Adam update: it runs in the scaling group's wave
         int sh_group = -1;

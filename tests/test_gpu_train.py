@@ -511,6 +511,49 @@ def test_sparse_adam_row_blocks_equal_elementwise(frac, monkeypatch):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("P", [70_001, 1])
+def test_dense_adam_flat_runs_equal_row_blocks(P, monkeypatch):
+    """The dense step (no relevance: torch.optim.Adam over every element, train_post's optimizer)
+    streams each group as one flat float4 run and merges a column-split pair into whole rows.
+    Parameters and moments are bit-identical to the row-block and element-per-thread kernels, for
+    float4 runs ((P,16,3) pair, (P,4)), scalar runs ((P,3), (P,1), a 4-B-offset (P,4) view) and a
+    column split that does not cover the row (that group alone goes to the row-block kernel)."""
+    from gs_train import Adam
+    g = torch.Generator().manual_seed(9)
+    shapes = [(3,), (16, 3), (1,), (4,), (8,), (6,)]
+    init = [torch.randn((P,) + s, generator=g) for s in shapes]
+    grads = [[torch.randn((P,) + s, generator=g) for s in shapes] for _ in range(3)]
+    out = {}
+    for mode in ("flat", "rows", "elementwise"):
+        monkeypatch.setenv("GSR_ADAM_DENSE_ROWS", "1" if mode == "rows" else "0")
+        monkeypatch.setenv("GSR_ADAM_ELEMENTWISE", "1" if mode == "elementwise" else "0")
+        params = [torch.nn.Parameter(h.to(DEV)) for h in init]
+        # an (P, 4) parameter whose storage starts 4 B past a 16-B boundary: the scalar run
+        store = torch.zeros(P * 4 + 1, device=DEV)
+        odd = torch.nn.Parameter(store[1:].view(P, 4))
+        with torch.no_grad():
+            odd.copy_(init[5][:, :4].to(DEV))
+        groups = [{"params": [params[0]], "lr": 1.6e-4},
+                  {"params": [params[1]], "lr": 2.5e-3, "column_lrs": [(0, 3, 2.5e-3), (3, 48, 1.25e-4)]},
+                  {"params": [params[2]], "lr": 5e-2}, {"params": [params[3]], "lr": 1e-3},
+                  {"params": [params[4]], "lr": 7e-3, "column_lrs": [(0, 2, 7e-3), (2, 6, 3e-3)]},
+                  {"params": [odd], "lr": 4e-3}]
+        opt = Adam(groups, lr=0.0, eps=1e-15)
+        for gr in grads:
+            for p, x in zip(params[:5], gr[:5]):
+                p.grad = x.to(DEV)
+            odd.grad = gr[5][:, :4].contiguous().to(DEV)
+            opt.step()
+        torch.cuda.synchronize()
+        out[mode] = [t.detach().clone() for p in params[:5] + [odd]
+                     for t in (p, opt.state[p]["exp_avg"], opt.state[p]["exp_avg_sq"])]
+    for name in ("rows", "elementwise"):
+        for a, b in zip(out["flat"], out[name]):
+            assert torch.equal(a, b), name
+    # and it moved every element of every run
+    assert not torch.equal(out["flat"][3], init[1].to(DEV))
+
+
 @pytest.mark.parametrize("lam,scale", [(0.2, 1.0), (0.35, 2.5)])
 def test_photo_loss_fused_equals_composed(lam, scale):
     """gsr_photo_loss_* (one autograd node) against l1_ssim composed with torch's scalar ops as
