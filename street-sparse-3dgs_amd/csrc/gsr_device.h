@@ -510,8 +510,9 @@ constexpr uint32_t kMinFwdSeg = 4096;
 __host__ __device__ __forceinline__ bool fseg_splits(uint32_t len, uint32_t fseg_min) { return fseg_min && len > fseg_min; }
 constexpr int kFwdWorkers = 256;
 constexpr int kFwdPartials = 6;  // r, g, b, inverse depth, T at the end, last contributor | stop << 31
-// bwd_cnt's words past the backward's: the item count tile_order wrote, the queue's next item
-constexpr int kFwdItemsWord = kBwdSegCount + 1, kFwdNextWord = kBwdSegCount + 2;
+// bwd_cnt's words past the backward's: the item count tile_order wrote, the queue's next item,
+// and (workers launched before tile_order) the queue-ready flag tile_order releases
+constexpr int kFwdItemsWord = kBwdSegCount + 1, kFwdNextWord = kBwdSegCount + 2, kFwdReadyWord = kBwdSegCount + 3;
 struct FwdSegLayout {
     uint32_t *items, *tickets, *flags, *nc;
     float *agg;  // per item x 256 pixels: the transmittance through the segment

@@ -48,7 +48,7 @@ void launch_preprocess_color(const GaussianInputs &in, const Camera &cam, const 
 void launch_tile_order(const uint32_t *work, const uint2 *ranges, int T, int shift, uint32_t *order, hipStream_t s,
                        const uint32_t *kdev = nullptr, uint32_t cap = 0, uint32_t *zero_classes = nullptr,
                        uint32_t *fctl = nullptr, void *bin_base = nullptr, uint32_t seg_len = 0, uint32_t fseg_len = 0,
-                       uint32_t *host_tilelist = nullptr);
+                       uint32_t *host_tilelist = nullptr, uint32_t *fwd_ready = nullptr);
 void launch_mark_visible(int P, const float *means3D, const float *view, uint8_t *present, hipStream_t s);
 
 // sort.hip (rocPRIM)
@@ -115,7 +115,16 @@ struct ZeroRows {
 void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                        const float *bg, float *out_color, float *out_invdepth, hipStream_t s, bool need_bwd = true,
                        bool sb_order = false, uint32_t seg_len = 0, uint32_t fseg_len = 0,
-                       hipStream_t worker_stream = nullptr);
+                       hipStream_t worker_stream = nullptr, bool workers_launched = false);
+// Forward segments' worker pool launched ahead of tile_order (on a side stream that has waited for
+// the binning and the colour pass): its workgroups are resident before render_fwd's grid fills the
+// CUs and start on the queue as soon as tile_order releases bwd_cnt[kFwdReadyWord] (zeroed by the
+// caller on the main stream first).
+void launch_render_fwd_workers(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
+                               const float *bg, float *out_color, float *out_invdepth, bool need_bwd, uint32_t seg_len,
+                               uint32_t fseg_len, hipStream_t ws);
+// GSR_FWD_EARLY_WORKERS=1: launch_render_fwd_workers before tile_order (default: beside render_fwd)
+bool fwd_early_workers();
 // seg_len != 0: the backward's heavy tiles are cut into segments of seg_len list positions
 // (gsr_set_bwd_segment; the backward must get the value its forward was made with)
 void launch_render_bwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,

@@ -802,12 +802,31 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
                 return fail(GSR_ERR_DEVICE, "side stream join failed");
         }
         if ((r = check("binning (tiles)", debug, s))) return r;
+        // forward segments: the worker pool launched now, on the second side stream once the binning
+        // (and the colour pass) are done, so its workgroups are resident before render_fwd's grid
+        // fills the CUs; they start on the queue when tile_order releases it.  Joined after render_fwd.
+        hipStream_t ws = s;
+        hipEvent_t wf = nullptr, wj = nullptr;
+        bool early = false;
+        if (fseg_used && !sb_order && fwd_early_workers() && !fwd_segments_in_kernel() &&
+            side_stream(s, &ws, &wf, &wj, 1) && ws != s) {
+            uint32_t *ready = is.bwd_cnt + kFwdReadyWord;
+            if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ready), 0, 1, s) != hipSuccess ||
+                hipEventRecord(wf, s) != hipSuccess || hipStreamWaitEvent(ws, wf, 0) != hipSuccess ||
+                (split && !GSR_COLOR_SERIAL && !joined && hipStreamWaitEvent(ws, join, 0) != hipSuccess))
+                return fail(GSR_ERR_DEVICE, "side stream fork failed");
+            launch_render_fwd_workers(cam, gs, bs, is, background, out_color, out_invdepth, need_bwd, seg_used,
+                                      fseg_used, ws);
+            if (hipEventRecord(wj, ws) != hipSuccess) return fail(GSR_ERR_DEVICE, "side stream join record failed");
+            early = true;
+        }
         if (!sb_order) {
             StageTimer st(4, s);
             // forward order: by list length (and the backward's class counters zeroed)
             launch_tile_order(nullptr, is.ranges, T, 4, is.tile_ids, s, bs.kdev, bs.cap,
                               GSR_BWD_CLS && need_bwd ? is.bwd_cnt : nullptr, is.bwd_cnt + kFwdItemsWord, bs.point_list,
-                              seg_used, fseg_used, P > 0 ? g_pinned_dev + kHostTileList : nullptr);
+                              seg_used, fseg_used, P > 0 ? g_pinned_dev + kHostTileList : nullptr,
+                              early ? is.bwd_cnt + kFwdReadyWord : nullptr);
         }
         if ((r = check("tile order", debug, s))) return r;
         if (split && !GSR_COLOR_SERIAL && !joined) {
@@ -821,14 +840,15 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
             // split tiles); joined before anything reads the frame
             hipStream_t wside = s;
             hipEvent_t wfork = nullptr, wjoin = nullptr;
-            if (fseg_used && !fwd_segments_in_kernel() && !side_stream(s, &wside, &wfork, &wjoin)) wside = s;
-            const bool forked = fseg_used && wside != s;
+            if (fseg_used && !early && !fwd_segments_in_kernel() && !side_stream(s, &wside, &wfork, &wjoin)) wside = s;
+            const bool forked = fseg_used && !early && wside != s;
             if (forked && (hipEventRecord(wfork, s) != hipSuccess || hipStreamWaitEvent(wside, wfork, 0) != hipSuccess))
                 return fail(GSR_ERR_DEVICE, "side stream fork failed");
             launch_render_fwd(cam, gs, bs, is, background, out_color, out_invdepth, s, need_bwd, sb_order, seg_used,
-                              fseg_used, wside);
+                              fseg_used, wside, early);
             if (forked && (hipEventRecord(wjoin, wside) != hipSuccess || hipStreamWaitEvent(s, wjoin, 0) != hipSuccess))
                 return fail(GSR_ERR_DEVICE, "side stream join failed");
+            if (early && hipStreamWaitEvent(s, wj, 0) != hipSuccess) return fail(GSR_ERR_DEVICE, "side stream join failed");
         }
         if (need_bwd && !GSR_BWD_CLS) {
             StageTimer st(9, s);  // backward launch order, from the forward's per-tile work

@@ -307,10 +307,28 @@ __device__ void fwd_seg_worker(const uint2 *__restrict__ ranges, const uint32_t 
                                uint32_t *__restrict__ tile_work, uint32_t kf, const uint32_t *__restrict__ sort_err,
                                uint32_t *__restrict__ bwd_cnt, uint32_t *__restrict__ bwd_cls, int ntiles, uint32_t seg_len,
                                uint32_t fseg_len, uint32_t *bin_base, uint32_t *fctl, float4 *sa, float4 *sb,
-                               float4 *sc, uint32_t *s_work, uint32_t *s_scalar) {
+                               float4 *sc, uint32_t *s_work, uint32_t *s_scalar, bool wait_ready) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const FwdSegLayout f = fseg_layout(bin_base, kf, seg_len, fseg_len);
     float *ck = seg_len && bwd_cnt ? reinterpret_cast<float *>(reinterpret_cast<char *>(bin_base) + ck_offset(kf)) : nullptr;
+    if (wait_ready) {
+        // launched ahead of tile_order: wait for its release of the queue (a bounded spin; never
+        // expected to give up -- the workers then leave and the split tiles keep no pixels)
+        if (threadIdx.x == 0) {
+            uint32_t ok = 1u, spins = 0;
+            while (!__hip_atomic_load(fctl + (kFwdReadyWord - kFwdItemsWord), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                if (++spins > (1u << 22)) {
+                    ok = 0u;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(4);
+            }
+            s_scalar[2] = ok;
+        }
+        wg_acquire();
+        if (!s_scalar[2]) return;
+        __syncthreads();  // s_scalar[2] is reused below
+    }
     const uint32_t nitems = fctl[0];
     if (blockIdx.x >= nitems) return;  // more workers than items: the rest leave without a dequeue
     for (;;) {
@@ -464,7 +482,7 @@ __global__ __launch_bounds__(kWave * kPixPerLane) void render_fwd_seg_kernel(
     float *__restrict__ out_invd, float *__restrict__ final_T, uint32_t *__restrict__ n_contrib,
     uint32_t *__restrict__ tile_work, const uint32_t *__restrict__ kdev, uint32_t cap,
     const uint32_t *__restrict__ sort_err, uint32_t *__restrict__ bwd_cnt, uint32_t *__restrict__ bwd_cls, int ntiles,
-    uint32_t seg_len, uint32_t *bin_base, uint32_t fseg_len, uint32_t *fctl) {
+    uint32_t seg_len, uint32_t *bin_base, uint32_t fseg_len, uint32_t *fctl, int wait_ready) {
     if (kdev && *kdev > cap) return;  // the point-list capacity is short: the host re-runs at K
     __shared__ float4 s_a[kPixPerLane][kWave];
     __shared__ float4 s_b[kPixPerLane][kWave];
@@ -473,7 +491,7 @@ __global__ __launch_bounds__(kWave * kPixPerLane) void render_fwd_seg_kernel(
     const int w = threadIdx.x >> 6;
     fwd_seg_worker(ranges, point_list, W, H, gx, rec, bg, out_color, out_invd, final_T, n_contrib, tile_work,
                    kdev ? *kdev : cap, sort_err, bwd_cnt, bwd_cls, ntiles, seg_len, fseg_len, bin_base, fctl, s_a[w],
-                   s_b[w], s_c[w], s_work, s_scalar);
+                   s_b[w], s_c[w], s_work, s_scalar, wait_ready != 0);
 }
 
 #ifndef GSR_FWD_SEG_INKERNEL
@@ -523,7 +541,7 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) GSR_FWD_ATTR void ren
                 fwd_seg_worker(ranges, point_list, W, H, gx, rec, bg, out_color, out_invd, final_T, n_contrib,
                                tile_work, kdev ? *kdev : cap, sort_err, bwd_cnt, bwd_cls, ntiles, seg_len, fseg_len,
                                bin_base, fctl, s_a[threadIdx.x >> 6], s_b[threadIdx.x >> 6], s_c[threadIdx.x >> 6],
-                               s_work, s_scalar);
+                               s_work, s_scalar, false);
                 return;
             }
             bidx -= (uint32_t)kFwdWorkers;
@@ -804,7 +822,8 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t *__rest
                                                           int T, int shift, uint32_t *__restrict__ order, const uint32_t *__restrict__ kdev, uint32_t cap,
                                                           uint32_t *__restrict__ zero_classes, uint32_t *__restrict__ fctl,
                                                           void *bin_base, uint32_t seg_len, uint32_t fseg_len,
-                                                          uint32_t fseg_min, uint32_t *__restrict__ host_tilelist) {
+                                                          uint32_t fseg_min, uint32_t *__restrict__ host_tilelist,
+                                                          uint32_t *fwd_ready) {
     // the forward order's launch also zeroes the backward class counters render_fwd fills
     if (zero_classes && threadIdx.x < kBwdClasses) zero_classes[threadIdx.x] = 0u;
     if (zero_classes && threadIdx.x == 0) zero_classes[kBwdSegCount] = 0u;
@@ -849,6 +868,11 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t *__rest
             fctl[1] = 0u;       // kFwdNextWord
         }
     }
+    if (fseg_len && fwd_ready) {
+        // the workers already wait: queue, tickets and flags released before the ready word
+        wg_release();
+        if (threadIdx.x == 0) __hip_atomic_store(fwd_ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     __syncthreads();
     if (threadIdx.x < 64) {  // exclusive scan of 256 counts, 4 per lane
         const int l = threadIdx.x;
@@ -871,11 +895,11 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t *__rest
 
 void launch_tile_order(const uint32_t *work, const uint2 *ranges, int T, int shift, uint32_t *order, hipStream_t s,
                        const uint32_t *kdev, uint32_t cap, uint32_t *zero_classes, uint32_t *fctl, void *bin_base,
-                       uint32_t seg_len, uint32_t fseg_len, uint32_t *host_tilelist) {
+                       uint32_t seg_len, uint32_t fseg_len, uint32_t *host_tilelist, uint32_t *fwd_ready) {
     if (T == 0) return;
     hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, s, work, ranges, T, shift, order, kdev, cap, zero_classes,
                        fctl, bin_base, seg_len, fctl ? fseg_len : 0u, fctl && fseg_len ? fseg_min_len(fseg_len) : 0u,
-                       host_tilelist);
+                       host_tilelist, fwd_ready);
 }
 
 // the worker pool's size: kFwdWorkers, or GSR_FWD_WORKERS from the environment (measurement A/B)
@@ -888,21 +912,44 @@ static int fwd_workers() {
     return n;
 }
 
+bool fwd_early_workers() {
+    static const bool on = [] {
+        const char *e = getenv("GSR_FWD_EARLY_WORKERS");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
+static void launch_workers(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
+                           const float *bg, float *out_color, float *out_invdepth, bool need_bwd, uint32_t seg_len,
+                           uint32_t fseg_len, hipStream_t ws, bool wait_ready) {
+    uint32_t *const bcnt = GSR_BWD_CLS && need_bwd ? is.bwd_cnt : nullptr;
+    hipLaunchKernelGGL(render_fwd_seg_kernel, dim3(fwd_workers()), dim3(kWave * kPixPerLane), 0, ws, is.ranges,
+                       bs.point_list, cam.W, cam.H, cam.gx, gs.rec, bg, out_color, out_invdepth, is.final_T,
+                       is.n_contrib, is.tile_work, bs.kdev, bs.cap, bs.kdev ? dsort_err_word(gs) : nullptr, bcnt,
+                       is.bwd_cls, cam.gx * cam.gy, seg_len, bs.point_list, fseg_len, is.bwd_cnt + kFwdItemsWord,
+                       wait_ready ? 1 : 0);
+}
+
+void launch_render_fwd_workers(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
+                               const float *bg, float *out_color, float *out_invdepth, bool need_bwd, uint32_t seg_len,
+                               uint32_t fseg_len, hipStream_t ws) {
+    if (cam.gx * cam.gy == 0 || !fseg_len || GSR_FWD_SUB != 1 || GSR_FWD_SEG_INKERNEL) return;
+    launch_workers(cam, gs, bs, is, bg, out_color, out_invdepth, need_bwd, seg_len, fseg_len, ws, true);
+}
+
 void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                        const float *bg, float *out_color, float *out_invdepth, hipStream_t s, bool need_bwd,
-                       bool sb_order, uint32_t seg_len, uint32_t fseg_len, hipStream_t worker_stream) {
+                       bool sb_order, uint32_t seg_len, uint32_t fseg_len, hipStream_t worker_stream,
+                       bool workers_launched) {
     const int T = cam.gx * cam.gy;
     if (T == 0) return;
     const SBGrid &sg = gs.sb;
     if (sb_order || GSR_FWD_SUB != 1) fseg_len = 0;
     const int grid = (sb_order ? sg.nsb << (2 * sg.shift) : T) + (GSR_FWD_SEG_INKERNEL && fseg_len ? kFwdWorkers : 0);
-    uint32_t *const bcnt = GSR_BWD_CLS && need_bwd ? is.bwd_cnt : nullptr;
-    if (fseg_len && !GSR_FWD_SEG_INKERNEL)
-        hipLaunchKernelGGL(render_fwd_seg_kernel, dim3(fwd_workers()), dim3(kWave * kPixPerLane), 0,
-                           worker_stream ? worker_stream : s, is.ranges,
-                           bs.point_list, cam.W, cam.H, cam.gx, gs.rec, bg, out_color, out_invdepth, is.final_T,
-                           is.n_contrib, is.tile_work, bs.kdev, bs.cap, bs.kdev ? dsort_err_word(gs) : nullptr, bcnt,
-                           is.bwd_cls, T, seg_len, bs.point_list, fseg_len, is.bwd_cnt + kFwdItemsWord);
+    if (fseg_len && !GSR_FWD_SEG_INKERNEL && !workers_launched)
+        launch_workers(cam, gs, bs, is, bg, out_color, out_invdepth, need_bwd, seg_len, fseg_len,
+                       worker_stream ? worker_stream : s, false);
     // launch order: is.tile_ids (rasterizer.hip, by list length)
 #define GSR_FWD_LAUNCH(K, NT)                                                                                       \
     hipLaunchKernelGGL(K, dim3(grid), dim3(NT), 0, s, is.ranges, bs.point_list, cam.W, cam.H, cam.gx, gs.rec, bg,   \

@@ -27,7 +27,8 @@ def main():
     ap.add_argument("--views", type=int, default=8)
     ap.add_argument("--size", type=int, default=1536)
     ap.add_argument("--segs", default="0:0,0:512,4096:512,8192:512",
-                    help="forward:backward segment lengths to time (A/B), comma separated")
+                    help="forward:backward[:fwd split minimum] segment lengths to time (A/B), comma separated")
+    ap.add_argument("--no-gate", action="store_true", help="arm the splits on every frame (gsr_set_split_gate off)")
     ap.add_argument("--reps", type=int, default=10)
     a = ap.parse_args()
     import torch
@@ -36,6 +37,8 @@ def main():
     from gs_train.native_step import NativeTrainStep
     from helpers import image_layout, view
     dev = torch.device("cuda:0")
+    if a.no_gate:
+        _C.set_split_gate(False)
     torch.manual_seed(0)
     ts, info = street_chunk(NativeTrainStep, W=a.size, H=a.size, iterations=30_000, device=dev)
     tc = TrainChunk(ts, ChunkSchedule())
@@ -117,8 +120,10 @@ def time_segments(g, c, H, W, segs, reps):
 
     rel = lambda ga, gb: max(float((a - b).norm() / b.norm().clamp_min(1e-30)) for a, b in zip(ga, gb))
     for cfg in segs:
-        fL, L = (int(x) for x in cfg.split(":"))
+        parts = [int(x) for x in cfg.split(":")]
+        fL, L = parts[:2]
         prev, fprev = _C.set_bwd_segment(L), _C.set_fwd_segment(fL)
+        mprev = _C.set_fwd_split_min(parts[2] if len(parts) > 2 else 0)
         st_all, wall, last2 = [], [], []
         for r in range(reps + 2):
             xs = [t.detach().clone().requires_grad_(True) for t in
@@ -148,6 +153,7 @@ def time_segments(g, c, H, W, segs, reps):
             ref_det = gd
         _C.set_bwd_segment(prev)
         _C.set_fwd_segment(fprev)
+        _C.set_fwd_split_min(mprev)
         med = lambda k: float(np.median([s_[k] for s_ in st_all]))
         # grad errors (max over tensors of relative L2): atomic vs the first length's atomic run, the
         # run-to-run atomic noise at this length, and record mode (bitwise ordered sums) vs the first
