@@ -912,12 +912,9 @@ static int fwd_workers() {
     return n;
 }
 
-bool fwd_early_workers() {
-    static const bool on = [] {
-        const char *e = getenv("GSR_FWD_EARLY_WORKERS");
-        return e && e[0] == '1';
-    }();
-    return on;
+bool fwd_early_workers() {  // read per frame, so a test can switch it
+    const char *e = getenv("GSR_FWD_EARLY_WORKERS");
+    return e && e[0] == '1';
 }
 
 static void launch_workers(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,

@@ -251,6 +251,28 @@ def test_fwd_segments_deterministic_and_repeatable():
             np.testing.assert_array_equal(v, h2["grads"][k], err_msg=k)
 
 
+@pytest.mark.parametrize("c", [FWD_CASES[0], FWD_CASES[2]], ids=[FWD_CASES[0]["name"], FWD_CASES[2]["name"]])
+def test_fwd_workers_launched_ahead_equal_beside(c, monkeypatch):
+    """GSR_FWD_EARLY_WORKERS=1 launches the worker pool before tile_order (waiting for its queue
+    release); the items, their order of sums and so the frame are those of the pool launched beside
+    render_fwd: record mode bitwise equal, and the oracle's bars."""
+    s = seg_scene(c)
+    dcol, dinv = upstream_grads(c)
+    st, g = run_oracle(s, c, dcol, dinv)
+    out = {}
+    for e in ("1", "0", "1"):
+        monkeypatch.setenv("GSR_FWD_EARLY_WORKERS", e)
+        with deterministic(), fwd_segment(4096), bwd_segment(512):
+            out.setdefault(e, []).append(run_hip(s, c, dcol, dinv))
+    fwd_compare(c, st, g, out["1"][0])
+    for h in (out["0"][0], out["1"][1]):
+        np.testing.assert_array_equal(out["1"][0]["color"], h["color"])
+        np.testing.assert_array_equal(out["1"][0]["state"]["n_contrib"], h["state"]["n_contrib"])
+        for k, v in out["1"][0]["grads"].items():
+            if v is not None:
+                np.testing.assert_array_equal(v, h["grads"][k], err_msg=k)
+
+
 def test_fwd_segments_no_backward_forward():
     """A no-grad forward (no backward state) with the forward split: same image."""
     import torch
