@@ -505,7 +505,9 @@ constexpr uint32_t kMinFwdSeg = 4096;
 // a tile is split when its list is longer than fseg_min (kFsegFactor segments by default: a tile
 // of a few segments whose pixels saturate early gains little)
 #ifndef GSR_FSEG_FACTOR
-#define GSR_FSEG_FACTOR 16  // config-3 A/B (r04v): 4 -> 58.8 s, 8 -> 58.6, 16 -> 58.1, forward split off -> 59.2
+// config-3 with the workers ahead of tile_order (r04zc): 4 -> 57.3 / 56.9 s, 16 -> 57.0 s (workers beside
+// render_fwd: 58.5 s); street views with 60k-110k lists: 4 -> 0.81 ms render_fwd, 16 -> 2.96 ms (r04zb)
+#define GSR_FSEG_FACTOR 4
 #endif
 __host__ __device__ __forceinline__ bool fseg_splits(uint32_t len, uint32_t fseg_min) { return fseg_min && len > fseg_min; }
 constexpr int kFwdWorkers = 256;

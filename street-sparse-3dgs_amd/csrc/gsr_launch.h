@@ -123,7 +123,7 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
 void launch_render_fwd_workers(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                                const float *bg, float *out_color, float *out_invdepth, bool need_bwd, uint32_t seg_len,
                                uint32_t fseg_len, hipStream_t ws);
-// GSR_FWD_EARLY_WORKERS=1: launch_render_fwd_workers before tile_order (default: beside render_fwd)
+// GSR_FWD_EARLY_WORKERS (default 1): launch_render_fwd_workers before tile_order; 0: beside render_fwd
 bool fwd_early_workers();
 // seg_len != 0: the backward's heavy tiles are cut into segments of seg_len list positions
 // (gsr_set_bwd_segment; the backward must get the value its forward was made with)

@@ -914,7 +914,7 @@ static int fwd_workers() {
 
 bool fwd_early_workers() {  // read per frame, so a test can switch it
     const char *e = getenv("GSR_FWD_EARLY_WORKERS");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
 }
 
 static void launch_workers(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
