@@ -493,8 +493,8 @@ inline int64_t bwd_grid(int T, int64_t K, uint32_t L) { return (int64_t)T + (L ?
 __host__ __device__ __forceinline__ size_t align256(size_t b) { return (b + 255) / 256 * 256; }
 
 // Forward segments (gsr_set_fwd_segment): a tile whose list is longer than fseg_min_len(Lf) is
-// blended as ceil(len / Lf) work items by render_fwd_seg_kernel's kFwdWorkers workgroups (an item
-// queue tile_order fills), launched beside render_fwd on a side stream.  Item s first multiplies
+// blended as ceil(len / Lf) work items by render_fwd_seg_kernel's kFwdPoolWorkers workgroups (an item
+// queue tile_order fills), launched ahead of tile_order on a side stream.  Item s first multiplies
 // out (1 - alpha) over its positions (the pixels' transmittance through the segment), publishes it,
 // waits for its predecessors' and takes their product in segment order, then blends its positions
 // from that transmittance with the usual stop rule; the tile's last item to finish sums the items' colours in order and writes the
@@ -510,7 +510,10 @@ constexpr uint32_t kMinFwdSeg = 4096;
 #define GSR_FSEG_FACTOR 4
 #endif
 __host__ __device__ __forceinline__ bool fseg_splits(uint32_t len, uint32_t fseg_min) { return fseg_min && len > fseg_min; }
-constexpr int kFwdWorkers = 256;
+constexpr int kFwdWorkers = 256;      // the in-kernel variant's pool (GSR_FWD_SEG_INKERNEL)
+// render_fwd_seg_kernel's pool, launched ahead of tile_order: street views with 300k+ lists 1.40 /
+// 1.59 ms render_fwd at 256, 1.24 / 1.28 at 512, 1.24 / 1.27 at 1024 (r04zd)
+constexpr int kFwdPoolWorkers = 512;
 constexpr int kFwdPartials = 6;  // r, g, b, inverse depth, T at the end, last contributor | stop << 31
 // bwd_cnt's words past the backward's: the item count tile_order wrote, the queue's next item,
 // and (workers launched before tile_order) the queue-ready flag tile_order releases

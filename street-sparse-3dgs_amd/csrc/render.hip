@@ -474,7 +474,7 @@ __device__ void fwd_seg_worker(const uint2 *__restrict__ ranges, const uint32_t 
     }
 }
 
-// Forward segments' worker pool: kFwdWorkers workgroups, launched beside render_fwd (which skips
+// Forward segments' worker pool: kFwdPoolWorkers workgroups, launched beside render_fwd (which skips
 // the split tiles) on a side stream, until the item queue is empty.
 __global__ __launch_bounds__(kWave * kPixPerLane) void render_fwd_seg_kernel(
     const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list, int W, int H, int gx,
@@ -902,12 +902,12 @@ void launch_tile_order(const uint32_t *work, const uint2 *ranges, int T, int shi
                        host_tilelist, fwd_ready);
 }
 
-// the worker pool's size: kFwdWorkers, or GSR_FWD_WORKERS from the environment (measurement A/B)
+// the worker pool's size: kFwdPoolWorkers, or GSR_FWD_WORKERS from the environment (measurement A/B)
 static int fwd_workers() {
     static const int n = [] {
         const char *e = getenv("GSR_FWD_WORKERS");
         const int v = e ? atoi(e) : 0;
-        return v > 0 ? v : kFwdWorkers;
+        return v > 0 ? v : kFwdPoolWorkers;
     }();
     return n;
 }
