@@ -515,9 +515,8 @@ constexpr int kFwdWorkers = 256;      // the in-kernel variant's pool (GSR_FWD_S
 // 1.59 ms render_fwd at 256, 1.24 / 1.28 at 512, 1.24 / 1.27 at 1024 (r04zd)
 constexpr int kFwdPoolWorkers = 512;
 constexpr int kFwdPartials = 6;  // r, g, b, inverse depth, T at the end, last contributor | stop << 31
-// bwd_cnt's words past the backward's: the item count tile_order wrote, the queue's next item,
-// and (workers launched before tile_order) the queue-ready flag tile_order releases
-constexpr int kFwdItemsWord = kBwdSegCount + 1, kFwdNextWord = kBwdSegCount + 2, kFwdReadyWord = kBwdSegCount + 3;
+// bwd_cnt's words past the backward's: the item count tile_order wrote, the queue's next item
+constexpr int kFwdItemsWord = kBwdSegCount + 1, kFwdNextWord = kBwdSegCount + 2;
 struct FwdSegLayout {
     uint32_t *items, *tickets, *flags, *nc;
     float *agg;  // per item x 256 pixels: the transmittance through the segment

@@ -73,6 +73,8 @@ uint32_t *dsort_aux_word(const GeomState &gs);
 // local-sort frames: the longest SB list (sb_colscan); the head words (tickets, counters, K, ...)
 // a frame re-run through the global sort must zero again
 uint32_t *dsort_maxsb_word(const GeomState &gs);
+// the forward split's queue-ready word (zeroed with the control words by every frame's preprocess)
+uint32_t *dsort_fwdready_word(const GeomState &gs);
 int dsort_head_words();
 // binning.hip: per-tile lists (two stable counting levels).  index_order: level 1 over the
 // Gaussians in index order (local sort: sb_sort_bin orders each SB list by depth in LDS); else over
@@ -118,11 +120,11 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
                        hipStream_t worker_stream = nullptr, bool workers_launched = false);
 // Forward segments' worker pool launched ahead of tile_order (on a side stream that has waited for
 // the binning and the colour pass): its workgroups are resident before render_fwd's grid fills the
-// CUs and start on the queue as soon as tile_order releases bwd_cnt[kFwdReadyWord] (zeroed by the
-// caller on the main stream first).
+// CUs and start on the queue as soon as tile_order (given the same word) releases `ready`
+// (dsort_fwdready_word: zero since the frame's preprocess).
 void launch_render_fwd_workers(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                                const float *bg, float *out_color, float *out_invdepth, bool need_bwd, uint32_t seg_len,
-                               uint32_t fseg_len, hipStream_t ws);
+                               uint32_t fseg_len, hipStream_t ws, const uint32_t *ready);
 // GSR_FWD_EARLY_WORKERS (default 1): launch_render_fwd_workers before tile_order; 0: beside render_fwd
 bool fwd_early_workers();
 // seg_len != 0: the backward's heavy tiles are cut into segments of seg_len list positions

@@ -810,13 +810,11 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
         bool early = false;
         if (fseg_used && !sb_order && fwd_early_workers() && !fwd_segments_in_kernel() &&
             side_stream(s, &ws, &wf, &wj, 1) && ws != s) {
-            uint32_t *ready = is.bwd_cnt + kFwdReadyWord;
-            if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ready), 0, 1, s) != hipSuccess ||
-                hipEventRecord(wf, s) != hipSuccess || hipStreamWaitEvent(ws, wf, 0) != hipSuccess ||
+            if (hipEventRecord(wf, s) != hipSuccess || hipStreamWaitEvent(ws, wf, 0) != hipSuccess ||
                 (split && !GSR_COLOR_SERIAL && !joined && hipStreamWaitEvent(ws, join, 0) != hipSuccess))
                 return fail(GSR_ERR_DEVICE, "side stream fork failed");
             launch_render_fwd_workers(cam, gs, bs, is, background, out_color, out_invdepth, need_bwd, seg_used,
-                                      fseg_used, ws);
+                                      fseg_used, ws, dsort_fwdready_word(gs));
             if (hipEventRecord(wj, ws) != hipSuccess) return fail(GSR_ERR_DEVICE, "side stream join record failed");
             early = true;
         }
@@ -826,7 +824,7 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
             launch_tile_order(nullptr, is.ranges, T, 4, is.tile_ids, s, bs.kdev, bs.cap,
                               GSR_BWD_CLS && need_bwd ? is.bwd_cnt : nullptr, is.bwd_cnt + kFwdItemsWord, bs.point_list,
                               seg_used, fseg_used, P > 0 ? g_pinned_dev + kHostTileList : nullptr,
-                              early ? is.bwd_cnt + kFwdReadyWord : nullptr);
+                              early ? dsort_fwdready_word(gs) : nullptr);
         }
         if ((r = check("tile order", debug, s))) return r;
         if (split && !GSR_COLOR_SERIAL && !joined) {

@@ -307,16 +307,16 @@ __device__ void fwd_seg_worker(const uint2 *__restrict__ ranges, const uint32_t 
                                uint32_t *__restrict__ tile_work, uint32_t kf, const uint32_t *__restrict__ sort_err,
                                uint32_t *__restrict__ bwd_cnt, uint32_t *__restrict__ bwd_cls, int ntiles, uint32_t seg_len,
                                uint32_t fseg_len, uint32_t *bin_base, uint32_t *fctl, float4 *sa, float4 *sb,
-                               float4 *sc, uint32_t *s_work, uint32_t *s_scalar, bool wait_ready) {
+                               float4 *sc, uint32_t *s_work, uint32_t *s_scalar, const uint32_t *ready) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const FwdSegLayout f = fseg_layout(bin_base, kf, seg_len, fseg_len);
     float *ck = seg_len && bwd_cnt ? reinterpret_cast<float *>(reinterpret_cast<char *>(bin_base) + ck_offset(kf)) : nullptr;
-    if (wait_ready) {
+    if (ready) {
         // launched ahead of tile_order: wait for its release of the queue (a bounded spin; never
         // expected to give up -- the workers then leave and the split tiles keep no pixels)
         if (threadIdx.x == 0) {
             uint32_t ok = 1u, spins = 0;
-            while (!__hip_atomic_load(fctl + (kFwdReadyWord - kFwdItemsWord), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            while (!__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
                 if (++spins > (1u << 22)) {
                     ok = 0u;
                     break;
@@ -482,7 +482,7 @@ __global__ __launch_bounds__(kWave * kPixPerLane) void render_fwd_seg_kernel(
     float *__restrict__ out_invd, float *__restrict__ final_T, uint32_t *__restrict__ n_contrib,
     uint32_t *__restrict__ tile_work, const uint32_t *__restrict__ kdev, uint32_t cap,
     const uint32_t *__restrict__ sort_err, uint32_t *__restrict__ bwd_cnt, uint32_t *__restrict__ bwd_cls, int ntiles,
-    uint32_t seg_len, uint32_t *bin_base, uint32_t fseg_len, uint32_t *fctl, int wait_ready) {
+    uint32_t seg_len, uint32_t *bin_base, uint32_t fseg_len, uint32_t *fctl, const uint32_t *ready) {
     if (kdev && *kdev > cap) return;  // the point-list capacity is short: the host re-runs at K
     __shared__ float4 s_a[kPixPerLane][kWave];
     __shared__ float4 s_b[kPixPerLane][kWave];
@@ -491,7 +491,7 @@ __global__ __launch_bounds__(kWave * kPixPerLane) void render_fwd_seg_kernel(
     const int w = threadIdx.x >> 6;
     fwd_seg_worker(ranges, point_list, W, H, gx, rec, bg, out_color, out_invd, final_T, n_contrib, tile_work,
                    kdev ? *kdev : cap, sort_err, bwd_cnt, bwd_cls, ntiles, seg_len, fseg_len, bin_base, fctl, s_a[w],
-                   s_b[w], s_c[w], s_work, s_scalar, wait_ready != 0);
+                   s_b[w], s_c[w], s_work, s_scalar, ready);
 }
 
 #ifndef GSR_FWD_SEG_INKERNEL
@@ -541,7 +541,7 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) GSR_FWD_ATTR void ren
                 fwd_seg_worker(ranges, point_list, W, H, gx, rec, bg, out_color, out_invd, final_T, n_contrib,
                                tile_work, kdev ? *kdev : cap, sort_err, bwd_cnt, bwd_cls, ntiles, seg_len, fseg_len,
                                bin_base, fctl, s_a[threadIdx.x >> 6], s_b[threadIdx.x >> 6], s_c[threadIdx.x >> 6],
-                               s_work, s_scalar, false);
+                               s_work, s_scalar, nullptr);
                 return;
             }
             bidx -= (uint32_t)kFwdWorkers;
@@ -919,20 +919,20 @@ bool fwd_early_workers() {  // read per frame, so a test can switch it
 
 static void launch_workers(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                            const float *bg, float *out_color, float *out_invdepth, bool need_bwd, uint32_t seg_len,
-                           uint32_t fseg_len, hipStream_t ws, bool wait_ready) {
+                           uint32_t fseg_len, hipStream_t ws, const uint32_t *ready) {
     uint32_t *const bcnt = GSR_BWD_CLS && need_bwd ? is.bwd_cnt : nullptr;
     hipLaunchKernelGGL(render_fwd_seg_kernel, dim3(fwd_workers()), dim3(kWave * kPixPerLane), 0, ws, is.ranges,
                        bs.point_list, cam.W, cam.H, cam.gx, gs.rec, bg, out_color, out_invdepth, is.final_T,
                        is.n_contrib, is.tile_work, bs.kdev, bs.cap, bs.kdev ? dsort_err_word(gs) : nullptr, bcnt,
                        is.bwd_cls, cam.gx * cam.gy, seg_len, bs.point_list, fseg_len, is.bwd_cnt + kFwdItemsWord,
-                       wait_ready ? 1 : 0);
+                       ready);
 }
 
 void launch_render_fwd_workers(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                                const float *bg, float *out_color, float *out_invdepth, bool need_bwd, uint32_t seg_len,
-                               uint32_t fseg_len, hipStream_t ws) {
+                               uint32_t fseg_len, hipStream_t ws, const uint32_t *ready) {
     if (cam.gx * cam.gy == 0 || !fseg_len || GSR_FWD_SUB != 1 || GSR_FWD_SEG_INKERNEL) return;
-    launch_workers(cam, gs, bs, is, bg, out_color, out_invdepth, need_bwd, seg_len, fseg_len, ws, true);
+    launch_workers(cam, gs, bs, is, bg, out_color, out_invdepth, need_bwd, seg_len, fseg_len, ws, ready);
 }
 
 void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
@@ -946,7 +946,7 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
     const int grid = (sb_order ? sg.nsb << (2 * sg.shift) : T) + (GSR_FWD_SEG_INKERNEL && fseg_len ? kFwdWorkers : 0);
     if (fseg_len && !GSR_FWD_SEG_INKERNEL && !workers_launched)
         launch_workers(cam, gs, bs, is, bg, out_color, out_invdepth, need_bwd, seg_len, fseg_len,
-                       worker_stream ? worker_stream : s, false);
+                       worker_stream ? worker_stream : s, nullptr);
     // launch order: is.tile_ids (rasterizer.hip, by list length)
 #define GSR_FWD_LAUNCH(K, NT)                                                                                       \
     hipLaunchKernelGGL(K, dim3(grid), dim3(NT), 0, s, is.ranges, bs.point_list, cam.W, cam.H, cam.gx, gs.rec, bg,   \
