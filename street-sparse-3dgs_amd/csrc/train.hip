@@ -164,6 +164,7 @@ __device__ __forceinline__ void vpass_tile(const float *hs, int pitch, int plane
     }
 }
 
+template <int kThreads = kLossThreads>
 __device__ __forceinline__ float block_sum(float v, float *red) {
     v = wave_sum(v);
     const int wv = threadIdx.x >> 6;
@@ -172,7 +173,7 @@ __device__ __forceinline__ float block_sum(float v, float *red) {
     __syncthreads();
     float s = 0.f;
 #pragma unroll
-    for (int k = 0; k < kLossThreads / 64; k++) s += red[k];
+    for (int k = 0; k < kThreads / 64; k++) s += red[k];
     return s;
 }
 
@@ -429,8 +430,16 @@ constexpr int kStW = 64;
 #ifndef GSR_SSIM_SEG_H
 #define GSR_SSIM_SEG_H 0  // rows per strip; 0: chosen per image (stream_seg)
 #endif
-constexpr int kStep = 4;
-constexpr int kRing = 16;
+// GSR_SSIM_STEP: rows per step (4: 256 threads, 16-row rings, 40 KiB, four workgroups per CU; 8: 512
+// threads, 32-row rings, 79 KiB, two per CU -- half the barriers per row and a thinner strip halo)
+#ifndef GSR_SSIM_STEP
+#define GSR_SSIM_STEP 4
+#endif
+static_assert(GSR_SSIM_STEP == 4 || GSR_SSIM_STEP == 8, "GSR_SSIM_STEP: 4 or 8");
+constexpr int kStep = GSR_SSIM_STEP;
+constexpr int kRing = kStep == 4 ? 16 : 32;
+constexpr int kStThreads = kStep * 64;
+constexpr int kStPerCU = kStep == 4 ? 4 : 2;  // resident workgroups per CU (LDS)
 #ifndef GSR_SSIM_PF
 #define GSR_SSIM_PF 1  // steps of input rows in flight; 2 measured no faster (r03j: train step 0.951-0.958 vs 0.949-0.958 ms)
 #endif
@@ -441,10 +450,10 @@ constexpr int kStIC = kStW + 4 * kR, kStMC = kStW + 2 * kR;  // 84 input, 74 SSI
 constexpr int kStIP = kStIC, kStMP = kStMC, kStTP = kStW;
 static_assert(kStIP % 2 == 0 && kStMP % 2 == 0 && kStTP % 2 == 0, "float2 rows");
 constexpr int kStInElems = kStep * kStIC;
-constexpr int kStInPer = (kStInElems + kLossThreads - 1) / kLossThreads;
+constexpr int kStInPer = (kStInElems + kStThreads - 1) / kStThreads;
 constexpr int kStHSeg = kStMC / 2;  // horizontal-moment tasks per row (two columns each)
-static_assert(kStMC % 2 == 0 && kStep * kStHSeg <= kLossThreads, "one horizontal-moment task per thread");
-static_assert(kStep * 64 == kLossThreads && kStep % 2 == 0 && 2 * kStMC <= kLossThreads, "one task per thread");
+static_assert(kStMC % 2 == 0 && kStep * kStHSeg <= kStThreads, "one horizontal-moment task per thread");
+static_assert(kStep % 2 == 0 && (kStep / 2) * kStMC <= kStThreads, "one task per thread");
 static_assert(kRing >= 2 * kR + 1 + kStep - 1 && (kRing & (kRing - 1)) == 0, "ring holds a step's window rows");
 
 // Workgroup barrier for LDS hand-offs only: drains this wave's LDS operations but not its global
@@ -452,7 +461,7 @@ static_assert(kRing >= 2 * kR + 1 + kStep - 1 && (kRing & (kRing - 1)) == 0, "ri
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 template <bool kMap>
-__global__ __launch_bounds__(kLossThreads) void l1_ssim_stream_kernel(const float *__restrict__ x,
+__global__ __launch_bounds__(kStThreads) void l1_ssim_stream_kernel(const float *__restrict__ x,
                                                                        const float *__restrict__ y, int H, int W,
                                                                        Window win, const float *__restrict__ dout,
                                                                        float inv_n, float *__restrict__ dx,
@@ -469,7 +478,7 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_stream_kernel(const floa
     __shared__ __attribute__((aligned(16))) float s_h3[3][kRing][kStTP];
     auto &s_in = s_u.in;
     auto &s_abc = s_u.abc;
-    __shared__ float s_red[8];
+    __shared__ float s_red[2 * kStThreads / 64];
     const size_t plane_off = (size_t)blockIdx.z * H * W;
     x += plane_off;
     y += plane_off;
@@ -494,7 +503,7 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_stream_kernel(const floa
     const auto fetch = [&](InRows &f, int p0) {
 #pragma unroll
         for (int k = 0; k < kStInPer; k++) {
-            const int e = min(tid + k * kLossThreads, kStInElems - 1);
+            const int e = min(tid + k * kStThreads, kStInElems - 1);
             const int r = e / kStIC, c = e - r * kStIC;
             const int gy = p0 + r, gx = cx - 2 * kR + c;
             f.pin[k] = gy >= 0 && gy < H && gx >= 0 && gx < W;
@@ -513,7 +522,7 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_stream_kernel(const floa
         // (1) stage input rows p0 .. p0 + kStep - 1 and start loading those kPf steps ahead
 #pragma unroll
         for (int k = 0; k < kStInPer; k++) {
-            const int e = tid + k * kLossThreads;
+            const int e = tid + k * kStThreads;
             if (e < kStInElems) {
                 const int r = e / kStIC, c = e - r * kStIC;
                 s_in[0][r][c] = cur.pin[k] ? cur.px[k] : 0.f;
@@ -521,7 +530,7 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_stream_kernel(const floa
             }
         }
         // (5)'s output pixels: rows orow, orow + 1 of column ocol (tasks tid < 128)
-        const int orow = p0 + 2 * ((tid >> 6) & 1) - 2 * kR, ocol = cx + (tid & 63);
+        const int orow = p0 + 2 * ((tid >> 6) % (kStep / 2)) - 2 * kR, ocol = cx + (tid & 63);
         float xv[2], yv[2];
 #pragma unroll
         for (int k = 0; k < 2; k++) {
@@ -573,7 +582,7 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_stream_kernel(const floa
 
         // (3) vertical moments and dS/d(moment) at map rows p0 - R .. p0 + kStep - 1 - R, two rows
         // per task.  Rows above r0 - R read ring rows never written; (5) never reads them.
-        if (tid < 2 * kStMC) {
+        if (tid < (kStep / 2) * kStMC) {
             const int pr = tid / kStMC, c = tid - pr * kStMC;
             const int qa = p0 + 2 * pr - kR;
             float m[5][2];
@@ -681,8 +690,8 @@ __global__ __launch_bounds__(kLossThreads) void l1_ssim_stream_kernel(const floa
         for (int st = 0; st < nsteps; st++) step(st, fa);
     }
     if (kMap) {
-        l1 = block_sum(l1, s_red);
-        ss = block_sum(ss, s_red + 4);
+        l1 = block_sum<kStThreads>(l1, s_red);
+        ss = block_sum<kStThreads>(ss, s_red + kStThreads / 64);
         if (tid == 0) {
             const int b = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
             partials[b] = make_float2(l1, ss);
@@ -1362,7 +1371,7 @@ int stream_seg(int C, int H, int W) {
         n = cus[dev];
     }
     const int cols = (W + kStW - 1) / kStW;
-    const int strips = std::max(1, 4 * n / std::max(1, C * cols));
+    const int strips = std::max(1, kStPerCU * n / std::max(1, C * cols));
     int seg = (H + strips - 1) / strips;
     seg = (seg + kStep - 1) / kStep * kStep;
     return std::max(seg, 64);
@@ -1743,7 +1752,7 @@ int step_loss_forward(const float *img, const float *gt, int H, int W, double la
         hipLaunchKernelGGL(l1_ssim_grad_kernel<true>, g, dim3(kLossThreads), kBwdLds, s, img, gt, H, W, ssim_window(),
                            nullptr, 0.f, gmap, pp);
     else
-        hipLaunchKernelGGL(l1_ssim_stream_kernel<true>, g, dim3(kLossThreads), 0, s, img, gt, H, W, ssim_window(),
+        hipLaunchKernelGGL(l1_ssim_stream_kernel<true>, g, dim3(kStThreads), 0, s, img, gt, H, W, ssim_window(),
                            nullptr, 0.f, gmap, pp, stream_seg(C, H, W),
                            PhotoOut{one, alpha, (float)(1.0 / (double)(3 * (int64_t)H * W)), (float)(1.0 - lambda_dssim),
                                     (float)lambda_dssim});
@@ -1886,7 +1895,7 @@ int gsr_l1_ssim_backward(const float *img, const float *gt, int C, int H, int W,
         hipLaunchKernelGGL(l1_ssim_grad_kernel<false>, loss_grid(C, H, W), dim3(kLossThreads), kBwdLds, s, img, gt, H,
                            W, ssim_window(), dL_dout, inv_n, dL_dimg, nullptr);
     else
-        hipLaunchKernelGGL(l1_ssim_stream_kernel<false>, stream_grid(C, H, W), dim3(kLossThreads), 0, s, img, gt, H,
+        hipLaunchKernelGGL(l1_ssim_stream_kernel<false>, stream_grid(C, H, W), dim3(kStThreads), 0, s, img, gt, H,
                            W, ssim_window(), dL_dout, inv_n, dL_dimg, nullptr, stream_seg(C, H, W), PhotoOut{});
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
@@ -1917,7 +1926,7 @@ int forward_with_map(const char *who, const float *img, const float *gt, int C, 
         hipLaunchKernelGGL(l1_ssim_grad_kernel<true>, g, dim3(kLossThreads), kBwdLds, s, img, gt, H, W, ssim_window(),
                            nullptr, 0.f, ssim_grad_map, part);
     else
-        hipLaunchKernelGGL(l1_ssim_stream_kernel<true>, g, dim3(kLossThreads), 0, s, img, gt, H, W, ssim_window(),
+        hipLaunchKernelGGL(l1_ssim_stream_kernel<true>, g, dim3(kStThreads), 0, s, img, gt, H, W, ssim_window(),
                            nullptr, 0.f, ssim_grad_map, part, stream_seg(C, H, W), PhotoOut{});
     hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(1024), 0, s, part, nb, 1.0 / ((double)C * H * W), out,
                        w_l1, w_ssim);
