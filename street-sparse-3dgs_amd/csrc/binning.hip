@@ -298,14 +298,16 @@ __global__ __launch_bounds__(kColThreads) void sb_colscan_kernel(SBGrid sg, uint
         // the longest SB list: for the split gate's hint (host_sblist), and on local-sort frames K
         // (= the instance total) and that maximum for the kernels and the host.  The host's K word
         // is stored last (the host reads the others once it is set).
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) mg = max(mg, (uint32_t)__shfl_xor((int)mg, o, 64));
+        mg = wave_max_u32(mg);  // DPP and row / half swaps: no LDS round trips
         __syncthreads();
         if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = mg;
         __syncthreads();
         if (threadIdx.x == 0) {
             for (int k = 1; k < kColThreads / 64; k++) mg = max(mg, wsum[k]);
-            if (host_sblist) __hip_atomic_store(host_sblist, mg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (host_sblist) {
+                if (GSR_HOST_WORDS == 2) *host_sblist = mg;  // a device word render_fwd forwards
+                else __hip_atomic_store(host_sblist, mg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
         }
     }
     if (fw.dev_K) {

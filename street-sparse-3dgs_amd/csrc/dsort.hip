@@ -51,6 +51,7 @@ constexpr int kCtlErr = 6;     // set when a bounded spin gave up (never expecte
 constexpr int kCtlAux = 7;     // per-frame counter lent to the binning (sb_colscan's last-workgroup count)
 constexpr int kCtlMaxSB = 8;   // local-sort frames: the longest SB list (sb_colscan)
 constexpr int kCtlFwdReady = 9;  // the forward split's queue released by tile_order (workers launched ahead)
+constexpr int kCtlLongest = 10;  // [2]: the frame's longest tile list and superblock list (split gate hints)
 constexpr int kCtlHead = 16;
 // The upsweep runs at most kUpMax workgroups, each over tpb consecutive tiles, so that a pass
 // reduces at most kUpMax histogram rows (kUpMax / 4 loads per thread, all in flight at once).
@@ -479,6 +480,7 @@ uint32_t *dsort_err_word(const GeomState &gs) { return gs.ctrl + kCtlErr; }
 uint32_t *dsort_aux_word(const GeomState &gs) { return gs.ctrl + kCtlAux; }
 uint32_t *dsort_maxsb_word(const GeomState &gs) { return gs.ctrl + kCtlMaxSB; }
 uint32_t *dsort_fwdready_word(const GeomState &gs) { return gs.ctrl + kCtlFwdReady; }
+uint32_t *dsort_longest_words(const GeomState &gs) { return gs.ctrl + kCtlLongest; }
 int dsort_head_words() { return kCtlHead; }
 
 }  // namespace gsr

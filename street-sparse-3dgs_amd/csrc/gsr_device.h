@@ -599,6 +599,9 @@ __host__ __device__ __forceinline__ const uint32_t *drect4_of(const GeomState &g
 // the pinned host words the host waits on.  host[kHostK] is stored last.
 // kHostSBList / kHostTileList: every frame's longest superblock list (sb_colscan) and longest tile
 // list (the forward's tile_order), read by the host as the split gate's hint (rasterizer.hip)
+#ifndef GSR_HOST_WORDS
+#define GSR_HOST_WORDS 1  // split gate hints: 1 stored by tile_order / sb_colscan, 2 forwarded by render_fwd, 0 none (A/B)
+#endif
 enum HostWord { kHostK = 0, kHostErr = 1, kHostMaxSB = 2, kHostP1 = 3, kHostSBList = 4, kHostTileList = 5, kHostWords = 6 };
 struct FrameWords {
     uint32_t *dev_K;      // nullptr: global-sort frame (dsort publishes K)

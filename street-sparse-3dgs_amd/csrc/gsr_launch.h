@@ -75,6 +75,9 @@ uint32_t *dsort_aux_word(const GeomState &gs);
 uint32_t *dsort_maxsb_word(const GeomState &gs);
 // the forward split's queue-ready word (zeroed with the control words by every frame's preprocess)
 uint32_t *dsort_fwdready_word(const GeomState &gs);
+// the frame's longest tile list and superblock list, [2] (zeroed by the preprocess; render_fwd copies
+// them to the pinned host words)
+uint32_t *dsort_longest_words(const GeomState &gs);
 int dsort_head_words();
 // binning.hip: per-tile lists (two stable counting levels).  index_order: level 1 over the
 // Gaussians in index order (local sort: sb_sort_bin orders each SB list by depth in LDS); else over
@@ -117,7 +120,8 @@ struct ZeroRows {
 void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                        const float *bg, float *out_color, float *out_invdepth, hipStream_t s, bool need_bwd = true,
                        bool sb_order = false, uint32_t seg_len = 0, uint32_t fseg_len = 0,
-                       hipStream_t worker_stream = nullptr, bool workers_launched = false);
+                       hipStream_t worker_stream = nullptr, bool workers_launched = false,
+                       const uint32_t *longest = nullptr, uint32_t *host_words = nullptr);
 // Forward segments' worker pool launched ahead of tile_order (on a side stream that has waited for
 // the binning and the colour pass): its workgroups are resident before render_fwd's grid fills the
 // CUs and start on the queue as soon as tile_order (given the same word) releases `ready`

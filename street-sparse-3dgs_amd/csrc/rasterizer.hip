@@ -784,7 +784,9 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
         {
             StageTimer st(2, s);
             if (!local && !counted)
-                launch_binning_count(P, cam, gs, false, fw_none, order_sb, zero_cls, s, tbs, g_pinned_dev + kHostSBList);
+                launch_binning_count(P, cam, gs, false, fw_none, order_sb, zero_cls, s, tbs,
+                                     GSR_HOST_WORDS == 2 ? dsort_longest_words(gs) + 1
+                                     : GSR_HOST_WORDS ? g_pinned_dev + kHostSBList : nullptr);
             launch_binning_scatter(P, cam, gs, bs, local, s);
         }
         if ((r = check("binning (superblocks)", debug, s))) return r;
@@ -823,7 +825,9 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
             // forward order: by list length (and the backward's class counters zeroed)
             launch_tile_order(nullptr, is.ranges, T, 4, is.tile_ids, s, bs.kdev, bs.cap,
                               GSR_BWD_CLS && need_bwd ? is.bwd_cnt : nullptr, is.bwd_cnt + kFwdItemsWord, bs.point_list,
-                              seg_used, fseg_used, P > 0 ? g_pinned_dev + kHostTileList : nullptr,
+                              seg_used, fseg_used,
+                              P > 0 && GSR_HOST_WORDS == 2 ? dsort_longest_words(gs)
+                              : P > 0 && GSR_HOST_WORDS ? g_pinned_dev + kHostTileList : nullptr,
                               early ? dsort_fwdready_word(gs) : nullptr);
         }
         if ((r = check("tile order", debug, s))) return r;
@@ -843,7 +847,8 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
             if (forked && (hipEventRecord(wfork, s) != hipSuccess || hipStreamWaitEvent(wside, wfork, 0) != hipSuccess))
                 return fail(GSR_ERR_DEVICE, "side stream fork failed");
             launch_render_fwd(cam, gs, bs, is, background, out_color, out_invdepth, s, need_bwd, sb_order, seg_used,
-                              fseg_used, wside, early);
+                              fseg_used, wside, early, P > 0 && GSR_HOST_WORDS == 2 ? dsort_longest_words(gs) : nullptr,
+                              g_pinned_dev);
             if (forked && (hipEventRecord(wjoin, wside) != hipSuccess || hipStreamWaitEvent(s, wjoin, 0) != hipSuccess))
                 return fail(GSR_ERR_DEVICE, "side stream join failed");
             if (early && hipStreamWaitEvent(s, wj, 0) != hipSuccess) return fail(GSR_ERR_DEVICE, "side stream join failed");

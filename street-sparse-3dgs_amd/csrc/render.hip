@@ -510,9 +510,17 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) GSR_FWD_ATTR void ren
     uint32_t *__restrict__ tile_work, const uint32_t *__restrict__ fwd_order, const uint32_t *__restrict__ kdev,
     uint32_t cap, const uint32_t *__restrict__ sort_err, float4 *__restrict__ acc, uint32_t acc_n4,
     uint32_t *__restrict__ bwd_cnt, uint32_t *__restrict__ bwd_cls, int ntiles, int gy, int sb_nsbx, int sb_shift,
-    uint32_t seg_len, uint32_t *__restrict__ bin_base, uint32_t fseg_len, uint32_t *__restrict__ fctl, uint32_t fseg_min) {
+    uint32_t seg_len, uint32_t *__restrict__ bin_base, uint32_t fseg_len, uint32_t *__restrict__ fctl, uint32_t fseg_min,
+    const uint32_t *__restrict__ longest, uint32_t *host_words) {
     constexpr int kWaves = kPixPerLane / kSub;
     if (kdev && *kdev > cap) return;  // the point-list capacity is short: the host re-runs at K
+    if (host_words && blockIdx.x == 0 && threadIdx.x == 0) {
+        // the split gate's hints, written to pinned host memory here rather than by tile_order /
+        // sb_colscan: the PCIe store's completion is hidden in this long launch instead of ending
+        // a short one
+        __hip_atomic_store(host_words + kHostTileList, longest[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(host_words + kHostSBList, longest[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     {
         // the backward's per-Gaussian accumulator rows (atomic mode) start at zero: every
         // workgroup clears one slice with streaming stores that drain while it blends (the
@@ -859,10 +867,17 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t *__rest
             }
         }
     }
-    if (host_tilelist) atomicMax(&s_max, mx);
+    if (host_tilelist) {
+        // the wave's maximum first (DPP): one LDS atomic per wave instead of 1024 on one word
+        mx = wave_max_u32(mx);
+        if ((threadIdx.x & 63) == 0) atomicMax(&s_max, mx);
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-        if (host_tilelist) __hip_atomic_store(host_tilelist, s_max, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (host_tilelist) {
+            if (GSR_HOST_WORDS == 2) *host_tilelist = s_max;  // a device word render_fwd forwards
+            else __hip_atomic_store(host_tilelist, s_max, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         if (fseg_len) {
             fctl[0] = s_items;  // kFwdItemsWord
             fctl[1] = 0u;       // kFwdNextWord
@@ -938,7 +953,7 @@ void launch_render_fwd_workers(const Camera &cam, const GeomState &gs, const Bin
 void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                        const float *bg, float *out_color, float *out_invdepth, hipStream_t s, bool need_bwd,
                        bool sb_order, uint32_t seg_len, uint32_t fseg_len, hipStream_t worker_stream,
-                       bool workers_launched) {
+                       bool workers_launched, const uint32_t *longest, uint32_t *host_words) {
     const int T = cam.gx * cam.gy;
     if (T == 0) return;
     const SBGrid &sg = gs.sb;
@@ -954,7 +969,7 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
                        bs.kdev ? dsort_err_word(gs) : nullptr, gs.acc, (uint32_t)(4 * (size_t)gs.nacc),              \
                        GSR_BWD_CLS && need_bwd ? is.bwd_cnt : nullptr, is.bwd_cls, T, cam.gy, sg.nsbx,        \
                        sb_order ? sg.shift : -1, seg_len, bs.point_list, fseg_len, is.bwd_cnt + kFwdItemsWord,       \
-                       fseg_len ? fseg_min_len(fseg_len) : 0u)
+                       fseg_len ? fseg_min_len(fseg_len) : 0u, longest, longest ? host_words : nullptr)
     static_assert(GSR_FWD_SUB == 1 || GSR_FWD_SUB == 2 || GSR_FWD_SUB == 4, "GSR_FWD_SUB: 1, 2 or 4");
     GSR_FWD_LAUNCH(render_fwd_kernel<GSR_FWD_SUB>, kWave * (kPixPerLane / GSR_FWD_SUB));
 #undef GSR_FWD_LAUNCH
