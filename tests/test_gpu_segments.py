@@ -339,3 +339,41 @@ def test_split_gate_arms_after_a_long_list_frame():
     _C.reset_capacity_hint()
     st3, _ = frame(long_)
     assert st3["tb_split_items"] == 0
+
+
+def test_split_frame_capacity_rerun_matches():
+    """A long-list frame whose K exceeds the capacity hint, with the forward split (workers
+    launched ahead of tile_order) and the superblock split armed: the first pass's workers, tile
+    order and render leave at the capacity test and the frame is binned and rendered again at K.
+    Record mode: bitwise the same frame as the next one, which fits the hint."""
+    import torch
+    from diff_gaussian_rasterization import GaussianRasterizer, _C
+    from helpers import settings, torch_inputs
+    dev = torch.device("cuda:0")
+    c = FWD_CASES[0]
+    s = seg_scene(c)
+    short = seg_scene(dict(name="short", P=2000, W=96, H=64, deg=1, seed=5, log_scale=-3.0, opac=(0.3, 0.9)))
+
+    def frame(sc, deg):
+        inp = torch_inputs(sc, dev)
+        for v in inp.values():
+            v.requires_grad_(True)
+        color, _, invd = GaussianRasterizer(settings(sc, dev, deg))(**inp)
+        g = torch.Generator(device=dev).manual_seed(3)
+        (color * torch.randn(color.shape, generator=g, device=dev)).sum().backward()
+        torch.cuda.synchronize()
+        return [color.detach(), invd.detach()] + [inp[k].grad for k in ("means3D", "shs", "opacities", "scales")]
+
+    reruns = lambda: _C.forward_stats()["reruns"]
+    with deterministic(), fwd_segment(4096), bwd_segment(512):
+        _C.reset_capacity_hint()
+        for _ in range(2):
+            frame(short, 1)
+        r0 = reruns()
+        a = frame(s, c["deg"])  # K far above the hint: binned and rendered twice
+        r1 = reruns()
+        b = frame(s, c["deg"])
+        r2 = reruns()
+    assert (r1 - r0, r2 - r1) == (1, 0)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
