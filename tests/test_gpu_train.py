@@ -478,11 +478,12 @@ def test_adam_column_blocks_equal_separate_groups():
     assert torch.equal(oj.state[joined]["exp_avg_sq"][:, 1:], os_.state[rest]["exp_avg_sq"])
 
 
-@pytest.mark.parametrize("frac", [0.12, 0.9, 0.0])
+@pytest.mark.parametrize("frac", [0.12, 0.9, 0.0, 1.0])
 def test_sparse_adam_row_blocks_equal_elementwise(frac, monkeypatch):
     """The row-block Adam kernel (one wave per 64 rows) and the element-per-thread kernel apply
     the same per-element arithmetic: parameters and moments bit-identical, for sparse and dense
-    relevance (frac 0: no relevant row, the dense fallback) and joined (P,16,3) column blocks."""
+    relevance (frac 0: no relevant row, the dense fallback; frac 1: every wave fully relevant, the
+    joined (P,16,3) column blocks then updated as whole float4 rows) and joined column blocks."""
     from gs_train import Adam
     P = 70_001
     g = torch.Generator().manual_seed(5)
