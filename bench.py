@@ -608,32 +608,51 @@ def quiet_gc():
         gc.unfreeze()
 
 
-def timed(step, steps, warmup, ranks, per_step=None):
+def timed(step, steps, warmup, ranks, per_step=None, host=None):
     """W untimed steps, then exactly `steps` steps bracketed by barrier + synchronize on both sides;
     the MAX over ranks of the elapsed seconds.  per_step (a list): receives each timed step's device
     duration in ms -- HIP events recorded on the current stream between consecutive steps (no
-    synchronisation inside the timed region)."""
+    synchronisation inside the timed region).  host (a dict): the host's side of the same steps --
+    the time each step() call took to return (perf_counter, ms) and the part of it the forward spent
+    waiting for K (gsr_forward_stats' k_wait_ns), so a line shows whether the host or the GPU bounds
+    the step."""
     import torch
+    from diff_gaussian_rasterization import _C
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
     ranks.barrier()
     torch.cuda.synchronize()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)] if per_step is not None else None
+    ht = [0.0] * (steps + 1)
     with quiet_gc():
+        k0 = _C.forward_stats()["k_wait_ns"] if host is not None else 0
         t0 = time.perf_counter()
         if ev is not None:
             ev[0].record()
+        ht[0] = time.perf_counter()
         for i in range(steps):
             step()
+            ht[i + 1] = time.perf_counter()
             if ev is not None:
                 ev[i + 1].record()
+        k1 = _C.forward_stats()["k_wait_ns"] if host is not None else 0
         torch.cuda.synchronize()
         ranks.barrier()
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
     if ev is not None:
         per_step.extend(ev[i].elapsed_time(ev[i + 1]) for i in range(steps))
+    if host is not None:
+        call = np.diff(np.asarray(ht)) * 1e3
+        kw = (k1 - k0) / max(1, steps) * 1e-6
+        host.update({"step_call_ms_median": round(float(np.median(call)), 5),
+                     "step_call_ms_mean": round(float(call.mean()), 5),
+                     "step_call_ms_max": round(float(call.max()), 5),
+                     "k_wait_ms_mean": round(kw, 5),
+                     "busy_ms_mean": round(float(call.mean()) - kw, 5),
+                     "source": "perf_counter around each timed step() call; k_wait from gsr_forward_stats[5] "
+                               "(the forward's wait for num_rendered); busy = call - k_wait"})
     return ranks.max(el)
 
 
@@ -911,8 +930,9 @@ def main():
     log("metric: timing")
     probe = ClockProbe(dev)
     per_step = []
+    host_side = {}
     clk_before = probe.read()
-    elapsed = timed(step, a.steps, a.warmup, ranks, per_step=per_step)
+    elapsed = timed(step, a.steps, a.warmup, ranks, per_step=per_step, host=host_side)
     clk_after = probe.read()
 
     # the clock under the bench's load: sampled over ~400 more (untimed) steps
@@ -978,6 +998,7 @@ def main():
                      "frac_strict_8d": round(strict_8d / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if dom == "render_bwd" else None},
         "valu_roofline": [r for r in (valu_roofline(k, stages.get(k)) for k in ("render_bwd", "render_fwd")) if r],
         "step_dispersion": dispersion(per_step),
+        "host_issue": host_side,
         "gpu_clock": {"before": clk_before, "after": clk_after, "under_load": clk_load,
                       "unit": "MHz / W / C (amdsmi GPU metrics)", "error": probe.err},
         "stages_ms": {k: round(v, 5) for k, v in stages.items()},

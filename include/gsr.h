@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 4
+#define GSR_ABI_VERSION 5
 
 typedef enum {
     GSR_OK = 0,
@@ -176,6 +176,14 @@ int gsr_set_fwd_segment(int L);
  * (GSR_FSEG_FACTOR); otherwise max(len, L).  Returns the previous setting. */
 int gsr_set_fwd_split_min(int len);
 
+/* The forward-split workers' bounded spins, process-wide (for tests; 0 = the default): `ready` loop
+ * trips (~256 clocks each) waiting for tile_order's release of the queue, after which a worker
+ * leaves (counted in gsr_forward_stats[4]; the pool's second launch blends its items), and `flag`
+ * trips (~128 clocks) waiting for a predecessor segment's transmittance, after which that tile's
+ * pixels are NaN and the next rasterizer call on the thread fails (GSR_ERR_DEVICE).  ready = -1 (fault
+ * injection): the workers leave without waiting, as if the release never came.  ABI 5. */
+int gsr_set_fwd_spin_limits(int64_t ready, int64_t flag);
+
 /* The split gate, process-wide.  1 (default): the forward split (gsr_set_fwd_segment) and the
  * tile binning's split of long superblock lists are armed only for the 256 frames (per device and
  * calling thread) after one whose longest tile / superblock list called for them -- they cost a few
@@ -199,7 +207,10 @@ int gsr_set_binning(int mode);
 /* Forward statistics since load: out[0] = frames rasterized (P > 0), out[1] = frames whose
  * binning ran twice because the capacity hint from the previous frame was short of K,
  * out[2] = frames binned by the local sort, out[3] = local frames re-run through the global sort
- * (a superblock list too long for LDS).  Returns the number of values written (<= n). */
+ * (a superblock list too long for LDS), out[4] = frames whose forward-split workers gave up waiting
+ * for tile_order's release of their queue (the side stream did not run beside the main one; the
+ * pool's second launch completed those frames exactly -- ABI 5), out[5] = host nanoseconds spent waiting
+ * for K (num_rendered) in forward calls (ABI 5).  Returns the number of values written (<= n). */
 int gsr_forward_stats(int64_t *out, int n);
 
 /* Forget the calling thread's point-list capacity hint (the largest K of its last 256 frames per
@@ -224,7 +235,9 @@ int gsr_blend_stats(int64_t *out, int n, int reset);
 
 /* Measurement builds only (-DGSR_SB_TRACE=1; zeros otherwise): per-workgroup phase stamps of the
  * local sort kernel, 8 words per superblock (s_memrealtime at 100 MHz; word 7 = list length).
- * reset != 0 zeroes them after the read.  Returns the count written. */
+ * -DGSR_HOST_TRACE=1 builds instead: the host nanoseconds spent issuing each stage (out[0..9], the
+ * gsr_stage_times_ms order), whole forward and backward calls (out[10], out[11]) and the matching
+ * counts (out[12..23]).  reset != 0 zeroes them after the read.  Returns the count written. */
 int gsr_debug_trace(int64_t *out, int n, int reset);
 
 /* Version / diagnostics. */

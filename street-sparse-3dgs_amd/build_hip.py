@@ -61,6 +61,37 @@ def _compile(src, force, objdir=OBJ, defines=()):
     return obj
 
 
+HOST_SRC = os.path.join(PKG_ROOT, "host", "rasterize_host.cpp")
+HOST_EXT = os.path.join(PKG_ROOT, "diff_gaussian_rasterization", "_gsr_host.so")
+
+
+def build_host(force: bool = False, out: str = HOST_EXT) -> str:
+    """The rasterizer's per-call host path (host/rasterize_host.cpp): a CPython extension against
+    torch's C++ API that calls libgsr_hip.so's C ABI.  Plain g++ -- host code only, no device code --
+    with torch's include paths and C++ ABI."""
+    import sysconfig
+
+    import torch
+    import torch.utils.cpp_extension as ce
+    if not force and not _stale(out, [HOST_SRC, os.path.join(REPO, "include", "gsr.h")]):
+        return out
+    tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
+    cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-w", "-DTORCH_EXTENSION_NAME=_gsr_host",
+           "-DTORCH_API_INCLUDE_EXTENSION_H", f"-D_GLIBCXX_USE_CXX11_ABI={int(torch._C._GLIBCXX_USE_CXX11_ABI)}",
+           "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1"]
+    for inc in ce.include_paths() + [sysconfig.get_paths()["include"], "/opt/rocm/include",
+                                     os.path.join(REPO, "include")]:
+        cmd += ["-I", inc]
+    # libgsr_hip.so is not linked: bind(path) dlopens the file the ctypes layer loaded (GSR_LIBRARY too)
+    cmd += [HOST_SRC, "-o", out + ".tmp", "-L", tlib, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_python",
+            "-ldl", "-Wl,-rpath," + tlib]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"host extension build failed:\n{r.stdout}\n{r.stderr}")
+    os.replace(out + ".tmp", out)
+    return out
+
+
 def build(force: bool = False, jobs: int = 4, defines=(), lib: str = LIB) -> str:
     """Build the library; `defines` (NAME or NAME=VALUE) with a different `lib` path builds a
     measurement variant in its own object directory (load it with GSR_LIBRARY=path)."""
@@ -92,4 +123,6 @@ if __name__ == "__main__":
     ap.add_argument("--out", default=LIB, help="library path (variants: anywhere outside the package)")
     a = ap.parse_args()
     print(build(a.force, a.jobs, a.define, a.out))
+    if a.out == LIB:
+        print(build_host(a.force))
     sys.exit(0)

@@ -602,7 +602,24 @@ __host__ __device__ __forceinline__ const uint32_t *drect4_of(const GeomState &g
 #ifndef GSR_HOST_WORDS
 #define GSR_HOST_WORDS 1  // split gate hints: 1 stored by tile_order / sb_colscan, 2 forwarded by render_fwd, 0 none (A/B)
 #endif
-enum HostWord { kHostK = 0, kHostErr = 1, kHostMaxSB = 2, kHostP1 = 3, kHostSBList = 4, kHostTileList = 5, kHostWords = 6 };
+// Sticky flags the kernels set with plain system-scope stores (read-modify-write atomics on pinned host
+// memory need PCIe atomics, which a host may not have) and the host's next call takes:
+// kHostErr: a depth-sort lookback spin gave up; kHostFwdErr: a forward worker's wait for a
+// predecessor segment gave up (both frames' images are NaN: the call fails); kHostFwdGiveUp: forward
+// workers gave up waiting for tile_order's ready word (the frame is completed exactly by the pool's
+// second launch; counted in gsr_forward_stats).
+enum HostWord { kHostK = 0, kHostErr = 1, kHostMaxSB = 2, kHostP1 = 3, kHostSBList = 4, kHostTileList = 5,
+                kHostFwdGiveUp = 6, kHostFwdErr = 7, kHostWords = 8 };
+// The forward workers' bounded spins (render.hip fwd_seg_worker): `ready` = tile_order's release of
+// the queue, `flag` = a predecessor item's transmittance row; loop trips of ~256 / ~128 clocks.
+// gsr_set_fwd_spin_limits changes them (tests); `host` = the pinned words above.
+struct FwdSpin {
+    uint32_t ready, flag;
+    uint32_t *host;
+};
+constexpr uint32_t kFwdReadySpins = 1u << 18;  // ~28 ms: tile_order normally releases within ~10 us
+constexpr uint32_t kFwdFlagSpins = 1u << 22;
+constexpr uint32_t kFwdReadyNever = 0xFFFFFFFFu;  // tests: the workers give up without waiting
 struct FrameWords {
     uint32_t *dev_K;      // nullptr: global-sort frame (dsort publishes K)
     uint32_t *dev_maxsb;  // longest SB list

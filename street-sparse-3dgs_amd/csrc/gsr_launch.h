@@ -48,7 +48,7 @@ void launch_preprocess_color(const GaussianInputs &in, const Camera &cam, const 
 void launch_tile_order(const uint32_t *work, const uint2 *ranges, int T, int shift, uint32_t *order, hipStream_t s,
                        const uint32_t *kdev = nullptr, uint32_t cap = 0, uint32_t *zero_classes = nullptr,
                        uint32_t *fctl = nullptr, void *bin_base = nullptr, uint32_t seg_len = 0, uint32_t fseg_len = 0,
-                       uint32_t *host_tilelist = nullptr, uint32_t *fwd_ready = nullptr);
+                       uint32_t *host_tilelist = nullptr, uint32_t *fwd_ready = nullptr, uint32_t fseg_min = 0);
 void launch_mark_visible(int P, const float *means3D, const float *view, uint8_t *present, hipStream_t s);
 
 // sort.hip (rocPRIM)
@@ -121,14 +121,24 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
                        const float *bg, float *out_color, float *out_invdepth, hipStream_t s, bool need_bwd = true,
                        bool sb_order = false, uint32_t seg_len = 0, uint32_t fseg_len = 0,
                        hipStream_t worker_stream = nullptr, bool workers_launched = false,
-                       const uint32_t *longest = nullptr, uint32_t *host_words = nullptr);
+                       const uint32_t *longest = nullptr, uint32_t *host_words = nullptr, uint32_t fseg_min = 0,
+                       FwdSpin spin = FwdSpin{kFwdReadySpins, kFwdFlagSpins, nullptr});
 // Forward segments' worker pool launched ahead of tile_order (on a side stream that has waited for
 // the binning and the colour pass): its workgroups are resident before render_fwd's grid fills the
 // CUs and start on the queue as soon as tile_order (given the same word) releases `ready`
 // (dsort_fwdready_word: zero since the frame's preprocess).
 void launch_render_fwd_workers(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                                const float *bg, float *out_color, float *out_invdepth, bool need_bwd, uint32_t seg_len,
-                               uint32_t fseg_len, hipStream_t ws, const uint32_t *ready);
+                               uint32_t fseg_len, hipStream_t ws, const uint32_t *ready, FwdSpin spin);
+// The pool's second launch, on the main stream after render_fwd when the pool was launched ahead:
+// a small grid that takes whatever the early workers left in the queue (nothing, unless some gave up
+// waiting for tile_order's ready word because the two streams did not run concurrently).
+void launch_render_fwd_cleanup(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
+                               const float *bg, float *out_color, float *out_invdepth, bool need_bwd, uint32_t seg_len,
+                               uint32_t fseg_len, hipStream_t s, FwdSpin spin);
+// the workers' spin limits (gsr_set_fwd_spin_limits) with the pinned host words
+FwdSpin fwd_spin(uint32_t *host_words);
+void set_fwd_spin_limits(uint32_t ready, uint32_t flag);
 // GSR_FWD_EARLY_WORKERS (default 1): launch_render_fwd_workers before tile_order; 0: beside render_fwd
 bool fwd_early_workers();
 // seg_len != 0: the backward's heavy tiles are cut into segments of seg_len list positions

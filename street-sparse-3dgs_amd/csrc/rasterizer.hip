@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstring>
 #include <atomic>
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <algorithm>
@@ -151,9 +152,29 @@ int fail(int code, const std::string &msg) {
 
 // A lookback timeout of this or an earlier frame's depth sort (the pass kernels store the pinned
 // word; its frame's render_fwd already wrote NaN pixels): fail this call, once per occurrence.
+// kHostFwdErr: a forward worker's predecessor wait timed out (that tile's pixels are NaN).  Forward
+// workers that gave up on tile_order's ready word are counted instead (kHostFwdGiveUp, frames with
+// give-ups; their items were blended by the pool's second launch, the frame is exact).
+// g_kwait_ns: host time spent waiting for K (num_rendered) in the forward, summed (gsr_forward_stats[5]).
+std::atomic<int64_t> g_fwd_giveups{0}, g_kwait_ns{0};
+constexpr int kFwdStats = 6;
+void collect_giveups() {
+    if (!g_pinned) return;
+    const uint32_t gu = __atomic_exchange_n(&g_pinned[kHostFwdGiveUp], 0u, __ATOMIC_SEQ_CST);
+    if (gu && g_fwd_giveups.fetch_add(1) == 0)
+        fprintf(stderr, "[gsr] forward split: workers gave up waiting for tile_order (side and main streams not "
+                        "concurrent); the frame was completed by the pool's second launch, slower "
+                        "(gsr_forward_stats[4] counts such frames)\n");
+}
 int sticky_sort_error() {
-    if (g_pinned && __atomic_exchange_n(&g_pinned[kHostErr], 0u, __ATOMIC_SEQ_CST) != 0u)
-        return fail(GSR_ERR_DEVICE, "depth sort: a lookback spin timed out (this or an earlier frame; its image is NaN)");
+    if (!g_pinned) return GSR_OK;
+    collect_giveups();
+    const uint32_t e = __atomic_exchange_n(&g_pinned[kHostErr], 0u, __ATOMIC_SEQ_CST);
+    const uint32_t fe = __atomic_exchange_n(&g_pinned[kHostFwdErr], 0u, __ATOMIC_SEQ_CST);
+    if (e) return fail(GSR_ERR_DEVICE, "depth sort: a lookback spin timed out (this or an earlier frame; its image is NaN)");
+    if (fe)
+        return fail(GSR_ERR_DEVICE, "forward split: a worker's wait for a predecessor segment timed out (this or an "
+                                    "earlier frame; the tile's pixels are NaN)");
     return GSR_OK;
 }
 
@@ -167,12 +188,35 @@ void ensure_events() {
     g_ev_init = true;
 }
 
+// Measurement builds only (-DGSR_HOST_TRACE=1, a variant library): the host time spent issuing each
+// stage (StageTimer's scope) and whole forward / backward calls, read with gsr_debug_trace:
+// out[0..11] = nanoseconds (stages 0-9, forward call, backward call), out[12..23] = counts.
+#ifndef GSR_HOST_TRACE
+#define GSR_HOST_TRACE 0
+#endif
+constexpr int kHostTrace = 12;
+std::atomic<int64_t> g_htrace_ns[kHostTrace], g_htrace_cnt[kHostTrace];
+struct HostScope {
+    int k;
+    std::chrono::steady_clock::time_point t0;
+    explicit HostScope(int slot) : k(slot) {
+        if (GSR_HOST_TRACE) t0 = std::chrono::steady_clock::now();
+    }
+    ~HostScope() {
+        if (!GSR_HOST_TRACE) return;
+        g_htrace_ns[k].fetch_add(
+            std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
+        g_htrace_cnt[k].fetch_add(1);
+    }
+};
+
 // Brackets exactly the device work of one stage (no host gaps inside the bracket).
 struct StageTimer {
     int k;
     hipStream_t s;
     bool on;
-    StageTimer(int stage, hipStream_t stream) : k(stage), s(stream), on(g_profile != 0) {
+    HostScope hs;
+    StageTimer(int stage, hipStream_t stream) : k(stage), s(stream), on(g_profile != 0), hs(stage) {
         if (on) (void)hipEventRecord(g_ev_begin[k], s);
     }
     ~StageTimer() {
@@ -435,18 +479,16 @@ std::atomic<uint32_t> g_bwd_seg{GSR_BWD_SEG_DEFAULT};
 std::atomic<uint32_t> g_fwd_seg{GSR_FWD_SEG_DEFAULT};
 std::mutex g_seg_mu;
 std::unordered_map<const void *, uint32_t> g_seg_of;
+// A forward made without segments (L = 0: switched off, or the 32-bit item-numbering guard) is
+// recorded as 0 too -- its backward must not cut tiles at the current setting and read checkpoints
+// render_fwd never wrote.  Only an entry dropped by the kUnclearedMax clear falls back to the setting.
 void note_forward_seg(const void *image, uint32_t L) {
     std::lock_guard<std::mutex> lk(g_seg_mu);
-    if (!L) {
-        if (!g_seg_of.empty()) g_seg_of.erase(image);
-        return;
-    }
     if (g_seg_of.size() >= kUnclearedMax) g_seg_of.clear();
     g_seg_of[image] = L;
 }
 uint32_t forward_seg(const void *image) {
     std::lock_guard<std::mutex> lk(g_seg_mu);
-    if (g_seg_of.empty()) return 0;
     const auto it = g_seg_of.find(image);
     return it == g_seg_of.end() ? g_bwd_seg.load(std::memory_order_relaxed) : it->second;
 }
@@ -516,6 +558,7 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
                              int debug, void *stream, int64_t *num_rendered, unsigned flags) {
     (void)prefiltered;
     (void)num_node_kids;  // accepted; render_post's blend (which this reproduces) does not read it
+    HostScope host_scope(10);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (flags & ~(unsigned)GSR_FWD_NO_BACKWARD) return fail(GSR_ERR_INVALID_ARGUMENT, "unknown forward flags");
     // the backward's accumulator rows are cleared (and its launch order built) only for a frame a
@@ -698,6 +741,7 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
     uint32_t maxsb = 0;
     bool have_K = P == 0;
     auto read_K = [&]() -> int {
+        const auto t_wait = std::chrono::steady_clock::now();
         if (k_ready) {
             if (hipEventSynchronize(k_ready) != hipSuccess) return fail(GSR_ERR_DEVICE, "num_rendered wait failed");
         } else {
@@ -711,6 +755,9 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
                 std::this_thread::yield();
             }
         }
+        g_kwait_ns.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() -
+                                                                                   t_wait).count(),
+                             std::memory_order_relaxed);
         uint32_t k = __atomic_load_n(&g_pinned[kHostK], __ATOMIC_ACQUIRE);
         uint32_t m = __atomic_load_n(&g_pinned[kHostMaxSB], __ATOMIC_ACQUIRE);
         if (k == kKPending) {  // not expected: read the device copies instead (a local frame's K
@@ -754,12 +801,16 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
     const uint32_t seg_req = need_bwd && bwd_segments_supported() ? g_bwd_seg.load(std::memory_order_relaxed) : 0u;
     uint32_t fseg_req = fwd_segments_supported() && !sb_order ? g_fwd_seg.load(std::memory_order_relaxed) : 0u;
     uint32_t tb_req = tb_split_len();
+    // the split's minimum list length, read once per frame: tile_order's queue, render_fwd's skip test
+    // and the gate must agree even if gsr_set_fwd_split_min runs meanwhile
+    const uint32_t fseg_min = fseg_req ? fseg_min_len(fseg_req) : 0u;
+    const FwdSpin spin = fwd_spin(g_pinned_dev);
     if (P > 0) {
         // the split gate: the longest lists of the frames before (whatever the pinned words hold now)
         const int64_t f = ++g_frame_no[dev];
         const uint32_t tl = __atomic_load_n(&g_pinned[kHostTileList], __ATOMIC_RELAXED);
         const uint32_t sl = __atomic_load_n(&g_pinned[kHostSBList], __ATOMIC_RELAXED);
-        if (fseg_req && tl > fseg_min_len(fseg_req)) g_long_tile_at[dev] = f;
+        if (fseg_req && tl > fseg_min) g_long_tile_at[dev] = f;
         if (tb_req && sl > tb_req) g_long_sb_at[dev] = f;
         if (g_split_gate.load(std::memory_order_relaxed)) {
             if (f - g_long_tile_at[dev] > kSplitMemory) fseg_req = 0;
@@ -816,7 +867,7 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
                 (split && !GSR_COLOR_SERIAL && !joined && hipStreamWaitEvent(ws, join, 0) != hipSuccess))
                 return fail(GSR_ERR_DEVICE, "side stream fork failed");
             launch_render_fwd_workers(cam, gs, bs, is, background, out_color, out_invdepth, need_bwd, seg_used,
-                                      fseg_used, ws, dsort_fwdready_word(gs));
+                                      fseg_used, ws, dsort_fwdready_word(gs), spin);
             if (hipEventRecord(wj, ws) != hipSuccess) return fail(GSR_ERR_DEVICE, "side stream join record failed");
             early = true;
         }
@@ -828,7 +879,7 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
                               seg_used, fseg_used,
                               P > 0 && GSR_HOST_WORDS == 2 ? dsort_longest_words(gs)
                               : P > 0 && GSR_HOST_WORDS ? g_pinned_dev + kHostTileList : nullptr,
-                              early ? dsort_fwdready_word(gs) : nullptr);
+                              early ? dsort_fwdready_word(gs) : nullptr, fseg_min);
         }
         if ((r = check("tile order", debug, s))) return r;
         if (split && !GSR_COLOR_SERIAL && !joined) {
@@ -848,7 +899,13 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
                 return fail(GSR_ERR_DEVICE, "side stream fork failed");
             launch_render_fwd(cam, gs, bs, is, background, out_color, out_invdepth, s, need_bwd, sb_order, seg_used,
                               fseg_used, wside, early, P > 0 && GSR_HOST_WORDS == 2 ? dsort_longest_words(gs) : nullptr,
-                              g_pinned_dev);
+                              g_pinned_dev, fseg_min, spin);
+            // the early pool's workers may have given up on the ready word (the two streams did not
+            // run concurrently): a small second launch on this stream, after tile_order, takes any
+            // item still queued -- no frame depends on the streams' concurrency
+            if (early)
+                launch_render_fwd_cleanup(cam, gs, bs, is, background, out_color, out_invdepth, need_bwd, seg_used,
+                                          fseg_used, s, spin);
             if (forked && (hipEventRecord(wjoin, wside) != hipSuccess || hipStreamWaitEvent(s, wjoin, 0) != hipSuccess))
                 return fail(GSR_ERR_DEVICE, "side stream join failed");
             if (early && hipStreamWaitEvent(s, wj, 0) != hipSuccess) return fail(GSR_ERR_DEVICE, "side stream join failed");
@@ -911,6 +968,7 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
                            const float *interpolation_weights, const int *num_node_kids, int num_render,
                            int debug, void *stream) {
     (void)num_node_kids;
+    HostScope host_scope(11);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int rc = validate_common(P, D, M, shs, colors_precomp, scales, rotations, cov3D_precomp, width, height);
     if (rc) return rc;
@@ -1034,6 +1092,13 @@ int gsr_set_deterministic(int enable) { return g_deterministic.exchange(enable ?
 
 int gsr_set_split_gate(int enable) { return g_split_gate.exchange(enable ? 1 : 0); }
 
+int gsr_set_fwd_spin_limits(int64_t ready, int64_t flag) {
+    if (ready < -1 || flag < 0 || ready >= UINT32_MAX || flag > UINT32_MAX)
+        return fail(GSR_ERR_INVALID_ARGUMENT, "spin limits: ready -1 or 0 (default) .. 2^32 - 2, flag 0 .. 2^32 - 1");
+    set_fwd_spin_limits(ready < 0 ? kFwdReadyNever : (uint32_t)ready, (uint32_t)flag);
+    return GSR_OK;
+}
+
 int gsr_set_fwd_split_min(int len) {
     if (len < 0) return fail(GSR_ERR_INVALID_ARGUMENT, "forward split minimum list length must be >= 0");
     return (int)set_fwd_split_min((uint32_t)len);
@@ -1062,9 +1127,11 @@ int gsr_set_binning(int mode) {
 
 int gsr_forward_stats(int64_t *out, int n) {
     if (!out || n < 0) return fail(GSR_ERR_INVALID_ARGUMENT, "NULL stats buffer");
-    const int64_t v[4] = {g_frames.load(), g_reruns.load(), g_local_frames.load(), g_fallbacks.load()};
+    collect_giveups();
+    const int64_t v[kFwdStats] = {g_frames.load(), g_reruns.load(), g_local_frames.load(), g_fallbacks.load(),
+                                  g_fwd_giveups.load(), g_kwait_ns.load()};
     int k = 0;
-    for (; k < n && k < 4; k++) out[k] = v[k];
+    for (; k < n && k < kFwdStats; k++) out[k] = v[k];
     return k;
 }
 
@@ -1118,7 +1185,16 @@ int gsr_frame_stats(const void *geom_buffer, int P, int width, int height, int64
     return k;
 }
 
-int gsr_debug_trace(int64_t *out, int n, int reset) { return gsr::debug_trace(out, n, reset); }
+int gsr_debug_trace(int64_t *out, int n, int reset) {
+    if (!GSR_HOST_TRACE) return gsr::debug_trace(out, n, reset);
+    if (!out || n < 0) return fail(GSR_ERR_INVALID_ARGUMENT, "NULL trace buffer");
+    int k = 0;
+    for (; k < n && k < 2 * kHostTrace; k++)
+        out[k] = k < kHostTrace ? g_htrace_ns[k].load() : g_htrace_cnt[k - kHostTrace].load();
+    if (reset)
+        for (int i = 0; i < kHostTrace; i++) g_htrace_ns[i] = g_htrace_cnt[i] = 0;
+    return k;
+}
 
 int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,
                      uint8_t *present, void *stream) {

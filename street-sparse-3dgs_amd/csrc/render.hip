@@ -307,18 +307,27 @@ __device__ void fwd_seg_worker(const uint2 *__restrict__ ranges, const uint32_t 
                                uint32_t *__restrict__ tile_work, uint32_t kf, const uint32_t *__restrict__ sort_err,
                                uint32_t *__restrict__ bwd_cnt, uint32_t *__restrict__ bwd_cls, int ntiles, uint32_t seg_len,
                                uint32_t fseg_len, uint32_t *bin_base, uint32_t *fctl, float4 *sa, float4 *sb,
-                               float4 *sc, uint32_t *s_work, uint32_t *s_scalar, const uint32_t *ready) {
+                               float4 *sc, uint32_t *s_work, uint32_t *s_scalar, const uint32_t *ready,
+                               FwdSpin spin) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const FwdSegLayout f = fseg_layout(bin_base, kf, seg_len, fseg_len);
     float *ck = seg_len && bwd_cnt ? reinterpret_cast<float *>(reinterpret_cast<char *>(bin_base) + ck_offset(kf)) : nullptr;
     if (ready) {
-        // launched ahead of tile_order: wait for its release of the queue (a bounded spin; never
-        // expected to give up -- the workers then leave and the split tiles keep no pixels)
+        // launched ahead of tile_order on another stream: wait for its release of the queue.  Nothing
+        // guarantees the two streams run concurrently (they may share a hardware queue, and counter
+        // collection serialises dispatches), so the spin is bounded: a worker that gives up has
+        // dequeued nothing, counts itself in the pinned kHostFwdGiveUp word (the host reports it:
+        // gsr_forward_stats) and leaves; the pool's second launch after render_fwd on the main
+        // stream (launch_render_fwd_cleanup) then takes every item still queued -- the frame stays
+        // exact, only slower.
         if (threadIdx.x == 0) {
             uint32_t ok = 1u, spins = 0;
-            while (!__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                if (++spins > (1u << 22)) {
+            // spin.ready == kFwdReadyNever (fault injection, tests): leave as if the word never came
+            while (spin.ready == kFwdReadyNever || !__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                if (++spins > spin.ready || spin.ready == kFwdReadyNever) {
                     ok = 0u;
+                    if (spin.host) __hip_atomic_store(spin.host + kHostFwdGiveUp, 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_SYSTEM);
                     break;
                 }
                 __builtin_amdgcn_s_sleep(4);
@@ -369,8 +378,13 @@ __device__ void fwd_seg_worker(const uint2 *__restrict__ ranges, const uint32_t 
                 for (uint32_t j = 0; j < sgi && ok; j++) {
                     uint32_t spins = 0;
                     while (!__hip_atomic_load(f.flags + i0 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                        if (++spins > (1u << 22)) {  // never expected: the tile's pixels become NaN (loud)
+                        if (++spins > spin.flag) {
+                            // never expected (every predecessor was dequeued earlier, so its workgroup
+                            // is resident): the tile's pixels become NaN and the sticky error word
+                            // makes the host's next rasterizer call fail (gsr_last_error)
                             ok = 0u;
+                            if (spin.host) __hip_atomic_store(spin.host + kHostFwdErr, 1u, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_SYSTEM);
                             break;
                         }
                         __builtin_amdgcn_s_sleep(2);
@@ -482,7 +496,7 @@ __global__ __launch_bounds__(kWave * kPixPerLane) void render_fwd_seg_kernel(
     float *__restrict__ out_invd, float *__restrict__ final_T, uint32_t *__restrict__ n_contrib,
     uint32_t *__restrict__ tile_work, const uint32_t *__restrict__ kdev, uint32_t cap,
     const uint32_t *__restrict__ sort_err, uint32_t *__restrict__ bwd_cnt, uint32_t *__restrict__ bwd_cls, int ntiles,
-    uint32_t seg_len, uint32_t *bin_base, uint32_t fseg_len, uint32_t *fctl, const uint32_t *ready) {
+    uint32_t seg_len, uint32_t *bin_base, uint32_t fseg_len, uint32_t *fctl, const uint32_t *ready, FwdSpin spin) {
     if (kdev && *kdev > cap) return;  // the point-list capacity is short: the host re-runs at K
     __shared__ float4 s_a[kPixPerLane][kWave];
     __shared__ float4 s_b[kPixPerLane][kWave];
@@ -491,7 +505,7 @@ __global__ __launch_bounds__(kWave * kPixPerLane) void render_fwd_seg_kernel(
     const int w = threadIdx.x >> 6;
     fwd_seg_worker(ranges, point_list, W, H, gx, rec, bg, out_color, out_invd, final_T, n_contrib, tile_work,
                    kdev ? *kdev : cap, sort_err, bwd_cnt, bwd_cls, ntiles, seg_len, fseg_len, bin_base, fctl, s_a[w],
-                   s_b[w], s_c[w], s_work, s_scalar, ready);
+                   s_b[w], s_c[w], s_work, s_scalar, ready, spin);
 }
 
 #ifndef GSR_FWD_SEG_INKERNEL
@@ -511,7 +525,7 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) GSR_FWD_ATTR void ren
     uint32_t cap, const uint32_t *__restrict__ sort_err, float4 *__restrict__ acc, uint32_t acc_n4,
     uint32_t *__restrict__ bwd_cnt, uint32_t *__restrict__ bwd_cls, int ntiles, int gy, int sb_nsbx, int sb_shift,
     uint32_t seg_len, uint32_t *__restrict__ bin_base, uint32_t fseg_len, uint32_t *__restrict__ fctl, uint32_t fseg_min,
-    const uint32_t *__restrict__ longest, uint32_t *host_words) {
+    const uint32_t *__restrict__ longest, uint32_t *host_words, FwdSpin spin) {
     constexpr int kWaves = kPixPerLane / kSub;
     if (kdev && *kdev > cap) return;  // the point-list capacity is short: the host re-runs at K
     if (host_words && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -549,7 +563,7 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) GSR_FWD_ATTR void ren
                 fwd_seg_worker(ranges, point_list, W, H, gx, rec, bg, out_color, out_invd, final_T, n_contrib,
                                tile_work, kdev ? *kdev : cap, sort_err, bwd_cnt, bwd_cls, ntiles, seg_len, fseg_len,
                                bin_base, fctl, s_a[threadIdx.x >> 6], s_b[threadIdx.x >> 6], s_c[threadIdx.x >> 6],
-                               s_work, s_scalar, nullptr);
+                               s_work, s_scalar, nullptr, spin);
                 return;
             }
             bidx -= (uint32_t)kFwdWorkers;
@@ -910,10 +924,12 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t *__rest
 
 void launch_tile_order(const uint32_t *work, const uint2 *ranges, int T, int shift, uint32_t *order, hipStream_t s,
                        const uint32_t *kdev, uint32_t cap, uint32_t *zero_classes, uint32_t *fctl, void *bin_base,
-                       uint32_t seg_len, uint32_t fseg_len, uint32_t *host_tilelist, uint32_t *fwd_ready) {
+                       uint32_t seg_len, uint32_t fseg_len, uint32_t *host_tilelist, uint32_t *fwd_ready, uint32_t fseg_min) {
     if (T == 0) return;
+    // fseg_min: the frame's split minimum, computed once by the caller (render_fwd's skip test must see
+    // the same value, or a tile could be skipped without being queued)
     hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, s, work, ranges, T, shift, order, kdev, cap, zero_classes,
-                       fctl, bin_base, seg_len, fctl ? fseg_len : 0u, fctl && fseg_len ? fseg_min_len(fseg_len) : 0u,
+                       fctl, bin_base, seg_len, fctl ? fseg_len : 0u, fctl && fseg_len ? fseg_min : 0u,
                        host_tilelist, fwd_ready);
 }
 
@@ -934,26 +950,49 @@ bool fwd_early_workers() {  // read per frame, so a test can switch it
 
 static void launch_workers(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                            const float *bg, float *out_color, float *out_invdepth, bool need_bwd, uint32_t seg_len,
-                           uint32_t fseg_len, hipStream_t ws, const uint32_t *ready) {
+                           uint32_t fseg_len, hipStream_t ws, const uint32_t *ready, FwdSpin spin, int grid) {
     uint32_t *const bcnt = GSR_BWD_CLS && need_bwd ? is.bwd_cnt : nullptr;
-    hipLaunchKernelGGL(render_fwd_seg_kernel, dim3(fwd_workers()), dim3(kWave * kPixPerLane), 0, ws, is.ranges,
+    hipLaunchKernelGGL(render_fwd_seg_kernel, dim3(grid), dim3(kWave * kPixPerLane), 0, ws, is.ranges,
                        bs.point_list, cam.W, cam.H, cam.gx, gs.rec, bg, out_color, out_invdepth, is.final_T,
                        is.n_contrib, is.tile_work, bs.kdev, bs.cap, bs.kdev ? dsort_err_word(gs) : nullptr, bcnt,
                        is.bwd_cls, cam.gx * cam.gy, seg_len, bs.point_list, fseg_len, is.bwd_cnt + kFwdItemsWord,
-                       ready);
+                       ready, spin);
 }
 
 void launch_render_fwd_workers(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                                const float *bg, float *out_color, float *out_invdepth, bool need_bwd, uint32_t seg_len,
-                               uint32_t fseg_len, hipStream_t ws, const uint32_t *ready) {
+                               uint32_t fseg_len, hipStream_t ws, const uint32_t *ready, FwdSpin spin) {
     if (cam.gx * cam.gy == 0 || !fseg_len || GSR_FWD_SUB != 1 || GSR_FWD_SEG_INKERNEL) return;
-    launch_workers(cam, gs, bs, is, bg, out_color, out_invdepth, need_bwd, seg_len, fseg_len, ws, ready);
+    launch_workers(cam, gs, bs, is, bg, out_color, out_invdepth, need_bwd, seg_len, fseg_len, ws, ready, spin,
+                   fwd_workers());
+}
+
+// 64 workgroups: normally they find the queue drained (or take a straggler's last items); if the early
+// pool gave up entirely they blend every item, slowly but exactly
+constexpr int kFwdCleanupWorkers = 64;
+void launch_render_fwd_cleanup(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
+                               const float *bg, float *out_color, float *out_invdepth, bool need_bwd, uint32_t seg_len,
+                               uint32_t fseg_len, hipStream_t s, FwdSpin spin) {
+    if (cam.gx * cam.gy == 0 || !fseg_len || GSR_FWD_SUB != 1 || GSR_FWD_SEG_INKERNEL) return;
+    launch_workers(cam, gs, bs, is, bg, out_color, out_invdepth, need_bwd, seg_len, fseg_len, s, nullptr, spin,
+                   kFwdCleanupWorkers);
+}
+
+std::atomic<uint32_t> g_fwd_ready_spins{kFwdReadySpins}, g_fwd_flag_spins{kFwdFlagSpins};
+FwdSpin fwd_spin(uint32_t *host_words) {
+    return FwdSpin{g_fwd_ready_spins.load(std::memory_order_relaxed), g_fwd_flag_spins.load(std::memory_order_relaxed),
+                   host_words};
+}
+void set_fwd_spin_limits(uint32_t ready, uint32_t flag) {
+    g_fwd_ready_spins.store(ready ? ready : kFwdReadySpins);
+    g_fwd_flag_spins.store(flag ? flag : kFwdFlagSpins);
 }
 
 void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,
                        const float *bg, float *out_color, float *out_invdepth, hipStream_t s, bool need_bwd,
                        bool sb_order, uint32_t seg_len, uint32_t fseg_len, hipStream_t worker_stream,
-                       bool workers_launched, const uint32_t *longest, uint32_t *host_words) {
+                       bool workers_launched, const uint32_t *longest, uint32_t *host_words, uint32_t fseg_min,
+                       FwdSpin spin) {
     const int T = cam.gx * cam.gy;
     if (T == 0) return;
     const SBGrid &sg = gs.sb;
@@ -961,7 +1000,7 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
     const int grid = (sb_order ? sg.nsb << (2 * sg.shift) : T) + (GSR_FWD_SEG_INKERNEL && fseg_len ? kFwdWorkers : 0);
     if (fseg_len && !GSR_FWD_SEG_INKERNEL && !workers_launched)
         launch_workers(cam, gs, bs, is, bg, out_color, out_invdepth, need_bwd, seg_len, fseg_len,
-                       worker_stream ? worker_stream : s, nullptr);
+                       worker_stream ? worker_stream : s, nullptr, spin, fwd_workers());
     // launch order: is.tile_ids (rasterizer.hip, by list length)
 #define GSR_FWD_LAUNCH(K, NT)                                                                                       \
     hipLaunchKernelGGL(K, dim3(grid), dim3(NT), 0, s, is.ranges, bs.point_list, cam.W, cam.H, cam.gx, gs.rec, bg,   \
@@ -969,7 +1008,7 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
                        bs.kdev ? dsort_err_word(gs) : nullptr, gs.acc, (uint32_t)(4 * (size_t)gs.nacc),              \
                        GSR_BWD_CLS && need_bwd ? is.bwd_cnt : nullptr, is.bwd_cls, T, cam.gy, sg.nsbx,        \
                        sb_order ? sg.shift : -1, seg_len, bs.point_list, fseg_len, is.bwd_cnt + kFwdItemsWord,       \
-                       fseg_len ? fseg_min_len(fseg_len) : 0u, longest, longest ? host_words : nullptr)
+                       fseg_len ? fseg_min : 0u, longest, longest ? host_words : nullptr, spin)
     static_assert(GSR_FWD_SUB == 1 || GSR_FWD_SUB == 2 || GSR_FWD_SUB == 4, "GSR_FWD_SUB: 1, 2 or 4");
     GSR_FWD_LAUNCH(render_fwd_kernel<GSR_FWD_SUB>, kWave * (kPixPerLane / GSR_FWD_SUB));
 #undef GSR_FWD_LAUNCH

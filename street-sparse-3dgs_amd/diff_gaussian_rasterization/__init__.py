@@ -9,7 +9,8 @@ takes means3D / means2D / opacities / shs | colors_precomp / scales+rotations | 
 by keyword and returns (color (3,H,W), radii (P,) int32, invdepth (1,H,W)), markVisible, and
 the autograd Function that routes gradients to means3D, means2D (screen-space, NDC-scaled),
 shs, colors_precomp, opacities, scales, rotations and cov3D_precomp.  Compute runs in the
-hand-written HIP kernels of libgsr_hip.so (street-sparse-3dgs_amd/csrc); there is no CPU path.
+hand-written HIP kernels of libgsr_hip.so (street-sparse-3dgs_amd/csrc), called from the C++ host
+extension _gsr_host.so (street-sparse-3dgs_amd/host); there is no CPU path.
 """
 from __future__ import annotations
 
@@ -44,6 +45,13 @@ def _dump(saved, path):
 
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
                         raster_settings):
+    """The autograd call.  Normally the C++ autograd Function of the host extension (_C._host.rasterize:
+    settings read, validation, buffers and both library calls in C++, the backward on autograd's
+    device thread without the GIL); debug mode keeps the Python Function below, whose input
+    snapshots and dumps are upstream's debug behaviour."""
+    if not raster_settings.debug:
+        return _C._host.rasterize(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
+                                  raster_settings)
     # a frame autograd will not record (torch.no_grad evaluation, or no input that requires grad)
     # can never reach the backward: it skips the backward's accumulator clear
     need_backward = torch.is_grad_enabled() and any(

@@ -70,6 +70,7 @@ SIGNATURES = {
     "gsr_set_fwd_segment": (_i, [_i]),
     "gsr_set_split_gate": (_i, [_i]),
     "gsr_set_fwd_split_min": (_i, [_i]),
+    "gsr_set_fwd_spin_limits": (_i, [_i64, _i64]),
     "gsr_segment_layout_check": (_i, [ctypes.c_int64, _i, _i, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     "gsr_frame_stats": (_i, [_vp, _i, _i, _i, ctypes.POINTER(_i64), _i]),
     "gsr_blend_stats": (_i, [ctypes.POINTER(_i64), _i, _i]),
@@ -128,7 +129,7 @@ SIGNATURES = {
     "gsr_zero_grad_rows": (_i, [_i, ctypes.POINTER(_vp), ctypes.POINTER(_i64), _i64, _i64, _vp, _i64, _vp]),
 }
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 _lib = None
 
 

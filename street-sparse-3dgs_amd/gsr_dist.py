@@ -29,6 +29,14 @@ import torch.distributed as dist
 # The capturing bucket: process-wide, because torch runs a CUDA backward on its own device thread.
 _ACTIVE = None
 _LOCK = threading.Lock()
+# called with the capturing bucket on capture entry and with None on exit (the rasterizer's C++
+# backward registers one: it then asks grad_out for its leaf gradients' outputs)
+_LISTENERS = []
+
+
+def add_capture_listener(fn) -> None:
+    if fn not in _LISTENERS:
+        _LISTENERS.append(fn)
 
 
 def world() -> int:
@@ -126,12 +134,16 @@ class GradBucket:
                         raise RuntimeError("GradBucket.capture: another bucket is capturing")
                     bucket._handed = set()
                     _ACTIVE = bucket
+                for f in _LISTENERS:
+                    f(bucket)
                 return bucket
 
             def __exit__(self_, *exc):
                 global _ACTIVE
                 with _LOCK:
                     _ACTIVE = None
+                for f in _LISTENERS:
+                    f(None)
                 return False
         return _Ctx()
 

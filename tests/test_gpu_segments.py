@@ -377,3 +377,66 @@ def test_split_frame_capacity_rerun_matches():
     assert (r1 - r0, r2 - r1) == (1, 0)
     for x, y in zip(a, b):
         assert torch.equal(x, y)
+
+
+@contextlib.contextmanager
+def fwd_spin_limits(ready=0, flag=0):
+    from diff_gaussian_rasterization import _C
+    _C.set_fwd_spin_limits(ready, flag)
+    try:
+        yield
+    finally:
+        _C.set_fwd_spin_limits(0, 0)
+
+
+def test_fwd_workers_that_give_up_on_the_queue_leave_the_frame_exact(monkeypatch):
+    """The early pool's workers wait for tile_order's release of the queue on another stream; if they
+    give up (here: a ready-spin limit of one trip, as when the two streams do not run concurrently),
+    they are counted (forward_stats) and the pool's second launch after render_fwd blends every item:
+    record mode, the frame bitwise the normal one's.  ready = -1 makes every worker leave at once
+    (normally tile_order has released the queue before the side stream's workers even start)."""
+    from diff_gaussian_rasterization import _C
+    monkeypatch.setenv("GSR_FWD_EARLY_WORKERS", "1")
+    c = FWD_CASES[0]
+    s = seg_scene(c)
+    dcol, dinv = upstream_grads(c)
+    with deterministic(), fwd_segment(4096), bwd_segment(512):
+        ref = run_hip(s, c, dcol, dinv)
+        g0 = _C.forward_stats()["fwd_worker_giveups"]
+        with fwd_spin_limits(ready=-1):
+            h = run_hip(s, c, dcol, dinv)
+        g1 = _C.forward_stats()["fwd_worker_giveups"]
+    assert g1 > g0, "no worker gave up: the test did not exercise the second launch"
+    assert not np.isnan(h["color"]).any()
+    np.testing.assert_array_equal(h["color"], ref["color"])
+    np.testing.assert_array_equal(h["state"]["n_contrib"], ref["state"]["n_contrib"])
+    for k, v in h["grads"].items():
+        if v is not None:
+            np.testing.assert_array_equal(v, ref["grads"][k], err_msg=k)
+
+
+def test_fwd_worker_predecessor_timeout_fails_loudly():
+    """A worker whose wait for a predecessor segment times out (never expected: a flag-spin limit of
+    one trip forces it here) leaves NaN pixels in its tile and sets the sticky device error word: the
+    next rasterizer call raises RuntimeError instead of training on the frame; after it, calls work."""
+    import torch
+    from diff_gaussian_rasterization import GaussianRasterizer
+    from helpers import settings, torch_inputs
+    dev = torch.device("cuda:0")
+    c = FWD_CASES[0]
+    s = seg_scene(c)
+    inp = torch_inputs(s, dev, requires_grad=False)
+    r = GaussianRasterizer(settings(s, dev, c["deg"]))
+    with fwd_segment(4096):
+        with fwd_spin_limits(flag=1):
+            with torch.no_grad():
+                color, _, _ = r(**inp)
+            torch.cuda.synchronize()
+        assert torch.isnan(color).any(), "no predecessor wait timed out"
+        with pytest.raises(RuntimeError, match="forward split"):
+            with torch.no_grad():
+                r(**inp)
+        with torch.no_grad():
+            color2, _, _ = r(**inp)
+        torch.cuda.synchronize()
+    assert not torch.isnan(color2).any()
