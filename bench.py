@@ -255,11 +255,15 @@ def config3(a, dev):
     psnr0 = view_psnr(ts)
     tc = TrainChunk(ts, sched)
     evs, losses = [], {}
+    # per iteration, for the attribution of the slowest ones: binning re-runs (capacity short), the
+    # executor's buffer growths, the torch caching allocator's reserved bytes
+    marks = []
 
     def cb(it, loss):
         e = torch.cuda.Event(enable_timing=True)
         e.record()
         evs.append(e)
+        marks.append((it, _C.forward_stats()["reruns"], ts.ctx_stats()["growths"], torch.cuda.memory_reserved(dev)))
         if it % 1000 == 0 or it == 1:
             losses[it] = loss
     r0 = _C.forward_stats()
@@ -285,6 +289,18 @@ def config3(a, dev):
     _C.set_profiling(False)
     late_K = int(ts.last_K)
     ev = tc.events
+    # the slowest iterations and what ran in them (verdict r04: the 28-127 ms spike)
+    ev_at = {e["iteration"]: e for e in ev}
+    slow = []
+    for i in np.argsort(per)[::-1][:10]:
+        it, rr, gr, res = marks[i]
+        prev = marks[i - 1] if i > 0 else (it - 1, r0["reruns"], 0, res)
+        e = ev_at.get(it, {})
+        slow.append({"iteration": int(it), "ms": round(float(per[i]), 3), "densify": "total" in e,
+                     "reset": bool(e.get("reset")), "after_event": (it - 1) in ev_at,
+                     "sh_increment": it % sched.sh_interval == 0,
+                     "binning_rerun": rr > prev[1], "buffer_growths": gr - prev[2],
+                     "torch_reserved_growth_mb": round((res - prev[3]) / 2 ** 20, 1)})
     out = {"workload": f"train_single.py loop on a synthetic Street-sparse chunk: {info['views']} views "
                        f"({info['depth_only_views']} depth-only) of {info['W']}x{info['H']} (90 deg cube faces), "
                        f"{info['P_init']} initial Gaussians (10k skybox + 20k scaffold + LiDAR-like points), "
@@ -293,6 +309,7 @@ def config3(a, dev):
            "iteration_ms": {"mean": round(float(per.mean()), 4), "median": round(float(np.median(per)), 4),
                             "p90": round(float(np.percentile(per, 90)), 4), "max": round(float(per.max()), 3),
                             "source": "HIP events between iterations"},
+           "slowest_iterations": slow, "executor_buffers": ts.ctx_stats(),
            "P_init": info["P_init"], "P_final": ts.g.P, "P_max": max([e["P_after"] for e in ev] + [info["P_init"]]),
            "densify_events": sum(1 for e in ev if "total" in e), "opacity_resets": sum(1 for e in ev if e.get("reset")),
            "event_s": round(tc.event_s, 3), "capacity_reruns": int(r1["reruns"] - r0["reruns"]),

@@ -168,6 +168,11 @@ typedef struct gsr_train_ctx gsr_train_ctx;
 gsr_train_ctx *gsr_train_ctx_create(void);
 /* Waits for the last step's stream, then frees the context's device buffers. */
 void gsr_train_ctx_destroy(gsr_train_ctx *ctx);
+/* The context's buffer statistics: out[0] = buffer growths since creation (each re-allocates one
+ * grow-only buffer 1/4 larger than asked; stream-ordered, hipFreeAsync / hipMallocAsync from the
+ * device's default pool, unless GSR_STEP_SYNC_ALLOC=1), out[1] = bytes held, out[2] = 1 when the
+ * growth is stream-ordered.  Returns the number of values written (<= n).  ABI 5. */
+int gsr_train_ctx_stats(const gsr_train_ctx *ctx, int64_t *out, int n);
 
 typedef struct {
     int64_t P;   /* Gaussians */

@@ -378,8 +378,71 @@ __device__ __forceinline__ float wave_rs10(const float *v, int lane) {
     const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(e0), __float_as_uint(e0), false, false);
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
+// The same reduce-scatter over TWO instances' ten values at once (v = instance A's, w = B's): the
+// same partners in the same order (l^8, l^7, l^2, l^1, then rows 0+1 / 2+3), so every sum has the
+// bits wave_rs10 gives it, but the 20 values fill the stages that pad a lone instance's 10, and the
+// row pair ends in a reduce-scatter too (row 0 keeps one value, row 1 another) instead of both rows
+// holding the same sum: 47 VALU per pair instead of 2 x 26.  Each lane ends with ONE half-wave partial,
+// of value index wave_rs20_slot(lane) (0..9: A's, 10..19: B's, -1: padding).
+__device__ __forceinline__ float wave_rs20(const float *v, const float *w, int lane) {
+    const bool b1 = (lane >> 1) & 1, b0 = lane & 1;
+    // stage 1 (l^8): banks 0,1 (bit 3 clear) keep A's ten values, banks 2,3 B's
+    float k0, k1, k2, k3, k4, k5, k6, k7, k8, k9;
+    asm volatile("s_nop 1\n"
+                 GSR_DPP_KEEP("row_ror:8", "0x3", 0, 10) GSR_DPP_KEEP("row_ror:8", "0xc", 0, 20)
+                 GSR_DPP_KEEP("row_ror:8", "0x3", 1, 11) GSR_DPP_KEEP("row_ror:8", "0xc", 1, 21)
+                 GSR_DPP_KEEP("row_ror:8", "0x3", 2, 12) GSR_DPP_KEEP("row_ror:8", "0xc", 2, 22)
+                 GSR_DPP_KEEP("row_ror:8", "0x3", 3, 13) GSR_DPP_KEEP("row_ror:8", "0xc", 3, 23)
+                 GSR_DPP_KEEP("row_ror:8", "0x3", 4, 14) GSR_DPP_KEEP("row_ror:8", "0xc", 4, 24)
+                 GSR_DPP_KEEP("row_ror:8", "0x3", 5, 15) GSR_DPP_KEEP("row_ror:8", "0xc", 5, 25)
+                 GSR_DPP_KEEP("row_ror:8", "0x3", 6, 16) GSR_DPP_KEEP("row_ror:8", "0xc", 6, 26)
+                 GSR_DPP_KEEP("row_ror:8", "0x3", 7, 17) GSR_DPP_KEEP("row_ror:8", "0xc", 7, 27)
+                 GSR_DPP_KEEP("row_ror:8", "0x3", 8, 18) GSR_DPP_KEEP("row_ror:8", "0xc", 8, 28)
+                 GSR_DPP_KEEP("row_ror:8", "0x3", 9, 19) GSR_DPP_KEEP("row_ror:8", "0xc", 9, 29)
+                 : "=&v"(k0), "=&v"(k1), "=&v"(k2), "=&v"(k3), "=&v"(k4), "=&v"(k5), "=&v"(k6), "=&v"(k7),
+                   "=&v"(k8), "=&v"(k9)
+                 : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]),
+                   "v"(v[8]), "v"(v[9]), "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]),
+                   "v"(w[6]), "v"(w[7]), "v"(w[8]), "v"(w[9]));
+    // stage 2 (l^7, row_half_mirror): banks 0,2 (bit 2 clear) keep k0..k4, banks 1,3 k5..k9
+    float c0, c1, c2, c3, c4;
+    asm volatile("s_nop 1\n"
+                 GSR_DPP_KEEP("row_half_mirror", "0x5", 0, 5) GSR_DPP_KEEP("row_half_mirror", "0xa", 0, 10)
+                 GSR_DPP_KEEP("row_half_mirror", "0x5", 1, 6) GSR_DPP_KEEP("row_half_mirror", "0xa", 1, 11)
+                 GSR_DPP_KEEP("row_half_mirror", "0x5", 2, 7) GSR_DPP_KEEP("row_half_mirror", "0xa", 2, 12)
+                 GSR_DPP_KEEP("row_half_mirror", "0x5", 3, 8) GSR_DPP_KEEP("row_half_mirror", "0xa", 3, 13)
+                 GSR_DPP_KEEP("row_half_mirror", "0x5", 4, 9) GSR_DPP_KEEP("row_half_mirror", "0xa", 4, 14)
+                 : "=&v"(c0), "=&v"(c1), "=&v"(c2), "=&v"(c3), "=&v"(c4)
+                 : "v"(k0), "v"(k1), "v"(k2), "v"(k3), "v"(k4), "v"(k5), "v"(k6), "v"(k7), "v"(k8), "v"(k9));
+    // stage 3 (l^2): c0..c4 (+ c5 = 0): bit 1 keeps c0..c2 or c3, c4, pad
+    float d0 = b1 ? c3 : c0, d1 = b1 ? c4 : c1, d2 = b1 ? 0.f : c2;
+    const float u0 = b1 ? c0 : c3, u1 = b1 ? c1 : c4, u2 = b1 ? c2 : 0.f;
+    asm volatile("s_nop 1\n" GSR_DPP_RS("quad_perm:[2,3,0,1]", 0, 3) GSR_DPP_RS("quad_perm:[2,3,0,1]", 1, 4)
+                     GSR_DPP_RS("quad_perm:[2,3,0,1]", 2, 5)
+                 : "+v"(d0), "+v"(d1), "+v"(d2)
+                 : "v"(u0), "v"(u1), "v"(u2));
+    // stage 4 (l^1): d0..d2 (+ d3 = 0): bit 0 keeps d0, d1 or d2, pad
+    float e0 = b0 ? d2 : d0, e1 = b0 ? 0.f : d1;
+    const float x0 = b0 ? d0 : d2, x1 = b0 ? d1 : 0.f;
+    asm volatile("s_nop 1\n" GSR_DPP_RS("quad_perm:[1,0,3,2]", 0, 2) GSR_DPP_RS("quad_perm:[1,0,3,2]", 1, 3)
+                 : "+v"(e0), "+v"(e1)
+                 : "v"(x0), "v"(x1));
+    // rows 0+1 and 2+3: v_permlane16_swap(e0, e1) hands the even row the odd row's e0 and the odd row
+    // the even row's e1, so the even row keeps e0's sum and the odd row e1's
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(e0), __float_as_uint(e1), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 #undef GSR_DPP_RS
 #undef GSR_DPP_KEEP
+
+// Value index of lane's wave_rs20 result (0..19), or -1 for a padding slot: 10 b3 + 5 b2 + c with
+// t = row bit + 2 b0 (3: pad) and c = t + 3 b1 (5: pad).
+__device__ __forceinline__ int wave_rs20_slot(int lane) {
+    const int b3 = (lane >> 3) & 1, b2 = (lane >> 2) & 1, b1 = (lane >> 1) & 1, b0 = lane & 1, row = (lane >> 4) & 1;
+    const int t = row + 2 * b0;
+    const int c = t + 3 * b1;
+    return (t == 3 || c >= 5) ? -1 : 10 * b3 + 5 * b2 + c;
+}
 
 // Value index of lane's wave_rs10 result: 5 b3 + 3 b2 + (2 b1 + b0), or -1 for a padding slot.
 __device__ __forceinline__ int wave_rs10_slot(int lane) {

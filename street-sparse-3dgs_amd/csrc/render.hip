@@ -1029,7 +1029,7 @@ void launch_render_fwd(const Camera &cam, const GeomState &gs, const BinningStat
 #define GSR_BWD_BG_IN_S 1  // 0: upstream's separate background term (one more FMA per pixel)
 #endif
 #ifndef GSR_BWD_WAVES_PER_EU
-#define GSR_BWD_WAVES_PER_EU 1
+#define GSR_BWD_WAVES_PER_EU 4  // 4 waves per SIMD: the instance pairs would otherwise take 129 VGPRs (3 waves)
 #endif
 #ifndef GSR_TILE_REVERSE
 #define GSR_TILE_REVERSE 0
@@ -1194,7 +1194,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
     }
     const float sx = 0.5f * (float)W, sy = 0.5f * (float)H;
     const int rs_slot = wave_rs10_slot(lane);
+    const int rs20_slot = wave_rs20_slot(lane);
     (void)rs_slot;
+    (void)rs20_slot;
     StatAcc bst;
     uint64_t b_inst = 0, b_batches = 0;
 
@@ -1250,7 +1252,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
             if (GSR_BWD_HALVES) s_d[slot] = make_float4(qa.z, qa.w, qb.x, 0.f);
         }
         __syncthreads();
-        for (uint32_t j = 0; j < cnt; j++) {
+        // one compacted instance's replay over its sub-blocks: the ten lane sums q (dx moments
+        // included); returns whether any lane's pixel took it
+        const auto replay = [&](uint32_t j, float (&q)[10]) -> bool {
             const float4 a = s_a[j];
             const float4 b = s_b[j];
             const float4 c = s_c[j];
@@ -1260,7 +1264,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
             const float dx = a.x - pfx;
             const float adxdx_s = a.z * dx * dx;
             const float bdx_s = a.w * dx;
-            float q[10];
             bool any = false;
             // Sub-block k's replay.  The first active sub-block sets the ten lane sums, later ones
             // add to them, so a culled sub-block 0 costs no zero moves (the compiler had peeled
@@ -1366,6 +1369,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
             q[0] = dx * q[5];
             q[2] = dx * q[0];
             q[3] = dx * q[1];
+            return any;
+        };
+        // Instances in pairs: the two instances' twenty sums share one reduce-scatter (wave_rs20:
+        // 23.5 instead of 26 VALU per instance, one LDS park per pair); a lone last instance takes
+        // wave_rs10.  The sums' bits are the same either way (same partners, same order).
+        uint32_t j = 0;
+#ifndef GSR_BWD_PAIRS
+#define GSR_BWD_PAIRS 1
+#endif
+        if (GSR_BWD_PAIRS && GSR_BWD_HALVES) {
+            for (; j + 1 < cnt; j += 2) {
+                float qa[10], qb[10];
+                const bool anya = replay(j, qa);
+                const bool anyb = replay(j + 1, qb);
+                const float h = __any(anya || anyb) ? wave_rs20(qa, qb, lane) : 0.f;
+                if (rs20_slot >= 0) s_red[((j + (rs20_slot >= 10 ? 1u : 0u)) * 2 + (lane >> 5)) * 10 + rs20_slot % 10] = h;
+            }
+        }
+        for (; j < cnt; j++) {
+            float q[10];
+            const bool any = replay(j, q);
             // reduce-scatter: lane `rs_slot` of rows 1 and 3 parks its half-wave partial; the two
             // halves are added once per batch below instead of per instance
             float h = __any(any) ? wave_rs10(q, lane) : 0.f;

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdint>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -54,19 +55,55 @@ struct gsr_train_ctx {
     hipStream_t stream = nullptr;
     bool failed_alloc = false;
     bool one_written = false;
+    int64_t growths = 0;  // gsr_train_ctx_stats
+    // Stream-ordered growth (hipFreeAsync / hipMallocAsync from the device's pool, which keeps what is
+    // freed): a training loop whose P and K grow over its densification events re-sizes its buffers
+    // without a host wait -- the synchronous form (GSR_STEP_SYNC_ALLOC=1: wait for the stream, hipFree,
+    // hipMalloc) stalls the host at every growth and hipMalloc of a large block maps its pages.
+    const bool async_alloc = [] {
+        const char *e = std::getenv("GSR_STEP_SYNC_ALLOC");
+        return !(e && e[0] == '1');
+    }();
+    bool pool_ready = false;
 
-    // grow-only: a larger request waits for the stream (queued kernels may still use the old
-    // allocation), frees it and allocates 1/8 more than asked (rasterizer buffers follow K)
+    void pool_setup() {
+        if (pool_ready) return;
+        pool_ready = true;
+        int dev = 0;
+        hipMemPool_t pool;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+            uint64_t keep = UINT64_MAX;  // freed blocks stay in the pool for the next growth
+            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+        }
+    }
+
+    // grow-only, 1/4 more than asked (rasterizer buffers follow K)
     void *get(int slot, size_t bytes) {
         Buf &b = buf[slot];
         if (bytes <= b.cap && b.p) return b.p;
-        if (b.p) {
+        growths++;
+        const size_t want = std::max<size_t>(256, bytes + bytes / 4);
+        if (async_alloc) {
+            pool_setup();
+            // in stream order: work queued before (and the side streams joined into it) still reads the
+            // old block; everything after uses the new one
+            if (b.p) (void)hipFreeAsync(b.p, stream);
+            b.p = nullptr;
+            b.cap = 0;
+            if (hipMallocAsync(&b.p, want, stream) != hipSuccess) {
+                b.p = nullptr;
+                failed_alloc = true;
+                return nullptr;
+            }
+            b.cap = want;
+            return b.p;
+        }
+        if (b.p) {  // queued kernels may still use the old allocation
             if (hipStreamSynchronize(stream) != hipSuccess) return nullptr;
             (void)hipFree(b.p);
             b.p = nullptr;
             b.cap = 0;
         }
-        const size_t want = std::max<size_t>(256, bytes + bytes / 8);
         if (hipMalloc(&b.p, want) != hipSuccess) {
             b.p = nullptr;
             failed_alloc = true;
@@ -74,6 +111,11 @@ struct gsr_train_ctx {
         }
         b.cap = want;
         return b.p;
+    }
+    int64_t held() const {
+        int64_t n = 0;
+        for (const auto &b : buf) n += (int64_t)b.cap;
+        return n;
     }
     float *f32(int slot, size_t n) { return static_cast<float *>(get(slot, n * sizeof(float))); }
 
@@ -127,6 +169,14 @@ int invalid(const char *msg) {
 extern "C" {
 
 gsr_train_ctx *gsr_train_ctx_create(void) { return new (std::nothrow) gsr_train_ctx(); }
+
+int gsr_train_ctx_stats(const gsr_train_ctx *ctx, int64_t *out, int n) {
+    if (!ctx || !out || n < 0) return invalid("NULL context or stats buffer");
+    const int64_t v[3] = {ctx->growths, ctx->held(), ctx->async_alloc ? 1 : 0};
+    int k = 0;
+    for (; k < n && k < 3; k++) out[k] = v[k];
+    return k;
+}
 
 void gsr_train_ctx_destroy(gsr_train_ctx *ctx) {
     if (!ctx) return;

@@ -106,6 +106,7 @@ SIGNATURES = {
     "gsr_exposure_backward": (_i, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
     "gsr_train_ctx_create": (_vp, []),
     "gsr_train_ctx_destroy": (None, [_vp]),
+    "gsr_train_ctx_stats": (_i, [_vp, ctypes.POINTER(_i64), _i]),
     "gsr_train_step": (_i, [_vp, ctypes.POINTER(TrainStepArgs), ctypes.POINTER(_i64)]),
     # include/gsr_hier.h
     "gsr_interpolate_cut_forward": (_i, [_i64, _i, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,

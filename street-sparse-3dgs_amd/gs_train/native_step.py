@@ -41,6 +41,13 @@ class NativeTrainStep(TrainStep):
             raise RuntimeError("gsr_train_ctx_create failed")
         self._ctx = ctypes.c_void_p(ctx)
 
+    def ctx_stats(self) -> dict:
+        """The executor's grow-only buffers: growths since creation, bytes held, stream-ordered
+        growth (gsr_train_ctx_stats)."""
+        buf = (ctypes.c_int64 * 3)()
+        lib().gsr_train_ctx_stats(self._ctx, buf, 3)
+        return {"growths": int(buf[0]), "bytes": int(buf[1]), "stream_ordered": bool(buf[2])}
+
     def __del__(self):
         ctx = getattr(self, "_ctx", None)
         if ctx is not None and ctx.value:

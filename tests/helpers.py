@@ -155,3 +155,28 @@ def record_margins(name, **values):
     with open(path, "a") as f:
         f.write(json.dumps(dict(case=name, **{k: (float(v) if v is not None else None) for k, v in values.items()}))
                 + "\n")
+
+
+def assert_adam_trajectories_close(name, x, y, x0, lr, steps, atol, frac=0.999, margin=1.1):
+    """Two trajectories of one parameter under Adam from the same start x0 (a fused step and the
+    reference's formulation), after `steps` updates of learning rate <= lr (a number, or a tensor
+    broadcastable to x for per-column rates).
+
+    Every element: |x - y| <= 2 * margin * lr * steps + atol.  Each side's Adam update of an element
+    is at most ~lr in magnitude per step over these few steps (|m_hat / sqrt(v_hat)| <= 1 for
+    consistent gradients, less otherwise), so even an element whose near-zero gradient flipped sign
+    in fp32 on one side ends within twice the travel; anything further off is an indexing or
+    arithmetic error, not rounding.  The bulk (>= frac of the elements) agrees within atol.
+    Returns the measured margins (max |x - y| over the travel bound, the close fraction)."""
+    import torch
+    x, y, x0 = x.detach(), y.detach(), x0.detach()
+    d = (x - y).abs()
+    travel = torch.as_tensor(lr, dtype=d.dtype, device=d.device) * float(steps)
+    bound = 2.0 * margin * travel + atol
+    over = d > bound
+    assert not bool(over.any()), (name, "elements beyond the Adam travel bound", int(over.sum()),
+                                  float((d - bound).max()))
+    close = float(torch.isclose(x, y, rtol=0, atol=atol).float().mean())
+    assert close >= frac, (name, close)
+    assert not torch.equal(x, x0), (name, "did not move")
+    return float((d / (2.0 * travel).clamp_min(1e-30)).max()), close

@@ -104,26 +104,36 @@ def test_native_step_with_depth_only_views_equals_python_step(skybox, alpha):
 
 def test_depth_only_step_matches_reference_structured_step():
     """The depth-only iteration against the reference's torch formulation (ReferenceTrainStep: the
-    torch expression of :152-156, SH and exposure gradients zeroed, no exposure step)."""
-    from gs_train.harness import make_problem
+    torch expression of :152-156, SH and exposure gradients zeroed, no exposure step).  Every element
+    within Adam's travel bound (helpers.assert_adam_trajectories_close), the bulk within 1e-5, and
+    the locked skybox rows unmoved on both sides."""
+    from gs_train.harness import LR, make_problem
+    from helpers import assert_adam_trajectories_close, record_margins
     from train_torch_ref import ReferenceTrainStep
     names = ("_xyz", "_features_dc", "_opacity", "_scaling", "_rotation")
+    steps, sky = 4, 300
     res = {}
     for fused in (True, False):
         torch.manual_seed(0)
-        ts = make_problem(20_000, 256, 192, n_views=2, seed=2, depth=True, depth_only=2,
+        ts = make_problem(20_000, 256, 192, n_views=2, seed=2, depth=True, depth_only=2, skybox_points=sky,
                           step_cls=None if fused else ReferenceTrainStep)
         init = [getattr(ts.g, n).detach().clone() for n in names]
-        losses = [ts.step().item() for _ in range(4)]
+        xyz_lr = max(ts.xyz_lr(it) for it in range(0, steps + 2))
+        losses = [ts.step().item() for _ in range(steps)]
         res[fused] = (losses, [getattr(ts.g, n).detach().clone() for n in names], init,
                       ts.g._exposure.detach().clone())
     (la, pa, ia, ea), (lb, pb, _, eb) = res[True], res[False]
     np.testing.assert_allclose(la, lb, rtol=1e-5, atol=1e-7)
+    lrs = dict(_xyz=xyz_lr, _features_dc=LR["feature_lr"], _opacity=LR["opacity_lr"], _scaling=LR["scaling_lr"],
+               _rotation=LR["rotation_lr"])
     for n, x, y, x0 in zip(names, pa, pb, ia):
-        close = torch.isclose(x, y, rtol=0, atol=1e-5).float().mean().item()
-        assert close >= 0.999, (n, close)
-        if n != "_features_dc":
-            assert not torch.equal(x, x0), n  # the depth loss moved it
+        # the skybox rows: all six gradients zeroed (train_single.py:217-223), so Adam never moves them
+        assert torch.equal(x[:sky], x0[:sky]) and torch.equal(y[:sky], x0[:sky]), n
+        if n == "_features_dc":  # a depth-only view zeroes the SH gradients: momentum only
+            assert torch.isclose(x, y, rtol=0, atol=1e-5).float().mean().item() >= 0.999
+            continue
+        worst, close = assert_adam_trajectories_close(n, x, y, x0, lrs[n], steps, atol=1e-5)
+        record_margins(f"depth_only_step{n}", travel_frac=worst, close=close)
     assert torch.equal(ea, eb) and torch.equal(ea, torch.eye(3, 4, device=DEV)[None].expand_as(ea))
 
 
@@ -292,8 +302,13 @@ def test_chunk_loop_matches_reference_structured_loop():
     for k, (x, y, x0) in enumerate(zip(pa, pb, since[-1])):
         checks.append(("end", k, drift(x, y, x0)))
     print("drift / update per interval and parameter:", [(it, k, round(d, 4)) for it, k, d in checks])
+    from helpers import record_margins
     for it, k, d in checks:
-        assert d <= 0.1, (it, k, d)
+        record_margins(f"chunk_lockstep_drift_{it}_{k}", drift=d)
+    # bars ~5x the recorded drift (profiles/r05_parity_margins.jsonl: <= 0.0117 over the 100-iteration
+    # intervals between events, <= 0.043 over the last ~200 iterations, which the bar of 0.1 keeps)
+    for it, k, d in checks:
+        assert d <= (0.06 if it != "end" else 0.1), (it, k, d)
     # the same number of Gaussian Adam steps on both sides
     steps_a = [float(ta.optimizer.state[p]["step"]) for p in (ta.g._xyz, ta.g._opacity)]
     steps_b = [float(tb.optimizer.state[p]["step"]) for p in (tb.g._xyz, tb.g._opacity)]

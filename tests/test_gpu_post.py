@@ -88,7 +88,8 @@ def test_zero_grad_rows_matches_indexing():
 @pytest.mark.parametrize("steps", [1, 3])
 def test_post_step_matches_reference_formulation(steps):
     """PostTrainStep vs ReferencePostStep on the same views and the same cut limits."""
-    from gs_train.post import synthetic_post_problem
+    from gs_train.post import POST_LR, synthetic_post_problem
+    from helpers import assert_adam_trajectories_close, record_margins
     from train_torch_ref import ReferencePostStep
     torch.manual_seed(0)
     post = synthetic_post_problem(60_000, 320, 240, n_views=3, skybox=2000, n_anchors=500, seed=2)
@@ -105,13 +106,17 @@ def test_post_step_matches_reference_formulation(steps):
     np.testing.assert_allclose(la, lb, rtol=2e-5, atol=1e-7)
     got = (m._xyz, m._features, m._opacity, m._scaling, m._rotation)
     want = (ref._xyz, ref.features(), ref._opacity, ref._scaling, ref._rotation)
+    # per-element Adam travel bound; the bulk within 1e-3 of the largest move (an fp32-noise gradient
+    # may take an element the other way: Adam's first steps move it by ~lr * sign(grad))
+    col_lr = torch.full((1, m._features.shape[1], 1), POST_LR["feature_lr"] / 20.0, device=DEV)
+    col_lr[:, 0] = POST_LR["feature_lr"]
+    lrs = dict(xyz=max(post.xyz_lr(it) for it in range(0, steps + 2)), features=col_lr,
+               opacity=POST_LR["opacity_lr"], scaling=POST_LR["scaling_lr"], rotation=POST_LR["rotation_lr"])
     for name, x, y, x0 in zip(("xyz", "features", "opacity", "scaling", "rotation"), got, want, init):
         x, y = x.detach(), y.detach()
-        # Adam's first steps move an element by ~lr * sign(grad): an fp32-noise gradient may go the
-        # other way, so the bulk must agree
-        close = torch.isclose(x, y, rtol=0, atol=2e-6 + 1e-3 * (x - x0).abs().max().item()).float().mean().item()
-        assert close >= 0.999, (name, close)
-        assert not torch.equal(x, x0), name
+        atol = 2e-6 + 1e-3 * (x - x0).abs().max().item()
+        worst, close = assert_adam_trajectories_close(name, x, y, x0, lrs[name], steps, atol)
+        record_margins(f"post_step{steps}_{name}", travel_frac=worst, close=close)
     # the locked rows never move: the skybox (last rows) and the anchors
     S = m.skybox_points
     for x, x0 in zip(got, init):

@@ -7,7 +7,7 @@ OUT=gpurun_out/ab_$TAG; mkdir -p "$OUT"
 ARGS="--steps 50 --warmup 10 --metric-only"
 for r in $(seq 1 "$ROUNDS"); do
   timeout -k 10 120 python3 bench.py $ARGS > "$OUT/base_$r.json" 2>/dev/null || exit 1
-  for lib in vlibs/*.so; do
+  for lib in ${AB_LIBS:-vlibs/*.so}; do
     n=$(basename "$lib" .so)
     GSR_LIBRARY="$lib" timeout -k 10 120 python3 bench.py $ARGS > "$OUT/${n}_$r.json" 2>/dev/null || exit 1
   done
