@@ -225,7 +225,7 @@ def train_step_ms(P, W, H, steps, warmup, dev, street=True, reference=False, see
     return ms
 
 
-def config3(a, dev):
+def config3(a, dev, seed=0, ranks=None):
     """The config-3 stand-in (BASELINE.json configs[2]: train_single.py's whole loop per chunk; the
     example_dataset is absent): gs_train.chunk.TrainChunk over a synthetic Street-sparse chunk
     (street_chunk: cube faces along a street, LiDAR-like initial points, skybox + scaffold rows,
@@ -245,7 +245,7 @@ def config3(a, dev):
                               opacity_reset_interval=max(1, round(3000 * f)), densify_from_iter=round(500 * f),
                               densify_until_iter=round(15_000 * f), sh_interval=max(1, round(1000 * f)))
     t_set = time.perf_counter()
-    torch.manual_seed(0)
+    torch.manual_seed(seed)
     ts, info = street_chunk(NativeTrainStep, W=a.chunk_size, H=a.chunk_size, positions=a.chunk_positions,
                             n_truth=a.chunk_truth, n_init=a.chunk_init, iterations=n_it, device=dev)
     torch.cuda.synchronize()
@@ -268,6 +268,9 @@ def config3(a, dev):
             losses[it] = loss
     r0 = _C.forward_stats()
     torch.cuda.synchronize()
+    if ranks is not None:
+        ranks.barrier()
+        torch.cuda.synchronize()
     with quiet_gc():
         start = torch.cuda.Event(enable_timing=True)
         start.record()
@@ -275,6 +278,10 @@ def config3(a, dev):
         tc.run(callback=cb)
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
+        if ranks is not None:  # the job ends when the last rank's chunk does
+            ranks.barrier()
+            torch.cuda.synchronize()
+            job_wall = time.perf_counter() - t0
     r1 = _C.forward_stats()
     per = np.array([start.elapsed_time(evs[0])] + [evs[i].elapsed_time(evs[i + 1]) for i in range(len(evs) - 1)])
     psnr1 = view_psnr(ts)
@@ -320,6 +327,10 @@ def config3(a, dev):
            "late_raster_stages_ms": {k_: round(v_, 4) for k_, v_ in acc.items()}, "late_tile_instances": late_K,
            "data": "synthetic street chunk generated on the device (gs_train.chunk.street_chunk); the example_dataset "
                    "is not available offline"}
+    out["seed"] = seed
+    out["chunk_iterations_per_s"] = round(n_it / wall, 2)
+    if ranks is not None:
+        out["job_wall_s"] = round(ranks.max(job_wall), 3)
     del ts, tc
     torch.cuda.empty_cache()
     return out
@@ -1062,6 +1073,21 @@ def main():
     if world == 1 and not a.no_config3:
         log("config 3 stand-in: train_single.py loop on a synthetic street chunk")
         out["config3_proxy"] = config3(a, dev)
+    if not a.no_config4 and not a.no_config3:
+        # config 4 as the product runs it (scripts/full_train.py:171-232): one whole chunk per GPU --
+        # every rank trains its own synthetic street chunk (seed = chunk id = rank) through the
+        # train_single.py loop, no collective on the data path.  At N = 1 the chunk is config 3's run.
+        log("config 4: one whole chunk per rank")
+        one = out.get("config3_proxy") if world == 1 else config3(a, dev, seed=rank, ranks=ranks)
+        if one is not None:
+            walls = ranks.gather(one["chunk_wall_s"])
+            job = one.get("job_wall_s", one["chunk_wall_s"])
+            out["config4"]["chunks"] = {
+                "workload": f"{world} synthetic street chunk(s), one per rank (seed = rank), {a.chunk_iterations} "
+                            f"train_single.py iterations each ({one['workload']})",
+                "chunk_iterations_per_s": round(world * a.chunk_iterations / job, 2), "unit": "chunk-iterations/s",
+                "job_wall_s": job, "chunk_wall_s_per_rank": walls, "n_gpus": world, "scaling": "weak",
+                "P_final_rank0": one["P_final"], "collectives": "none on the data path (barriers + MAX of the walls)"}
     if world == 1 and not a.no_config5:
         log("config 5")
         out["config5"] = config5(a, dev)

@@ -210,7 +210,9 @@ int gsr_set_binning(int mode);
  * (a superblock list too long for LDS), out[4] = frames whose forward-split workers gave up waiting
  * for tile_order's release of their queue (the side stream did not run beside the main one; the
  * pool's second launch completed those frames exactly -- ABI 5), out[5] = host nanoseconds spent waiting
- * for K (num_rendered) in forward calls (ABI 5).  Returns the number of values written (<= n). */
+ * for K (num_rendered) in forward calls, out[6] / out[7] = frames forwarded with the forward split /
+ * the tile binning's superblock split armed (gsr_set_split_gate; ABI 5).  Returns the number of
+ * values written (<= n). */
 int gsr_forward_stats(int64_t *out, int n);
 
 /* Forget the calling thread's point-list capacity hint (the largest K of its last 256 frames per

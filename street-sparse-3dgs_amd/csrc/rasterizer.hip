@@ -157,7 +157,9 @@ int fail(int code, const std::string &msg) {
 // give-ups; their items were blended by the pool's second launch, the frame is exact).
 // g_kwait_ns: host time spent waiting for K (num_rendered) in the forward, summed (gsr_forward_stats[5]).
 std::atomic<int64_t> g_fwd_giveups{0}, g_kwait_ns{0};
-constexpr int kFwdStats = 6;
+// frames whose forward ran with the forward split / the tile binning's superblock split armed
+std::atomic<int64_t> g_fsplit_frames{0}, g_tbsplit_frames{0};
+constexpr int kFwdStats = 8;
 void collect_giveups() {
     if (!g_pinned) return;
     const uint32_t gu = __atomic_exchange_n(&g_pinned[kHostFwdGiveUp], 0u, __ATOMIC_SEQ_CST);
@@ -818,12 +820,15 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
         }
     }
     uint32_t seg_used = 0;
+    bool fsplit_armed = false, tbsplit_armed = false;
     auto bin_and_render = [&](int64_t cap, bool counted) -> int {
         const uint32_t tbs = !local && P > 0 ? tb_req : 0u;
+        tbsplit_armed = tbs != 0u;
         // backward / forward items are numbered tile + T * segment (32 bits)
         seg_used = seg_req && (uint64_t)T * (uint64_t)(cap / seg_req + 1) < (1ull << 32) ? seg_req : 0u;
         const uint32_t fseg_used =
             fseg_req && cap > 0 && (uint64_t)T * (uint64_t)(cap / fseg_req + 1) < (1ull << 32) ? fseg_req : 0u;
+        fsplit_armed = fseg_used != 0u;
         size_t bbytes = 0;
         carve_binning(nullptr, cap, &bbytes);
         void *bbase = binning_buffer(resize_ctx, bbytes);
@@ -926,6 +931,8 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
         if ((int64_t)bi != K) return fail(GSR_ERR_DEVICE, "binning: superblock instance total differs from K");
     }
     if (P > 0) g_frames.fetch_add(1, std::memory_order_relaxed);
+    if (fsplit_armed) g_fsplit_frames.fetch_add(1, std::memory_order_relaxed);
+    if (tbsplit_armed) g_tbsplit_frames.fetch_add(1, std::memory_order_relaxed);
     if (local && maxsb > (uint32_t)sort_cap()) {
         // an SB list too long for the LDS sort (the sort kernel wrote nothing): the frame again
         // through the global depth sort, at the capacity it needs
@@ -1129,7 +1136,8 @@ int gsr_forward_stats(int64_t *out, int n) {
     if (!out || n < 0) return fail(GSR_ERR_INVALID_ARGUMENT, "NULL stats buffer");
     collect_giveups();
     const int64_t v[kFwdStats] = {g_frames.load(), g_reruns.load(), g_local_frames.load(), g_fallbacks.load(),
-                                  g_fwd_giveups.load(), g_kwait_ns.load()};
+                                  g_fwd_giveups.load(), g_kwait_ns.load(), g_fsplit_frames.load(),
+                                  g_tbsplit_frames.load()};
     int k = 0;
     for (; k < n && k < kFwdStats; k++) out[k] = v[k];
     return k;

@@ -145,9 +145,10 @@ def forward_stats() -> dict:
     the local sort and how many of those fell back to the global sort, forward-split workers that
     gave up waiting for tile_order (their frames completed by the pool's second launch) and the host
     nanoseconds spent waiting for K (gsr_forward_stats)."""
-    buf = (ctypes.c_int64 * 6)()
-    n = _L.gsr_forward_stats(buf, 6)
-    keys = ("frames", "reruns", "local_sort", "fallbacks", "fwd_worker_giveups", "k_wait_ns")
+    buf = (ctypes.c_int64 * 8)()
+    n = _L.gsr_forward_stats(buf, 8)
+    keys = ("frames", "reruns", "local_sort", "fallbacks", "fwd_worker_giveups", "k_wait_ns", "fwd_split_frames",
+            "tb_split_frames")
     return {k: (int(buf[i]) if n > i else 0) for i, k in enumerate(keys)}
 
 

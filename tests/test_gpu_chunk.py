@@ -388,3 +388,42 @@ def test_native_dense_fallback_zeroes_skybox_rows(monkeypatch):
             ts.step()
             out[native] = _snapshot(ts)
     _assert_equal_snapshots(out[False], out[True])
+
+
+@pytest.mark.timeout(240)
+def test_street_chunk_full_size_through_densify_and_reset():
+    """The config-3 stand-in at full size in the suite (not only in bench): street_chunk's 1536^2 cube
+    faces (48 stations, 1M-Gaussian truth street, 330k initial rows) through train_single.py's loop on a
+    compressed schedule -- two densify events, an opacity reset (after which nothing saturates and the
+    vanishing-point tiles hold 100k+ instances) and SH increments.  Properties: every loss finite, P
+    grows, no NaN pixel in the views afterwards, capacity re-runs bounded, and the long-list paths
+    (the forward split and the tile binning's superblock split) armed after the reset."""
+    from diff_gaussian_rasterization import _C
+    from gs_train.chunk import ChunkSchedule, TrainChunk, street_chunk
+    from gs_train.native_step import NativeTrainStep
+    n_it = 400
+    torch.manual_seed(0)
+    ts, info = street_chunk(NativeTrainStep, iterations=n_it, device=DEV)
+    assert (info["W"], info["H"]) == (1536, 1536)
+    sched = ChunkSchedule(iterations=n_it, densification_interval=100, opacity_reset_interval=200,
+                          densify_from_iter=100, densify_until_iter=n_it, sh_interval=100)
+    P0 = ts.g.P
+    r0 = _C.forward_stats()
+    losses = []
+    tc = TrainChunk(ts, sched)
+    tc.run(callback=lambda it, loss: losses.append(loss.detach().reshape(-1)[:1]))
+    torch.cuda.synchronize()
+    r1 = _C.forward_stats()
+    assert torch.isfinite(torch.cat(losses)).all()
+    ev = tc.events
+    assert sum(1 for e in ev if "total" in e) >= 2 and any(e.get("reset") for e in ev), ev
+    assert max(e["P_after"] for e in ev) > P0
+    for k in range(0, len(ts.cams), 9):
+        img, invd, _, _ = ts.render(k, torch.zeros(3, device=DEV))
+        assert torch.isfinite(img).all() and torch.isfinite(invd).all(), k
+    d = {k: r1[k] - r0[k] for k in r1}
+    print("street chunk, full size:", {k: d[k] for k in ("frames", "reruns", "fwd_split_frames", "tb_split_frames",
+                                                          "fwd_worker_giveups")}, "P", P0, "->", ts.g.P)
+    assert d["reruns"] <= 0.1 * d["frames"], d
+    assert d["fwd_split_frames"] > 0 and d["tb_split_frames"] > 0, d
+    assert d["fwd_worker_giveups"] == 0, d
