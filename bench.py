@@ -419,34 +419,76 @@ def config5(a, dev):
                 split.append(time.perf_counter())
             return n, out
 
-    for _ in range(3):
-        frame()
-    torch.cuda.synchronize()
-    nf = 10
-    t0 = time.perf_counter()
-    for _ in range(nf):
-        n, (color, radii, _) = frame()
-    torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) / nf * 1e3
-    parts = []
-    for _ in range(3):  # synced split, separate from the timed frames
-        sp = [time.perf_counter()]
-        frame(sp)
-        parts.append([1e3 * (sp[i + 1] - sp[i]) for i in range(3)])
-    parts = np.median(np.array(parts), 0)
-    # the rasterizer's own stages for one more frame (HIP events on its stream)
+    # the same frame through the rasterizer's own cut (non-empty render_indices: render_post's blend
+    # fused into its preprocess and SH colour pass, the cut's rows read in place); the skybox rows
+    # ride in render_indices with weight 1, as render_post blends them
+    S = h["skybox"]
+    sky = torch.arange(N - S, N, dtype=torch.int32, device=dev)
+    ri2, pi2 = (torch.zeros(N + S, dtype=torch.int32, device=dev) for _ in range(2))
+    w2 = torch.ones(N + S, device=dev)
+    zero2 = torch.zeros(N + S, 3, device=dev)
+
+    def frame_fused(split=None):
+        with torch.no_grad():
+            n = expand_to_size(h["nodes"], h["boxes"], thr, cam, zero3, ri2, pi2, ni)
+            get_interpolation_weights(ni[:n], thr, h["nodes"], h["boxes"], cam_cpu, zero3, w2, kids)
+            ri2[n:n + S] = sky
+            pi2[n:n + S] = sky
+            w2[n:n + S] = 1.0
+            if split is not None:
+                torch.cuda.synchronize()
+                split.append(time.perf_counter())
+                split.append(split[-1])  # no blend pass of its own
+            rsf = rs._replace(render_indices=ri2[:n + S], parent_indices=pi2, interpolation_weights=w2)
+            out = GaussianRasterizer(rsf)(means3D=h["means3D"], means2D=zero2[:N], shs=h["shs"], colors_precomp=None,
+                                          opacities=h["opacities"], scales=h["scales"], rotations=h["rotations"],
+                                          cov3D_precomp=None)
+            if split is not None:
+                torch.cuda.synchronize()
+                split.append(time.perf_counter())
+            return n, out
+
     from diff_gaussian_rasterization import _C
-    _C.set_profiling(True)
-    frame()
-    stages = {k: round(v, 4) for k, v in _C.stage_times_ms().items()}
-    _C.set_profiling(False)
-    out = {"ms_per_frame": round(ms, 3), "raster_stages_ms": stages, "fwd_mpix_s": round(W * H / ms / 1e3, 1), "nodes": N,
-           "leaves": a.c5_leaves, "tau": a.c5_tau, "leaf_log_scale": a.c5_log_scale, "cut": n, "rendered": n + h["skybox"],
-           "visible": int((radii > 0).sum().item()), "width": W, "height": H,
-           "split_ms": {"cut_and_weights": round(float(parts[0]), 3), "blend": round(float(parts[1]), 3),
-                        "raster_fwd": round(float(parts[2]), 3)},
-           "workload": "expand_to_size + get_interpolation_weights + render_post LOD blend (fused) + rasterizer "
-                       "forward of the cut, no_grad, do_depth",
+
+    def measure(fr):
+        for _ in range(3):
+            fr()
+        torch.cuda.synchronize()
+        nf = 10
+        t0 = time.perf_counter()
+        for _ in range(nf):
+            n, (color, radii, _) = fr()
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / nf * 1e3
+        parts = []
+        for _ in range(3):  # synced split, separate from the timed frames
+            sp = [time.perf_counter()]
+            fr(sp)
+            parts.append([1e3 * (sp[i + 1] - sp[i]) for i in range(3)])
+        parts = np.median(np.array(parts), 0)
+        # the rasterizer's own stages for one more frame (HIP events on its stream)
+        _C.set_profiling(True)
+        fr()
+        stages = {k: round(v, 4) for k, v in _C.stage_times_ms().items()}
+        _C.set_profiling(False)
+        return ms, n, radii, parts, stages
+
+    ms, n, radii, parts, stages = measure(frame)
+    fms, fn, fradii, fparts, fstages = measure(frame_fused)
+    out = {"ms_per_frame": round(fms, 3), "raster_stages_ms": fstages, "fwd_mpix_s": round(W * H / fms / 1e3, 1),
+           "nodes": N, "leaves": a.c5_leaves, "tau": a.c5_tau, "leaf_log_scale": a.c5_log_scale, "cut": fn,
+           "rendered": fn + S, "visible": int((fradii > 0).sum().item()), "width": W, "height": H,
+           "split_ms": {"cut_and_weights": round(float(fparts[0]), 3), "raster_fwd": round(float(fparts[2]), 3)},
+           "workload": "expand_to_size + get_interpolation_weights + the rasterizer's own cut (render_indices / "
+                       "parent_indices / interpolation_weights: the LOD blend fused into its preprocess and SH colour "
+                       "pass), no_grad, do_depth",
+           "render_post_order": {
+               "ms_per_frame": round(ms, 3), "raster_stages_ms": stages, "cut": n,
+               "split_ms": {"cut_and_weights": round(float(parts[0]), 3), "blend": round(float(parts[1]), 3),
+                            "raster_fwd": round(float(parts[2]), 3)},
+               "workload": "the same frame in render_post's order: expand_to_size + get_interpolation_weights + the "
+                           "materialised LOD blend (interpolate_cut, one fused kernel) + the rasterizer forward of the "
+                           "blended rows"},
            "data": "synthetic hierarchy generated on the device (Morton-grouped tree, branching 4, 100k skybox)"}
     del h, raster
     torch.cuda.empty_cache()

@@ -146,6 +146,24 @@ __device__ __forceinline__ float quad_form(const float a[3], const float c[6], c
     return a[0] * s0 + a[1] * s1 + a[2] * s2;
 }
 
+// A hierarchy cut read in place (render_post's LOD blend fused into the preprocess and the SH colour
+// pass): row r of the frame is t x[c] + (1 - t) x[p] with c = ri[r], p = pi[r] (-1: the last of the
+// N rows, as torch's gather reads it), t = w[r], and the parent quaternion sign-aligned to the
+// child's -- the expressions of hier.hip's cut_fwd_kernel (gaussian_renderer/__init__.py:200-220),
+// so the fused frame's rows are bitwise the materialised blend's.  ri == nullptr: no cut.
+struct CutRef {
+    const int *ri, *pi;
+    const float *w;
+    int64_t N;
+};
+__device__ __forceinline__ float cut_lerp(float t, float a, float b) { return t * a + (1.f - t) * b; }
+__device__ __forceinline__ void cut_source(const CutRef &c, int64_t r, int64_t &ci, int64_t &pi, float &t) {
+    ci = c.ri[r];
+    pi = c.pi[r];
+    if (pi < 0) pi += c.N;
+    t = c.w[r];
+}
+
 // Parameter activations (scene/gaussian_model.py:39-47, getters :125-156), in torch's op order:
 // exp, x / max(||x||, 1e-12), sigmoid.  train.hip's activate kernels and the raw-parameter mode of
 // the rasterizer (GaussianInputs.raw: the native train step) use these, so both form the same bits.

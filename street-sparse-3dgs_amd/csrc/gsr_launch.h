@@ -29,7 +29,12 @@ struct GaussianInputs {
     const float *means3D, *shs, *colors_precomp, *opacities, *scales, *rotations, *cov3D_precomp;
     float scale_modifier;
     int raw;
+    // cut.ri != nullptr (render_post's blend fused, forwards without a backward): the P rows are
+    // blended on the fly from the cut.N rows the pointers above address (gsr_device.h CutRef)
+    CutRef cut{};
 };
+// the fused cut is supported for SH frames the colour pass takes (M = 16), scales + rotations
+bool cut_fusable(const GaussianInputs &in);
 // rasterizer.hip: gsr_rasterize_forward_ex / gsr_rasterize_backward on this thread take raw
 // parameters (plain frames: no precomputed covariance, no hierarchy cut)
 void set_raw_params(bool on);

@@ -26,7 +26,7 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
     const float *__restrict__ colors_precomp, const float *__restrict__ cov3D_precomp,
     const float *__restrict__ viewmatrix, const float *__restrict__ projmatrix, const float *__restrict__ campos,
     int W, int H, float tanx, float tany, float fx, float fy, int gx, int gy, GeomState gs, int *__restrict__ radii,
-    int raw) {
+    int raw, CutRef cut) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     // the depth sort's control words (tickets, histograms, lookback status) start at zero
     for (uint32_t c = (uint32_t)i; c < gs.ctrl_zero; c += gridDim.x * blockDim.x) gs.ctrl[c] = 0u;
@@ -40,7 +40,16 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
         gs.rect4[i] = 0u;
     else
         gs.rect8[i] = make_uint2(0u, 0u);
-    const float3 p = make_float3(ldp(means3D + 3 * i), ldp(means3D + 3 * i + 1), ldp(means3D + 3 * i + 2));
+    // a fused hierarchy cut: the row is the blend of its child and parent rows (plain loads: siblings
+    // share their parent's row, which then hits in cache)
+    const bool fused = cut.ri != nullptr;
+    int64_t ci = i, pi = i;
+    float ct = 1.f;
+    if (fused) cut_source(cut, i, ci, pi, ct);
+    const float3 p = fused ? make_float3(cut_lerp(ct, means3D[3 * ci], means3D[3 * pi]),
+                                         cut_lerp(ct, means3D[3 * ci + 1], means3D[3 * pi + 1]),
+                                         cut_lerp(ct, means3D[3 * ci + 2], means3D[3 * pi + 2]))
+                           : make_float3(ldp(means3D + 3 * i), ldp(means3D + 3 * i + 1), ldp(means3D + 3 * i + 2));
     const float3 pv = xf_point43(p, V);
     if (pv.z <= 0.2f) return;  // in_frustum (prefiltered is treated as a plain cull)
     const float4 ph = xf_point44(p, Pm);
@@ -52,9 +61,22 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
 #pragma unroll
         for (int k = 0; k < 6; k++) c3[k] = cov3D_precomp[6 * i + k];
     } else {
-        float3 s = make_float3(ldp(scales + 3 * i), ldp(scales + 3 * i + 1), ldp(scales + 3 * i + 2));
-        float4 q = make_float4(ldp(rotations + 4 * i), ldp(rotations + 4 * i + 1), ldp(rotations + 4 * i + 2),
-                               ldp(rotations + 4 * i + 3));
+        float3 s;
+        float4 q;
+        if (fused) {
+            s = make_float3(cut_lerp(ct, scales[3 * ci], scales[3 * pi]), cut_lerp(ct, scales[3 * ci + 1], scales[3 * pi + 1]),
+                            cut_lerp(ct, scales[3 * ci + 2], scales[3 * pi + 2]));
+            const float4 qc = reinterpret_cast<const float4 *>(rotations)[ci];
+            float4 qp = reinterpret_cast<const float4 *>(rotations)[pi];
+            const float dot = qc.x * qp.x + qc.y * qp.y + qc.z * qp.z + qc.w * qp.w;  // torch.bmm, left to right
+            if (dot < 0.f) qp = make_float4(-qp.x, -qp.y, -qp.z, -qp.w);
+            q = make_float4(cut_lerp(ct, qc.x, qp.x), cut_lerp(ct, qc.y, qp.y), cut_lerp(ct, qc.z, qp.z),
+                            cut_lerp(ct, qc.w, qp.w));
+        } else {
+            s = make_float3(ldp(scales + 3 * i), ldp(scales + 3 * i + 1), ldp(scales + 3 * i + 2));
+            q = make_float4(ldp(rotations + 4 * i), ldp(rotations + 4 * i + 1), ldp(rotations + 4 * i + 2),
+                            ldp(rotations + 4 * i + 3));
+        }
         if (raw) {  // the native step's pre-activation parameters (GaussianInputs.raw)
             s = make_float3(act_scale(s.x), act_scale(s.y), act_scale(s.z));
             q = act_rot(q);
@@ -113,7 +135,8 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
         col = make_float4(rgb[0], rgb[1], rgb[2], 0.f);
     }
     if (!kSplitColor) col.w = 1.f / pv.z;
-    const float op = raw ? act_opacity(ldp(opacities + i)) : ldp(opacities + i);
+    const float op = fused ? cut_lerp(ct, opacities[ci], opacities[pi])
+                           : raw ? act_opacity(ldp(opacities + i)) : ldp(opacities + i);
     const float ca_ = cc * det_inv, cb_ = -cb * det_inv, cc_ = ca * det_inv;
     // Half-extents of the region where alpha = op * exp(power) can reach 1/255:
     // power >= -t, t = ln(255 op)  <=>  d^T Q d <= 2t  ->  |dx| <= sqrt(2t (Q^-1)_xx).  Evaluated
@@ -180,11 +203,17 @@ constexpr int kColorThreads = kColorWaves * kWave;
 struct ShRows {
     float4 v[kShRow];
     bool vis;
+    int64_t c, p;  // a fused cut: the lane's row's child and parent rows, weight t
+    float t;
 };
 
 // The wave's 64 SH rows of row block vb into registers, 1 KiB contiguous per load instruction.
+// kCut (a fused hierarchy cut): each row is the blend of a child and a parent row -- both fetched
+// float4 by float4 as above from the rows' own places (the (child, parent, weight) of the wave's 64
+// rows staged in the wave's slice of s_idx), the blend formed in registers.
+template <bool kCut>
 __device__ __forceinline__ void color_fetch(int vb, ShRows &r, int P, int D, const float *__restrict__ shs,
-                                            const int *__restrict__ radii) {
+                                            const int *__restrict__ radii, const CutRef &cut, int4 *s_idx) {
     const int i = vb * blockDim.x + threadIdx.x;
     r.vis = i < P && radii[i] > 0;
     const int nc = (D + 1) * (D + 1);
@@ -192,11 +221,30 @@ __device__ __forceinline__ void color_fetch(int vb, ShRows &r, int P, int D, con
     const uint64_t need = __ballot(r.vis);
     const int64_t row0 = (int64_t)vb * blockDim.x + wv * kWave;
     const int cols = (nc * 3 + 3) / 4;  // float4 per row that hold active coefficients
-    const float4 *src4 = reinterpret_cast<const float4 *>(shs) + row0 * kShRow;
+    const float4 *src4 = reinterpret_cast<const float4 *>(shs) + (kCut ? 0 : row0 * kShRow);
+    if (kCut) {
+        r.c = r.p = 0;
+        r.t = 1.f;
+        if (r.vis) cut_source(cut, i, r.c, r.p, r.t);
+        __builtin_amdgcn_wave_barrier();  // the wave's previous reads of its slice are done
+        s_idx[wv * kWave + lane] = make_int4((int)r.c, (int)r.p, __float_as_int(r.t), 0);
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+    }
 #pragma unroll
     for (int k = 0; k < kShRow; k++) {
         const int f = k * kWave + lane, row = f / kShRow, col = f - row * kShRow;
         r.v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (kCut) {
+            if (((need >> row) & 1ull) && col < cols) {
+                const int4 x = s_idx[wv * kWave + row];
+                const float t = __int_as_float(x.z);
+                const float4 a = src4[(int64_t)x.x * kShRow + col], b = src4[(int64_t)x.y * kShRow + col];
+                r.v[k] = make_float4(cut_lerp(t, a.x, b.x), cut_lerp(t, a.y, b.y), cut_lerp(t, a.z, b.z),
+                                     cut_lerp(t, a.w, b.w));
+            }
+            continue;
+        }
         if (((need >> row) & 1ull) && col < cols) {
             if (GSR_SH_NT) {
                 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -210,6 +258,7 @@ __device__ __forceinline__ void color_fetch(int vb, ShRows &r, int P, int D, con
 }
 
 // Rows through the wave's LDS tile to one row per lane, then the colour of that lane's Gaussian.
+template <bool kCut>
 __device__ __forceinline__ void color_finish(int vb, const ShRows &r, float4 *s_sh, int P, int D,
                                              const float *__restrict__ means3D, const float *__restrict__ campos,
                                              const float *__restrict__ viewmatrix, const GeomState &gs) {
@@ -238,7 +287,11 @@ __device__ __forceinline__ void color_finish(int vb, const ShRows &r, float4 *s_
     }
 #pragma unroll
     for (int k = 0; k < 48; k++) sh[k] = k < nc * 3 ? sh[k] : 0.f;  // tail of a partial float4
-    const float3 p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
+    // the mean as the preprocess formed it (a fused cut: the same blend)
+    const float3 p = kCut ? make_float3(cut_lerp(r.t, means3D[3 * r.c], means3D[3 * r.p]),
+                                        cut_lerp(r.t, means3D[3 * r.c + 1], means3D[3 * r.p + 1]),
+                                        cut_lerp(r.t, means3D[3 * r.c + 2], means3D[3 * r.p + 2]))
+                          : make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
     float dir[3], dor[3];
     sh_dir(p, make_float3(campos[0], campos[1], campos[2]), dir, dor);
     uint8_t clamp_bits = 0;
@@ -259,30 +312,38 @@ __device__ __forceinline__ void color_finish(int vb, const ShRows &r, float4 *s_
 // GSR_COLOR_BLOCKS > 0: a persistent grid of that many blocks walks the row blocks (so the pass
 // can be held to part of the chip while latency-bound work runs beside it).  Each wave owns its
 // LDS tile (no block-wide barrier between row blocks).
+template <bool kCut>
 __global__ __launch_bounds__(kColorThreads) void preprocess_color_kernel(int P, int D, const float *__restrict__ means3D,
                                                                          const float *__restrict__ shs,
                                                                          const float *__restrict__ campos,
                                                                          const float *__restrict__ viewmatrix,
                                                                          const int *__restrict__ radii, GeomState gs,
-                                                                         int nvb) {
+                                                                         int nvb, CutRef cut) {
     __shared__ float4 s_sh[kColorWaves * kWave * kShPitch];
+    __shared__ int4 s_idx[kCut ? kColorWaves * kWave : 1];
     if (GSR_COLOR_PF) {
         ShRows cur, nxt;
         int vb = blockIdx.x;
-        if (vb < nvb) color_fetch(vb, cur, P, D, shs, radii);
+        if (vb < nvb) color_fetch<kCut>(vb, cur, P, D, shs, radii, cut, s_idx);
         for (; vb < nvb; vb += gridDim.x) {
             const int vn = vb + (int)gridDim.x;
-            if (vn < nvb) color_fetch(vn, nxt, P, D, shs, radii);
-            color_finish(vb, cur, s_sh, P, D, means3D, campos, viewmatrix, gs);
+            if (vn < nvb) color_fetch<kCut>(vn, nxt, P, D, shs, radii, cut, s_idx);
+            color_finish<kCut>(vb, cur, s_sh, P, D, means3D, campos, viewmatrix, gs);
             cur = nxt;
         }
     } else {
         for (int vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
             ShRows cur;
-            color_fetch(vb, cur, P, D, shs, radii);
-            color_finish(vb, cur, s_sh, P, D, means3D, campos, viewmatrix, gs);
+            color_fetch<kCut>(vb, cur, P, D, shs, radii, cut, s_idx);
+            color_finish<kCut>(vb, cur, s_sh, P, D, means3D, campos, viewmatrix, gs);
         }
     }
+}
+
+bool cut_fusable(const GaussianInputs &in) {
+    return in.shs && !in.colors_precomp && in.M == 16 && (reinterpret_cast<uintptr_t>(in.shs) % 16 == 0) &&
+           in.scales && in.rotations && !in.cov3D_precomp && (reinterpret_cast<uintptr_t>(in.rotations) % 16 == 0) &&
+           !in.raw;
 }
 
 bool color_split_supported(const GaussianInputs &in) {
@@ -297,7 +358,7 @@ void launch_preprocess(const GaussianInputs &in, const Camera &cam, const GeomSt
 #define GSR_PRE_ARGS                                                                                                 \
     in.P, in.D, in.M, in.means3D, in.scales, in.scale_modifier, in.rotations, in.opacities, in.shs, in.colors_precomp, \
         in.cov3D_precomp, cam.view, cam.proj, cam.campos, cam.W, cam.H, cam.tanx, cam.tany, cam.fx, cam.fy, cam.gx,   \
-        cam.gy, gs, radii, in.raw
+        cam.gy, gs, radii, in.raw, in.cut
     if (split_color)
         hipLaunchKernelGGL((preprocess_kernel<true, true>), dim3(blocks), dim3(256), 0, s, GSR_PRE_ARGS);
     else if (vec)
@@ -313,8 +374,12 @@ void launch_preprocess_color(const GaussianInputs &in, const Camera &cam, const 
     const int nvb = (in.P + kColorThreads - 1) / kColorThreads;
     const int cap = blocks > 0 ? blocks : GSR_COLOR_BLOCKS;
     const int grid = cap > 0 ? std::min(nvb, cap) : nvb;
-    hipLaunchKernelGGL(preprocess_color_kernel, dim3(grid), dim3(kColorThreads), 0, s, in.P, in.D, in.means3D, in.shs,
-                       cam.campos, cam.view, radii, gs, nvb);
+    if (in.cut.ri)
+        hipLaunchKernelGGL(preprocess_color_kernel<true>, dim3(grid), dim3(kColorThreads), 0, s, in.P, in.D, in.means3D,
+                           in.shs, cam.campos, cam.view, radii, gs, nvb, in.cut);
+    else
+        hipLaunchKernelGGL(preprocess_color_kernel<false>, dim3(grid), dim3(kColorThreads), 0, s, in.P, in.D,
+                           in.means3D, in.shs, cam.campos, cam.view, radii, gs, nvb, in.cut);
 }
 
 __global__ __launch_bounds__(256) void mark_visible_kernel(int P, const float *__restrict__ means3D,

@@ -587,13 +587,23 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
     const int64_t Nin = P;
     const int R = num_render;
     if (R > 0) P = R;
+    // render_post's blend fused into the preprocess and the SH colour pass (the cut's rows read in
+    // place, no R-row copy written and re-read) for frames no backward follows (render_hierarchy.py's
+    // no_grad frames); a frame a backward may follow keeps the blended rows in its geometry buffer,
+    // where the backward reads them
+#ifndef GSR_CUT_FUSED
+#define GSR_CUT_FUSED 1
+#endif
+    GaussianInputs probe{P, D, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp,
+                         scale_modifier, g_raw_params ? 1 : 0};
+    const bool fuse_cut = GSR_CUT_FUSED && R > 0 && !need_bwd && cut_fusable(probe);
 
     const Camera cam = make_camera(viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, width, height);
     const int T = cam.gx * cam.gy;
     const int npix = width * height;
 
     size_t ibytes = 0;
-    const size_t gbytes = geom_bytes(P, cam.gx, cam.gy, R, M);
+    const size_t gbytes = geom_bytes(P, cam.gx, cam.gy, fuse_cut ? 0 : R, M);
     if (!sb_grid_supported(sb_grid(cam.gx, cam.gy, P)))
         return fail(GSR_ERR_UNSUPPORTED, "image too large for the superblock grid");
     carve_image(nullptr, T, npix, &ibytes);
@@ -604,7 +614,7 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
     if (!clear_acc) gs.nacc = 0;
     note_forward_geom(gbase, need_bwd, clear_acc);
     const ImageState is = carve_image(ibase, T, npix, nullptr);
-    if (R > 0) {
+    if (R > 0 && !fuse_cut) {
         const CutRows cr = cut_rows_of(gbase, P, cam.gx, cam.gy, M);
         if ((rc = gsr_interpolate_cut_forward(Nin, M, R, 0, render_indices, parent_indices, interpolation_weights,
                                               means3D, scales, rotations, opacities, shs, cr.means, cr.scales,
@@ -622,6 +632,7 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
         return fail(GSR_ERR_UNSUPPORTED, "raw parameters with a hierarchy cut or precomputed covariances");
     GaussianInputs in{P, D, M, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp,
                       scale_modifier, g_raw_params ? 1 : 0};
+    if (fuse_cut) in.cut = CutRef{render_indices, parent_indices, interpolation_weights, Nin};
     hipStream_t side = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
     // GSR_COLOR_SERIAL=1 runs the SH colour pass on the main stream right after the preprocess:
@@ -630,6 +641,7 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
     // stream stays the default.
     const bool split = P > 0 && color_split_supported(in) &&
                        (GSR_COLOR_SERIAL || side_stream(s, &side, &fork, &join));
+    if (fuse_cut && !split) return fail(GSR_ERR_DEVICE, "hierarchy cut: the fused blend needs the SH colour pass");
     SideJoin sj;
     {
         StageTimer st(0, s);

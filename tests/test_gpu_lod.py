@@ -206,6 +206,52 @@ def _render_indices_equal_render_post_blend():
     assert torch.equal(m2a.grad[:n], m2b.grad) and int(m2a.grad[n:].abs().sum()) == 0
 
 
+@pytest.mark.parametrize("skybox", [0, 3000])
+def test_fused_cut_frame_equals_render_post_blend(skybox):
+    """A no_grad frame with non-empty render_indices (render_hierarchy.py's evaluation) reads the cut's
+    rows in place: render_post's blend fused into the preprocess and the SH colour pass, no R-row copy
+    (gsr_device.h CutRef).  Against render_post's order of work (interpolate_cut, then the rasterizer
+    on the R rows, skybox rows appended): image, inverse depth, radii and K bitwise equal.  The skybox
+    rides in render_indices as rows with weight 1 (their own parent), as render_post blends them."""
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, _C
+    from gs_train.hier import interpolate_cut
+    from gs_train.synthetic import synthetic_lod_hierarchy, tau_threshold
+    W, H = 1280, 720
+    h = synthetic_lod_hierarchy(300_000, W, H, DEV, seed=11, zmin=1.0, zmax=25.0, log_scale_mean=-3.5, skybox=skybox)
+    thr = tau_threshold(12.0, h["tanfovx"], W)
+    n, ri, pi, ni, w, k = _cut_hip(h, thr)
+    N = h["means3D"].shape[0]
+    assert 1000 < n < N
+    S = h["skybox"]
+    sky = torch.arange(N - S, N, dtype=torch.int32, device=DEV)
+    ri2 = torch.cat([ri[:n], sky])
+    pi2 = torch.cat([pi[:n], sky])
+    w2 = torch.cat([w[:n], torch.ones(S, device=DEV)])
+    t = lambda x: torch.tensor(x, dtype=torch.float32, device=DEV)
+    rs = dict(bg=t([0.1, 0.2, 0.3]), viewmatrix=t(h["view"]).reshape(4, 4), projmatrix=t(h["proj"]).reshape(4, 4),
+              campos=t(h["campos"]))
+    e = torch.empty(0, device=DEV)
+    with torch.no_grad():
+        f = _C.rasterize_gaussians(rs["bg"], h["means3D"], e, h["opacities"], h["scales"], h["rotations"], 1.0, e,
+                                   rs["viewmatrix"], rs["projmatrix"], float(h["tanfovx"]), float(h["tanfovy"]), H, W,
+                                   h["shs"], 3, rs["campos"], False, False, ri2, pi2, w2, k, True, need_backward=False)
+        bm, bs, br, bo, bsh = interpolate_cut(h["means3D"], h["scales"], h["rotations"], h["opacities"], h["shs"],
+                                              ri[:n], pi, w, S)
+        g = _C.rasterize_gaussians(rs["bg"], bm, e, bo, bs, br, 1.0, e, rs["viewmatrix"], rs["projmatrix"],
+                                   float(h["tanfovx"]), float(h["tanfovy"]), H, W, bsh, 3, rs["campos"], False, False,
+                                   None, None, None, None, True, need_backward=False)
+        # the same cut in a frame a backward may follow: blended rows kept in its geometry buffer
+        m = _C.rasterize_gaussians(rs["bg"], h["means3D"], e, h["opacities"], h["scales"], h["rotations"], 1.0, e,
+                                   rs["viewmatrix"], rs["projmatrix"], float(h["tanfovx"]), float(h["tanfovy"]), H, W,
+                                   h["shs"], 3, rs["campos"], False, False, ri2, pi2, w2, k, True, need_backward=True)
+    torch.cuda.synchronize()
+    assert f[0] == g[0] == m[0] > 0  # K
+    for a_, b_, c_ in zip(f[1:4], g[1:4], m[1:4]):  # colour, inverse depth, radii
+        assert torch.equal(a_, b_) and torch.equal(a_, c_)
+    # no R-row copy in the fused frame's geometry buffer (59 floats per row in the other)
+    assert f[4].numel() + 236 * (n + S) <= m[4].numel()
+
+
 def test_expand_to_size_capacity_with_multi_gaussian_nodes():
     """A node can hold several Gaussians (count_leafs + count_merged > 1), so the cut can be longer
     than the node count N: output arrays of N entries are refused (nothing written past them), and
