@@ -289,11 +289,17 @@ def config3(a, dev, seed=0, ranks=None):
     # of the trained chunk (the view cycle continues; these steps are outside the timed run)
     _C.set_profiling(True)
     acc, nprof = {}, 32
+    rel = []
     for _ in range(nprof):
         ts.step()
         for k_, v_ in _C.stage_times_ms().items():
             acc[k_] = acc.get(k_, 0.0) + v_ / nprof
+        # the sparse Adam's relevant rows (nonzero opacity gradient, train_single.py:226)
+        og = ts.grads["_opacity"] if hasattr(ts, "grads") else ts.g._opacity.grad
+        if og is not None:
+            rel.append((og != 0).float().mean())
     _C.set_profiling(False)
+    relevant_frac = round(float(torch.stack(rel).mean()), 4) if rel else None
     late_K = int(ts.last_K)
     ev = tc.events
     # the slowest iterations and what ran in them (verdict r04: the 28-127 ms spike)
@@ -325,6 +331,7 @@ def config3(a, dev, seed=0, ranks=None):
            "train_view_psnr_db": {"before": psnr0, "after": psnr1},
            "P_trace": [[e["iteration"], e["P_after"]] for e in ev][::4],
            "late_raster_stages_ms": {k_: round(v_, 4) for k_, v_ in acc.items()}, "late_tile_instances": late_K,
+           "late_relevant_row_frac": relevant_frac,
            "data": "synthetic street chunk generated on the device (gs_train.chunk.street_chunk); the example_dataset "
                    "is not available offline"}
     out["seed"] = seed

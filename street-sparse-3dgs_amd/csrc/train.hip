@@ -1084,6 +1084,104 @@ int flat_adam_runs(int n_groups, const gsr_adam_group *groups, int64_t P, FlatAd
     return fa.n;
 }
 
+// The relevant rows compacted first (sparse steps: OurAdam's `relevant` rows, train_single.py:226).
+// The row-block kernel above launches a wave per (64 rows, group) -- P / 64 x groups waves, most of
+// which (88% of the rows are irrelevant late in a street chunk) only read 64 flags and leave -- and
+// updates a relevant row's narrow groups lane = row, one 64-B line per few useful bytes.  Here:
+//   adam_compact_kernel  a grid-stride pass over the flags: each wave's relevant rows appended to a
+//                        list (one atomic per wave; Adam's rows are independent, so the order is
+//                        free), and the scale shrink of the rows no update touches;
+//   adam_rowlist_kernel  one wave per listed row (grid-stride): lane l updates element l of the
+//                        row's groups concatenated (59 at SH degree 3: xyz 3, f_dc 3, f_rest 45,
+//                        opacity 1, scaling 3, rotation 4), so the SH pair's 48 floats are ONE
+//                        192-B contiguous access per array, then the shrink of the row's scales.
+// With no relevant row (the dense fallback, OurAdam.py:214) the list pass is skipped and the row
+// kernel walks every row (the sparse-rows zero gradients of DenseRows applied).  Same per-element
+// arithmetic as adam_narrow (bits unchanged).  GSR_ADAM_ROWBLOCK=1: the row-block kernel (A/B).
+constexpr int kAdamListMaxLanes = 64;
+__device__ __forceinline__ uint32_t lane_prefix_u64(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+struct AdamLaneMap {
+    uint8_t group[kAdamListMaxLanes], col[kAdamListMaxLanes];
+    int lanes;      // elements per row (sum of the group widths)
+    int sh_lane0;   // the first of the three scaling lanes (the shrink), -1: none
+};
+
+__global__ __launch_bounds__(256) void adam_compact_kernel(const float *__restrict__ rel, int64_t P,
+                                                           const int *__restrict__ flag, int *__restrict__ list,
+                                                           int *__restrict__ count, ShrinkArgs sh) {
+    if (*flag == 0) return;  // the dense fallback: the row kernel takes every row (and shrinks them)
+    const int lane = threadIdx.x & 63;
+    const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t r0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; r0 < P; r0 += waves * 64) {
+        const int64_t row = r0 + lane;
+        const bool relv = row < P && rel[row] != 0.f;
+        const uint64_t m = __ballot(relv);
+        if (m) {
+            int base = 0;
+            if (lane == 0) base = atomicAdd(count, __popcll(m));
+            base = __builtin_amdgcn_readfirstlane(base);
+            if (relv) list[base + (int)lane_prefix_u64(m)] = (int)row;
+        }
+        if (!relv && sh.s_raw && row >= sh.first && row < P) {  // rows no update touches: shrunk here
+            float *sr = sh.s_raw + 3 * row;
+            const float x = expf(sr[0]), y = expf(sr[1]), z = expf(sr[2]);
+            if (fmaxf(fmaxf(x, y), z) > sh.limit) {
+                sr[0] = logf(x * 0.8f);
+                sr[1] = logf(y * 0.8f);
+                sr[2] = logf(z * 0.8f);
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void adam_rowlist_kernel(AdamArgs a, AdamLaneMap lm, const int *__restrict__ list,
+                                                           const int *__restrict__ count, int64_t P,
+                                                           const int *__restrict__ flag, float b1, float b2, float omb1,
+                                                           float omb2, float eps, ShrinkArgs sh, DenseRows dr) {
+    const int lane = threadIdx.x & 63;
+    const bool dense = *flag == 0;
+    const int64_t n = dense ? P : (int64_t)*count;
+    const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const bool act = lane < lm.lanes;
+    const gsr_adam_group &G = a.g[act ? lm.group[lane] : 0];
+    const int64_t col = act ? lm.col[lane] : 0;
+    for (int64_t k = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); k < n; k += waves) {
+        const int64_t row = dense ? k : (int64_t)list[k];
+        // the dense fallback over sparse rows: rows whose gradient reads as zero
+        const bool z = dense && (row < dr.skybox || (dr.live3 && dr.live3[3 * row + 2] == 0.f));
+        float p = 0.f;
+        if (act) {
+            const int64_t e = row * G.row_stride + col;
+            const float g = z ? 0.f : G.grad[e];
+            const float m0 = G.exp_avg[e], v0 = G.exp_avg_sq[e], p0 = G.param[e];
+            const float mm = m0 * b1 + omb1 * g;
+            const float vv = v0 * b2 + omb2 * (g * g);
+            const float denom = sqrtf(vv) / G.bias_correction2_sqrt + eps;
+            G.exp_avg[e] = mm;
+            G.exp_avg_sq[e] = vv;
+            p = p0 + (-G.step_size) * (mm / denom);
+            G.param[e] = p;
+        }
+        if (sh.s_raw && lm.sh_lane0 >= 0 && row >= sh.first) {
+            // the shrink of the row's freshly updated scales (shrink_scales_kernel's arithmetic)
+            const float sx = __shfl(p, lm.sh_lane0, 64), sy = __shfl(p, lm.sh_lane0 + 1, 64),
+                        sz = __shfl(p, lm.sh_lane0 + 2, 64);
+            const float x = expf(sx), y = expf(sy), zz = expf(sz);
+            if (fmaxf(fmaxf(x, y), zz) > sh.limit && lane >= lm.sh_lane0 && lane < lm.sh_lane0 + 3) {
+                const float c = lane == lm.sh_lane0 ? x : lane == lm.sh_lane0 + 1 ? y : zz;
+                sh.s_raw[3 * row + (lane - lm.sh_lane0)] = logf(c * 0.8f);
+            }
+        }
+    }
+}
+
+bool adam_rowblock() {  // read per call: A/B runs switch it
+    const char *e = std::getenv("GSR_ADAM_ROWBLOCK");
+    return e != nullptr && e[0] == '1';
+}
+
 // GSR_ADAM_DENSE_ROWS=1 sends a dense step through the row-block kernel instead (A/B).
 bool adam_dense_rows() {
     const char *e = std::getenv("GSR_ADAM_DENSE_ROWS");
@@ -1718,7 +1816,40 @@ int sparse_adam(int n_groups, const gsr_adam_group *groups, int64_t P, const flo
         int sh_group = -1;
         for (int i = 0; i < n_groups; i++)
             if (shrink_raw && groups[i].param == shrink_raw) sh_group = i;
-        hipLaunchKernelGGL(sparse_adam_rows_kernel,
+        // the compacted form when the row's elements fit one wave (and the shrink, if any, has its
+        // three scale lanes)
+        AdamLaneMap lm;
+        std::memset(&lm, 0, sizeof(lm));
+        lm.sh_lane0 = -1;
+        bool fits = relevance != nullptr && !adam_rowblock() && (!shrink_raw || (sh_group >= 0 && groups[sh_group].width == 3));
+        for (int i = 0; fits && i < n_groups; i++) {
+            if (lm.lanes + groups[i].width > kAdamListMaxLanes) {
+                fits = false;
+                break;
+            }
+            if (i == sh_group) lm.sh_lane0 = lm.lanes;
+            for (int c = 0; c < (int)groups[i].width; c++) {
+                lm.group[lm.lanes] = (uint8_t)i;
+                lm.col[lm.lanes++] = (uint8_t)c;
+            }
+        }
+        if (fits && P <= 0x7fffffff) {
+            int *buf = nullptr;  // the row list and its counter: stream-ordered scratch from the device pool
+            if (hipMallocAsync(reinterpret_cast<void **>(&buf), sizeof(int) * ((size_t)P + 64), s) != hipSuccess) {
+                set_last_error("gsr_sparse_adam_step: row list allocation failed");
+                return GSR_ERR_ALLOCATION;
+            }
+            int *count = buf, *list = buf + 64;
+            const ShrinkArgs sha{shrink_raw, shrink_first, shrink_limit};
+            (void)hipMemsetAsync(count, 0, sizeof(int), s);
+            const unsigned cb = (unsigned)std::min<int64_t>((P + 255) / 256, 4096);
+            hipLaunchKernelGGL(adam_compact_kernel, dim3(cb), dim3(256), 0, s, relevance, P, flag, list, count, sha);
+            hipLaunchKernelGGL(adam_rowlist_kernel, dim3(4096), dim3(256), 0, s, a, lm, (const int *)list,
+                               (const int *)count, P, flag, (float)beta1, (float)beta2, (float)(1.0 - beta1),
+                               (float)(1.0 - beta2), (float)eps, sha, DenseRows{live3, skybox});
+            (void)hipFreeAsync(buf, s);
+        } else
+            hipLaunchKernelGGL(sparse_adam_rows_kernel,
                            dim3((unsigned)((P + kAdamThreads - 1) / kAdamThreads), (unsigned)n_groups),
                            dim3(kAdamThreads), 0, s, a, relevance, P, (float)beta1, (float)beta2,
                            (float)(1.0 - beta1), (float)(1.0 - beta2), (float)eps, flag,
