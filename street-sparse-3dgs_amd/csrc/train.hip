@@ -1108,23 +1108,29 @@ struct AdamLaneMap {
     int sh_lane0;   // the first of the three scaling lanes (the shrink), -1: none
 };
 
-__global__ __launch_bounds__(256) void adam_compact_kernel(const float *__restrict__ rel, int64_t P,
-                                                           const int *__restrict__ flag, int *__restrict__ list,
-                                                           int *__restrict__ count, ShrinkArgs sh) {
+// Workgroup b owns the contiguous rows [b * per, (b + 1) * per): a first walk counts its relevant
+// rows (ballots) and shrinks the rows no update touches, ONE atomic reserves the workgroup's run
+// of the list, a second walk (the flags again, now cache-hot) writes the rows.  One atomic per
+// wave instead (the first version) put ~16K returning atomics on one word per call, which
+// saturates at ~88 per us (MI355X_MICROARCH.md, dequeue): 164 us per call at 1M rows.
+constexpr int kCompactThreads = 1024;
+constexpr int kCompactWaves = kCompactThreads / 64;
+constexpr int kCompactMaxBlocks = 256;
+__global__ __launch_bounds__(kCompactThreads) void adam_compact_kernel(const float *__restrict__ rel, int64_t P,
+                                                                       const int *__restrict__ flag, int *__restrict__ list,
+                                                                       int *__restrict__ count, ShrinkArgs sh) {
     if (*flag == 0) return;  // the dense fallback: the row kernel takes every row (and shrinks them)
-    const int lane = threadIdx.x & 63;
-    const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
-    for (int64_t r0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; r0 < P; r0 += waves * 64) {
-        const int64_t row = r0 + lane;
-        const bool relv = row < P && rel[row] != 0.f;
-        const uint64_t m = __ballot(relv);
-        if (m) {
-            int base = 0;
-            if (lane == 0) base = atomicAdd(count, __popcll(m));
-            base = __builtin_amdgcn_readfirstlane(base);
-            if (relv) list[base + (int)lane_prefix_u64(m)] = (int)row;
-        }
-        if (!relv && sh.s_raw && row >= sh.first && row < P) {  // rows no update touches: shrunk here
+    __shared__ uint32_t s_wc[kCompactWaves];
+    __shared__ int s_base;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t per = ((P + gridDim.x - 1) / gridDim.x + kCompactThreads - 1) / kCompactThreads * kCompactThreads;
+    const int64_t r0 = (int64_t)blockIdx.x * per, r1 = min(P, r0 + per);
+    uint32_t cnt = 0;
+    for (int64_t b = r0 + (int64_t)w * 64; b < r1; b += kCompactThreads) {
+        const int64_t row = b + lane;
+        const bool relv = row < r1 && rel[row] != 0.f;
+        cnt += (uint32_t)__popcll(__ballot(relv));
+        if (!relv && sh.s_raw && row >= sh.first && row < r1) {  // rows no update touches: shrunk here
             float *sr = sh.s_raw + 3 * row;
             const float x = expf(sr[0]), y = expf(sr[1]), z = expf(sr[2]);
             if (fmaxf(fmaxf(x, y), z) > sh.limit) {
@@ -1133,6 +1139,24 @@ __global__ __launch_bounds__(256) void adam_compact_kernel(const float *__restri
                 sr[2] = logf(z * 0.8f);
             }
         }
+    }
+    if (lane == 0) s_wc[w] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (int k = 0; k < kCompactWaves; k++) tot += s_wc[k];
+        s_base = tot ? atomicAdd(count, (int)tot) : 0;
+    }
+    __syncthreads();
+    if (r0 >= r1) return;
+    int at = s_base;
+    for (int k = 0; k < w; k++) at += (int)s_wc[k];
+    for (int64_t b = r0 + (int64_t)w * 64; b < r1; b += kCompactThreads) {
+        const int64_t row = b + lane;
+        const bool relv = row < r1 && rel[row] != 0.f;
+        const uint64_t m = __ballot(relv);
+        if (relv) list[at + (int)lane_prefix_u64(m)] = (int)row;
+        at += __popcll(m);
     }
 }
 
@@ -1842,8 +1866,10 @@ int sparse_adam(int n_groups, const gsr_adam_group *groups, int64_t P, const flo
             int *count = buf, *list = buf + 64;
             const ShrinkArgs sha{shrink_raw, shrink_first, shrink_limit};
             (void)hipMemsetAsync(count, 0, sizeof(int), s);
-            const unsigned cb = (unsigned)std::min<int64_t>((P + 255) / 256, 4096);
-            hipLaunchKernelGGL(adam_compact_kernel, dim3(cb), dim3(256), 0, s, relevance, P, flag, list, count, sha);
+            const unsigned cb = (unsigned)std::max<int64_t>(
+                1, std::min<int64_t>((P + kCompactThreads - 1) / kCompactThreads, kCompactMaxBlocks));
+            hipLaunchKernelGGL(adam_compact_kernel, dim3(cb), dim3(kCompactThreads), 0, s, relevance, P, flag, list,
+                               count, sha);
             hipLaunchKernelGGL(adam_rowlist_kernel, dim3(4096), dim3(256), 0, s, a, lm, (const int *)list,
                                (const int *)count, P, flag, (float)beta1, (float)beta2, (float)(1.0 - beta1),
                                (float)(1.0 - beta2), (float)eps, sha, DenseRows{live3, skybox});
