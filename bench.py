@@ -263,11 +263,15 @@ def config3(a, dev, seed=0, ranks=None):
         e = torch.cuda.Event(enable_timing=True)
         e.record()
         evs.append(e)
-        marks.append((it, _C.forward_stats()["reruns"], ts.ctx_stats()["growths"], torch.cuda.memory_reserved(dev)))
+        fs = _C.forward_stats()
+        marks.append((it, fs["reruns"], ts.ctx_stats()["growths"], torch.cuda.memory_reserved(dev),
+                      fs["fwd_split_frames"], fs["tb_split_frames"], fs["fwd_worker_giveups"],
+                      int(getattr(getattr(ts, "_args", None), "image_index", -1)), int(getattr(ts, "last_K", 0))))
         if it % 1000 == 0 or it == 1:
             losses[it] = loss
     r0 = _C.forward_stats()
     torch.cuda.synchronize()
+    _C.fwd_pool_stats(reset=True)
     if ranks is not None:
         ranks.barrier()
         torch.cuda.synchronize()
@@ -283,6 +287,7 @@ def config3(a, dev, seed=0, ranks=None):
             torch.cuda.synchronize()
             job_wall = time.perf_counter() - t0
     r1 = _C.forward_stats()
+    pool = _C.fwd_pool_stats()
     per = np.array([start.elapsed_time(evs[0])] + [evs[i].elapsed_time(evs[i + 1]) for i in range(len(evs) - 1)])
     psnr1 = view_psnr(ts)
     # where a late iteration's time goes: the rasterizer's stages (HIP events) over 32 more steps
@@ -306,14 +311,19 @@ def config3(a, dev, seed=0, ranks=None):
     ev_at = {e["iteration"]: e for e in ev}
     slow = []
     for i in np.argsort(per)[::-1][:10]:
-        it, rr, gr, res = marks[i]
-        prev = marks[i - 1] if i > 0 else (it - 1, r0["reruns"], 0, res)
+        it, rr, gr, res, fsf, tbf, gup, view_k, kk = marks[i]
+        prev = marks[i - 1] if i > 0 else (it - 1, r0["reruns"], 0, res, r0["fwd_split_frames"],
+                                           r0["tb_split_frames"], r0["fwd_worker_giveups"], -1, 0)
         e = ev_at.get(it, {})
+        # the view, its instance count and whether the frame's forward / tile-binning splits were armed
+        # (the split gate arms them for 256 frames after a frame with long lists)
         slow.append({"iteration": int(it), "ms": round(float(per[i]), 3), "densify": "total" in e,
                      "reset": bool(e.get("reset")), "after_event": (it - 1) in ev_at,
                      "sh_increment": it % sched.sh_interval == 0,
                      "binning_rerun": rr > prev[1], "buffer_growths": gr - prev[2],
-                     "torch_reserved_growth_mb": round((res - prev[3]) / 2 ** 20, 1)})
+                     "torch_reserved_growth_mb": round((res - prev[3]) / 2 ** 20, 1),
+                     "view": view_k, "K": kk, "fwd_split_armed": fsf > prev[4], "tb_split_armed": tbf > prev[5],
+                     "fwd_worker_giveups": gup - prev[6]})
     out = {"workload": f"train_single.py loop on a synthetic Street-sparse chunk: {info['views']} views "
                        f"({info['depth_only_views']} depth-only) of {info['W']}x{info['H']} (90 deg cube faces), "
                        f"{info['P_init']} initial Gaussians (10k skybox + 20k scaffold + LiDAR-like points), "
@@ -332,6 +342,11 @@ def config3(a, dev, seed=0, ranks=None):
            "P_trace": [[e["iteration"], e["P_after"]] for e in ev][::4],
            "late_raster_stages_ms": {k_: round(v_, 4) for k_, v_ in acc.items()}, "late_tile_instances": late_K,
            "late_relevant_row_frac": relevant_frac,
+           "fwd_split_frames": int(r1["fwd_split_frames"] - r0["fwd_split_frames"]),
+           "tb_split_frames": int(r1["tb_split_frames"] - r0["tb_split_frames"]),
+           "fwd_pool": {**{k_: (round(v_, 4) if isinstance(v_, float) else v_) for k_, v_ in pool.items()},
+                        "source": "s_memrealtime ticks summed over the worker pool's workgroups (gsr_fwd_pool_stats): "
+                                  "busy = lifetime - waits for tile_order's release - waits for predecessor segments"},
            "data": "synthetic street chunk generated on the device (gs_train.chunk.street_chunk); the example_dataset "
                    "is not available offline"}
     out["seed"] = seed

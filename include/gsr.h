@@ -215,6 +215,13 @@ int gsr_set_binning(int mode);
  * values written (<= n). */
 int gsr_forward_stats(int64_t *out, int n);
 
+/* The forward-split worker pool's time since load (or the last reset), in s_memrealtime ticks of
+ * 10 ns summed over its workgroups: out[0] waiting for tile_order's release of the queue, out[1]
+ * waiting for predecessor segments' transmittance, out[2] the workgroups' lifetimes, out[3] the
+ * workgroups.  The pool's busy fraction is 1 - (out[0] + out[1]) / out[2].  Synchronises the
+ * device; reset != 0 zeroes the counters.  Returns the number of values written (<= n). */
+int gsr_fwd_pool_stats(int64_t *out, int n, int reset);
+
 /* Forget the calling thread's point-list capacity hint (the largest K of its last 256 frames per
  * device) and its split-gate history: the next frame reads K before binning, as the first one does,
  * and the gated splits wait for a long-list frame again.  For a caller that switches to a much

@@ -39,6 +39,14 @@ __device__ __forceinline__ float gexp2(float x) { return __builtin_amdgcn_exp2f(
 #define GSR_BLEND_STATS 0
 #endif
 __device__ unsigned long long g_blend_stats[16];
+// The forward-split worker pool's time (always on; gsr_fwd_pool_stats): s_memrealtime ticks (100 MHz)
+// summed over workgroups -- [0] waiting for tile_order's release of the queue (workers launched
+// ahead), [1] waiting for predecessor segments' transmittance rows, [2] workgroup lifetimes, [3]
+// workgroups.  Busy = [2] - [0] - [1] (dequeues, blends, the tiles' final sums).
+#ifndef GSR_FWD_POOL_STATS
+#define GSR_FWD_POOL_STATS 1
+#endif
+__device__ unsigned long long g_fwd_pool_ticks[4];
 // StatAcc::flush writes (pairs, live lanes, live halves, live rows, live quads) at its base index
 enum BlendStat { kBwdPairs, kBwdLive, kBwdHalves, kBwdRows, kBwdQuads, kBwdInst, kBwdBatches, kFwdPairs, kFwdLive,
                  kFwdHalves, kFwdRows, kFwdQuads, kFwdAcc, kBwdTiles };
@@ -308,7 +316,9 @@ __device__ void fwd_seg_worker(const uint2 *__restrict__ ranges, const uint32_t 
                                uint32_t *__restrict__ bwd_cnt, uint32_t *__restrict__ bwd_cls, int ntiles, uint32_t seg_len,
                                uint32_t fseg_len, uint32_t *bin_base, uint32_t *fctl, float4 *sa, float4 *sb,
                                float4 *sc, uint32_t *s_work, uint32_t *s_scalar, const uint32_t *ready,
-                               FwdSpin spin) {
+                               FwdSpin spin, uint64_t &t_ready, uint64_t &t_flags) {
+    // t_ready / t_flags (thread 0, GSR_FWD_POOL_STATS): s_memrealtime ticks spent waiting for the
+    // queue's release and for predecessor segments' flags
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const FwdSegLayout f = fseg_layout(bin_base, kf, seg_len, fseg_len);
     float *ck = seg_len && bwd_cnt ? reinterpret_cast<float *>(reinterpret_cast<char *>(bin_base) + ck_offset(kf)) : nullptr;
@@ -321,6 +331,7 @@ __device__ void fwd_seg_worker(const uint2 *__restrict__ ranges, const uint32_t 
         // stream (launch_render_fwd_cleanup) then takes every item still queued -- the frame stays
         // exact, only slower.
         if (threadIdx.x == 0) {
+            const uint64_t t0 = GSR_FWD_POOL_STATS ? __builtin_amdgcn_s_memrealtime() : 0ull;
             uint32_t ok = 1u, spins = 0;
             // spin.ready == kFwdReadyNever (fault injection, tests): leave as if the word never came
             while (spin.ready == kFwdReadyNever || !__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
@@ -332,6 +343,7 @@ __device__ void fwd_seg_worker(const uint2 *__restrict__ ranges, const uint32_t 
                 }
                 __builtin_amdgcn_s_sleep(4);
             }
+            if (GSR_FWD_POOL_STATS) t_ready += __builtin_amdgcn_s_memrealtime() - t0;
             s_scalar[2] = ok;
         }
         wg_acquire();
@@ -374,6 +386,7 @@ __device__ void fwd_seg_worker(const uint2 *__restrict__ ranges, const uint32_t 
         bool hung = false;
         if (sgi > 0) {
             if (threadIdx.x == 0) {
+                const uint64_t t0 = GSR_FWD_POOL_STATS ? __builtin_amdgcn_s_memrealtime() : 0ull;
                 uint32_t ok = 1u;
                 for (uint32_t j = 0; j < sgi && ok; j++) {
                     uint32_t spins = 0;
@@ -390,6 +403,7 @@ __device__ void fwd_seg_worker(const uint2 *__restrict__ ranges, const uint32_t 
                         __builtin_amdgcn_s_sleep(2);
                     }
                 }
+                if (GSR_FWD_POOL_STATS) t_flags += __builtin_amdgcn_s_memrealtime() - t0;
                 s_scalar[2] = ok;
             }
             wg_acquire();
@@ -503,9 +517,19 @@ __global__ __launch_bounds__(kWave * kPixPerLane) void render_fwd_seg_kernel(
     __shared__ float4 s_c[kPixPerLane][kWave];
     __shared__ uint32_t s_work[kPixPerLane], s_scalar[3];
     const int w = threadIdx.x >> 6;
+    const uint64_t t0 = GSR_FWD_POOL_STATS ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    uint64_t t_ready = 0, t_flags = 0;
     fwd_seg_worker(ranges, point_list, W, H, gx, rec, bg, out_color, out_invd, final_T, n_contrib, tile_work,
                    kdev ? *kdev : cap, sort_err, bwd_cnt, bwd_cls, ntiles, seg_len, fseg_len, bin_base, fctl, s_a[w],
-                   s_b[w], s_c[w], s_work, s_scalar, ready, spin);
+                   s_b[w], s_c[w], s_work, s_scalar, ready, spin, t_ready, t_flags);
+    if (GSR_FWD_POOL_STATS && threadIdx.x == 0) {
+        // the pool's time split (gsr_fwd_pool_stats): four no-return atomics per workgroup and frame
+        const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+        atomicAdd(&g_fwd_pool_ticks[0], (unsigned long long)t_ready);
+        atomicAdd(&g_fwd_pool_ticks[1], (unsigned long long)t_flags);
+        atomicAdd(&g_fwd_pool_ticks[2], (unsigned long long)(t1 - t0));
+        atomicAdd(&g_fwd_pool_ticks[3], 1ull);
+    }
 }
 
 #ifndef GSR_FWD_SEG_INKERNEL
@@ -560,10 +584,11 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) GSR_FWD_ATTR void ren
         if (fseg_len) {
             if (bidx < (uint32_t)kFwdWorkers) {
                 __shared__ uint32_t s_scalar[3];
+                uint64_t t_ready = 0, t_flags = 0;
                 fwd_seg_worker(ranges, point_list, W, H, gx, rec, bg, out_color, out_invd, final_T, n_contrib,
                                tile_work, kdev ? *kdev : cap, sort_err, bwd_cnt, bwd_cls, ntiles, seg_len, fseg_len,
                                bin_base, fctl, s_a[threadIdx.x >> 6], s_b[threadIdx.x >> 6], s_c[threadIdx.x >> 6],
-                               s_work, s_scalar, nullptr, spin);
+                               s_work, s_scalar, nullptr, spin, t_ready, t_flags);
                 return;
             }
             bidx -= (uint32_t)kFwdWorkers;
@@ -1531,5 +1556,18 @@ extern "C" int gsr_blend_stats(int64_t *out, int n, int reset) {
     }
     int k = 0;
     for (; k < n && k < 16; k++) out[k] = (int64_t)v[k];
+    return k;
+}
+
+extern "C" int gsr_fwd_pool_stats(int64_t *out, int n, int reset) {
+    unsigned long long v[4] = {};
+    if (!out || n < 0) return -1;
+    if (hipMemcpyFromSymbol(v, HIP_SYMBOL(gsr::g_fwd_pool_ticks), sizeof(v)) != hipSuccess) return -3;
+    if (reset) {
+        const unsigned long long z[4] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(gsr::g_fwd_pool_ticks), z, sizeof(z)) != hipSuccess) return -3;
+    }
+    int k = 0;
+    for (; k < n && k < 4; k++) out[k] = (int64_t)v[k];
     return k;
 }

@@ -152,6 +152,19 @@ def forward_stats() -> dict:
     return {k: (int(buf[i]) if n > i else 0) for i, k in enumerate(keys)}
 
 
+def fwd_pool_stats(reset: bool = False) -> dict:
+    """The forward-split worker pool's time (gsr_fwd_pool_stats; synchronises the device): seconds
+    its workgroups spent waiting for tile_order's release of the queue (ready), waiting for
+    predecessor segments (flags), in total, the workgroup count and the busy fraction."""
+    buf = (ctypes.c_int64 * 4)()
+    n = _L.gsr_fwd_pool_stats(buf, 4, 1 if reset else 0)
+    if n < 4:
+        raise RuntimeError(f"gsr_fwd_pool_stats failed ({n})")
+    ready, flags, total = (buf[i] * 1e-8 for i in range(3))
+    return {"ready_wait_s": ready, "flag_wait_s": flags, "total_s": total, "workgroups": int(buf[3]),
+            "busy_frac": (1.0 - (ready + flags) / total) if total > 0 else None}
+
+
 def frame_stats(geomBuffer, P, image_height, image_width) -> dict:
     """Level-1 binning entries, tile instances, tile_bin split items and the longest superblock
     list of the frame whose geometry buffer this is (gsr_frame_stats; one device sync)."""

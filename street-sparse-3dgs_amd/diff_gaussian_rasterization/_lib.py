@@ -74,6 +74,7 @@ SIGNATURES = {
     "gsr_segment_layout_check": (_i, [ctypes.c_int64, _i, _i, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     "gsr_frame_stats": (_i, [_vp, _i, _i, _i, ctypes.POINTER(_i64), _i]),
     "gsr_blend_stats": (_i, [ctypes.POINTER(_i64), _i, _i]),
+    "gsr_fwd_pool_stats": (_i, [ctypes.POINTER(_i64), _i, _i]),
     "gsr_debug_trace": (_i, [ctypes.POINTER(_i64), _i, _i]),
     "gsr_set_true_scale_gradient": (_i, [_i]),
     "gsr_set_deterministic": (_i, [_i]),
