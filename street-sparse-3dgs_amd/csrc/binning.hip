@@ -112,8 +112,9 @@ __global__ __launch_bounds__(1024) void sb_count_kernel(int P, SBGrid sg, const 
     extern __shared__ uint32_t lds[];
     uint32_t *cg = lds, *ci = lds + sg.nsb;
     for (int i = threadIdx.x; i < 2 * sg.nsb; i += 1024) lds[i] = 0u;
+    const int chunk = chunk_of_block(blockIdx.x);
+    if (chunk >= sg.nchunks) return;  // padding of the last XCD group
     __syncthreads();
-    const int chunk = blockIdx.x;
     const int j0 = chunk * sg.chunk, j1 = min(P, j0 + sg.chunk);
     const int side = 1 << sg.shift;
     // instances of Gaussian footprint r in SB `key`
@@ -361,12 +362,13 @@ __global__ __launch_bounds__(64 * kScatterWaves) void sb_scatter_kernel(int P, S
     // the point-list capacity is short: the host re-runs at K (SB instances <= K, so K <= cap
     // bounds the level-1 lists too; the same test as every other binning / render kernel)
     if (*kdev > cap) return;
+    const int chunk = chunk_of_block(blockIdx.x);
+    if (chunk >= sg.nchunks) return;  // padding of the last XCD group
     extern __shared__ uint32_t wc[];  // [W][nsb] per-wave running positions, then [W][nsb] u64 masks
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int nsb = sg.nsb;
     for (int i = threadIdx.x; i < 3 * kScatterWaves * nsb; i += 64 * kScatterWaves) wc[i] = 0u;
     __syncthreads();
-    const int chunk = blockIdx.x;
     const int per_wave = sg.chunk / kScatterWaves;
     const int jw0 = chunk * sg.chunk + w * per_wave, jw1 = min(P, jw0 + per_wave);
     uint32_t *run = wc + w * nsb;
@@ -1007,7 +1009,7 @@ SBGrid sb_grid(int gx, int gy, int P) {
     while ((P + g.chunk - 1) / g.chunk > kMaxChunks) g.chunk *= 2;
     g.nchunks = (P + g.chunk - 1) / g.chunk;
     if (g.nchunks < 1) g.nchunks = 1;
-    g.cper = (g.nchunks + 7) / 8;
+    g.cper = sb_blocks(g) / 8 + (sb_blocks(g) % 8 != 0);
     g.ccols = GSR_CNT_XCD ? 8 * g.cper : g.nchunks;
     return g;
 }
@@ -1022,7 +1024,7 @@ void launch_binning_count(int P, const Camera &cam, const GeomState &gs, bool in
     const size_t l1 = sizeof(uint32_t) * 2 * (size_t)sg.nsb;
     const uint2 *rects = index_order ? gs.rect8 : gs.drect;
     const uint32_t *rects4 = index_order ? gs.rect4 : drect4_of(gs);
-    hipLaunchKernelGGL(sb_count_kernel, dim3(sg.nchunks), dim3(1024), l1, s, P, sg, rects, rects4, gs.sb_cnt_g,
+    hipLaunchKernelGGL(sb_count_kernel, dim3(sb_blocks(sg)), dim3(1024), l1, s, P, sg, rects, rects4, gs.sb_cnt_g,
                        gs.sb_cnt_i);
     hipLaunchKernelGGL(sb_colscan_kernel, dim3(sg.nsb), dim3(kColThreads), 0, s, sg, gs.sb_cnt_g, gs.sb_cnt_i,
                        gs.sb_base_g, gs.sb_base_i, dsort_aux_word(gs), fw, sb_order, zero_classes,
@@ -1036,7 +1038,7 @@ void launch_binning_scatter(int P, const Camera &cam, const GeomState &gs, const
     const size_t l3 = sizeof(uint32_t) * 3 * kScatterWaves * (size_t)sg.nsb;
     const uint2 *rects = index_order ? gs.rect8 : gs.drect;
     const uint32_t *rects4 = index_order ? gs.rect4 : drect4_of(gs);
-    hipLaunchKernelGGL(sb_scatter_kernel, dim3(sg.nchunks), dim3(64 * kScatterWaves), l3, s, P, sg,
+    hipLaunchKernelGGL(sb_scatter_kernel, dim3(sb_blocks(sg)), dim3(64 * kScatterWaves), l3, s, P, sg,
                        index_order ? (const uint32_t *)nullptr : gs.order, rects, rects4, gs.sb_cnt_g, gs.sb_base_g,
                        bs.sblist, index_order ? bs.sblist4 : (uint4 *)nullptr, gs.dkey, bs.kdev, bs.cap);
 }

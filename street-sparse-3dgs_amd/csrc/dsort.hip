@@ -170,15 +170,28 @@ __global__ __launch_bounds__(kDsThreads) void dsort_upsweep_kernel(int P, int nb
     __syncthreads();
     uint32_t run = 0;  // thread 0: tiles_touched of the workgroup's earlier tiles
     const int v1 = min(nb, (u + 1) * tpb);
+    // tile v + 1's keys and counts are loaded while tile v is counted (large P: several tiles per
+    // workgroup, each a dependent round trip otherwise)
+    uint32_t knx[kDsItems], tnx[kDsItems];
+    const auto load_tile = [&](int v, uint32_t (&kk)[kDsItems], uint32_t (&tt)[kDsItems]) {
+        const size_t base = (size_t)v * kDsTile + (size_t)w * kDsItems * kWave;
+#pragma unroll
+        for (int k = 0; k < kDsItems; k++) {
+            const size_t e = base + (size_t)k * kWave + lane;
+            kk[k] = v < v1 && e < (size_t)P ? keys[e] : 0u;
+            tt[k] = v < v1 && e < (size_t)P ? tiles[e] : 0u;
+        }
+    };
+    load_tile(u * tpb, knx, tnx);
     for (int v = u * tpb; v < v1; v++) {
         const size_t base = (size_t)v * kDsTile + (size_t)w * kDsItems * kWave;
         uint32_t key[kDsItems], tl[kDsItems];
 #pragma unroll
         for (int k = 0; k < kDsItems; k++) {
-            const size_t e = base + (size_t)k * kWave + lane;
-            key[k] = e < (size_t)P ? keys[e] : 0u;
-            tl[k] = e < (size_t)P ? tiles[e] : 0u;
+            key[k] = knx[k];
+            tl[k] = tnx[k];
         }
+        if (v + 1 < v1) load_tile(v + 1, knx, tnx);
         uint32_t sum = 0;
 #pragma unroll
         for (int k = 0; k < kDsItems; k++) {

@@ -632,8 +632,25 @@ __host__ __device__ __forceinline__ FwdSegLayout fseg_layout(void *bin_base, int
 // Counter column of a level-1 chunk.  Chunk c runs as workgroup c, and workgroups are dealt to
 // the 8 XCDs round-robin, so the columns of one XCD's chunks are made adjacent: its 4-B counter
 // stores then fill whole lines in its own L2 instead of sharing every line with the 7 other XCDs.
+// GSR_SB_XCD_GROUP = G > 1: runs of G consecutive chunks go to one XCD (workgroup b runs chunk
+// chunk_of_block(b)), so the adjacent level-1 list runs that consecutive chunks write meet in one L2
+// (a chunk's run per superblock is ~7 entries, less than a line); G = 1 is the plain order.
+#ifndef GSR_SB_XCD_GROUP
+#define GSR_SB_XCD_GROUP 4  // r05g A/B: bin_superblocks 0.0808 (G = 1) -> 0.0803 (2) -> 0.0783 ms (4), parity bit-exact
+#endif
+constexpr int kXcdGroup = GSR_SB_XCD_GROUP;
+__host__ __device__ __forceinline__ int chunk_of_block(int b) {
+    const int k = b >> 3;
+    return kXcdGroup == 1 ? b : (k / kXcdGroup) * 8 * kXcdGroup + (b & 7) * kXcdGroup + k % kXcdGroup;
+}
+// workgroups of the level-1 kernels: the chunks rounded up to whole XCD groups
+__host__ __device__ __forceinline__ int sb_blocks(const SBGrid &g) {
+    return kXcdGroup == 1 ? g.nchunks : (g.nchunks + 8 * kXcdGroup - 1) / (8 * kXcdGroup) * 8 * kXcdGroup;
+}
 __host__ __device__ __forceinline__ int cnt_col(const SBGrid &g, int chunk) {
-    return GSR_CNT_XCD ? (chunk & 7) * g.cper + (chunk >> 3) : chunk;
+    if (!GSR_CNT_XCD) return chunk;
+    if (kXcdGroup == 1) return (chunk & 7) * g.cper + (chunk >> 3);
+    return ((chunk / kXcdGroup) & 7) * g.cper + (chunk / (8 * kXcdGroup)) * kXcdGroup + chunk % kXcdGroup;
 }
 
 struct GeomState {          // per Gaussian, written by preprocess

@@ -312,15 +312,15 @@ __device__ __forceinline__ void color_finish(int vb, const ShRows &r, float4 *s_
 // GSR_COLOR_BLOCKS > 0: a persistent grid of that many blocks walks the row blocks (so the pass
 // can be held to part of the chip while latency-bound work runs beside it).  Each wave owns its
 // LDS tile (no block-wide barrier between row blocks).
-template <bool kCut>
-__global__ __launch_bounds__(kColorThreads) void preprocess_color_kernel(int P, int D, const float *__restrict__ means3D,
-                                                                         const float *__restrict__ shs,
-                                                                         const float *__restrict__ campos,
-                                                                         const float *__restrict__ viewmatrix,
-                                                                         const int *__restrict__ radii, GeomState gs,
-                                                                         int nvb, CutRef cut) {
-    __shared__ float4 s_sh[kColorWaves * kWave * kShPitch];
-    __shared__ int4 s_idx[kCut ? kColorWaves * kWave : 1];
+template <bool kCut, int kWaves>
+__global__ __launch_bounds__(kWaves * kWave) void preprocess_color_kernel(int P, int D, const float *__restrict__ means3D,
+                                                                          const float *__restrict__ shs,
+                                                                          const float *__restrict__ campos,
+                                                                          const float *__restrict__ viewmatrix,
+                                                                          const int *__restrict__ radii, GeomState gs,
+                                                                          int nvb, CutRef cut) {
+    __shared__ float4 s_sh[kWaves * kWave * kShPitch];
+    __shared__ int4 s_idx[kCut ? kWaves * kWave : 1];
     if (GSR_COLOR_PF) {
         ShRows cur, nxt;
         int vb = blockIdx.x;
@@ -368,18 +368,29 @@ void launch_preprocess(const GaussianInputs &in, const Camera &cam, const GeomSt
 #undef GSR_PRE_ARGS
 }
 
+// blocks < 0: a full grid of 4-wave blocks (52 KiB, three per CU), for a pass forked after the depth
+// sort beside the binning: config 5's 7.46M-row pass 1.16 -> 1.06 ms (r05f, vlibs cw4).  Beside the
+// sort itself they take the CUs its passes need (config 5: sort 0.36 -> 1.05 ms, r05g), so a pass
+// forked before the sort (blocks == 0) or a persistent grid (blocks > 0) runs 8-wave blocks.
 void launch_preprocess_color(const GaussianInputs &in, const Camera &cam, const GeomState &gs, const int *radii,
                              hipStream_t s, int blocks) {
     if (in.P == 0) return;
-    const int nvb = (in.P + kColorThreads - 1) / kColorThreads;
+    const bool four = blocks < 0;
+    if (blocks < 0) blocks = 0;
     const int cap = blocks > 0 ? blocks : GSR_COLOR_BLOCKS;
-    const int grid = cap > 0 ? std::min(nvb, cap) : nvb;
-    if (in.cut.ri)
-        hipLaunchKernelGGL(preprocess_color_kernel<true>, dim3(grid), dim3(kColorThreads), 0, s, in.P, in.D, in.means3D,
-                           in.shs, cam.campos, cam.view, radii, gs, nvb, in.cut);
-    else
-        hipLaunchKernelGGL(preprocess_color_kernel<false>, dim3(grid), dim3(kColorThreads), 0, s, in.P, in.D,
-                           in.means3D, in.shs, cam.campos, cam.view, radii, gs, nvb, in.cut);
+    const auto go = [&](auto kw) {
+        constexpr int kW = decltype(kw)::value, kT = kW * kWave;
+        const int nvb = (in.P + kT - 1) / kT;
+        const int grid = cap > 0 ? std::min(nvb, cap) : nvb;
+        if (in.cut.ri)
+            hipLaunchKernelGGL((preprocess_color_kernel<true, kW>), dim3(grid), dim3(kT), 0, s, in.P, in.D, in.means3D,
+                               in.shs, cam.campos, cam.view, radii, gs, nvb, in.cut);
+        else
+            hipLaunchKernelGGL((preprocess_color_kernel<false, kW>), dim3(grid), dim3(kT), 0, s, in.P, in.D,
+                               in.means3D, in.shs, cam.campos, cam.view, radii, gs, nvb, in.cut);
+    };
+    if (four && cap == 0) go(std::integral_constant<int, 4>{});
+    else go(std::integral_constant<int, kColorWaves>{});
 }
 
 __global__ __launch_bounds__(256) void mark_visible_kernel(int P, const float *__restrict__ means3D,

@@ -145,6 +145,37 @@ int device_cus() {
     return cache[dev];
 }
 
+// Frames whose depth sort fills every CU (P above ~1M): the SH colour pass forks right after the
+// preprocess at full width instead of after the sort (GSR_COLOR_EARLY_BIG=0 for the A/B).
+// Measured on config 5 (7.46M rows, GSR_COLOR_FORK=0 variant, r05e): 3.73 -> 3.63 ms per frame.
+bool color_early_big() {
+    static const bool v = [] {
+        const char *e = std::getenv("GSR_COLOR_EARLY_BIG");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+// The same frames' colour pass as a persistent grid of this many blocks (GSR_COLOR_BIG_BLOCKS; 0 = a
+// full grid of 4-wave blocks), for the A/B of config 3's 20-30 ms stalls (a depth-sort or binning
+// kernel and the full-grid colour pass both stretched to the same end, r05f spikes.json)
+// A full-grid colour pass forked after the sort: 8-wave blocks (0, default) or 4-wave blocks
+// (GSR_COLOR_LATE_WAVES=4, -1; launch_preprocess_color).  Config 3 (r05h): 8 waves 55.8 s, 4 waves
+// 56.3 s -- the colour pass itself 0.224 -> 0.139 ms, but beside it bin_superblocks 0.153 -> 0.186 ms.
+int color_late_grid() {
+    static const int v = [] {
+        const char *e = std::getenv("GSR_COLOR_LATE_WAVES");
+        return e && std::atoi(e) == 4 ? -1 : 0;
+    }();
+    return v;
+}
+int color_big_blocks() {
+    static const int v = [] {
+        const char *e = std::getenv("GSR_COLOR_BIG_BLOCKS");
+        return e ? std::max(0, std::atoi(e)) : 0;
+    }();
+    return v;
+}
+
 int fail(int code, const std::string &msg) {
     g_err = msg;
     return code;
@@ -686,6 +717,13 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
             if (free_cus >= 2 * per_xcd) {
                 color_early = true;
                 color_blocks = free_cus;
+            } else {
+                // the sort fills the chip (large P).  Two rounds of it or more (config 5's 7.46M rows):
+                // the colour pass forks right after the preprocess, so it overlaps the sort as well
+                // as the binning (config 5 3.62 -> 3.51 ms, r05f); config 3's 3M-row frames measured
+                // no gain (55.0 vs 55.3 s), so they keep the fork after the sort
+                color_early = color_early_big() && dsort_blocks(P) >= 2 * device_cus();
+                color_blocks = color_big_blocks() ? color_big_blocks() : color_early ? 0 : color_late_grid();
             }
         }
     }

@@ -1160,10 +1160,18 @@ __global__ __launch_bounds__(kCompactThreads) void adam_compact_kernel(const flo
     }
 }
 
+// Four listed rows per wave and trip: the four rows' list entries, then all their loads, then the
+// updates -- one row at a time left each wave a chain of dependent round trips per row (~32 rows per
+// resident wave at 3M rows, 8.5% relevant: 140 us per call in the config-3 chunk, r05e).
+#ifndef GSR_ADAM_ROWS
+#define GSR_ADAM_ROWS 4
+#endif
+constexpr int kAdamRowsPerTrip = GSR_ADAM_ROWS;
 __global__ __launch_bounds__(256) void adam_rowlist_kernel(AdamArgs a, AdamLaneMap lm, const int *__restrict__ list,
                                                            const int *__restrict__ count, int64_t P,
                                                            const int *__restrict__ flag, float b1, float b2, float omb1,
                                                            float omb2, float eps, ShrinkArgs sh, DenseRows dr) {
+    constexpr int R = kAdamRowsPerTrip;
     const int lane = threadIdx.x & 63;
     const bool dense = *flag == 0;
     const int64_t n = dense ? P : (int64_t)*count;
@@ -1171,31 +1179,52 @@ __global__ __launch_bounds__(256) void adam_rowlist_kernel(AdamArgs a, AdamLaneM
     const bool act = lane < lm.lanes;
     const gsr_adam_group &G = a.g[act ? lm.group[lane] : 0];
     const int64_t col = act ? lm.col[lane] : 0;
-    for (int64_t k = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); k < n; k += waves) {
-        const int64_t row = dense ? k : (int64_t)list[k];
-        // the dense fallback over sparse rows: rows whose gradient reads as zero
-        const bool z = dense && (row < dr.skybox || (dr.live3 && dr.live3[3 * row + 2] == 0.f));
-        float p = 0.f;
-        if (act) {
-            const int64_t e = row * G.row_stride + col;
-            const float g = z ? 0.f : G.grad[e];
-            const float m0 = G.exp_avg[e], v0 = G.exp_avg_sq[e], p0 = G.param[e];
-            const float mm = m0 * b1 + omb1 * g;
-            const float vv = v0 * b2 + omb2 * (g * g);
-            const float denom = sqrtf(vv) / G.bias_correction2_sqrt + eps;
-            G.exp_avg[e] = mm;
-            G.exp_avg_sq[e] = vv;
-            p = p0 + (-G.step_size) * (mm / denom);
-            G.param[e] = p;
+    const bool shrink = sh.s_raw && lm.sh_lane0 >= 0;
+    for (int64_t k0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * R; k0 < n; k0 += waves * R) {
+        int64_t row[R];
+        bool ok[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            ok[r] = k0 + r < n;
+            row[r] = !ok[r] ? 0 : dense ? k0 + r : (int64_t)list[k0 + r];
         }
-        if (sh.s_raw && lm.sh_lane0 >= 0 && row >= sh.first) {
-            // the shrink of the row's freshly updated scales (shrink_scales_kernel's arithmetic)
-            const float sx = __shfl(p, lm.sh_lane0, 64), sy = __shfl(p, lm.sh_lane0 + 1, 64),
-                        sz = __shfl(p, lm.sh_lane0 + 2, 64);
-            const float x = expf(sx), y = expf(sy), zz = expf(sz);
-            if (fmaxf(fmaxf(x, y), zz) > sh.limit && lane >= lm.sh_lane0 && lane < lm.sh_lane0 + 3) {
-                const float c = lane == lm.sh_lane0 ? x : lane == lm.sh_lane0 + 1 ? y : zz;
-                sh.s_raw[3 * row + (lane - lm.sh_lane0)] = logf(c * 0.8f);
+        float g[R], m0[R], v0[R], p0[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            g[r] = m0[r] = v0[r] = p0[r] = 0.f;
+            if (act && ok[r]) {
+                // the dense fallback over sparse rows: rows whose gradient reads as zero
+                const bool z = dense && (row[r] < dr.skybox || (dr.live3 && dr.live3[3 * row[r] + 2] == 0.f));
+                const int64_t e = row[r] * G.row_stride + col;
+                g[r] = z ? 0.f : G.grad[e];
+                m0[r] = G.exp_avg[e];
+                v0[r] = G.exp_avg_sq[e];
+                p0[r] = G.param[e];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            if (!ok[r]) break;  // wave-uniform
+            float p = 0.f;
+            if (act) {
+                const int64_t e = row[r] * G.row_stride + col;
+                const float mm = m0[r] * b1 + omb1 * g[r];
+                const float vv = v0[r] * b2 + omb2 * (g[r] * g[r]);
+                const float denom = sqrtf(vv) / G.bias_correction2_sqrt + eps;
+                G.exp_avg[e] = mm;
+                G.exp_avg_sq[e] = vv;
+                p = p0[r] + (-G.step_size) * (mm / denom);
+                G.param[e] = p;
+            }
+            if (shrink && row[r] >= sh.first) {
+                // the shrink of the row's freshly updated scales (shrink_scales_kernel's arithmetic)
+                const float sx = __shfl(p, lm.sh_lane0, 64), sy = __shfl(p, lm.sh_lane0 + 1, 64),
+                            sz = __shfl(p, lm.sh_lane0 + 2, 64);
+                const float x = expf(sx), y = expf(sy), zz = expf(sz);
+                if (fmaxf(fmaxf(x, y), zz) > sh.limit && lane >= lm.sh_lane0 && lane < lm.sh_lane0 + 3) {
+                    const float c = lane == lm.sh_lane0 ? x : lane == lm.sh_lane0 + 1 ? y : zz;
+                    sh.s_raw[3 * row[r] + (lane - lm.sh_lane0)] = logf(c * 0.8f);
+                }
             }
         }
     }
