@@ -162,7 +162,7 @@ int gsr_set_deterministic(int enable);
 int gsr_set_bwd_segment(int L);
 
 /* Forward work split, process-wide.  L = 0: render_fwd blends every tile in one workgroup.  L > 0
- * (a multiple of 64, >= 4096; default 4096, behind the split gate): a tile whose list is longer than
+ * (a multiple of 64, >= 1024; default 2048, behind the split gate): a tile whose list is longer than
  * 4 L is blended as
  * ceil(len / L) work items by a pool of worker workgroups -- each item multiplies out the
  * transmittance through its positions, takes its predecessors' product (in segment order) and

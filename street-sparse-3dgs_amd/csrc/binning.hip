@@ -107,15 +107,27 @@ __device__ __forceinline__ SBFoot lane_foot(const SBFoot &f, int b) {
 }
 
 // Level 1, pass 1: per chunk and SB, the number of Gaussians and of tile instances.
+// The depth order's last `*culled` slots hold the culled Gaussians (no tiles: key 0xFFFFFFFF sorts
+// last), so chunks wholly past P - *culled have no footprint -- the level-1 kernels skip them and
+// the column scan stops before them (a 90-degree street view culls ~70% of a chunk's rows).
+__device__ __forceinline__ int visible_chunks(const SBGrid &sg, int P, const uint32_t *culled) {
+    if (!culled) return sg.nchunks;
+    const int pv = P - (int)min(*culled, (uint32_t)P);
+    return min(sg.nchunks, (pv + sg.chunk - 1) / sg.chunk);
+}
+
 __global__ __launch_bounds__(1024) void sb_count_kernel(int P, SBGrid sg, const uint2 *__restrict__ drect, const uint32_t *__restrict__ drect4,
-                                                       uint32_t *__restrict__ cnt_g, uint32_t *__restrict__ cnt_i) {
+                                                       uint32_t *__restrict__ cnt_g, uint32_t *__restrict__ cnt_i,
+                                                       const uint32_t *__restrict__ culled) {
     extern __shared__ uint32_t lds[];
     uint32_t *cg = lds, *ci = lds + sg.nsb;
-    for (int i = threadIdx.x; i < 2 * sg.nsb; i += 1024) lds[i] = 0u;
     const int chunk = chunk_of_block(blockIdx.x);
-    if (chunk >= sg.nchunks) return;  // padding of the last XCD group
+    if (chunk >= visible_chunks(sg, P, culled)) return;  // culled rows only, or the last XCD group's padding
+    for (int i = threadIdx.x; i < 2 * sg.nsb; i += 1024) lds[i] = 0u;
     __syncthreads();
-    const int j0 = chunk * sg.chunk, j1 = min(P, j0 + sg.chunk);
+    // depth-ordered slots past the visible Gaussians were not written by the sort (dsort.hip)
+    const int pv = culled ? P - (int)min(*culled, (uint32_t)P) : P;
+    const int j0 = chunk * sg.chunk, j1 = min(pv, j0 + sg.chunk);
     const int side = 1 << sg.shift;
     // instances of Gaussian footprint r in SB `key`
     const auto count = [&](const TileRect &r, uint32_t key) {
@@ -194,7 +206,8 @@ __global__ __launch_bounds__(kColThreads) void sb_colscan_kernel(SBGrid sg, uint
                                                                  uint32_t *__restrict__ zero_classes,
                                                                  uint32_t *__restrict__ tb_flag,
                                                                  uint32_t *__restrict__ tb_items, uint32_t tb_len,
-                                                                 uint32_t *__restrict__ host_sblist) {
+                                                                 uint32_t *__restrict__ host_sblist, int P,
+                                                                 const uint32_t *__restrict__ culled) {
     __shared__ uint32_t wsum[kColThreads / 64];
     __shared__ uint32_t s_last, s_tb;
     __shared__ uint32_t s_ci[GSR_FWD_SB_ORDER ? kMaxSB : 1];  // last workgroup: SB instance totals
@@ -203,13 +216,14 @@ __global__ __launch_bounds__(kColThreads) void sb_colscan_kernel(SBGrid sg, uint
     uint32_t *row = cnt_g + (size_t)s * sg.ccols;
     const uint32_t *rowi = cnt_i + (size_t)s * sg.ccols;
     uint32_t carry = 0, isum = 0;
-    for (int b = 0; b < sg.nchunks; b += kColThreads) {
+    const int nch = visible_chunks(sg, P, culled);  // later chunks' counters were not written (all zero)
+    for (int b = 0; b < nch; b += kColThreads) {
         const int c = b + (int)threadIdx.x;
-        const uint32_t v = c < sg.nchunks ? row[cnt_col(sg, c)] : 0u;
-        isum += c < sg.nchunks ? rowi[cnt_col(sg, c)] : 0u;
+        const uint32_t v = c < nch ? row[cnt_col(sg, c)] : 0u;
+        isum += c < nch ? rowi[cnt_col(sg, c)] : 0u;
         uint32_t tot;
         const uint32_t ex = block_exclusive_scan<kColThreads>(v, wsum, tot);
-        if (c < sg.nchunks) row[cnt_col(sg, c)] = carry + ex;
+        if (c < nch) row[cnt_col(sg, c)] = carry + ex;
         carry += tot;
     }
     uint32_t itot;
@@ -358,19 +372,21 @@ __global__ __launch_bounds__(64 * kScatterWaves) void sb_scatter_kernel(int P, S
                                                                          uint2 *__restrict__ sblist,
                                                                          uint4 *__restrict__ sblist4,
                                                                          const uint32_t *__restrict__ dkey,
-                                                                         const uint32_t *__restrict__ kdev, uint32_t cap) {
+                                                                         const uint32_t *__restrict__ kdev, uint32_t cap,
+                                                                         const uint32_t *__restrict__ culled) {
     // the point-list capacity is short: the host re-runs at K (SB instances <= K, so K <= cap
     // bounds the level-1 lists too; the same test as every other binning / render kernel)
     if (*kdev > cap) return;
     const int chunk = chunk_of_block(blockIdx.x);
-    if (chunk >= sg.nchunks) return;  // padding of the last XCD group
+    if (chunk >= visible_chunks(sg, P, culled)) return;  // culled rows only, or the XCD group's padding
     extern __shared__ uint32_t wc[];  // [W][nsb] per-wave running positions, then [W][nsb] u64 masks
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int nsb = sg.nsb;
     for (int i = threadIdx.x; i < 3 * kScatterWaves * nsb; i += 64 * kScatterWaves) wc[i] = 0u;
     __syncthreads();
     const int per_wave = sg.chunk / kScatterWaves;
-    const int jw0 = chunk * sg.chunk + w * per_wave, jw1 = min(P, jw0 + per_wave);
+    const int pv = culled ? P - (int)min(*culled, (uint32_t)P) : P;  // slots past pv: not written by the sort
+    const int jw0 = chunk * sg.chunk + w * per_wave, jw1 = min(pv, jw0 + per_wave);
     uint32_t *run = wc + w * nsb;
     uint64_t *msk = reinterpret_cast<uint64_t *>(wc + kScatterWaves * nsb) + w * nsb;
     const uint64_t lt = (1ull << lane) - 1ull;
@@ -1024,11 +1040,12 @@ void launch_binning_count(int P, const Camera &cam, const GeomState &gs, bool in
     const size_t l1 = sizeof(uint32_t) * 2 * (size_t)sg.nsb;
     const uint2 *rects = index_order ? gs.rect8 : gs.drect;
     const uint32_t *rects4 = index_order ? gs.rect4 : drect4_of(gs);
+    const uint32_t *culled = index_order ? nullptr : dsort_culled_word(gs);  // index order: culled rows anywhere
     hipLaunchKernelGGL(sb_count_kernel, dim3(sb_blocks(sg)), dim3(1024), l1, s, P, sg, rects, rects4, gs.sb_cnt_g,
-                       gs.sb_cnt_i);
+                       gs.sb_cnt_i, culled);
     hipLaunchKernelGGL(sb_colscan_kernel, dim3(sg.nsb), dim3(kColThreads), 0, s, sg, gs.sb_cnt_g, gs.sb_cnt_i,
                        gs.sb_base_g, gs.sb_base_i, dsort_aux_word(gs), fw, sb_order, zero_classes,
-                       index_order ? nullptr : gs.tb_flag, gs.tb_items, tb_split, host_sblist);
+                       index_order ? nullptr : gs.tb_flag, gs.tb_items, tb_split, host_sblist, P, culled);
 }
 
 void launch_binning_scatter(int P, const Camera &cam, const GeomState &gs, const BinningState &bs, bool index_order,
@@ -1040,7 +1057,8 @@ void launch_binning_scatter(int P, const Camera &cam, const GeomState &gs, const
     const uint32_t *rects4 = index_order ? gs.rect4 : drect4_of(gs);
     hipLaunchKernelGGL(sb_scatter_kernel, dim3(sb_blocks(sg)), dim3(64 * kScatterWaves), l3, s, P, sg,
                        index_order ? (const uint32_t *)nullptr : gs.order, rects, rects4, gs.sb_cnt_g, gs.sb_base_g,
-                       bs.sblist, index_order ? bs.sblist4 : (uint4 *)nullptr, gs.dkey, bs.kdev, bs.cap);
+                       bs.sblist, index_order ? bs.sblist4 : (uint4 *)nullptr, gs.dkey, bs.kdev, bs.cap,
+                       index_order ? (const uint32_t *)nullptr : dsort_culled_word(gs));
 }
 
 void launch_binning_tiles(int P, const Camera &cam, const GeomState &gs, const BinningState &bs, const ImageState &is,

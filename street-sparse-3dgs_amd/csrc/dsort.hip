@@ -52,6 +52,7 @@ constexpr int kCtlAux = 7;     // per-frame counter lent to the binning (sb_cols
 constexpr int kCtlMaxSB = 8;   // local-sort frames: the longest SB list (sb_colscan)
 constexpr int kCtlFwdReady = 9;  // the forward split's queue released by tile_order (workers launched ahead)
 constexpr int kCtlLongest = 10;  // [2]: the frame's longest tile list and superblock list (split gate hints)
+constexpr int kCtlCulled = 12;   // culled Gaussians (key 0xFFFFFFFF): the depth order's last P - visible slots
 constexpr int kCtlHead = 16;
 // The upsweep runs at most kUpMax workgroups, each over tpb consecutive tiles, so that a pass
 // reduces at most kUpMax histogram rows (kUpMax / 4 loads per thread, all in flight at once).
@@ -161,42 +162,37 @@ __global__ __launch_bounds__(kDsThreads) void dsort_upsweep_kernel(int P, int nb
     __shared__ uint32_t s_hist[kPasses * kRadix];
     __shared__ uint32_t s_top[kTopCopies][kRadix];
     __shared__ uint32_t s_wsum[kDsWaves];
+    __shared__ uint32_t s_cull;
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     const int u = blockIdx.x, tpb = up_tpb(nb);
     DS_STAMP(0, 0);
     s_hist[t] = 0u;
+    if (t == 0) s_cull = 0u;
 #pragma unroll
     for (int k = 0; k < kTopCopies * kRadix / kDsThreads; k++) (&s_top[0][0])[t + k * kDsThreads] = 0u;
     __syncthreads();
     uint32_t run = 0;  // thread 0: tiles_touched of the workgroup's earlier tiles
+    uint32_t culled = 0;  // this wave's culled keys (wave-uniform)
     const int v1 = min(nb, (u + 1) * tpb);
-    // tile v + 1's keys and counts are loaded while tile v is counted (large P: several tiles per
-    // workgroup, each a dependent round trip otherwise)
-    uint32_t knx[kDsItems], tnx[kDsItems];
-    const auto load_tile = [&](int v, uint32_t (&kk)[kDsItems], uint32_t (&tt)[kDsItems]) {
-        const size_t base = (size_t)v * kDsTile + (size_t)w * kDsItems * kWave;
-#pragma unroll
-        for (int k = 0; k < kDsItems; k++) {
-            const size_t e = base + (size_t)k * kWave + lane;
-            kk[k] = v < v1 && e < (size_t)P ? keys[e] : 0u;
-            tt[k] = v < v1 && e < (size_t)P ? tiles[e] : 0u;
-        }
-    };
-    load_tile(u * tpb, knx, tnx);
     for (int v = u * tpb; v < v1; v++) {
         const size_t base = (size_t)v * kDsTile + (size_t)w * kDsItems * kWave;
         uint32_t key[kDsItems], tl[kDsItems];
 #pragma unroll
         for (int k = 0; k < kDsItems; k++) {
-            key[k] = knx[k];
-            tl[k] = tnx[k];
+            const size_t e = base + (size_t)k * kWave + lane;
+            key[k] = e < (size_t)P ? keys[e] : 0u;
+            tl[k] = e < (size_t)P ? tiles[e] : 0u;
         }
-        if (v + 1 < v1) load_tile(v + 1, knx, tnx);
         uint32_t sum = 0;
 #pragma unroll
         for (int k = 0; k < kDsItems; k++) {
             const size_t e = base + (size_t)k * kWave + lane;
-            if (e < (size_t)P) {
+            // culled Gaussians (key 0xFFFFFFFF) are left out of the sort: counted by a ballot (LDS
+            // atomics would all hit one word -- 70% of a street view's rows lie outside its 90-degree
+            // frustum: config-3 upsweep 59 us per call at 3M rows, r05i), and dropped by pass 0
+            const bool cull = e < (size_t)P && key[k] == 0xFFFFFFFFu;
+            culled += (uint32_t)__popcll(__ballot(cull));
+            if (e < (size_t)P && !cull) {
 #pragma unroll
                 for (int p = 0; p < kPasses - 1; p++) atomicAdd(&s_hist[p * kRadix + ((key[k] >> (8 * p)) & 0xFFu)], 1u);
                 atomicAdd(&s_top[lane & (kTopCopies - 1)][key[k] >> 24], 1u);
@@ -214,6 +210,8 @@ __global__ __launch_bounds__(kDsThreads) void dsort_upsweep_kernel(int P, int nb
         }
         __syncthreads();
     }
+    if (lane == 0 && culled) atomicAdd(&s_cull, culled);
+    __syncthreads();
     DS_STAMP(0, 1);
     uint32_t hv = s_hist[t];
     if (t >= (kPasses - 1) * kRadix) {
@@ -224,6 +222,7 @@ __global__ __launch_bounds__(kDsThreads) void dsort_upsweep_kernel(int P, int nb
     if (t == 0) {
         ctl[ctl_btot(nb) + u] = run;
         __hip_atomic_fetch_add(&ctl[kCtlK], run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (s_cull) __hip_atomic_fetch_add(&ctl[kCtlCulled], s_cull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t done = __hip_atomic_fetch_add(&ctl[kCtlDone], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
         if (done == (uint32_t)gridDim.x - 1u && host_K) {
             const uint32_t K = ld_agent(&ctl[kCtlK]);
@@ -259,7 +258,7 @@ __global__ __launch_bounds__(kDsThreads) void dsort_pass_kernel(int P, int nb, c
     __shared__ uint32_t s_bex[kRadix];           // tile-local digit base
     __shared__ uint32_t s_dst[kRadix];           // global slot of tile-local position 0 of each digit
     __shared__ uint32_t s_wsum[kDsWaves];
-    __shared__ uint32_t s_v, s_pre;
+    __shared__ uint32_t s_v, s_pre, s_nsort;
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     DS_STAMP(1 + kPass, 0);
 #pragma unroll
@@ -288,11 +287,16 @@ __global__ __launch_bounds__(kDsThreads) void dsort_pass_kernel(int P, int nb, c
         __builtin_amdgcn_s_waitcnt(0xc07f);  // s_wh zeroed: LDS only (the row loads stay in flight)
         __builtin_amdgcn_s_barrier();
     }
-    if (v >= (uint32_t)nb) return;  // control words not zeroed: never index past P
+    // Culled Gaussians (key 0xFFFFFFFF, no tiles) are not sorted: pass 0 reads every key in index
+    // order and drops them, so passes 1-3 run over the Pv = P - culled visible keys only and the
+    // depth order's slots [Pv, P) are never written (nothing reads them: the binning stops at Pv).
+    const size_t Pn = kFirst ? (size_t)P : (size_t)P - min((size_t)ctl[kCtlCulled], (size_t)P);
+    const uint32_t nbv = (uint32_t)((Pn + kDsTile - 1) / kDsTile);
+    if (v >= nbv) return;  // control words not zeroed past nb; tiles past the visible keys: nothing to do
     DS_STAMP(1 + kPass, 5);
     const int wbase = w * kDsItems * kWave;
     const size_t tile0 = (size_t)v * kDsTile;
-    const int n = (int)min((size_t)kDsTile, (size_t)P - tile0);
+    const int n = (int)min((size_t)kDsTile, Pn - tile0);
     uint32_t key[kDsItems], val[kDsItems], tl[kDsItems], rc[kDsItems];
     const uint32_t *rsrc = kFirst ? rect4 : rin;
 #pragma unroll
@@ -332,7 +336,7 @@ __global__ __launch_bounds__(kDsThreads) void dsort_pass_kernel(int P, int nb, c
     uint32_t rk[kDsItems];
 #pragma unroll
     for (int k = 0; k < kDsItems; k++) {
-        const bool valid = wbase + k * kWave + lane < n;
+        const bool valid = wbase + k * kWave + lane < n && key[k] != 0xFFFFFFFFu;
         const uint32_t d = (key[k] >> kShift) & 0xFFu;
         const uint64_t m = match8(d, __ballot(valid));
         const uint32_t b = below(m);
@@ -379,15 +383,19 @@ __global__ __launch_bounds__(kDsThreads) void dsort_pass_kernel(int P, int nb, c
         s_gb[0][t] += s_gb[1][t] + s_gb[2][t] + s_gb[3][t];
     }
     __syncthreads();
-    if (w == 0) (void)scan256_wave(s_bex, lane);
+    if (w == 0) {
+        const uint32_t nv = scan256_wave(s_bex, lane);  // the tile's sorted (visible) keys
+        if (lane == 0) s_nsort = nv;
+    }
     if (w == 1) (void)scan256_wave(s_gb[0], lane);
     __syncthreads();
+    const int nsort = (int)s_nsort;
     DS_STAMP(1 + kPass, 2);
     // the tile in digit order, through LDS
 #pragma unroll
     for (int k = 0; k < kDsItems; k++) {
         const int i = wbase + k * kWave + lane;
-        if (i < n) {
+        if (i < n && key[k] != 0xFFFFFFFFu) {
             const uint32_t d = (key[k] >> kShift) & 0xFFu;
             const uint32_t lp = s_bex[d] + s_wh[w][d] + rk[k];
             s_key[lp] = key[k];
@@ -437,7 +445,7 @@ __global__ __launch_bounds__(kDsThreads) void dsort_pass_kernel(int P, int nb, c
     }
     __syncthreads();
     DS_STAMP(1 + kPass, 3);
-    for (int i = t; i < n; i += kDsThreads) {
+    for (int i = t; i < nsort; i += kDsThreads) {
         const uint32_t k = s_key[i];
         const uint32_t j = s_dst[(k >> kShift) & 0xFFu] + (uint32_t)i;
         const uint32_t g = s_val[i];
@@ -494,6 +502,7 @@ uint32_t *dsort_aux_word(const GeomState &gs) { return gs.ctrl + kCtlAux; }
 uint32_t *dsort_maxsb_word(const GeomState &gs) { return gs.ctrl + kCtlMaxSB; }
 uint32_t *dsort_fwdready_word(const GeomState &gs) { return gs.ctrl + kCtlFwdReady; }
 uint32_t *dsort_longest_words(const GeomState &gs) { return gs.ctrl + kCtlLongest; }
+uint32_t *dsort_culled_word(const GeomState &gs) { return gs.ctrl + kCtlCulled; }
 int dsort_head_words() { return kCtlHead; }
 
 }  // namespace gsr

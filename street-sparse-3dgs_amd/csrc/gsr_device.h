@@ -582,7 +582,7 @@ __host__ __device__ __forceinline__ size_t align256(size_t b) { return (b + 255)
 // pixels.  Per item, past the backward's region: its queue entry, a ticket (the tile's first
 // item's counts the finished items), a flag (1: its transmittance row is published; zeroed with
 // the queue), 4 checkpoint counts, the per-pixel transmittance row and 256 x 6 partials.
-constexpr uint32_t kMinFwdSeg = 4096;
+constexpr uint32_t kMinFwdSeg = 1024;
 // a tile is split when its list is longer than fseg_min (kFsegFactor segments by default: a tile
 // of a few segments whose pixels saturate early gains little)
 #ifndef GSR_FSEG_FACTOR

@@ -83,6 +83,7 @@ uint32_t *dsort_fwdready_word(const GeomState &gs);
 // the frame's longest tile list and superblock list, [2] (zeroed by the preprocess; render_fwd copies
 // them to the pinned host words)
 uint32_t *dsort_longest_words(const GeomState &gs);
+uint32_t *dsort_culled_word(const GeomState &gs);  // culled Gaussians of the frame (the upsweep's sum)
 int dsort_head_words();
 // binning.hip: per-tile lists (two stable counting levels).  index_order: level 1 over the
 // Gaussians in index order (local sort: sb_sort_bin orders each SB list by depth in LDS); else over

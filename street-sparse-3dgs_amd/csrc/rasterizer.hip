@@ -317,7 +317,21 @@ GeomState carve_geom(void *base, int P, int gx, int gy, size_t *bytes) {
 
 // point_list first: the backward re-carves this buffer with num_rendered, which may be smaller
 // than the capacity the forward carved it with.
-BinningState carve_binning(void *base, int64_t K, size_t *bytes) {
+// End of the backward checkpoints (L) and the forward items (Lf) past the start of the binning
+// buffer (they use the level-1 lists' room past the point list).
+size_t segment_end(int64_t K, uint32_t L, uint32_t Lf) {
+    size_t end = ck_offset(K);
+    if (L) end += align256(ck_slots(K, L) * (kCkFloats * 256) * 4 + ck_slots(K, L) * 4);
+    if (Lf) {
+        const FwdSegLayout f = fseg_layout(nullptr, K, L, Lf);
+        end = (size_t)reinterpret_cast<uintptr_t>(f.part) + fseg_max_items(K, Lf) * kFwdPartials * 256 * 4;
+    }
+    return end;
+}
+
+// L / Lf: the frame's segment lengths -- the buffer reaches past the level-1 lists when their
+// regions need it (L = 512 with Lf = 1024: 28 B per instance against the lists' 20 B)
+BinningState carve_binning(void *base, int64_t K, size_t *bytes, uint32_t L = 0, uint32_t Lf = 0) {
     Carver c(base);
     BinningState b;
     b.point_list = c.take<uint32_t>(K);
@@ -325,7 +339,9 @@ BinningState carve_binning(void *base, int64_t K, size_t *bytes) {
     // -) on the local-sort path -- carved for the larger
     b.sblist4 = c.take<uint4>(K);
     b.sblist = reinterpret_cast<uint2 *>(b.sblist4);
-    (void)c.take<uint8_t>(kSegReserve);  // backward segments: the checkpoints use the level-1 lists' room
+    const size_t end = (L || Lf) ? segment_end(K, L, Lf) : 0;
+    if (end > c.off) (void)c.take<uint8_t>(end - c.off);
+    (void)c.take<uint8_t>(kSegReserve);
     b.cap = (uint32_t)K;
     b.kdev = nullptr;
     if (bytes) *bytes = align_up(c.off, 256);
@@ -507,7 +523,7 @@ uint8_t forward_uncleared(const void *geom) {
 #endif
 std::atomic<uint32_t> g_bwd_seg{GSR_BWD_SEG_DEFAULT};
 #ifndef GSR_FWD_SEG_DEFAULT
-#define GSR_FWD_SEG_DEFAULT 4096  // behind the split gate (gsr_set_split_gate)
+#define GSR_FWD_SEG_DEFAULT 2048  // behind the split gate; config 3 (r05j/r05k): 4096 55.8-56.0 s, 2048 53.9 s, 1024 54.2-54.8 s
 #endif
 std::atomic<uint32_t> g_fwd_seg{GSR_FWD_SEG_DEFAULT};
 std::mutex g_seg_mu;
@@ -880,10 +896,10 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
             fseg_req && cap > 0 && (uint64_t)T * (uint64_t)(cap / fseg_req + 1) < (1ull << 32) ? fseg_req : 0u;
         fsplit_armed = fseg_used != 0u;
         size_t bbytes = 0;
-        carve_binning(nullptr, cap, &bbytes);
+        carve_binning(nullptr, cap, &bbytes, seg_used, fseg_used);
         void *bbase = binning_buffer(resize_ctx, bbytes);
         if (!bbase) return fail(GSR_ERR_ALLOCATION, "binning buffer allocation failed");
-        BinningState bs = carve_binning(bbase, cap, nullptr);
+        BinningState bs = carve_binning(bbase, cap, nullptr, seg_used, fseg_used);
         // P == 0: no depth sort ran, its control words are not initialised (no capacity test)
         bs.kdev = P > 0 ? dsort_K_word(gs) : nullptr;
         int r;
@@ -1163,7 +1179,7 @@ int gsr_set_fwd_split_min(int len) {
 
 int gsr_set_fwd_segment(int L) {
     if (L < 0 || (L > 0 && (L < (int)kMinFwdSeg || L % kWave != 0)))
-        return fail(GSR_ERR_INVALID_ARGUMENT, "forward segment length: 0 (off) or a multiple of 64 >= 4096");
+        return fail(GSR_ERR_INVALID_ARGUMENT, "forward segment length: 0 (off) or a multiple of 64 >= 1024");
     if (L > 0 && !fwd_segments_supported())
         return fail(GSR_ERR_UNSUPPORTED, "forward segments need the list-length launch order and the 1-row sub-block forward");
     return (int)g_fwd_seg.exchange((uint32_t)L);
@@ -1196,14 +1212,8 @@ int gsr_forward_stats(int64_t *out, int n) {
 int gsr_segment_layout_check(int64_t K, int L, int Lf, int64_t *need, int64_t *have) {
     if (K < 0 || L < 0 || Lf < 0) return fail(GSR_ERR_INVALID_ARGUMENT, "negative size");
     size_t bytes = 0;
-    carve_binning(nullptr, K, &bytes);
-    size_t end = ck_offset(K);
-    if (L) end += align256(ck_slots(K, (uint32_t)L) * (kCkFloats * 256) * 4 + ck_slots(K, (uint32_t)L) * 4);
-    if (Lf) {
-        // the forward items' arrays end past the partials
-        const FwdSegLayout f = fseg_layout(nullptr, K, (uint32_t)L, (uint32_t)Lf);
-        end = (size_t)reinterpret_cast<uintptr_t>(f.part) + fseg_max_items(K, (uint32_t)Lf) * kFwdPartials * 256 * 4;
-    }
+    carve_binning(nullptr, K, &bytes, (uint32_t)L, (uint32_t)Lf);
+    const size_t end = segment_end(K, (uint32_t)L, (uint32_t)Lf);
     if (need) *need = (int64_t)end;
     if (have) *have = (int64_t)bytes;
     return end <= bytes ? GSR_OK : GSR_ERR_INVALID_ARGUMENT;

@@ -1164,7 +1164,7 @@ __global__ __launch_bounds__(kCompactThreads) void adam_compact_kernel(const flo
 // updates -- one row at a time left each wave a chain of dependent round trips per row (~32 rows per
 // resident wave at 3M rows, 8.5% relevant: 140 us per call in the config-3 chunk, r05e).
 #ifndef GSR_ADAM_ROWS
-#define GSR_ADAM_ROWS 4
+#define GSR_ADAM_ROWS 1  // r05i: 4 rows per trip 42.9 / 163.4 us per call (1M / 3M rows), 1 row 38.0 / 161.5 us
 #endif
 constexpr int kAdamRowsPerTrip = GSR_ADAM_ROWS;
 __global__ __launch_bounds__(256) void adam_rowlist_kernel(AdamArgs a, AdamLaneMap lm, const int *__restrict__ list,

@@ -44,7 +44,7 @@ def test_library_metadata_calls_without_gpu():
     assert L.gsr_stage_times_ms(buf, 8) >= 0
 
 
-@pytest.mark.parametrize("L,Lf", [(512, 0), (0, 4096), (512, 4096), (1024, 8192), (64 * 9, 64 * 65)])
+@pytest.mark.parametrize("L,Lf", [(512, 0), (0, 4096), (512, 4096), (512, 2048), (512, 1024), (1024, 8192), (64 * 9, 64 * 17)])
 def test_segment_regions_fit_the_binning_buffer(L, Lf):
     """The backward checkpoints / segment list and the forward items' arrays fit
     in the binning buffer past the point list for every K (host arithmetic, no GPU)."""

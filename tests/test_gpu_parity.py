@@ -157,13 +157,13 @@ def compare(c, st, g, h, check_grads=True, global_sort=False):
     np.testing.assert_array_equal(S["ranges"], st["ranges"])
     vis = (h["radii"] > 0) & (S["tiles_touched"] > 0)
     if global_sort:
-        # the global depth order itself: visible Gaussians by (depth bits, id), then the culled
-        # ones; and the Gaussian-major record offsets its first pass writes
+        # the global depth order itself: visible Gaussians by (depth bits, id) (the culled ones are
+        # not sorted: the slots past them are never read); and the Gaussian-major record offsets
+        # its first pass writes
         nv = int(vis.sum())
         ids = np.nonzero(vis)[0]
         want = ids[np.lexsort((ids, S["depths"].view(np.uint32)[ids]))]
         np.testing.assert_array_equal(S["order"][:nv], want)
-        np.testing.assert_array_equal(np.sort(S["order"][nv:]), np.nonzero(~vis)[0])
         check_record_offsets(S, vis, h["K"])
     # the raw (superblock-major) ranges partition [0, K) exactly
     r = S["ranges_raw"].astype(np.int64)
@@ -434,9 +434,10 @@ def test_street_frame_1536_vs_oracle(deg, seed):
 
 @pytest.mark.gpu
 def test_depth_order_large():
-    """The global depth sort at 3M Gaussians (367 sort tiles) with 25% culled: the order is the
-    stable (depth bits, id) order of the visible Gaussians, then the culled ones; the record
-    offsets partition [0, K); K is the sum of tiles_touched."""
+    """The global depth sort at 3M Gaussians (367 sort tiles) with 25% culled: the order's first
+    slots are the stable (depth bits, id) order of the visible Gaussians (the culled ones are not
+    sorted: nothing reads the slots past them); the record offsets partition [0, K); K is the sum
+    of tiles_touched."""
     import torch
     from diff_gaussian_rasterization import _C
     c = dict(name="large", P=3_000_000, W=1920, H=1080, deg=0, seed=21, log_scale=-4.0, behind=0.25)
@@ -467,7 +468,6 @@ def test_depth_order_large():
     ids = np.nonzero(vis)[0]
     dbits = rec[:, 14].view(np.uint32)
     np.testing.assert_array_equal(order[:nv], ids[np.lexsort((ids, dbits[ids]))])
-    np.testing.assert_array_equal(np.sort(order[nv:]), np.nonzero(~vis)[0])
     check_record_offsets(dict(offsets=offsets, tiles_touched=tiles), vis, K)
 
 

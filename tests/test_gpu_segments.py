@@ -220,15 +220,16 @@ def fwd_compare(c, st, g, h, base=None):
             assert v <= GRAD_TOL, (k, m)
 
 
+@pytest.mark.parametrize("Lf", [4096, 2048])  # 2048: the default since r05 (twice the items per tile)
 @pytest.mark.parametrize("bwd_L", [0, 512])
 @pytest.mark.parametrize("c", FWD_CASES, ids=[c["name"] for c in FWD_CASES])
-def test_fwd_segments_vs_oracle(c, bwd_L):
+def test_fwd_segments_vs_oracle(c, bwd_L, Lf):
     s = seg_scene(c)
     dcol, dinv = upstream_grads(c)
     st, g = run_oracle(s, c, dcol, dinv)
     lens = np.diff(st["ranges"].astype(np.int64), axis=1)
     assert lens.max() > 4 * 4096, f"lists too short for the split (4 segments): {lens.max()}"
-    with fwd_segment(4096), bwd_segment(bwd_L):
+    with fwd_segment(Lf), bwd_segment(bwd_L):
         h = run_hip(s, c, dcol, dinv)
     fwd_compare(c, st, g, h)
 
@@ -294,7 +295,7 @@ def test_set_fwd_segment_validation():
     from diff_gaussian_rasterization import _C
     prev = _C.set_fwd_segment(0)
     try:
-        for bad in (-64, 512, 4000, 4097):
+        for bad in (-64, 512, 960, 2000, 4097):
             with pytest.raises(RuntimeError):
                 _C.set_fwd_segment(bad)
         assert _C.set_fwd_segment(8192) == 0
