@@ -433,6 +433,22 @@ def test_street_frame_1536_vs_oracle(deg, seed):
 
 
 @pytest.mark.gpu
+def test_street_frame_3M_culled_vs_oracle():
+    """A street-chunk-sized frame: 3M Gaussians on a 1536x1536 90-degree view, 70% of them behind
+    the camera (a cube face of a late street chunk culls about that share): the depth sort and the
+    level-1 binning skip the culled rows (dsort.hip, binning.hip), and the sort fills the chip, so
+    the SH colour pass forks after it.  Bit-exact binning, image and gradients vs the oracle."""
+    c = dict(name="street1536_3M_culled", P=3_000_000, W=1536, H=1536, deg=3, seed=8, log_scale=-4.5, fovx=90.0,
+             behind=0.7)
+    s = make_scene(c)
+    dcol, dinv = upstream_grads(c)
+    st, g = run_oracle(s, c, dcol, dinv)
+    h = run_hip(s, c, dcol, dinv)
+    assert int((h["radii"] > 0).sum()) < 0.4 * c["P"]
+    compare(c, st, g, h, global_sort=True)
+
+
+@pytest.mark.gpu
 def test_depth_order_large():
     """The global depth sort at 3M Gaussians (367 sort tiles) with 25% culled: the order's first
     slots are the stable (depth bits, id) order of the visible Gaussians (the culled ones are not
