@@ -332,6 +332,8 @@ def config3(a, dev, seed=0, ranks=None):
            "iteration_ms": {"mean": round(float(per.mean()), 4), "median": round(float(np.median(per)), 4),
                             "p90": round(float(np.percentile(per, 90)), 4), "max": round(float(per.max()), 3),
                             "source": "HIP events between iterations"},
+           # where the chunk's time goes over its schedule: mean ms per block of 1000 iterations
+           "iteration_ms_per_1000": [round(float(per[i:i + 1000].mean()), 3) for i in range(0, len(per), 1000)],
            "slowest_iterations": slow, "executor_buffers": ts.ctx_stats(),
            "P_init": info["P_init"], "P_final": ts.g.P, "P_max": max([e["P_after"] for e in ev] + [info["P_init"]]),
            "densify_events": sum(1 for e in ev if "total" in e), "opacity_resets": sum(1 for e in ev if e.get("reset")),
