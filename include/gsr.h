@@ -163,7 +163,7 @@ int gsr_set_bwd_segment(int L);
 
 /* Forward work split, process-wide.  L = 0: render_fwd blends every tile in one workgroup.  L > 0
  * (a multiple of 64, >= 1024; default 2048, behind the split gate): a tile whose list is longer than
- * 4 L is blended as
+ * 6 L (gsr_set_fwd_split_min) is blended as
  * ceil(len / L) work items by a pool of worker workgroups -- each item multiplies out the
  * transmittance through its positions, takes its predecessors' product (in segment order) and
  * blends its positions from there; the tile's last item adds the items' colours in order.  Colours
@@ -172,7 +172,7 @@ int gsr_set_bwd_segment(int L);
  * GSR_ERR_UNSUPPORTED. */
 int gsr_set_fwd_segment(int L);
 
-/* The shortest tile list the forward split takes, process-wide: 0 (default) = 4 segments
+/* The shortest tile list the forward split takes, process-wide: 0 (default) = 6 segments
  * (GSR_FSEG_FACTOR); otherwise max(len, L).  Returns the previous setting. */
 int gsr_set_fwd_split_min(int len);
 

@@ -586,9 +586,10 @@ constexpr uint32_t kMinFwdSeg = 1024;
 // a tile is split when its list is longer than fseg_min (kFsegFactor segments by default: a tile
 // of a few segments whose pixels saturate early gains little)
 #ifndef GSR_FSEG_FACTOR
-// config-3 with the workers ahead of tile_order (r04zc): 4 -> 57.3 / 56.9 s, 16 -> 57.0 s (workers beside
-// render_fwd: 58.5 s); street views with 60k-110k lists: 4 -> 0.81 ms render_fwd, 16 -> 2.96 ms (r04zb)
-#define GSR_FSEG_FACTOR 4
+// config-3 with the workers ahead of tile_order (r04zc, Lf 4096): 4 -> 57.3 / 56.9 s, 16 -> 57.0 s (workers
+// beside render_fwd: 58.5 s); street views with 60k-110k lists: 4 -> 0.81 ms render_fwd, 16 -> 2.96 ms
+// (r04zb).  At Lf 2048 (r05t, two rounds): 3 -> 51.8 s, 4 -> 52.2 / 51.1 s, 6 -> 50.9 / 50.9 s, 8 -> 50.9 s
+#define GSR_FSEG_FACTOR 6
 #endif
 __host__ __device__ __forceinline__ bool fseg_splits(uint32_t len, uint32_t fseg_min) { return fseg_min && len > fseg_min; }
 constexpr int kFwdWorkers = 256;      // the in-kernel variant's pool (GSR_FWD_SEG_INKERNEL)
