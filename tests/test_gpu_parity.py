@@ -449,6 +449,31 @@ def test_street_frame_3M_culled_vs_oracle():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n_vis", [0, 1, 8191, 8192, 8193, 16385])
+def test_sort_tile_boundaries_with_culled_rows(n_vis):
+    """Visible-row counts at the depth sort's 8192-key tile boundaries: the culled rows (key
+    0xFFFFFFFF) are counted by the upsweep and left out of the passes, which run ceil(visible / 8192)
+    tiles (dsort.hip), and the level-1 binning stops at the last visible chunk (binning.hip).  20000
+    rows, the first n_vis on screen and the rest behind the camera, through the global sort;
+    bit-exact binning and order, image and gradients vs the oracle."""
+    c = dict(name=f"sort_tile_edge_{n_vis}", P=20000, W=128, H=96, deg=1, seed=30, log_scale=-3.5)
+    s = make_scene(c)
+    rng = np.random.default_rng(31)
+    m = s["means3D"]
+    z = rng.uniform(2.0, 10.0, c["P"]).astype(np.float32)
+    m[:, 0] = z * rng.uniform(-0.6, 0.6, c["P"]).astype(np.float32) * np.float32(s["tanfovx"])
+    m[:, 1] = z * rng.uniform(-0.6, 0.6, c["P"]).astype(np.float32) * np.float32(s["tanfovy"])
+    m[:, 2] = z
+    m[n_vis:, 2] = -z[n_vis:]  # behind the camera: culled
+    dcol, dinv = upstream_grads(c)
+    st, g = run_oracle(s, c, dcol, dinv)
+    with binning_mode(1):
+        h = run_hip(s, c, dcol, dinv)
+    assert int(((h["radii"] > 0) & (h["state"]["tiles_touched"] > 0)).sum()) == n_vis
+    compare(c, st, g, h, global_sort=True)
+
+
+@pytest.mark.gpu
 def test_depth_order_large():
     """The global depth sort at 3M Gaussians (367 sort tiles) with 25% culled: the order's first
     slots are the stable (depth bits, id) order of the visible Gaussians (the culled ones are not
