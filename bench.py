@@ -68,6 +68,9 @@ def parse():
     ap.add_argument("--chunk-positions", type=int, default=48, help="camera stations (4 cube faces each)")
     ap.add_argument("--chunk-truth", type=int, default=1_000_000, help="Gaussians of the synthetic truth street")
     ap.add_argument("--chunk-init", type=int, default=300_000, help="LiDAR-like initial points")
+    ap.add_argument("--chunk-spatial", type=int, default=1,
+                    help="1 (default): keep the chunk's rows in spatial (Morton) order (TrainChunk(spatial=True): "
+                         "gs_train.chunk.reorder_rows after every densification); 0: the reference's row order")
     ap.add_argument("--post-leaves", type=int, default=3_000_000,
                     help="leaves of the train_post step's synthetic hierarchy (0 = skip that step)")
     ap.add_argument("--bwd-seg", type=int, default=None,
@@ -253,7 +256,7 @@ def config3(a, dev, seed=0, ranks=None):
 
     from gs_train.chunk import view_psnr
     psnr0 = view_psnr(ts)
-    tc = TrainChunk(ts, sched)
+    tc = TrainChunk(ts, sched, spatial=bool(a.chunk_spatial))
     evs, losses = [], {}
     # per iteration, for the attribution of the slowest ones: binning re-runs (capacity short), the
     # executor's buffer growths, the torch caching allocator's reserved bytes
@@ -352,6 +355,7 @@ def config3(a, dev, seed=0, ranks=None):
            "data": "synthetic street chunk generated on the device (gs_train.chunk.street_chunk); the example_dataset "
                    "is not available offline"}
     out["seed"] = seed
+    out["spatial_rows"] = bool(a.chunk_spatial)
     out["chunk_iterations_per_s"] = round(n_it / wall, 2)
     if ranks is not None:
         out["job_wall_s"] = round(ranks.max(job_wall), 3)

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 5
+#define GSR_ABI_VERSION 6
 
 typedef enum {
     GSR_OK = 0,
@@ -191,6 +191,15 @@ int gsr_set_fwd_spin_limits(int64_t ready, int64_t flag);
  * every frame (the outputs are the same either way, to fp32 summation order).  Returns the previous
  * setting. */
 int gsr_set_split_gate(int enable);
+
+/* How the backward walks the live rows (the Gaussians with a nonzero screen-space gradient),
+ * process-wide.  0 (default): each 2048-row range's workgroup walks its own live rows -- one launch,
+ * the better choice when the live rows are scattered over the model (rows in the order training
+ * appends them).  1: the ranges append their live rows to one list that a grid of two workgroups
+ * per CU walks -- one more launch, every thread the same share, the better choice when the rows are
+ * in spatial order and a view's live rows come in runs (gs_train.chunk.reorder_rows).  The
+ * gradients are the same bits either way.  Returns the previous setting (ABI 6). */
+int gsr_set_live_list(int enable);
 
 /* Diagnostic (host arithmetic only): the bytes the backward checkpoints and the forward items need
  * past the start of a binning buffer carved for K instances with segment lengths L / Lf (*need),

@@ -654,7 +654,7 @@ __global__ __launch_bounds__(256) void preprocess_bwd_kernel(
 // the dead rows' zero stores, and its 53-KiB SH staging tile held occupancy to 3 blocks per CU:
 // ~4.2 TB/s.  grad_rows_kernel streams every row's screen-space mean / opacity gradient and the
 // dead rows' zero rows (skipped in sparse-rows mode) and publishes the live rows as one 64-bit
-// mask per wave; grad_live_kernel compacts each 2048-row range's live rows in LDS, so its lanes are
+// mask per wave; grad_live_kernel compacts each kLiveRange-row range's live rows in LDS, so its lanes are
 // all live, and runs the chain rule on them.  The arithmetic is the single kernel's (geom_chain,
 // sh_backward, dir_chain, scale_rot_chain): the bits do not change.
 // The ten per-Gaussian sums: the atomic accumulator row, or (record mode) record_sum's gsum row
@@ -776,25 +776,135 @@ __global__ __launch_bounds__(256) void grad_rows_kernel(int P, const int *__rest
     }
 }
 
-constexpr int kLiveRange = 2048;  // rows per grad_live_kernel block (32 live masks)
+// The live rows' chain rule: per 2048-row range, 256 threads of 8 rows each (a byte of a 64-row live
+// mask) compact the range's live rows in LDS (range_compact), then either
+//   grad_range_kernel  the range's own workgroup walks them (one launch; the default), or
+//   grad_live_list_kernel + grad_live_kernel  the ranges append them to one list (one atomic per
+//                      workgroup on a frame control word) and a grid of two workgroups per CU walks
+//                      that list, every thread the same share of rows however they fall
+//                      (gsr_set_live_list(1)).
+// Rows in spatial order (gs_train.chunk.reorder_rows) put a view's live rows in runs: a range can be
+// all live and its 256 threads walk 8 rows each, one after the other, while most ranges have none
+// (config-3 chunk: 0.155 ms per call per range, 0.125 through the list).  Scattered live rows
+// (the bench frame, a chunk in the reference's row order) fill every range a little: the list's
+// second launch and its ~1500 same-word atomics cost more than they balance (0.025 -> 0.054 ms).
+constexpr int kLiveRange = 2048;
+constexpr int kLiveBlocksPerCU = 2;  // 185 VGPRs: two 256-thread workgroups per CU
 
-__global__ __launch_bounds__(256) void grad_live_kernel(
-    int P, int D, const float *__restrict__ means3D, const float *__restrict__ shs, const uint8_t *__restrict__ clamped,
-    const float *__restrict__ scales, const float *__restrict__ rotations, float mod, float dscale_mod,
-    const float *__restrict__ viewmatrix, const float *__restrict__ projmatrix, const float *__restrict__ campos_p,
-    float tanx, float tany, float fx, float fy, BwdScratch sc, GaussianGrads out, int raw,
-    const uint32_t *__restrict__ stamps, uint32_t stamp, StepAct act) {
-    __shared__ uint16_t s_list[kLiveRange];
-    __shared__ uint32_t s_off[kLiveRange / 64 + 1];
-    __shared__ uint8_t s_byte[256];
+struct LiveArgs {
+    int P, D;
+    const float *means3D, *shs;
+    const uint8_t *clamped;
+    const float *scales, *rotations;
+    float mod, dscale_mod;
+    const float *viewmatrix, *projmatrix, *campos;
+    float tanx, tany, fx, fy;
+    BwdScratch sc;
+    GaussianGrads out;
+    int raw, stamped;  // stamped: render_bwd zeroed the dense rows and stamped the live ones
+    StepAct act;
+};
+
+// One live row: the chain rule from its ten screen-space sums to its parameters' gradients.
+// (pointer arguments __restrict__: the inputs' loads are not ordered behind the gradient stores)
+__device__ __forceinline__ void live_row(int i, const Mat4 &V, int D, const float *__restrict__ means3D,
+                                         const float *__restrict__ shs, const uint8_t *__restrict__ clamped,
+                                         const float *__restrict__ scales, const float *__restrict__ rotations,
+                                         float mod, float dscale_mod, const float *__restrict__ projmatrix,
+                                         const float *__restrict__ campos_p, float tanx, float tany, float fx, float fy,
+                                         const BwdScratch &sc, const GaussianGrads &out, int raw, int stamped,
+                                         const StepAct &act) {
+    float g[10];
+    load_sums(sc, out, i, true, g);
+    const float3 p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
+    float dm[3] = {0.f, 0.f, 0.f};
+    float dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float c3[6];
+    float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+    float3 s_in = make_float3(0.f, 0.f, 0.f);
+    geom_chain(i, p, V, projmatrix, fx, fy, tanx, tany, true, scales, rotations, mod, nullptr, g, c3, q,
+               s_in, dm, dcov, raw);
+    if (stamped) {  // the live rows' screen-space mean / opacity gradients (render_bwd zeroed the rest)
+        st_out(&out.dmeans2D[3 * i + 0], g[0]);
+        st_out(&out.dmeans2D[3 * i + 1], g[1]);
+        st_out(&out.dmeans2D[3 * i + 2], out.sparse_rows ? 1.f : 0.f);
+        st_out(&out.dopacity[i], g[5]);
+    }
+    if (sc.atomic) {
+        // the row is consumed: cleared for a repeated backward (see preprocess_bwd_kernel)
+        float4 *acc = sc.acc + 4 * (size_t)i;
+        const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int k = 0; k < 4; k++) acc[k] = z4;
+    }
+    float dir[3], dor[3];
+    sh_dir(p, make_float3(campos_p[0], campos_p[1], campos_p[2]), dir, dor);
+    const uint8_t cl = clamped[i];
+    float gc[3];
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) gc[ch] = (cl >> ch) & 1 ? 0.f : g[6 + ch];
+    float gd[3];
+    const float *sh = shs + (size_t)i * 48;
+    float *dsh = out.dsh + (size_t)i * 48;
+    switch (D) {
+        case 0: sh_backward<0>(sh, 16, true, dir, gc, dsh, gd); break;
+        case 1: sh_backward<1>(sh, 16, true, dir, gc, dsh, gd); break;
+        case 2: sh_backward<2>(sh, 16, true, dir, gc, dsh, gd); break;
+        default: sh_backward<3>(sh, 16, true, dir, gc, dsh, gd); break;
+    }
+    dir_chain(dor, gd, dm);
+    st_out(&out.dmeans3D[3 * i + 0], dm[0]);
+    st_out(&out.dmeans3D[3 * i + 1], dm[1]);
+    st_out(&out.dmeans3D[3 * i + 2], dm[2]);
+    float ds[3], dq[4];
+    scale_rot_chain(q, s_in, mod, dscale_mod, dcov, ds, dq);
+    if (act.on) {
+        // the activation backward (train.hip activate_bwd_step_kernel's expressions): exp,
+        // normalise and sigmoid with the skybox lock, the densification statistics and the
+        // relevance flag of this live row
+#pragma unroll
+        for (int k = 0; k < 3; k++) ds[k] = ds[k] * act_scale(act.s_raw[3 * i + k]);
+        const float4 x = act.q_raw[i];
+        const float4 gq = make_float4(dq[0], dq[1], dq[2], dq[3]);
+        const float nq = sqrtf(x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w);
+        const float d = fmaxf(nq, 1e-12f);
+        const float gd =
+            -(gq.x * ((x.x / d) / d) + gq.y * ((x.y / d) / d) + gq.z * ((x.z / d) / d) + gq.w * ((x.w / d) / d));
+        const float gn = nq >= 1e-12f && nq != 0.f ? gd / nq : 0.f;
+        dq[0] = gq.x / d + x.x * gn;
+        dq[1] = gq.y / d + x.y * gn;
+        dq[2] = gq.z / d + x.z * gn;
+        dq[3] = gq.w / d + x.w * gn;
+        const float y = act_opacity(act.o_raw[i]);
+        const float go = (int64_t)i < act.skybox ? 0.f : g[5] * (1.f - y) * y;
+        st_out(&out.dopacity[i], go);
+        if (go != 0.f) *act.flag = 1;
+        const int r = act.radii[i];
+        if (r > 0) {
+            const float gx = g[0], gy = g[1];
+            const float nn = sqrtf(gx * gx + gy * gy);
+            act.maxr[i] = fmaxf(act.maxr[i], (float)r);
+            act.accum[i] = fmaxf(nn, act.accum[i]);
+            act.denom[i] = act.denom[i] + 1.f;
+        }
+    }
+    st_out(&out.dscales[3 * i + 0], ds[0]);
+    st_out(&out.dscales[3 * i + 1], ds[1]);
+    st_out(&out.dscales[3 * i + 2], ds[2]);
+    st_out(&reinterpret_cast<float4 *>(out.drots)[i], make_float4(dq[0], dq[1], dq[2], dq[3]));
+}
+
+// The range's live rows compacted: thread t's mask bits, s_off[] their exclusive offsets, s_off[nw]
+// the range's count.
+__device__ __forceinline__ void range_compact(const LiveArgs a, int64_t base, const uint32_t *__restrict__ stamps,
+                                              uint32_t stamp, uint32_t *s_off, uint8_t *s_byte, uint64_t &m,
+                                              uint32_t &byte) {
     const int t = threadIdx.x;
-    const int64_t base = (int64_t)blockIdx.x * kLiveRange;
+    const int P = a.P;
     const int nw = (P + 63) / 64;
     // thread t owns rows [8t, 8t + 8) of the range: byte t % 8 of live mask t / 8 -- from
     // grad_rows_kernel's masks, or (stamps != NULL) from the rows render_bwd stamped this backward
     const int wi = (int)(base / 64) + t / 8;
-    uint64_t m;
-    uint32_t byte;
     if (stamps) {
         byte = 0u;
         const int64_t r0 = base + 8 * t;
@@ -807,7 +917,7 @@ __global__ __launch_bounds__(256) void grad_live_kernel(
 #pragma unroll
         for (int k = 0; k < 8; k++) m |= (uint64_t)s_byte[(t & ~7) + k] << (8 * k);
     } else {
-        m = wi < nw ? sc.live[wi] : 0ull;
+        m = wi < nw ? a.sc.live[wi] : 0ull;
         byte = (uint32_t)(m >> (8 * (t & 7))) & 0xFFu;
     }
     if ((t & 7) == 0) s_off[t / 8] = (uint32_t)__popcll(m);
@@ -822,110 +932,94 @@ __global__ __launch_bounds__(256) void grad_live_kernel(
         s_off[kLiveRange / 64] = run;
     }
     __syncthreads();
+}
+
+// The native step: densification statistics of this thread's visible rows that are not live (their
+// screen-space gradient is zero: densify_stats_kernel's arithmetic with n = 0).
+__device__ __forceinline__ void nonlive_stats(const LiveArgs a, int64_t base, uint32_t byte) {
+    if (!a.act.on) return;
+    const int64_t r0 = base + 8 * threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const int64_t i = r0 + k;
+        if (i >= a.P || ((byte >> k) & 1u)) continue;
+        const int r = a.act.radii[i];
+        if (r > 0) {
+            const float nn = sqrtf(0.f * 0.f + 0.f * 0.f);
+            a.act.maxr[i] = fmaxf(a.act.maxr[i], (float)r);
+            a.act.accum[i] = fmaxf(nn, a.act.accum[i]);
+            a.act.denom[i] = a.act.denom[i] + 1.f;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void grad_range_kernel(
+    int P, int D, const float *__restrict__ means3D, const float *__restrict__ shs, const uint8_t *__restrict__ clamped,
+    const float *__restrict__ scales, const float *__restrict__ rotations, float mod, float dscale_mod,
+    const float *__restrict__ viewmatrix, const float *__restrict__ projmatrix, const float *__restrict__ campos_p,
+    float tanx, float tany, float fx, float fy, BwdScratch sc, GaussianGrads out, int raw,
+    const uint32_t *__restrict__ stamps, uint32_t stamp, StepAct act) {
+    __shared__ uint16_t s_list[kLiveRange];
+    __shared__ uint32_t s_off[kLiveRange / 64 + 1];
+    __shared__ uint8_t s_byte[256];
+    const int t = threadIdx.x;
+    const int64_t base = (int64_t)blockIdx.x * kLiveRange;
+    LiveArgs a{};
+    a.P = P;
+    a.sc = sc;
+    a.act = act;
+    uint64_t m;
+    uint32_t byte;
+    range_compact(a, base, stamps, stamp, s_off, s_byte, m, byte);
     {
         uint32_t pos = s_off[t / 8] + (uint32_t)__popcll(m & ((1ull << (8 * (t & 7))) - 1ull));
         for (uint32_t b = byte; b; b &= b - 1u) s_list[pos++] = (uint16_t)(8 * t + __builtin_ctz(b));
     }
     __syncthreads();
     const uint32_t n = s_off[kLiveRange / 64];
-    if (act.on) {
-        // the native step: densification statistics of this thread's visible rows that are not
-        // live (their screen-space gradient is zero: densify_stats_kernel's arithmetic with n = 0)
-        const int64_t r0 = base + 8 * t;
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const int64_t i = r0 + k;
-            if (i >= P || ((byte >> k) & 1u)) continue;
-            const int r = act.radii[i];
-            if (r > 0) {
-                const float nn = sqrtf(0.f * 0.f + 0.f * 0.f);
-                act.maxr[i] = fmaxf(act.maxr[i], (float)r);
-                act.accum[i] = fmaxf(nn, act.accum[i]);
-                act.denom[i] = act.denom[i] + 1.f;
-            }
-        }
-    }
+    nonlive_stats(a, base, byte);
     const Mat4 V = load_mat4(viewmatrix);
-    for (uint32_t e = (uint32_t)t; e < n; e += blockDim.x) {
-        const int i = (int)(base + s_list[e]);
-        float g[10];
-        load_sums(sc, out, i, true, g);
-        const float3 p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
-        float dm[3] = {0.f, 0.f, 0.f};
-        float dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        float c3[6];
-        float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
-        float3 s_in = make_float3(0.f, 0.f, 0.f);
-        geom_chain(i, p, V, projmatrix, fx, fy, tanx, tany, true, scales, rotations, mod, nullptr, g, c3, q, s_in, dm,
-                   dcov, raw);
-        if (stamps) {  // the live rows' screen-space mean / opacity gradients (render_bwd zeroed the rest)
-            st_out(&out.dmeans2D[3 * i + 0], g[0]);
-            st_out(&out.dmeans2D[3 * i + 1], g[1]);
-            st_out(&out.dmeans2D[3 * i + 2], out.sparse_rows ? 1.f : 0.f);
-            st_out(&out.dopacity[i], g[5]);
-        }
-        if (sc.atomic) {
-            // the row is consumed: cleared for a repeated backward (see preprocess_bwd_kernel)
-            float4 *a = sc.acc + 4 * (size_t)i;
-            const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-            for (int k = 0; k < 4; k++) a[k] = z4;
-        }
-        float dir[3], dor[3];
-        sh_dir(p, make_float3(campos_p[0], campos_p[1], campos_p[2]), dir, dor);
-        const uint8_t cl = clamped[i];
-        float gc[3];
-#pragma unroll
-        for (int ch = 0; ch < 3; ch++) gc[ch] = (cl >> ch) & 1 ? 0.f : g[6 + ch];
-        float gd[3];
-        const float *sh = shs + (size_t)i * 48;
-        float *dsh = out.dsh + (size_t)i * 48;
-        switch (D) {
-            case 0: sh_backward<0>(sh, 16, true, dir, gc, dsh, gd); break;
-            case 1: sh_backward<1>(sh, 16, true, dir, gc, dsh, gd); break;
-            case 2: sh_backward<2>(sh, 16, true, dir, gc, dsh, gd); break;
-            default: sh_backward<3>(sh, 16, true, dir, gc, dsh, gd); break;
-        }
-        dir_chain(dor, gd, dm);
-        st_out(&out.dmeans3D[3 * i + 0], dm[0]);
-        st_out(&out.dmeans3D[3 * i + 1], dm[1]);
-        st_out(&out.dmeans3D[3 * i + 2], dm[2]);
-        float ds[3], dq[4];
-        scale_rot_chain(q, s_in, mod, dscale_mod, dcov, ds, dq);
-        if (act.on) {
-            // the activation backward (train.hip activate_bwd_step_kernel's expressions): exp,
-            // normalise and sigmoid with the skybox lock, the densification statistics and the
-            // relevance flag of this live row
-#pragma unroll
-            for (int k = 0; k < 3; k++) ds[k] = ds[k] * act_scale(act.s_raw[3 * i + k]);
-            const float4 x = act.q_raw[i];
-            const float4 gq = make_float4(dq[0], dq[1], dq[2], dq[3]);
-            const float nq = sqrtf(x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w);
-            const float d = fmaxf(nq, 1e-12f);
-            const float gd =
-                -(gq.x * ((x.x / d) / d) + gq.y * ((x.y / d) / d) + gq.z * ((x.z / d) / d) + gq.w * ((x.w / d) / d));
-            const float gn = nq >= 1e-12f && nq != 0.f ? gd / nq : 0.f;
-            dq[0] = gq.x / d + x.x * gn;
-            dq[1] = gq.y / d + x.y * gn;
-            dq[2] = gq.z / d + x.z * gn;
-            dq[3] = gq.w / d + x.w * gn;
-            const float y = act_opacity(act.o_raw[i]);
-            const float go = (int64_t)i < act.skybox ? 0.f : g[5] * (1.f - y) * y;
-            st_out(&out.dopacity[i], go);
-            if (go != 0.f) *act.flag = 1;
-            const int r = act.radii[i];
-            if (r > 0) {
-                const float gx = g[0], gy = g[1];
-                const float nn = sqrtf(gx * gx + gy * gy);
-                act.maxr[i] = fmaxf(act.maxr[i], (float)r);
-                act.accum[i] = fmaxf(nn, act.accum[i]);
-                act.denom[i] = act.denom[i] + 1.f;
-            }
-        }
-        st_out(&out.dscales[3 * i + 0], ds[0]);
-        st_out(&out.dscales[3 * i + 1], ds[1]);
-        st_out(&out.dscales[3 * i + 2], ds[2]);
-        st_out(&reinterpret_cast<float4 *>(out.drots)[i], make_float4(dq[0], dq[1], dq[2], dq[3]));
+    for (uint32_t e = (uint32_t)t; e < n; e += blockDim.x)
+        live_row((int)(base + s_list[e]), V, D, means3D, shs, clamped, scales, rotations, mod, dscale_mod, projmatrix,
+                 campos_p, tanx, tany, fx, fy, sc, out, raw, stamps != nullptr, act);
+}
+
+__global__ __launch_bounds__(256) void grad_live_list_kernel(LiveArgs a, const uint32_t *__restrict__ stamps,
+                                                             uint32_t stamp, uint32_t *__restrict__ ctr) {
+    __shared__ uint32_t s_off[kLiveRange / 64 + 1];
+    __shared__ uint8_t s_byte[256];
+    __shared__ uint32_t s_base;
+    const int t = threadIdx.x;
+    const int64_t base = (int64_t)blockIdx.x * kLiveRange;
+    uint64_t m;
+    uint32_t byte;
+    range_compact(a, base, stamps, stamp, s_off, s_byte, m, byte);
+    if (t == 0) {
+        const uint32_t n = s_off[kLiveRange / 64];
+        s_base = n ? __hip_atomic_fetch_add(ctr, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    }
+    __syncthreads();
+    uint32_t pos = s_base + s_off[t / 8] + (uint32_t)__popcll(m & ((1ull << (8 * (t & 7))) - 1ull));
+    for (uint32_t b = byte; b; b &= b - 1u) a.sc.list[pos++] = (uint32_t)(base + 8 * t + __builtin_ctz(b));
+    nonlive_stats(a, base, byte);
+}
+
+// ctr[0]: the list's length (grad_live_list_kernel), ctr[1]: finished workgroups; the last one
+// to finish zeroes both for the next backward of the frame (the preprocess zeroed them first).
+__global__ __launch_bounds__(256) void grad_live_kernel(LiveArgs a, uint32_t *__restrict__ ctr) {
+    const uint32_t n = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const Mat4 V = load_mat4(a.viewmatrix);
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+        const int i_ = (int)a.sc.list[e];
+        live_row(i_, V, a.D, a.means3D, a.shs, a.clamped, a.scales, a.rotations, a.mod, a.dscale_mod, a.projmatrix, a.campos,
+                 a.tanx, a.tany, a.fx, a.fy, a.sc, a.out, a.raw, a.stamped, a.act);
+    }
+    // every workgroup has read n before it counts itself in
+    __syncthreads();
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(&ctr[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u) {
+        __hip_atomic_store(&ctr[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ctr[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -1014,11 +1108,22 @@ void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const Ge
         if (!rows_zeroed)
             hipLaunchKernelGGL(grad_rows_kernel, dim3((in.P + 255) / 256), dim3(256), 0, s, in.P, radii, sc, out,
                                fill ? 0 : 1);
-        hipLaunchKernelGGL(grad_live_kernel, dim3((in.P + kLiveRange - 1) / kLiveRange), dim3(256), 0, s, in.P, in.D,
-                           in.means3D, in.shs, gs.clamped, in.scales, in.rotations, in.scale_modifier,
-                           true_scale_gradient() ? in.scale_modifier : 1.0f, cam.view, cam.proj, cam.campos, cam.tanx,
-                           cam.tany, cam.fx, cam.fy, sc, out, in.raw, rows_zeroed ? zr->stamps : nullptr,
-                           rows_zeroed ? zr->stamp : 0u, act);
+        const LiveArgs la{in.P, in.D, in.means3D, in.shs, gs.clamped, in.scales, in.rotations, in.scale_modifier,
+                          true_scale_gradient() ? in.scale_modifier : 1.0f, cam.view, cam.proj, cam.campos, cam.tanx,
+                          cam.tany, cam.fx, cam.fy, sc, out, in.raw, rows_zeroed ? 1 : 0, act};
+        const uint32_t *stamps = rows_zeroed ? zr->stamps : nullptr;
+        const uint32_t stamp = rows_zeroed ? zr->stamp : 0u;
+        const int nr = (in.P + kLiveRange - 1) / kLiveRange;
+        if (sc.list) {  // gsr_set_live_list(1) when the scratch was carved
+            uint32_t *const ctr = dsort_live_words(gs);
+            hipLaunchKernelGGL(grad_live_list_kernel, dim3(nr), dim3(256), 0, s, la, stamps, stamp, ctr);
+            const int nb = std::max(1, std::min((in.P + 255) / 256, kLiveBlocksPerCU * device_cus()));
+            hipLaunchKernelGGL(grad_live_kernel, dim3(nb), dim3(256), 0, s, la, ctr);
+        } else {
+            hipLaunchKernelGGL(grad_range_kernel, dim3(nr), dim3(256), 0, s, in.P, in.D, in.means3D, in.shs, gs.clamped,
+                               in.scales, in.rotations, in.scale_modifier, la.dscale_mod, cam.view, cam.proj,
+                               cam.campos, cam.tanx, cam.tany, cam.fx, cam.fy, sc, out, in.raw, stamps, stamp, act);
+        }
         note_step_act_done(act.on != 0);
         return;
     }

@@ -53,6 +53,8 @@ constexpr int kCtlMaxSB = 8;   // local-sort frames: the longest SB list (sb_col
 constexpr int kCtlFwdReady = 9;  // the forward split's queue released by tile_order (workers launched ahead)
 constexpr int kCtlLongest = 10;  // [2]: the frame's longest tile list and superblock list (split gate hints)
 constexpr int kCtlCulled = 12;   // culled Gaussians (key 0xFFFFFFFF): the depth order's last P - visible slots
+constexpr int kCtlLive = 13;     // [2]: the backward's live-row list length and finished workgroups (backward.hip;
+                                 // zeroed again by grad_live_kernel's last workgroup)
 constexpr int kCtlHead = 16;
 // The upsweep runs at most kUpMax workgroups, each over tpb consecutive tiles, so that a pass
 // reduces at most kUpMax histogram rows (kUpMax / 4 loads per thread, all in flight at once).
@@ -161,6 +163,10 @@ __global__ __launch_bounds__(kDsThreads) void dsort_upsweep_kernel(int P, int nb
     constexpr int kTopCopies = 16;
     __shared__ uint32_t s_hist[kPasses * kRadix];
     __shared__ uint32_t s_top[kTopCopies][kRadix];
+    // the third digit (exponent bit 0 + 7 mantissa bits) repeats inside a wave when neighbouring rows
+    // have similar depths (rows in spatial order, gs_train.chunk.reorder_rows: 64-way conflicts,
+    // config-3 upsweep 15.5 -> 25.0 us per call): replicated the same way
+    __shared__ uint32_t s_mid[kTopCopies][kRadix];
     __shared__ uint32_t s_wsum[kDsWaves];
     __shared__ uint32_t s_cull;
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
@@ -169,7 +175,10 @@ __global__ __launch_bounds__(kDsThreads) void dsort_upsweep_kernel(int P, int nb
     s_hist[t] = 0u;
     if (t == 0) s_cull = 0u;
 #pragma unroll
-    for (int k = 0; k < kTopCopies * kRadix / kDsThreads; k++) (&s_top[0][0])[t + k * kDsThreads] = 0u;
+    for (int k = 0; k < kTopCopies * kRadix / kDsThreads; k++) {
+        (&s_top[0][0])[t + k * kDsThreads] = 0u;
+        (&s_mid[0][0])[t + k * kDsThreads] = 0u;
+    }
     __syncthreads();
     uint32_t run = 0;  // thread 0: tiles_touched of the workgroup's earlier tiles
     uint32_t culled = 0;  // this wave's culled keys (wave-uniform)
@@ -194,7 +203,8 @@ __global__ __launch_bounds__(kDsThreads) void dsort_upsweep_kernel(int P, int nb
             culled += (uint32_t)__popcll(__ballot(cull));
             if (e < (size_t)P && !cull) {
 #pragma unroll
-                for (int p = 0; p < kPasses - 1; p++) atomicAdd(&s_hist[p * kRadix + ((key[k] >> (8 * p)) & 0xFFu)], 1u);
+                for (int p = 0; p < kPasses - 2; p++) atomicAdd(&s_hist[p * kRadix + ((key[k] >> (8 * p)) & 0xFFu)], 1u);
+                atomicAdd(&s_mid[lane & (kTopCopies - 1)][(key[k] >> 16) & 0xFFu], 1u);
                 atomicAdd(&s_top[lane & (kTopCopies - 1)][key[k] >> 24], 1u);
             }
             sum += tl[k];
@@ -217,6 +227,9 @@ __global__ __launch_bounds__(kDsThreads) void dsort_upsweep_kernel(int P, int nb
     if (t >= (kPasses - 1) * kRadix) {
 #pragma unroll
         for (int c = 0; c < kTopCopies; c++) hv += s_top[c][t - (kPasses - 1) * kRadix];
+    } else if (t >= (kPasses - 2) * kRadix) {
+#pragma unroll
+        for (int c = 0; c < kTopCopies; c++) hv += s_mid[c][t - (kPasses - 2) * kRadix];
     }
     ctl[ctl_blkhist(nb) + (size_t)u * kPasses * kRadix + t] = hv;
     if (t == 0) {
@@ -503,6 +516,7 @@ uint32_t *dsort_maxsb_word(const GeomState &gs) { return gs.ctrl + kCtlMaxSB; }
 uint32_t *dsort_fwdready_word(const GeomState &gs) { return gs.ctrl + kCtlFwdReady; }
 uint32_t *dsort_longest_words(const GeomState &gs) { return gs.ctrl + kCtlLongest; }
 uint32_t *dsort_culled_word(const GeomState &gs) { return gs.ctrl + kCtlCulled; }
+uint32_t *dsort_live_words(const GeomState &gs) { return gs.ctrl + kCtlLive; }
 int dsort_head_words() { return kCtlHead; }
 
 }  // namespace gsr

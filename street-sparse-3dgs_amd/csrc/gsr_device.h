@@ -758,6 +758,7 @@ struct BwdScratch {
     float4 *gsum;  // per Gaussian: {dconic a, b, c, dinvdepth}, {drgb r, g, b, 0} (record_sum -> preprocess_bwd)
     float4 *acc;   // atomic mode: GeomState.acc (rec / gsum unused)
     uint64_t *live;  // atomic mode: one mask of live rows (nonzero sums) per 64 Gaussians (backward.hip)
+    uint32_t *list;  // the live rows, grad_live_list_kernel -> grad_live_kernel (P entries)
     int atomic;
 };
 

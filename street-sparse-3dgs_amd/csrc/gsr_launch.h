@@ -83,6 +83,8 @@ uint32_t *dsort_fwdready_word(const GeomState &gs);
 // the frame's longest tile list and superblock list, [2] (zeroed by the preprocess; render_fwd copies
 // them to the pinned host words)
 uint32_t *dsort_longest_words(const GeomState &gs);
+int device_cus();  // compute units of the current device (rasterizer.hip, cached)
+uint32_t *dsort_live_words(const GeomState &gs);
 uint32_t *dsort_culled_word(const GeomState &gs);  // culled Gaussians of the frame (the upsweep's sum)
 int dsort_head_words();
 // binning.hip: per-tile lists (two stable counting levels).  index_order: level 1 over the
@@ -189,6 +191,7 @@ struct StepAct {
 };
 void set_step_act(const StepAct *a);
 StepAct step_act();
+bool live_list();  // gsr_set_live_list
 void note_step_act_done(bool done);
 bool step_act_done();
 void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const GeomState &gs, const ImageState &is,

@@ -21,6 +21,20 @@
 
 using namespace gsr;
 
+namespace gsr {
+// compute units of the current device (cached per device)
+int device_cus() {
+    static int cache[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cache[dev]) {
+        int n = 0;
+        cache[dev] = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
+    }
+    return cache[dev];
+}
+}  // namespace gsr
+
 namespace {
 
 thread_local std::string g_err;
@@ -45,6 +59,7 @@ std::atomic<int> g_binning_mode{GSR_BINNING_DEFAULT};
 thread_local bool g_sparse_grad_rows = false;
 thread_local bool g_raw_params = false;  // GaussianInputs.raw, per calling thread
 thread_local gsr::StepAct g_step_act{};    // set_step_act
+std::atomic<int> g_live_list{0};           // gsr_set_live_list
 thread_local bool g_step_act_done = false;
 constexpr int kMaxDevicesK = 64;
 thread_local hipEvent_t g_k_ready[kMaxDevicesK] = {};
@@ -133,17 +148,6 @@ struct SideJoin {
     }
 };
 
-// compute units of the current device (cached per device)
-int device_cus() {
-    static int cache[kMaxDevices] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return 256;
-    if (!cache[dev]) {
-        int n = 0;
-        cache[dev] = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
-    }
-    return cache[dev];
-}
 
 // Frames whose depth sort fills every CU (P above ~1M): the SH colour pass forks right after the
 // preprocess at full width instead of after the sort (GSR_COLOR_EARLY_BIG=0 for the A/B).
@@ -365,7 +369,7 @@ ImageState carve_image(void *base, int T, int npix, size_t *bytes) {
 }
 
 // atomic mode needs no scratch (the accumulators live in the geometry buffer, GeomState.acc)
-BwdScratch carve_bwd(void *base, int64_t K, int P, bool atomic, size_t *bytes) {
+BwdScratch carve_bwd(void *base, int64_t K, int P, bool atomic, size_t *bytes, bool list) {
     Carver c(base);
     BwdScratch s{};
     s.atomic = atomic ? 1 : 0;
@@ -374,6 +378,7 @@ BwdScratch carve_bwd(void *base, int64_t K, int P, bool atomic, size_t *bytes) {
         s.gsum = c.take<float4>(2 * (size_t)P);
     }
     s.live = c.take<uint64_t>(((size_t)P + 63) / 64);
+    if (list) s.list = c.take<uint32_t>((size_t)P);  // the backward's live-row list (gsr_set_live_list)
     if (bytes) *bytes = align_up(c.off, 256);
     return s;
 }
@@ -483,6 +488,7 @@ bool gsr::true_scale_gradient() { return g_true_scale_grad.load(std::memory_orde
 void gsr::set_sparse_grad_rows(bool on) { g_sparse_grad_rows = on; }
 void gsr::set_raw_params(bool on) { g_raw_params = on; }
 void gsr::set_step_act(const StepAct *a) { g_step_act = a ? *a : StepAct{}; }
+bool gsr::live_list() { return g_live_list.load(std::memory_order_relaxed) != 0; }
 gsr::StepAct gsr::step_act() { return g_step_act; }
 void gsr::note_step_act_done(bool done) { g_step_act_done = done; }
 bool gsr::step_act_done() { return g_step_act_done; }
@@ -1079,7 +1085,8 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
     // may have no record offsets (the local sort computes none)
     const bool atomic = uncleared != kDeterministicFwd;
     size_t sbytes = 0;
-    carve_bwd(nullptr, R_inst, P, atomic, &sbytes);
+    const bool list = live_list();  // read once: the carve must match the size
+    carve_bwd(nullptr, R_inst, P, atomic, &sbytes, list);
     // hierarchy cut: gradients of the R blended rows first, then scattered to the input rows
     size_t cut_off = 0;
     if (R > 0) {
@@ -1091,7 +1098,7 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
     }
     void *sbase = scratch(resize_ctx, std::max<size_t>(sbytes, 256));  // atomic mode: the live masks only
     if (!sbase) return fail(GSR_ERR_ALLOCATION, "backward scratch allocation failed");
-    BwdScratch sc = carve_bwd(sbase, R_inst, P, atomic, nullptr);
+    BwdScratch sc = carve_bwd(sbase, R_inst, P, atomic, nullptr, list);
     sc.acc = gs.acc;
 
     // sparse rows only for plain frames (the cut's rows are scattered to the input rows below)
@@ -1164,6 +1171,8 @@ int gsr_set_true_scale_gradient(int enable) {
 int gsr_set_deterministic(int enable) { return g_deterministic.exchange(enable ? 1 : 0); }
 
 int gsr_set_split_gate(int enable) { return g_split_gate.exchange(enable ? 1 : 0); }
+
+int gsr_set_live_list(int enable) { return g_live_list.exchange(enable ? 1 : 0); }
 
 int gsr_set_fwd_spin_limits(int64_t ready, int64_t flag) {
     if (ready < -1 || flag < 0 || ready >= UINT32_MAX || flag > UINT32_MAX)

@@ -123,6 +123,13 @@ def set_fwd_split_min(length: int) -> int:
     return r
 
 
+def set_live_list(enable: bool) -> bool:
+    """gsr_set_live_list: True walks the backward's live rows through one list spread over the chip
+    (rows in spatial order: gs_train.chunk.reorder_rows); False (default) per 2048-row range.  Same
+    gradients either way.  Returns the previous setting."""
+    return bool(_L.gsr_set_live_list(int(bool(enable))))
+
+
 def set_split_gate(enable: bool) -> bool:
     """gsr_set_split_gate: True (default) arms the forward split and the tile binning's superblock
     split only for the 256 frames after one whose lists called for them; False arms them on every

@@ -69,6 +69,7 @@ SIGNATURES = {
     "gsr_set_bwd_segment": (_i, [_i]),
     "gsr_set_fwd_segment": (_i, [_i]),
     "gsr_set_split_gate": (_i, [_i]),
+    "gsr_set_live_list": (_i, [_i]),
     "gsr_set_fwd_split_min": (_i, [_i]),
     "gsr_set_fwd_spin_limits": (_i, [_i64, _i64]),
     "gsr_segment_layout_check": (_i, [ctypes.c_int64, _i, _i, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
@@ -131,7 +132,7 @@ SIGNATURES = {
     "gsr_zero_grad_rows": (_i, [_i, ctypes.POINTER(_vp), ctypes.POINTER(_i64), _i64, _i64, _vp, _i64, _vp]),
 }
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 _lib = None
 
 

@@ -86,6 +86,61 @@ def reset_opacity(g, optimizer, skybox: int) -> None:
 _PARAMS = ("_xyz", "_features", "_opacity", "_scaling", "_rotation")
 
 
+def _spread3(x):
+    """The low 10 bits of x, two zero bits after each (int64): one axis of a 30-bit Morton code."""
+    x = x & 0x3FF
+    x = (x | (x << 16)) & 0x30000FF
+    x = (x | (x << 8)) & 0x300F00F
+    x = (x | (x << 4)) & 0x30C30C3
+    x = (x | (x << 2)) & 0x9249249
+    return x
+
+
+def spatial_order(xyz: torch.Tensor) -> torch.Tensor:
+    """A stable permutation of the rows of xyz (N, 3) by the 30-bit Morton code of their positions
+    quantised to 1024 steps per axis over the rows' bounding box: rows near each other in space end
+    up near each other in memory."""
+    lo = xyz.min(0).values
+    ext = (xyz.max(0).values - lo).clamp_min(1e-12)
+    q = ((xyz - lo) / ext * 1023.0).clamp(0.0, 1023.0).to(torch.int64)
+    key = _spread3(q[:, 0]) | (_spread3(q[:, 1]) << 1) | (_spread3(q[:, 2]) << 2)
+    return torch.argsort(key, stable=True)
+
+
+@torch.no_grad()
+def reorder_rows(ts, first_row: int) -> None:
+    """Permute the Gaussians after `first_row` (the skybox and scaffold rows keep their places: the
+    skybox lock and the scale shrink address them by index) into spatial order (spatial_order):
+    every parameter, its Adam moments and the densification statistics, replaced as densification
+    replaces them.  A view then covers runs of adjacent rows instead of rows scattered over the whole
+    model, so the per-row passes that touch only its visible rows (the backward's live-row chain
+    rule, the sparse Adam step, the preprocess) read and write whole cache lines instead of a line
+    per row.  The rendered images and every per-row update are the same up to the permutation."""
+    g = ts.g
+    P = g.P
+    if P - first_row < 2:
+        return
+    dev = g._xyz.device
+    perm = torch.cat((torch.arange(first_row, device=dev),
+                      spatial_order(g._xyz.detach()[first_row:]) + first_row))
+    opts = [o for o in (getattr(ts, "optimizer", None),) if o is not None]
+    for n in _PARAMS:
+        old = getattr(g, n)
+        newp = torch.nn.Parameter(old.detach().index_select(0, perm).contiguous())
+        for opt in opts:
+            st = opt.state.pop(old, None)
+            if st is not None:
+                for key in ("exp_avg", "exp_avg_sq"):
+                    if key in st and st[key].shape[:1] == (P,):
+                        st[key] = st[key].index_select(0, perm).contiguous()
+                opt.state[newp] = st
+            for group in opt.param_groups:
+                group["params"] = [newp if q is old else q for q in group["params"]]
+        setattr(g, n, newp)
+    for n in ("max_radii2D", "xyz_gradient_accum", "denom"):
+        setattr(g, n, getattr(g, n).index_select(0, perm).contiguous())
+
+
 def capture(ts) -> dict:
     """gaussians.capture() (scene/gaussian_model.py) for a joined-layout step: every parameter, the
     optimizers' moments and step counts, the densification statistics, the SH degree, the iteration
@@ -146,10 +201,24 @@ class TrainChunk:
     normals: optional callable(iteration, n_split) -> (2 n_split, 3) tensor of the standard-normal
     draws behind the split samples (parity tests inject the same draws into two runs); by default
     each run draws them from the device generator as the reference does.
-    on_checkpoint: callable(iteration, capture dict)."""
+    on_checkpoint: callable(iteration, capture dict).
+    spatial: keep the rows after the skybox / scaffold prefix in spatial order (reorder_rows) from the
+    start and again after every densification (which appends its clones and splits at the end) --
+    a row permutation the reference does not make: the images, losses and per-row updates are the
+    reference's up to it, but its split draws go to the split rows in the new index order.  It also
+    switches the library's backward to its list walk of the live rows (gsr_set_live_list), for the
+    whole process."""
 
-    def __init__(self, step, schedule: ChunkSchedule | None = None, normals=None, on_checkpoint=None):
+    def __init__(self, step, schedule: ChunkSchedule | None = None, normals=None, on_checkpoint=None,
+                 spatial: bool = False):
         self.ts = step
+        self.spatial = spatial
+        if spatial:
+            reorder_rows(step, self._fixed_rows())
+            # a view's live rows now come in runs: the backward walks them through one list
+            # (gsr_set_live_list, process-wide)
+            from diff_gaussian_rasterization import _C
+            _C.set_live_list(True)
         self.sched = schedule or ChunkSchedule()
         if getattr(step, "iterations", self.sched.iterations) != self.sched.iterations:
             raise ValueError("the step's schedules were built for a different iteration count")
@@ -157,6 +226,9 @@ class TrainChunk:
         self.on_checkpoint = on_checkpoint
         self.events = []       # one dict per densify / reset iteration
         self.event_s = 0.0     # host wall-clock inside the events (synchronised)
+
+    def _fixed_rows(self):
+        return max(int(getattr(self.ts, "skybox", 0)), int(getattr(self.ts, "scaffold", 0)))
 
     def _between(self, it, dens, reset):
         ts, s = self.ts, self.sched
@@ -168,6 +240,8 @@ class TrainChunk:
                 nrm = self.normals
                 rec.update(ts.densify_and_prune(s.densify_grad_threshold, s.min_opacity, s.percent_dense,
                                                 normals=(lambda n: nrm(it, n)) if nrm is not None else None))
+                if self.spatial:
+                    reorder_rows(ts, self._fixed_rows())
             if reset:
                 ts.reset_opacity()
                 rec["reset"] = True

@@ -155,10 +155,21 @@ def _chunk_problem(step_cls, iterations, seed=3):
     return ts
 
 
-def test_chunk_loop_native_equals_python():
+@pytest.fixture
+def live_list_restored():
+    from diff_gaussian_rasterization import _C
+    prev = _C.set_live_list(False)
+    yield
+    _C.set_live_list(prev)
+
+
+@pytest.mark.parametrize("spatial", [False, True], ids=["index_order", "spatial_order"])
+def test_chunk_loop_native_equals_python(spatial, live_list_restored):
     """train_single.py's loop with 4 densify / prune events, an opacity reset, SH increments and
     depth-only views: native executor vs Python-driven step, bit for bit (deterministic backward),
-    P after every event identical, the Adam step counts showing the skipped Gaussian updates."""
+    P after every event identical, the Adam step counts showing the skipped Gaussian updates.
+    spatial: the rows kept in spatial order (TrainChunk(spatial=True): reorder_rows after every
+    densification, the backward's live-row list walk) on both sides."""
     from helpers import deterministic
     from gs_train.chunk import TrainChunk
     from gs_train.native_step import NativeTrainStep
@@ -169,7 +180,7 @@ def test_chunk_loop_native_equals_python():
             torch.manual_seed(0)
             ts = _chunk_problem(NativeTrainStep if native else None, iters)
             torch.manual_seed(5)
-            tc = TrainChunk(ts, _small_schedule(iters))
+            tc = TrainChunk(ts, _small_schedule(iters), spatial=spatial)
             tc.run()
             out[native] = ([(e["iteration"], e["P_before"], e["P_after"]) for e in tc.events], _snapshot(ts))
     (ea, sa), (eb, sb) = out[False], out[True]
@@ -180,6 +191,48 @@ def test_chunk_loop_native_equals_python():
     assert sa[4] == 3  # degree 0 -> 3 at iterations 100, 200, 300
     # Gaussian Adam steps: iterations 1..319 minus the 3 event iterations
     assert sa[2] == [316.0] * 5
+
+
+def test_spatial_order_is_a_row_permutation(live_list_restored):
+    """TrainChunk(spatial=True) without densification (an opacity reset, SH increments, depth-only
+    views): the rows after the skybox / scaffold prefix permuted once by Morton code, and after 240
+    iterations every parameter, moment and statistic is the index-order run's, permuted -- up to the
+    rounding of exactly equal depths, whose blending order follows the row index (upstream's (depth
+    bits, index) key): the first such frame here is iteration 41, and from there the two runs drift
+    apart by fp32 noise, relative to each tensor's travel ~7e-5 (r05ao), bar 1e-3."""
+    from helpers import deterministic, record_margins
+    from gs_train.chunk import ChunkSchedule, TrainChunk, spatial_order
+    from gs_train.native_step import NativeTrainStep
+    iters = 240
+    sched = ChunkSchedule(iterations=iters, densification_interval=60, opacity_reset_interval=120,
+                          densify_from_iter=iters, densify_until_iter=iters, sh_interval=60)
+    out = {}
+    with deterministic():
+        for spatial in (False, True):
+            torch.manual_seed(0)
+            ts = _chunk_problem(NativeTrainStep, iters)
+            first = max(ts.skybox, ts.scaffold)
+            xyz0 = ts.g._xyz.detach().clone()
+            init = [getattr(ts.g, n).detach().clone() for n in NAMES]
+            torch.manual_seed(5)
+            tc = TrainChunk(ts, sched, spatial=spatial)
+            tc.run()
+            assert [e["iteration"] for e in tc.events] == [120]
+            out[spatial] = _snapshot(ts)
+    perm = torch.cat((torch.arange(first, device=DEV), spatial_order(xyz0[first:]) + first))
+    assert not torch.equal(perm, torch.arange(perm.numel(), device=DEV))
+    (pa, ma, sa, ta, da), (pb, mb, sb, tb, db) = out[False], out[True]
+    assert sa == sb and da == db
+    for n, x, y, x0 in zip(NAMES, pa, pb, init):
+        if n == "_exposure":
+            torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-6)
+            continue
+        d = ((x[perm] - y).norm() / (x - x0).norm().clamp_min(1e-30)).item()
+        record_margins(f"spatial_order_drift{n}", drift=d)
+        print(f"spatial-order drift {n}: {d:.3g}")
+        assert d <= 1e-3, (n, d)
+    # the densification statistics: the same rows saw the same views
+    assert torch.equal(ta[2][perm], tb[2])
 
 
 def _split_params(ts):

@@ -474,6 +474,42 @@ def test_sort_tile_boundaries_with_culled_rows(n_vis):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("P", [10_000, 600_000])
+def test_live_list_walk_same_bits(P):
+    """gsr_set_live_list: the backward's live rows walked through one list spread over the chip give
+    the bits the per-range walk gives (deterministic mode: record sums in a fixed order), here with
+    more live rows than the list grid's threads (600k tiny splats at 1080p: several trips each), and
+    the list's counters come back to zero for the next frame."""
+    import torch
+    from diff_gaussian_rasterization import GaussianRasterizer, _C
+    c = dict(name=f"live_list_{P}", P=P, W=1920 if P > 100_000 else 256, H=1080 if P > 100_000 else 256, deg=3,
+             seed=40, log_scale=-4.6 if P > 100_000 else -4.0)
+    s = make_scene(c)
+    dev = torch.device("cuda:0")
+    dcol, dinv = upstream_grads(c)
+    prev = _C.set_deterministic(True)
+    prev_ll = _C.set_live_list(False)
+    try:
+        out = {}
+        for mode in (False, True, True, False):
+            _C.set_live_list(mode)
+            inp = torch_inputs(s, dev)
+            color, radii, invd = GaussianRasterizer(settings(s, dev, 3))(**inp)
+            loss = (color * torch.tensor(dcol, device=dev)).sum() + (invd * torch.tensor(dinv, device=dev)).sum()
+            loss.backward()
+            out.setdefault(mode, []).append({k: v.grad.clone() for k, v in inp.items()})
+    finally:
+        _C.set_deterministic(prev)
+        _C.set_live_list(prev_ll)
+    ref = out[False][0]
+    for run in out[False][1:] + out[True]:
+        for k in ref:
+            assert torch.equal(ref[k], run[k]), k
+    live = int((ref["opacities"] != 0).sum())  # nonzero for every live row
+    assert live > (2 * 256 * 256 if P > 100_000 else 1000), live
+
+
+@pytest.mark.gpu
 def test_depth_order_large():
     """The global depth sort at 3M Gaussians (367 sort tiles) with 25% culled: the order's first
     slots are the stable (depth bits, id) order of the visible Gaussians (the culled ones are not
@@ -540,12 +576,14 @@ def test_scratch_is_released_every_frame():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("live_list", [False, True], ids=["per_range", "live_list"])
 @pytest.mark.parametrize("deterministic", [False, True])
-def test_backward_twice_through_saved_buffers(deterministic):
+def test_backward_twice_through_saved_buffers(deterministic, live_list):
     """A second backward through the same forward (loss.backward(retain_graph=True) twice,
     torch.autograd.grad twice, gradcheck-style reuse) returns the same gradients: upstream's
-    backward keeps no state between calls, and render_bwd's accumulator rows are cleared by the
-    pass that consumes them."""
+    backward keeps no state between calls, render_bwd's accumulator rows are cleared by the
+    pass that consumes them, and the live-row list's counters (gsr_set_live_list) by the last
+    workgroup that walks it."""
     import torch
     from diff_gaussian_rasterization import GaussianRasterizer, _C
     c = dict(name="twice", P=4000, W=128, H=96, deg=3, seed=31, log_scale=-3.2)
@@ -553,6 +591,7 @@ def test_backward_twice_through_saved_buffers(deterministic):
     dev = torch.device("cuda:0")
     dcol, dinv = upstream_grads(c)
     prev = _C.set_deterministic(deterministic)
+    prev_ll = _C.set_live_list(live_list)
     try:
         inp = torch_inputs(s, dev)
         color, radii, invd = GaussianRasterizer(settings(s, dev, 3))(**inp)
@@ -564,6 +603,7 @@ def test_backward_twice_through_saved_buffers(deterministic):
         g3 = [v.grad.clone() for v in leaves]
     finally:
         _C.set_deterministic(prev)
+        _C.set_live_list(prev_ll)
     for a, b, d in zip(g1, g2, g3):
         if deterministic:
             assert torch.equal(a, b) and torch.equal(a, d)

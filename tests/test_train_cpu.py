@@ -184,3 +184,50 @@ def test_chunk_schedule_events_follow_train_single():
     assert set(resets) <= set(dens)
     w = ChunkSchedule(white_background=True)
     assert w.events(500) == (False, True)
+
+
+def test_spatial_reorder_is_a_row_permutation():
+    """gs_train.chunk.reorder_rows: the rows after the fixed prefix are permuted by Morton code --
+    every parameter, both Adam moments and the densification statistics by the same permutation,
+    the optimizer's groups and state re-keyed to the new parameters, the prefix rows untouched --
+    and spatial_order is stable and groups nearby points."""
+    import types
+    from gs_train.chunk import reorder_rows, spatial_order
+    from gs_train.harness import GaussianSet
+    from gs_train.optim import Adam
+    rng = np.random.default_rng(3)
+    P, first = 500, 37
+    g = GaussianSet(rng.normal(size=(P, 3)) * 5, rng.normal(size=(P, 16, 3)), rng.uniform(0.1, 0.9, (P, 1)),
+                    np.exp(rng.normal(-3, 0.3, (P, 3))), rng.normal(size=(P, 4)), device="cpu", joined_features=True)
+    opt = Adam(g.param_groups(), lr=0.0, eps=1e-15)
+    names = ("_xyz", "_features", "_opacity", "_scaling", "_rotation")
+    for n in names:
+        p = getattr(g, n)
+        opt.state[p] = {"step": torch.tensor(3.0), "exp_avg": torch.randn_like(p), "exp_avg_sq": torch.rand_like(p)}
+    g.max_radii2D = torch.arange(P, dtype=torch.float32)
+    g.xyz_gradient_accum = torch.rand(P, 1)
+    g.denom = torch.rand(P, 1)
+    before = {n: (getattr(g, n).detach().clone(), opt.state[getattr(g, n)]["exp_avg"].clone(),
+                  opt.state[getattr(g, n)]["exp_avg_sq"].clone()) for n in names}
+    stats = {n: getattr(g, n).clone() for n in ("max_radii2D", "xyz_gradient_accum", "denom")}
+    reorder_rows(types.SimpleNamespace(g=g, optimizer=opt), first)
+    perm = g.max_radii2D.long()  # the statistics carried the row numbers
+    assert torch.equal(perm[:first], torch.arange(first))
+    assert sorted(perm.tolist()) == list(range(P))
+    want = torch.cat((torch.arange(first), spatial_order(before["_xyz"][0][first:]) + first))
+    assert torch.equal(perm, want)
+    for n in names:
+        p = getattr(g, n)
+        st = opt.state[p]
+        p0, m0, v0 = before[n]
+        assert torch.equal(p.detach(), p0[perm])
+        assert torch.equal(st["exp_avg"], m0[perm]) and torch.equal(st["exp_avg_sq"], v0[perm])
+        assert float(st["step"]) == 3.0
+        assert sum(q is p for grp in opt.param_groups for q in grp["params"]) == 1
+    assert len(opt.state) == len(names)
+    for n in ("xyz_gradient_accum", "denom"):
+        assert torch.equal(getattr(g, n), stats[n][perm])
+    # stable, and nearby points adjacent: two tight clusters come out as two runs
+    pts = torch.cat((torch.full((5, 3), 1.0), torch.full((5, 3), -1.0), torch.full((5, 3), 1.0)))
+    o = spatial_order(pts)
+    assert o.tolist() == [5, 6, 7, 8, 9, 0, 1, 2, 3, 4, 10, 11, 12, 13, 14]
