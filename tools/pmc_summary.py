@@ -23,7 +23,8 @@ STAGE_OF = [("render_bwd_kernel<true, true>", "render_bwd"), ("render_bwd_kernel
             ("render_bwd_kernel<false, true>", "render_bwd:nodepth"),
             ("render_bwd_kernel<false, false>", "render_bwd:nodepth_records"),
             ("render_bwd_kernel<true>", "render_bwd"), ("render_bwd_kernel<false>", "render_bwd:nodepth"),
-            ("render_bwd_kernel", "render_bwd"), ("render_fwd", "render_fwd"),
+            ("render_bwd_kernel", "render_bwd"), ("render_fwd_seg", "render_fwd:pool"),
+            ("render_fwd_cleanup", "render_fwd:cleanup"), ("render_fwd", "render_fwd"),
             ("preprocess_bwd_kernel", "preprocess_bwd"), ("record_sum_kernel", "record_sum"),
             ("preprocess_color_kernel", "sh_color"), ("preprocess_kernel", "preprocess"),
             ("depth_gather_kernel", "depth_gather"), ("dsort_upsweep", "depth_sort:upsweep"),
@@ -33,7 +34,9 @@ STAGE_OF = [("render_bwd_kernel<true, true>", "render_bwd"), ("render_bwd_kernel
             ("sb_base_kernel", "bin_superblocks:base"), ("sb_scatter_kernel", "bin_superblocks:scatter"),
             ("tile_bin_kernel", "bin_tiles"), ("tile_order_kernel", "tile_order"), ("mark_visible", "mark_visible"),
             ("l1_ssim_fwd", "loss_fwd"), ("l1_ssim_bwd", "loss_bwd"), ("sparse_adam", "adam"),
-            ("exposure_", "exposure"), ("densify_stats", "densify")]
+            ("exposure_", "exposure"), ("densify_stats", "densify"), ("adam_rowlist", "adam:rows"),
+            ("adam_compact", "adam:compact"), ("grad_live_list", "grad_live:list"), ("grad_live", "grad_live"),
+            ("grad_range", "grad_live"), ("l1_ssim_stream", "loss:ssim_stream")]
 # rocPRIM kernels are all `trampoline_kernel<wrapped_<algo>_config<cfg, KeyT, ...>>`: the algorithm
 # and key type tell the depth sort (u32 keys over P) from the tile sort (u16 keys over K).
 ROCPRIM = re.compile(r"wrapped_(\w+?)_config<[^,]+(?:<[^>]*>)?, (unsigned \w+)")
@@ -54,7 +57,7 @@ def stage(name):
         return f"{who}:{algo}"
     if "init_lookback" in name:
         return "rocprim:init_lookback"
-    return name.split("(")[0][:60]
+    return name.replace("(anonymous namespace)::", "").split("(")[0][:60]
 
 
 def read_pmc(d, counter):
