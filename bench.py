@@ -360,6 +360,7 @@ def config3(a, dev, seed=0, ranks=None):
     if ranks is not None:
         out["job_wall_s"] = round(ranks.max(job_wall), 3)
     del ts, tc
+    _C.set_live_list(False)  # TrainChunk(spatial=True) turned it on for the process: the later legs' rows are not spatial
     torch.cuda.empty_cache()
     return out
 
