@@ -172,3 +172,22 @@ def test_debug_mode_dumps_inputs_of_a_failing_call(tmp_path, monkeypatch, host_s
     # upstream's argument order (_RasterizeGaussians.forward): bg, means3D, colors, opacities, ...
     assert torch.equal(saved[1], m) and torch.equal(saved[14], shs) and saved[15] == 1 and saved[18] is True
     assert all(a.device.type == "cpu" for a in saved if isinstance(a, torch.Tensor))
+
+
+def test_pmc_summary_stage_names():
+    """tools/pmc_summary.py's kernel -> stage map, which the committed profiles and bench.py's
+    roofline lookups key on: the metric kernels keep their stage names, and kernels in an anonymous
+    namespace get their own (not one shared 'void gsr::' entry)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("pmc_summary", os.path.join(REPO, "tools", "pmc_summary.py"))
+    ps = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ps)
+    assert ps.stage("void gsr::render_bwd_kernel<true, true>(HIP_vector_type<unsigned int, 2u> const*)") == "render_bwd"
+    assert ps.stage("void gsr::render_fwd_kernel<1>(HIP_vector_type<unsigned int, 2u> const*)") == "render_fwd"
+    assert ps.stage("gsr::render_fwd_seg_kernel(HIP_vector_type<unsigned int, 2u> const*)") == "render_fwd:pool"
+    assert ps.stage("gsr::(anonymous namespace)::sb_scatter_kernel(int, gsr::SBGrid)") == "bin_superblocks:scatter"
+    assert ps.stage("gsr::(anonymous namespace)::adam_rowlist_kernel(gsr::AdamArgs)") == "adam:rows"
+    assert ps.stage("gsr::grad_live_list_kernel(gsr::LiveArgs, unsigned int const*)") == "grad_live:list"
+    assert ps.stage("gsr::grad_range_kernel(int, int)") == "grad_live"
+    assert ps.stage("void gsr::(anonymous namespace)::l1_ssim_stream_kernel<true>(float const*)") == "loss:ssim_stream"
+    assert ps.stage("gsr::(anonymous namespace)::tb_split_kernel(int)") == "gsr::tb_split_kernel"
