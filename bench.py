@@ -68,9 +68,18 @@ def parse():
     ap.add_argument("--chunk-positions", type=int, default=48, help="camera stations (4 cube faces each)")
     ap.add_argument("--chunk-truth", type=int, default=1_000_000, help="Gaussians of the synthetic truth street")
     ap.add_argument("--chunk-init", type=int, default=300_000, help="LiDAR-like initial points")
-    ap.add_argument("--chunk-spatial", type=int, default=1,
-                    help="1 (default): keep the chunk's rows in spatial (Morton) order (TrainChunk(spatial=True): "
-                         "gs_train.chunk.reorder_rows after every densification); 0: the reference's row order")
+    ap.add_argument("--chunk-spatial", type=int, default=0,
+                    help="row order of the headline config-3 run: 0 (default) the reference's row order; 1 the rows "
+                         "in spatial (Morton) order (TrainChunk(spatial=True): gs_train.chunk.reorder_rows after every "
+                         "densification -- a permutation the reference does not make, DESIGN.md 10.9)")
+    ap.add_argument("--no-chunk-spatial-variant", action="store_true",
+                    help="skip the second config-3 run in the other row order (reported as config3_proxy.variant)")
+    ap.add_argument("--prewarm-s", type=float, default=0.5,
+                    help="cap of the time-based pre-warm before the counted warm-ups (fwd+bwd steps until the shader "
+                         "clock settles; 0 = none)")
+    ap.add_argument("--detail-out", default=os.environ.get("GSR_BENCH_DETAIL_OUT") or None,
+                    help="also write the long diagnostics the line summarises (config 3's per-iteration record, the "
+                         "clock samples) to this JSON file")
     ap.add_argument("--post-leaves", type=int, default=3_000_000,
                     help="leaves of the train_post step's synthetic hierarchy (0 = skip that step)")
     ap.add_argument("--bwd-seg", type=int, default=None,
@@ -95,8 +104,10 @@ def algorithmic_bytes(P, Pv, K, T, npix, P1, M=16, Pl=None):
     them with the rects twice and writes the K-entry point list + ranges.  Upstream's 64-bit
     6-pass key sort alone would be 24*K*6.  The dense gradient outputs (56 + 12 M B per Gaussian:
     means2D 12, opacity 4, means3D 12, SH, scales 12, rotations 16) are zeroed by render_bwd's
-    waves after their replay; preprocess_bwd reads every row's live stamp (4 B), and for the Pl live rows the accumulator (48 B), parameters (40 B) and SH row
-    in and the full gradient row out."""
+    waves after their replay (counted under preprocess_bwd, as 8(d) counts every gradient row there, so
+    render_bwd's figure is 8(d)'s own 44 K + 24 Npix + 40 Pv); preprocess_bwd reads every row's live
+    stamp (4 B), and for the Pl live rows the accumulator (48 B), parameters (40 B) and SH row in and
+    the full gradient row out."""
     sh = 12 * M
     grad_row = 56 + sh
     Pl = Pv if Pl is None else Pl
@@ -116,8 +127,10 @@ def algorithmic_bytes(P, Pv, K, T, npix, P1, M=16, Pl=None):
         "tile_order": 16 * T,
         "tile_order_bwd": 12 * T,
         "render_fwd": 44 * K + 24 * npix,
-        "render_bwd": 44 * K + 24 * npix + 40 * Pv + grad_row * P,
-        "preprocess_bwd": 4 * P + (48 + 40 + sh + 12 + grad_row) * Pl,
+        # SURVEY.md 8(d)'s render-bwd term exactly; the dense zero gradient rows render_bwd's waves
+        # also write are booked where 8(d) books every gradient row, under preprocess-bwd
+        "render_bwd": 44 * K + 24 * npix + 40 * Pv,
+        "preprocess_bwd": 4 * P + (48 + 40 + sh + 12 + grad_row) * Pl + grad_row * P,
     }
 
 
@@ -228,7 +241,7 @@ def train_step_ms(P, W, H, steps, warmup, dev, street=True, reference=False, see
     return ms
 
 
-def config3(a, dev, seed=0, ranks=None):
+def config3(a, dev, seed=0, ranks=None, spatial=False):
     """The config-3 stand-in (BASELINE.json configs[2]: train_single.py's whole loop per chunk; the
     example_dataset is absent): gs_train.chunk.TrainChunk over a synthetic Street-sparse chunk
     (street_chunk: cube faces along a street, LiDAR-like initial points, skybox + scaffold rows,
@@ -256,7 +269,7 @@ def config3(a, dev, seed=0, ranks=None):
 
     from gs_train.chunk import view_psnr
     psnr0 = view_psnr(ts)
-    tc = TrainChunk(ts, sched, spatial=bool(a.chunk_spatial))
+    tc = TrainChunk(ts, sched, spatial=bool(spatial))
     evs, losses = [], {}
     # per iteration, for the attribution of the slowest ones: binning re-runs (capacity short), the
     # executor's buffer growths, the torch caching allocator's reserved bytes
@@ -326,43 +339,42 @@ def config3(a, dev, seed=0, ranks=None):
                      "binning_rerun": rr > prev[1], "buffer_growths": gr - prev[2],
                      "torch_reserved_growth_mb": round((res - prev[3]) / 2 ** 20, 1),
                      "view": view_k, "K": kk, "fwd_split_armed": fsf > prev[4], "tb_split_armed": tbf > prev[5],
-                     "fwd_worker_giveups": gup - prev[6]})
-    out = {"workload": f"train_single.py loop on a synthetic Street-sparse chunk: {info['views']} views "
-                       f"({info['depth_only_views']} depth-only) of {info['W']}x{info['H']} (90 deg cube faces), "
-                       f"{info['P_init']} initial Gaussians (10k skybox + 20k scaffold + LiDAR-like points), "
-                       f"{n_it} iterations with the default schedule" + ("" if n_it == 30_000 else " compressed"),
-           "iterations": n_it, "updates": len(per), "chunk_wall_s": round(wall, 3), "setup_s": round(setup_s, 2),
+                     "fwd_worker_giveups": gup - prev[6], "event_ms": e.get("ms"), "event_densify_ms": e.get("ms_densify")})
+    detail = {"slowest_iterations": slow, "iteration_ms_per_1000": [round(float(per[i:i + 1000].mean()), 3)
+                                                                    for i in range(0, len(per), 1000)],
+              "loss": {str(k): round(float(v), 5) for k, v in sorted(losses.items())},
+              "P_trace": [[e["iteration"], e["P_after"]] for e in ev],
+              "late_raster_stages_ms": {k_: round(v_, 4) for k_, v_ in acc.items()},
+              "fwd_pool": pool, "executor_buffers": ts.ctx_stats()}
+    blk = detail["iteration_ms_per_1000"]
+    # the line keeps a summary (the driver's record holds only the tail of stdout); --detail-out the rest
+    out = {"workload": f"train_single.py loop, synthetic Street-sparse chunk: {info['views']} views "
+                       f"({info['depth_only_views']} depth-only) of {info['W']}x{info['H']}, {info['P_init']} initial "
+                       f"Gaussians, {n_it} iterations, default schedule" + ("" if n_it == 30_000 else " compressed"),
+           "spatial_rows": bool(spatial), "chunk_wall_s": round(wall, 3),
+           "chunk_iterations_per_s": round(n_it / wall, 2), "setup_s": round(setup_s, 2),
            "iteration_ms": {"mean": round(float(per.mean()), 4), "median": round(float(np.median(per)), 4),
                             "p90": round(float(np.percentile(per, 90)), 4), "max": round(float(per.max()), 3),
-                            "source": "HIP events between iterations"},
-           # where the chunk's time goes over its schedule: mean ms per block of 1000 iterations
-           "iteration_ms_per_1000": [round(float(per[i:i + 1000].mean()), 3) for i in range(0, len(per), 1000)],
-           "slowest_iterations": slow, "executor_buffers": ts.ctx_stats(),
+                            "first_1000_mean": blk[0] if blk else None, "last_1000_mean": blk[-1] if blk else None},
+           # [iteration, ms, events in it: d(ensify) r(eset) s(h increment)]
+           # [iteration, ms, events in it: d(ensify) r(eset) s(h increment), host ms of its densify / reset]
+           "slowest3": [[e["iteration"], e["ms"], ("d" if e["densify"] else "") + ("r" if e["reset"] else "") +
+                         ("s" if e["sh_increment"] else ""), e["event_ms"]] for e in slow[:3]],
            "P_init": info["P_init"], "P_final": ts.g.P, "P_max": max([e["P_after"] for e in ev] + [info["P_init"]]),
            "densify_events": sum(1 for e in ev if "total" in e), "opacity_resets": sum(1 for e in ev if e.get("reset")),
            "event_s": round(tc.event_s, 3), "capacity_reruns": int(r1["reruns"] - r0["reruns"]),
            "final_sh_degree": ts.g.active_sh_degree,
-           "loss": {str(k): round(float(v), 5) for k, v in sorted(losses.items())},
+           "loss_first_last": [round(float(losses[min(losses)]), 5), round(float(losses[max(losses)]), 5)] if losses else None,
            "train_view_psnr_db": {"before": psnr0, "after": psnr1},
-           "P_trace": [[e["iteration"], e["P_after"]] for e in ev][::4],
-           "late_raster_stages_ms": {k_: round(v_, 4) for k_, v_ in acc.items()}, "late_tile_instances": late_K,
-           "late_relevant_row_frac": relevant_frac,
-           "fwd_split_frames": int(r1["fwd_split_frames"] - r0["fwd_split_frames"]),
-           "tb_split_frames": int(r1["tb_split_frames"] - r0["tb_split_frames"]),
-           "fwd_pool": {**{k_: (round(v_, 4) if isinstance(v_, float) else v_) for k_, v_ in pool.items()},
-                        "source": "s_memrealtime ticks summed over the worker pool's workgroups (gsr_fwd_pool_stats): "
-                                  "busy = lifetime - waits for tile_order's release - waits for predecessor segments"},
-           "data": "synthetic street chunk generated on the device (gs_train.chunk.street_chunk); the example_dataset "
-                   "is not available offline"}
-    out["seed"] = seed
-    out["spatial_rows"] = bool(a.chunk_spatial)
-    out["chunk_iterations_per_s"] = round(n_it / wall, 2)
+           "late_frame_ms": {k_: round(v_, 3) for k_, v_ in acc.items() if v_ > 0},
+           "late_tile_instances": late_K, "late_relevant_row_frac": relevant_frac,
+           "fwd_pool_busy_frac": round(pool.get("busy_frac", 0.0), 4) if isinstance(pool.get("busy_frac"), float) else None,
+           "seed": seed}
     if ranks is not None:
         out["job_wall_s"] = round(ranks.max(job_wall), 3)
     del ts, tc
-    _C.set_live_list(False)  # TrainChunk(spatial=True) turned it on for the process: the later legs' rows are not spatial
     torch.cuda.empty_cache()
-    return out
+    return out, detail
 
 
 def train_post_ms(a, dev):
@@ -849,6 +861,64 @@ class ClockProbe:
         return summ
 
 
+SECONDARY_LEGS = ("train_step", "config4", "street_frame", "coarse_debug", "train_post_step", "config3_proxy",
+                  "config5", "cpu_baseline_torch", "psnr_vs_oracle")
+PROSE_KEYS = ("workload", "data", "source", "collectives", "reference")
+
+
+def compact_legs(out, detail):
+    """Keep the line short (the driver's record holds only the last ~8 kB of stdout, and the metric's
+    diagnostics come last): the secondary legs' prose fields (workload descriptions, data and source
+    notes) move to the detail file, keyed by their path; the numbers stay in the line."""
+    prose = detail.setdefault("prose", {})
+
+    def strip(d, path):
+        for k in list(d):
+            if k in PROSE_KEYS and isinstance(d[k], str):
+                prose[path + "." + k] = d.pop(k)
+            elif isinstance(d[k], dict):
+                strip(d[k], path + "." + k)
+    for leg in SECONDARY_LEGS:
+        if isinstance(out.get(leg), dict):
+            strip(out[leg], leg)
+    c5 = out.get("config5")
+    if isinstance(c5, dict) and isinstance(c5.get("render_post_order"), dict):
+        detail["config5_render_post_order_stages_ms"] = c5["render_post_order"].pop("raster_stages_ms", None)
+
+
+def prewarm(step, probe, max_s=0.5, min_s=0.1, tol=0.03, burst=20):
+    """Time-based pre-warm before the counted warm-ups: the bench's own fwd+bwd step in bursts of
+    `burst` steps (synchronised), the shader clock read after each, until it has settled -- the last
+    two readings within `tol` of each other and of the highest seen, after at least `min_s` -- or
+    `max_s` has passed.  The GPU leaves the set-up idle at 1.6-1.8 GHz and reaches its ~2.37 GHz
+    under this load only after some ms (gpu_clock.before in round 5's lines): without this the
+    driver's 20-step timed region started on the ramp.  Returns what it did, for the line."""
+    import torch
+    if max_s <= 0:
+        return {"ms": 0.0, "steps": 0}
+    clks, n = [], 0
+    t0 = time.perf_counter()
+    while True:
+        for _ in range(burst):
+            step()
+        torch.cuda.synchronize()
+        n += burst
+        r = probe.read()
+        if r and r.get("current_gfxclk"):
+            clks.append(float(r["current_gfxclk"]))
+        el = time.perf_counter() - t0
+        if el >= max_s:
+            break
+        if el >= min_s and len(clks) >= 2:
+            hi = max(clks)
+            if clks[-1] >= (1 - tol) * hi and abs(clks[-1] - clks[-2]) <= tol * hi:
+                break
+    return {"ms": round((time.perf_counter() - t0) * 1e3, 1), "steps": n, "settled": el < max_s,
+            "gfxclk_samples_mhz": clks[-4:],
+            "rule": f"bursts of {burst} steps until two clock readings within {tol:.0%} of each other and of the "
+                    f"highest seen, after >= {min_s} s, cap {max_s} s"}
+
+
 def stage_profile(step, n):
     """Per-stage device time (HIP events on the rasterizer's stream) averaged over n extra steps."""
     from diff_gaussian_rasterization import _C
@@ -1030,7 +1100,10 @@ def main():
     probe = ClockProbe(dev)
     per_step = []
     host_side = {}
+    clk_idle = probe.read()
+    pw = prewarm(step, probe, max_s=a.prewarm_s)
     clk_before = probe.read()
+    pw["gfxclk_at_timed_start"] = (clk_before or {}).get("current_gfxclk")
     elapsed = timed(step, a.steps, a.warmup, ranks, per_step=per_step, host=host_side)
     clk_after = probe.read()
 
@@ -1064,6 +1137,8 @@ def main():
 
     ms_per_step = elapsed / a.steps * 1e3
     value = world * npix * a.steps / elapsed / 1e6
+    strict_frac = strict_8d / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if dom == "render_bwd" and dom_ms > 0 else None
+    zero_rows = (56 + 12 * inp["shs"].shape[1]) * P
     out = {
         "metric": "fwd+bwd Mpix/s at 1080p (1M Gaussians)",  # + "train_step" ms below
         "value": round(value, 3),
@@ -1082,31 +1157,43 @@ def main():
                    "level1_entries": P1, "max_sb_list": wl["max_sb_list"],
                    "tb_split_items": wl["tb_split_items"], "live_rows": Pl, "tiles": T, "bwd_segment": bwd_seg, "fwd_segment": fwd_seg,
                    "parallelism": f"chunk-per-gpu x{world}"},
-        # frac: algorithmic bytes / the kernel's HIP-event time measured here; frac_rocprof: the same
-        # bytes / the average duration in the committed rocprofv3 summary of these kernel sources
-        # (profiles/, null when no summary of the current sources is committed)
+        # frac: SURVEY.md 8(d)'s algorithmic bytes of the dominant kernel (render_bwd: 44 K + 24 Npix +
+        # 40 Pv) / its HIP-event time measured here; frac_rocprof: the same bytes / the average duration
+        # in the committed rocprofv3 summary of these kernel sources (profiles/, null when no summary
+        # of the current sources is committed); frac_with_zero_rows: also counting the dense zero
+        # gradient rows render_bwd's waves write (8(d) books them under preprocess-bwd)
         "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "algorithmic_bytes": abytes[dom], "avg_ms": round(dom_ms, 5),
                      "traffic_source": traffic_src, "profile_is_current": traffic_cur, "rocprof_avg_ms": rp_ms,
                      "frac_rocprof": round(abytes[dom] / (rp_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if rp_ms else None,
                      "kernel_source_sha": kernel_source_sha(),
-                     # SURVEY.md 8(d)'s own render-bwd term (44 K + 24 Npix + 40 Pv), without the dense
-                     # zero gradient rows render_bwd also writes (they belong to preprocess-bwd's 260 P there)
-                     "algorithmic_bytes_strict_8d": strict_8d,
-                     "frac_strict_8d": round(strict_8d / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if dom == "render_bwd" else None},
-        "valu_roofline": [r for r in (valu_roofline(k, stages.get(k)) for k in ("render_bwd", "render_fwd")) if r],
-        "step_dispersion": dispersion(per_step),
-        "host_issue": host_side,
-        "gpu_clock": {"before": clk_before, "after": clk_after, "under_load": clk_load,
-                      "unit": "MHz / W / C (amdsmi GPU metrics)", "error": probe.err},
-        "stages_ms": {k: round(v, 5) for k, v in stages.items()},
+                     "frac_strict_8d": round(strict_frac, 5) if strict_frac is not None else None,
+                     "frac_with_zero_rows": round((abytes[dom] + zero_rows) / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+                     if dom == "render_bwd" and dom_ms > 0 else None},
+    }
+    diag = {
+        "valu_roofline": [{k_: r[k_] for k_ in ("kernel", "achieved", "unit", "frac_of_sustained",
+                                                 "valu_instr_per_launch", "avg_ms", "rocprof_avg_ms")}
+                          for r in (valu_roofline(k, stages.get(k)) for k in ("render_bwd", "render_fwd")) if r],
         "stage_bytes": {k: int(v) for k, v in abytes.items()},
         # stages on the main stream (sh_color overlaps the sort / binning on a side stream)
         "pipeline_roofline": {"algorithmic_bytes": sum(abytes.values()),
                               "frac": round(sum(abytes.values()) / (serial_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
                               if serial_ms > 0 else None},
+        "stages_ms": {k: round(v, 5) for k, v in stages.items()},
+        "step_dispersion": dispersion(per_step),
+        "host_issue": host_side,
+        "gpu_clock": {"idle_mhz": (clk_idle or {}).get("current_gfxclk"),
+                      "timed_start_mhz": (clk_before or {}).get("current_gfxclk"),
+                      "timed_end_mhz": (clk_after or {}).get("current_gfxclk"),
+                      "under_load_median_mhz": (clk_load or {}).get("current_gfxclk_median"),
+                      "under_load_power_w": (clk_load or {}).get("current_socket_power_median"),
+                      "under_load_hotspot_c_max": (clk_load or {}).get("temperature_hotspot_max"),
+                      "source": "amdsmi GPU metrics", "error": probe.err},
+        "prewarm": pw,
     }
+    detail = {"gpu_clock": {"idle": clk_idle, "before": clk_before, "after": clk_after, "under_load": clk_load}}
     del step, raster
     if a.train_steps > 0:
         log("train step")
@@ -1143,13 +1230,19 @@ def main():
         out["train_post_step"] = train_post_ms(a, dev)
     if world == 1 and not a.no_config3:
         log("config 3 stand-in: train_single.py loop on a synthetic street chunk")
-        out["config3_proxy"] = config3(a, dev)
+        out["config3_proxy"], detail["config3"] = config3(a, dev, spatial=bool(a.chunk_spatial))
+        if not a.no_chunk_spatial_variant:
+            log("config 3 stand-in, rows in the other order")
+            v, detail["config3_variant"] = config3(a, dev, spatial=not a.chunk_spatial)
+            out["config3_proxy"]["variant"] = {k_: v[k_] for k_ in ("spatial_rows", "chunk_wall_s", "iteration_ms",
+                                                                      "slowest3", "P_final", "train_view_psnr_db")}
     if not a.no_config4 and not a.no_config3:
         # config 4 as the product runs it (scripts/full_train.py:171-232): one whole chunk per GPU --
         # every rank trains its own synthetic street chunk (seed = chunk id = rank) through the
         # train_single.py loop, no collective on the data path.  At N = 1 the chunk is config 3's run.
         log("config 4: one whole chunk per rank")
-        one = out.get("config3_proxy") if world == 1 else config3(a, dev, seed=rank, ranks=ranks)
+        one = out.get("config3_proxy") if world == 1 else config3(a, dev, seed=rank, ranks=ranks,
+                                                                   spatial=bool(a.chunk_spatial))[0]
         if one is not None:
             walls = ranks.gather(one["chunk_wall_s"])
             job = one.get("job_wall_s", one["chunk_wall_s"])
@@ -1170,7 +1263,17 @@ def main():
             color, _, invd = raster_again(s, inp, W, H, deg, dev)
         out["psnr_vs_oracle"] = psnr_vs_oracle(color, invd, st)
     out["process_group"] = dist.get_backend() if use_pg else None
+    # the metric's own diagnostics last: the driver's record keeps only the tail of stdout
+    compact_legs(out, detail)
+    for k_ in ("step_dispersion", "host_issue", "prewarm"):
+        for p_ in ("source", "rule"):
+            if isinstance(diag.get(k_), dict) and p_ in diag[k_]:
+                detail.setdefault("prose", {})[k_ + "." + p_] = diag[k_].pop(p_)
+    out.update(diag)
     if rank == 0:
+        if a.detail_out:
+            with open(a.detail_out, "w") as f:
+                json.dump(detail, f)
         print(json.dumps(out), flush=True)
     if use_pg:
         dist.barrier()

@@ -209,9 +209,13 @@ bool bwd_zero_rows(const GaussianInputs &in, const GaussianGrads &out, const Bwd
 // live3 != NULL (sparse gradient rows): when no row is relevant, the dense fallback takes a zero
 // gradient for rows whose live3[3 row + 2] is 0 (never written) and for the locked skybox rows
 // below `skybox` (train_single.py:217-223 zeroes all six of their gradients).
+// row_list: scratch of >= P + 64 ints for the compacted row list (the train context's grow-only
+// slot); NULL: allocated per call in stream order, and the row-block kernel (no scratch) runs when
+// that allocation fails.
 int sparse_adam(int n_groups, const gsr_adam_group *groups, int64_t P, const float *relevance, double beta1,
                 double beta2, double eps, int *flag_scratch, bool flag_ready, hipStream_t s, float *shrink_raw,
-                int64_t shrink_first, float shrink_limit, const float *live3 = nullptr, int64_t skybox = 0);
+                int64_t shrink_first, float shrink_limit, const float *live3 = nullptr, int64_t skybox = 0,
+                int *row_list = nullptr);
 // SSIM map forward (+ masked inverse-depth L1 forward with its gradient for an upstream of 1 when
 // mono != NULL) and the loss epilogue: losses[0..2] photometric, [3..4] depth, [5] total; *flag = 0.
 // one != NULL: gmap receives the photometric gradient itself (dL/dloss = *one, times alpha when

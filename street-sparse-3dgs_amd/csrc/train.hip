@@ -1804,7 +1804,7 @@ void set_lds_attr() {
 // activate_bwd_step_kernel computed it), so the any_nonzero pass is skipped.
 int sparse_adam(int n_groups, const gsr_adam_group *groups, int64_t P, const float *relevance, double beta1,
                 double beta2, double eps, int *flag_scratch, bool flag_ready, hipStream_t s, float *shrink_raw,
-                int64_t shrink_first, float shrink_limit, const float *live3, int64_t skybox) {
+                int64_t shrink_first, float shrink_limit, const float *live3, int64_t skybox, int *row_list) {
     if ((shrink_raw || live3) && adam_elementwise()) {
         set_last_error("sparse Adam: the fused scale shrink / sparse rows need the row-block kernel");
         return GSR_ERR_UNSUPPORTED;
@@ -1886,12 +1886,18 @@ int sparse_adam(int n_groups, const gsr_adam_group *groups, int64_t P, const flo
                 lm.col[lm.lanes++] = (uint8_t)c;
             }
         }
-        if (fits && P <= 0x7fffffff) {
-            int *buf = nullptr;  // the row list and its counter: stream-ordered scratch from the device pool
-            if (hipMallocAsync(reinterpret_cast<void **>(&buf), sizeof(int) * ((size_t)P + 64), s) != hipSuccess) {
-                set_last_error("gsr_sparse_adam_step: row list allocation failed");
-                return GSR_ERR_ALLOCATION;
+        // the row list and its counter: the caller's scratch, or stream-ordered scratch of this call;
+        // if that allocation fails the row-block kernel (which needs none) runs instead
+        int *buf = row_list;
+        bool own = false;
+        if (fits && P <= 0x7fffffff && !buf) {
+            if (hipMallocAsync(reinterpret_cast<void **>(&buf), sizeof(int) * ((size_t)P + 64), s) == hipSuccess) own = true;
+            else {
+                (void)hipGetLastError();
+                buf = nullptr;
             }
+        }
+        if (fits && P <= 0x7fffffff && buf) {
             int *count = buf, *list = buf + 64;
             const ShrinkArgs sha{shrink_raw, shrink_first, shrink_limit};
             (void)hipMemsetAsync(count, 0, sizeof(int), s);
@@ -1902,7 +1908,7 @@ int sparse_adam(int n_groups, const gsr_adam_group *groups, int64_t P, const flo
             hipLaunchKernelGGL(adam_rowlist_kernel, dim3(4096), dim3(256), 0, s, a, lm, (const int *)list,
                                (const int *)count, P, flag, (float)beta1, (float)beta2, (float)(1.0 - beta1),
                                (float)(1.0 - beta2), (float)eps, sha, DenseRows{live3, skybox});
-            (void)hipFreeAsync(buf, s);
+            if (own) (void)hipFreeAsync(buf, s);
         } else
             hipLaunchKernelGGL(sparse_adam_rows_kernel,
                            dim3((unsigned)((P + kAdamThreads - 1) / kAdamThreads), (unsigned)n_groups),

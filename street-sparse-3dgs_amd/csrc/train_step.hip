@@ -38,6 +38,7 @@ enum Slot {
     kColor, kInvDepth, kExposed, kGradMap, kDColor, kDInvDepth,            // image-sized
     kScales, kRots, kOpac, kDScales, kDRots, kDOpac, kDMeans2D, kRadii,    // per-Gaussian
     kLossScratch, kExpScratch, kDepthScratch, kWords,                      // small
+    kAdamList,                                                             // sparse Adam's row list
     kSlots
 };
 
@@ -56,25 +57,37 @@ struct gsr_train_ctx {
     bool failed_alloc = false;
     bool one_written = false;
     int64_t growths = 0;  // gsr_train_ctx_stats
-    // Stream-ordered growth (hipFreeAsync / hipMallocAsync from the device's pool, which keeps what is
-    // freed): a training loop whose P and K grow over its densification events re-sizes its buffers
-    // without a host wait -- the synchronous form (GSR_STEP_SYNC_ALLOC=1: wait for the stream, hipFree,
-    // hipMalloc) stalls the host at every growth and hipMalloc of a large block maps its pages.
+    // Stream-ordered growth (hipFreeAsync / hipMallocFromPoolAsync from the context's own memory pool,
+    // which keeps what is freed): a training loop whose P and K grow over its densification events
+    // re-sizes its buffers without a host wait -- the synchronous form (GSR_STEP_SYNC_ALLOC=1: wait for
+    // the stream, hipFree, hipMalloc) stalls the host at every growth and hipMalloc of a large block
+    // maps its pages.  The pool is the context's, not the device's default pool, so other
+    // stream-ordered users in the process keep the default pool's release behaviour.
     const bool async_alloc = [] {
         const char *e = std::getenv("GSR_STEP_SYNC_ALLOC");
         return !(e && e[0] == '1');
     }();
     bool pool_ready = false;
+    hipMemPool_t pool = nullptr;
 
     void pool_setup() {
         if (pool_ready) return;
         pool_ready = true;
         int dev = 0;
-        hipMemPool_t pool;
-        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-            uint64_t keep = UINT64_MAX;  // freed blocks stay in the pool for the next growth
-            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+        if (hipGetDevice(&dev) != hipSuccess) return;
+        hipMemPoolProps props;
+        std::memset(&props, 0, sizeof(props));
+        props.allocType = hipMemAllocationTypePinned;
+        props.handleTypes = hipMemHandleTypeNone;
+        props.location.type = hipMemLocationTypeDevice;
+        props.location.id = dev;
+        if (hipMemPoolCreate(&pool, &props) != hipSuccess) {
+            pool = nullptr;  // hipMallocAsync from the default pool, with its own release threshold
+            (void)hipGetLastError();
+            return;
         }
+        uint64_t keep = UINT64_MAX;  // freed blocks stay in this pool for the next growth
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
     }
 
     // grow-only, 1/4 more than asked (rasterizer buffers follow K)
@@ -90,7 +103,9 @@ struct gsr_train_ctx {
             if (b.p) (void)hipFreeAsync(b.p, stream);
             b.p = nullptr;
             b.cap = 0;
-            if (hipMallocAsync(&b.p, want, stream) != hipSuccess) {
+            const hipError_t e = pool ? hipMallocFromPoolAsync(&b.p, want, pool, stream)
+                                      : hipMallocAsync(&b.p, want, stream);
+            if (e != hipSuccess) {
                 b.p = nullptr;
                 failed_alloc = true;
                 return nullptr;
@@ -120,8 +135,15 @@ struct gsr_train_ctx {
     float *f32(int slot, size_t n) { return static_cast<float *>(get(slot, n * sizeof(float))); }
 
     ~gsr_train_ctx() {
-        for (auto &b : buf)
-            if (b.p) (void)hipFree(b.p);
+        if (async_alloc) {
+            for (auto &b : buf)
+                if (b.p) (void)hipFreeAsync(b.p, stream);
+            (void)hipStreamSynchronize(stream);
+            if (pool) (void)hipMemPoolDestroy(pool);
+        } else {
+            for (auto &b : buf)
+                if (b.p) (void)hipFree(b.p);
+        }
     }
 };
 
@@ -236,6 +258,8 @@ int gsr_train_step(gsr_train_ctx *ctx, const gsr_train_step_args *a, int64_t *nu
         ctx->get(kDepthScratch, std::max(gsr_depth_l1_scratch_bytes(npix), gsr_depth_only_scratch_bytes(npix)));
     // words: [0] the Adam relevance flag, [1] dL/dloss = 1 (the upstream of loss.backward())
     void *words = ctx->get(kWords, 64);
+    // the sparse Adam's compacted row list (grow-only; without it the row-block kernel runs)
+    int *adam_list = static_cast<int *>(ctx->get(kAdamList, sizeof(int) * ((size_t)P + 64)));
     if (ctx->failed_alloc || !scales || !rots || !opac || !d_scales || !d_rots || !d_opac || !d_means2D || !radii ||
         !color || !invd || !image || !gmap || !d_color || !d_invd || !loss_scratch || !exp_scratch ||
         !depth_scratch || !words) {
@@ -342,7 +366,7 @@ int gsr_train_step(gsr_train_ctx *ctx, const gsr_train_step_args *a, int64_t *nu
     if (!a->skip_gaussian_step &&
         (rc = sparse_adam(a->n_groups, a->groups, P, a->opacity_grad, a->beta1, a->beta2, a->eps, flag, true, s,
                           a->scaling, a->scaffold_rows, a->max_scale, sparse_rows ? d_means2D : nullptr,
-                          a->skybox_rows)))
+                          a->skybox_rows, adam_list)))
         return fail_step(rc, "sparse Adam + shrink");
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {

@@ -62,15 +62,31 @@ def inverse_sigmoid(x):
     return torch.log(x / (1 - x))
 
 
+def _reset_values(op, skybox):
+    """The reset's new opacity column (scene/gaussian_model.py:528-532), in the reference's torch ops."""
+    rest = torch.sigmoid(op[skybox:])
+    return torch.cat((op[:skybox], inverse_sigmoid(torch.min(rest, torch.ones_like(rest) * 0.01))), 0)
+
+
+@torch.no_grad()
+def warm_event_ops(device) -> None:
+    """Run the opacity reset's torch ops once on a few rows.  torch's ROCm kernels load their code
+    objects on first use, ~90 ms for this op sequence (tools/first_call_cost.py, r06a: min 31 ms,
+    log / division 40 ms, ...); in a fresh process the first reset (iteration 3000) paid it inside
+    its iteration (config 3's slowest iteration, 116-121 ms).  TrainChunk calls this at set-up."""
+    op = torch.linspace(-2.0, 2.0, 64, device=device).reshape(64, 1)
+    _reset_values(op, 8)
+    torch.zeros_like(op)
+    torch.nn.Parameter(op.contiguous())
+
+
 @torch.no_grad()
 def reset_opacity(g, optimizer, skybox: int) -> None:
     """scene/gaussian_model.py:528-532 + replace_tensor_to_optimizer (:546-559) on a joined-layout
     GaussianSet and its gs_train.optim.Adam: opacities of the rows after the skybox become
     min(opacity, 0.01) (in logit space), the opacity group's moments restart at zero, its step
     count stays."""
-    op = g._opacity.detach()
-    rest = torch.sigmoid(op[skybox:])
-    new = torch.cat((op[:skybox], inverse_sigmoid(torch.min(rest, torch.ones_like(rest) * 0.01))), 0)
+    new = _reset_values(g._opacity.detach(), skybox)
     old = g._opacity
     newp = torch.nn.Parameter(new.contiguous())
     st = optimizer.state.pop(old, None)
@@ -205,9 +221,10 @@ class TrainChunk:
     spatial: keep the rows after the skybox / scaffold prefix in spatial order (reorder_rows) from the
     start and again after every densification (which appends its clones and splits at the end) --
     a row permutation the reference does not make: the images, losses and per-row updates are the
-    reference's up to it, but its split draws go to the split rows in the new index order.  It also
-    switches the library's backward to its list walk of the live rows (gsr_set_live_list), for the
-    whole process."""
+    reference's up to it, but its split draws go to the split rows in the new index order.  While
+    run() runs it also switches the library's backward to its list walk of the live rows
+    (gsr_set_live_list, a process-wide knob); the previous setting is restored when run() returns or
+    raises, so later work in the process with rows in index order keeps the per-range walk."""
 
     def __init__(self, step, schedule: ChunkSchedule | None = None, normals=None, on_checkpoint=None,
                  spatial: bool = False):
@@ -215,11 +232,8 @@ class TrainChunk:
         self.spatial = spatial
         if spatial:
             reorder_rows(step, self._fixed_rows())
-            # a view's live rows now come in runs: the backward walks them through one list
-            # (gsr_set_live_list, process-wide)
-            from diff_gaussian_rasterization import _C
-            _C.set_live_list(True)
         self.sched = schedule or ChunkSchedule()
+        warm_event_ops(step.g._xyz.device)
         if getattr(step, "iterations", self.sched.iterations) != self.sched.iterations:
             raise ValueError("the step's schedules were built for a different iteration count")
         self.normals = normals
@@ -242,12 +256,16 @@ class TrainChunk:
                                                 normals=(lambda n: nrm(it, n)) if nrm is not None else None))
                 if self.spatial:
                     reorder_rows(ts, self._fixed_rows())
+            t1 = time.perf_counter()
             if reset:
                 ts.reset_opacity()
                 rec["reset"] = True
             rec["P_after"] = ts.g.P
             torch.cuda.synchronize()
-            self.event_s += time.perf_counter() - t0
+            t2 = time.perf_counter()
+            rec["ms"] = round((t2 - t0) * 1e3, 3)  # host wall clock of the event (densify part to t1)
+            rec["ms_densify"] = round((t1 - t0) * 1e3, 3)
+            self.event_s += t2 - t0
             self.events.append(rec)
         return run
 
@@ -267,11 +285,20 @@ class TrainChunk:
         """Iterations from the step's current one up to `until` (default: iterations - 1, the last
         one that updates the model).  callback(iteration, loss tensor) after each."""
         last = self.sched.iterations - 1 if until is None else until
-        while self.ts.iteration <= last:
-            it = self.ts.iteration
-            loss = self.iteration()
-            if callback is not None:
-                callback(it, loss)
+        prev = None
+        if self.spatial:
+            # a view's live rows come in runs: the backward walks them through one list
+            from diff_gaussian_rasterization import _C
+            prev = _C.set_live_list(True)
+        try:
+            while self.ts.iteration <= last:
+                it = self.ts.iteration
+                loss = self.iteration()
+                if callback is not None:
+                    callback(it, loss)
+        finally:
+            if prev is not None:
+                _C.set_live_list(prev)
 
 
 # ---- a synthetic Street-sparse chunk (the config-3 stand-in; the example_dataset is absent) ------

@@ -44,17 +44,32 @@ def test_library_metadata_calls_without_gpu():
     assert L.gsr_stage_times_ms(buf, 8) >= 0
 
 
-@pytest.mark.parametrize("L,Lf", [(512, 0), (0, 4096), (512, 4096), (512, 2048), (512, 1024), (1024, 8192), (64 * 9, 64 * 17)])
+# (L, Lf) -> the largest extension of the binning buffer past the point and level-1 lists' own room,
+# as a fraction of that room, at K >= 1M (the default 512 / 2048 measured 5.2%; 512 / 1024 40%)
+SEG_EXTENSION_BOUND = {(512, 0): 0.0, (0, 4096): 0.0, (512, 4096): 0.0, (512, 2048): 0.08, (512, 1024): 0.45,
+                       (1024, 8192): 0.0, (64 * 9, 64 * 17): 0.35}
+
+
+@pytest.mark.parametrize("L,Lf", sorted(SEG_EXTENSION_BOUND))
 def test_segment_regions_fit_the_binning_buffer(L, Lf):
     """The backward checkpoints / segment list and the forward items' arrays fit
-    in the binning buffer past the point list for every K (host arithmetic, no GPU)."""
+    in the binning buffer past the point list for every K (host arithmetic, no GPU), and the buffer
+    reaches past the point and level-1 lists' own room (the carve without segments, L = Lf = 0) by
+    no more than SEG_EXTENSION_BOUND: carve_binning extends the buffer to the segment regions' end
+    by construction, so need <= have alone cannot fail; the extension bound shows when the regions
+    outgrow the lists' room (a layout change that grows the forward items or checkpoints)."""
     from diff_gaussian_rasterization import _lib
     lib = _lib.load()
-    need, have = ctypes.c_int64(), ctypes.c_int64()
+    need, have, need0, room = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
     for K in [0, 1, 63, 64, 511, 512, 513, 4095, 4096, 8193, 10_000, 123_457, 1 << 20, 13_900_000,
               (1 << 31) - 1, 3_000_000_000]:
         rc = lib.gsr_segment_layout_check(K, L, Lf, ctypes.byref(need), ctypes.byref(have))
         assert rc == 0 and need.value <= have.value, (K, need.value, have.value)
+        assert lib.gsr_segment_layout_check(K, 0, 0, ctypes.byref(need0), ctypes.byref(room)) == 0
+        assert have.value >= room.value, (K, have.value, room.value)  # the lists are always carved
+        if K >= 1 << 20:
+            ext = (have.value - room.value) / room.value
+            assert ext <= SEG_EXTENSION_BOUND[(L, Lf)] + 1e-9, (K, L, Lf, ext)
     assert lib.gsr_segment_layout_check(-1, L, Lf, None, None) != 0
 
 

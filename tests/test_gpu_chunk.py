@@ -171,6 +171,7 @@ def test_chunk_loop_native_equals_python(spatial, live_list_restored):
     spatial: the rows kept in spatial order (TrainChunk(spatial=True): reorder_rows after every
     densification, the backward's live-row list walk) on both sides."""
     from helpers import deterministic
+    from diff_gaussian_rasterization import _C
     from gs_train.chunk import TrainChunk
     from gs_train.native_step import NativeTrainStep
     iters = 320
@@ -182,6 +183,8 @@ def test_chunk_loop_native_equals_python(spatial, live_list_restored):
             torch.manual_seed(5)
             tc = TrainChunk(ts, _small_schedule(iters), spatial=spatial)
             tc.run()
+            # run() restores the process-wide live-list knob it sets for spatial rows
+            assert _C.set_live_list(False) is False
             out[native] = ([(e["iteration"], e["P_before"], e["P_after"]) for e in tc.events], _snapshot(ts))
     (ea, sa), (eb, sb) = out[False], out[True]
     assert ea == eb

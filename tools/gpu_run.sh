@@ -8,6 +8,8 @@
 #   host             tools/host_overhead.py (host cost of the API step)
 #   metric           bench.py --metric-only (the headline line only) -> metric.json
 #   bench            the full default bench line                    -> bench.json
+#   driver           exactly the driver's command, `python3 bench.py --gpus 1 --steps 20 --warmup 5`
+#                    (its long diagnostics via GSR_BENCH_DETAIL_OUT)  -> driver.json, driver_detail.json
 #   profile          tools/profile_gpu.sh <tag> (rocprofv3 stats + PMC) -> gpurun_out/prof_<tag>/summary.json
 #   c3               the config-3 stand-in only (bench.py, a 30k-iteration street chunk) -> c3.json
 #   py=<script args> python3 -u <script args>                       -> py.log (appended)
@@ -25,6 +27,8 @@ for st in "$@"; do
         host) timeout -k 10 300 python3 -u tools/host_overhead.py > "$O/host.log" 2>&1 ;;
         metric) timeout -k 10 300 python3 -u bench.py --metric-only > "$O/metric.json" 2> "$O/metric.err" ;;
         bench) timeout -k 10 900 python3 -u bench.py > "$O/bench.json" 2> "$O/bench.err" ;;
+        driver) GSR_BENCH_DETAIL_OUT="$O/driver_detail.json" timeout -k 10 900 python3 bench.py --gpus 1 --steps 20 --warmup 5 \
+                    > "$O/driver.json" 2> "$O/driver.err" ;;
         profile) bash tools/profile_gpu.sh "$TAG" ;;
         c3) timeout -k 10 600 python3 -u bench.py $C3 > "$O/c3.json" 2> "$O/c3.err" ;;
         py=*) timeout -k 10 600 python3 -u ${st#py=} >> "$O/py.log" 2>&1 ;;
