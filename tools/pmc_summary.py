@@ -26,7 +26,8 @@ STAGE_OF = [("render_bwd_kernel<true, true>", "render_bwd"), ("render_bwd_kernel
             ("render_bwd_kernel", "render_bwd"), ("render_fwd_seg", "render_fwd:pool"),
             ("render_fwd_cleanup", "render_fwd:cleanup"), ("render_fwd", "render_fwd"),
             ("preprocess_bwd_kernel", "preprocess_bwd"), ("record_sum_kernel", "record_sum"),
-            ("preprocess_color_kernel", "sh_color"), ("preprocess_kernel", "preprocess"),
+            ("preprocess_color_kernel<true", "sh_color:cut"), ("preprocess_color_kernel", "sh_color"),
+            ("lod_count_kernel", "lod:count"), ("lod_put_kernel", "lod:put"), ("lod_weights_kernel", "lod:weights"), ("preprocess_kernel", "preprocess"),
             ("depth_gather_kernel", "depth_gather"), ("dsort_upsweep", "depth_sort:upsweep"),
             ("dsort_pass_kernel<0>", "depth_sort:pass0"), ("dsort_pass_kernel<1>", "depth_sort:pass1"),
             ("dsort_pass_kernel<2>", "depth_sort:pass2"), ("dsort_pass_kernel<3>", "depth_sort:pass3"),
@@ -73,7 +74,8 @@ def read_pmc(d, counter):
 SQ_COUNTERS = ("SQ_INSTS_VALU", "SQ_INSTS_VALU_TRANS_F32", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM",
                "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_ANY",
                "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_LDS_BANK_CONFLICT", "SQ_WAIT_INST_LDS", "GRBM_GUI_ACTIVE",
-               "SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_ADD_F32")
+               "SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_ADD_F32", "TCC_HIT_sum", "TCC_MISS_sum",
+               "TCC_EA0_RDREQ_sum", "TCP_TOTAL_CACHE_ACCESSES_sum", "TCP_TCC_READ_REQ_sum")
 
 
 def read_sq(dirs):
