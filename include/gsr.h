@@ -258,6 +258,12 @@ int gsr_blend_stats(int64_t *out, int n, int reset);
  * counts (out[12..23]).  reset != 0 zeroes them after the read.  Returns the count written. */
 int gsr_debug_trace(int64_t *out, int n, int reset);
 
+/* Measurement builds only (-DGSR_KSTAMP=1; GSR_ERR_UNSUPPORTED otherwise): the instrumented kernels'
+ * last 4 launches on the GPU's clock, out[24 * 9]: per kernel id (gsr_device.h KsId) its launch
+ * count, 4 starts and 4 ends (s_memrealtime ticks, 100 MHz).  tools/kstamp.py turns them into the
+ * frame's timeline with the idle gaps between kernels. */
+int gsr_kstamp_read(unsigned long long *out, int n);
+
 /* Version / diagnostics. */
 int gsr_abi_version(void);
 const char *gsr_last_error(void);

@@ -959,6 +959,7 @@ __global__ __launch_bounds__(256) void grad_range_kernel(
     const float *__restrict__ viewmatrix, const float *__restrict__ projmatrix, const float *__restrict__ campos_p,
     float tanx, float tany, float fx, float fy, BwdScratch sc, GaussianGrads out, int raw,
     const uint32_t *__restrict__ stamps, uint32_t stamp, StepAct act) {
+    GSR_KS(kKsGradRange);
     __shared__ uint16_t s_list[kLiveRange];
     __shared__ uint32_t s_off[kLiveRange / 64 + 1];
     __shared__ uint8_t s_byte[256];
@@ -986,6 +987,7 @@ __global__ __launch_bounds__(256) void grad_range_kernel(
 
 __global__ __launch_bounds__(256) void grad_live_list_kernel(LiveArgs a, const uint32_t *__restrict__ stamps,
                                                              uint32_t stamp, uint32_t *__restrict__ ctr) {
+    GSR_KS(kKsLiveList);
     __shared__ uint32_t s_off[kLiveRange / 64 + 1];
     __shared__ uint8_t s_byte[256];
     __shared__ uint32_t s_base;
@@ -1007,6 +1009,7 @@ __global__ __launch_bounds__(256) void grad_live_list_kernel(LiveArgs a, const u
 // ctr[0]: the list's length (grad_live_list_kernel), ctr[1]: finished workgroups; the last one
 // to finish zeroes both for the next backward of the frame (the preprocess zeroed them first).
 __global__ __launch_bounds__(256) void grad_live_kernel(LiveArgs a, uint32_t *__restrict__ ctr) {
+    GSR_KS(kKsGradLive);
     const uint32_t n = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const Mat4 V = load_mat4(a.viewmatrix);
     for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
@@ -1133,5 +1136,7 @@ void launch_preprocess_bwd(const GaussianInputs &in, const Camera &cam, const Ge
                        cam.view, cam.proj, cam.campos, cam.tanx, cam.tany, cam.fx, cam.fy, cam.gx, gs.tiles, gs.rec,
                        is.boundary, sc, out, in.raw);
 }
+
+GSR_KSTAMP_READER(kstamp_read_backward)
 
 }  // namespace gsr

@@ -119,6 +119,7 @@ __device__ __forceinline__ int visible_chunks(const SBGrid &sg, int P, const uin
 __global__ __launch_bounds__(1024) void sb_count_kernel(int P, SBGrid sg, const uint2 *__restrict__ drect, const uint32_t *__restrict__ drect4,
                                                        uint32_t *__restrict__ cnt_g, uint32_t *__restrict__ cnt_i,
                                                        const uint32_t *__restrict__ culled) {
+    GSR_KS(kKsSbCount);
     extern __shared__ uint32_t lds[];
     uint32_t *cg = lds, *ci = lds + sg.nsb;
     const int chunk = chunk_of_block(blockIdx.x);
@@ -208,6 +209,7 @@ __global__ __launch_bounds__(kColThreads) void sb_colscan_kernel(SBGrid sg, uint
                                                                  uint32_t *__restrict__ tb_items, uint32_t tb_len,
                                                                  uint32_t *__restrict__ host_sblist, int P,
                                                                  const uint32_t *__restrict__ culled) {
+    GSR_KS(kKsSbColscan);
     __shared__ uint32_t wsum[kColThreads / 64];
     __shared__ uint32_t s_last, s_tb;
     __shared__ uint32_t s_ci[GSR_FWD_SB_ORDER ? kMaxSB : 1];  // last workgroup: SB instance totals
@@ -374,6 +376,7 @@ __global__ __launch_bounds__(64 * kScatterWaves) void sb_scatter_kernel(int P, S
                                                                          const uint32_t *__restrict__ dkey,
                                                                          const uint32_t *__restrict__ kdev, uint32_t cap,
                                                                          const uint32_t *__restrict__ culled) {
+    GSR_KS(kKsSbScatter);
     // the point-list capacity is short: the host re-runs at K (SB instances <= K, so K <= cap
     // bounds the level-1 lists too; the same test as every other binning / render kernel)
     if (*kdev > cap) return;
@@ -649,6 +652,7 @@ __global__ __launch_bounds__(64 * kTBWaves) void tile_bin_kernel(SBGrid sg, int 
                                                                  uint2 *__restrict__ ranges,
                                                                  const uint32_t *__restrict__ kdev, uint32_t cap,
                                                                  const uint32_t *__restrict__ tb_flag) {
+    GSR_KS(kKsTileBin);
     if (*kdev > cap) return;  // the point-list capacity is short: the host re-runs at K
     const int s = blockIdx.x;
     if (tb_flag && tb_flag[s]) return;  // a long list: binned in slices (tb_split_kernel)
@@ -1095,5 +1099,7 @@ void launch_binning_tiles(int P, const Camera &cam, const GeomState &gs, const B
         hipLaunchKernelGGL(tile_bin_kernel<GSR_TB_WAVES>, dim3(sg.nsb), dim3(64 * GSR_TB_WAVES), 0, s, sg, cam.gx, cam.gy, gs.sb_base_g,
                        gs.sb_base_i, bs.sblist, bs.point_list, is.ranges, bs.kdev, bs.cap, flag);
 }
+
+GSR_KSTAMP_READER(kstamp_read_binning)
 
 }  // namespace gsr

@@ -158,6 +158,7 @@ __global__ __launch_bounds__(kDsThreads) void dsort_upsweep_kernel(int P, int nb
                                                                     const uint32_t *__restrict__ tiles,
                                                                     uint32_t *__restrict__ ctl,
                                                                     uint32_t *__restrict__ host_K) {
+    GSR_KS(kKsUpsweep);
     // the top digit (sign + exponent + 1 mantissa bit) takes a handful of values: its counters are
     // replicated 16x (lane & 15 picks the copy) so a wave's LDS adds collide at most 4 ways
     constexpr int kTopCopies = 16;
@@ -258,6 +259,7 @@ __global__ __launch_bounds__(kDsThreads) void dsort_pass_kernel(int P, int nb, c
                                                                  const uint32_t *__restrict__ rin,
                                                                  uint32_t *__restrict__ rout,
                                                                  uint32_t *__restrict__ host_err) {
+    GSR_KS(kKsPass0 + kPass);
     constexpr bool kFirst = kPass == 0, kLast = kPass == kPasses - 1;
     // rect carry (GSR_DSORT_CARRY): pass 0 reads rect4 itself, the others rin; pass 3 stores into
     // drect's 4-B form, the others into rout
@@ -518,5 +520,7 @@ uint32_t *dsort_longest_words(const GeomState &gs) { return gs.ctrl + kCtlLonges
 uint32_t *dsort_culled_word(const GeomState &gs) { return gs.ctrl + kCtlCulled; }
 uint32_t *dsort_live_words(const GeomState &gs) { return gs.ctrl + kCtlLive; }
 int dsort_head_words() { return kCtlHead; }
+
+GSR_KSTAMP_READER(kstamp_read_dsort)
 
 }  // namespace gsr

@@ -762,4 +762,72 @@ struct BwdScratch {
     int atomic;
 };
 
+
+// ---- kernel stamps (measurement builds only: -DGSR_KSTAMP=1, tools/kstamp.py) ----------------------
+// The frame's kernels on the GPU's own clock, without a profiler in the way (rocprofv3's kernel
+// trace adds ~10 us between some kernels): each instrumented kernel's block 0 stores its start
+// (s_memrealtime, 100 MHz) into a 4-entry ring, every wave's lane 0 stores its end into a slot of its
+// own (plain stores; the reader takes the max -- atomics on shared lines serialised at the L2 and
+// doubled the step).  Kernels of more than 16384 waves alias slots.
+// The arrays are per translation unit (no relocatable device code); each TU exports a reader.
+#ifndef GSR_KSTAMP
+#define GSR_KSTAMP 0
+#endif
+constexpr int kKsIds = 24, kKsRing = 4, kKsSlots = 16384;
+enum KsId {
+    kKsPreprocess, kKsColor, kKsUpsweep, kKsPass0, kKsPass1, kKsPass2, kKsPass3, kKsSbCount, kKsSbColscan,
+    kKsSbScatter, kKsTileBin, kKsTileOrder, kKsRenderFwd, kKsRenderBwd, kKsGradRange, kKsFwdSeg, kKsLiveList,
+    kKsGradLive
+};
+#if GSR_KSTAMP
+static __device__ unsigned long long g_ks_start[kKsIds][kKsRing];
+static __device__ unsigned long long g_ks_end[kKsIds][kKsRing][kKsSlots];
+static __device__ unsigned int g_ks_cnt[kKsIds];
+struct KStampScope {
+    int id;
+    __device__ __forceinline__ explicit KStampScope(int i) : id(i) {
+        if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0) {
+            const unsigned c = __hip_atomic_load(&g_ks_cnt[id], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            g_ks_start[id][c % kKsRing] = wall_clock64();
+            __hip_atomic_store(&g_ks_cnt[id], c + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __device__ __forceinline__ ~KStampScope() {
+        if ((threadIdx.x & 63) == 0) {
+            const unsigned c = __hip_atomic_load(&g_ks_cnt[id], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - 1u;  // relaxed: an acquire invalidates the CU's L1 per wave
+            const unsigned w = ((blockIdx.x + blockIdx.y * gridDim.x) * ((blockDim.x + 63) / 64) + threadIdx.x / 64);
+            __hip_atomic_store(&g_ks_end[id][c % kKsRing][w % kKsSlots], wall_clock64(), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+};
+#define GSR_KS(id) const gsr::KStampScope gsr_ks_scope_((int)(id))
+// out[id * (1 + 2 kKsRing)]: the kernel's launch count, then the ring's starts, then its ends
+#define GSR_KSTAMP_READER(name)                                                                         \
+    int name(unsigned long long *out) {                                                                 \
+        static unsigned long long st[kKsIds][kKsRing], en[kKsIds][kKsRing][kKsSlots];                   \
+        static unsigned int cnt[kKsIds];                                                                \
+        if (hipDeviceSynchronize() != hipSuccess ||                                                     \
+            hipMemcpyFromSymbol(st, HIP_SYMBOL(g_ks_start), sizeof(st)) != hipSuccess ||               \
+            hipMemcpyFromSymbol(en, HIP_SYMBOL(g_ks_end), sizeof(en)) != hipSuccess ||                 \
+            hipMemcpyFromSymbol(cnt, HIP_SYMBOL(g_ks_cnt), sizeof(cnt)) != hipSuccess)                 \
+            return -1;                                                                                  \
+        for (int i = 0; i < kKsIds; i++) {                                                              \
+            unsigned long long *o = out + (size_t)i * (1 + 2 * kKsRing);                                \
+            o[0] = cnt[i];                                                                              \
+            for (int r = 0; r < kKsRing; r++) {                                                         \
+                o[1 + r] = st[i][r];                                                                    \
+                unsigned long long m = 0;                                                               \
+                for (int k = 0; k < kKsSlots; k++) m = en[i][r][k] > m ? en[i][r][k] : m;               \
+                o[1 + kKsRing + r] = m;                                                                 \
+            }                                                                                           \
+        }                                                                                               \
+        return 0;                                                                                       \
+    }
+#else
+#define GSR_KS(id) ((void)0)
+#define GSR_KSTAMP_READER(name) \
+    int name(unsigned long long *) { return -1; }
+#endif
+
 }  // namespace gsr

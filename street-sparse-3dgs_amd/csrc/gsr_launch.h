@@ -247,4 +247,11 @@ int step_activate_backward(int64_t P, const float *rotation_raw, const float *sc
                            bool sparse_rows = false, const float *scaling_raw = nullptr,
                            const float *opacity_raw = nullptr);
 
+// kernel stamps of each translation unit (GSR_KSTAMP builds; gsr_kstamp_read)
+int kstamp_read_preprocess(unsigned long long *out);
+int kstamp_read_dsort(unsigned long long *out);
+int kstamp_read_binning(unsigned long long *out);
+int kstamp_read_render(unsigned long long *out);
+int kstamp_read_backward(unsigned long long *out);
+
 }  // namespace gsr

@@ -27,6 +27,7 @@ __global__ __launch_bounds__(256) void preprocess_kernel(
     const float *__restrict__ viewmatrix, const float *__restrict__ projmatrix, const float *__restrict__ campos,
     int W, int H, float tanx, float tany, float fx, float fy, int gx, int gy, GeomState gs, int *__restrict__ radii,
     int raw, CutRef cut) {
+    GSR_KS(kKsPreprocess);
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     // the depth sort's control words (tickets, histograms, lookback status) start at zero
     for (uint32_t c = (uint32_t)i; c < gs.ctrl_zero; c += gridDim.x * blockDim.x) gs.ctrl[c] = 0u;
@@ -319,6 +320,7 @@ __global__ __launch_bounds__(kWaves * kWave) void preprocess_color_kernel(int P,
                                                                           const float *__restrict__ viewmatrix,
                                                                           const int *__restrict__ radii, GeomState gs,
                                                                           int nvb, CutRef cut) {
+    GSR_KS(kKsColor);
     __shared__ float4 s_sh[kWaves * kWave * kShPitch];
     __shared__ int4 s_idx[kCut ? kWaves * kWave : 1];
     if (GSR_COLOR_PF) {
@@ -407,5 +409,7 @@ void launch_mark_visible(int P, const float *means3D, const float *view, uint8_t
     if (P == 0) return;
     hipLaunchKernelGGL(mark_visible_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, means3D, view, present);
 }
+
+GSR_KSTAMP_READER(kstamp_read_preprocess)
 
 }  // namespace gsr

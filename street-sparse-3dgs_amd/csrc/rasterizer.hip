@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <thread>
 #include <unordered_map>
+#include <vector>
 
 #include "../../include/gsr.h"
 #include "../../include/gsr_hier.h"
@@ -1260,6 +1261,26 @@ int gsr_frame_stats(const void *geom_buffer, int P, int width, int height, int64
     int k = 0;
     for (; k < n && k < 4; k++) out[k] = (int64_t)v[k];
     return k;
+}
+
+// Kernel stamps (GSR_KSTAMP measurement builds, tools/kstamp.py): out[kKsIds * (1 + 2 * kKsRing)], per
+// kernel id its launch count, then its last 64 launches' starts and ends (s_memrealtime ticks,
+// 100 MHz).  GSR_ERR_UNSUPPORTED in a normal build.
+int gsr_kstamp_read(unsigned long long *out, int n) {
+    constexpr int per = 1 + 2 * kKsRing;
+    if (!out || n < kKsIds * per) return fail(GSR_ERR_INVALID_ARGUMENT, "kstamp buffer too small");
+    if (!GSR_KSTAMP) return fail(GSR_ERR_UNSUPPORTED, "not a GSR_KSTAMP build");
+    static std::vector<unsigned long long> tmp((size_t)kKsIds * per);
+    for (int i = 0; i < kKsIds * per; i++) out[i] = 0;
+    int (*readers[])(unsigned long long *) = {kstamp_read_preprocess, kstamp_read_dsort, kstamp_read_binning,
+                                              kstamp_read_render, kstamp_read_backward};
+    for (auto rd : readers) {
+        if (rd(tmp.data()) != 0) return fail(GSR_ERR_DEVICE, "kstamp read failed");
+        for (int i = 0; i < kKsIds; i++)
+            if (tmp[(size_t)i * per] > out[(size_t)i * per])
+                for (int k = 0; k < per; k++) out[(size_t)i * per + k] = tmp[(size_t)i * per + k];
+    }
+    return GSR_OK;
 }
 
 int gsr_debug_trace(int64_t *out, int n, int reset) {

@@ -511,6 +511,7 @@ __global__ __launch_bounds__(kWave * kPixPerLane) void render_fwd_seg_kernel(
     uint32_t *__restrict__ tile_work, const uint32_t *__restrict__ kdev, uint32_t cap,
     const uint32_t *__restrict__ sort_err, uint32_t *__restrict__ bwd_cnt, uint32_t *__restrict__ bwd_cls, int ntiles,
     uint32_t seg_len, uint32_t *bin_base, uint32_t fseg_len, uint32_t *fctl, const uint32_t *ready, FwdSpin spin) {
+    GSR_KS(kKsFwdSeg);
     if (kdev && *kdev > cap) return;  // the point-list capacity is short: the host re-runs at K
     __shared__ float4 s_a[kPixPerLane][kWave];
     __shared__ float4 s_b[kPixPerLane][kWave];
@@ -550,6 +551,7 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) GSR_FWD_ATTR void ren
     uint32_t *__restrict__ bwd_cnt, uint32_t *__restrict__ bwd_cls, int ntiles, int gy, int sb_nsbx, int sb_shift,
     uint32_t seg_len, uint32_t *__restrict__ bin_base, uint32_t fseg_len, uint32_t *__restrict__ fctl, uint32_t fseg_min,
     const uint32_t *__restrict__ longest, uint32_t *host_words, FwdSpin spin) {
+    GSR_KS(kKsRenderFwd);
     constexpr int kWaves = kPixPerLane / kSub;
     if (kdev && *kdev > cap) return;  // the point-list capacity is short: the host re-runs at K
     if (host_words && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -871,6 +873,7 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t *__rest
                                                           void *bin_base, uint32_t seg_len, uint32_t fseg_len,
                                                           uint32_t fseg_min, uint32_t *__restrict__ host_tilelist,
                                                           uint32_t *fwd_ready) {
+    GSR_KS(kKsTileOrder);
     // the forward order's launch also zeroes the backward class counters render_fwd fills
     if (zero_classes && threadIdx.x < kBwdClasses) zero_classes[threadIdx.x] = 0u;
     if (zero_classes && threadIdx.x == 0) zero_classes[kBwdSegCount] = 0u;
@@ -1119,6 +1122,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVE
     const uint32_t *__restrict__ tile_order, const uint32_t *__restrict__ goff, uint64_t *__restrict__ boundary,
     float4 *__restrict__ out, ZeroRows zr, const uint32_t *__restrict__ bwd_cnt, const uint32_t *__restrict__ bwd_cls,
     uint32_t ntiles, uint32_t seg_len, const float *__restrict__ ck, const uint32_t *__restrict__ seg_items) {
+    GSR_KS(kKsRenderBwd);
     // 9 KiB of LDS per wave: each compacted instance's mean and conic (scaled for gauss_p2 by the
     // lane that stages it, once per instance instead of by the whole wave), opacity, list position
     // << 4 | sub-block mask, Gaussian id (atomic mode) or record index, colour, and the unscaled
@@ -1543,6 +1547,8 @@ void launch_render_bwd(const Camera &cam, const GeomState &gs, const BinningStat
     }
 #undef GSR_BWD_LAUNCH
 }
+
+GSR_KSTAMP_READER(kstamp_read_render)
 
 }  // namespace gsr
 

@@ -77,6 +77,7 @@ SIGNATURES = {
     "gsr_blend_stats": (_i, [ctypes.POINTER(_i64), _i, _i]),
     "gsr_fwd_pool_stats": (_i, [ctypes.POINTER(_i64), _i, _i]),
     "gsr_debug_trace": (_i, [ctypes.POINTER(_i64), _i, _i]),
+    "gsr_kstamp_read": (_i, [ctypes.POINTER(ctypes.c_uint64), _i]),
     "gsr_set_true_scale_gradient": (_i, [_i]),
     "gsr_set_deterministic": (_i, [_i]),
     "gsr_set_binning": (_i, [_i]),

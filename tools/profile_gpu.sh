@@ -23,4 +23,7 @@ if [ -n "${PROFILE_CACHE:-}" ]; then  # L2 hit / miss and request counts (one mo
 fi
 cd "$ROOT"
 python3 tools/pmc_summary.py --trace "$OUT/trace" --fetch "$OUT/fetch" --write "$OUT/write" --sq "$OUT/sq1" --sq "$OUT/sq2" --sq "$OUT/sq3" $SQ4 --out "$OUT/summary.json" --note "$TAG: bench.py $ARGS" > /dev/null
+# keep the summary and the kernel stats; the raw traces and counter CSVs can exceed what gpurun copies back
+cp "$(find "$OUT/trace" -name '*kernel_stats.csv' | head -1)" "$OUT/kernel_stats.csv" 2>/dev/null || true
+if [ -z "${PROFILE_KEEP_RAW:-}" ]; then rm -rf "$OUT/trace" "$OUT/fetch" "$OUT/write" "$OUT/sq1" "$OUT/sq2" "$OUT/sq3" "$OUT/sq4"; fi
 echo "profile $TAG done"
