@@ -227,6 +227,7 @@ def train_step_ms(P, W, H, steps, warmup, dev, street=True, reference=False, see
         from train_torch_ref import ReferenceTrainStep as step_cls
     ts = make_problem(P, W, H, n_views=4 if street else 1, seed=seed, step_cls=step_cls, depth=street,
                       skybox_points=10_000 if street else 0, fovx_deg=fovx_deg, depth_only=4 if depth_only else 0)
+    settle()
     for _ in range(warmup):
         ts.step()
     torch.cuda.synchronize()
@@ -270,6 +271,7 @@ def config3(a, dev, seed=0, ranks=None, spatial=False):
     from gs_train.chunk import view_psnr
     psnr0 = view_psnr(ts)
     tc = TrainChunk(ts, sched, spatial=bool(spatial))
+    settle()
     evs, losses = [], {}
     # per iteration, for the attribution of the slowest ones: binning re-runs (capacity short), the
     # executor's buffer growths, the torch caching allocator's reserved bytes
@@ -389,6 +391,7 @@ def train_post_ms(a, dev):
     W = H = a.chunk_size
     torch.manual_seed(0)
     post = synthetic_post_problem(a.post_leaves, W, H, n_views=4, skybox=10_000, n_anchors=10_000, seed=1, device=dev)
+    settle()
     for _ in range(5):
         post.step()
     torch.cuda.synchronize()
@@ -705,18 +708,25 @@ def fwd_bwd_step(raster, inp, gcol, ginv):
 
 @contextlib.contextmanager
 def quiet_gc():
-    """Python's cyclic collector settled before a timed region: one full collection, then every
-    surviving object frozen (gc.freeze), so a generation-2 pass over the interpreter's ~10^5
-    long-lived objects (torch's modules, the synthetic scene's builders) cannot land inside the
-    timed steps -- a few-ms host stall that showed up as a 10% low sample now and then.  Collection
-    stays enabled; the objects the steps themselves create are collected as usual."""
+    """Python's cyclic collector kept out of a timed region: every object alive is frozen (gc.freeze),
+    so a generation-2 pass over the interpreter's ~10^5 long-lived objects (torch's modules, the
+    synthetic scene's builders) cannot land inside the timed steps -- a few-ms host stall that showed
+    up as a 10% low sample now and then.  No gc.collect() here: a collection right before the timed
+    steps made the next ~20 steps 7% slower on the GPU (0.66 -> 0.71 ms per step, tools/timing_ab.py
+    r06i: the buffers it frees change where the steps' allocations land); settle() collects once,
+    before the pre-warm.  Collection stays enabled; the objects the steps create are collected as usual."""
     import gc
-    gc.collect()
     gc.freeze()
     try:
         yield
     finally:
         gc.unfreeze()
+
+
+def settle():
+    """One full collection after the set-up, before any warm-up (see quiet_gc)."""
+    import gc
+    gc.collect()
 
 
 def timed(step, steps, warmup, ranks, per_step=None, host=None):
@@ -791,6 +801,9 @@ class ClockProbe:
     def __init__(self, dev):
         self.h = None
         self.err = None
+        if os.environ.get("GSR_BENCH_NO_SMI") == "1":  # A/B: the bench without amdsmi in the process
+            self.err = "disabled (GSR_BENCH_NO_SMI=1)"
+            return
         try:
             import amdsmi
             import torch
@@ -1105,6 +1118,7 @@ def main():
         pr.disable()
         pstats.Stats(pr, stream=sys.stderr).sort_stats("cumulative").print_stats(18)
     log("metric: timing")
+    settle()
     probe = ClockProbe(dev)
     per_step = []
     host_side = {}
