@@ -850,16 +850,11 @@ __device__ __forceinline__ int bwd_tile_of(uint32_t b, const uint32_t *__restric
 }
 
 // the shortest list the forward split takes: gsr_set_fwd_split_min's length, else GSR_FSEG_FACTOR
-// segments (or the environment's GSR_FSEG_FACTOR: measurement A/B)
+// segments (measurement A/B: gsr_set_fwd_split_min, or a -DGSR_FSEG_FACTOR build)
 std::atomic<uint32_t> g_fseg_min{0};
 uint32_t fseg_min_len(uint32_t Lf) {
-    static const uint32_t f = [] {
-        const char *e = getenv("GSR_FSEG_FACTOR");
-        const int v = e ? atoi(e) : 0;
-        return (uint32_t)(v > 0 ? v : GSR_FSEG_FACTOR);
-    }();
     const uint32_t m = g_fseg_min.load(std::memory_order_relaxed);
-    return m ? std::max(m, Lf) : f * Lf;
+    return m ? std::max(m, Lf) : (uint32_t)GSR_FSEG_FACTOR * Lf;
 }
 uint32_t set_fwd_split_min(uint32_t len) { return g_fseg_min.exchange(len); }
 

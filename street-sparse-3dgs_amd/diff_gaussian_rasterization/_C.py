@@ -108,16 +108,17 @@ def set_bwd_segment(length: int) -> int:
 
 def set_fwd_segment(length: int) -> int:
     """Forward work split (gsr_set_fwd_segment): 0 = one workgroup per tile, L = a multiple of 64
-    >= 4096 (default 4096, behind the split gate) = tiles with lists longer than 4 L blended as
-    segments of L positions by a worker pool.  Process-wide; returns the previous length."""
+    >= 1024 (default 2048, behind the split gate) = tiles with lists longer than the split minimum
+    (6 L by default, gsr_set_fwd_split_min) blended as segments of L positions by a worker pool.
+    Process-wide; returns the previous length."""
     r = _L.gsr_set_fwd_segment(int(length))
     _check(0 if r >= 0 else r, "set_fwd_segment")
     return r
 
 
 def set_fwd_split_min(length: int) -> int:
-    """gsr_set_fwd_split_min: the shortest tile list the forward split takes (0 = 4 segments, the
-    default).  Process-wide; returns the previous setting."""
+    """gsr_set_fwd_split_min: the shortest tile list the forward split takes (0 = 6 segments of the
+    forward segment length, the default).  Process-wide; returns the previous setting."""
     r = _L.gsr_set_fwd_split_min(int(length))
     _check(0 if r >= 0 else r, "set_fwd_split_min")
     return r
