@@ -194,6 +194,15 @@ constexpr int kColorWaves = GSR_COLOR_WAVES;  // waves per block (13 KiB of LDS 
 #endif
 constexpr int kColorThreads = kColorWaves * kWave;
 
+// GSR_COLOR_CHUNKED: the rows pass through LDS in three 16-float chunks instead of whole (5 instead of
+// 13 float4 of LDS per row), so a block holds 40 instead of 104 KiB and the VGPRs, not the LDS,
+// bound the waves per CU; each load instruction reads 64 B of each of 16 rows.
+#ifndef GSR_COLOR_CHUNKED
+#define GSR_COLOR_CHUNKED 0
+#endif
+constexpr int kChPitch = 5;  // chunked LDS row pitch, in float4 (20 dwords: ds_read_b128 of 16 lanes conflict-free)
+constexpr int kColorPitch = GSR_COLOR_CHUNKED ? kChPitch : kShPitch;
+
 // GSR_COLOR_PF: each wave issues the next row block's SH loads before it evaluates the current
 // one (the persistent grid walks row blocks; with one 8-wave block per CU the VGPR budget, not
 // occupancy, pays for the second 48-VGPR buffer), so a CU keeps twice the bytes in flight
@@ -234,7 +243,11 @@ __device__ __forceinline__ void color_fetch(int vb, ShRows &r, int P, int D, con
     }
 #pragma unroll
     for (int k = 0; k < kShRow; k++) {
-        const int f = k * kWave + lane, row = f / kShRow, col = f - row * kShRow;
+        // whole rows: float4 k*64 + l of the wave's rows; chunked: chunk k / 4 (float4 4(k/4) .. +3 of
+        // every row), 16 rows per instruction
+        const int f = GSR_COLOR_CHUNKED ? (k & 3) * kWave + lane : k * kWave + lane;
+        const int row = GSR_COLOR_CHUNKED ? f >> 2 : f / kShRow;
+        const int col = GSR_COLOR_CHUNKED ? 4 * (k >> 2) + (f & 3) : f - row * kShRow;
         r.v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (kCut) {
             if (((need >> row) & 1ull) && col < cols) {
@@ -247,12 +260,13 @@ __device__ __forceinline__ void color_fetch(int vb, ShRows &r, int P, int D, con
             continue;
         }
         if (((need >> row) & 1ull) && col < cols) {
+            const int e = row * kShRow + col;  // == f for whole rows
             if (GSR_SH_NT) {
                 typedef float f4 __attribute__((ext_vector_type(4)));
-                const f4 t = __builtin_nontemporal_load(reinterpret_cast<const f4 *>(src4 + f));
+                const f4 t = __builtin_nontemporal_load(reinterpret_cast<const f4 *>(src4 + e));
                 r.v[k] = make_float4(t.x, t.y, t.z, t.w);
             } else {
-                r.v[k] = src4[f];
+                r.v[k] = src4[e];
             }
         }
     }
@@ -266,20 +280,40 @@ __device__ __forceinline__ void color_finish(int vb, const ShRows &r, float4 *s_
     const int i = vb * blockDim.x + threadIdx.x;
     const int nc = (D + 1) * (D + 1);
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    float4 *S = s_sh + wv * kWave * kShPitch;
-    __builtin_amdgcn_wave_barrier();  // the wave's previous reads of its tile are done
-#pragma unroll
-    for (int k = 0; k < kShRow; k++) {
-        const int f = k * kWave + lane, row = f / kShRow, col = f - row * kShRow;
-        S[row * kShPitch + col] = r.v[k];
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS writes landed
-    __builtin_amdgcn_wave_barrier();
+    float4 *S = s_sh + wv * kWave * kColorPitch;
     float sh[48];
+    if (GSR_COLOR_CHUNKED) {
 #pragma unroll
-    for (int c = 0; c < kShRow; c++) {
-        const float4 w = S[lane * kShPitch + c];
-        sh[4 * c] = w.x; sh[4 * c + 1] = w.y; sh[4 * c + 2] = w.z; sh[4 * c + 3] = w.w;
+        for (int q = 0; q < 3; q++) {
+            __builtin_amdgcn_wave_barrier();  // the wave's previous reads of its tile are done
+#pragma unroll
+            for (int kk = 0; kk < 4; kk++) {
+                const int f = kk * kWave + lane;
+                S[(f >> 2) * kChPitch + (f & 3)] = r.v[4 * q + kk];
+            }
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS writes landed
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const float4 w = S[lane * kChPitch + c];
+                sh[16 * q + 4 * c] = w.x; sh[16 * q + 4 * c + 1] = w.y;
+                sh[16 * q + 4 * c + 2] = w.z; sh[16 * q + 4 * c + 3] = w.w;
+            }
+        }
+    } else {
+        __builtin_amdgcn_wave_barrier();  // the wave's previous reads of its tile are done
+#pragma unroll
+        for (int k = 0; k < kShRow; k++) {
+            const int f = k * kWave + lane, row = f / kShRow, col = f - row * kShRow;
+            S[row * kShPitch + col] = r.v[k];
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS writes landed
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int c = 0; c < kShRow; c++) {
+            const float4 w = S[lane * kShPitch + c];
+            sh[4 * c] = w.x; sh[4 * c + 1] = w.y; sh[4 * c + 2] = w.z; sh[4 * c + 3] = w.w;
+        }
     }
     if (i >= P) return;
     if (!r.vis) {
@@ -321,7 +355,7 @@ __global__ __launch_bounds__(kWaves * kWave) void preprocess_color_kernel(int P,
                                                                           const int *__restrict__ radii, GeomState gs,
                                                                           int nvb, CutRef cut) {
     GSR_KS(kKsColor);
-    __shared__ float4 s_sh[kWaves * kWave * kShPitch];
+    __shared__ float4 s_sh[kWaves * kWave * kColorPitch];
     __shared__ int4 s_idx[kCut ? kWaves * kWave : 1];
     if (GSR_COLOR_PF) {
         ShRows cur, nxt;
