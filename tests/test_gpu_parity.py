@@ -54,6 +54,14 @@ CASES = [
     dict(name="huge_splats_sb", P=300, W=640, H=480, deg=1, seed=15, log_scale=-0.5),
     # more than 255 tiles across: the 8-B tile rects (every other case packs them into 4 B)
     dict(name="wide_frame_rect8", P=3000, W=4200, H=64, deg=1, seed=17, log_scale=-3.0),
+    # frame shapes at the grid's edges: one pixel, one partial tile, one-tile-wide column and
+    # two-pixel-high row (superblock grids of 1 x n), a single Gaussian, and a 2 x 2 tile frame
+    dict(name="single_pixel", P=60, W=1, H=1, deg=1, seed=18, log_scale=-2.0),
+    dict(name="one_tile_15x17", P=200, W=15, H=17, deg=2, seed=19, log_scale=-2.5),
+    dict(name="thin_column_3x300", P=400, W=3, H=300, deg=0, seed=20, log_scale=-2.5),
+    dict(name="thin_row_500x2", P=400, W=500, H=2, deg=3, seed=21, log_scale=-2.5),
+    dict(name="single_gaussian", P=1, W=48, H=40, deg=3, seed=22, log_scale=-1.0),
+    dict(name="tile_edges_32x32", P=3000, W=32, H=32, deg=1, seed=23, log_scale=-3.2),
 ]
 
 
