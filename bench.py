@@ -729,7 +729,7 @@ def settle():
     gc.collect()
 
 
-def timed(step, steps, warmup, ranks, per_step=None, host=None):
+def timed(step, steps, warmup, ranks, per_step=None, host=None, per_call=None):
     """W untimed steps, then exactly `steps` steps bracketed by barrier + synchronize on both sides;
     the MAX over ranks of the elapsed seconds.  per_step (a list): receives each timed step's device
     duration in ms -- HIP events recorded on the current stream between consecutive steps (no
@@ -764,6 +764,8 @@ def timed(step, steps, warmup, ranks, per_step=None, host=None):
         el = time.perf_counter() - t0
     if ev is not None:
         per_step.extend(ev[i].elapsed_time(ev[i + 1]) for i in range(steps))
+    if per_call is not None:  # the timed steps' own host call times (ms)
+        per_call.extend(float(v) for v in np.diff(np.asarray(ht)) * 1e3)
     if host is not None:
         call = np.diff(np.asarray(ht)) * 1e3
         kw = (k1 - k0) / max(1, steps) * 1e-6
@@ -778,15 +780,18 @@ def timed(step, steps, warmup, ranks, per_step=None, host=None):
 
 
 def dispersion(ms):
-    """Median / p10 / p90 / min / max of per-step device times (ms): SURVEY.md 8(d) asks for the
-    median; the mean comes from the wall clock."""
+    """Median / p10 / p90 / min / max of the timed steps' per-step times (ms): SURVEY.md 8(d) asks for
+    the median; the mean comes from the wall clock.  The times are each step() call's host duration:
+    the step is GPU-bound (the forward waits for its frame's K, which the GPU produces one frame after
+    the previous), so in steady state the calls follow the GPU's frames; per-step HIP events would
+    put a marker packet (~7 us) between every two steps."""
     if not ms:
         return None
     a = np.asarray(ms, np.float64)
     return {"median_ms": round(float(np.median(a)), 5), "p10_ms": round(float(np.percentile(a, 10)), 5),
             "p90_ms": round(float(np.percentile(a, 90)), 5), "min_ms": round(float(a.min()), 5),
             "max_ms": round(float(a.max()), 5), "n": int(a.size),
-            "source": "HIP events between consecutive steps, over as many untimed steps right after the timed ones"}
+            "source": "perf_counter around each timed step() call (GPU-bound steps: the host waits for each frame's K)"}
 
 
 class ClockProbe:
@@ -1128,10 +1133,8 @@ def main():
     pw["gfxclk_at_timed_start"] = (clk_before or {}).get("current_gfxclk")
     # the timed region carries no per-step event records: each is a marker packet on the stream, and
     # a marker costs ~7 us of idle between the kernels around it (tools/kstamp.py, r06e)
-    elapsed = timed(step, a.steps, a.warmup, ranks, host=host_side)
+    elapsed = timed(step, a.steps, a.warmup, ranks, host=host_side, per_call=per_step)
     clk_after = probe.read()
-    # per-step device times (HIP events between consecutive steps) over as many more, untimed steps
-    timed(step, max(a.steps, 20), 0, Ranks(1, 0, False, dev), per_step=per_step)
 
     # the clock under the bench's load: sampled over ~400 more (untimed) steps
     def burst():
