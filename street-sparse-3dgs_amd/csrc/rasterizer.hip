@@ -63,6 +63,61 @@ thread_local gsr::StepAct g_step_act{};    // set_step_act
 std::atomic<int> g_live_list{0};           // gsr_set_live_list
 thread_local bool g_step_act_done = false;
 constexpr int kMaxDevicesK = 64;
+// The backward's per-Gaussian accumulator rows (64 B each: render_bwd's ten float-atomic sums),
+// GSR_PERSISTENT_ACC (default): one grow-only array per device, all zero between backwards --
+// render_bwd adds into the rows of the Gaussians it reaches and the consumer (preprocess_bwd or
+// the live-row pass) zeroes every row it reads (it always did, for a repeated backward), so the
+// forward no longer clears P rows per frame (1M x 64 B on the bench frame: 10 us of the step,
+// r06r).  A backward that fails between render_bwd and the consumer leaves the rows marked dirty
+// (cleared by the next backward); a backward on another stream than the previous one first waits
+// for that stream.  GSR_PERSISTENT_ACC=0: the rows in the frame's geometry buffer, cleared by
+// render_fwd (rounds 1-5).
+#ifndef GSR_PERSISTENT_ACC
+#define GSR_PERSISTENT_ACC 1
+#endif
+struct AccRows {
+    float4 *p = nullptr;
+    size_t rows = 0;
+    bool dirty = false;
+    hipStream_t last = nullptr;  // the stream of the last backward that used the rows
+};
+std::mutex g_acc_mu;
+AccRows g_acc_rows[kMaxDevicesK];
+// The device's rows for a backward of n rows on stream s (stream-ordered growth and clears); marked
+// dirty until acc_rows_consumed() -- the backward has queued the consumer.  NULL on failure.
+float4 *acc_rows(hipStream_t s, size_t n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevicesK) return nullptr;
+    std::lock_guard<std::mutex> lk(g_acc_mu);
+    AccRows &a = g_acc_rows[dev];
+    // another stream's backward may still be adding into / consuming the rows (a stream may since
+    // have been destroyed, so the whole device is waited for; backwards on one stream need nothing)
+    if (a.last && a.last != s && hipDeviceSynchronize() != hipSuccess) return nullptr;
+    const size_t row = 4 * sizeof(float4);
+    if (a.rows < n) {
+        const size_t want = std::max(n, a.rows + a.rows / 4);
+        float4 *p = nullptr;
+        if (hipMallocAsync(reinterpret_cast<void **>(&p), want * row, s) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        if (hipMemsetAsync(p, 0, want * row, s) != hipSuccess) return nullptr;
+        if (a.p) (void)hipFreeAsync(a.p, s);  // after the work queued before on this stream
+        a.p = p;
+        a.rows = want;
+    } else if (a.dirty && hipMemsetAsync(a.p, 0, a.rows * row, s) != hipSuccess) {
+        return nullptr;
+    }
+    a.dirty = true;
+    a.last = s;
+    return a.p;
+}
+void acc_rows_consumed() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevicesK) return;
+    std::lock_guard<std::mutex> lk(g_acc_mu);
+    g_acc_rows[dev].dirty = false;
+}
 thread_local hipEvent_t g_k_ready[kMaxDevicesK] = {};
 // per device: capacity for the next frame's point list, 0 = none yet.  It is the largest K of the
 // last kKHist (256) frames + 1/8 + 4096, so a training loop cycling its cameras (whose K differs from
@@ -310,8 +365,10 @@ GeomState carve_geom(void *base, int P, int gx, int gy, size_t *bytes) {
     g.sb_cnt_i = c.take<uint32_t>((size_t)g.sb.nsb * g.sb.ccols);
     g.sb_base_g = c.take<uint32_t>((size_t)g.sb.nsb + 1);
     g.sb_base_i = c.take<uint32_t>((size_t)g.sb.nsb + 1);
-    g.acc = c.take<float4>(4 * (size_t)P);
-    g.nacc = P;
+    // GSR_PERSISTENT_ACC: the backward's accumulator rows are the device's persistent rows
+    // (acc_rows below), not part of the frame's buffer
+    g.acc = GSR_PERSISTENT_ACC ? nullptr : c.take<float4>(4 * (size_t)P);
+    g.nacc = GSR_PERSISTENT_ACC ? 0 : P;
     g.live_stamp = c.take<uint32_t>(P);
     g.tb_flag = c.take<uint32_t>((size_t)g.sb.nsb + 1);
     g.tb_items = c.take<uint32_t>(kTBMaxItems);
@@ -1101,6 +1158,8 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
     if (!sbase) return fail(GSR_ERR_ALLOCATION, "backward scratch allocation failed");
     BwdScratch sc = carve_bwd(sbase, R_inst, P, atomic, nullptr, list);
     sc.acc = gs.acc;
+    if (GSR_PERSISTENT_ACC && atomic && P > 0 && !(sc.acc = acc_rows(s, (size_t)P)))
+        return fail(GSR_ERR_ALLOCATION, "backward accumulator rows allocation failed");
 
     // sparse rows only for plain frames (the cut's rows are scattered to the input rows below)
     GaussianGrads out{dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
@@ -1146,6 +1205,7 @@ int gsr_rasterize_backward(gsr_resize_fn scratch, void *resize_ctx, int P, int D
         StageTimer st(7, s);
         launch_preprocess_bwd(in, cam, gs, is, radii, sc, out, s, zeroed ? &zr : nullptr);
     }
+    if (GSR_PERSISTENT_ACC && atomic && P > 0) acc_rows_consumed();  // the consumer zeroes what it reads
     if ((rc = check("preprocess backward", debug, s))) return rc;
     if (R > 0) {
         const size_t n3 = sizeof(float) * 3 * (size_t)Nin;

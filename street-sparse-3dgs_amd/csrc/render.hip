@@ -107,6 +107,9 @@ __device__ __forceinline__ uint32_t lane_prefix(uint64_t mask) {
 #ifndef GSR_ACC_NT
 #define GSR_ACC_NT 1
 #endif
+#ifndef GSR_FWD_ACC_CLEAR
+#define GSR_FWD_ACC_CLEAR 1  // 0: measurement builds only (the backward's sums then start from garbage)
+#endif
 #ifndef GSR_FWD_SUB
 #define GSR_FWD_SUB 1  // 16x4 sub-blocks per wave (measured: 1 -> 0.139 ms, 2 -> 0.176, 4 -> 0.242)
 #endif
@@ -561,7 +564,7 @@ __global__ __launch_bounds__(kWave * (kPixPerLane / kSub)) GSR_FWD_ATTR void ren
         __hip_atomic_store(host_words + kHostTileList, longest[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(host_words + kHostSBList, longest[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    {
+    if (GSR_FWD_ACC_CLEAR) {
         // the backward's per-Gaussian accumulator rows (atomic mode) start at zero: every
         // workgroup clears one slice with streaming stores that drain while it blends (the
         // blend is VALU-bound; HBM is nearly idle here)
