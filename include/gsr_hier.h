@@ -88,10 +88,10 @@ int gsr_zero_grad_rows(int n, float *const *grads, const int64_t *widths, int64_
  * node's first Gaussian, -1 for roots) and nodes_for_render_indices (node ids), in node order --
  * and returns its length in *to_render (the value the Python function returns; one host read, as
  * upstream).  viewpoint is a DEVICE float[3] (the caller's camera_center on the GPU).
- * `capacity` = the entries each output array holds: the write pass never stores past it, and a
- * cut longer than it (possible when nodes hold several Gaussians: the cut can reach the sum of
- * count_leafs + count_merged, more than N) fails with GSR_ERR_INVALID_ARGUMENT, *to_render set to
- * the length it needs.  scratch: a device buffer of gsr_expand_to_size_scratch_bytes(N) bytes. */
+ * `capacity` = the entries each output array holds: nothing is stored past it, and a cut longer
+ * than it (possible when nodes hold several Gaussians: the cut can reach the sum of count_leafs +
+ * count_merged, more than N) fails with GSR_ERR_INVALID_ARGUMENT, *to_render set to the length it
+ * needs (the entries that fit may have been written: one pass counts and writes).  scratch: a device buffer of gsr_expand_to_size_scratch_bytes(N) bytes. */
 size_t gsr_expand_to_size_scratch_bytes(int64_t N);
 int gsr_expand_to_size(int64_t N, const int *nodes, const float *boxes, float target_size, const float *viewpoint,
                        int *render_indices, int *parent_indices, int *nodes_for_render_indices, int64_t capacity,

@@ -50,6 +50,32 @@ def test_lod_cut_matches_oracle(tau, vp):
     assert int(ri[n:].abs().sum()) == 0 and float(w[n:].abs().sum()) == 0.0
 
 
+@pytest.mark.parametrize("leaves,offset", [(600, 0), (5000, 1), (70_000, 3)])
+def test_lod_cut_ragged_tiles_and_unaligned_nodes(leaves, offset):
+    """The one-pass cut (lod.hip lod_cut_kernel: 1024-node tiles, nodes staged through LDS, a decoupled
+    lookback for the offsets) on one ragged tile, on several, and with the nodes array starting
+    `offset` rows into its buffer (28-B rows: not 16-B aligned, the staging's dword path) --
+    bit-exact with the oracle."""
+    import gs_oracle as O
+    from gs_train.synthetic import synthetic_lod_hierarchy, tau_threshold
+    h = synthetic_lod_hierarchy(leaves, 640, 360, DEV, seed=13, zmin=1.0, zmax=20.0, log_scale_mean=-3.0)
+    N = h["nodes"].shape[0]
+    if offset:
+        buf = torch.zeros(N + offset, 7, dtype=torch.int32, device=DEV)
+        buf[offset:] = h["nodes"]
+        h = dict(h, nodes=buf[offset:])
+        assert h["nodes"].data_ptr() % 16 != 0
+    thr = float(np.float32(tau_threshold(10.0, h["tanfovx"], 640)))
+    n, ri, pi, ni, w, k = _cut_hip(h, thr)
+    nodes, boxes = h["nodes"].cpu().numpy(), h["boxes"].cpu().numpy()
+    ori, opi, oni = O.expand_to_size(nodes, boxes, np.float32(thr), np.asarray(h["campos"], np.float32))
+    assert n == len(ori) and 0 < n < N
+    np.testing.assert_array_equal(ri[:n].cpu().numpy(), ori)
+    np.testing.assert_array_equal(pi[:n].cpu().numpy(), opi)
+    np.testing.assert_array_equal(ni[:n].cpu().numpy(), oni)
+    assert int(ri[n:].abs().sum()) == 0
+
+
 def _covered_once(h, ri, n):
     """Every leaf of the tree is rendered exactly once: by itself or through exactly one ancestor
     in the cut (each node holds one Gaussian, Gaussian i = node i).  Level by level on the device:
@@ -254,8 +280,8 @@ def test_fused_cut_frame_equals_render_post_blend(skybox):
 
 def test_expand_to_size_capacity_with_multi_gaussian_nodes():
     """A node can hold several Gaussians (count_leafs + count_merged > 1), so the cut can be longer
-    than the node count N: output arrays of N entries are refused (nothing written past them), and
-    arrays of the needed length get the full cut."""
+    than the node count N: output arrays of N entries are refused (the call fails; nothing is written
+    past them), and arrays of the needed length get the full cut."""
     from gaussian_hierarchy._C import expand_to_size
     # root (1 merged Gaussian) with three leaf nodes of 3 Gaussians each; every box contains the
     # viewpoint, so every node is "too big" and renders its leaf Gaussians: 9 entries from 4 nodes
@@ -264,10 +290,12 @@ def test_expand_to_size_capacity_with_multi_gaussian_nodes():
     boxes = torch.zeros(4, 2, 4, device=DEV)
     boxes[:, 0, :3], boxes[:, 0, 3], boxes[:, 1, :3] = -10.0, 20.0, 10.0
     cam = torch.zeros(3, device=DEV)
-    small = [torch.full((4,), -7, dtype=torch.int32, device=DEV) for _ in range(3)]
+    # 4-entry views of 12-entry buffers: the one pass writes the entries that fit, never past them
+    room = [torch.full((12,), -7, dtype=torch.int32, device=DEV) for _ in range(3)]
+    small = [t[:4] for t in room]
     with pytest.raises(RuntimeError, match="needs 9 entries"):
         expand_to_size(nodes, boxes, 0.01, cam, torch.zeros(3), *small)
-    assert all(bool(torch.all(t == -7)) for t in small)
+    assert all(bool(torch.all(t[4:] == -7)) for t in room)
     big = [torch.full((12,), -7, dtype=torch.int32, device=DEV) for _ in range(3)]
     n = expand_to_size(nodes, boxes, 0.01, cam, torch.zeros(3), *big)
     assert n == 9

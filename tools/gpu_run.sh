@@ -12,12 +12,14 @@
 #                    (its long diagnostics via GSR_BENCH_DETAIL_OUT)  -> driver.json, driver_detail.json
 #   profile          tools/profile_gpu.sh <tag> (rocprofv3 stats + PMC) -> gpurun_out/prof_<tag>/summary.json
 #   c3               the config-3 stand-in only (bench.py, a 30k-iteration street chunk) -> c3.json
+#   c5               config 5 only (bench.py: the LOD cut + fused frame at 1080p)  -> c5.json
 #   py=<script args> python3 -u <script args>                       -> py.log (appended)
 set -u -o pipefail
 TAG=${1:?tag}; shift
 O=gpurun_out/$TAG
 mkdir -p "$O"
 C3="--steps 5 --warmup 2 --train-steps 0 --no-config5 --no-street --no-config4 --no-coarse-debug --no-cpu-baseline --post-leaves 0"
+C5="--steps 3 --warmup 2 --train-steps 0 --no-config3 --no-street --no-config4 --no-coarse-debug --no-cpu-baseline --post-leaves 0 --prewarm-s 0"
 for st in "$@"; do
     echo "== $st" >&2
     case "$st" in
@@ -31,6 +33,7 @@ for st in "$@"; do
                     > "$O/driver.json" 2> "$O/driver.err" ;;
         profile) bash tools/profile_gpu.sh "$TAG" ;;
         c3) timeout -k 10 600 python3 -u bench.py $C3 > "$O/c3.json" 2> "$O/c3.err" ;;
+        c5) timeout -k 10 600 python3 -u bench.py $C5 > "$O/c5.json" 2> "$O/c5.err" ;;
         py=*) timeout -k 10 600 python3 -u ${st#py=} >> "$O/py.log" 2>&1 ;;
         *) echo "unknown step $st" >&2; exit 64 ;;
     esac
