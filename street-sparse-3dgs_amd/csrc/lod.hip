@@ -77,7 +77,8 @@ __device__ __forceinline__ HBox load_box(const float *__restrict__ boxes, int64_
 //                         into the tile's slot; the tile's sum stored and added to its group's
 //                         (groups of kCutGroup tiles, one no-return atomic per tile);
 //   lod_cut_write_kernel  per tile: its offset (the earlier groups' sums plus the group's earlier
-//                         tiles', one round of loads) and its records' entries there.
+//                         tiles', one round of loads; past kCutDirectGroups groups the group sums
+//                         are scanned by one workgroup in between) and its records' entries there.
 // The nodes and boxes are read once; the records (16 B per rendered node) are written and read once.
 // A count pass, a library scan and a write pass read the nodes twice and a 4-byte count per node
 // three times (config 5's 50M nodes: 0.66 + 0.18 + 0.21 ms); one pass with a decoupled lookback
@@ -89,11 +90,16 @@ constexpr int kCutThreads = 256, kCutItems = GSR_CUT_ITEMS, kCutTile = kCutThrea
 constexpr int kCutWaves = kCutThreads / kWave;
 constexpr int kCutTotal = 0, kCutHead = 4;  // control words (uint64)
 
-constexpr int kCutGroup = 256;  // tiles per group: the groups' sums are scanned, a tile adds its group's earlier tiles
+constexpr int kCutGroup = 256;  // tiles per group: a tile adds its group's earlier tiles to the earlier groups' sum
+// Up to this many groups (16M nodes) each write workgroup sums the earlier groups itself (one load
+// per thread); past it a one-workgroup scan of the group sums runs between the two launches, so the
+// write launch's work stays linear in the node count (config 5's 50M nodes take the scan).
+constexpr int64_t kCutDirectGroups = 64;
 struct CutScratch {
     uint64_t *ctl;         // [kCutHead + ngroups]: control words, then the group sums; zeroed per call
     uint32_t *tile_sum;    // [ntiles] entries per tile
     uint32_t *tile_nrec;   // [ntiles] rendered nodes per tile
+    uint64_t *group_off;   // [ngroups] exclusive scan of the group sums (past kCutDirectGroups groups)
     uint4 *recs;           // [ntiles * kCutTile]
 };
 __host__ __device__ inline int64_t cut_groups(int64_t ntiles) { return (ntiles + kCutGroup - 1) / kCutGroup; }
@@ -108,9 +114,11 @@ __host__ __device__ inline size_t cut_scratch_bytes(int64_t ntiles, CutScratch *
     char *ctl = take(sizeof(uint64_t) * (size_t)(kCutHead + cut_groups(ntiles)));
     char *sum = take(sizeof(uint32_t) * (size_t)ntiles);
     char *nrec = take(sizeof(uint32_t) * (size_t)ntiles);
+    char *goff = take(sizeof(uint64_t) * (size_t)cut_groups(ntiles));
     char *recs = take(sizeof(uint4) * (size_t)ntiles * kCutTile);
     if (sc) *sc = CutScratch{reinterpret_cast<uint64_t *>(ctl), reinterpret_cast<uint32_t *>(sum),
-                             reinterpret_cast<uint32_t *>(nrec), reinterpret_cast<uint4 *>(recs)};
+                             reinterpret_cast<uint32_t *>(nrec), reinterpret_cast<uint64_t *>(goff),
+                             reinterpret_cast<uint4 *>(recs)};
     return at;
 }
 
@@ -218,6 +226,34 @@ __global__ __launch_bounds__(kCutThreads) void lod_cut_count_kernel(int64_t N, i
     }
 }
 
+// Past kCutDirectGroups groups: the group offsets in one workgroup, kScanThreads groups at a time.
+constexpr int kScanThreads = 1024;
+__global__ __launch_bounds__(kScanThreads) void lod_cut_scan_kernel(int64_t ngroups, CutScratch sc) {
+    __shared__ uint64_t s_w[kScanThreads / kWave];
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+    uint64_t carry = 0;
+    for (int64_t b0 = 0; b0 < ngroups; b0 += kScanThreads) {
+        const int64_t gi = b0 + tid;
+        const uint64_t v = gi < ngroups ? sc.ctl[kCutHead + gi] : 0ull;
+        uint64_t inc = v;
+#pragma unroll
+        for (int o = 1; o < kWave; o <<= 1) {
+            const uint64_t u = __shfl_up(inc, o, kWave);
+            if (lane >= o) inc += u;
+        }
+        __syncthreads();  // the previous round's reads of s_w are done
+        if (lane == kWave - 1) s_w[w] = inc;
+        __syncthreads();
+        uint64_t before = 0, tot = 0;
+        for (int k = 0; k < kScanThreads / kWave; k++) {
+            before += k < w ? s_w[k] : 0ull;
+            tot += s_w[k];
+        }
+        if (gi < ngroups) sc.group_off[gi] = carry + before + inc - v;
+        carry += tot;
+    }
+}
+
 __global__ __launch_bounds__(kCutThreads) void lod_cut_write_kernel(int64_t ntiles, CutScratch sc,
                                                                     int *__restrict__ render_indices,
                                                                     int *__restrict__ parent_indices,
@@ -232,7 +268,11 @@ __global__ __launch_bounds__(kCutThreads) void lod_cut_write_kernel(int64_t ntil
     static_assert(kCutGroup == kCutThreads, "one earlier tile per thread");
     const int nrec = (int)sc.tile_nrec[tile];
     uint64_t acc = g0 + tid < tile ? sc.tile_sum[g0 + tid] : 0u;
-    for (int64_t j = tid; j < g; j += kCutThreads) acc += sc.ctl[kCutHead + j];
+    if (cut_groups(ntiles) > kCutDirectGroups) {
+        if (tid == 0) acc += sc.group_off[g];
+    } else {
+        for (int64_t j = tid; j < g; j += kCutThreads) acc += sc.ctl[kCutHead + j];
+    }
 #pragma unroll
     for (int o = kWave / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, kWave);
     if (lane == 0) s_red[w] = acc;
@@ -335,6 +375,8 @@ int gsr_expand_to_size(int64_t N, const int *nodes, const float *boxes, float ta
     if (e == hipSuccess) {
         hipLaunchKernelGGL(lod_cut_count_kernel, dim3((unsigned)ntiles), dim3(kCutThreads), 0, s, N, ntiles, nodes,
                            boxes, target_size, viewpoint, sc);
+        if (cut_groups(ntiles) > kCutDirectGroups)
+            hipLaunchKernelGGL(lod_cut_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, cut_groups(ntiles), sc);
         hipLaunchKernelGGL(lod_cut_write_kernel, dim3((unsigned)ntiles), dim3(kCutThreads), 0, s, ntiles, sc, render_indices,
                            parent_indices, nodes_for_render_indices, capacity < 0 ? (int64_t)0 : capacity);
         e = hipGetLastError();
