@@ -189,6 +189,13 @@ constexpr int kShPitch = 13;               // padded LDS row pitch, in float4
 #define GSR_COLOR_WAVES 8  // 104 KiB per block, one block per CU: it interferes less with the binning beside it
 #endif
 constexpr int kColorWaves = GSR_COLOR_WAVES;  // waves per block (13 KiB of LDS each)
+// A fused hierarchy cut (config 5: two SH-row gathers per row) in 10-wave blocks, still one per CU
+// (140 KiB with the cut's index slice): the pass 1.42-1.44 -> 1.39-1.40 ms, the frame's raster part
+// 2.28-2.30 -> 2.25-2.28 ms (r06zk, r06zm, interleaved; a next-row-block prefetch instead,
+// GSR_COLOR_PF: 3.31 against 3.26 ms per frame)
+#ifndef GSR_COLOR_WAVES_CUT
+#define GSR_COLOR_WAVES_CUT 10
+#endif
 #ifndef GSR_COLOR_BLOCKS
 #define GSR_COLOR_BLOCKS 0
 #endif
@@ -426,6 +433,7 @@ void launch_preprocess_color(const GaussianInputs &in, const Camera &cam, const 
                                in.means3D, in.shs, cam.campos, cam.view, radii, gs, nvb, in.cut);
     };
     if (four && cap == 0) go(std::integral_constant<int, 4>{});
+    else if (in.cut.ri) go(std::integral_constant<int, GSR_COLOR_WAVES_CUT>{});
     else go(std::integral_constant<int, kColorWaves>{});
 }
 
