@@ -73,6 +73,20 @@ def test_segment_regions_fit_the_binning_buffer(L, Lf):
     assert lib.gsr_segment_layout_check(-1, L, Lf, None, None) != 0
 
 
+def test_expand_to_size_scratch_is_linear_in_nodes():
+    """gsr_expand_to_size's scratch (host arithmetic, no GPU): the two-launch cut's record slots
+    (16 B per node, 1024-node tiles), the per-tile words and the group sums -- at least 16 B per
+    node, at most 16.1 B per node plus a constant, and never shrinking as N grows."""
+    from diff_gaussian_rasterization import _lib
+    lib = _lib.load()
+    prev = 0
+    for N in [0, 1, 1023, 1024, 1025, 65_536, 262_145, 16_777_216, 50_000_006, (1 << 31) - 1]:
+        b = int(lib.gsr_expand_to_size_scratch_bytes(N))
+        assert b >= 16 * N and b <= 16.1 * N + (1 << 16), (N, b)
+        assert b >= prev, (N, b, prev)
+        prev = b
+
+
 def test_library_is_gfx950_code_object():
     from diff_gaussian_rasterization import _lib
     data = open(_lib.LIB_PATH, "rb").read()
