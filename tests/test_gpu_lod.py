@@ -76,6 +76,46 @@ def test_lod_cut_ragged_tiles_and_unaligned_nodes(leaves, offset):
     assert int(ri[n:].abs().sum()) == 0
 
 
+@pytest.mark.parametrize("case", ["root_small", "root_big", "empty", "multi_tile_empty_tiles"])
+def test_lod_cut_edge_cases(case):
+    """The two-launch cut on degenerate hierarchies, against the oracle: a lone root that fits the
+    target (it renders its leaf and merged Gaussians), a lone root that is too big (its leaves
+    only), a cut with nothing to render (every node too big, no leaf Gaussians), and 3000 nodes whose
+    first tiles render nothing (whole tiles of zero counts before and after the rendered ones)."""
+    import gs_oracle as O
+    from gaussian_hierarchy._C import expand_to_size
+    cam = np.zeros(3, np.float32)
+    if case in ("root_small", "root_big", "empty"):
+        nodes = np.array([[0, -1, 5, 2 if case != "empty" else 0, 3, -1, 0]], np.int32)
+        boxes = np.zeros((1, 2, 4), np.float32)
+        if case == "root_small":  # a small box far away: size / distance below the target
+            boxes[0, 0, :3], boxes[0, 0, 3], boxes[0, 1, :3] = 99.0, 0.01, 100.0
+        else:  # the viewpoint inside the box: +inf size, always too big
+            boxes[0, 0, :3], boxes[0, 0, 3], boxes[0, 1, :3] = -1.0, 2.0, 1.0
+    else:
+        N = 3000
+        nodes = np.zeros((N, 7), np.int32)
+        nodes[:, 1] = -1
+        nodes[:, 2] = np.arange(N)
+        nodes[:, 4] = 1  # merged Gaussian each; rendered only when small
+        boxes = np.zeros((N, 2, 4), np.float32)
+        boxes[:, 0, :3], boxes[:, 0, 3], boxes[:, 1, :3] = -1.0, 2.0, 1.0  # contains the viewpoint
+        small = np.arange(N)[(np.arange(N) >= 1500) & (np.arange(N) < 2100)]  # tiles 1-2 only
+        boxes[small, 0, :3], boxes[small, 0, 3], boxes[small, 1, :3] = 99.0, 0.01, 100.0
+    N = nodes.shape[0]
+    thr = np.float32(0.5)
+    dn, db = torch.tensor(nodes, device=DEV), torch.tensor(boxes, device=DEV)
+    ri, pi, ni = (torch.full((N + 8,), -7, dtype=torch.int32, device=DEV) for _ in range(3))
+    n = expand_to_size(dn, db, float(thr), torch.tensor(cam, device=DEV), torch.zeros(3), ri, pi, ni)
+    ori, opi, oni = O.expand_to_size(nodes, boxes, thr, cam)
+    assert n == len(ori), (n, len(ori))
+    assert n == {"root_small": 5, "root_big": 2, "empty": 0, "multi_tile_empty_tiles": 600}[case]
+    np.testing.assert_array_equal(ri[:n].cpu().numpy(), ori)
+    np.testing.assert_array_equal(pi[:n].cpu().numpy(), opi)
+    np.testing.assert_array_equal(ni[:n].cpu().numpy(), oni)
+    assert bool(torch.all(ri[n:] == -7))
+
+
 def _covered_once(h, ri, n):
     """Every leaf of the tree is rendered exactly once: by itself or through exactly one ancestor
     in the cut (each node holds one Gaussian, Gaussian i = node i).  Level by level on the device:
