@@ -232,7 +232,7 @@ template <bool kCut>
 __device__ __forceinline__ void color_fetch(int vb, ShRows &r, int P, int D, const float *__restrict__ shs,
                                             const int *__restrict__ radii, const CutRef &cut, int4 *s_idx) {
     const int i = vb * blockDim.x + threadIdx.x;
-    r.vis = i < P && radii[i] > 0;
+    r.vis = i < P && (!radii || radii[i] > 0);  // radii NULL: forked before the preprocess, every row
     const int nc = (D + 1) * (D + 1);
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t need = __ballot(r.vis);

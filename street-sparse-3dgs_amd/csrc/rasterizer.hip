@@ -754,18 +754,6 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
                        (GSR_COLOR_SERIAL || side_stream(s, &side, &fork, &join));
     if (fuse_cut && !split) return fail(GSR_ERR_DEVICE, "hierarchy cut: the fused blend needs the SH colour pass");
     SideJoin sj;
-    {
-        StageTimer st(0, s);
-        launch_preprocess(in, cam, gs, radii, s, split);
-    }
-    if ((rc = check("preprocess", debug, s))) return rc;
-    if (split && GSR_COLOR_SERIAL) {
-        {
-            StageTimer st(8, s);
-            launch_preprocess_color(in, cam, gs, radii, s);
-        }
-        if ((rc = check("preprocess colour", debug, s))) return rc;
-    }
 #ifndef GSR_COLOR_FORK
 #define GSR_COLOR_FORK 2  // 0: beside the sort and the binning; 1: beside the binning only; 2: chosen per frame
 #endif
@@ -807,13 +795,13 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
             }
         }
     }
-    auto fork_color = [&]() -> int {
+    auto fork_color = [&](const int *vis_radii) -> int {
         // fork: the SH colours stream in beside latency-bound main-stream stages; joined before render_fwd
         if (hipEventRecord(fork, s) != hipSuccess || hipStreamWaitEvent(side, fork, 0) != hipSuccess)
             return fail(GSR_ERR_DEVICE, "side stream fork failed");
         {
             StageTimer st(8, side);
-            launch_preprocess_color(in, cam, gs, radii, side, color_blocks);
+            launch_preprocess_color(in, cam, gs, vis_radii, side, color_blocks);
         }
         if (hipEventRecord(join, side) != hipSuccess) return fail(GSR_ERR_DEVICE, "side stream join record failed");
         sj.s = s;
@@ -821,7 +809,29 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
         sj.pending = true;
         return check("preprocess colour", debug, side);
     };
-    if (split && !GSR_COLOR_SERIAL && color_early && (rc = fork_color())) return rc;
+#ifndef GSR_COLOR_PRE_CUT
+#define GSR_COLOR_PRE_CUT 1
+#endif
+    // A fused hierarchy cut whose colour pass forks early (config 5): forked before the preprocess,
+    // so it overlaps the preprocess as well; it then colours every row (no radii yet: a cut frame's
+    // rows are all in view) and writes only the colour quarter of each render record and the clamp
+    // bits, which the preprocess leaves to it.  Config 5's raster part 2.30 -> 2.28 ms (r06zt,
+    // interleaved; the pass itself 1.44 -> 1.85 ms, longer but off the critical path).
+    const bool pre_fork = GSR_COLOR_PRE_CUT && fuse_cut && split && !GSR_COLOR_SERIAL && color_early;
+    if (pre_fork && (rc = fork_color(nullptr))) return rc;
+    {
+        StageTimer st(0, s);
+        launch_preprocess(in, cam, gs, radii, s, split);
+    }
+    if ((rc = check("preprocess", debug, s))) return rc;
+    if (split && GSR_COLOR_SERIAL) {
+        {
+            StageTimer st(8, s);
+            launch_preprocess_color(in, cam, gs, radii, s);
+        }
+        if ((rc = check("preprocess colour", debug, s))) return rc;
+    }
+    if (split && !GSR_COLOR_SERIAL && color_early && !pre_fork && (rc = fork_color(radii))) return rc;
     // K sizes the point list.  With a capacity hint from this device's previous frame the binning
     // and the forward render are queued first and K is read afterwards (the GPU never waits on
     // the host's hand-off); kernels that would overrun the capacity exit at once (they compare the
@@ -928,7 +938,7 @@ int gsr_rasterize_forward_ex(gsr_resize_fn geom_buffer, gsr_resize_fn binning_bu
         if ((rc = read_K())) return rc;
         if (local && maxsb > (uint32_t)sort_cap() && (rc = to_global())) return rc;
     }
-    if (split && !GSR_COLOR_SERIAL && !color_early && (rc = fork_color())) return rc;
+    if (split && !GSR_COLOR_SERIAL && !color_early && (rc = fork_color(radii))) return rc;
     bool joined = false;
     const uint32_t seg_req = need_bwd && bwd_segments_supported() ? g_bwd_seg.load(std::memory_order_relaxed) : 0u;
     uint32_t fseg_req = fwd_segments_supported() && !sb_order ? g_fwd_seg.load(std::memory_order_relaxed) : 0u;
