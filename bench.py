@@ -883,6 +883,16 @@ class ClockProbe:
 SECONDARY_LEGS = ("train_step", "config4", "street_frame", "coarse_debug", "train_post_step", "config3_proxy",
                   "config5", "cpu_baseline_torch", "psnr_vs_oracle")
 PROSE_KEYS = ("workload", "data", "source", "collectives", "reference")
+MOVED_KEYS = {
+    "config3_proxy": ("setup_s", "P_init", "P_max", "capacity_reruns", "final_sh_degree", "loss_first_last",
+                      "train_view_psnr_db", "late_tile_instances", "late_relevant_row_frac", "seed",
+                      "variant.iteration_ms", "variant.slowest3", "variant.P_final", "variant.train_view_psnr_db"),
+    "config5": ("nodes", "leaves", "tau", "leaf_log_scale", "width", "height", "visible", "rendered", "fwd_mpix_s",
+                "render_post_order.cut", "render_post_order.split_ms"),
+    "street_frame": ("stages_ms", "tiles", "level1_entries"),
+    "cpu_baseline_torch": ("sample",),
+    "config4": ("visible_rank0", "tile_instances_rank0", "chunks.chunk_wall_s_per_rank", "chunks.P_final_rank0"),
+}
 
 
 def compact_legs(out, detail):
@@ -903,6 +913,22 @@ def compact_legs(out, detail):
     c5 = out.get("config5")
     if isinstance(c5, dict) and isinstance(c5.get("render_post_order"), dict):
         detail["config5_render_post_order_stages_ms"] = c5["render_post_order"].pop("raster_stages_ms", None)
+    # descriptive numbers of the secondary legs (sizes, schedules, per-stage splits) to the detail file
+    # too: the line stays under ~5 kB with the metric's diagnostics last
+    if isinstance(c5, dict) and isinstance(c5.get("raster_stages_ms"), dict):  # a forward-only frame's zero stages
+        c5["raster_stages_ms"] = {k: v for k, v in c5["raster_stages_ms"].items() if v}
+    moved = detail.setdefault("moved", {})
+    for leg, keys in MOVED_KEYS.items():
+        d = out.get(leg)
+        if not isinstance(d, dict):
+            continue
+        for k in keys:
+            sub = d
+            path = k.split(".")
+            for part in path[:-1]:
+                sub = sub.get(part) if isinstance(sub, dict) else None
+            if isinstance(sub, dict) and path[-1] in sub:
+                moved[leg + "." + k] = sub.pop(path[-1])
 
 
 def prewarm(step, probe, max_s=0.6, min_s=0.25, tol=0.03, burst=20):

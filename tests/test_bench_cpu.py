@@ -37,6 +37,20 @@ def test_compact_legs_moves_prose_only():
     assert detail["config5_render_post_order_stages_ms"] == {"a": 1}
 
 
+def test_compact_legs_moves_descriptive_numbers():
+    import bench
+    out = {"config3_proxy": {"chunk_wall_s": 50.0, "seed": 0, "P_init": 330000,
+                             "variant": {"spatial_rows": True, "chunk_wall_s": 49.4, "slowest3": [[1, 2.0]]}},
+           "config5": {"ms_per_frame": 3.3, "nodes": 50, "raster_stages_ms": {"render_fwd": 0.4, "render_bwd": 0.0}},
+           "config": {"gaussians": 1}}
+    detail = {}
+    bench.compact_legs(out, detail)
+    assert out["config3_proxy"] == {"chunk_wall_s": 50.0, "variant": {"spatial_rows": True, "chunk_wall_s": 49.4}}
+    assert out["config5"] == {"ms_per_frame": 3.3, "raster_stages_ms": {"render_fwd": 0.4}}
+    assert out["config"] == {"gaussians": 1}  # the metric's own config is never touched
+    assert detail["moved"]["config3_proxy.variant.slowest3"] == [[1, 2.0]] and detail["moved"]["config5.nodes"] == 50
+
+
 def test_dispersion_of_step_times():
     import bench
     d = bench.dispersion([0.65, 0.66, 0.70, 0.64, 0.90])
