@@ -891,7 +891,7 @@ MOVED_KEYS = {
                 "render_post_order.cut", "render_post_order.split_ms"),
     "street_frame": ("stages_ms", "tiles", "level1_entries"),
     "cpu_baseline_torch": ("sample",),
-    "config4": ("visible_rank0", "tile_instances_rank0", "chunks.chunk_wall_s_per_rank", "chunks.P_final_rank0"),
+    "config4": ("visible_rank0", "tile_instances_rank0"),
 }
 
 
