@@ -209,6 +209,22 @@ def test_config5_end_to_end_vs_oracle(leaves, tau, log_scale, skybox):
     # ~10x from the observed 147.9 dB / no pixel off (profiles/r04_parity_margins.jsonl)
     assert p >= 137.0, p
     assert off <= 1e-6, off
+    # the same frame through the rasterizer's own cut (render_indices: the blend fused into its
+    # preprocess and colour pass -- at this size the colour pass forks ahead of the preprocess and
+    # colours every row): bitwise the render_post-order frame above, as bench.py's config 5 runs it
+    from diff_gaussian_rasterization import _C
+    N = h["means3D"].shape[0]
+    sky = torch.arange(N - S, N, dtype=torch.int32, device=DEV)
+    ri2, pi2 = torch.cat([ri[:n], sky]), torch.cat([pi[:n], sky])
+    w2 = torch.cat([w[:n], torch.ones(S, device=DEV)])
+    e = torch.empty(0, device=DEV)
+    with torch.no_grad():
+        f = _C.rasterize_gaussians(t(bg), h["means3D"], e, h["opacities"], h["scales"], h["rotations"], 1.0, e,
+                                   t(h["view"]).reshape(4, 4), t(h["proj"]).reshape(4, 4), float(h["tanfovx"]),
+                                   float(h["tanfovy"]), H, W, h["shs"], 3, t(h["campos"]), False, False, ri2, pi2, w2, k,
+                                   True, need_backward=False)
+    torch.cuda.synchronize()
+    assert torch.equal(f[1], color) and torch.equal(f[2], invd) and torch.equal(f[3], radii)  # K, colour, invdepth, radii
 
 
 def test_rasterizer_render_indices_equal_render_post_blend():
